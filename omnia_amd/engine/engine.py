@@ -1,0 +1,366 @@
+"""The in-node inference engine: the piece that replaces Omnia's remote
+``Provider`` (``internal/runtime/provider.go:95-151``).
+
+``LLMEngine``      synchronous core: add requests, ``step()`` runs one
+                   scheduled prefill or decode step, streams tokens through
+                   per-sequence callbacks.
+``AsyncLLMEngine`` owns a background engine thread and exposes
+                   ``async generate()`` yielding incremental text/token events
+                   to asyncio consumers (the runtime's agent loop / OpenAI shim).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import threading
+import time
+import uuid
+from dataclasses import dataclass, field
+
+import torch
+
+from ..models import build_model
+from ..models.config import ModelConfig, resolve
+from ..models.llama import KVCache
+from ..observability import metrics as M
+from .kv_manager import BlockManager
+from .model_runner import ModelRunner
+from .sampling_params import SamplingParams
+from .scheduler import Scheduler, SchedulerConfig
+from .sequence import FinishReason, Sequence
+from .swap import SwapSpace
+from .tokenizer import Detokenizer, make_tokenizer
+
+log = logging.getLogger("omnia.engine")
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama-3-8b"
+    device: str = "cuda"
+    dtype: str = "bfloat16"
+    tp: int = 1
+    block_size: int = 32
+    max_batch: int = 256
+    max_model_len: int = 8192
+    max_prefill_tokens: int = 16384
+    kv_fraction: float = 0.85  # of free HBM after weights
+    num_blocks: int | None = None  # override
+    use_graphs: bool = True
+    seed: int = 0
+    swap_gib: float = 0.0  # host-DRAM warm tier for evicted session KV
+    tokenizer: str | None = None
+    decode_part_size: int = 512
+
+    @classmethod
+    def from_env(cls, **kw) -> "EngineConfig":
+        env = os.environ
+        m = {
+            "OMNIA_ENGINE_MODEL": ("model", str), "OMNIA_ENGINE_TP": ("tp", int),
+            "OMNIA_ENGINE_MAX_BATCH": ("max_batch", int),
+            "OMNIA_ENGINE_KV_FRACTION": ("kv_fraction", float),
+            "OMNIA_ENGINE_DTYPE": ("dtype", str),
+            "OMNIA_ENGINE_MAX_MODEL_LEN": ("max_model_len", int),
+            "OMNIA_ENGINE_BLOCK_SIZE": ("block_size", int),
+            "OMNIA_ENGINE_DEVICE": ("device", str),
+            "OMNIA_ENGINE_SWAP_GIB": ("swap_gib", float),
+        }
+        for k, (f, t) in m.items():
+            if k in env:
+                kw.setdefault(f, t(env[k]))
+        return cls(**kw)
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, model_cfg: ModelConfig | None = None):
+        self.cfg = cfg
+        self.model_cfg = model_cfg or resolve(cfg.model)
+        dev = torch.device(cfg.device if (cfg.device != "cuda" or torch.cuda.is_available())
+                           else "cpu")
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        dtype = getattr(torch, cfg.dtype)
+        t0 = time.perf_counter()
+        self.model = build_model(self.model_cfg, device=dev, dtype=dtype, seed=cfg.seed,
+                                 decode_part_size=cfg.decode_part_size)
+        self.load_s = time.perf_counter() - t0
+        nb = cfg.num_blocks or self._size_kv_pool(dtype)
+        self.kv = KVCache.allocate(self.model_cfg, nb, cfg.block_size, dev,
+                                   tp_size=self.model.tp, dtype=dtype)
+        swap = None
+        if cfg.swap_gib > 0 and dev.type == "cuda":
+            swap = SwapSpace(self.kv, cfg.swap_gib)
+        self.blocks = BlockManager(nb, cfg.block_size, swap=swap)
+        self.scheduler = Scheduler(
+            SchedulerConfig(max_batch=cfg.max_batch, max_prefill_tokens=cfg.max_prefill_tokens,
+                            max_model_len=cfg.max_model_len), self.blocks)
+        self.runner = ModelRunner(self.model, self.kv, max_batch=cfg.max_batch,
+                                  max_model_len=cfg.max_model_len, use_graphs=cfg.use_graphs,
+                                  max_prefill_tokens=cfg.max_prefill_tokens)
+        self.tokenizer = make_tokenizer(self.model_cfg, cfg.tokenizer)
+        self.eos = set(self.tokenizer.eos_token_ids)
+        self.seqs: dict[int, Sequence] = {}
+        self.detok: dict[int, Detokenizer] = {}
+        self.step_count = 0
+        self.counters = {"prefill_tokens": 0, "decode_tokens": 0, "steps_prefill": 0,
+                         "steps_decode": 0, "finished": 0}
+        log.info("engine ready: %s on %s, %d KV blocks x %d tokens, load %.1fs",
+                 self.model_cfg.name, dev, nb, cfg.block_size, self.load_s)
+
+    def _size_kv_pool(self, dtype) -> int:
+        cfg, mc = self.cfg, self.model_cfg
+        per_block = (mc.kv_bytes_per_token(torch.tensor([], dtype=dtype).element_size())
+                     // self.model.tp) * cfg.block_size
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+            free, total = torch.cuda.mem_get_info(self.device)
+            # leave room for activations / graphs
+            reserve = 6 * 2**30 + cfg.max_prefill_tokens * mc.hidden_size * 40
+            budget = max(0, int(free * cfg.kv_fraction) - reserve)
+        else:
+            budget = 256 * 2**20
+        nb = max(16, budget // per_block)
+        # cap to what max_batch sequences of max_model_len could ever use (+ session cache)
+        return int(nb)
+
+    # --------------------------------------------------------------- requests
+    def add_request(self, prompt: list[int] | str, params: SamplingParams | None = None,
+                    session_id: str | None = None, request_id: str | None = None,
+                    on_token=None, on_finish=None) -> Sequence:
+        params = (params or SamplingParams()).validate()
+        if isinstance(prompt, str):
+            prompt = self.tokenizer.encode(prompt, add_bos=True)
+        s = Sequence(prompt=list(prompt), params=params, session_id=session_id,
+                     request_id=request_id or uuid.uuid4().hex, on_token=on_token,
+                     on_finish=on_finish)
+        self.scheduler.add(s)
+        self.seqs[s.seq_id] = s
+        self.detok[s.seq_id] = Detokenizer(self.tokenizer)
+        M.ENGINE_WAITING.set(len(self.scheduler.waiting))
+        return s
+
+    def abort(self, seq_id: int) -> None:
+        s = self.scheduler.abort(seq_id)
+        if s is not None:
+            self._finalize(s)
+
+    def has_work(self) -> bool:
+        return self.scheduler.has_work()
+
+    def drop_session(self, session_id: str) -> bool:
+        return self.blocks.drop_session(session_id)
+
+    # --------------------------------------------------------------- stepping
+    def step(self) -> int:
+        """Run one engine iteration.  Returns number of tokens produced."""
+        plan = self.scheduler.schedule()
+        if plan.kind == "idle":
+            return 0
+        t0 = time.perf_counter()
+        if plan.kind == "prefill":
+            sampled = self.runner.run_prefill(plan.prefill)
+            done = self.scheduler.on_prefill_done(plan.prefill, sampled)
+            ntok = sum(n for _, n in plan.prefill)
+            self.counters["prefill_tokens"] += ntok
+            self.counters["steps_prefill"] += 1
+            M.PREFILL_TOKENS.inc(ntok)
+        else:
+            toks = self.runner.run_decode(plan.decode)
+            done = self.scheduler.on_decode_done(plan.decode, toks)
+            self.counters["decode_tokens"] += len(toks)
+            self.counters["steps_decode"] += 1
+            M.DECODE_TOKENS.inc(len(toks))
+            M.BATCH_SIZE.observe(len(toks))
+        dt = time.perf_counter() - t0
+        M.STEP_SECONDS.labels(plan.kind).observe(dt)
+        now = time.perf_counter()
+        for s, tok in done:
+            self._append(s, tok, now)
+        self.step_count += 1
+        M.KV_UTIL.set(self.blocks.utilization())
+        return len(done)
+
+    def _append(self, s: Sequence, tok: int, now: float) -> None:
+        if s.is_finished:
+            return
+        if s.first_token_time is None:
+            s.first_token_time = now
+            M.TTFT.observe(now - s.arrival)
+        s.output.append(tok)
+        p = s.params
+        reason = None
+        if not p.ignore_eos and tok in self.eos and len(s.output) > p.min_tokens:
+            reason = FinishReason.STOP
+        elif tok in p.stop_token_ids:
+            reason = FinishReason.STOP
+        elif len(s.output) >= p.max_tokens:
+            reason = FinishReason.LENGTH
+        elif s.length >= self.cfg.max_model_len:
+            reason = FinishReason.LENGTH
+        text = ""
+        if s.on_token is not None or p.stop:
+            if not (reason == FinishReason.STOP and tok in self.eos):
+                text = self.detok[s.seq_id].push(tok)
+            if p.stop and text:
+                s.text_tail = (s.text_tail + text)[-256:]
+                for st in p.stop:
+                    if st and st in s.text_tail:
+                        reason = FinishReason.STOP
+                        break
+        if s.on_token is not None:
+            s.on_token(s, tok, text)
+        if reason is not None:
+            self.scheduler.finish(s, reason)
+            self._finalize(s)
+
+    def _finalize(self, s: Sequence) -> None:
+        self.counters["finished"] += 1
+        if s.finish_time is None:
+            s.finish_time = time.perf_counter()
+        if s.on_token is not None:
+            tail = self.detok[s.seq_id].flush()
+            if tail:
+                s.on_token(s, None, tail)
+        self.detok.pop(s.seq_id, None)
+        self.seqs.pop(s.seq_id, None)
+        M.TURN_SECONDS.observe(s.finish_time - s.arrival)
+        if s.on_finish is not None:
+            s.on_finish(s)
+
+    def run_until_done(self, max_steps: int = 10**9) -> None:
+        n = 0
+        while self.has_work() and n < max_steps:
+            self.step()
+            n += 1
+
+    def generate(self, prompts: list, params: SamplingParams | None = None,
+                 session_ids: list | None = None) -> list[Sequence]:
+        seqs = [self.add_request(p, params, session_id=(session_ids[i] if session_ids else None))
+                for i, p in enumerate(prompts)]
+        finished = set()
+        while len(finished) < len(seqs):
+            self.step()
+            for s in seqs:
+                if s.is_finished:
+                    finished.add(s.seq_id)
+        return seqs
+
+
+# ===================================================================== async
+@dataclass
+class GenEvent:
+    text: str = ""
+    token: int | None = None
+    finished: bool = False
+    finish_reason: str | None = None
+    prompt_tokens: int = 0
+    output_tokens: int = 0
+    cached_tokens: int = 0
+    ttft: float | None = None
+
+
+class AsyncLLMEngine:
+    """Background engine thread + asyncio streaming API."""
+
+    def __init__(self, engine: LLMEngine):
+        self.engine = engine
+        self._inbox: list = []
+        self._lock = threading.Lock()
+        self._wake = threading.Event()
+        self._stop = False
+        self._thread = threading.Thread(target=self._loop, name="omnia-engine", daemon=True)
+        self._thread.start()
+        self.error: Exception | None = None
+
+    @classmethod
+    def from_config(cls, cfg: EngineConfig) -> "AsyncLLMEngine":
+        return cls(LLMEngine(cfg))
+
+    @property
+    def tokenizer(self):
+        return self.engine.tokenizer
+
+    def _loop(self):
+        eng = self.engine
+        if eng.device.type == "cuda":
+            torch.cuda.set_device(eng.device)
+        while not self._stop:
+            with self._lock:
+                inbox, self._inbox = self._inbox, []
+            for fn in inbox:
+                try:
+                    fn()
+                except Exception as e:  # surface to the submitter
+                    log.exception("engine request failed: %s", e)
+            if eng.has_work():
+                try:
+                    eng.step()
+                except Exception as e:
+                    log.exception("engine step failed")
+                    self.error = e
+                    self._fail_all(e)
+            else:
+                self._wake.wait(0.05)
+                self._wake.clear()
+
+    def _fail_all(self, e: Exception):
+        eng = self.engine
+        for s in list(eng.seqs.values()):
+            eng.scheduler.abort(s.seq_id)
+            s.finish_reason = FinishReason.ERROR
+            eng._finalize(s)
+
+    def submit(self, fn):
+        with self._lock:
+            self._inbox.append(fn)
+        self._wake.set()
+
+    async def generate(self, prompt, params: SamplingParams | None = None,
+                       session_id: str | None = None, request_id: str | None = None):
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        holder = {}
+
+        def on_token(s, tok, text):
+            loop.call_soon_threadsafe(q.put_nowait, GenEvent(text=text or "", token=tok))
+
+        def on_finish(s):
+            ev = GenEvent(finished=True, finish_reason=(s.finish_reason.value
+                                                        if s.finish_reason else None),
+                          prompt_tokens=len(s.prompt), output_tokens=len(s.output),
+                          cached_tokens=s.prefix_hit, ttft=s.ttft())
+            loop.call_soon_threadsafe(q.put_nowait, ev)
+
+        def add():
+            try:
+                holder["seq"] = self.engine.add_request(prompt, params, session_id, request_id,
+                                                        on_token=on_token, on_finish=on_finish)
+            except Exception as e:
+                loop.call_soon_threadsafe(q.put_nowait, e)
+
+        self.submit(add)
+        try:
+            while True:
+                ev = await q.get()
+                if isinstance(ev, Exception):
+                    raise ev
+                yield ev
+                if ev.finished:
+                    return
+        finally:
+            s = holder.get("seq")
+            if s is not None and not s.is_finished:
+                self.submit(lambda: self.engine.abort(s.seq_id))
+
+    def has_session(self, session_id: str) -> bool:
+        return self.engine.blocks.has_session(session_id)
+
+    def drop_session(self, session_id: str):
+        self.submit(lambda: self.engine.drop_session(session_id))
+
+    def shutdown(self):
+        self._stop = True
+        self._wake.set()
+        self._thread.join(timeout=5)

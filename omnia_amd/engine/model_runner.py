@@ -1,0 +1,286 @@
+"""Turns scheduled sequences into device batches, runs the model and the fused
+sampler, and replays hipGraph-captured decode steps.
+
+Decode graphs are captured lazily per (batch bucket, context bucket); the
+context bucket fixes the split-K grid of the paged-attention kernel.  All
+per-step host->device metadata goes through ONE pinned staging buffer and one
+async copy.  Only sampled token ids come back to the host.
+"""
+from __future__ import annotations
+
+import bisect
+import time
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.llama import ForwardBatch, KVCache
+from .sequence import Sequence
+
+BATCH_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384,
+                 448, 512, 640, 768, 896, 1024]
+
+
+class _Staging:
+    """Packed pinned host buffer + device twin with typed section views."""
+
+    def __init__(self, spec: dict, device, pin: bool):
+        self.off = {}
+        o = 0
+        for name, (dtype, n) in spec.items():
+            o = (o + 63) // 64 * 64
+            self.off[name] = (o, dtype, n)
+            o += n * torch.tensor([], dtype=dtype).element_size()
+        self.nbytes = (o + 63) // 64 * 64
+        self.host = torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=pin)
+        self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+        self.h = {}
+        self.d = {}
+        for name, (o, dtype, n) in self.off.items():
+            es = torch.tensor([], dtype=dtype).element_size()
+            self.h[name] = self.host[o:o + n * es].view(dtype)
+            self.d[name] = self.dev[o:o + n * es].view(dtype)
+        self.np = {k: v.numpy() for k, v in self.h.items()}
+
+    def upload(self, nbytes: int | None = None):
+        n = self.nbytes if nbytes is None else nbytes
+        self.dev[:n].copy_(self.host[:n], non_blocking=True)
+
+
+class ModelRunner:
+    def __init__(self, model, kv: KVCache, max_batch: int = 256, max_model_len: int = 8192,
+                 use_graphs: bool = True, max_prefill_tokens: int = 16384):
+        self.model = model
+        self.kv = kv
+        self.device = model.device
+        self.is_gpu = self.device.type == "cuda"
+        self.bs = kv.block_size
+        self.max_model_len = max_model_len
+        self.max_blocks = (max_model_len + self.bs - 1) // self.bs
+        self.max_batch = max_batch
+        self.max_prefill_tokens = max_prefill_tokens
+        self.vocab = model.cfg.vocab_size
+        self.use_graphs = use_graphs and self.is_gpu
+        self.buckets = [b for b in BATCH_BUCKETS if b < max_batch] + [max_batch]
+        pin = self.is_gpu
+        B, MB = max_batch, self.max_blocks
+        self.dec = _Staging({
+            "ids": (torch.int32, B), "pos": (torch.int32, B), "slots": (torch.int64, B),
+            "seq_lens": (torch.int32, B), "temp": (torch.float32, B), "top_k": (torch.int32, B),
+            "top_p": (torch.float32, B), "seeds": (torch.int64, B), "steps": (torch.int64, B),
+            "bt": (torch.int32, B * MB),
+        }, self.device, pin)
+        self.logits_idx = torch.arange(B, dtype=torch.int64, device=self.device)
+        self.out_tok = torch.zeros(B, dtype=torch.int32, device=self.device)
+        self.out_host = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        self.graphs: dict = {}
+        self.graph_pool = None
+        self.stats = {"graph_replays": 0, "eager_decodes": 0, "prefill_steps": 0,
+                      "captures": 0, "capture_s": 0.0}
+
+    # ------------------------------------------------------------------ utils
+    def _ctx_bucket(self, max_len: int) -> int:
+        """Number of block-table columns (a power-of-two context bucket)."""
+        nb = (max_len + self.bs - 1) // self.bs
+        c = 1024 // self.bs
+        while c < nb:
+            c *= 2
+        return min(c, self.max_blocks)
+
+    def _fill_sampling(self, st: _Staging, seqs: list[Sequence], n: int):
+        temp, topk, topp = st.np["temp"], st.np["top_k"], st.np["top_p"]
+        seeds, steps = st.np["seeds"], st.np["steps"]
+        for i, s in enumerate(seqs):
+            p = s.params
+            temp[i] = p.temperature
+            topk[i] = p.top_k
+            topp[i] = p.top_p
+            seeds[i] = p.seed if p.seed is not None else (s.seq_id * 7919 + 17)
+            steps[i] = len(s.output)
+        for i in range(len(seqs), n):
+            temp[i] = 0.0
+            topk[i] = 0
+            topp[i] = 1.0
+
+    def _penalty_counts(self, seqs: list[Sequence], rows: int):
+        if not any(s.params.needs_penalties for s in seqs):
+            return None
+        counts = torch.zeros(rows, self.vocab, dtype=torch.int32, device=self.device)
+        r, t = [], []
+        for i, s in enumerate(seqs):
+            if s.params.needs_penalties:
+                r.extend([i] * len(s.output))
+                t.extend(s.output)
+        if r:
+            counts.index_put_((torch.tensor(r, device=self.device),
+                               torch.tensor(t, device=self.device)),
+                              torch.ones(len(r), dtype=torch.int32, device=self.device),
+                              accumulate=True)
+        pen = {
+            "freq": torch.tensor([s.params.frequency_penalty for s in seqs], device=self.device),
+            "pres": torch.tensor([s.params.presence_penalty for s in seqs], device=self.device),
+            "rep": torch.tensor([s.params.repetition_penalty for s in seqs], device=self.device),
+        }
+        return counts, pen
+
+    # ------------------------------------------------------------------ prefill
+    def run_prefill(self, chunks: list[tuple[Sequence, int]]) -> dict[int, int]:
+        """chunks: (seq, n_new) -- prefill n_new uncached tokens of each seq.
+
+        Returns {seq_id: sampled token} for sequences whose prompt completed."""
+        ids, pos, slots, qsl, seq_lens, sample_rows, sample_seqs = [], [], [], [0], [], [], []
+        bs = self.bs
+        maxb = 1
+        for s, n in chunks:
+            toks = s.all_tokens
+            start = s.num_cached
+            ids.extend(toks[start:start + n])
+            pos.extend(range(start, start + n))
+            blk = s.blocks
+            slots.extend(blk[p // bs] * bs + p % bs for p in range(start, start + n))
+            qsl.append(qsl[-1] + n)
+            seq_lens.append(start + n)
+            maxb = max(maxb, len(blk))
+            if start + n == s.length:
+                sample_rows.append(qsl[-1] - 1)
+                sample_seqs.append(s)
+        B = len(chunks)
+        bt = np.zeros((B, maxb), dtype=np.int32)
+        for i, (s, _) in enumerate(chunks):
+            bt[i, :len(s.blocks)] = s.blocks
+        tseq, tq0 = ops.prefill_tiles([qsl[i + 1] - qsl[i] for i in range(B)])
+        dev = self.device
+        # one pinned packed upload
+        arr = np.concatenate([
+            np.asarray(ids, np.int64), np.asarray(pos, np.int64), np.asarray(slots, np.int64),
+            np.asarray(qsl, np.int64), np.asarray(seq_lens, np.int64), np.asarray(tseq, np.int64),
+            np.asarray(tq0, np.int64), np.asarray(sample_rows or [0], np.int64),
+            bt.reshape(-1).astype(np.int64)])
+        t = torch.from_numpy(arr)
+        if self.is_gpu:
+            t = t.pin_memory().to(dev, non_blocking=True)
+        T = len(ids)
+        o = 0
+
+        def take(n, dtype):
+            nonlocal o
+            v = t[o:o + n]
+            o += n
+            return v.to(dtype)
+
+        fb = ForwardBatch(
+            input_ids=take(T, torch.int32), positions=take(T, torch.int32),
+            slots=take(T, torch.int64), block_tables=None, seq_lens=None, logits_indices=None,
+            is_decode=False, num_seqs=B)
+        fb.q_start_loc = take(B + 1, torch.int32)
+        fb.seq_lens = take(B, torch.int32)
+        fb.tile_seq = take(len(tseq), torch.int32)
+        fb.tile_q0 = take(len(tq0), torch.int32)
+        fb.logits_indices = take(max(1, len(sample_rows)), torch.int64)
+        fb.block_tables = take(B * maxb, torch.int32).view(B, maxb)
+        logits = self.model.forward(fb, self.kv)
+        self.stats["prefill_steps"] += 1
+        if not sample_seqs:
+            return {}
+        toks = self._sample_eager(logits[: len(sample_seqs)], sample_seqs)
+        return {s.seq_id: t for s, t in zip(sample_seqs, toks)}
+
+    def _sample_eager(self, logits, seqs: list[Sequence]) -> list[int]:
+        n = len(seqs)
+        dev = self.device
+        temp = torch.tensor([s.params.temperature for s in seqs], dtype=torch.float32, device=dev)
+        top_k = torch.tensor([s.params.top_k for s in seqs], dtype=torch.int32, device=dev)
+        top_p = torch.tensor([s.params.top_p for s in seqs], dtype=torch.float32, device=dev)
+        seeds = torch.tensor([s.params.seed if s.params.seed is not None else s.seq_id * 7919 + 17
+                              for s in seqs], dtype=torch.int64, device=dev)
+        steps = torch.tensor([len(s.output) for s in seqs], dtype=torch.int64, device=dev)
+        pc = self._penalty_counts(seqs, n)
+        kw = {}
+        if pc is not None:
+            kw = dict(counts=pc[0], freq_pen=pc[1]["freq"], pres_pen=pc[1]["pres"],
+                      rep_pen=pc[1]["rep"])
+        tok = ops.sample(logits, temp, top_k, top_p, seeds=seeds, steps=steps, **kw)
+        return tok.cpu().tolist()
+
+    # ------------------------------------------------------------------ decode
+    def _decode_inputs(self, seqs: list[Sequence], nrows: int, ncols: int):
+        st = self.dec
+        n = len(seqs)
+        ids, pos, slots, lens = st.np["ids"], st.np["pos"], st.np["slots"], st.np["seq_lens"]
+        bt = st.np["bt"].reshape(self.max_batch, self.max_blocks)
+        bs = self.bs
+        for i, s in enumerate(seqs):
+            p = s.length - 1
+            ids[i] = s.output[-1] if s.output else s.prompt[-1]
+            pos[i] = p
+            slots[i] = s.blocks[p // bs] * bs + p % bs
+            lens[i] = p + 1
+            nb = len(s.blocks)
+            bt[i, :nb] = s.blocks
+        for i in range(n, nrows):  # padded rows -> null page, no KV write
+            ids[i] = 0
+            pos[i] = 0
+            slots[i] = -1
+            lens[i] = 1
+            bt[i, 0] = 0
+        self._fill_sampling(st, seqs, nrows)
+        st.upload()
+
+    def _decode_fb(self, nrows: int, ncols: int) -> ForwardBatch:
+        d = self.dec.d
+        return ForwardBatch(
+            input_ids=d["ids"][:nrows], positions=d["pos"][:nrows], slots=d["slots"][:nrows],
+            block_tables=d["bt"].view(self.max_batch, self.max_blocks)[:nrows, :ncols],
+            seq_lens=d["seq_lens"][:nrows], logits_indices=self.logits_idx[:nrows],
+            is_decode=True, num_seqs=nrows)
+
+    def _decode_body(self, nrows: int, ncols: int):
+        d = self.dec.d
+        fb = self._decode_fb(nrows, ncols)
+        logits = self.model.forward(fb, self.kv)
+        ops.sample(logits, d["temp"][:nrows], d["top_k"][:nrows], d["top_p"][:nrows],
+                   seeds=d["seeds"][:nrows], steps=d["steps"][:nrows],
+                   out=self.out_tok[:nrows])
+
+    def _capture(self, nrows: int, ncols: int):
+        t0 = time.perf_counter()
+        if self.graph_pool is None:
+            self.graph_pool = torch.cuda.graph_pool_handle()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._decode_body(nrows, ncols)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self.graph_pool):
+            self._decode_body(nrows, ncols)
+        torch.cuda.synchronize()
+        self.graphs[(nrows, ncols)] = g
+        self.stats["captures"] += 1
+        self.stats["capture_s"] += time.perf_counter() - t0
+        return g
+
+    def run_decode(self, seqs: list[Sequence]) -> list[int]:
+        n = len(seqs)
+        if n > self.max_batch:
+            raise ValueError("decode batch exceeds max_batch")
+        max_len = max(s.length for s in seqs)
+        ncols = self._ctx_bucket(max_len)
+        needs_pen = any(s.params.needs_penalties for s in seqs)
+        if self.use_graphs and not needs_pen:
+            nrows = self.buckets[bisect.bisect_left(self.buckets, n)]
+            self._decode_inputs(seqs, nrows, ncols)
+            g = self.graphs.get((nrows, ncols)) or self._capture(nrows, ncols)
+            g.replay()
+            self.stats["graph_replays"] += 1
+            self.out_host[:n].copy_(self.out_tok[:n], non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            return self.out_host[:n].tolist()
+        # eager path (CPU engine, penalties)
+        self._decode_inputs(seqs, n, ncols)
+        fb = self._decode_fb(n, ncols)
+        logits = self.model.forward(fb, self.kv)
+        self.stats["eager_decodes"] += 1
+        return self._sample_eager(logits, seqs)

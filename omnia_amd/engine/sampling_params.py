@@ -1,0 +1,72 @@
+"""Sampling parameters -- the PromptPack ``parameters`` block
+(``internal/schema/promptpack.schema.json`` ``$defs.Parameters``: temperature,
+max_tokens, top_p, top_k, frequency_penalty, presence_penalty) plus the
+AgentRuntime ``ProviderDefaults`` (``api/v1alpha1/agentruntime_types.go:431-459``)."""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+
+@dataclass
+class SamplingParams:
+    temperature: float = 1.0
+    top_p: float = 1.0
+    top_k: int = 0  # 0 = disabled
+    max_tokens: int = 256
+    min_tokens: int = 0
+    frequency_penalty: float = 0.0
+    presence_penalty: float = 0.0
+    repetition_penalty: float = 1.0
+    seed: int | None = None
+    stop: list[str] = field(default_factory=list)
+    stop_token_ids: list[int] = field(default_factory=list)
+    ignore_eos: bool = False
+    logprobs: bool = False
+
+    @property
+    def greedy(self) -> bool:
+        return self.temperature <= 0.0
+
+    @property
+    def needs_penalties(self) -> bool:
+        return (self.frequency_penalty != 0.0 or self.presence_penalty != 0.0
+                or self.repetition_penalty != 1.0)
+
+    def validate(self) -> "SamplingParams":
+        if self.temperature < 0:
+            raise ValueError("temperature must be >= 0")
+        if not 0.0 < self.top_p <= 1.0:
+            raise ValueError("top_p must be in (0, 1]")
+        if self.top_k < 0:
+            raise ValueError("top_k must be >= 0")
+        if self.max_tokens < 1:
+            raise ValueError("max_tokens must be >= 1")
+        if self.repetition_penalty <= 0:
+            raise ValueError("repetition_penalty must be > 0")
+        return self
+
+    @classmethod
+    def from_dict(cls, d: dict | None, **defaults) -> "SamplingParams":
+        """Build from a PromptPack ``parameters`` / OpenAI-style dict."""
+        d = dict(d or {})
+        kw = dict(defaults)
+        mapping = {
+            "temperature": "temperature", "top_p": "top_p", "topP": "top_p", "top_k": "top_k",
+            "topK": "top_k", "max_tokens": "max_tokens", "maxTokens": "max_tokens",
+            "frequency_penalty": "frequency_penalty", "presence_penalty": "presence_penalty",
+            "repetition_penalty": "repetition_penalty", "seed": "seed", "stop": "stop",
+            "ignore_eos": "ignore_eos", "min_tokens": "min_tokens", "logprobs": "logprobs",
+        }
+        for k, v in d.items():
+            if k in mapping and v is not None:
+                kw[mapping[k]] = v
+        if isinstance(kw.get("stop"), str):
+            kw["stop"] = [kw["stop"]]
+        for f in ("temperature", "top_p", "frequency_penalty", "presence_penalty",
+                  "repetition_penalty"):
+            if f in kw:
+                kw[f] = float(kw[f])
+        for f in ("top_k", "max_tokens", "min_tokens"):
+            if f in kw:
+                kw[f] = int(kw[f])
+        return cls(**kw).validate()

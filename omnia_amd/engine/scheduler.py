@@ -1,0 +1,193 @@
+"""Continuous-batching scheduler with chunked prefill and session-affine KV.
+
+Each engine step is either a PREFILL step (new/partially-prefilled sequences,
+packed up to ``max_prefill_tokens`` new tokens -- long prompts are chunked) or a
+DECODE step over every running sequence.  Prefill has priority while the
+running set is below ``max_batch`` so TTFT stays low; decode steps are the
+hipGraph-captured hot loop.  When the KV pool runs dry, idle session caches are
+evicted first (LRU, optionally to host DRAM), then the youngest running
+sequence is preempted (its pages are freed and it is re-queued for recompute).
+"""
+from __future__ import annotations
+
+import time
+from collections import deque
+from dataclasses import dataclass
+
+from .kv_manager import BlockManager, OutOfBlocks
+from .sequence import FinishReason, Sequence, SeqStatus
+
+
+@dataclass
+class SchedulerConfig:
+    max_batch: int = 256
+    max_prefill_tokens: int = 16384
+    max_model_len: int = 8192
+    prefill_chunk: int = 8192  # max new tokens of ONE sequence per prefill step
+
+
+@dataclass
+class StepPlan:
+    kind: str  # "prefill" | "decode" | "idle"
+    prefill: list  # [(seq, n_new)]
+    decode: list  # [seq]
+
+
+class Scheduler:
+    def __init__(self, cfg: SchedulerConfig, blocks: BlockManager):
+        self.cfg = cfg
+        self.blocks = blocks
+        self.waiting: deque[Sequence] = deque()
+        self.running: list[Sequence] = []
+        self.partial: list[Sequence] = []  # prompts mid-way through chunked prefill
+
+    # ------------------------------------------------------------ admission
+    def add(self, seq: Sequence) -> None:
+        if len(seq.prompt) == 0:
+            raise ValueError("empty prompt")
+        if len(seq.prompt) >= self.cfg.max_model_len:
+            raise ValueError(f"prompt of {len(seq.prompt)} tokens exceeds max_model_len "
+                             f"{self.cfg.max_model_len}")
+        seq.status = SeqStatus.WAITING
+        self.waiting.append(seq)
+
+    def abort(self, seq_id: int) -> Sequence | None:
+        for q in (self.waiting, self.running, self.partial):
+            for s in list(q):
+                if s.seq_id == seq_id:
+                    q.remove(s)
+                    self._free(s, retain=False)
+                    s.status = SeqStatus.FINISHED
+                    s.finish_reason = FinishReason.ABORT
+                    return s
+        return None
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running or self.partial)
+
+    @property
+    def num_active(self) -> int:
+        return len(self.running) + len(self.partial)
+
+    # ------------------------------------------------------------ KV helpers
+    def _ensure_blocks(self, s: Sequence, upto_tokens: int) -> None:
+        need = self.blocks.blocks_needed(upto_tokens) - len(s.blocks)
+        if need > 0:
+            s.blocks.extend(self.blocks.allocate(need))
+
+    def _free(self, s: Sequence, retain: bool) -> None:
+        if retain and s.session_id:
+            self.blocks.retain(s.session_id, s.blocks, s.all_tokens[: s.num_cached])
+        else:
+            self.blocks.release(s.blocks)
+        s.blocks = []
+
+    def _admit(self, s: Sequence) -> None:
+        blocks, n = self.blocks.acquire_prefix(s.session_id, s.prompt)
+        s.blocks = blocks
+        s.num_cached = n
+        s.prefix_hit = n
+
+    def _preempt_one(self, protect: Sequence | None = None) -> bool:
+        for victim in reversed(self.running):
+            if victim is protect:
+                continue
+            self.running.remove(victim)
+            self.blocks.release(victim.blocks)
+            victim.blocks = []
+            victim.num_cached = 0
+            victim.preemptions += 1
+            victim.status = SeqStatus.WAITING
+            # re-admission re-prefills prompt + generated-so-far (all_tokens)
+            self.waiting.appendleft(victim)
+            return True
+        return False
+
+    # ------------------------------------------------------------ planning
+    def schedule(self) -> StepPlan:
+        cfg = self.cfg
+        chunks: list[tuple[Sequence, int]] = []
+        budget = cfg.max_prefill_tokens
+        # continue chunked prompts first
+        for s in list(self.partial):
+            n = min(s.num_uncached, cfg.prefill_chunk, budget)
+            if n <= 0:
+                break
+            try:
+                self._ensure_blocks(s, s.num_cached + n)
+            except OutOfBlocks:
+                break
+            chunks.append((s, n))
+            budget -= n
+        while self.waiting and budget > 0 and (self.num_active + len(
+                [c for c in chunks if c[0] not in self.partial])) < cfg.max_batch:
+            s = self.waiting[0]
+            if s.num_cached == 0 and not s.blocks:
+                self._admit(s)
+            n = min(s.num_uncached, cfg.prefill_chunk, budget)
+            try:
+                self._ensure_blocks(s, s.num_cached + n + (1 if n == s.num_uncached else 0))
+            except OutOfBlocks:
+                if not chunks and not self.running:
+                    # nothing else can free memory: fail the request
+                    self.waiting.popleft()
+                    self._free(s, retain=False)
+                    s.status = SeqStatus.FINISHED
+                    s.finish_reason = FinishReason.ERROR
+                    if s.on_finish:
+                        s.on_finish(s)
+                    continue
+                break
+            self.waiting.popleft()
+            s.status = SeqStatus.RUNNING
+            chunks.append((s, n))
+            budget -= n
+            if n < s.num_uncached:
+                self.partial.append(s)
+        if chunks:
+            return StepPlan("prefill", chunks, [])
+        if self.running:
+            # every running seq needs a slot for its next token
+            for s in list(self.running):
+                while True:
+                    try:
+                        self._ensure_blocks(s, s.length)
+                        break
+                    except OutOfBlocks:
+                        if not self._preempt_one(protect=s):
+                            raise
+                if s not in self.running:
+                    continue
+            return StepPlan("decode", [], list(self.running))
+        return StepPlan("idle", [], [])
+
+    # ------------------------------------------------------------ results
+    def on_prefill_done(self, chunks, sampled: dict[int, int]) -> list[tuple[Sequence, int]]:
+        """Advance cached counters; returns (seq, token) for completed prompts."""
+        out = []
+        for s, n in chunks:
+            s.num_cached += n
+            if s.num_cached >= s.length:
+                if s in self.partial:
+                    self.partial.remove(s)
+                if s not in self.running:
+                    self.running.append(s)
+                tok = sampled.get(s.seq_id)
+                if tok is not None:
+                    out.append((s, tok))
+        return out
+
+    def on_decode_done(self, seqs: list[Sequence], toks: list[int]) -> list[tuple[Sequence, int]]:
+        for s in seqs:
+            s.num_cached = s.length  # the fed token's KV is now cached
+        return list(zip(seqs, toks))
+
+    def finish(self, s: Sequence, reason: FinishReason) -> None:
+        s.status = SeqStatus.FINISHED
+        s.finish_reason = reason
+        s.finish_time = time.perf_counter()
+        if s in self.running:
+            self.running.remove(s)
+        if s in self.partial:
+            self.partial.remove(s)
+        self._free(s, retain=reason != FinishReason.ERROR)

@@ -1,0 +1,209 @@
+"""Llama-3 family forward on the engine's paged KV cache (TP-aware).
+
+Per layer (T tokens, hidden d):
+    fused_add_rmsnorm -> QKV GEMM (hipBLASLt) -> RoPE + paged KV write (HIP) ->
+    paged attention (HIP prefill / decode) -> O GEMM [-> TP all-reduce] ->
+    fused_add_rmsnorm -> gate_up GEMM -> SwiGLU (HIP) -> down GEMM [-> all-reduce]
+Weights are kept in their natural [out, in] layout so ``F.linear`` maps onto a
+single hipBLASLt GEMM; column-parallel shards (QKV, gate_up) and row-parallel
+shards (O, down) follow Megatron.  The reference has no model code at all
+(SURVEY §0.2); this replaces its remote Provider (``internal/runtime/provider.go:95-151``).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import reference as ref
+from ..parallel import state as pstate
+from .config import ModelConfig
+
+
+@dataclass
+class ForwardBatch:
+    """Flattened step inputs.  All tensors live on the model device."""
+
+    input_ids: torch.Tensor  # int32 [T]
+    positions: torch.Tensor  # int32 [T]
+    slots: torch.Tensor  # int64 [T]  flat KV slot of each token
+    block_tables: torch.Tensor  # int32 [B, max_blocks]
+    seq_lens: torch.Tensor  # int32 [B] total context incl. this step's tokens
+    logits_indices: torch.Tensor  # int64 [B] rows of T whose logits are needed
+    is_decode: bool = True
+    q_start_loc: torch.Tensor | None = None  # int32 [B+1] (prefill)
+    tile_seq: torch.Tensor | None = None  # int32 [n_tiles] (prefill)
+    tile_q0: torch.Tensor | None = None
+    num_seqs: int = 0
+
+
+@dataclass
+class KVCache:
+    k: list  # per layer [NB, Hkv_local, BS, D]
+    v: list
+    block_size: int
+    num_blocks: int
+
+    @staticmethod
+    def allocate(cfg: ModelConfig, num_blocks: int, block_size: int, device, tp_size: int = 1,
+                 dtype=torch.bfloat16) -> "KVCache":
+        hkv = max(1, cfg.num_kv_heads // tp_size)
+        buf = torch.empty(cfg.num_layers, 2, num_blocks, hkv, block_size, cfg.head_dim,
+                          dtype=dtype, device=device)
+        return KVCache(k=[buf[i, 0] for i in range(cfg.num_layers)],
+                       v=[buf[i, 1] for i in range(cfg.num_layers)],
+                       block_size=block_size, num_blocks=num_blocks)
+
+
+def _init(shape, std, device, dtype, gen):
+    t = torch.empty(shape, dtype=torch.float32, device=device)
+    t.normal_(0.0, std, generator=gen)
+    return t.to(dtype)
+
+
+class LlamaModel:
+    def __init__(self, cfg: ModelConfig, device="cpu", dtype=torch.bfloat16, seed: int = 0,
+                 weights: dict | None = None, decode_part_size: int = 512):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        st = pstate.get_state()
+        self.tp, self.tpr = st.tp_size, st.tp_rank
+        if cfg.num_heads % self.tp:
+            raise ValueError("num_heads not divisible by tp")
+        self.hq = cfg.num_heads // self.tp
+        self.hkv = max(1, cfg.num_kv_heads // self.tp)
+        self.inter = cfg.intermediate_size // self.tp
+        self.vocab_local = cfg.vocab_size // self.tp if cfg.vocab_size % self.tp == 0 else None
+        if self.vocab_local is None:
+            raise ValueError("vocab not divisible by tp")
+        self.vocab_start = self.tpr * self.vocab_local
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.decode_part_size = decode_part_size
+        self.cos_sin = ref.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
+                                        cfg.rope_scaling, device=self.device)
+        self.w = weights if weights is not None else self._random_weights(seed)
+        self._ws = {}
+
+    # ------------------------------------------------------------ weights
+    def _random_weights(self, seed: int) -> dict:
+        """Random-init shard of this TP rank (no checkpoint available offline).
+
+        Std 0.02 like HF init; norms at 1.  Initialised directly on the device."""
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed * 1000 + self.tpr)
+        d, D = cfg.hidden_size, cfg.head_dim
+        w = {
+            "embed": _init((self.vocab_local, d), 0.02, dev, dt, g),
+            "final_norm": torch.ones(d, dtype=dt, device=dev),
+            "layers": [],
+        }
+        w["lm_head"] = w["embed"] if cfg.tie_embeddings else _init((self.vocab_local, d), 0.02,
+                                                                   dev, dt, g)
+        for _ in range(cfg.num_layers):
+            layer = {
+                "in_norm": torch.ones(d, dtype=dt, device=dev),
+                "post_norm": torch.ones(d, dtype=dt, device=dev),
+                "qkv": _init(((self.hq + 2 * self.hkv) * D, d), 0.02, dev, dt, g),
+                "o": _init((d, self.hq * D), 0.02 / math.sqrt(2 * cfg.num_layers), dev, dt, g),
+            }
+            layer.update(self._random_mlp(g))
+            w["layers"].append(layer)
+        return w
+
+    def _random_mlp(self, g) -> dict:
+        cfg, dev, dt, d = self.cfg, self.device, self.dtype, self.cfg.hidden_size
+        return {
+            "gate_up": _init((2 * self.inter, d), 0.02, dev, dt, g),
+            "down": _init((d, self.inter), 0.02 / math.sqrt(2 * cfg.num_layers), dev, dt, g),
+        }
+
+    def weight_bytes(self) -> int:
+        n = 0
+        seen = set()
+
+        def add(t):
+            nonlocal n
+            if isinstance(t, torch.Tensor) and t.data_ptr() not in seen:
+                seen.add(t.data_ptr())
+                n += t.numel() * t.element_size()
+
+        for k, v in self.w.items():
+            if k == "layers":
+                for layer in v:
+                    for t in layer.values():
+                        if isinstance(t, list):
+                            for x in t:
+                                add(x)
+                        else:
+                            add(t)
+            else:
+                add(v)
+        return n
+
+    # ------------------------------------------------------------ forward
+    def mlp(self, layer: dict, h: torch.Tensor) -> torch.Tensor:
+        gu = F.linear(h, layer["gate_up"])
+        a = ops.silu_mul(gu)
+        return F.linear(a, layer["down"])
+
+    def attention(self, li: int, h: torch.Tensor, fb: ForwardBatch, kv: KVCache) -> torch.Tensor:
+        T = h.shape[0]
+        D = self.cfg.head_dim
+        qkv = F.linear(h, self.w["layers"][li]["qkv"])
+        q = qkv[:, : self.hq * D]
+        k = qkv[:, self.hq * D: (self.hq + self.hkv) * D]
+        v = qkv[:, (self.hq + self.hkv) * D:]
+        ops.rope_kv(q, k, v, fb.positions, self.cos_sin, kv.k[li], kv.v[li], fb.slots, self.hq,
+                    self.hkv, kv.block_size)
+        q3 = q.view(T, self.hq, D)
+        if fb.is_decode:
+            ws = self._decode_ws(T, fb.block_tables.shape[1], kv.block_size, h.device)
+            o = ops.decode_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.seq_lens,
+                                     self.scale, part_size=self.decode_part_size, workspace=ws)
+        else:
+            o = ops.prefill_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.q_start_loc,
+                                      fb.seq_lens, self.scale, fb.tile_seq, fb.tile_q0)
+        out = F.linear(o.view(T, self.hq * D), self.w["layers"][li]["o"])
+        return pstate.tp_all_reduce(out)
+
+    def _decode_ws(self, B, max_blocks, bs, device):
+        key = (B, max_blocks, bs, str(device))
+        ws = self._ws.get(key)
+        if ws is None:
+            if device.type != "cuda":
+                return None
+            ws = ops.decode_workspace(B, self.hq, max_blocks, bs, self.decode_part_size, device)
+            self._ws[key] = ws
+        return ws
+
+    def embed(self, ids: torch.Tensor) -> torch.Tensor:
+        h = ops.embedding(ids, self.w["embed"], self.vocab_start)
+        return pstate.tp_all_reduce(h) if self.tp > 1 else h
+
+    def hidden_states(self, fb: ForwardBatch, kv: KVCache) -> torch.Tensor:
+        cfg = self.cfg
+        eps = cfg.rms_eps
+        residual = self.embed(fb.input_ids)
+        h = ops.rmsnorm(residual, self.w["layers"][0]["in_norm"], eps)
+        for li, layer in enumerate(self.w["layers"]):
+            if li > 0:
+                ops.fused_add_rmsnorm(h, residual, layer["in_norm"], eps)
+            h = self.attention(li, h, fb, kv)
+            ops.fused_add_rmsnorm(h, residual, layer["post_norm"], eps)
+            h = pstate.tp_all_reduce(self.mlp(layer, h)) if self.tp > 1 else self.mlp(layer, h)
+        ops.fused_add_rmsnorm(h, residual, self.w["final_norm"], eps)
+        return h
+
+    def logits(self, h: torch.Tensor) -> torch.Tensor:
+        lg = F.linear(h, self.w["lm_head"])
+        return pstate.tp_all_gather_lastdim(lg) if self.tp > 1 else lg
+
+    def forward(self, fb: ForwardBatch, kv: KVCache) -> torch.Tensor:
+        h = self.hidden_states(fb, kv)
+        sel = h.index_select(0, fb.logits_indices)
+        return self.logits(sel)

@@ -1,0 +1,201 @@
+"""Kernel front-end for the in-node engine.
+
+On a GPU tensor every op runs the hand-written gfx950 HIP kernel from
+``_omnia_kernels.so`` -- and fails LOUDLY if the extension is missing (a silent
+eager fallback would hide a broken build).  On CPU tensors the plain-PyTorch
+reference in :mod:`omnia_amd.ops.reference` runs instead (the CPU test-suite and
+the mock/CPU engine path).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+import torch
+
+from . import reference as ref
+
+_lock = threading.Lock()
+_ext = None
+_ext_err: Exception | None = None
+
+
+def kernels():
+    """Return the loaded extension module, building it in-tree on first use if needed."""
+    global _ext, _ext_err
+    if _ext is not None:
+        return _ext
+    with _lock:
+        if _ext is not None:
+            return _ext
+        try:
+            _ext = importlib.import_module("omnia_amd.ops._omnia_kernels")
+        except ImportError as e:  # pragma: no cover - exercised on fresh checkouts
+            if os.environ.get("OMNIA_NO_AUTOBUILD"):
+                _ext_err = e
+                raise RuntimeError(
+                    "omnia_amd HIP extension not built; run `python -m omnia_amd.ops.build`"
+                ) from e
+            from .build import build
+
+            build(verbose=True)
+            _ext = importlib.import_module("omnia_amd.ops._omnia_kernels")
+    return _ext
+
+
+def extension_available() -> bool:
+    try:
+        kernels()
+        return True
+    except Exception:
+        return False
+
+
+# --------------------------------------------------------------------- ops
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None):
+    if x.is_cuda:
+        out = torch.empty_like(x) if out is None else out
+        kernels().rmsnorm(out, x, w, eps)
+        return out
+    r = ref.rmsnorm(x, w, eps)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float):
+    """In place: residual += x; x = rmsnorm(residual) * w.  Returns (x, residual)."""
+    if x.is_cuda:
+        kernels().fused_add_rmsnorm(x, residual, w, eps)
+        return x, residual
+    y, r = ref.fused_add_rmsnorm(x, residual, w, eps)
+    x.copy_(y)
+    residual.copy_(r)
+    return x, residual
+
+
+def rope_kv(q, k, v, positions, cos_sin, k_cache, v_cache, slots, hq, hkv, block_size):
+    """Rotate q/k in place (neox) and write k/v rows into the paged cache at `slots`."""
+    if q.is_cuda:
+        kernels().rope_kv(q, k, v, positions, cos_sin, k_cache, v_cache, slots, hq, hkv,
+                          block_size)
+        return
+    T = q.shape[0]
+    D = q.shape[1] // hq
+    qr = ref.apply_rope(q.view(T, hq, D), positions, cos_sin)
+    kr = ref.apply_rope(k.reshape(T, hkv, D), positions, cos_sin)
+    q.copy_(qr.view(T, hq * D))
+    k.copy_(kr.reshape(T, hkv * D))
+    if slots is not None:
+        ref.write_kv(k_cache, v_cache, kr, v.reshape(T, hkv, D), slots)
+
+
+def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None):
+    inter = x.shape[-1] // 2
+    if x.is_cuda:
+        out = x.new_empty(*x.shape[:-1], inter) if out is None else out
+        kernels().silu_mul(out, x)
+        return out
+    r = ref.silu_mul(x)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def embedding(ids: torch.Tensor, w: torch.Tensor, vocab_start: int = 0,
+              out: torch.Tensor | None = None):
+    if ids.is_cuda:
+        out = w.new_empty(ids.numel(), w.shape[1]) if out is None else out
+        kernels().embedding(out, ids, w, vocab_start)
+        return out
+    local = (ids >= vocab_start) & (ids < vocab_start + w.shape[0])
+    idx = torch.where(local, ids - vocab_start, torch.zeros_like(ids)).long()
+    r = w[idx] * local[:, None].to(w.dtype)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def decode_workspace(batch: int, hq: int, max_blocks: int, block_size: int, part_size: int,
+                     device) -> tuple[torch.Tensor, torch.Tensor]:
+    max_parts = (max_blocks * block_size + part_size - 1) // part_size
+    part_o = torch.empty(batch * hq * max_parts * 128, dtype=torch.float32, device=device)
+    part_ml = torch.empty(batch * hq * max_parts * 2, dtype=torch.float32, device=device)
+    return part_o, part_ml
+
+
+def decode_attention(q, k_cache, v_cache, block_tables, seq_lens, scale, part_size=512,
+                     workspace=None, out=None):
+    """q: [B, Hq, D] one query per sequence at position seq_len-1."""
+    if q.is_cuda:
+        B, hq, _ = q.shape
+        if out is None:
+            out = torch.empty(B, hq, q.shape[2], dtype=q.dtype, device=q.device)
+        if workspace is None:
+            workspace = decode_workspace(B, hq, block_tables.shape[1], k_cache.shape[2],
+                                         part_size, q.device)
+        kernels().decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens,
+                                   workspace[0], workspace[1], part_size, scale)
+        return out
+    B = q.shape[0]
+    qsl = torch.arange(B + 1, dtype=torch.int32)
+    r = ref.paged_attention(q, k_cache, v_cache, block_tables, qsl, seq_lens, scale)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def prefill_tiles(q_lens: list[int], tile: int = 64) -> tuple[list[int], list[int]]:
+    seqs, q0s = [], []
+    for s, n in enumerate(q_lens):
+        for q0 in range(0, n, tile):
+            seqs.append(s)
+            q0s.append(q0)
+    return seqs, q0s
+
+
+def prefill_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, scale,
+                      tile_seq=None, tile_q0=None, out=None):
+    """q: [T, Hq, D] new tokens of several sequences (varlen, causal w/ cached prefix)."""
+    if q.is_cuda:
+        if tile_seq is None:
+            qsl = q_start_loc.cpu().tolist()
+            s, q0 = prefill_tiles([qsl[i + 1] - qsl[i] for i in range(len(qsl) - 1)])
+            tile_seq = torch.tensor(s, dtype=torch.int32, device=q.device)
+            tile_q0 = torch.tensor(q0, dtype=torch.int32, device=q.device)
+        out = torch.empty_like(q) if out is None else out
+        kernels().prefill_attention(out, q, k_cache, v_cache, block_tables, q_start_loc,
+                                    seq_lens, tile_seq, tile_q0, scale)
+        return out
+    r = ref.paged_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, scale)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def sample(logits, temperature, top_k=None, top_p=None, seeds=None, steps=None, counts=None,
+           freq_pen=None, pres_pen=None, rep_pen=None, out=None, out_logprob=None):
+    """Fused GPU sampler; returns int32 [B] token ids."""
+    if logits.is_cuda:
+        B = logits.shape[0]
+        out = torch.empty(B, dtype=torch.int32, device=logits.device) if out is None else out
+        kernels().sample(out, out_logprob, logits, temperature, top_k, top_p, seeds, steps,
+                         counts, freq_pen, pres_pen, rep_pen)
+        return out
+    x = ref.apply_penalties(logits, counts, freq_pen, pres_pen, rep_pen)
+    g = None
+    if seeds is not None:
+        g = torch.Generator().manual_seed(int(seeds[0]) + int(steps[0] if steps is not None else 0))
+    r = ref.sample(x, temperature, top_k, top_p, generator=g)
+    if counts is not None:
+        counts[torch.arange(r.numel()), r.long()] += 1
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r

@@ -1,0 +1,453 @@
+// Paged attention for the in-node engine on gfx950.
+//
+// KV cache layout (shared with rope_kv in elementwise.hip):
+//     k_cache, v_cache : [num_blocks, Hkv, BS, 128] bf16
+// i.e. one kv-head's rows of a page are contiguous, so a 16-lane group reads a
+// whole 256-B token row and a wave-instruction reads 4 consecutive tokens = 1 KiB.
+//
+// decode  : split-K ("flash-decoding") over partitions of the context, GQA
+//           group of G query heads per workgroup sharing one K/V stream;
+//           Q.K^T on the MFMA (16x16x32 bf16, heads padded to 16 columns),
+//           softmax in LDS, P.V on the VALU (8 dims per lane), partitions merged
+//           by a second tiny kernel.
+// prefill : flash-attention over (cached prefix + new tokens) with causal
+//           offset, 64 query rows x 1 head per workgroup (16 rows per wave),
+//           K/V tiles of 64 keys gathered from pages into XOR-swizzled LDS,
+//           S^T = K.Q^T so each lane owns one query row (softmax row stats are
+//           lane-local + 2 shuffles), P^T reused in-register as the B operand of
+//           O^T = V^T.P^T with V^T fragments from ds_read_b64_tr_b16.
+#include "common.h"
+
+using namespace omnia;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float4v mfma16(short8 a, short8 b, float4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+constexpr int D = 128;
+
+// ============================================================== decode
+// grid: (B, Hkv, max_parts)   block: 256 (4 waves)
+template <int G, int BS>
+__global__ __launch_bounds__(256) void decode_attn_kernel(
+    bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
+    int hkv, int64_t q_stride, int part_size, int max_parts, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* stat = reinterpret_cast<float*>(smem);                    // [2*G] (padded to 16 floats)
+  float* scores = stat + 16;                                       // [G][part_size]
+  float* red = scores + G * part_size;                             // [4][G][D]
+  int* pages = reinterpret_cast<int*>(red + 4 * G * D);            // [part_size/BS]
+
+  const int b = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
+  const int len = seq_lens[b];
+  const int p0 = part * part_size;
+  if (p0 >= len) return;
+  const int n = min(part_size, len - p0);
+  const int nparts = (len + part_size - 1) / part_size;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h0 = kvh * G;
+
+  for (int i = tid; i < (n + BS - 1) / BS; i += 256)
+    pages[i] = block_tables[(int64_t)b * bt_stride + p0 / BS + i];
+
+  // Q^T as the MFMA B operand: column = head (l&15, only < G real), k = dims
+  short8 qf[4];
+  {
+    const int g = lane & 15;
+    const int hh = h0 + (g < G ? g : 0);
+    const bf16_t* qrow = q + (int64_t)b * q_stride + hh * D;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      short8 v = *reinterpret_cast<const short8*>(qrow + kk * 32 + 8 * (lane >> 4));
+      if (g >= G) v = short8{0, 0, 0, 0, 0, 0, 0, 0};
+      qf[kk] = v;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 1: scores. each wave takes 16-key groups round-robin.
+  const int ngroups = (n + 15) / 16;
+  for (int grp = w; grp < ngroups; grp += 4) {
+    const int key = grp * 16 + (lane & 15);      // this lane's A-row key
+    const int kk_ = min(key, n - 1);
+    const int tok = p0 + kk_;
+    const bf16_t* krow = kc + (((int64_t)pages[kk_ / BS] * hkv + kvh) * BS + (tok % BS)) * D;
+    short8 a[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      a[kk] = *reinterpret_cast<const short8*>(krow + kk * 32 + 8 * (lane >> 4));
+    float4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) acc = mfma16(a[kk], qf[kk], acc);
+    // acc[r] = S^T[key grp*16 + 4*(lane>>4) + r][head lane&15]
+    const int g = lane & 15;
+    if (g < G) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kidx = grp * 16 + 4 * (lane >> 4) + r;
+        if (kidx < n) scores[g * part_size + kidx] = acc[r] * scale_log2;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: softmax per head (wave w handles heads w, w+4)
+  for (int g = w; g < G; g += 4) {
+    float m = -INFINITY;
+    for (int i = lane; i < n; i += 64) m = fmaxf(m, scores[g * part_size + i]);
+    m = wave_max(m);
+    float s = 0.f;
+    for (int i = lane; i < n; i += 64) {
+      const float p = exp2f(scores[g * part_size + i] - m);
+      scores[g * part_size + i] = p;
+      s += p;
+    }
+    s = wave_sum(s);
+    if (lane == 0) {
+      stat[2 * g] = m;
+      stat[2 * g + 1] = s;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 3: P.V. lane = (token sub-index tg = lane>>4, dim chunk ch = lane&15)
+  float acc[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+  const int tg = lane >> 4, ch = lane & 15;
+  constexpr int U = 4;
+  for (int base = w * 4; base < n; base += 16 * U) {
+    short8 vv[U];
+    int ti[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ti[u] = base + u * 16 + tg;
+      const int t = min(ti[u], n - 1);
+      const int tok = p0 + t;
+      vv[u] = *reinterpret_cast<const short8*>(
+          vc + (((int64_t)pages[t / BS] * hkv + kvh) * BS + (tok % BS)) * D + ch * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ti[u] < n) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const float p = scores[g * part_size + ti[u]];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[g][j] += p * bf2f((uint16_t)vv[u][j]);
+        }
+      }
+    }
+  }
+  // reduce over the 4 token sub-lanes of the wave
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = acc[g][j];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      acc[g][j] = v;
+    }
+  if (tg == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(w * G + g) * D + ch * 8 + j] = acc[g][j];
+  }
+  __syncthreads();
+  for (int i = tid; i < G * D; i += 256) {
+    const int g = i / D, d = i % D;
+    const float v = red[(0 * G + g) * D + d] + red[(1 * G + g) * D + d] +
+                    red[(2 * G + g) * D + d] + red[(3 * G + g) * D + d];
+    const float inv = 1.f / stat[2 * g + 1];
+    const int h = h0 + g;
+    if (nparts == 1) {
+      out[((int64_t)b * gridDim.y * G + h) * D + d] = f2bf(v * inv);
+    } else {
+      const int64_t slot = ((int64_t)b * gridDim.y * G + h) * max_parts + part;
+      part_o[slot * D + d] = v * inv;
+      if (d == 0) {
+        part_ml[slot * 2] = stat[2 * g];
+        part_ml[slot * 2 + 1] = stat[2 * g + 1];
+      }
+    }
+  }
+}
+
+// grid: (B * Hq)   block: 128
+__global__ __launch_bounds__(128) void decode_reduce_kernel(
+    bf16_t* __restrict__ out, const float* __restrict__ part_o, const float* __restrict__ part_ml,
+    const int* __restrict__ seq_lens, int hq, int part_size, int max_parts) {
+  const int bh = blockIdx.x;
+  const int b = bh / hq;
+  const int len = seq_lens[b];
+  const int nparts = (len + part_size - 1) / part_size;
+  if (nparts <= 1) return;
+  const float* ml = part_ml + (int64_t)bh * max_parts * 2;
+  float m = -INFINITY;
+  for (int p = 0; p < nparts; ++p) m = fmaxf(m, ml[2 * p]);
+  float tot = 0.f, acc = 0.f;
+  const int d = threadIdx.x;
+  for (int p = 0; p < nparts; ++p) {
+    const float wgt = exp2f(ml[2 * p] - m) * ml[2 * p + 1];
+    tot += wgt;
+    acc += wgt * part_o[((int64_t)bh * max_parts + p) * D + d];
+  }
+  out[(int64_t)bh * D + d] = f2bf(acc / tot);
+}
+
+// ============================================================== prefill
+__device__ __forceinline__ int kswz(int row, int ch) { return ch ^ (row & 15); }
+__device__ __forceinline__ int vswz(int row, int ch) {
+  return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
+}
+
+// grid: (Hq, n_tiles)   block: 256 (4 waves x 16 query rows)
+template <int BS>
+__global__ __launch_bounds__(256) void prefill_attn_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+    const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ q_start_loc, const int* __restrict__ seq_lens,
+    const int* __restrict__ tile_seq, const int* __restrict__ tile_q0, int hkv, int64_t q_stride,
+    int64_t out_stride, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 64 * 256];
+  char* Kl = lds;
+  char* Vl = lds + 64 * 256;
+
+  const int h = blockIdx.x, tile = blockIdx.y;
+  const int hq = gridDim.x;
+  const int G = hq / hkv;
+  const int kvh = h / G;
+  const int s = tile_seq[tile], q0 = tile_q0[tile];
+  const int qs = q_start_loc[s], qlen = q_start_loc[s + 1] - qs;
+  const int ctx = seq_lens[s];
+  const int off = ctx - qlen;  // absolute position of query row 0
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int* bt = block_tables + (int64_t)s * bt_stride;
+
+  // query row owned by this lane (as the MFMA column)
+  const int qr = q0 + w * 16 + c16;
+  const bool row_ok = qr < qlen;
+  const int qr_c = row_ok ? qr : qlen - 1;
+  const int qpos = off + qr_c;
+  short8 qf[4];
+  {
+    const bf16_t* qrow = q + (int64_t)(qs + qr_c) * q_stride + h * D;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      qf[kk] = *reinterpret_cast<const short8*>(qrow + kk * 32 + 8 * g4);
+  }
+
+  const int last_row = min(q0 + 63, qlen - 1);
+  const int kv_end = off + last_row + 1;  // keys [0, kv_end)
+  const int ntiles = (kv_end + 63) / 64;
+  const int min_qpos = off + q0;
+
+  float m_run = -INFINITY, l_run = 0.f;
+  float4v o[8];
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb) o[mb] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  short8 kreg[4], vreg[4];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = i * 256 + tid;
+      const int row = c >> 4, ch = c & 15;
+      const int key = t * 64 + row;
+      if (key < kv_end) {
+        const int64_t base = (((int64_t)bt[key / BS] * hkv + kvh) * BS + (key % BS)) * D + ch * 8;
+        kreg[i] = *reinterpret_cast<const short8*>(kc + base);
+        vreg[i] = *reinterpret_cast<const short8*>(vc + base);
+      } else {
+        kreg[i] = short8{0, 0, 0, 0, 0, 0, 0, 0};
+        vreg[i] = short8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+  };
+  auto lwrite = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = i * 256 + tid;
+      const int row = c >> 4, ch = c & 15;
+      *reinterpret_cast<short8*>(Kl + row * 256 + 16 * kswz(row, ch)) = kreg[i];
+      *reinterpret_cast<short8*>(Vl + row * 256 + 16 * vswz(row, ch)) = vreg[i];
+    }
+  };
+
+  gload(0);
+  lwrite();
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) gload(t + 1);
+    const int k0 = t * 64;
+    // ---- S^T = K . Q^T
+    float4v sacc[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      sacc[nb] = float4v{0.f, 0.f, 0.f, 0.f};
+      const int row = nb * 16 + c16;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        short8 a = *reinterpret_cast<const short8*>(Kl + row * 256 + 16 * kswz(row, kk * 4 + g4));
+        sacc[nb] = mfma16(a, qf[kk], sacc[nb]);
+      }
+    }
+    const bool need_mask = (k0 + 63 > min_qpos) || (k0 + 63 >= ctx);
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = sacc[nb][r] * scale_log2;
+        if (need_mask) {
+          const int key = k0 + nb * 16 + g4 * 4 + r;
+          if (key > qpos) v = -INFINITY;
+        }
+        sacc[nb][r] = v;
+        mloc = fmaxf(mloc, v);
+      }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float m_new = fmaxf(m_run, mloc);
+    const float alpha = exp2f(m_run - m_new);
+    float lsum = 0.f;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(sacc[nb][r] - m_new);
+        sacc[nb][r] = p;
+        lsum += p;
+      }
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    l_run = l_run * alpha + lsum;
+    m_run = m_new;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) o[mb] *= alpha;
+
+    // ---- P^T as B operand (k order permuted consistently with the V^T reads)
+    short8 pb[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[ks][j] = (short)f2bf(sacc[2 * ks][j]);
+        pb[ks][4 + j] = (short)f2bf(sacc[2 * ks + 1][j]);
+      }
+    }
+    // ---- O^T += V^T . P^T
+    const int qq = c16 >> 2, pp = c16 & 3;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r1 = ks * 32 + g4 * 4 + qq;
+      const int r2 = r1 + 16;
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        const int ch = 2 * mb + (pp >> 1);
+        typedef short v4s __attribute__((ext_vector_type(4)));
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)(Vl + r1 * 256 + 16 * vswz(r1, ch) + 8 * (pp & 1)));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)(Vl + r2 * 256 + 16 * vswz(r2, ch) + 8 * (pp & 1)));
+        short8 a = short8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[mb] = mfma16(a, pb[ks], o[mb]);
+      }
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      lwrite();
+      __syncthreads();
+    }
+  }
+
+  if (row_ok) {
+    const float inv = 1.f / l_run;
+    bf16_t* orow = out + (int64_t)(qs + qr) * out_stride + h * D;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) {
+      uint2v pk;
+      pk[0] = pack_bf2(o[mb][0] * inv, o[mb][1] * inv);
+      pk[1] = pack_bf2(o[mb][2] * inv, o[mb][3] * inv);
+      *reinterpret_cast<uint2v*>(orow + mb * 16 + g4 * 4) = pk;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// workspace: part_o [B*Hq*max_parts*128] f32, part_ml [B*Hq*max_parts*2] f32
+int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void* q,
+                           const void* k_cache, const void* v_cache, const int* block_tables,
+                           int bt_stride, const int* seq_lens, int B, int hq, int hkv,
+                           int head_dim, int block_size, int64_t q_stride, int part_size,
+                           int max_parts, float scale, hipStream_t s) {
+  if (head_dim != 128) return -1;
+  if (part_size % 64 || part_size % block_size) return -2;
+  if (B == 0) return 0;
+  const int G = hq / hkv;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(B, hkv, max_parts), block(256);
+  const size_t lds = 64 + (size_t)G * part_size * 4 + 4 * G * D * 4 + (part_size / block_size) * 4;
+#define OMNIA_DEC(GG, BB)                                                                     \
+  decode_attn_kernel<GG, BB><<<grid, block, lds, s>>>(                                        \
+      (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, (const bf16_t*)k_cache,               \
+      (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, hkv, q_stride, part_size,   \
+      max_parts, scale_log2)
+#define OMNIA_DEC_BS(GG)                                \
+  if (block_size == 16) OMNIA_DEC(GG, 16);              \
+  else if (block_size == 32) OMNIA_DEC(GG, 32);         \
+  else if (block_size == 64) OMNIA_DEC(GG, 64);         \
+  else return -3;
+  if (G == 1) { OMNIA_DEC_BS(1) }
+  else if (G == 2) { OMNIA_DEC_BS(2) }
+  else if (G == 4) { OMNIA_DEC_BS(4) }
+  else if (G == 8) { OMNIA_DEC_BS(8) }
+  else return -4;
+#undef OMNIA_DEC_BS
+#undef OMNIA_DEC
+  if (max_parts > 1)
+    decode_reduce_kernel<<<B * hq, 128, 0, s>>>((bf16_t*)out, part_o, part_ml, seq_lens, hq,
+                                                part_size, max_parts);
+  return (int)hipGetLastError();
+}
+
+int omnia_prefill_attention(void* out, const void* q, const void* k_cache, const void* v_cache,
+                            const int* block_tables, int bt_stride, const int* q_start_loc,
+                            const int* seq_lens, const int* tile_seq, const int* tile_q0,
+                            int n_tiles, int hq, int hkv, int head_dim, int block_size,
+                            int64_t q_stride, int64_t out_stride, float scale, hipStream_t s) {
+  if (head_dim != 128) return -1;
+  if (hq % hkv) return -2;
+  if (n_tiles == 0) return 0;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(hq, n_tiles), block(256);
+#define OMNIA_PRE(BB)                                                                        \
+  prefill_attn_kernel<BB><<<grid, block, 0, s>>>(                                            \
+      (bf16_t*)out, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache,        \
+      block_tables, bt_stride, q_start_loc, seq_lens, tile_seq, tile_q0, hkv, q_stride,      \
+      out_stride, scale_log2)
+  if (block_size == 16) OMNIA_PRE(16);
+  else if (block_size == 32) OMNIA_PRE(32);
+  else if (block_size == 64) OMNIA_PRE(64);
+  else return -3;
+#undef OMNIA_PRE
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

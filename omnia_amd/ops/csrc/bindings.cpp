@@ -1,0 +1,203 @@
+// Python bindings for the omnia_amd gfx950 kernels.  Each entry validates the
+// operand shapes/dtypes on the host BEFORE launching (a bad launch on the box
+// can take every GPU of the host down), then launches on the current HIP
+// stream so the calls are capturable into hipGraphs by the engine.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int omnia_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows, int d,
+                  int64_t x_stride, int64_t out_stride, float eps, hipStream_t s);
+int omnia_rope_kv(void* q, void* k, const void* v, const int* positions, const float* cos_sin,
+                  void* k_cache, void* v_cache, const int64_t* slots, int T, int hq, int hkv,
+                  int head_dim, int64_t q_stride, int64_t kv_stride, int block_size,
+                  hipStream_t s);
+int omnia_silu_mul(void* out, const void* x, int64_t T, int inter, hipStream_t s);
+int omnia_embedding(void* out, const int* ids, const void* w, int T, int d, int vocab_start,
+                    int vocab_end, hipStream_t s);
+int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void* q,
+                           const void* k_cache, const void* v_cache, const int* block_tables,
+                           int bt_stride, const int* seq_lens, int B, int hq, int hkv,
+                           int head_dim, int block_size, int64_t q_stride, int part_size,
+                           int max_parts, float scale, hipStream_t s);
+int omnia_prefill_attention(void* out, const void* q, const void* k_cache, const void* v_cache,
+                            const int* block_tables, int bt_stride, const int* q_start_loc,
+                            const int* seq_lens, const int* tile_seq, const int* tile_q0,
+                            int n_tiles, int hq, int hkv, int head_dim, int block_size,
+                            int64_t q_stride, int64_t out_stride, float scale, hipStream_t s);
+int omnia_sample(int* out_tok, float* out_logprob, const void* logits, int logits_is_bf16,
+                 int rows, int64_t row_stride, int vocab, const float* temperature,
+                 const int* top_k, const float* top_p, const uint64_t* seeds,
+                 const int64_t* steps, int* counts, const float* freq_pen, const float* pres_pen,
+                 const float* rep_pen, hipStream_t s);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_GPU(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
+#define CHECK_RC(rc, what) TORCH_CHECK((rc) == 0, what " launch failed rc=", (rc))
+
+template <typename T>
+T* opt_ptr(const c10::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_BF16(w);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2, "rmsnorm expects 2-D");
+  TORCH_CHECK(x.stride(1) == 1 && out.stride(1) == 1 && w.is_contiguous(), "inner dim contiguous");
+  const int d = x.size(1);
+  TORCH_CHECK(w.numel() == d && out.size(1) == d && out.size(0) == x.size(0), "shape mismatch");
+  CHECK_RC(omnia_rmsnorm(out.data_ptr(), x.data_ptr(), nullptr, w.data_ptr(), x.size(0), d,
+                         x.stride(0), out.stride(0), (float)eps, cur_stream()), "rmsnorm");
+}
+
+// residual += x ; x = rmsnorm(residual) * w      (both in place)
+void fused_add_rmsnorm(at::Tensor x, at::Tensor residual, at::Tensor w, double eps) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(residual); CHECK_BF16(w);
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && residual.is_contiguous(), "contiguous 2-D");
+  TORCH_CHECK(residual.sizes() == x.sizes() && w.numel() == x.size(1), "shape mismatch");
+  CHECK_RC(omnia_rmsnorm(x.data_ptr(), x.data_ptr(), residual.data_ptr(), w.data_ptr(),
+                         x.size(0), x.size(1), x.stride(0), x.stride(0), (float)eps,
+                         cur_stream()), "fused_add_rmsnorm");
+}
+
+void rope_kv(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor positions, at::Tensor cos_sin,
+             c10::optional<at::Tensor> k_cache, c10::optional<at::Tensor> v_cache,
+             c10::optional<at::Tensor> slots, int64_t hq, int64_t hkv, int64_t block_size) {
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_I32(positions);
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous(), "cos_sin f32");
+  TORCH_CHECK(q.dim() == 2 && k.dim() == 2 && v.dim() == 2, "q/k/v as [T, H*D] views");
+  TORCH_CHECK(q.stride(1) == 1 && k.stride(1) == 1 && v.stride(1) == 1, "inner contiguous");
+  TORCH_CHECK(k.stride(0) == v.stride(0), "k/v share row stride");
+  const int T = q.size(0);
+  const int D = q.size(1) / hq;
+  TORCH_CHECK(D == 128 && k.size(1) == hkv * D && v.size(1) == hkv * D, "head_dim 128");
+  TORCH_CHECK(positions.numel() == T && k.size(0) == T, "T mismatch");
+  TORCH_CHECK(cos_sin.size(1) == D, "cos_sin width");
+  const int64_t* sl = nullptr;
+  void *kc = nullptr, *vc = nullptr;
+  if (slots.has_value() && slots->defined()) {
+    TORCH_CHECK(slots->scalar_type() == at::kLong && slots->numel() == T, "slots int64[T]");
+    TORCH_CHECK(k_cache.has_value() && v_cache.has_value(), "caches required with slots");
+    CHECK_BF16(*k_cache);
+    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == hkv && k_cache->size(2) == block_size &&
+                k_cache->size(3) == D && k_cache->is_contiguous() && v_cache->is_contiguous(),
+                "cache layout [NB, Hkv, BS, D]");
+    sl = slots->data_ptr<int64_t>();
+    kc = k_cache->data_ptr();
+    vc = v_cache->data_ptr();
+  }
+  CHECK_RC(omnia_rope_kv(q.data_ptr(), k.data_ptr(), v.data_ptr(), positions.data_ptr<int>(),
+                         cos_sin.data_ptr<float>(), kc, vc, sl, T, hq, hkv, D, q.stride(0),
+                         k.stride(0), block_size, cur_stream()), "rope_kv");
+}
+
+void silu_mul(at::Tensor out, at::Tensor x) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(out);
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous(), "contiguous");
+  const int64_t inter = out.size(-1);
+  TORCH_CHECK(x.size(-1) == 2 * inter && x.numel() == 2 * out.numel(), "shape mismatch");
+  CHECK_RC(omnia_silu_mul(out.data_ptr(), x.data_ptr(), out.numel() / inter, inter,
+                          cur_stream()), "silu_mul");
+}
+
+void embedding(at::Tensor out, at::Tensor ids, at::Tensor w, int64_t vocab_start) {
+  CHECK_GPU(ids); CHECK_I32(ids); CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(w.is_contiguous() && out.is_contiguous(), "contiguous");
+  TORCH_CHECK(out.size(0) == ids.numel() && out.size(1) == w.size(1), "shape mismatch");
+  CHECK_RC(omnia_embedding(out.data_ptr(), ids.data_ptr<int>(), w.data_ptr(), ids.numel(),
+                           w.size(1), vocab_start, vocab_start + w.size(0), cur_stream()),
+           "embedding");
+}
+
+void decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                      at::Tensor block_tables, at::Tensor seq_lens, at::Tensor part_o,
+                      at::Tensor part_ml, int64_t part_size, double scale) {
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_I32(block_tables); CHECK_I32(seq_lens);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous(),
+              "cache [NB, Hkv, BS, D]");
+  const int hkv = k_cache.size(1), bs = k_cache.size(2), D = k_cache.size(3);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == D, "q [B, Hq, D]");
+  const int B = q.size(0), hq = q.size(1);
+  TORCH_CHECK(out.is_contiguous() && out.size(0) == B && out.size(1) == hq, "out [B, Hq, D]");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1,
+              "block_tables [B, max_blocks]");
+  TORCH_CHECK(seq_lens.numel() >= B, "seq_lens");
+  const int max_ctx = block_tables.size(1) * bs;
+  const int max_parts = (max_ctx + part_size - 1) / part_size;
+  TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat,
+              "workspace f32");
+  TORCH_CHECK(part_o.numel() >= (int64_t)B * hq * max_parts * D &&
+              part_ml.numel() >= (int64_t)B * hq * max_parts * 2, "workspace too small");
+  CHECK_RC(omnia_decode_attention(out.data_ptr(), part_o.data_ptr<float>(),
+                                  part_ml.data_ptr<float>(), q.data_ptr(), k_cache.data_ptr(),
+                                  v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                  block_tables.stride(0), seq_lens.data_ptr<int>(), B, hq, hkv, D,
+                                  bs, q.stride(0), part_size, max_parts, (float)scale,
+                                  cur_stream()), "decode_attention");
+}
+
+void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                       at::Tensor block_tables, at::Tensor q_start_loc, at::Tensor seq_lens,
+                       at::Tensor tile_seq, at::Tensor tile_q0, double scale) {
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_BF16(k_cache);
+  CHECK_I32(block_tables); CHECK_I32(q_start_loc); CHECK_I32(seq_lens); CHECK_I32(tile_seq);
+  CHECK_I32(tile_q0);
+  const int hkv = k_cache.size(1), bs = k_cache.size(2), D = k_cache.size(3);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == D, "q [T, Hq, D]");
+  TORCH_CHECK(out.dim() == 3 && out.stride(2) == 1 && out.stride(1) == D, "out [T, Hq, D]");
+  TORCH_CHECK(tile_seq.numel() == tile_q0.numel(), "tiles");
+  TORCH_CHECK(block_tables.stride(1) == 1, "block_tables rows contiguous");
+  CHECK_RC(omnia_prefill_attention(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(),
+                                   v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                   block_tables.stride(0), q_start_loc.data_ptr<int>(),
+                                   seq_lens.data_ptr<int>(), tile_seq.data_ptr<int>(),
+                                   tile_q0.data_ptr<int>(), tile_seq.numel(), q.size(1), hkv, D,
+                                   bs, q.stride(0), out.stride(0), (float)scale, cur_stream()),
+           "prefill_attention");
+}
+
+void sample(at::Tensor out_tok, c10::optional<at::Tensor> out_logprob, at::Tensor logits,
+            at::Tensor temperature, c10::optional<at::Tensor> top_k,
+            c10::optional<at::Tensor> top_p, c10::optional<at::Tensor> seeds,
+            c10::optional<at::Tensor> steps, c10::optional<at::Tensor> counts,
+            c10::optional<at::Tensor> freq_pen, c10::optional<at::Tensor> pres_pen,
+            c10::optional<at::Tensor> rep_pen) {
+  CHECK_GPU(logits); CHECK_I32(out_tok);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V]");
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat,
+              "logits bf16/f32");
+  const int rows = logits.size(0), vocab = logits.size(1);
+  TORCH_CHECK(out_tok.numel() >= rows && temperature.numel() >= rows, "per-row params");
+  if (counts.has_value() && counts->defined())
+    TORCH_CHECK(counts->scalar_type() == at::kInt && counts->size(0) >= rows &&
+                counts->size(1) == vocab && counts->is_contiguous(), "counts int32 [B, V]");
+  CHECK_RC(omnia_sample(out_tok.data_ptr<int>(), opt_ptr<float>(out_logprob), logits.data_ptr(),
+                        logits.scalar_type() == at::kBFloat16, rows, logits.stride(0), vocab,
+                        temperature.data_ptr<float>(), opt_ptr<int>(top_k), opt_ptr<float>(top_p),
+                        opt_ptr<uint64_t>(seeds), opt_ptr<int64_t>(steps), opt_ptr<int>(counts),
+                        opt_ptr<float>(freq_pen), opt_ptr<float>(pres_pen),
+                        opt_ptr<float>(rep_pen), cur_stream()), "sample");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_omnia_kernels, m) {
+  m.doc() = "omnia_amd hand-written CDNA4 (gfx950) HIP kernels";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
+  m.def("rope_kv", &rope_kv);
+  m.def("silu_mul", &silu_mul);
+  m.def("embedding", &embedding);
+  m.def("decode_attention", &decode_attention);
+  m.def("prefill_attention", &prefill_attention);
+  m.def("sample", &sample);
+  m.attr("arch") = "gfx950";
+}

@@ -1,0 +1,239 @@
+// Fused token sampler -- one 1024-thread workgroup per sequence.
+//
+// Per row: penalties (frequency / presence / repetition from a per-sequence
+// token-count table) -> greedy argmax when temperature == 0, otherwise
+// temperature scaling -> exact top-k threshold (4-pass 8-bit radix select on
+// the order-preserving key of the logits) -> exact top-p threshold (4-pass
+// radix select on probability MASS, applied to the top-k survivors as
+// PromptPack `parameters` define them) -> Gumbel-max draw from the survivors
+// with a counter-based RNG keyed by (seed, step, token index).  Only the token
+// id (and its log-prob under the temperature-scaled distribution) leave the
+// GPU.  Rows stay resident in L2 across the passes (<= 512 KiB per row).
+#include "common.h"
+
+using namespace omnia;
+
+namespace {
+
+constexpr int kThreads = 1024;
+
+__device__ __forceinline__ uint32_t fkey(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+template <typename T>
+__device__ __forceinline__ float load_logit(const T* p, int i);
+template <>
+__device__ __forceinline__ float load_logit<float>(const float* p, int i) { return p[i]; }
+template <>
+__device__ __forceinline__ float load_logit<uint16_t>(const uint16_t* p, int i) {
+  return bf2f(p[i]);
+}
+
+struct RowCtx {
+  const int* counts;
+  float freq, pres, rep, inv_t;
+};
+
+template <typename T>
+__device__ __forceinline__ float value_at(const T* row, int i, const RowCtx& c) {
+  float x = load_logit<T>(row, i);
+  if (c.counts) {
+    const int n = c.counts[i];
+    if (n > 0) {
+      if (c.rep != 1.f) x = x > 0.f ? x / c.rep : x * c.rep;
+      x -= c.freq * (float)n + c.pres;
+    }
+  }
+  return x * c.inv_t;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void sample_kernel(
+    int* __restrict__ out_tok, float* __restrict__ out_logprob, const T* __restrict__ logits,
+    int64_t row_stride, int vocab, const float* __restrict__ temperature,
+    const int* __restrict__ top_k, const float* __restrict__ top_p,
+    const uint64_t* __restrict__ seeds, const int64_t* __restrict__ steps,
+    int* __restrict__ counts, const float* __restrict__ freq_pen,
+    const float* __restrict__ pres_pen, const float* __restrict__ rep_pen) {
+  __shared__ float red_f[kThreads / 64];
+  __shared__ int red_i[kThreads / 64];
+  __shared__ int hist[256];
+  __shared__ float hmass[256];
+  __shared__ uint32_t sh_prefix, sh_mask;
+  __shared__ int sh_k;
+  __shared__ float sh_target;
+
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const T* lr = logits + (int64_t)row * row_stride;
+  const float temp = temperature ? temperature[row] : 0.f;
+  const bool greedy = !(temp > 0.f);
+  RowCtx c;
+  c.counts = counts ? counts + (int64_t)row * vocab : nullptr;
+  c.freq = freq_pen ? freq_pen[row] : 0.f;
+  c.pres = pres_pen ? pres_pen[row] : 0.f;
+  c.rep = rep_pen ? rep_pen[row] : 1.f;
+  c.inv_t = greedy ? 1.f : 1.f / temp;
+
+  // ---- pass A: max (+ argmax)
+  float best = -INFINITY;
+  int besti = 0;
+  for (int i = tid; i < vocab; i += kThreads) {
+    const float x = value_at<T>(lr, i, c);
+    if (x > best) { best = x; besti = i; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(besti, o, 64);
+    if (ob > best || (ob == best && oi < besti)) { best = ob; besti = oi; }
+  }
+  if (lane == 0) { red_f[wid] = best; red_i[wid] = besti; }
+  __syncthreads();
+  float M = red_f[0];
+  int argm = red_i[0];
+  for (int i = 1; i < kThreads / 64; ++i)
+    if (red_f[i] > M || (red_f[i] == M && red_i[i] < argm)) { M = red_f[i]; argm = red_i[i]; }
+  __syncthreads();
+
+  // ---- pass B: partition function of the (temperature-scaled) distribution
+  float z = 0.f;
+  for (int i = tid; i < vocab; i += kThreads) z += __expf(value_at<T>(lr, i, c) - M);
+  const float Z = block_sum(z, red_f);
+  __syncthreads();
+
+  if (greedy) {
+    if (tid == 0) {
+      out_tok[row] = argm;
+      if (out_logprob) out_logprob[row] = -__logf(Z);
+      if (c.counts) counts[(int64_t)row * vocab + argm] += 1;
+    }
+    return;
+  }
+
+  // ---- top-k: exact k-th largest key by radix select
+  uint32_t thr_key = 0;  // keep keys >= thr_key
+  const int k = top_k ? top_k[row] : 0;
+  if (k > 0 && k < vocab) {
+    if (tid == 0) { sh_prefix = 0; sh_mask = 0; sh_k = k; }
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      if (tid < 256) hist[tid] = 0;
+      __syncthreads();
+      const uint32_t pre = sh_prefix, msk = sh_mask;
+      for (int i = tid; i < vocab; i += kThreads) {
+        const uint32_t key = fkey(value_at<T>(lr, i, c));
+        if ((key & msk) == pre) atomicAdd(&hist[(key >> shift) & 255], 1);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int kk = sh_k, b = 255;
+        for (; b > 0; --b) {
+          if (hist[b] >= kk) break;
+          kk -= hist[b];
+        }
+        sh_k = kk;
+        sh_prefix = pre | ((uint32_t)b << shift);
+        sh_mask = msk | (255u << shift);
+      }
+      __syncthreads();
+    }
+    thr_key = sh_prefix;
+  }
+
+  // ---- top-p over the top-k survivors (mass renormalised to the survivors)
+  const float p = top_p ? top_p[row] : 1.f;
+  if (p < 1.f) {
+    float zk = 0.f;
+    for (int i = tid; i < vocab; i += kThreads) {
+      const float x = value_at<T>(lr, i, c);
+      if (fkey(x) >= thr_key) zk += __expf(x - M);
+    }
+    zk = block_sum(zk, red_f);
+    if (tid == 0) { sh_prefix = 0; sh_mask = 0; sh_target = p * zk; }
+    __syncthreads();
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      if (tid < 256) hmass[tid] = 0.f;
+      __syncthreads();
+      const uint32_t pre = sh_prefix, msk = sh_mask;
+      for (int i = tid; i < vocab; i += kThreads) {
+        const float x = value_at<T>(lr, i, c);
+        const uint32_t key = fkey(x);
+        if (key >= thr_key && (key & msk) == pre)
+          atomicAdd(&hmass[(key >> shift) & 255], __expf(x - M));
+      }
+      __syncthreads();
+      if (tid == 0) {
+        float tgt = sh_target;
+        int b = 255;
+        for (; b > 0; --b) {
+          if (hmass[b] >= tgt) break;
+          tgt -= hmass[b];
+        }
+        sh_target = tgt;
+        sh_prefix = pre | ((uint32_t)b << shift);
+        sh_mask = msk | (255u << shift);
+      }
+      __syncthreads();
+    }
+    if (sh_prefix > thr_key) thr_key = sh_prefix;
+  }
+
+  // ---- Gumbel-max draw among survivors
+  const uint64_t seed = seeds ? seeds[row] : 0x5eedull;
+  const uint64_t step = steps ? (uint64_t)steps[row] : 0ull;
+  const uint64_t rs = mix64(seed ^ (step * 0x9e3779b97f4a7c15ull) ^ ((uint64_t)row << 48));
+  float gbest = -INFINITY, xsel = -INFINITY;
+  int gi = argm;
+  for (int i = tid; i < vocab; i += kThreads) {
+    const float x = value_at<T>(lr, i, c);
+    if (fkey(x) >= thr_key) {
+      const float u = uniform01(rs, (uint64_t)i);
+      const float g = x - __logf(-__logf(u));
+      if (g > gbest) { gbest = g; gi = i; xsel = x; }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(gbest, o, 64);
+    const int oi = __shfl_xor(gi, o, 64);
+    const float ox = __shfl_xor(xsel, o, 64);
+    if (ob > gbest || (ob == gbest && oi < gi)) { gbest = ob; gi = oi; xsel = ox; }
+  }
+  __syncthreads();
+  __shared__ float red_x[kThreads / 64];
+  if (lane == 0) { red_f[wid] = gbest; red_i[wid] = gi; red_x[wid] = xsel; }
+  __syncthreads();
+  if (tid == 0) {
+    float bb = red_f[0], bx = red_x[0];
+    int bi = red_i[0];
+    for (int i = 1; i < kThreads / 64; ++i)
+      if (red_f[i] > bb || (red_f[i] == bb && red_i[i] < bi)) {
+        bb = red_f[i]; bi = red_i[i]; bx = red_x[i];
+      }
+    out_tok[row] = bi;
+    if (out_logprob) out_logprob[row] = bx - M - __logf(Z);
+    if (c.counts) counts[(int64_t)row * vocab + bi] += 1;
+  }
+}
+
+}  // namespace
+
+extern "C" int omnia_sample(int* out_tok, float* out_logprob, const void* logits,
+                            int logits_is_bf16, int rows, int64_t row_stride, int vocab,
+                            const float* temperature, const int* top_k, const float* top_p,
+                            const uint64_t* seeds, const int64_t* steps, int* counts,
+                            const float* freq_pen, const float* pres_pen, const float* rep_pen,
+                            hipStream_t s) {
+  if (rows == 0) return 0;
+  if (logits_is_bf16)
+    sample_kernel<uint16_t><<<rows, kThreads, 0, s>>>(
+        out_tok, out_logprob, (const uint16_t*)logits, row_stride, vocab, temperature, top_k,
+        top_p, seeds, steps, counts, freq_pen, pres_pen, rep_pen);
+  else
+    sample_kernel<float><<<rows, kThreads, 0, s>>>(out_tok, out_logprob, (const float*)logits,
+                                                   row_stride, vocab, temperature, top_k, top_p,
+                                                   seeds, steps, counts, freq_pen, pres_pen,
+                                                   rep_pen);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,164 @@
+"""Plain-PyTorch fp32 reference implementations of every hand-written kernel.
+
+These are the numerics oracles for ``tests/test_kernels_gpu.py`` and the CPU
+execution path used by the CPU test-suite (no GPU in the build container).
+They define the exact semantics the HIP kernels must reproduce.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    inv = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (xf * inv * w.float()).to(x.dtype)
+
+
+def fused_add_rmsnorm(x, residual, w, eps):
+    """residual <- x + residual (rounded to the storage dtype); returns norm(residual)*w."""
+    r = (x.float() + residual.float()).to(residual.dtype)
+    return rmsnorm(r, w, eps), r
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, scaling: dict | None = None,
+                 device="cpu") -> torch.Tensor:
+    """[max_pos, head_dim] fp32 table = (cos[D/2] | sin[D/2]) with optional llama3 scaling."""
+    half = head_dim // 2
+    inv_freq = 1.0 / (theta ** (torch.arange(0, half, dtype=torch.float64) * 2.0 / head_dim))
+    if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        factor = scaling.get("factor", 8.0)
+        lo = scaling.get("low_freq_factor", 1.0)
+        hi = scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        low_wl, high_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv_freq
+        smooth = (old / wl - lo) / (hi - lo)
+        scaled = torch.where(wl > low_wl, inv_freq / factor, inv_freq)
+        mid = (wl <= low_wl) & (wl >= high_wl)
+        scaled = torch.where(mid, (1 - smooth) * inv_freq / factor + smooth * inv_freq, scaled)
+        inv_freq = scaled
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv_freq)
+    return torch.cat([f.cos(), f.sin()], dim=-1).float().to(device)
+
+
+def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) -> torch.Tensor:
+    """x: [T, H, D] neox half-rotation."""
+    d = x.shape[-1]
+    half = d // 2
+    cs = cos_sin[positions.long()]
+    cos = cs[:, None, :half]
+    sin = cs[:, None, half:]
+    xf = x.float()
+    x1, x2 = xf[..., :half], xf[..., half:]
+    return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(x.dtype)
+
+
+def write_kv(k_cache, v_cache, k, v, slots):
+    """k/v: [T, Hkv, D]; caches [NB, Hkv, BS, D]."""
+    bs = k_cache.shape[2]
+    blk = (slots // bs).long()
+    off = (slots % bs).long()
+    k_cache[blk, :, off] = k.to(k_cache.dtype)
+    v_cache[blk, :, off] = v.to(v_cache.dtype)
+
+
+def gather_kv(cache, block_table, length):
+    """-> [length, Hkv, D] from paged cache."""
+    bs = cache.shape[2]
+    nb = (length + bs - 1) // bs
+    pages = cache[block_table[:nb].long()]  # [nb, Hkv, BS, D]
+    return pages.permute(0, 2, 1, 3).reshape(nb * bs, cache.shape[1], cache.shape[3])[:length]
+
+
+def paged_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, scale):
+    """Causal attention of each sequence's new queries against its whole paged context.
+
+    q: [T, Hq, D]; returns [T, Hq, D].  Query row i of sequence s sits at absolute
+    position ctx - qlen + i.
+    """
+    out = torch.empty_like(q)
+    hq = q.shape[1]
+    hkv = k_cache.shape[1]
+    g = hq // hkv
+    B = seq_lens.numel()
+    for s in range(B):
+        a, b = int(q_start_loc[s]), int(q_start_loc[s + 1])
+        ctx = int(seq_lens[s])
+        qlen = b - a
+        if qlen == 0:
+            continue
+        kk = gather_kv(k_cache, block_tables[s], ctx).float().repeat_interleave(g, dim=1)
+        vv = gather_kv(v_cache, block_tables[s], ctx).float().repeat_interleave(g, dim=1)
+        qq = q[a:b].float()
+        scores = torch.einsum("qhd,khd->hqk", qq, kk) * scale
+        qpos = torch.arange(ctx - qlen, ctx, device=q.device)[:, None]
+        kpos = torch.arange(ctx, device=q.device)[None, :]
+        scores = scores.masked_fill((kpos > qpos)[None], float("-inf"))
+        p = torch.softmax(scores, dim=-1)
+        out[a:b] = torch.einsum("hqk,khd->qhd", p, vv).to(q.dtype)
+    return out
+
+
+def silu_mul(x: torch.Tensor) -> torch.Tensor:
+    inter = x.shape[-1] // 2
+    g, u = x[..., :inter].float(), x[..., inter:].float()
+    return (torch.nn.functional.silu(g) * u).to(x.dtype)
+
+
+def apply_penalties(logits, counts, freq, pres, rep):
+    x = logits.float().clone()
+    if counts is None:
+        return x
+    seen = counts > 0
+    if rep is not None:
+        r = rep[:, None].float()
+        x = torch.where(seen, torch.where(x > 0, x / r, x * r), x)
+    f = freq[:, None].float() if freq is not None else 0.0
+    p = pres[:, None].float() if pres is not None else 0.0
+    x = torch.where(seen, x - f * counts.float() - p, x)
+    return x
+
+
+def sample_mask(logits, temperature, top_k, top_p):
+    """Boolean [B, V] of tokens allowed after temperature / top-k / top-p (exact semantics)."""
+    B, V = logits.shape
+    x = logits.float() / temperature.clamp_min(1e-6)[:, None]
+    allowed = torch.ones_like(x, dtype=torch.bool)
+    for r in range(B):
+        k = int(top_k[r]) if top_k is not None else 0
+        if 0 < k < V:
+            kth = torch.topk(x[r], k).values[-1]
+            allowed[r] &= x[r] >= kth
+        p = float(top_p[r]) if top_p is not None else 1.0
+        if p < 1.0:
+            xr = torch.where(allowed[r], x[r], torch.tensor(float("-inf")))
+            probs = torch.softmax(xr, -1)
+            sp, idx = probs.sort(descending=True)
+            cum = sp.cumsum(0)
+            # smallest prefix with mass >= p
+            n = int((cum < p).sum().item()) + 1
+            thr = sp[min(n, V) - 1]
+            allowed[r] &= probs >= thr
+    return allowed
+
+
+def sample(logits, temperature, top_k=None, top_p=None, generator=None):
+    """Greedy when temperature == 0 else a draw from the filtered distribution."""
+    B = logits.shape[0]
+    out = torch.empty(B, dtype=torch.int32)
+    for r in range(B):
+        if float(temperature[r]) <= 0:
+            out[r] = int(torch.argmax(logits[r].float()))
+            continue
+        allowed = sample_mask(logits[r:r + 1], temperature[r:r + 1],
+                              None if top_k is None else top_k[r:r + 1],
+                              None if top_p is None else top_p[r:r + 1])[0]
+        x = logits[r].float() / float(temperature[r])
+        x = torch.where(allowed, x, torch.tensor(float("-inf")))
+        probs = torch.softmax(x, -1)
+        out[r] = int(torch.multinomial(probs, 1, generator=generator))
+    return out

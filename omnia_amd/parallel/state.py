@@ -1,0 +1,130 @@
+"""Process-group state: one process per GPU, ``torch.distributed`` over RCCL.
+
+Scaling model (MI355X-first):
+  * DP  -- independent engine replicas, one per GPU (Llama-3-8B fits one GPU
+           with ~250 GB left for KV); sessions are routed session-affine.
+  * TP  -- Megatron column/row split (QKV & gate-up column, O & down row),
+           two all-reduces per layer.  Decode-size all-reduces use the one-shot
+           IPC all-reduce in :mod:`omnia_amd.parallel.custom_allreduce`; RCCL for
+           the rest (and as its oracle).
+  * EP  -- Mixtral experts spread over the TP group, token dispatch/combine by
+           all-to-all (:mod:`omnia_amd.parallel.expert`).
+The backend string ``"nccl"`` IS RCCL on ROCm; ``gloo`` drives the CPU tests.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ParallelState:
+    world_size: int = 1
+    rank: int = 0
+    local_rank: int = 0
+    tp_size: int = 1
+    tp_rank: int = 0
+    dp_size: int = 1
+    dp_rank: int = 0
+    tp_group: object = None
+    dp_group: object = None
+    backend: str = "none"
+    custom_ar: object = None  # CustomAllReduce when available
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_STATE = ParallelState()
+
+
+def get_state() -> ParallelState:
+    return _STATE
+
+
+def set_state(st: ParallelState) -> None:
+    global _STATE
+    _STATE = st
+
+
+def env_world() -> tuple[int, int, int]:
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return ws, rank, local
+
+
+def init_distributed(tp_size: int = 1, backend: str | None = None, device: str | None = None,
+                     timeout_s: int = 600) -> ParallelState:
+    """Initialise torch.distributed from torchrun env vars and carve TP/DP groups.
+
+    Ranks [k*tp, (k+1)*tp) form TP group k; ranks with equal tp_rank form a DP group.
+    """
+    ws, rank, local = env_world()
+    if ws % tp_size:
+        raise ValueError(f"world_size {ws} not divisible by tp_size {tp_size}")
+    use_gpu = device != "cpu" and torch.cuda.is_available()
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    if use_gpu:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    st = ParallelState(world_size=ws, rank=rank, local_rank=local, tp_size=tp_size,
+                       tp_rank=rank % tp_size, dp_size=ws // tp_size, dp_rank=rank // tp_size,
+                       backend=backend if ws > 1 else "none")
+    if ws > 1:
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29500")
+            kw = {}
+            if use_gpu and backend == "nccl":
+                kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+            dist.init_process_group(backend=backend, rank=rank, world_size=ws,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        for k in range(ws // tp_size):
+            ranks = list(range(k * tp_size, (k + 1) * tp_size))
+            g = dist.new_group(ranks) if tp_size > 1 else None
+            if rank in ranks:
+                st.tp_group = g
+        for t in range(tp_size):
+            ranks = list(range(t, ws, tp_size))
+            g = dist.new_group(ranks) if len(ranks) > 1 else None
+            if rank in ranks:
+                st.dp_group = g
+    set_state(st)
+    return st
+
+
+def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
+    st = _STATE
+    if st.tp_size == 1:
+        return x
+    if st.custom_ar is not None and x.is_cuda and st.custom_ar.should_use(x):
+        return st.custom_ar.all_reduce(x)
+    dist.all_reduce(x, group=st.tp_group)
+    return x
+
+
+def tp_all_gather_lastdim(x: torch.Tensor) -> torch.Tensor:
+    st = _STATE
+    if st.tp_size == 1:
+        return x
+    parts = [torch.empty_like(x) for _ in range(st.tp_size)]
+    dist.all_gather(parts, x.contiguous(), group=st.tp_group)
+    return torch.cat(parts, dim=-1)
+
+
+def shard_range(total: int, parts: int, idx: int) -> tuple[int, int]:
+    if total % parts:
+        raise ValueError(f"{total} not divisible by {parts}")
+    n = total // parts
+    return idx * n, (idx + 1) * n
+
+
+def barrier():
+    if dist.is_initialized():
+        dist.barrier()

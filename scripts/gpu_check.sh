@@ -1,0 +1,14 @@
+#!/bin/bash
+# One GPU session: kernel numerics -> smoke -> short bench.  Stops at the first
+# crash/timeout (anything other than a clean pass/fail exit).
+mkdir -p gpurun_out
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "gpu tests rc=$rc"; tail -3 gpurun_out/gpu_tests.log
+ok $rc || exit $rc
+timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 2 --warmup 1} > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
+exit $rc

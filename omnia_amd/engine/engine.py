@@ -82,6 +82,10 @@ class LLMEngine:
             dev = torch.device("cuda", torch.cuda.current_device())
         self.device = dev
         dtype = getattr(torch, cfg.dtype)
+        if dev.type == "cuda":
+            from ..ops.gemm_tuning import enable_tuned_gemms
+
+            self.tuned_gemms = enable_tuned_gemms(dev.index or 0)
         t0 = time.perf_counter()
         self.model = build_model(self.model_cfg, device=dev, dtype=dtype, seed=cfg.seed,
                                  decode_part_size=cfg.decode_part_size)

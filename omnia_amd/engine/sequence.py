@@ -25,7 +25,7 @@ class FinishReason(str, enum.Enum):
     ERROR = "error"
 
 
-@dataclass
+@dataclass(eq=False)  # identity semantics: `in` on lists must not compare token lists
 class Sequence:
     prompt: list[int]
     params: SamplingParams

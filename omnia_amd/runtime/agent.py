@@ -1,0 +1,314 @@
+"""The agent loop: one conversation turn = render -> LLM stream -> tools -> ... -> Done.
+
+Reference behaviour (``internal/runtime/message.go:40-431``, PromptKit pipeline):
+  * the conversation is resumed from the context store or opened fresh with the
+    PromptPack system prompt (``conversation.go:260-276``);
+  * text deltas stream as Chunk frames; server-side tool calls run inside the
+    runtime (policy broker, retry, circuit breaker) and are NOT sent to the
+    facade; client-side tools are emitted as ``ToolCall{execution: CLIENT}`` and
+    the loop blocks for their ``ClientToolResult`` (``message.go:268-357``);
+  * ``tool_policy.max_rounds`` (default 5) and ``max_tool_calls_per_turn``
+    (default 10) bound the loop; ``tool_choice: none`` hides tools;
+  * the turn ends with Done{final_content, usage{input, output, cost}}.
+  * context window: ``ProviderDefaults.contextWindow`` + ``truncationStrategy``
+    (sliding = drop oldest, summarize = fold oldest turns into a summary,
+    custom = warn and fall back to sliding) (``agentruntime_types.go:417-476``).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import time
+import uuid
+from dataclasses import dataclass, field
+
+from ..engine.sampling_params import SamplingParams
+from ..observability import metrics as M
+from ..observability import tracing
+from ..tools.executor import CallContext, OmniaExecutor
+from .chat import Message, ToolCallReq
+from .context_store import StoreUnavailable
+from .promptpack import PromptPack, run_validators
+from .providers import Provider, ProviderEvent, Usage
+
+log = logging.getLogger("omnia.runtime.agent")
+
+
+@dataclass
+class TurnResult:
+    content: str = ""
+    usage: Usage = field(default_factory=Usage)
+    cost: float = 0.0
+    tool_calls: int = 0
+    rounds: int = 0
+    violations: list = field(default_factory=list)
+    ttft: float | None = None
+    finish_reason: str = ""
+
+
+@dataclass
+class AgentConfig:
+    prompt_name: str | None = None
+    variables: dict = field(default_factory=dict)
+    context_window: int = 0  # tokens; 0 = unlimited
+    truncation: str = "sliding"
+    defaults: dict = field(default_factory=dict)  # ProviderDefaults
+    response_format: str = ""  # "" | text | json | json_schema (function mode)
+    response_schema: dict | None = None
+    max_rounds: int | None = None
+
+
+class TurnIO:
+    """Transport hooks for one turn (implemented by the gRPC Converse handler)."""
+
+    async def chunk(self, text: str) -> None:  # pragma: no cover - interface
+        pass
+
+    async def client_tool_calls(self, calls: list[ToolCallReq], meta: dict) -> dict[str, dict]:
+        """Emit CLIENT tool calls and wait for results {call_id: {result_json, is_rejected...}}."""
+        raise RuntimeError("client tools unsupported on this transport")
+
+
+def _approx_tokens(text: str) -> int:
+    return max(1, len(text) // 4)
+
+
+class Agent:
+    def __init__(self, pack: PromptPack, provider: Provider, store, executor: OmniaExecutor | None,
+                 cfg: AgentConfig | None = None, extra_providers: dict | None = None,
+                 memory=None, event_sink=None, evaluator=None, tokenizer=None):
+        self.pack = pack
+        self.provider = provider
+        self.store = store
+        self.executor = executor
+        self.cfg = cfg or AgentConfig()
+        self.extra = extra_providers or {}
+        self.memory = memory  # retriever with async retrieve(session, query, ctx) -> str
+        self.event_sink = event_sink  # async record(kind, session_id, payload)
+        self.evaluator = evaluator
+        self.tokenizer = tokenizer
+        self.prompt = pack.prompt(self.cfg.prompt_name)
+
+    # ------------------------------------------------------------ state
+    def _system_message(self, variables: dict | None) -> Message:
+        vs = {**self.cfg.variables, **(variables or {})}
+        return Message("system", self.pack.render_system(self.prompt, vs))
+
+    async def load_state(self, session_id: str) -> dict | None:
+        return await self.store.load(session_id)
+
+    async def new_state(self, variables=None) -> dict:
+        return {"messages": [self._system_message(variables).to_dict()], "turn": 0,
+                "created": time.time()}
+
+    def params(self, overrides: dict | None = None) -> SamplingParams:
+        d = {}
+        dd = self.cfg.defaults or {}
+        for k_src, k in (("temperature", "temperature"), ("topP", "top_p"),
+                         ("maxTokens", "max_tokens")):
+            if dd.get(k_src) is not None:
+                d[k] = dd[k_src]
+        d.update(self.prompt.parameters or {})
+        d.update(overrides or {})
+        return SamplingParams.from_dict(d)
+
+    def _count(self, m: Message) -> int:
+        if self.tokenizer is not None:
+            return len(self.tokenizer.encode(m.content)) + 4
+        return _approx_tokens(m.content) + 4
+
+    async def _truncate(self, msgs: list[Message], budget: int) -> list[Message]:
+        if budget <= 0:
+            return msgs
+        total = sum(self._count(m) for m in msgs)
+        if total <= budget:
+            return msgs
+        system = [m for m in msgs if m.role == "system"][:1]
+        rest = [m for m in msgs if not (m.role == "system" and system and m is system[0])]
+        strategy = self.cfg.truncation or "sliding"
+        if strategy == "custom":
+            log.warning("custom truncation strategy not supported; falling back to sliding")
+            strategy = "sliding"
+        if strategy == "summarize" and len(rest) > 2:
+            cut = len(rest) // 2
+            old, keep = rest[:cut], rest[cut:]
+            convo = "\n".join(f"{m.role}: {m.content}" for m in old)
+            try:
+                summary, _, _ = await self.provider.complete(
+                    [Message("system", "Summarize the conversation so far in a few sentences."),
+                     Message("user", convo)],
+                    params=SamplingParams(temperature=0.0, max_tokens=128))
+            except Exception:  # noqa: BLE001
+                summary = ""
+            rest = [Message("system", f"Summary of earlier conversation: {summary}")] + keep
+            msgs = system + rest
+            if sum(self._count(m) for m in msgs) <= budget:
+                return msgs
+        # sliding: drop oldest non-system messages (keep tool call/result pairs together)
+        while rest and sum(self._count(m) for m in system + rest) > budget:
+            drop = rest.pop(0)
+            while rest and rest[0].role == "tool" and drop.role == "assistant":
+                rest.pop(0)
+        return system + rest
+
+    # ------------------------------------------------------------ the turn
+    async def run_turn(self, session_id: str, content: str, io: TurnIO, parts: list | None = None,
+                       metadata: dict | None = None, ctx: CallContext | None = None,
+                       variables: dict | None = None, persist: bool = True) -> TurnResult:
+        t_start = time.perf_counter()
+        M.PIPELINES_ACTIVE.inc()
+        ctx = ctx or CallContext(session_id=session_id)
+        res = TurnResult()
+        span = tracing.start_span("omnia.runtime.conversation.turn",
+                                  {"session.id": session_id})
+        try:
+            state = await self.load_state(session_id) if persist else None
+            if state is None:
+                state = await self.new_state(variables)
+            msgs = [Message.from_dict(d) for d in state["messages"]]
+            user = Message("user", content, parts=parts or [])
+            if self.memory is not None:
+                try:
+                    mem = await self.memory.retrieve(session_id, content, ctx)
+                except Exception as e:  # noqa: BLE001
+                    log.warning("memory retrieval failed: %s", e)
+                    mem = ""
+                if mem:
+                    msgs.append(Message("system", f"Relevant memories:\n{mem}"))
+            msgs.append(user)
+            policy = self.prompt.tool_policy
+            tools = []
+            if self.executor is not None and policy.tool_choice != "none":
+                tools = self.pack.tool_specs(self.prompt, self.executor.specs())
+            params = self.params((metadata or {}).get("parameters")
+                                 if isinstance((metadata or {}).get("parameters"), dict) else None)
+            max_rounds = self.cfg.max_rounds or policy.max_rounds
+            text_acc: list[str] = []
+            calls_total = 0
+            while True:
+                window = await self._truncate(msgs, self.cfg.context_window)
+                round_text: list[str] = []
+                round_calls: list[ToolCallReq] = []
+                span_llm = tracing.start_span("genai.chat", {
+                    "gen_ai.system": self.provider.type, "gen_ai.request.model": self.provider.model})
+                t_llm = time.perf_counter()
+                status = "ok"
+                try:
+                    async for ev in self.provider.stream(window, tools, params, session_id,
+                                                         metadata):
+                        if ev.type == "text" and ev.text:
+                            round_text.append(ev.text)
+                            text_acc.append(ev.text)
+                            await io.chunk(ev.text)
+                        elif ev.type == "tool_calls":
+                            round_calls.extend(ev.tool_calls)
+                        elif ev.type == "error":
+                            raise RuntimeError(ev.text or "provider error")
+                        elif ev.type == "done":
+                            if ev.usage:
+                                res.usage += ev.usage
+                            if res.ttft is None and ev.ttft is not None:
+                                res.ttft = ev.ttft
+                            res.finish_reason = ev.finish_reason
+                except Exception:
+                    status = "error"
+                    raise
+                finally:
+                    M.PROVIDER_REQUESTS.labels(self.provider.type, self.provider.model,
+                                               status).inc()
+                    M.PROVIDER_DURATION.labels(self.provider.type, self.provider.model).observe(
+                        time.perf_counter() - t_llm)
+                    tracing.end_span(span_llm, {"gen_ai.usage.input_tokens": res.usage.input_tokens,
+                                                "gen_ai.usage.output_tokens":
+                                                    res.usage.output_tokens})
+                res.rounds += 1
+                msgs.append(Message("assistant", "".join(round_text), tool_calls=round_calls))
+                if not round_calls:
+                    break
+                if res.rounds > max_rounds:
+                    log.warning("max_rounds %d reached; ending turn", max_rounds)
+                    msgs[-1].tool_calls = []
+                    break
+                budget = policy.max_tool_calls_per_turn - calls_total
+                allowed = round_calls[:max(0, budget)]
+                calls_total += len(round_calls)
+                results = await self._run_tools(allowed, io, ctx, metadata or {})
+                for c in round_calls:
+                    r = results.get(c.id) or {"result_json": json.dumps(
+                        {"error": "max_tool_calls_per_turn exceeded"}), "is_error": True}
+                    msgs.append(Message("tool", r["result_json"], tool_call_id=c.id, name=c.name))
+                res.tool_calls = calls_total
+            res.content = "".join(text_acc) if not msgs[-1].content else msgs[-1].content
+            if res.rounds > 1:
+                res.content = msgs[-1].content or "".join(text_acc)
+            res.violations = run_validators(self.prompt, res.content)
+            for v in res.violations:
+                M.VALIDATIONS.labels(v.split(":")[0], "fail").inc()
+            res.cost = self.provider.pricing.cost(res.usage)
+            M.PROVIDER_INPUT_TOKENS.labels(self.provider.type, self.provider.model).inc(
+                res.usage.input_tokens)
+            M.PROVIDER_OUTPUT_TOKENS.labels(self.provider.type, self.provider.model).inc(
+                res.usage.output_tokens)
+            M.PROVIDER_COST.labels(self.provider.type, self.provider.model).inc(res.cost)
+            if persist:
+                state["messages"] = [m.to_dict() for m in msgs
+                                     if not (m.role == "system" and m.content.startswith(
+                                         "Relevant memories:"))]
+                state["turn"] = state.get("turn", 0) + 1
+                try:
+                    await self.store.save(session_id, state)
+                except StoreUnavailable as e:
+                    log.warning("context store save failed: %s", e)
+            if self.event_sink is not None:
+                await self._record(session_id, content, res)
+            if self.evaluator is not None:
+                asyncio.get_running_loop().create_task(
+                    self.evaluator.on_turn(session_id, content, res, self.prompt))
+            return res
+        finally:
+            M.PIPELINES_ACTIVE.dec()
+            M.PIPELINE_DURATION.observe(time.perf_counter() - t_start)
+            tracing.end_span(span, {"gen_ai.usage.input_tokens": res.usage.input_tokens,
+                                    "gen_ai.usage.output_tokens": res.usage.output_tokens,
+                                    "gen_ai.usage.cost": res.cost})
+
+    async def _run_tools(self, calls: list[ToolCallReq], io: TurnIO, ctx: CallContext,
+                         metadata: dict) -> dict[str, dict]:
+        out: dict[str, dict] = {}
+        server = [c for c in calls if not self.executor.is_client_tool(c.name)]
+        client = [c for c in calls if self.executor.is_client_tool(c.name)]
+
+        async def run(c):
+            span = tracing.start_span("omnia.tool.call", {"tool.name": c.name})
+            r, err = await self.executor.execute(c.name, c.arguments, ctx)
+            tracing.end_span(span, {"tool.error": err})
+            out[c.id] = {"result_json": r, "is_error": err}
+
+        if server:
+            await asyncio.gather(*(run(c) for c in server))
+        if client:
+            meta = {c.id: self.executor.tools[c.name].meta for c in client}
+            got = await io.client_tool_calls(client, meta)
+            for c in client:
+                r = got.get(c.id)
+                if r is None:
+                    out[c.id] = {"result_json": json.dumps({"error": "no result"}),
+                                 "is_error": True}
+                elif r.get("is_rejected"):
+                    out[c.id] = {"result_json": json.dumps(
+                        {"rejected": True, "reason": r.get("rejection_reason", "")}),
+                        "is_error": True}
+                else:
+                    out[c.id] = {"result_json": r.get("result_json", "null"), "is_error": False}
+        return out
+
+    async def _record(self, session_id: str, user: str, res: TurnResult):
+        try:
+            await self.event_sink.record(session_id, "provider_call", {
+                "provider": self.provider.type, "model": self.provider.model,
+                "input_tokens": res.usage.input_tokens, "output_tokens": res.usage.output_tokens,
+                "cached_tokens": res.usage.cached_tokens, "cost_usd": res.cost,
+                "rounds": res.rounds, "tool_calls": res.tool_calls})
+        except Exception as e:  # noqa: BLE001
+            log.debug("event sink failed: %s", e)

@@ -1,0 +1,149 @@
+"""Runtime assembly: config -> pack, provider (local engine by default), context
+store, tool executor, policy broker, event recording, memory -> RuntimeService.
+
+Mirrors ``pkg/runtime/promptkit/runtime.go:100-330`` (newFromBuilder / Serve /
+shutdown) and ``internal/runtime/conversation.go:104-257`` (conversation
+options).  ``python -m omnia_amd.runtime`` runs gRPC :9000 + health :9001.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+import signal
+
+from ..observability import metrics as M
+from ..observability import tracing
+from ..tools.executor import OmniaExecutor, PolicyBrokerClient, load_tools_config
+from .agent import Agent, AgentConfig
+from .config import RuntimeConfig
+from .context_store import make_store
+from .promptpack import PackError, PromptPack
+from .providers import build_provider
+from .server import CAPABILITIES, RuntimeService, serve_grpc, serve_health
+
+log = logging.getLogger("omnia.runtime")
+
+_ENGINES: dict = {}
+
+
+def shared_engine(engine_cfg: dict | None = None):
+    """One AsyncLLMEngine per process (the runtime owns the GPU)."""
+    from ..engine.engine import AsyncLLMEngine, EngineConfig
+
+    key = json.dumps(engine_cfg or {}, sort_keys=True)
+    eng = _ENGINES.get(key)
+    if eng is None:
+        kw = {}
+        for k, v in (engine_cfg or {}).items():
+            if k in EngineConfig.__dataclass_fields__:
+                t = EngineConfig.__dataclass_fields__[k].type
+                kw[k] = (int(v) if "int" in str(t) else float(v) if "float" in str(t)
+                         else (str(v).lower() == "true") if "bool" in str(t) else v)
+        eng = AsyncLLMEngine.from_config(EngineConfig.from_env(**kw))
+        _ENGINES[key] = eng
+    return eng
+
+
+def response_format_instruction(fmt: str, schema: dict | None) -> str:
+    """``internal/runtime/response_format.go``: constrain function-mode output."""
+    if fmt in ("json", "json_schema"):
+        s = "\n\nRespond ONLY with a single JSON object and no other text."
+        if fmt == "json_schema" and schema:
+            s += " It must validate against this JSON schema: " + json.dumps(schema)
+        return s
+    return ""
+
+
+async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None = None,
+                        executor: OmniaExecutor | None = None, provider=None,
+                        store=None) -> RuntimeService:
+    if pack is None:
+        try:
+            pack = PromptPack.load(cfg.promptpack_path)
+        except (FileNotFoundError, PackError) as e:
+            log.warning("prompt pack unavailable (%s); using a minimal default pack", e)
+            pack = PromptPack.minimal()
+    ptype = (cfg.provider or {}).get("type", "mock")
+    if provider is None:
+        if ptype in ("local", "omnia", "rocm", "engine") and engine is None:
+            engine = shared_engine(cfg.engine)
+        provider = build_provider(cfg.provider or {"type": "mock"}, engine=engine)
+    extra = {}
+    for p in cfg.extra_providers:
+        try:
+            extra[p.get("role", p.get("name", "extra"))] = build_provider(p, engine=engine)
+        except ValueError as e:
+            log.warning("extra provider skipped: %s", e)
+    store = store or make_store(cfg.context_type, cfg.context_url, cfg.context_ttl_s)
+    if executor is None:
+        policy = PolicyBrokerClient(cfg.policy_broker_url) if cfg.policy_broker_url else None
+        executor = OmniaExecutor(load_tools_config(cfg.tools_config_path),
+                                 secrets_dir=cfg.tool_secrets_dir, policy=policy)
+    try:
+        await executor.discover()
+    except Exception as e:  # noqa: BLE001
+        log.warning("tool discovery failed: %s", e)
+    event_sink = None
+    if cfg.session_api_url:
+        from ..session.httpclient import SessionEventSink
+
+        event_sink = SessionEventSink(cfg.session_api_url)
+    memory = None
+    if cfg.memory_enabled and cfg.memory_api_url:
+        from ..memory.retriever import HTTPMemoryRetriever
+
+        memory = HTTPMemoryRetriever(cfg.memory_api_url, workspace=cfg.workspace_uid or
+                                     cfg.workspace, agent=cfg.agent_name)
+    evaluator = None
+    if cfg.eval_enabled:
+        from .evals import InlineEvaluator
+
+        evaluator = InlineEvaluator(event_sink)
+    acfg = AgentConfig(prompt_name=cfg.prompt_name or None, context_window=cfg.context_window,
+                       truncation=cfg.truncation, defaults=(cfg.provider or {}).get("defaults",
+                                                                                   {}),
+                       response_format=cfg.output_format, response_schema=cfg.output_schema)
+    tok = getattr(engine, "tokenizer", None) if engine is not None else None
+    agent = Agent(pack, provider, store, executor, acfg, extra, memory, event_sink, evaluator,
+                  tokenizer=tok)
+    invoke_agent = agent
+    if cfg.mode == "function" or cfg.output_format:
+        prompt = agent.prompt
+        instr = response_format_instruction(cfg.output_format or "json", cfg.output_schema)
+        fpack = PromptPack(json.loads(json.dumps(pack.data)))
+        for p in fpack.prompts.values():
+            if p.id == prompt.id:
+                p.system_template = p.system_template + instr
+        invoke_agent = Agent(fpack, provider, store, executor, acfg, extra, memory, event_sink,
+                             evaluator, tokenizer=tok)
+    M.RUNTIME_INFO.info({"agent": cfg.agent_name, "namespace": cfg.namespace,
+                         "promptpack": pack.id, "promptpack_version": pack.version,
+                         "provider": provider.type, "contract_version": "1.3.0"})
+    return RuntimeService(agent, capabilities=list(CAPABILITIES), invoke_agent=invoke_agent)
+
+
+async def run(cfg: RuntimeConfig | None = None):
+    cfg = cfg or RuntimeConfig.from_env()
+    logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO").upper(),
+                        format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    if cfg.tracing_enabled:
+        tracing.configure("omnia-runtime", cfg.tracing_endpoint or None, cfg.tracing_sample_rate)
+    svc = await build_runtime(cfg)
+    server, gport = await serve_grpc(svc, cfg.grpc_port)
+    runner, hport = await serve_health(svc, cfg.health_port)
+    log.info("runtime %s/%s serving gRPC :%d health :%d (provider %s)", cfg.namespace,
+             cfg.agent_name, gport, hport, svc.agent.provider.type)
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            loop.add_signal_handler(sig, stop.set)
+        except NotImplementedError:  # pragma: no cover
+            pass
+    await stop.wait()
+    # graceful: stop accepting, drain for 10 s, hard stop (runtime.go:64-67,292-312)
+    svc.ready = False
+    await runner.cleanup()
+    await server.stop(10)

@@ -1,0 +1,130 @@
+"""Runtime configuration (``internal/runtime/config.go:31-316``).
+
+Sources, in priority order (as the reference): the AgentRuntime / Provider CRDs
+read through the cluster API when available (``config_crd.go:56-260``), then the
+``OMNIA_*`` environment injected by the operator, then defaults.  Engine
+settings live under ``OMNIA_ENGINE_*``.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass, field
+
+from .context_store import parse_ttl
+
+
+@dataclass
+class RuntimeConfig:
+    agent_name: str = "agent"
+    namespace: str = "default"
+    workspace: str = ""
+    workspace_uid: str = ""
+    promptpack_path: str = "/etc/omnia/pack"
+    promptpack_name: str = ""
+    promptpack_version: str = ""
+    prompt_name: str = ""
+    mode: str = "agent"  # agent | function
+    output_format: str = ""  # "" | text | json | json_schema
+    output_schema: dict | None = None
+    context_type: str = "memory"
+    context_url: str = ""
+    context_ttl_s: int = 24 * 3600
+    provider: dict = field(default_factory=lambda: {"type": "mock"})
+    extra_providers: list = field(default_factory=list)
+    context_window: int = 0
+    truncation: str = "sliding"
+    tools_config_path: str = "/etc/omnia/tools"
+    tool_secrets_dir: str = "/etc/omnia/tool-secrets"
+    session_api_url: str = ""
+    memory_enabled: bool = False
+    memory_api_url: str = ""
+    policy_broker_url: str = ""
+    eval_enabled: bool = False
+    tracing_enabled: bool = False
+    tracing_endpoint: str = ""
+    tracing_sample_rate: float = 1.0
+    grpc_port: int = 9000
+    health_port: int = 9001
+    engine: dict = field(default_factory=dict)
+
+    @classmethod
+    def from_env(cls, env=None) -> "RuntimeConfig":
+        e = env if env is not None else os.environ
+        c = cls()
+        c.agent_name = e.get("OMNIA_AGENT_NAME", c.agent_name)
+        c.namespace = e.get("OMNIA_NAMESPACE", c.namespace)
+        c.workspace = e.get("OMNIA_WORKSPACE", "")
+        c.workspace_uid = e.get("OMNIA_WORKSPACE_UID", "")
+        c.promptpack_path = e.get("OMNIA_PROMPTPACK_PATH", c.promptpack_path)
+        c.promptpack_name = e.get("OMNIA_PROMPTPACK_NAME", "")
+        c.promptpack_version = e.get("OMNIA_PROMPTPACK_VERSION", "")
+        c.prompt_name = e.get("OMNIA_PROMPT_NAME", "")
+        c.mode = e.get("OMNIA_MODE", c.mode)
+        c.output_format = e.get("OMNIA_OUTPUT_FORMAT", "")
+        if e.get("OMNIA_OUTPUT_SCHEMA"):
+            c.output_schema = json.loads(e["OMNIA_OUTPUT_SCHEMA"])
+        c.context_type = e.get("OMNIA_CONTEXT_TYPE", "redis" if e.get("OMNIA_CONTEXT_URL")
+                               else "memory")
+        c.context_url = e.get("OMNIA_CONTEXT_URL", "")
+        if e.get("OMNIA_CONTEXT_TTL"):
+            c.context_ttl_s = parse_ttl(e["OMNIA_CONTEXT_TTL"])
+        ptype = e.get("OMNIA_PROVIDER_TYPE") or ("mock" if e.get("OMNIA_MOCK_PROVIDER",
+                                                                  "").lower() == "true"
+                                                 else "mock")
+        c.provider = {"type": ptype, "model": e.get("OMNIA_PROVIDER_MODEL", ""),
+                      "baseURL": e.get("OMNIA_PROVIDER_BASE_URL", "")}
+        if e.get("OMNIA_PROVIDER_JSON"):
+            c.provider.update(json.loads(e["OMNIA_PROVIDER_JSON"]))
+        if e.get("OMNIA_MOCK_CONFIG"):
+            c.provider.setdefault("mock", {})["path"] = e["OMNIA_MOCK_CONFIG"]
+        c.context_window = int(e.get("OMNIA_CONTEXT_WINDOW", "0") or 0)
+        c.truncation = e.get("OMNIA_TRUNCATION_STRATEGY", c.truncation)
+        c.tools_config_path = e.get("OMNIA_TOOLS_CONFIG_PATH", c.tools_config_path)
+        c.tool_secrets_dir = e.get("OMNIA_TOOL_SECRETS_PATH", c.tool_secrets_dir)
+        c.session_api_url = e.get("OMNIA_SESSION_API_URL", "")
+        c.memory_enabled = e.get("OMNIA_MEMORY_ENABLED", "false").lower() == "true"
+        c.memory_api_url = e.get("OMNIA_MEMORY_API_URL", "")
+        c.policy_broker_url = e.get("OMNIA_POLICY_BROKER_URL", "")
+        c.eval_enabled = e.get("OMNIA_EVAL_ENABLED", "false").lower() == "true"
+        c.tracing_enabled = e.get("OMNIA_TRACING_ENABLED", "false").lower() == "true"
+        c.tracing_endpoint = e.get("OMNIA_TRACING_ENDPOINT", "")
+        c.tracing_sample_rate = float(e.get("OMNIA_TRACING_SAMPLE_RATE", "1.0"))
+        c.grpc_port = int(e.get("OMNIA_GRPC_PORT", c.grpc_port))
+        c.health_port = int(e.get("OMNIA_HEALTH_PORT", c.health_port))
+        c.engine = {k[len("OMNIA_ENGINE_"):].lower(): v for k, v in e.items()
+                    if k.startswith("OMNIA_ENGINE_")}
+        return c
+
+    def to_env(self) -> dict:
+        """Inverse of from_env (used by the operator's pod builder)."""
+        env = {
+            "OMNIA_AGENT_NAME": self.agent_name, "OMNIA_NAMESPACE": self.namespace,
+            "OMNIA_PROMPTPACK_PATH": self.promptpack_path, "OMNIA_PROMPT_NAME": self.prompt_name,
+            "OMNIA_MODE": self.mode, "OMNIA_CONTEXT_TYPE": self.context_type,
+            "OMNIA_CONTEXT_TTL": f"{self.context_ttl_s}s",
+            "OMNIA_GRPC_PORT": str(self.grpc_port), "OMNIA_HEALTH_PORT": str(self.health_port),
+            "OMNIA_PROVIDER_JSON": json.dumps(self.provider),
+            "OMNIA_TOOLS_CONFIG_PATH": self.tools_config_path,
+            "OMNIA_CONTEXT_WINDOW": str(self.context_window),
+            "OMNIA_TRUNCATION_STRATEGY": self.truncation,
+        }
+        if self.context_url:
+            env["OMNIA_CONTEXT_URL"] = self.context_url
+        if self.output_format:
+            env["OMNIA_OUTPUT_FORMAT"] = self.output_format
+        if self.output_schema is not None:
+            env["OMNIA_OUTPUT_SCHEMA"] = json.dumps(self.output_schema)
+        for k, v in (("OMNIA_SESSION_API_URL", self.session_api_url),
+                     ("OMNIA_MEMORY_API_URL", self.memory_api_url),
+                     ("OMNIA_POLICY_BROKER_URL", self.policy_broker_url),
+                     ("OMNIA_WORKSPACE", self.workspace)):
+            if v:
+                env[k] = v
+        if self.memory_enabled:
+            env["OMNIA_MEMORY_ENABLED"] = "true"
+        if self.eval_enabled:
+            env["OMNIA_EVAL_ENABLED"] = "true"
+        for k, v in self.engine.items():
+            env["OMNIA_ENGINE_" + k.upper()] = str(v)
+        return env

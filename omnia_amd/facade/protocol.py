@@ -1,0 +1,154 @@
+"""WebSocket facade wire protocol (JSON + binary OMNI frames).
+
+JSON shapes mirror ``internal/facade/protocol.go:93-362``: client types
+``message | upload_request | tool_result | tool_call_ack | tool_call_nack |
+hangup``; server types ``connected | chunk | done | tool_call | tool_result |
+error | upload_ready | upload_complete | media_chunk | interrupt |
+session_config``; every server message carries an RFC3339 ``timestamp``.
+
+Binary frames (``internal/facade/binary.go:26-139``): 32-byte big-endian header
+``"OMNI" | version u8 | flags u8 | type u8 | reserved u8 | metaLen u32 |
+payloadLen u32 | sequence u32 | mediaID[12]`` followed by JSON metadata and the
+payload.  Flags: compressed 0x01, chunked 0x02, last 0x04.  Payloads above
+1 MiB are split into 64 KiB chunks.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import json
+import struct
+
+PROTOCOL_VERSION = 1
+
+# client -> server
+MESSAGE = "message"
+UPLOAD_REQUEST = "upload_request"
+TOOL_RESULT = "tool_result"
+TOOL_CALL_ACK = "tool_call_ack"
+TOOL_CALL_NACK = "tool_call_nack"
+HANGUP = "hangup"
+CLIENT_TYPES = {MESSAGE, UPLOAD_REQUEST, TOOL_RESULT, TOOL_CALL_ACK, TOOL_CALL_NACK, HANGUP}
+
+# server -> client
+CONNECTED = "connected"
+CHUNK = "chunk"
+DONE = "done"
+TOOL_CALL = "tool_call"
+ERROR = "error"
+UPLOAD_READY = "upload_ready"
+UPLOAD_COMPLETE = "upload_complete"
+MEDIA_CHUNK = "media_chunk"
+INTERRUPT = "interrupt"
+SESSION_CONFIG = "session_config"
+
+# error codes
+E_INVALID_MESSAGE = "INVALID_MESSAGE"
+E_SESSION_NOT_FOUND = "SESSION_NOT_FOUND"
+E_SESSION_EXPIRED = "SESSION_EXPIRED"
+E_INTERNAL = "INTERNAL_ERROR"
+E_AGENT_UNAVAILABLE = "AGENT_UNAVAILABLE"
+E_TOOL_FAILED = "TOOL_FAILED"
+E_UPLOAD_FAILED = "UPLOAD_FAILED"
+E_MEDIA_NOT_ENABLED = "MEDIA_NOT_ENABLED"
+E_RATE_LIMITED = "RATE_LIMITED"
+E_UNSATISFIABLE_FORMAT = "UNSATISFIABLE_FORMAT"
+
+
+def now_rfc3339() -> str:
+    return _dt.datetime.now(_dt.timezone.utc).isoformat().replace("+00:00", "Z")
+
+
+def server_msg(mtype: str, session_id: str = "", **fields) -> dict:
+    m = {"type": mtype}
+    if session_id:
+        m["session_id"] = session_id
+    for k, v in fields.items():
+        if v is not None and v != "" and v != [] and v != {}:
+            m[k] = v
+    m["timestamp"] = now_rfc3339()
+    return m
+
+
+def connected(session_id: str, binary: bool, max_payload: int, resumed: bool = False) -> dict:
+    return server_msg(CONNECTED, session_id, connected={
+        "capabilities": {"binary_frames": binary, "max_payload_size": max_payload,
+                         "protocol_version": PROTOCOL_VERSION},
+        **({"resumed": True} if resumed else {})})
+
+
+def chunk(session_id: str, content: str, role: str = "") -> dict:
+    return server_msg(CHUNK, session_id, content=content, role=role)
+
+
+def done(session_id: str, content: str, parts=None, usage: dict | None = None) -> dict:
+    return server_msg(DONE, session_id, content=content, parts=parts, usage=usage)
+
+
+def error(session_id: str, code: str, message: str, details: dict | None = None) -> dict:
+    return server_msg(ERROR, session_id, error={"code": code, "message": message,
+                                                **({"details": details} if details else {})})
+
+
+def tool_call(session_id: str, call_id: str, name: str, arguments: dict,
+              consent_message: str = "", categories=None) -> dict:
+    tc = {"id": call_id, "name": name}
+    if arguments:
+        tc["arguments"] = arguments
+    if consent_message:
+        tc["consent_message"] = consent_message
+    if categories:
+        tc["categories"] = list(categories)
+    return server_msg(TOOL_CALL, session_id, tool_call=tc)
+
+
+def parse_client(raw: str | bytes) -> dict:
+    m = json.loads(raw)
+    if not isinstance(m, dict) or m.get("type") not in CLIENT_TYPES:
+        raise ValueError("unknown or missing message type")
+    return m
+
+
+# ------------------------------------------------------------------ binary frames
+MAGIC = b"OMNI"
+HEADER_SIZE = 32
+FLAG_COMPRESSED, FLAG_CHUNKED, FLAG_LAST = 0x01, 0x02, 0x04
+TYPE_MEDIA_CHUNK, TYPE_UPLOAD = 1, 2
+CHUNK_THRESHOLD = 1 << 20
+CHUNK_SIZE = 64 << 10
+_HDR = struct.Struct(">4sBBBBIII12s")
+
+
+def encode_frame(ftype: int, payload: bytes, meta: dict | None = None, seq: int = 0,
+                 media_id: bytes = b"", flags: int = 0) -> bytes:
+    mb = json.dumps(meta or {}, separators=(",", ":")).encode() if meta else b""
+    mid = (media_id or b"")[:12].ljust(12, b"\0")
+    return _HDR.pack(MAGIC, PROTOCOL_VERSION, flags, ftype, 0, len(mb), len(payload), seq,
+                     mid) + mb + payload
+
+
+def decode_frame(buf: bytes) -> dict:
+    if len(buf) < HEADER_SIZE:
+        raise ValueError("frame shorter than header")
+    magic, ver, flags, ftype, _, mlen, plen, seq, mid = _HDR.unpack_from(buf)
+    if magic != MAGIC:
+        raise ValueError("bad magic")
+    if ver != PROTOCOL_VERSION:
+        raise ValueError(f"unsupported frame version {ver}")
+    if HEADER_SIZE + mlen + plen != len(buf):
+        raise ValueError("length mismatch")
+    meta = json.loads(buf[HEADER_SIZE:HEADER_SIZE + mlen]) if mlen else {}
+    return {"version": ver, "flags": flags, "type": ftype, "seq": seq,
+            "media_id": mid.rstrip(b"\0"), "meta": meta,
+            "payload": buf[HEADER_SIZE + mlen:]}
+
+
+def split_payload(ftype: int, payload: bytes, meta: dict | None, media_id: bytes) -> list[bytes]:
+    if len(payload) <= CHUNK_THRESHOLD:
+        return [encode_frame(ftype, payload, meta, 0, media_id, FLAG_LAST)]
+    frames = []
+    n = (len(payload) + CHUNK_SIZE - 1) // CHUNK_SIZE
+    for i in range(n):
+        part = payload[i * CHUNK_SIZE:(i + 1) * CHUNK_SIZE]
+        fl = FLAG_CHUNKED | (FLAG_LAST if i == n - 1 else 0)
+        frames.append(encode_frame(ftype, part, meta if i == 0 else None, i, media_id, fl))
+    return frames

@@ -1,0 +1,433 @@
+"""WebSocket / REST facade server (``internal/facade/server.go``, ``cmd/agent``).
+
+Endpoints on the facade port (8080):
+  GET  /ws  (also /)          WebSocket agent protocol (protocol.py)
+  POST /functions/{name}      function mode: input schema -> Invoke -> output schema
+  GET  /healthz /readyz /metrics
+  A2A (a2a.py) and MCP (mcp.py) routers are mounted when enabled.
+
+Connection semantics (``server_config.go:78-101``, ``connection.go``,
+``message.go``, ``session.go``): 500 connections max, 16 MiB max message,
+30 s ping / 60 s pong, 50 msg/s (burst 100) text and 2 MiB/s (burst 16 MiB)
+media budgets, ONE in-flight message per connection (extra -> RATE_LIMITED,
+connection stays up), ``connected`` frame sent immediately on upgrade, a
+client-supplied foreign session id triggers the HasConversation resume probe
+(NOT_FOUND -> SESSION_EXPIRED, UNAVAILABLE -> INTERNAL_ERROR), the trace id is
+derived from the session UUID, and SIGTERM drains: no new upgrades, live
+sessions get ``drain_timeout`` to finish.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import time
+import uuid
+from dataclasses import dataclass, field
+
+from aiohttp import WSMsgType, web
+
+from ..api.proto import runtime_v1 as pb
+from ..observability import metrics as M
+from ..observability import tracing
+from ..utils import jsonschema
+from ..utils.ratelimit import TokenBucket
+from . import protocol as P
+from .auth import AuthChain, AuthError
+from .handlers import PendingTools, RuntimeHandler, Writer
+
+log = logging.getLogger("omnia.facade")
+
+
+@dataclass
+class FacadeConfig:
+    agent: str = "agent"
+    namespace: str = "default"
+    port: int = 8080
+    max_connections: int = 500
+    max_message_bytes: int = 16 * 2**20
+    ping_interval_s: float = 30.0
+    pong_timeout_s: float = 60.0
+    msg_rate: float = 50.0
+    msg_burst: float = 100.0
+    media_rate: float = 2 * 2**20
+    media_burst: float = 16 * 2**20
+    max_inflight: int = 1
+    max_audio_sessions: int = 8
+    binary_frames: bool = True
+    media_enabled: bool = False
+    drain_timeout_s: float = 30.0
+    functions: dict = field(default_factory=dict)  # name -> {"input_schema", "output_schema"}
+    allowed_origins: list = field(default_factory=list)  # [] = any
+
+
+class _WSWriter(Writer):
+    def __init__(self, ws, labels):
+        self.ws = ws
+        self.labels = labels
+        self.lock = asyncio.Lock()
+
+    async def write(self, msg: dict) -> None:
+        async with self.lock:
+            if not self.ws.closed:
+                await self.ws.send_str(json.dumps(msg, separators=(",", ":")))
+                M.MESSAGES_SENT.labels(*self.labels).inc()
+
+
+class FacadeServer:
+    def __init__(self, cfg: FacadeConfig, handler=None, runtime_client=None,
+                 auth: AuthChain | None = None, recorder=None, media_store=None):
+        self.cfg = cfg
+        self.client = runtime_client
+        self.handler = handler or (RuntimeHandler(runtime_client) if runtime_client else None)
+        self.auth = auth or AuthChain()
+        self.recorder = recorder
+        self.media = media_store
+        self.connections = 0
+        self.draining = False
+        self.sessions: set = set()
+        self.labels = (cfg.agent, cfg.namespace)
+        self._conn_done = asyncio.Event()
+        self.app = web.Application(client_max_size=cfg.max_message_bytes)
+        r = self.app.router
+        r.add_get("/ws", self.ws_handler)
+        r.add_get("/", self.ws_handler)
+        r.add_post("/functions/{name}", self.function_handler)
+        r.add_get("/healthz", self.healthz)
+        r.add_get("/readyz", self.readyz)
+        r.add_get("/metrics", self.metrics)
+        self.runner = None
+
+    # ---------------------------------------------------------------- health
+    async def healthz(self, request):
+        return web.json_response({"status": "ok"})
+
+    async def readyz(self, request):
+        if self.draining:
+            return web.json_response({"ready": False, "reason": "draining"}, status=503)
+        if self.client is not None:
+            try:
+                h = await self.client.health(timeout=2.0)
+                if not h.healthy:
+                    return web.json_response({"ready": False, "reason": "runtime"}, status=503)
+            except Exception:  # noqa: BLE001
+                return web.json_response({"ready": False, "reason": "runtime"}, status=503)
+        return web.json_response({"ready": True})
+
+    async def metrics(self, request):
+        return web.Response(body=M.exposition(), content_type="text/plain")
+
+    # ---------------------------------------------------------------- auth
+    def _authenticate(self, request):
+        peer = request.remote or ""
+        return self.auth.authenticate(request.headers, dict(request.query), peer)
+
+    def _metadata(self, ident, session_id: str, request) -> dict:
+        md = {"x-omnia-agent-name": self.cfg.agent, "x-omnia-namespace": self.cfg.namespace,
+              "x-omnia-session-id": session_id,
+              "x-omnia-request-id": request.headers.get("X-Request-Id", uuid.uuid4().hex)}
+        md.update(ident.to_metadata())
+        tp = request.headers.get("traceparent")
+        if tp:
+            md["traceparent"] = tp
+        return md
+
+    # ---------------------------------------------------------------- websocket
+    async def ws_handler(self, request):
+        if self.draining:
+            return web.Response(status=503, text="draining")
+        if self.connections >= self.cfg.max_connections:
+            return web.Response(status=503, text="too many connections")
+        origin = request.headers.get("Origin")
+        if self.cfg.allowed_origins and origin and origin not in self.cfg.allowed_origins:
+            return web.Response(status=403, text="origin not allowed")
+        try:
+            ident = self._authenticate(request)
+        except AuthError as e:
+            return web.Response(status=401, text=str(e))
+        ws = web.WebSocketResponse(heartbeat=self.cfg.ping_interval_s,
+                                   max_msg_size=self.cfg.max_message_bytes)
+        await ws.prepare(request)
+        self.connections += 1
+        M.CONNECTIONS_ACTIVE.labels(*self.labels).inc()
+        M.CONNECTIONS_TOTAL.labels(*self.labels).inc()
+        binary = request.query.get("binary", "false").lower() == "true" and self.cfg.binary_frames
+        resume = request.query.get("resume")
+        session_id = resume or str(uuid.uuid4())
+        writer = _WSWriter(ws, self.labels)
+        await writer.write(P.connected(session_id, binary, self.cfg.max_message_bytes,
+                                       resumed=bool(resume)))
+        conn = _Connection(self, ws, writer, ident, request, session_id)
+        try:
+            await conn.read_loop()
+        finally:
+            self.connections -= 1
+            M.CONNECTIONS_ACTIVE.labels(*self.labels).dec()
+            for t in list(conn.tasks):
+                t.cancel()
+            if self.connections == 0:
+                self._conn_done.set()
+        return ws
+
+    # ---------------------------------------------------------------- function mode
+    async def function_handler(self, request):
+        """POST /functions/{name} (``internal/facade/functions_handler.go:159-300``)."""
+        name = request.match_info.get("name", "")
+        if not name:
+            return web.json_response({"error": "missing_function_name"}, status=400)
+        try:
+            ident = self._authenticate(request)
+        except AuthError as e:
+            return web.json_response({"error": "unauthorized", "message": str(e)}, status=401)
+        try:
+            raw = await request.read()
+            body = json.loads(raw or b"{}")
+        except Exception:  # noqa: BLE001
+            return web.json_response({"error": "read_body_failed"}, status=400)
+        spec = self.cfg.functions.get(name) or self.cfg.functions.get("*") or {}
+        if spec.get("input_schema"):
+            errs = jsonschema.Validator(spec["input_schema"]).errors(body)
+            if errs:
+                M.FUNCTION_REQUESTS.labels(name, "input_invalid").inc()
+                return web.json_response({"error": "input_invalid",
+                                          "details": [str(e) for e in errs[:10]]}, status=400)
+        inv = str(uuid.uuid4())
+        md = self._metadata(ident, inv, request)
+        if self.recorder is not None:
+            await self.recorder.ensure_session(inv, self.cfg.agent, self.cfg.namespace,
+                                               {"mode": "function", "function": name})
+            await self.recorder.record(inv, "user", json.dumps(body))
+        try:
+            resp = await self.client.invoke(pb.InvocationRequest(
+                input_json=json.dumps(body), invocation_id=inv,
+                metadata={"function": name}), metadata=md, timeout=120)
+        except Exception as e:  # noqa: BLE001
+            log.warning("invoke failed: %s", e)
+            M.FUNCTION_REQUESTS.labels(name, "runtime_error").inc()
+            return web.json_response({"error": "runtime_error"}, status=502)
+        raw_out = resp.output_json
+        try:
+            out = json.loads(raw_out)
+        except json.JSONDecodeError:
+            out = None
+            if spec.get("output_schema") is not None:
+                M.FUNCTION_REQUESTS.labels(name, "output_invalid").inc()
+                return web.json_response({"error": "output_invalid", "raw": raw_out,
+                                          "details": ["output is not JSON"]}, status=502)
+        if spec.get("output_schema") is not None:
+            errs = jsonschema.Validator(spec["output_schema"]).errors(out)
+            if errs:
+                M.FUNCTION_REQUESTS.labels(name, "output_invalid").inc()
+                return web.json_response({"error": "output_invalid", "raw": raw_out,
+                                          "details": [str(e) for e in errs[:10]]}, status=502)
+        if self.recorder is not None:
+            await self.recorder.record(inv, "assistant", raw_out, usage={
+                "input_tokens": resp.usage.input_tokens,
+                "output_tokens": resp.usage.output_tokens, "cost_usd": resp.usage.cost_usd})
+            await self.recorder.close_session(inv)
+        M.FUNCTION_REQUESTS.labels(name, "ok").inc()
+        return web.json_response(out if out is not None else {"output": raw_out},
+                                 headers={"X-Omnia-Invocation-Id": inv,
+                                          "X-Omnia-Duration-Ms": str(resp.duration_ms)})
+
+    # ---------------------------------------------------------------- lifecycle
+    async def start(self, host: str = "0.0.0.0", port: int | None = None) -> int:
+        self.runner = web.AppRunner(self.app)
+        await self.runner.setup()
+        site = web.TCPSite(self.runner, host, self.cfg.port if port is None else port)
+        await site.start()
+        return site._server.sockets[0].getsockname()[1]
+
+    async def drain(self):
+        """SIGTERM: stop upgrades, give live sessions drain_timeout (drain.go:51-92)."""
+        self.draining = True
+        M.DRAINING.set(1)
+        if self.connections:
+            self._conn_done.clear()
+            try:
+                await asyncio.wait_for(self._conn_done.wait(), self.cfg.drain_timeout_s)
+            except asyncio.TimeoutError:
+                pass
+
+    async def stop(self):
+        if self.runner is not None:
+            await self.runner.cleanup()
+
+
+class _Connection:
+    def __init__(self, srv: FacadeServer, ws, writer, ident, request, session_id):
+        self.srv = srv
+        self.ws = ws
+        self.writer = writer
+        self.ident = ident
+        self.request = request
+        self.session_id = session_id
+        self.inflight = 0
+        self.pending = PendingTools()
+        self.text_bucket = TokenBucket(srv.cfg.msg_rate, srv.cfg.msg_burst)
+        self.media_bucket = TokenBucket(srv.cfg.media_rate, srv.cfg.media_burst)
+        self.tasks: set = set()
+        self.session_ensured = False
+
+    async def read_loop(self):
+        labels = self.srv.labels
+        async for m in self.ws:
+            if m.type == WSMsgType.TEXT:
+                M.MESSAGES_RECEIVED.labels(*labels).inc()
+                if not self.text_bucket.allow():
+                    M.RATE_LIMITED.labels("text").inc()
+                    await self.writer.write(P.error(self.session_id, P.E_RATE_LIMITED,
+                                                    "message rate limit exceeded"))
+                    continue
+                try:
+                    msg = P.parse_client(m.data)
+                except (ValueError, json.JSONDecodeError) as e:
+                    await self.writer.write(P.error(self.session_id, P.E_INVALID_MESSAGE,
+                                                    f"invalid message: {e}"))
+                    continue
+                if await self.on_message(msg) == "hangup":
+                    await self.ws.close()
+                    break
+            elif m.type == WSMsgType.BINARY:
+                if not self.media_bucket.allow(len(m.data)):
+                    M.RATE_LIMITED.labels("media").inc()
+                    await self.writer.write(P.error(self.session_id, P.E_RATE_LIMITED,
+                                                    "media rate limit exceeded"))
+                    continue
+                await self.on_binary(m.data)
+            elif m.type in (WSMsgType.ERROR, WSMsgType.CLOSE):
+                break
+        for t in list(self.tasks):
+            await asyncio.gather(t, return_exceptions=True)
+
+    async def on_binary(self, data: bytes):
+        if not self.srv.cfg.media_enabled or self.srv.media is None:
+            await self.writer.write(P.error(self.session_id, P.E_MEDIA_NOT_ENABLED,
+                                            "media uploads are not enabled"))
+            return
+        try:
+            fr = P.decode_frame(data)
+        except ValueError as e:
+            await self.writer.write(P.error(self.session_id, P.E_INVALID_MESSAGE, str(e)))
+            return
+        try:
+            ref = await self.srv.media.put_frame(self.session_id, fr)
+        except Exception as e:  # noqa: BLE001
+            await self.writer.write(P.error(self.session_id, P.E_UPLOAD_FAILED, str(e)))
+            return
+        if ref:
+            await self.writer.write(P.server_msg(P.UPLOAD_COMPLETE, self.session_id,
+                                                 upload_complete=ref))
+
+    async def on_message(self, msg: dict):
+        t = msg["type"]
+        if t == P.HANGUP:
+            return "hangup"
+        if t == P.TOOL_RESULT:
+            tr = msg.get("tool_result") or {}
+            self.pending.result(tr.get("call_id", ""), tr)
+            return None
+        if t == P.TOOL_CALL_ACK:
+            self.pending.ack((msg.get("tool_call_ack") or {}).get("call_id", ""), True)
+            return None
+        if t == P.TOOL_CALL_NACK:
+            n = msg.get("tool_call_nack") or {}
+            self.pending.ack(n.get("call_id", ""), False, n.get("reason", ""))
+            return None
+        if t == P.UPLOAD_REQUEST:
+            if not self.srv.cfg.media_enabled or self.srv.media is None:
+                await self.writer.write(P.error(self.session_id, P.E_MEDIA_NOT_ENABLED,
+                                                "media uploads are not enabled"))
+                return None
+            info = await self.srv.media.upload_url(self.session_id, msg.get("upload_request")
+                                                   or {})
+            await self.writer.write(P.server_msg(P.UPLOAD_READY, self.session_id,
+                                                 upload_ready=info))
+            return None
+        # message
+        if self.inflight >= self.srv.cfg.max_inflight:
+            M.RATE_LIMITED.labels("inflight").inc()
+            await self.writer.write(P.error(self.session_id, P.E_RATE_LIMITED,
+                                            "a message is already in flight"))
+            return None
+        if not msg.get("content") and not msg.get("parts"):
+            await self.writer.write(P.error(self.session_id, P.E_INVALID_MESSAGE,
+                                            "message content is empty"))
+            return None
+        self.inflight += 1
+        task = asyncio.get_running_loop().create_task(self.process(msg))
+        self.tasks.add(task)
+        task.add_done_callback(self.tasks.discard)
+        return None
+
+    async def ensure_session(self, sid: str) -> bool:
+        """Resume probe for a client-chosen foreign session id (session.go:263-372)."""
+        srv = self.srv
+        if sid != self.session_id and srv.client is not None:
+            try:
+                r = await srv.client.has_conversation(sid)
+            except Exception:  # noqa: BLE001
+                r = pb.HasConversationResponse(state=pb.RESUME_STATE_UNAVAILABLE)
+            if r.state == pb.RESUME_STATE_NOT_FOUND:
+                await self.writer.write(P.error(sid, P.E_SESSION_EXPIRED,
+                                                "session has expired or does not exist"))
+                return False
+            if r.state != pb.RESUME_STATE_RESUMABLE:
+                await self.writer.write(P.error(sid, P.E_INTERNAL,
+                                                "session store temporarily unavailable"))
+                return False
+            self.session_id = sid
+        if not self.session_ensured and srv.recorder is not None:
+            try:
+                await srv.recorder.ensure_session(self.session_id, srv.cfg.agent,
+                                                  srv.cfg.namespace,
+                                                  {"user": self.ident.end_user or
+                                                   self.ident.subject})
+            except Exception as e:  # noqa: BLE001
+                log.warning("session ensure failed: %s", e)
+        self.session_ensured = True
+        return True
+
+    async def process(self, msg: dict):
+        srv = self.srv
+        labels = srv.labels
+        t0 = time.perf_counter()
+        M.REQUESTS_INFLIGHT.labels(*labels).inc()
+        status = "ok"
+        sid = msg.get("session_id") or self.session_id
+        span = tracing.start_span("omnia.facade.message", {"session.id": sid},
+                                  trace_id=tracing.session_trace_id(sid),
+                                  link=tracing.parse_traceparent(
+                                      self.request.headers.get("traceparent")))
+        try:
+            if not await self.ensure_session(sid):
+                status = "session_error"
+                return
+            sid = self.session_id
+            if srv.recorder is not None:
+                srv.recorder.submit(sid, "user", msg.get("content", ""))
+            md = srv._metadata(self.ident, sid, self.request)
+            md["traceparent"] = span.traceparent
+            if srv.handler is None:
+                await self.writer.write(P.error(sid, P.E_AGENT_UNAVAILABLE, "no agent handler"))
+                status = "error"
+                return
+            try:
+                res = await srv.handler.handle(sid, msg, self.writer, self.pending, md)
+            except Exception as e:  # noqa: BLE001
+                log.exception("turn failed")
+                await self.writer.write(P.error(sid, P.E_AGENT_UNAVAILABLE,
+                                                "agent unavailable"))
+                status = "error"
+                return
+            if res.get("error"):
+                status = "error"
+            elif srv.recorder is not None:
+                srv.recorder.submit(sid, "assistant", res.get("content", ""),
+                                    usage=res.get("usage"))
+        finally:
+            self.inflight -= 1
+            M.REQUESTS_INFLIGHT.labels(*labels).dec()
+            M.REQUESTS_TOTAL.labels(*labels, status).inc()
+            M.REQUEST_DURATION.labels(*labels).observe(time.perf_counter() - t0)
+            tracing.end_span(span, error=status != "ok")

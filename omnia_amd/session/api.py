@@ -1,0 +1,306 @@
+"""session-api service (``cmd/session-api``, ``internal/session/api``).
+
+REST over the tiered store; message appends publish ``message.appended`` events
+to Redis Streams ``omnia:eval-events:<namespace>``
+(``internal/session/api/event_publisher.go:34,91-98``) for the eval worker;
+per-client-IP rate limiting; optional service-account bearer auth with
+subject / namespace allowlists (TokenReview stand-in: a static token map);
+EE middleware hooks for PII redaction and privacy opt-out.
+
+``python -m omnia_amd.session.api --port 8300 --db /var/lib/omnia/sessions.db``
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import time
+
+from aiohttp import web
+
+from ..observability import metrics as M
+from ..utils.ratelimit import KeyedLimiter
+from .model import (EvalResult, Message, ProviderCall, RuntimeEvent, Session, ToolCall,
+                    STATUS_ACTIVE, TERMINAL)
+from .store import ColdArchive, HotCache, LocalBlobStore, TierError, TieredSessionService, WarmStore
+
+log = logging.getLogger("omnia.session.api")
+
+
+class StreamPublisher:
+    """XADD to omnia:eval-events:<ns> (MAXLEN ~ 100k)."""
+
+    def __init__(self, redis_client, maxlen: int = 100_000):
+        self.r = redis_client
+        self.maxlen = maxlen
+
+    async def __call__(self, ev: dict):
+        ns = ev.get("namespace") or "default"
+        try:
+            await self.r.xadd(f"omnia:eval-events:{ns}", {"event": json.dumps(ev)},
+                              maxlen=self.maxlen)
+        except Exception as e:  # noqa: BLE001 - publishing is best effort
+            log.debug("event publish failed: %s", e)
+
+
+class MemoryPublisher:
+    def __init__(self):
+        self.events: list[dict] = []
+
+    async def __call__(self, ev):
+        self.events.append(ev)
+
+
+def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400.0,
+              tokens: dict | None = None, allowed_namespaces: set | None = None,
+              redactor=None, optout=None) -> web.Application:
+    limiter = KeyedLimiter(rate, burst)
+
+    @web.middleware
+    async def guard(request, handler):
+        if request.path == "/healthz":
+            return await handler(request)
+        if not limiter.allow(request.remote or "?"):
+            return web.json_response({"error": "rate_limited"}, status=429)
+        if tokens is not None:
+            h = request.headers.get("Authorization", "")
+            tok = h[7:] if h.lower().startswith("bearer ") else ""
+            ident = tokens.get(tok)
+            if ident is None:
+                return web.json_response({"error": "unauthorized"}, status=401)
+            sa_ns = ident.split(":")[2] if ident.count(":") >= 3 else ""
+            if allowed_namespaces is not None and sa_ns not in allowed_namespaces \
+                    and ident not in allowed_namespaces:
+                return web.json_response({"error": "forbidden"}, status=403)
+        return await handler(request)
+
+    app = web.Application(middlewares=[guard], client_max_size=32 * 2**20)
+    r = app.router
+
+    def nf(sid):
+        return web.json_response({"error": "session_not_found", "sessionId": sid}, status=404)
+
+    async def healthz(_):
+        return web.json_response({"status": "ok"})
+
+    async def create(request):
+        body = await request.json()
+        s = Session.from_json(body)
+        if optout is not None and optout(s):
+            return web.Response(status=204)
+        s = svc.create(s)
+        return web.json_response(s.to_json(), status=201)
+
+    async def list_sessions(request):
+        q = request.query
+        rows = svc.warm.list_sessions(namespace=q.get("namespace"), agent=q.get("agent"),
+                                      status=q.get("status"), user=q.get("user"),
+                                      before=float(q["before"]) if q.get("before") else None,
+                                      after=float(q["after"]) if q.get("after") else None,
+                                      limit=int(q.get("limit", 100)),
+                                      offset=int(q.get("offset", 0)), q=q.get("q"))
+        return web.json_response({"sessions": [s.to_json() for s in rows],
+                                  "total": len(rows)})
+
+    async def search(request):
+        q = request.query
+        rows = svc.warm.list_sessions(namespace=q.get("namespace"), agent=q.get("agent"),
+                                      q=q.get("q", ""), limit=int(q.get("limit", 50)))
+        return web.json_response({"sessions": [s.to_json() for s in rows]})
+
+    async def get(request):
+        sid = request.match_info["id"]
+        try:
+            v = svc.get(sid, with_messages=False)
+        except TierError:
+            return web.json_response({"error": "store_unavailable"}, status=503)
+        if v is None:
+            return nf(sid)
+        return web.json_response(v[0].to_json())
+
+    async def get_messages(request):
+        sid = request.match_info["id"]
+        try:
+            v = svc.get(sid)
+        except TierError:
+            return web.json_response({"error": "store_unavailable"}, status=503)
+        if v is None:
+            return nf(sid)
+        msgs = v[1]
+        lim = int(request.query.get("limit", 1000))
+        off = int(request.query.get("offset", 0))
+        return web.json_response({"messages": [m.to_json() for m in msgs[off:off + lim]]})
+
+    async def append(request):
+        sid = request.match_info["id"]
+        body = await request.json()
+        m = Message.from_json(body)
+        if redactor is not None:
+            m.content = redactor(m.content)
+        try:
+            m = await svc.append_message(sid, m)
+        except KeyError:
+            return nf(sid)
+        return web.json_response(m.to_json(), status=201)
+
+    def recorder(table, cls):
+        async def post(request):
+            sid = request.match_info["id"]
+            body = await request.json()
+            obj = cls.from_json({**body, "sessionId": sid})
+            try:
+                svc.record(table, sid, obj)
+            except KeyError:
+                return nf(sid)
+            return web.json_response(obj.to_json(), status=201)
+
+        async def get_(request):
+            sid = request.match_info["id"]
+            return web.json_response({table.replace("_", "-"): svc.warm.list_rows(table, sid)})
+
+        return post, get_
+
+    async def eval_results_post(request):
+        body = await request.json()
+        items = body if isinstance(body, list) else body.get("results", [body])
+        out = []
+        for it in items:
+            e = EvalResult.from_json(it)
+            try:
+                svc.record("eval_results", e.session_id, e)
+            except KeyError:
+                return nf(e.session_id)
+            out.append(e.to_json())
+        return web.json_response({"results": out}, status=201)
+
+    async def eval_results_summary(request):
+        sid = request.match_info["id"]
+        rows = svc.warm.list_rows("eval_results", sid)
+        total = len(rows)
+        passed = sum(1 for r in rows if r.get("passed"))
+        return web.json_response({"sessionId": sid, "total": total, "passed": passed,
+                                  "passRate": passed / total if total else 0.0})
+
+    async def eval_aggregate(request):
+        return web.json_response({"evals": svc.warm.aggregate_evals(
+            request.query.get("namespace"))})
+
+    async def provider_aggregate(request):
+        return web.json_response({"groups": svc.warm.aggregate_provider_calls(
+            request.query.get("namespace"), request.query.get("groupBy", "model"))})
+
+    async def provider_usage(request):
+        body = await request.json()
+        svc.warm.provider_usage(body.get("workspace", ""), body)
+        return web.json_response({"ok": True}, status=201)
+
+    async def ttl(request):
+        sid = request.match_info["id"]
+        body = await request.json()
+        try:
+            s = svc.refresh_ttl(sid, float(body.get("ttlSeconds", svc.default_ttl_s)))
+        except KeyError:
+            return nf(sid)
+        return web.json_response(s.to_json())
+
+    async def status(request):
+        sid = request.match_info["id"]
+        body = await request.json()
+        st = body.get("status", STATUS_ACTIVE)
+        if st not in TERMINAL | {STATUS_ACTIVE}:
+            return web.json_response({"error": "invalid_status"}, status=400)
+        try:
+            s = svc.update_status(sid, st, body.get("endedAt"))
+        except KeyError:
+            return nf(sid)
+        return web.json_response(s.to_json())
+
+    async def decorate(request):
+        sid = request.match_info["id"]
+        body = await request.json()
+        try:
+            s = svc.decorate(sid, body.get("tags"), body.get("state"))
+        except KeyError:
+            return nf(sid)
+        return web.json_response(s.to_json())
+
+    async def delete(request):
+        sid = request.match_info["id"]
+        return web.Response(status=204) if svc.delete(sid) else nf(sid)
+
+    async def bulk_delete(request):
+        ns = request.query.get("namespace")
+        if not ns:
+            return web.json_response({"error": "namespace required"}, status=400)
+        before = float(request.query["before"]) if request.query.get("before") else None
+        rows = svc.warm.list_sessions(namespace=ns, agent=request.query.get("agent"),
+                                      before=before, limit=100000)
+        n = sum(1 for s in rows if svc.delete(s.id))
+        M.RETENTION_DELETED.labels("warm").inc(n)
+        return web.json_response({"deleted": n})
+
+    async def delete_by_user(request):
+        body = await request.json()
+        uid = body.get("virtual_user_id", "")
+        if not uid:
+            return web.json_response({"error": "virtual_user_id required"}, status=400)
+        rows = svc.warm.list_sessions(user=uid, limit=100000)
+        n = sum(1 for s in rows if svc.delete(s.id))
+        return web.json_response({"sessions_deleted": n, "errors": []})
+
+    r.add_get("/healthz", healthz)
+    r.add_post("/api/v1/sessions", create)
+    r.add_get("/api/v1/sessions", list_sessions)
+    r.add_delete("/api/v1/sessions", bulk_delete)
+    r.add_get("/api/v1/sessions/search", search)
+    r.add_get("/api/v1/sessions/{id}", get)
+    r.add_delete("/api/v1/sessions/{id}", delete)
+    r.add_get("/api/v1/sessions/{id}/messages", get_messages)
+    r.add_post("/api/v1/sessions/{id}/messages", append)
+    for path, table, cls in (("tool-calls", "tool_calls", ToolCall),
+                             ("provider-calls", "provider_calls", ProviderCall),
+                             ("events", "events", RuntimeEvent)):
+        p, g = recorder(table, cls)
+        r.add_post(f"/api/v1/sessions/{{id}}/{path}", p)
+        r.add_get(f"/api/v1/sessions/{{id}}/{path}", g)
+    r.add_post("/api/v1/eval-results", eval_results_post)
+    r.add_get("/api/v1/eval-results/aggregate", eval_aggregate)
+    r.add_get("/api/v1/sessions/{id}/eval-results",
+              lambda req: _rows(svc, "eval_results", req))
+    r.add_get("/api/v1/sessions/{id}/eval-results/summary", eval_results_summary)
+    r.add_get("/api/v1/provider-calls/aggregate", provider_aggregate)
+    r.add_post("/api/v1/provider-usage", provider_usage)
+    r.add_post("/api/v1/sessions/{id}/ttl", ttl)
+    r.add_patch("/api/v1/sessions/{id}/status", status)
+    r.add_patch("/api/v1/sessions/{id}/stats", status)
+    r.add_patch("/api/v1/sessions/{id}/decorate", decorate)
+    r.add_post("/api/v1/privacy/sessions/delete-by-user", delete_by_user)
+    return app
+
+
+async def _rows(svc, table, request):
+    sid = request.match_info["id"]
+    return web.json_response({"results": svc.warm.list_rows(table, sid)})
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("session-api")
+    ap.add_argument("--port", type=int, default=8300)
+    ap.add_argument("--db", default=":memory:")
+    ap.add_argument("--cold-dir", default="")
+    ap.add_argument("--redis-url", default="")
+    ap.add_argument("--ttl", type=float, default=24 * 3600)
+    a = ap.parse_args(argv)
+    cold = ColdArchive(LocalBlobStore(a.cold_dir)) if a.cold_dir else None
+    pub = None
+    if a.redis_url:
+        from ..utils.resp import RedisClient
+
+        pub = StreamPublisher(RedisClient(a.redis_url))
+    svc = TieredSessionService(HotCache(), WarmStore(a.db), cold, a.ttl, pub)
+    web.run_app(build_app(svc), port=a.port)
+
+
+if __name__ == "__main__":
+    main()

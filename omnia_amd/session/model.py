@@ -1,0 +1,149 @@
+"""Session data model (``internal/session/store.go:40-523``), JSON in the
+reference's camelCase field names so dashboards/clients interoperate."""
+from __future__ import annotations
+
+import time
+import uuid
+from dataclasses import asdict, dataclass, field, fields
+
+ROLE_USER, ROLE_ASSISTANT, ROLE_SYSTEM = "user", "assistant", "system"
+STATUS_ACTIVE, STATUS_COMPLETED, STATUS_ERROR, STATUS_EXPIRED = (
+    "active", "completed", "error", "expired")
+TERMINAL = {STATUS_COMPLETED, STATUS_ERROR, STATUS_EXPIRED}
+
+
+def _camel(s: str) -> str:
+    p = s.split("_")
+    return p[0] + "".join(x.capitalize() for x in p[1:])
+
+
+def _snake(s: str) -> str:
+    out = []
+    for ch in s:
+        if ch.isupper():
+            out.append("_" + ch.lower())
+        else:
+            out.append(ch)
+    return "".join(out)
+
+
+class _JSON:
+    def to_json(self) -> dict:
+        d = {}
+        for f in fields(self):
+            v = getattr(self, f.name)
+            if v in (None, "", [], {}) and f.name not in ("messages",):
+                continue
+            if isinstance(v, list) and v and hasattr(v[0], "to_json"):
+                v = [x.to_json() for x in v]
+            d[_camel(f.name)] = v
+        return d
+
+    @classmethod
+    def from_json(cls, d: dict):
+        names = {f.name for f in fields(cls)}
+        kw = {}
+        for k, v in (d or {}).items():
+            sk = _snake(k) if _snake(k) in names else k
+            if sk in names:
+                kw[sk] = v
+        return cls(**kw)
+
+
+@dataclass
+class Message(_JSON):
+    id: str = field(default_factory=lambda: uuid.uuid4().hex)
+    role: str = ROLE_USER
+    content: str = ""
+    timestamp: float = field(default_factory=time.time)
+    metadata: dict = field(default_factory=dict)
+    input_tokens: int = 0
+    output_tokens: int = 0
+    cost_usd: float = 0.0
+    tool_call_id: str = ""
+    sequence_num: int = 0
+    has_media: bool = False
+    media_types: list = field(default_factory=list)
+
+
+@dataclass
+class Session(_JSON):
+    id: str = field(default_factory=lambda: str(uuid.uuid4()))
+    agent_name: str = ""
+    namespace: str = ""
+    created_at: float = field(default_factory=time.time)
+    updated_at: float = field(default_factory=time.time)
+    expires_at: float = 0.0
+    state: dict = field(default_factory=dict)
+    workspace_name: str = ""
+    status: str = STATUS_ACTIVE
+    ended_at: float = 0.0
+    message_count: int = 0
+    tool_call_count: int = 0
+    total_input_tokens: int = 0
+    total_output_tokens: int = 0
+    estimated_cost_usd: float = 0.0
+    tags: list = field(default_factory=list)
+    last_message_preview: str = ""
+    prompt_pack_name: str = ""
+    prompt_pack_version: str = ""
+    cohort_id: str = ""
+    variant: str = ""
+    virtual_user_id: str = ""
+
+    def is_expired(self, now: float | None = None) -> bool:
+        return bool(self.expires_at) and (now or time.time()) > self.expires_at
+
+
+@dataclass
+class ToolCall(_JSON):
+    id: str = field(default_factory=lambda: uuid.uuid4().hex)
+    session_id: str = ""
+    call_id: str = ""
+    name: str = ""
+    arguments: dict = field(default_factory=dict)
+    result: object = None
+    status: str = "success"  # success | error | pending
+    duration_ms: int = 0
+    execution: str = "server"
+    created_at: float = field(default_factory=time.time)
+
+
+@dataclass
+class ProviderCall(_JSON):
+    id: str = field(default_factory=lambda: uuid.uuid4().hex)
+    session_id: str = ""
+    provider: str = ""
+    model: str = ""
+    input_tokens: int = 0
+    output_tokens: int = 0
+    cached_tokens: int = 0
+    cost_usd: float = 0.0
+    duration_ms: int = 0
+    status: str = "success"
+    created_at: float = field(default_factory=time.time)
+
+
+@dataclass
+class RuntimeEvent(_JSON):
+    id: str = field(default_factory=lambda: uuid.uuid4().hex)
+    session_id: str = ""
+    type: str = ""
+    data: dict = field(default_factory=dict)
+    created_at: float = field(default_factory=time.time)
+
+
+@dataclass
+class EvalResult(_JSON):
+    id: str = field(default_factory=lambda: uuid.uuid4().hex)
+    session_id: str = ""
+    message_id: str = ""
+    eval_id: str = ""
+    eval_type: str = ""
+    passed: bool = True
+    score: float = 0.0
+    details: dict = field(default_factory=dict)
+    source: str = "inline"
+    agent_name: str = ""
+    namespace: str = ""
+    created_at: float = field(default_factory=time.time)

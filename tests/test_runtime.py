@@ -47,6 +47,17 @@ SCEN = {
 }
 
 
+def _run_sync(coro):
+    try:
+        asyncio.get_running_loop()
+    except RuntimeError:
+        return asyncio.run(coro)
+    import concurrent.futures
+
+    with concurrent.futures.ThreadPoolExecutor(1) as ex:
+        return ex.submit(asyncio.run, coro).result()
+
+
 def make_service(store=None):
     pack = PromptPack(PACK)
     calls = []
@@ -61,7 +72,7 @@ def make_service(store=None):
                                                        "categories": ["location"]}}]})
     ex.add_handler(InProcessHandler("builtin", {"get_weather": (
         "weather", {"type": "object"}, weather)}))
-    asyncio.run(ex.discover())
+    _run_sync(ex.discover())
     prov = MockProvider(scenarios=SCEN)
     agent = Agent(pack, prov, store or MemoryContextStore(), ex, AgentConfig())
     return RuntimeService(agent), prov, calls

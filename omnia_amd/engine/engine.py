@@ -274,9 +274,27 @@ class AsyncLLMEngine:
         self._lock = threading.Lock()
         self._wake = threading.Event()
         self._stop = False
+        self._outbox: dict = {}  # loop -> [(queue, event)] flushed once per engine step
         self._thread = threading.Thread(target=self._loop, name="omnia-engine", daemon=True)
         self._thread.start()
         self.error: Exception | None = None
+
+    def _emit(self, loop, q, ev):
+        self._outbox.setdefault(loop, []).append((q, ev))
+
+    @staticmethod
+    def _deliver(batch):
+        for q, ev in batch:
+            q.put_nowait(ev)
+
+    def _flush(self):
+        if self._outbox:
+            out, self._outbox = self._outbox, {}
+            for loop, batch in out.items():
+                try:
+                    loop.call_soon_threadsafe(self._deliver, batch)
+                except RuntimeError:  # loop closed
+                    pass
 
     @classmethod
     def from_config(cls, cfg: EngineConfig) -> "AsyncLLMEngine":
@@ -305,7 +323,9 @@ class AsyncLLMEngine:
                     log.exception("engine step failed")
                     self.error = e
                     self._fail_all(e)
+                self._flush()
             else:
+                self._flush()
                 self._wake.wait(0.05)
                 self._wake.clear()
 
@@ -328,21 +348,21 @@ class AsyncLLMEngine:
         holder = {}
 
         def on_token(s, tok, text):
-            loop.call_soon_threadsafe(q.put_nowait, GenEvent(text=text or "", token=tok))
+            self._emit(loop, q, GenEvent(text=text or "", token=tok))
 
         def on_finish(s):
             ev = GenEvent(finished=True, finish_reason=(s.finish_reason.value
                                                         if s.finish_reason else None),
                           prompt_tokens=len(s.prompt), output_tokens=len(s.output),
                           cached_tokens=s.prefix_hit, ttft=s.ttft())
-            loop.call_soon_threadsafe(q.put_nowait, ev)
+            self._emit(loop, q, ev)
 
         def add():
             try:
                 holder["seq"] = self.engine.add_request(prompt, params, session_id, request_id,
                                                         on_token=on_token, on_finish=on_finish)
             except Exception as e:
-                loop.call_soon_threadsafe(q.put_nowait, e)
+                self._emit(loop, q, e)
 
         self.submit(add)
         try:

@@ -1,0 +1,535 @@
+"""Reconcilers (``internal/controller``).
+
+Each reconciler is ``reconcile(store, ns, name) -> requeue_after | None`` and is
+idempotent.  The manager (manager.py) feeds them from watch events, including
+cross-kind mappings (a PromptPack/Provider/ToolRegistry change re-queues the
+AgentRuntimes that reference it, a Deployment change re-queues its owner).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import time
+
+from ..api import crds
+from ..models.config import REGISTRY as MODEL_REGISTRY
+from ..runtime.promptpack import PackError, PromptPack
+from . import builders as B
+from .apistore import APIStore, NotFound, get_condition, owner_ref, set_condition
+
+log = logging.getLogger("omnia.operator")
+
+PENDING, RUNNING, FAILED = "Pending", "Running", "Failed"
+
+
+def _semver_key(v: str):
+    v = v.lstrip("v")
+    core, _, pre = v.partition("-")
+    nums = [int(x) for x in core.split(".")[:3] if x.isdigit()]
+    while len(nums) < 3:
+        nums.append(0)
+    # a release sorts after its prereleases
+    return (nums, 1 if not pre else 0, pre)
+
+
+def packs_for(store: APIStore, ns: str, pack_name: str) -> list[dict]:
+    return [p for p in store.list("PromptPack", ns)
+            if p["spec"].get("packName") == pack_name or
+            p["metadata"].get("labels", {}).get(B.LABEL_PACK_NAME) == pack_name or
+            p["metadata"]["name"] == pack_name]
+
+
+def resolve_promptpack(store: APIStore, ns: str, ref: dict) -> dict | None:
+    """By exact version, else by track (stable = highest non-prerelease, prerelease =
+    highest overall) (``internal/controller/promptpack_resolve.go:20-70``)."""
+    cands = [p for p in packs_for(store, ns, ref["name"])
+             if (p.get("status") or {}).get("phase") in ("Active", "Superseded", None, "")]
+    if not cands:
+        return None
+    if ref.get("version"):
+        for p in cands:
+            if p["spec"]["version"].lstrip("v") == ref["version"].lstrip("v"):
+                return p
+        return None
+    track = ref.get("track", "stable")
+    pool = cands if track == "prerelease" else [p for p in cands if "-" not in
+                                                 p["spec"]["version"]]
+    if not pool:
+        return None
+    return max(pool, key=lambda p: _semver_key(p["spec"]["version"]))
+
+
+# ===================================================================== PromptPack
+class PromptPackReconciler:
+    kind = "PromptPack"
+
+    def reconcile(self, store: APIStore, ns: str, name: str):
+        pp = store.try_get("PromptPack", name, ns)
+        if pp is None:
+            return None
+        st = pp.get("status") or {}
+        src = pp["spec"]["source"]
+        ref = src.get("configMapRef") or {}
+        cm = store.try_get("ConfigMap", ref.get("name", ""), ns)
+        ok, msg = True, ""
+        if cm is None:
+            ok, msg = False, f"ConfigMap {ref.get('name')} not found"
+        else:
+            raw = (cm.get("data") or {}).get(ref.get("key", "pack.json"))
+            if raw is None:
+                ok, msg = False, "pack.json key missing from ConfigMap"
+            else:
+                try:
+                    pack = PromptPack(json.loads(raw))
+                    st["packId"] = pack.id
+                    st["prompts"] = sorted(pack.prompts)
+                except (json.JSONDecodeError, PackError) as e:
+                    ok, msg = False, str(e)[:300]
+        set_condition(st, "PackContentValid", ok, "Valid" if ok else "Invalid", msg,
+                      pp["metadata"]["generation"])
+        if not ok:
+            st["phase"] = "Failed"
+        else:
+            siblings = [p for p in packs_for(store, ns, pp["spec"]["packName"])
+                        if get_condition(p, "PackContentValid") is None or
+                        get_condition(p, "PackContentValid")["status"] == "True"
+                        or p["metadata"]["name"] == name]
+            newest = max(siblings, key=lambda p: _semver_key(p["spec"]["version"]))
+            st["phase"] = "Active" if newest["metadata"]["name"] == name else "Superseded"
+        st["observedGeneration"] = pp["metadata"]["generation"]
+        pp["status"] = st
+        store.update_status(pp)
+        return None
+
+
+# ===================================================================== Provider
+class ProviderReconciler:
+    kind = "Provider"
+
+    def __init__(self, gpu_count: int | None = None):
+        self.gpu_count = gpu_count
+
+    def reconcile(self, store: APIStore, ns: str, name: str):
+        pv = store.try_get("Provider", name, ns)
+        if pv is None:
+            return None
+        spec, st = pv["spec"], pv.get("status") or {}
+        gen = pv["metadata"]["generation"]
+        cred_ok, cred_msg = True, ""
+        cred = spec.get("credential") or {}
+        if spec["type"] in crds.NEEDS_CREDENTIAL and not cred:
+            cred_ok, cred_msg = False, f"type {spec['type']} requires a credential"
+        if cred.get("secretRef"):
+            sref = cred["secretRef"]
+            sec = store.try_get("Secret", sref["name"], ns)
+            if sec is None:
+                cred_ok, cred_msg = False, f"secret {sref['name']} not found"
+            elif sref.get("key") and sref["key"] not in (sec.get("data") or {}) and \
+                    sref["key"] not in (sec.get("stringData") or {}):
+                cred_ok, cred_msg = False, f"secret {sref['name']} has no key {sref['key']}"
+        set_condition(st, "CredentialValid", cred_ok, "Valid" if cred_ok else "Invalid",
+                      cred_msg, gen)
+        model_ok, model_msg = True, ""
+        if spec["type"] == "local":
+            eng = spec.get("engine") or {}
+            m = eng.get("model") or spec.get("model")
+            from ..models.config import ALIASES
+
+            if (ALIASES.get(m, m)) not in MODEL_REGISTRY:
+                model_ok, model_msg = False, f"unknown engine model {m}"
+            tp = int(eng.get("tp", 1))
+            if self.gpu_count is not None and tp > self.gpu_count:
+                model_ok, model_msg = False, f"engine.tp={tp} exceeds {self.gpu_count} GPUs"
+            cfg = MODEL_REGISTRY.get(ALIASES.get(m, m))
+            if cfg is not None and cfg.num_heads % tp:
+                model_ok, model_msg = False, f"tp={tp} does not divide {cfg.num_heads} heads"
+            st["engine"] = {"model": m, "tp": tp, "kvBytesPerToken":
+                            cfg.kv_bytes_per_token() // tp if cfg else None}
+        set_condition(st, "ModelValid", model_ok, "Valid" if model_ok else "Invalid", model_msg,
+                      gen)
+        ok = cred_ok and model_ok
+        st["phase"] = "Ready" if ok else "Error"
+        set_condition(st, "Ready", ok, "Ready" if ok else "NotReady", cred_msg or model_msg, gen)
+        st["observedGeneration"] = gen
+        pv["status"] = st
+        store.update_status(pv)
+        return None
+
+
+# ===================================================================== ToolRegistry
+class ToolRegistryReconciler:
+    kind = "ToolRegistry"
+
+    def reconcile(self, store: APIStore, ns: str, name: str):
+        tr = store.try_get("ToolRegistry", name, ns)
+        if tr is None:
+            return None
+        st = tr.get("status") or {}
+        tools = []
+        for h in tr["spec"].get("handlers", []):
+            t = h.get("tool")
+            if t:
+                tools.append({"name": t["name"], "description": t.get("description", ""),
+                              "handlerName": h["name"], "handlerType": h["type"],
+                              "status": "Available"})
+            else:
+                tools.append({"name": h["name"] + ".*", "handlerName": h["name"],
+                              "handlerType": h["type"], "status": "Discoverable"})
+        st["discoveredTools"] = tools
+        st["toolCount"] = len(tools)
+        st["phase"] = "Ready"
+        set_condition(st, "Ready", True, "HandlersValid", "", tr["metadata"]["generation"])
+        st["observedGeneration"] = tr["metadata"]["generation"]
+        tr["status"] = st
+        store.update_status(tr)
+        probe = tr["spec"].get("probe") or {}
+        return 60.0 if probe.get("enabled") else None
+
+
+# ===================================================================== AgentRuntime
+class AgentRuntimeReconciler:
+    kind = "AgentRuntime"
+
+    def __init__(self, gpu_count: int | None = None):
+        self.gpu_count = gpu_count
+
+    def _fail(self, store, ar, st, cond, reason, msg, phase=PENDING):
+        set_condition(st, cond, False, reason, msg, ar["metadata"]["generation"])
+        set_condition(st, "Ready", False, reason, msg, ar["metadata"]["generation"])
+        st["phase"] = phase
+        ar["status"] = st
+        store.update_status(ar)
+        return 10.0
+
+    def reconcile(self, store: APIStore, ns: str, name: str):
+        ar = store.try_get("AgentRuntime", name, ns)
+        if ar is None:
+            return None
+        md = ar["metadata"]
+        if md.get("deletionTimestamp"):
+            md["finalizers"] = [f for f in md.get("finalizers", []) if f != B.FINALIZER]
+            store.update(ar)
+            return None
+        if B.FINALIZER not in md.get("finalizers", []):
+            md.setdefault("finalizers", []).append(B.FINALIZER)
+            ar = store.update(ar)
+        spec = ar["spec"]
+        st = ar.get("status") or {}
+        st["observedGeneration"] = ar["metadata"]["generation"]
+        gen = ar["metadata"]["generation"]
+        # ---- references
+        pack = resolve_promptpack(store, ns, spec["promptPackRef"])
+        if pack is None:
+            return self._fail(store, ar, st, "PromptPackReady", "NotFound",
+                              f"no PromptPack matches {spec['promptPackRef']}")
+        if (pack.get("status") or {}).get("phase") == "Failed":
+            return self._fail(store, ar, st, "PromptPackReady", "Invalid",
+                              "referenced PromptPack failed validation", FAILED)
+        set_condition(st, "PromptPackReady", True, "Resolved", pack["spec"]["version"], gen)
+        providers = []
+        for pref in spec.get("providers") or []:
+            ref = pref.get("providerRef") or {"name": pref.get("name")}
+            pns = ref.get("namespace") or ns
+            pv = store.try_get("Provider", ref["name"], pns)
+            if pv is None:
+                return self._fail(store, ar, st, "ProviderReady", "NotFound",
+                                  f"Provider {ref['name']} not found")
+            if (pv.get("status") or {}).get("phase") != "Ready":
+                return self._fail(store, ar, st, "ProviderReady", "NotReady",
+                                  f"Provider {ref['name']} is not Ready")
+            want_role = pref.get("role")
+            if want_role and pv["spec"].get("role", "llm") != want_role:
+                return self._fail(store, ar, st, "ProviderReady", "RoleMismatch",
+                                  f"Provider {ref['name']} has role "
+                                  f"{pv['spec'].get('role', 'llm')}, want {want_role}")
+            caps = set(pv["spec"].get("capabilities") or [])
+            missing = [c for c in pref.get("requiredCapabilities") or [] if caps and c not in caps]
+            if missing:
+                return self._fail(store, ar, st, "ProviderReady", "CapabilityMissing",
+                                  f"Provider {ref['name']} lacks {missing}")
+            providers.append(pv)
+        set_condition(st, "ProviderReady", True, "Resolved",
+                      ",".join(p["metadata"]["name"] for p in providers) or "mock", gen)
+        registry = None
+        trr = spec.get("toolRegistryRef")
+        if trr:
+            if trr.get("namespace") and trr["namespace"] != ns:
+                return self._fail(store, ar, st, "ToolRegistryReady", "CrossNamespace",
+                                  "cross-namespace ToolRegistry references are not allowed",
+                                  FAILED)
+            registry = store.try_get("ToolRegistry", trr["name"], ns)
+            if registry is None:
+                return self._fail(store, ar, st, "ToolRegistryReady", "NotFound",
+                                  f"ToolRegistry {trr['name']} not found")
+            set_condition(st, "ToolRegistryReady", True, "Resolved", "", gen)
+        set_condition(st, "FrameworkReady", True, "Resolved",
+                      (spec.get("framework") or {}).get("type", "omnia-mi355x"), gen)
+        # ---- capability gate: a local engine needs GPUs on the node
+        rc = B.runtime_config(ar, pack, providers, registry)
+        replicas = None
+        cap_ok = True
+        if rc.provider.get("type") == "local" and self.gpu_count is not None:
+            need = int(rc.engine.get("tp", 1))
+            if need > self.gpu_count:
+                cap_ok = False
+                replicas = 0
+        set_condition(st, "CapabilitiesSatisfied", cap_ok,
+                      "CapabilitiesSatisfied" if cap_ok else "CapabilitiesMissing",
+                      "" if cap_ok else "insufficient GPUs for engine.tp", gen)
+        # ---- owned objects
+        store.apply(B.tools_configmap(ar, registry))
+        pack_cm = pack["spec"]["source"].get("configMapRef", {}).get("name", "")
+        a = ((spec.get("runtime") or {}).get("autoscaling") or {})
+        if a.get("enabled") and replicas is None:
+            cur = store.try_get("Deployment", name, ns)
+            if cur is not None:
+                replicas = cur["spec"].get("replicas")
+        dep = B.deployment(ar, rc, pack_cm, "stable", replicas,
+                           extra_hash=[pack["spec"]["version"], (registry or {}).get("spec")])
+        store.apply(dep)
+        store.apply(B.service(ar))
+        want_r = dep["spec"]["replicas"]
+        if want_r and want_r > 1:
+            store.apply(B.pdb(ar))
+        else:
+            store.delete("PodDisruptionBudget", name, ns)
+        # autoscaling
+        if a.get("enabled"):
+            if a.get("type", "hpa") == "keda":
+                store.apply(B.scaled_object(ar, a))
+                store.delete("HorizontalPodAutoscaler", name, ns)
+            else:
+                store.apply(B.hpa(ar, a))
+                store.delete("ScaledObject", name, ns)
+            set_condition(st, "AutoscalingReady", True, "Scaling", a.get("type", "hpa"), gen)
+        else:
+            store.delete("ScaledObject", name, ns)
+            store.delete("HorizontalPodAutoscaler", name, ns)
+            set_condition(st, "AutoscalingReady", True, "Disabled", "", gen)
+        requeue = self._rollout(store, ar, st, rc, pack_cm, pack)
+        # ---- status from the Deployment
+        d = store.try_get("Deployment", name, ns) or {}
+        ds = d.get("status") or {}
+        st["replicas"] = {"desired": d.get("spec", {}).get("replicas", 0),
+                          "ready": ds.get("readyReplicas", 0),
+                          "available": ds.get("availableReplicas", 0)}
+        st["activeVersion"] = pack["spec"]["version"]
+        svc = store.try_get("Service", name, ns) or {}
+        ep = (svc.get("status") or {}).get("endpoint") or \
+            f"{name}.{ns}.svc.cluster.local:{B.FACADE_PORT}"
+        st["serviceEndpoint"] = ep
+        st["facade"] = {"endpoints": [{"type": f["type"], "url": (
+            f"ws://{ep}/ws" if f["type"] == "websocket" else f"http://{ep}")}
+            for f in spec.get("facades", [])]}
+        dep_ok = st["replicas"]["ready"] > 0
+        set_condition(st, "DeploymentReady", dep_ok, "Available" if dep_ok else "Progressing",
+                      "", gen)
+        set_condition(st, "ServiceReady", bool(svc), "Created", "", gen)
+        if not cap_ok:
+            st["phase"] = PENDING
+        else:
+            st["phase"] = RUNNING if dep_ok else PENDING
+        set_condition(st, "Ready", dep_ok and cap_ok, "Ready" if dep_ok else "Pending", "", gen)
+        ar["status"] = st
+        store.update_status(ar)
+        if not dep_ok:
+            return 2.0
+        return requeue
+
+    # ---------------------------------------------------------------- rollout
+    def _rollout(self, store, ar, st, rc, pack_cm, pack):
+        """Canary rollout (``internal/controller/rollout.go:73-851``): candidate
+        Deployment + setWeight/pause/analysis steps; promote on completion,
+        roll back on a failed analysis."""
+        spec, md = ar["spec"], ar["metadata"]
+        ro = spec.get("rollout") or {}
+        ns, name = md["namespace"], md["name"]
+        cand_spec = ro.get("candidate")
+        if not cand_spec:
+            store.delete("Deployment", name + "-candidate", ns)
+            if st.get("rollout"):
+                st.pop("rollout")
+            set_condition(st, "RolloutActive", False, "NoRollout", "", md["generation"])
+            return None
+        ros = st.get("rollout") or {"currentStep": 0, "weight": 0, "phase": "Progressing",
+                                    "stepStarted": time.time()}
+        cand_ar = json.loads(json.dumps(ar))
+        if cand_spec.get("promptPackVersion"):
+            cand_ar["spec"]["promptPackRef"] = {"name": spec["promptPackRef"]["name"],
+                                                "version": cand_spec["promptPackVersion"]}
+        cand_pack = resolve_promptpack(store, ns, cand_ar["spec"]["promptPackRef"]) or pack
+        steps = ro.get("steps") or [{"setWeight": 100}]
+        if ros["phase"] == "Progressing":
+            store.apply(B.deployment(cand_ar, rc, cand_pack["spec"]["source"]["configMapRef"][
+                "name"], "candidate", 1, extra_hash=[cand_pack["spec"]["version"]]))
+            i = ros["currentStep"]
+            if i >= len(steps):
+                ros["phase"] = "Promoted"
+                ros["weight"] = 100
+                ros["promotedVersion"] = cand_pack["spec"]["version"]
+            else:
+                stp = steps[i]
+                if "setWeight" in stp:
+                    ros["weight"] = stp["setWeight"]
+                    ros["currentStep"] = i + 1
+                    ros["stepStarted"] = time.time()
+                elif "pause" in stp:
+                    from ..runtime.context_store import parse_ttl
+
+                    dur = parse_ttl((stp["pause"] or {}).get("duration", "0s")) or 0
+                    if time.time() - ros["stepStarted"] >= dur:
+                        ros["currentStep"] = i + 1
+                        ros["stepStarted"] = time.time()
+                elif "analysis" in stp:
+                    verdict = self._analysis(store, ns, stp["analysis"])
+                    if verdict is False:
+                        ros["phase"] = "RolledBack"
+                        ros["weight"] = 0
+                    elif verdict is True:
+                        ros["currentStep"] = i + 1
+                        ros["stepStarted"] = time.time()
+        if ros["phase"] == "Promoted":
+            store.delete("Deployment", name + "-candidate", ns)
+        if ros["phase"] == "RolledBack" and (ro.get("rollback") or {}).get("mode",
+                                                                            "automatic") != "manual":
+            store.delete("Deployment", name + "-candidate", ns)
+        st["rollout"] = ros
+        active = ros["phase"] == "Progressing"
+        set_condition(st, "RolloutActive", active, ros["phase"], f"weight={ros['weight']}",
+                      md["generation"])
+        set_condition(st, "TrafficRouting", True, "WeightedService", f"candidate={ros['weight']}%",
+                      md["generation"])
+        return 1.0 if active else None
+
+    def _analysis(self, store, ns, a):
+        ra = store.try_get("RolloutAnalysis", (a or {}).get("templateName", ""), ns)
+        if ra is None:
+            return None
+        res = (ra.get("status") or {}).get("result")
+        if res == "Failed":
+            return False
+        if res == "Successful":
+            return True
+        return None
+
+
+# ===================================================================== Workspace
+class WorkspaceReconciler:
+    """Namespace, service accounts, RBAC, network policy, storage and the
+    per-service-group session-api / memory-api (``workspace_services.go``)."""
+
+    kind = "Workspace"
+
+    def reconcile(self, store: APIStore, ns_unused, name: str):
+        ws = store.try_get("Workspace", name, None)
+        if ws is None:
+            return None
+        spec, st = ws["spec"], ws.get("status") or {}
+        nsname = spec["namespace"]["name"]
+        own = [owner_ref(ws)]
+        if spec["namespace"].get("create", True):
+            store.apply({"apiVersion": "v1", "kind": "Namespace", "metadata": {
+                "name": nsname, "labels": {"omnia.altairalabs.ai/workspace": name,
+                                           **(spec["namespace"].get("labels") or {})},
+                "ownerReferences": own}})
+        for role in ("owner", "editor", "viewer"):
+            store.apply({"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {
+                "name": f"workspace-{name}-{role}-sa", "namespace": nsname,
+                "ownerReferences": own}})
+        for i, rb in enumerate(spec.get("roleBindings") or []):
+            store.apply({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding",
+                         "metadata": {"name": f"workspace-{name}-{i}", "namespace": nsname,
+                                      "ownerReferences": own},
+                         "roleRef": {"kind": "ClusterRole",
+                                     "name": f"omnia-workspace-{rb.get('role', 'viewer')}"},
+                         "subjects": rb.get("groups") or rb.get("subjects") or []})
+        np = spec.get("networkPolicy") or {}
+        if np.get("isolate"):
+            store.apply({"apiVersion": "networking.k8s.io/v1", "kind": "NetworkPolicy",
+                         "metadata": {"name": f"workspace-{name}-isolation",
+                                      "namespace": nsname, "ownerReferences": own},
+                         "spec": {"podSelector": {}, "policyTypes": ["Ingress", "Egress"],
+                                  "ingress": [{"from": [{"podSelector": {}}] +
+                                               (np.get("allowFrom") or [])}],
+                                  "egress": [{"to": [{"podSelector": {}}] +
+                                              (np.get("allowTo") or [])}]}})
+        stor = spec.get("storage") or {}
+        if stor.get("enabled"):
+            store.apply({"apiVersion": "v1", "kind": "PersistentVolumeClaim",
+                         "metadata": {"name": f"workspace-{name}-storage", "namespace": nsname,
+                                      "ownerReferences": own},
+                         "spec": {"accessModes": stor.get("accessModes", ["ReadWriteMany"]),
+                                  "resources": {"requests": {"storage": stor.get("size",
+                                                                                 "10Gi")}}}})
+        groups = {}
+        for sg in spec.get("services") or [{"name": "default"}]:
+            g = sg.get("name", "default")
+            for svc in ("session-api", "memory-api"):
+                dn = f"{svc}-{name}-{g}"
+                store.apply({"apiVersion": "apps/v1", "kind": "Deployment",
+                             "metadata": {"name": dn, "namespace": nsname,
+                                          "labels": {"omnia.altairalabs.ai/component": svc,
+                                                     "omnia.altairalabs.ai/service-group": g},
+                                          "ownerReferences": own},
+                             "spec": {"replicas": 1, "selector": {"matchLabels": {
+                                 "app": dn}}, "template": {"metadata": {"labels": {"app": dn}},
+                                                           "spec": {"containers": [{
+                                                               "name": svc,
+                                                               "image": f"omnia-{svc}"}]}}}})
+                store.apply({"apiVersion": "v1", "kind": "Service",
+                             "metadata": {"name": dn, "namespace": nsname,
+                                          "ownerReferences": own},
+                             "spec": {"selector": {"app": dn},
+                                      "ports": [{"name": "http", "port": 8080}]}})
+            groups[g] = {"sessionURL": f"http://session-api-{name}-{g}.{nsname}:8080",
+                         "memoryURL": f"http://memory-api-{name}-{g}.{nsname}:8080"}
+        st["serviceGroups"] = groups
+        st["namespace"] = nsname
+        st["phase"] = "Ready"
+        set_condition(st, "Ready", True, "Reconciled", "", ws["metadata"]["generation"])
+        st["observedGeneration"] = ws["metadata"]["generation"]
+        ws["status"] = st
+        store.update_status(ws)
+        return None
+
+
+# ===================================================================== policies
+class SimplePolicyReconciler:
+    """AgentPolicy / ToolPolicy / MemoryPolicy / SessionRetentionPolicy /
+    SkillSource / Arena*: admission already validated; mark Active and count."""
+
+    def __init__(self, kind: str):
+        self.kind = kind
+
+    def reconcile(self, store: APIStore, ns, name: str):
+        ns_eff = ns if crds.KINDS[self.kind].scope == "Namespaced" else None
+        o = store.try_get(self.kind, name, ns_eff)
+        if o is None:
+            return None
+        st = o.get("status") or {}
+        spec = o["spec"]
+        if self.kind == "AgentPolicy":
+            agents = set((spec.get("selector") or {}).get("agents") or [])
+            ars = store.list("AgentRuntime", ns)
+            st["matchedCount"] = sum(1 for a in ars if not agents or
+                                     a["metadata"]["name"] in agents)
+        if self.kind == "ToolPolicy":
+            st["ruleCount"] = len(spec.get("rules") or [])
+        if self.kind == "RolloutAnalysis":
+            st["metricCount"] = len(spec.get("metrics") or [])
+        st["phase"] = "Active"
+        set_condition(st, "Ready", True, "Valid", "", o["metadata"]["generation"])
+        st["observedGeneration"] = o["metadata"]["generation"]
+        o["status"] = st
+        store.update_status(o)
+        return None
+
+
+def default_reconcilers(gpu_count: int | None = None) -> list:
+    rs = [PromptPackReconciler(), ProviderReconciler(gpu_count), ToolRegistryReconciler(),
+          AgentRuntimeReconciler(gpu_count), WorkspaceReconciler()]
+    for k in ("AgentPolicy", "ToolPolicy", "MemoryPolicy", "SessionRetentionPolicy",
+              "SkillSource", "SessionPrivacyPolicy", "RolloutAnalysis", "ArenaSource",
+              "ArenaTemplateSource", "PromptPackSource", "ArenaDevSession"):
+        rs.append(SimplePolicyReconciler(k))
+    return rs

@@ -1,0 +1,219 @@
+"""Controller manager (``cmd/main.go:400-660``): watch -> rate-limited work
+queue -> reconcile, with cross-kind enqueue mappings
+(``internal/controller/agentruntime_watches.go:36-60``), requeue-after, leader
+election on a Lease object, and the admission webhooks
+(``internal/webhook/*``: AgentRuntime input/output schemas must compile,
+Provider/Workspace sanity).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+import socket
+import time
+
+from ..api import crds
+from ..utils import jsonschema
+from .apistore import APIStore
+from .controllers import default_reconcilers
+
+log = logging.getLogger("omnia.operator.manager")
+
+
+# ------------------------------------------------------------------ webhooks
+def agentruntime_webhook(obj, old):
+    errs = []
+    for f in ("inputSchema", "outputSchema"):
+        sch = obj["spec"].get(f)
+        if sch is not None:
+            try:
+                jsonschema.check_schema(sch)
+            except Exception as e:  # noqa: BLE001
+                errs.append(f"spec.{f} does not compile: {e}")
+    return errs
+
+
+def workspace_webhook(obj, old):
+    if old is not None and old["spec"]["namespace"]["name"] != obj["spec"]["namespace"]["name"]:
+        return ["spec.namespace.name is immutable"]
+    return []
+
+
+def promptpack_webhook(obj, old):
+    if old is not None and old["spec"].get("version") != obj["spec"].get("version"):
+        return ["PromptPack spec.version is immutable; create a new PromptPack"]
+    return []
+
+
+WEBHOOKS = {"AgentRuntime": agentruntime_webhook, "Workspace": workspace_webhook,
+            "PromptPack": promptpack_webhook}
+
+
+def new_store() -> APIStore:
+    return APIStore(webhooks=dict(WEBHOOKS))
+
+
+# ------------------------------------------------------------------ manager
+class Manager:
+    def __init__(self, store: APIStore, reconcilers=None, gpu_count: int | None = None,
+                 identity: str | None = None, leader_elect: bool = False,
+                 namespace: str = "omnia-system"):
+        self.store = store
+        self.reconcilers = {r.kind: r for r in (reconcilers or default_reconcilers(gpu_count))}
+        self.queue: asyncio.Queue | None = None
+        self.pending: set = set()
+        self.delayed: dict = {}
+        self.identity = identity or f"{socket.gethostname()}-{os.getpid()}"
+        self.leader_elect = leader_elect
+        self.lease_ns = namespace
+        self.tasks: list = []
+        self.stats = {"reconciles": 0, "errors": 0}
+        self._idle = None
+        self._gens: dict = {}
+
+    def enqueue(self, kind: str, ns: str | None, name: str, after: float = 0.0):
+        key = (kind, ns or "", name)
+        if after > 0:
+            self.delayed[key] = time.monotonic() + after
+            return
+        if key not in self.pending:
+            self.pending.add(key)
+            self.queue.put_nowait(key)
+
+    def _map(self, etype: str, obj: dict):
+        kind = obj["kind"]
+        md = obj["metadata"]
+        ns = md.get("namespace", "")
+        if kind in self.reconcilers:
+            # GenerationChangedPredicate: status-only writes of the primary kind
+            # do not re-trigger its own reconcile
+            gk = (kind, ns, md["name"])
+            gen = md.get("generation")
+            if etype != "MODIFIED" or self._gens.get(gk) != gen or \
+                    md.get("deletionTimestamp"):
+                self.enqueue(kind, ns, md["name"])
+            self._gens[gk] = gen
+        # owner -> re-queue
+        for ref in md.get("ownerReferences", []) or []:
+            if ref.get("kind") in self.reconcilers:
+                self.enqueue(ref["kind"], ns, ref["name"])
+        # reference mappings
+        if kind in ("PromptPack", "Provider", "ToolRegistry", "ConfigMap", "Secret",
+                    "RolloutAnalysis"):
+            for ar in self.store.list("AgentRuntime", ns):
+                spec = ar["spec"]
+                hit = False
+                if kind == "PromptPack":
+                    hit = spec["promptPackRef"]["name"] in (obj["spec"].get("packName"),
+                                                            md["name"])
+                elif kind == "Provider":
+                    hit = any((p.get("providerRef") or {}).get("name", p.get("name")) ==
+                              md["name"] for p in spec.get("providers") or [])
+                elif kind == "ToolRegistry":
+                    hit = (spec.get("toolRegistryRef") or {}).get("name") == md["name"]
+                else:
+                    hit = True
+                if hit:
+                    self.enqueue("AgentRuntime", ns, ar["metadata"]["name"])
+        if kind == "ConfigMap":
+            for pp in self.store.list("PromptPack", ns):
+                if (pp["spec"]["source"].get("configMapRef") or {}).get("name") == md["name"]:
+                    self.enqueue("PromptPack", ns, pp["metadata"]["name"])
+        if kind == "Secret":
+            for pv in self.store.list("Provider", ns):
+                if ((pv["spec"].get("credential") or {}).get("secretRef") or {}).get(
+                        "name") == md["name"]:
+                    self.enqueue("Provider", ns, pv["metadata"]["name"])
+        if kind == "PromptPack":
+            for pp in self.store.list("PromptPack", ns):
+                if pp["spec"].get("packName") == obj["spec"].get("packName") and \
+                        pp["metadata"]["name"] != md["name"]:
+                    self.enqueue("PromptPack", ns, pp["metadata"]["name"])
+
+    async def _acquire_lease(self) -> bool:
+        if not self.leader_elect:
+            return True
+        name = "omnia-operator-leader"
+        now = time.time()
+        lease = self.store.try_get("Lease", name, self.lease_ns)
+        if lease is None:
+            self.store.create({"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
+                               "metadata": {"name": name, "namespace": self.lease_ns},
+                               "spec": {"holderIdentity": self.identity, "renewTime": now,
+                                        "leaseDurationSeconds": 15}})
+            return True
+        sp = lease["spec"]
+        if sp["holderIdentity"] == self.identity or now - sp["renewTime"] > \
+                sp["leaseDurationSeconds"]:
+            lease["spec"] = {**sp, "holderIdentity": self.identity, "renewTime": now}
+            self.store.update(lease)
+            return True
+        return False
+
+    async def _watch_loop(self, q):
+        try:
+            while True:
+                etype, obj = await q.get()
+                self._map(etype, obj)
+        finally:
+            self.store.unwatch(q)
+
+    async def _timer_loop(self):
+        while True:
+            await asyncio.sleep(0.05)
+            now = time.monotonic()
+            for key, t in list(self.delayed.items()):
+                if t <= now:
+                    self.delayed.pop(key, None)
+                    self.enqueue(*key)
+
+    async def _worker(self):
+        while True:
+            key = await self.queue.get()
+            self.pending.discard(key)
+            kind, ns, name = key
+            r = self.reconcilers.get(kind)
+            if r is None:
+                continue
+            try:
+                after = r.reconcile(self.store, ns or None, name)
+                self.stats["reconciles"] += 1
+                if after:
+                    self.enqueue(kind, ns, name, after)
+            except Exception:  # noqa: BLE001
+                self.stats["errors"] += 1
+                log.exception("reconcile %s %s/%s failed", kind, ns, name)
+                self.enqueue(kind, ns, name, 1.0)
+
+    async def start(self, workers: int = 4):
+        self.queue = asyncio.Queue()
+        while not await self._acquire_lease():
+            await asyncio.sleep(2)
+        q = self.store.watch(None)  # register before listing: no missed events
+        for o in [o for kind in self.reconcilers for o in self.store.list(kind)]:
+            self._map("ADDED", o)
+        self.tasks = [asyncio.ensure_future(self._watch_loop(q)),
+                      asyncio.ensure_future(self._timer_loop())]
+        self.tasks += [asyncio.ensure_future(self._worker()) for _ in range(workers)]
+
+    async def settle(self, timeout: float = 10.0, quiet: float = 0.2) -> None:
+        """Wait until the queue drains and stays empty for `quiet` seconds."""
+        t0 = time.monotonic()
+        calm = None
+        while time.monotonic() - t0 < timeout:
+            busy = not self.queue.empty() or bool(self.pending) or any(
+                t <= time.monotonic() + quiet for t in self.delayed.values())
+            if busy:
+                calm = None
+            else:
+                calm = calm or time.monotonic()
+                if time.monotonic() - calm >= quiet:
+                    return
+            await asyncio.sleep(0.02)
+
+    async def stop(self):
+        for t in self.tasks:
+            t.cancel()
+        await asyncio.gather(*self.tasks, return_exceptions=True)

@@ -28,6 +28,7 @@ from .kv_manager import BlockManager
 from .model_runner import ModelRunner
 from .sampling_params import SamplingParams
 from .scheduler import Scheduler, SchedulerConfig
+from .model_runner import PLACEHOLDER
 from .sequence import FinishReason, Sequence
 from .swap import SwapSpace
 from .tokenizer import Detokenizer, make_tokenizer
@@ -52,6 +53,7 @@ class EngineConfig:
     swap_gib: float = 0.0  # host-DRAM warm tier for evicted session KV
     tokenizer: str | None = None
     decode_part_size: int = 512
+    pipeline: bool = True  # one-deep async decode scheduling
 
     @classmethod
     def from_env(cls, **kw) -> "EngineConfig":
@@ -108,6 +110,7 @@ class LLMEngine:
         self.seqs: dict[int, Sequence] = {}
         self.detok: dict[int, Detokenizer] = {}
         self.step_count = 0
+        self.inflight = None
         self.counters = {"prefill_tokens": 0, "decode_tokens": 0, "steps_prefill": 0,
                          "steps_decode": 0, "finished": 0}
         log.info("engine ready: %s on %s, %d KV blocks x %d tokens, load %.1fs",
@@ -150,18 +153,75 @@ class LLMEngine:
         if s is not None:
             self._finalize(s)
 
-    def has_work(self) -> bool:
-        return self.scheduler.has_work()
-
     def drop_session(self, session_id: str) -> bool:
         return self.blocks.drop_session(session_id)
 
     # --------------------------------------------------------------- stepping
     def step(self) -> int:
-        """Run one engine iteration.  Returns number of tokens produced."""
+        """Run one engine iteration.  Returns number of tokens produced.
+
+        Decode steps are pipelined one deep ("async scheduling"): step N+1 is
+        launched -- its input tokens gathered on the GPU from step N's sampler
+        output -- before step N's tokens are pulled to the host and processed,
+        so host work (scheduling, detokenisation, streaming, stop checks)
+        overlaps the GPU instead of idling it."""
+        if self.cfg.pipeline and self.runner.use_graphs:
+            return self._step_pipelined()
+        return self._step_sync()
+
+    def has_work(self) -> bool:
+        return self.inflight is not None or self.scheduler.has_work()
+
+    def _flush_inflight(self) -> int:
+        h, self.inflight = self.inflight, None
+        if h is None:
+            return 0
+        toks = self.runner.collect(h)
+        now = time.perf_counter()
+        for sq, tok in zip(h.seqs, toks):
+            self._append(sq, tok, now)
+        return len(toks)
+
+    def _steady(self) -> bool:
+        sch = self.scheduler
+        return (not sch.waiting and not sch.partial and
+                self.blocks.num_free >= len(sch.running) + 1)
+
+    def _step_pipelined(self) -> int:
+        if self.inflight is not None and not self._steady():
+            return self._flush_inflight()
+        plan = self.scheduler.schedule()
+        if plan.kind == "decode" and self.runner.can_pipeline(plan.decode):
+            t0 = time.perf_counter()
+            h = self.runner.launch_decode(plan.decode)
+            for sq in plan.decode:
+                sq.num_cached = sq.length  # the fed token's KV is written by this step
+                sq.output.append(PLACEHOLDER)
+            n = self._flush_inflight()
+            self.inflight = h
+            self.counters["decode_tokens"] += len(plan.decode)
+            self.counters["steps_decode"] += 1
+            M.DECODE_TOKENS.inc(len(plan.decode))
+            M.BATCH_SIZE.observe(len(plan.decode))
+            M.STEP_SECONDS.labels("decode").observe(time.perf_counter() - t0)
+            self.step_count += 1
+            return n
+        n = self._flush_inflight()
+        if plan.kind == "idle":
+            return n
+        if plan.kind == "decode":
+            plan.decode = [sq for sq in plan.decode if not sq.is_finished]
+            if not plan.decode:
+                return n
+        return n + self._run_plan(plan)
+
+    def _step_sync(self) -> int:
         plan = self.scheduler.schedule()
         if plan.kind == "idle":
             return 0
+        return self._run_plan(plan)
+
+    def _run_plan(self, plan) -> int:
         t0 = time.perf_counter()
         if plan.kind == "prefill":
             sampled = self.runner.run_prefill(plan.prefill)
@@ -192,16 +252,21 @@ class LLMEngine:
         if s.first_token_time is None:
             s.first_token_time = now
             M.TTFT.observe(now - s.arrival)
-        s.output.append(tok)
+        if s.n_real < len(s.output):  # fill the oldest in-flight placeholder
+            s.output[s.n_real] = tok
+        else:
+            s.output.append(tok)
+        s.n_real += 1
+        nout = s.n_real
         p = s.params
         reason = None
-        if not p.ignore_eos and tok in self.eos and len(s.output) > p.min_tokens:
+        if not p.ignore_eos and tok in self.eos and nout > p.min_tokens:
             reason = FinishReason.STOP
         elif tok in p.stop_token_ids:
             reason = FinishReason.STOP
-        elif len(s.output) >= p.max_tokens:
+        elif nout >= p.max_tokens:
             reason = FinishReason.LENGTH
-        elif s.length >= self.cfg.max_model_len:
+        elif len(s.prompt) + nout >= self.cfg.max_model_len:
             reason = FinishReason.LENGTH
         text = ""
         if s.on_token is not None or p.stop:
@@ -216,6 +281,9 @@ class LLMEngine:
         if s.on_token is not None:
             s.on_token(s, tok, text)
         if reason is not None:
+            if s.n_real < len(s.output):  # drop tokens speculatively in flight
+                del s.output[s.n_real:]
+                s.num_cached = min(s.num_cached, s.length - 1)
             self.scheduler.finish(s, reason)
             self._finalize(s)
 

@@ -25,7 +25,8 @@ BATCH_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224
 class _Staging:
     """Packed pinned host buffer + device twin with typed section views."""
 
-    def __init__(self, spec: dict, device, pin: bool):
+    def __init__(self, spec: dict, device, pin: bool, dev=None):
+        self.event = None
         self.off = {}
         o = 0
         for name, (dtype, n) in spec.items():
@@ -34,7 +35,8 @@ class _Staging:
             o += n * torch.tensor([], dtype=dtype).element_size()
         self.nbytes = (o + 63) // 64 * 64
         self.host = torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=pin)
-        self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+        self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=device) if dev is None \
+            else dev
         self.h = {}
         self.d = {}
         for name, (o, dtype, n) in self.off.items():
@@ -65,15 +67,21 @@ class ModelRunner:
         self.buckets = [b for b in BATCH_BUCKETS if b < max_batch] + [max_batch]
         pin = self.is_gpu
         B, MB = max_batch, self.max_blocks
-        self.dec = _Staging({
-            "ids": (torch.int32, B), "pos": (torch.int32, B), "slots": (torch.int64, B),
-            "seq_lens": (torch.int32, B), "temp": (torch.float32, B), "top_k": (torch.int32, B),
+        spec = {
+            "ids": (torch.int32, B), "src": (torch.int64, B), "pos": (torch.int32, B),
+            "slots": (torch.int64, B), "seq_lens": (torch.int32, B),
+            "temp": (torch.float32, B), "top_k": (torch.int32, B),
             "top_p": (torch.float32, B), "seeds": (torch.int64, B), "steps": (torch.int64, B),
             "bt": (torch.int32, B * MB),
-        }, self.device, pin)
+        }
+        # double-buffered pinned host staging (step N+1 is prepared while N runs);
+        # both halves upload into ONE device twin that the captured graphs read.
+        self.dec = _Staging(spec, self.device, pin)
+        self.stage = [self.dec, _Staging(spec, self.device, pin, dev=self.dec.dev)]
+        self.flip = 0
         self.logits_idx = torch.arange(B, dtype=torch.int64, device=self.device)
         self.out_tok = torch.zeros(B, dtype=torch.int32, device=self.device)
-        self.out_host = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        self.out_hosts = [torch.zeros(B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self.graphs: dict = {}
         self.graph_pool = None
         self.stats = {"graph_replays": 0, "eager_decodes": 0, "prefill_steps": 0,
@@ -204,15 +212,22 @@ class ModelRunner:
         return tok.cpu().tolist()
 
     # ------------------------------------------------------------------ decode
-    def _decode_inputs(self, seqs: list[Sequence], nrows: int, ncols: int):
-        st = self.dec
+    def _decode_inputs(self, seqs: list[Sequence], nrows: int, ncols: int, st: "_Staging"):
         n = len(seqs)
         ids, pos, slots, lens = st.np["ids"], st.np["pos"], st.np["slots"], st.np["seq_lens"]
+        src = st.np["src"]
         bt = st.np["bt"].reshape(self.max_batch, self.max_blocks)
         bs = self.bs
         for i, s in enumerate(seqs):
             p = s.length - 1
-            ids[i] = s.output[-1] if s.output else s.prompt[-1]
+            last = s.output[-1] if s.output else s.prompt[-1]
+            if last == PLACEHOLDER:
+                # token still on the device: gather it from the previous step's sampler output
+                src[i] = s.slot
+                ids[i] = 0
+            else:
+                src[i] = -1
+                ids[i] = last
             pos[i] = p
             slots[i] = s.blocks[p // bs] * bs + p % bs
             lens[i] = p + 1
@@ -220,24 +235,31 @@ class ModelRunner:
             bt[i, :nb] = s.blocks
         for i in range(n, nrows):  # padded rows -> null page, no KV write
             ids[i] = 0
+            src[i] = -1
             pos[i] = 0
             slots[i] = -1
             lens[i] = 1
             bt[i, 0] = 0
         self._fill_sampling(st, seqs, nrows)
-        st.upload()
+        # upload into the (single) device twin the graphs read from
+        self.dec.dev.copy_(st.host, non_blocking=True)
 
-    def _decode_fb(self, nrows: int, ncols: int) -> ForwardBatch:
+    def _decode_fb(self, nrows: int, ncols: int, ids=None) -> ForwardBatch:
         d = self.dec.d
         return ForwardBatch(
-            input_ids=d["ids"][:nrows], positions=d["pos"][:nrows], slots=d["slots"][:nrows],
+            input_ids=d["ids"][:nrows] if ids is None else ids, positions=d["pos"][:nrows],
+            slots=d["slots"][:nrows],
             block_tables=d["bt"].view(self.max_batch, self.max_blocks)[:nrows, :ncols],
             seq_lens=d["seq_lens"][:nrows], logits_indices=self.logits_idx[:nrows],
             is_decode=True, num_seqs=nrows)
 
     def _decode_body(self, nrows: int, ncols: int):
         d = self.dec.d
-        fb = self._decode_fb(nrows, ncols)
+        src = d["src"][:nrows]
+        # tokens sampled by the previous step stay on the GPU (async scheduling)
+        ids = torch.where(src >= 0, self.out_tok.index_select(0, src.clamp(min=0)),
+                          d["ids"][:nrows])
+        fb = self._decode_fb(nrows, ncols, ids)
         logits = self.model.forward(fb, self.kv)
         ops.sample(logits, d["temp"][:nrows], d["top_k"][:nrows], d["top_p"][:nrows],
                    seeds=d["seeds"][:nrows], steps=d["steps"][:nrows],
@@ -247,6 +269,8 @@ class ModelRunner:
         t0 = time.perf_counter()
         if self.graph_pool is None:
             self.graph_pool = torch.cuda.graph_pool_handle()
+        # warm-up/capture must not clobber live sampler outputs of an in-flight step
+        saved = self.out_tok.clone()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -257,30 +281,67 @@ class ModelRunner:
         with torch.cuda.graph(g, pool=self.graph_pool):
             self._decode_body(nrows, ncols)
         torch.cuda.synchronize()
+        self.out_tok.copy_(saved)
         self.graphs[(nrows, ncols)] = g
         self.stats["captures"] += 1
         self.stats["capture_s"] += time.perf_counter() - t0
         return g
 
-    def run_decode(self, seqs: list[Sequence]) -> list[int]:
+    def can_pipeline(self, seqs: list[Sequence]) -> bool:
+        return self.use_graphs and not any(s.params.needs_penalties for s in seqs)
+
+    def launch_decode(self, seqs: list[Sequence]) -> "DecodeHandle":
+        """Enqueue one decode step (graph replay) without waiting for it."""
         n = len(seqs)
         if n > self.max_batch:
             raise ValueError("decode batch exceeds max_batch")
         max_len = max(s.length for s in seqs)
         ncols = self._ctx_bucket(max_len)
-        needs_pen = any(s.params.needs_penalties for s in seqs)
-        if self.use_graphs and not needs_pen:
-            nrows = self.buckets[bisect.bisect_left(self.buckets, n)]
-            self._decode_inputs(seqs, nrows, ncols)
-            g = self.graphs.get((nrows, ncols)) or self._capture(nrows, ncols)
-            g.replay()
-            self.stats["graph_replays"] += 1
-            self.out_host[:n].copy_(self.out_tok[:n], non_blocking=True)
-            torch.cuda.current_stream().synchronize()
-            return self.out_host[:n].tolist()
-        # eager path (CPU engine, penalties)
-        self._decode_inputs(seqs, n, ncols)
+        nrows = self.buckets[bisect.bisect_left(self.buckets, n)]
+        st = self.stage[self.flip]
+        out_host = self.out_hosts[self.flip]
+        self.flip ^= 1
+        if st.event is not None:
+            st.event.synchronize()  # host staging buffer free again
+        self._decode_inputs(seqs, nrows, ncols, st)
+        g = self.graphs.get((nrows, ncols)) or self._capture(nrows, ncols)
+        g.replay()
+        self.stats["graph_replays"] += 1
+        out_host[:n].copy_(self.out_tok[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        st.event = ev
+        for i, s in enumerate(seqs):
+            s.slot = i
+        return DecodeHandle(seqs, out_host, ev, n)
+
+    @staticmethod
+    def collect(h: "DecodeHandle") -> list[int]:
+        h.event.synchronize()
+        return h.out_host[: h.n].tolist()
+
+    def run_decode(self, seqs: list[Sequence]) -> list[int]:
+        if self.can_pipeline(seqs):
+            return self.collect(self.launch_decode(seqs))
+        # eager path (CPU engine, penalties): real tokens only
+        n = len(seqs)
+        ncols = self._ctx_bucket(max(s.length for s in seqs))
+        st = self.stage[0]
+        self._decode_inputs(seqs, n, ncols, st)
         fb = self._decode_fb(n, ncols)
         logits = self.model.forward(fb, self.kv)
         self.stats["eager_decodes"] += 1
         return self._sample_eager(logits, seqs)
+
+
+PLACEHOLDER = -1
+
+
+class DecodeHandle:
+    __slots__ = ("seqs", "out_host", "event", "n")
+
+    def __init__(self, seqs, out_host, event, n):
+        self.seqs = seqs
+        self.out_host = out_host
+        self.event = event
+        self.n = n

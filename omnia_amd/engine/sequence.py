@@ -46,7 +46,8 @@ class Sequence:
     preemptions: int = 0
     prefix_hit: int = 0
     text_tail: str = ""  # recent decoded text for stop-string matching
-    slot: int = -1  # persistent-batch row
+    slot: int = -1  # row in the last launched decode step
+    n_real: int = 0  # output tokens whose value is known on the host
 
     @property
     def all_tokens(self) -> list[int]:

@@ -162,22 +162,33 @@ class LlamaModel:
                     self.hkv, kv.block_size)
         q3 = q.view(T, self.hq, D)
         if fb.is_decode:
-            ws = self._decode_ws(T, fb.block_tables.shape[1], kv.block_size, h.device)
+            part = self.decode_part(T, fb.block_tables.shape[1] * kv.block_size)
+            ws = self._decode_ws(T, fb.block_tables.shape[1], kv.block_size, h.device, part)
             o = ops.decode_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.seq_lens,
-                                     self.scale, part_size=self.decode_part_size, workspace=ws)
+                                     self.scale, part_size=part, workspace=ws)
         else:
             o = ops.prefill_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.q_start_loc,
                                       fb.seq_lens, self.scale, fb.tile_seq, fb.tile_q0)
         out = F.linear(o.view(T, self.hq * D), self.w["layers"][li]["o"])
         return pstate.tp_all_reduce(out)
 
-    def _decode_ws(self, B, max_blocks, bs, device):
-        key = (B, max_blocks, bs, str(device))
+    def decode_part(self, batch: int, max_ctx: int) -> int:
+        """Split-K partition length: as long as possible (fewer partials to merge,
+        no merge kernel when one partition covers the context) while keeping
+        >= ~2048 workgroups in flight to fill 256 CUs."""
+        part = self.decode_part_size
+        while part < 2048 and part < max_ctx and \
+                batch * self.hkv * ((max_ctx + 2 * part - 1) // (2 * part)) >= 2048:
+            part *= 2
+        return part
+
+    def _decode_ws(self, B, max_blocks, bs, device, part):
+        key = (B, max_blocks, bs, str(device), part)
         ws = self._ws.get(key)
         if ws is None:
             if device.type != "cuda":
                 return None
-            ws = ops.decode_workspace(B, self.hq, max_blocks, bs, self.decode_part_size, device)
+            ws = ops.decode_workspace(B, self.hq, max_blocks, bs, part, device)
             self._ws[key] = ws
         return ws
 

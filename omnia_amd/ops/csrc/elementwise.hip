@@ -20,25 +20,32 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   const int row = blockIdx.x;
   const bf16_t* xr = x + (int64_t)row * x_stride;
   bf16_t* rr = ADD ? residual + (int64_t)row * d : nullptr;
-  short8 v[VEC];
-  float ss = 0.f;
+  short8 v[VEC], r[VEC], wv[VEC];
+  // all global loads first (x, residual, weight are independent): one memory
+  // round trip before the reduction instead of three
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     const int c = (i * 256 + threadIdx.x) * 8;
     if (c < d) {
       v[i] = *reinterpret_cast<const short8*>(xr + c);
-      if (ADD) {
-        short8 r = *reinterpret_cast<const short8*>(rr + c);
+      if (ADD) r[i] = *reinterpret_cast<const short8*>(rr + c);
+      wv[i] = *reinterpret_cast<const short8*>(w + c);
+    }
+  }
+  float ss = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float s = bf2f((uint16_t)v[i][j]) + bf2f((uint16_t)r[j]);
-          v[i][j] = (short)f2bf(s);
-        }
+  for (int i = 0; i < VEC; ++i) {
+    const int c = (i * 256 + threadIdx.x) * 8;
+    if (c < d) {
+      if (ADD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[i][j] = (short)f2bf(bf2f((uint16_t)v[i][j]) + bf2f((uint16_t)r[i][j]));
         *reinterpret_cast<short8*>(rr + c) = v[i];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float f = bf2f((uint16_t)v[i][j]);
+        const float f = bf2f((uint16_t)v[i][j]);
         ss += f * f;
       }
     }
@@ -50,11 +57,10 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   for (int i = 0; i < VEC; ++i) {
     const int c = (i * 256 + threadIdx.x) * 8;
     if (c < d) {
-      short8 wv = *reinterpret_cast<const short8*>(w + c);
       short8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        o[j] = (short)f2bf(bf2f((uint16_t)v[i][j]) * inv * bf2f((uint16_t)wv[j]));
+        o[j] = (short)f2bf(bf2f((uint16_t)v[i][j]) * inv * bf2f((uint16_t)wv[i][j]));
       *reinterpret_cast<short8*>(orow + c) = o;
     }
   }
@@ -115,26 +121,25 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(
 }
 
 // --------------------------------------------------------------- SwiGLU
-// x: [T, 2*I] (gate | up), out: [T, I]
+// x: [T, 2*I] (gate | up), out: [T, I].  grid (ceil(I/8/256), T): one token row per
+// blockIdx.y, so no 64-bit division in the index math.
 __global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out,
                                                        const bf16_t* __restrict__ x,
-                                                       int64_t T, int inter) {
-  const int64_t nvec = (int64_t)T * (inter / 8);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = i / (inter / 8);
-    const int c = (int)(i % (inter / 8)) * 8;
-    short8 g = *reinterpret_cast<const short8*>(x + t * 2 * inter + c);
-    short8 u = *reinterpret_cast<const short8*>(x + t * 2 * inter + inter + c);
-    short8 o;
+                                                       int inter) {
+  const int t = blockIdx.y;
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= inter) return;
+  const bf16_t* row = x + (int64_t)t * 2 * inter;
+  const short8 g = *reinterpret_cast<const short8*>(row + c);
+  const short8 u = *reinterpret_cast<const short8*>(row + inter + c);
+  short8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float gf = bf2f((uint16_t)g[j]);
-      const float sg = gf / (1.f + __expf(-gf));
-      o[j] = (short)f2bf(sg * bf2f((uint16_t)u[j]));
-    }
-    *reinterpret_cast<short8*>(out + t * inter + c) = o;
+  for (int j = 0; j < 8; ++j) {
+    const float gf = bf2f((uint16_t)g[j]);
+    const float sg = gf * __builtin_amdgcn_rcpf(1.f + __expf(-gf));
+    o[j] = (short)f2bf(sg * bf2f((uint16_t)u[j]));
   }
+  *reinterpret_cast<short8*>(out + (int64_t)t * inter + c) = o;
 }
 
 // --------------------------------------------------------------- embedding
@@ -194,10 +199,9 @@ int omnia_rope_kv(void* q, void* k, const void* v, const int* positions, const f
 int omnia_silu_mul(void* out, const void* x, int64_t T, int inter, hipStream_t s) {
   if (inter % 8) return -1;
   if (T == 0) return 0;
-  const int64_t nvec = T * (inter / 8);
-  int64_t blocks = (nvec + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  silu_mul_kernel<<<(int)blocks, 256, 0, s>>>((bf16_t*)out, (const bf16_t*)x, T, inter);
+  if (T > 2147483647LL) return -2;
+  dim3 grid((inter / 8 + 255) / 256, (unsigned)T);
+  silu_mul_kernel<<<grid, 256, 0, s>>>((bf16_t*)out, (const bf16_t*)x, inter);
   return (int)hipGetLastError();
 }
 

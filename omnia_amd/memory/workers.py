@@ -1,0 +1,105 @@
+"""Background workers of memory-api.
+
+* :class:`ReembedWorker` -- backfills missing / stale-model embeddings in
+  batches (``internal/memory/reembed_worker.go:81-148``); batching is what makes
+  the in-node embedder efficient (one packed varlen forward per batch).
+* :class:`RetentionWorker` -- TTL expiry + purge of forgotten rows
+  (``internal/memory/retention.go``).
+* :class:`CompactionWorker` -- LLM-summarises old observations of a scope into
+  one ``summary`` memory that supersedes them
+  (``internal/memory/compaction_worker.go:93-218``); the summariser is any
+  async callable ``(texts) -> str`` (the local engine provider in-node).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+
+from .model import SCOPE_WORKSPACE, Memory
+
+log = logging.getLogger("omnia.memory.workers")
+
+
+class ReembedWorker:
+    def __init__(self, svc, interval: float = 5.0, batch: int = 64):
+        self.svc, self.interval, self.batch = svc, interval, batch
+
+    async def run_once(self) -> int:
+        total = 0
+        while True:
+            n = await self.svc.reembed(self.batch)
+            total += n
+            if n < self.batch:
+                return total
+
+    async def run(self):
+        while True:
+            try:
+                await self.run_once()
+            except Exception as e:  # noqa: BLE001
+                log.warning("reembed pass failed: %s", e)
+            await asyncio.sleep(self.interval)
+
+
+class RetentionWorker:
+    def __init__(self, svc, interval: float = 300.0, forgotten_grace_s: float = 30 * 86400):
+        self.svc, self.interval, self.grace = svc, interval, forgotten_grace_s
+
+    def run_once(self) -> int:
+        obs = self.svc.store.expire() + self.svc.store.purge_forgotten(self.grace)
+        self.svc._drop_vectors(obs)
+        return len(obs)
+
+    async def run(self):
+        while True:
+            try:
+                self.run_once()
+            except Exception as e:  # noqa: BLE001
+                log.warning("retention pass failed: %s", e)
+            await asyncio.sleep(self.interval)
+
+
+def default_summarizer_prompt(texts: list[str]) -> str:
+    joined = "\n".join(f"- {t}" for t in texts)
+    return ("Consolidate these memories about the same subject into a short list of durable "
+            "facts. Drop duplicates and superseded details.\n" + joined)
+
+
+class CompactionWorker:
+    def __init__(self, svc, summarize, workspaces: list[str], older_than_s: float = 30 * 86400,
+                 min_count: int = 10, interval: float = 3600.0):
+        self.svc, self.summarize = svc, summarize
+        self.workspaces = workspaces
+        self.older_than_s, self.min_count, self.interval = older_than_s, min_count, interval
+
+    async def run_once(self) -> int:
+        done = 0
+        for ws in self.workspaces:
+            for cand in self.svc.store.compaction_candidates(ws, self.older_than_s,
+                                                             self.min_count):
+                texts = [e["content"] for e in cand["entries"]]
+                try:
+                    summary = await self.summarize(texts)
+                except Exception as e:  # noqa: BLE001
+                    log.warning("summarize failed for %s: %s", cand["scope"], e)
+                    continue
+                if not summary:
+                    continue
+                mem = Memory(type="summary", content=summary, confidence=0.8,
+                             scope=dict(cand["scope"]),
+                             metadata={"source_type": "system_generated",
+                                       "compacted_from": len(texts)})
+                await self.svc.supersede([e["id"] for e in cand["entries"]], mem)
+                done += 1
+        return done
+
+    async def run(self):
+        while True:
+            try:
+                await self.run_once()
+            except Exception as e:  # noqa: BLE001
+                log.warning("compaction pass failed: %s", e)
+            await asyncio.sleep(self.interval)
+
+
+__all__ = ["ReembedWorker", "RetentionWorker", "CompactionWorker", "SCOPE_WORKSPACE"]

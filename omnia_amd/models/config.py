@@ -74,6 +74,15 @@ MIXTRAL_8X7B = ModelConfig(name="mixtral-8x7b", arch="mixtral", vocab_size=32000
                            num_heads=32, num_kv_heads=8, rope_theta=1e6, max_position=32768,
                            num_experts=8, experts_per_token=2, bos_token_id=1,
                            eos_token_ids=(2,))
+# in-node embedding model for the memory tier (K17): a small Llama-shaped encoder
+# whose last hidden states are mean-pooled + L2-normalised (1024-d vectors)
+EMBED_1B = ModelConfig(name="omnia-embed-1b", vocab_size=128256, hidden_size=1024,
+                       intermediate_size=4096, num_layers=16, num_heads=8, num_kv_heads=8,
+                       max_position=8192, tie_embeddings=True)
+TINY_EMBED = ModelConfig(name="tiny-embed", vocab_size=512, hidden_size=256,
+                         intermediate_size=512, num_layers=2, num_heads=2, num_kv_heads=2,
+                         max_position=4096, tie_embeddings=True, bos_token_id=256,
+                         eos_token_ids=(257,))
 # tiny shapes for CPU tests / smoke (same code paths, head_dim fixed at 128)
 TINY_LLAMA = ModelConfig(name="tiny-llama", vocab_size=512, hidden_size=256,
                          intermediate_size=512, num_layers=2, num_heads=4, num_kv_heads=2,
@@ -84,7 +93,8 @@ TINY_MIXTRAL = ModelConfig(name="tiny-mixtral", arch="mixtral", vocab_size=512,
                            experts_per_token=2, bos_token_id=256, eos_token_ids=(257,))
 
 REGISTRY: dict[str, ModelConfig] = {
-    c.name: c for c in [LLAMA3_8B, LLAMA31_8B, LLAMA3_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_MIXTRAL]
+    c.name: c for c in [LLAMA3_8B, LLAMA31_8B, LLAMA3_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_MIXTRAL,
+                   EMBED_1B, TINY_EMBED]
 }
 ALIASES = {
     "meta-llama/Meta-Llama-3-8B": "llama-3-8b",

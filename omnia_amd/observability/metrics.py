@@ -100,6 +100,32 @@ ENGINE_WAITING = Gauge("omnia_engine_requests_waiting", "Queued requests", regis
 KV_HIT_TOKENS = Counter("omnia_engine_kv_hit_tokens_total", "Prompt tokens served from session KV",
                         registry=REGISTRY)
 
+# ----------------------------------------------------------------- memory-api
+# cmd/memory-api/SERVICE.md "Metrics" (classification + embedding pipeline health)
+MEMORY_CLASSIFY_OVERRIDES = Counter("omnia_memory_classify_overrides_total",
+                                    "Consent category upgraded by classification",
+                                    ["from", "to", "source"], registry=REGISTRY)
+MEMORY_CLASSIFY_FILLED = Counter("omnia_memory_classify_filled_total",
+                                 "Consent category filled in by classification",
+                                 ["category", "source"], registry=REGISTRY)
+MEMORY_CLASSIFY_CATEGORY = Counter("omnia_memory_classify_category_total",
+                                   "Stored consent categories", ["category", "source"],
+                                   registry=REGISTRY)
+MEMORY_EMBED_ERRORS = Counter("omnia_memory_classify_errors_total", "Embedding failures",
+                              registry=REGISTRY)
+MEMORY_EMBED_COVERAGE = Gauge("omnia_memory_embedding_coverage",
+                              "Fraction of live entities with an embedded active observation",
+                              ["workspace"], registry=REGISTRY)
+MEMORY_REEMBED_BACKLOG = Gauge("omnia_memory_reembed_backlog",
+                               "Active observations awaiting (re-)embedding", ["workspace"],
+                               registry=REGISTRY)
+MEMORY_EMBED_SECONDS = Histogram("omnia_memory_embed_seconds", "Embedding batch latency",
+                                 registry=REGISTRY)
+MEMORY_RETRIEVE_SECONDS = Histogram("omnia_memory_retrieve_seconds", "Retrieval latency",
+                                    ["mode"], registry=REGISTRY)
+MEMORY_OPS = Counter("omnia_memory_operations_total", "Memory API operations", ["op", "status"],
+                     registry=REGISTRY)
+
 
 def exposition() -> bytes:
     return generate_latest(REGISTRY)

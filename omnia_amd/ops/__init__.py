@@ -199,3 +199,50 @@ def sample(logits, temperature, top_k=None, top_p=None, seeds=None, steps=None, 
         out.copy_(r)
         return out
     return r
+
+
+# ------------------------------------------------------------- memory tier (K17 / K18)
+def mean_pool_l2(hidden: torch.Tensor, cu_seqlens: torch.Tensor) -> torch.Tensor:
+    """[T, D] bf16 hidden states + [B+1] int32 offsets -> [B, D] fp32 unit vectors."""
+    if hidden.is_cuda:
+        B = cu_seqlens.numel() - 1
+        out = torch.empty(B, hidden.shape[1], dtype=torch.float32, device=hidden.device)
+        kernels().mean_pool_l2(out, hidden, cu_seqlens.to(device=hidden.device,
+                                                          dtype=torch.int32).contiguous())
+        return out
+    return ref.mean_pool_l2(hidden, cu_seqlens)
+
+
+def cosine_topk(q: torch.Tensor, m: torch.Tensor, k: int, valid: torch.Tensor | None = None):
+    """Exact top-k of q . m over unit vectors.
+
+    q: [NQ, D] (any float dtype, normalised), m: [N, D] bf16 (normalised rows),
+    valid: optional uint8 [N] (0 = tombstoned).  Returns (scores fp32 [NQ, k],
+    indices int64 [NQ, k]) sorted by descending score, ties by ascending index."""
+    nq, N = q.shape[0], m.shape[0]
+    k = min(k, N)
+    if k == 0:
+        return (torch.empty(nq, 0, dtype=torch.float32, device=m.device),
+                torch.empty(nq, 0, dtype=torch.long, device=m.device))
+    if m.is_cuda:
+        kk = kernels()
+        D = m.shape[1]
+        vals, idxs = [], []
+        # the kernel stages up to 64 KiB of queries in LDS: chunk by 8/4/2/1
+        max_nq = max(1, min(8, (64 * 1024) // (4 * D)))
+        i = 0
+        while i < nq:
+            n = min(max_nq, nq - i)
+            npad = 1 if n == 1 else 2 if n == 2 else 4 if n <= 4 else 8
+            qq = torch.zeros(npad, D, dtype=torch.float32, device=m.device)
+            qq[:n] = q[i:i + n].to(device=m.device, dtype=torch.float32)
+            scores = torch.empty(npad, N, dtype=torch.float32, device=m.device)
+            kk.cosine_scores(scores, qq, m, valid)
+            oi = torch.empty(npad, k, dtype=torch.int32, device=m.device)
+            ov = torch.empty(npad, k, dtype=torch.float32, device=m.device)
+            kk.topk(oi, ov, scores, k)
+            vals.append(ov[:n])
+            idxs.append(oi[:n].long())
+            i += n
+        return torch.cat(vals), torch.cat(idxs)
+    return ref.cosine_topk(q, m, k, valid)

@@ -31,6 +31,12 @@ int omnia_sample(int* out_tok, float* out_logprob, const void* logits, int logit
                  const int* top_k, const float* top_p, const uint64_t* seeds,
                  const int64_t* steps, int* counts, const float* freq_pen, const float* pres_pen,
                  const float* rep_pen, hipStream_t s);
+int omnia_mean_pool_l2(float* out, const void* hidden, int64_t stride, const int* cu, int B,
+                       int D, hipStream_t s);
+int omnia_cosine_scores(float* scores, const float* q, int nq, const void* m, int64_t N, int D,
+                        const uint8_t* valid, hipStream_t s);
+int omnia_topk(int* out_idx, float* out_val, const float* scores, int nq, int64_t N, int k,
+               hipStream_t s);
 }
 
 namespace {
@@ -187,6 +193,58 @@ void sample(at::Tensor out_tok, c10::optional<at::Tensor> out_logprob, at::Tenso
                         opt_ptr<float>(rep_pen), cur_stream()), "sample");
 }
 
+// K17: out[b] = normalize(mean(hidden[cu[b]:cu[b+1]]))   fp32
+void mean_pool_l2(at::Tensor out, at::Tensor hidden, at::Tensor cu) {
+  CHECK_GPU(hidden); CHECK_BF16(hidden); CHECK_I32(cu);
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous(), "out fp32 contiguous");
+  TORCH_CHECK(hidden.dim() == 2 && hidden.stride(1) == 1, "hidden [T, D] inner-contiguous");
+  TORCH_CHECK(cu.dim() == 1 && cu.is_contiguous() && cu.is_cuda(), "cu [B+1] on device");
+  const int B = cu.size(0) - 1, D = hidden.size(1);
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == B && out.size(1) == D, "out [B, D]");
+  TORCH_CHECK(D % 8 == 0 && D <= 8192, "D must be a multiple of 8, <= 8192");
+  CHECK_RC(omnia_mean_pool_l2(out.data_ptr<float>(), hidden.data_ptr(), hidden.stride(0),
+                              cu.data_ptr<int>(), B, D, cur_stream()), "mean_pool_l2");
+}
+
+// K18: scores[q, n] = Q[q] . M[n]  (fp32 out, -inf where valid[n] == 0)
+void cosine_scores(at::Tensor scores, at::Tensor q, at::Tensor m,
+                   c10::optional<at::Tensor> valid) {
+  CHECK_GPU(m); CHECK_BF16(m);
+  TORCH_CHECK(q.scalar_type() == at::kFloat && q.is_contiguous() && q.is_cuda(), "q fp32");
+  TORCH_CHECK(m.dim() == 2 && m.is_contiguous(), "m [N, D] contiguous");
+  TORCH_CHECK(q.dim() == 2 && q.size(1) == m.size(1), "q [NQ, D]");
+  const int nq = q.size(0), D = m.size(1);
+  const int64_t N = m.size(0);
+  TORCH_CHECK(nq == 1 || nq == 2 || nq == 4 || nq == 8, "NQ must be 1/2/4/8 (pad on host)");
+  TORCH_CHECK((int64_t)nq * D * 4 <= 64 * 1024, "NQ*D too large for the LDS stage");
+  TORCH_CHECK(D % 8 == 0, "D % 8");
+  TORCH_CHECK(scores.scalar_type() == at::kFloat && scores.is_contiguous() &&
+              scores.size(0) == nq && scores.size(1) == N, "scores [NQ, N] fp32");
+  const uint8_t* vp = nullptr;
+  if (valid.has_value() && valid->defined()) {
+    TORCH_CHECK(valid->scalar_type() == at::kByte && valid->numel() >= N && valid->is_cuda(),
+                "valid uint8 [>= N]");
+    vp = valid->data_ptr<uint8_t>();
+  }
+  CHECK_RC(omnia_cosine_scores(scores.data_ptr<float>(), q.data_ptr<float>(), nq, m.data_ptr(),
+                               N, D, vp, cur_stream()), "cosine_scores");
+}
+
+void topk(at::Tensor out_idx, at::Tensor out_val, at::Tensor scores, int64_t k) {
+  CHECK_GPU(scores);
+  TORCH_CHECK(scores.scalar_type() == at::kFloat && scores.is_contiguous() && scores.dim() == 2,
+              "scores [NQ, N] fp32 contiguous");
+  const int nq = scores.size(0);
+  const int64_t N = scores.size(1);
+  TORCH_CHECK(k >= 1 && k <= 1024 && k <= N, "1 <= k <= min(1024, N)");
+  CHECK_I32(out_idx);
+  TORCH_CHECK(out_val.scalar_type() == at::kFloat, "out_val fp32");
+  TORCH_CHECK(out_idx.numel() == nq * k && out_val.numel() == nq * k && out_idx.is_contiguous() &&
+              out_val.is_contiguous(), "outputs [NQ, k]");
+  CHECK_RC(omnia_topk(out_idx.data_ptr<int>(), out_val.data_ptr<float>(),
+                      scores.data_ptr<float>(), nq, N, (int)k, cur_stream()), "topk");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_omnia_kernels, m) {
@@ -199,5 +257,8 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("decode_attention", &decode_attention);
   m.def("prefill_attention", &prefill_attention);
   m.def("sample", &sample);
+  m.def("mean_pool_l2", &mean_pool_l2);
+  m.def("cosine_scores", &cosine_scores);
+  m.def("topk", &topk);
   m.attr("arch") = "gfx950";
 }

@@ -162,3 +162,25 @@ def sample(logits, temperature, top_k=None, top_p=None, generator=None):
         probs = torch.softmax(x, -1)
         out[r] = int(torch.multinomial(probs, 1, generator=generator))
     return out
+
+
+def mean_pool_l2(hidden: torch.Tensor, cu_seqlens: torch.Tensor) -> torch.Tensor:
+    cu = cu_seqlens.tolist()
+    h = hidden.float()
+    out = torch.zeros(len(cu) - 1, h.shape[1], dtype=torch.float32, device=h.device)
+    for b in range(len(cu) - 1):
+        if cu[b + 1] > cu[b]:
+            v = h[cu[b]:cu[b + 1]].mean(0)
+            n = v.norm()
+            out[b] = v / n if n > 0 else v
+    return out
+
+
+def cosine_topk(q: torch.Tensor, m: torch.Tensor, k: int, valid: torch.Tensor | None = None):
+    s = q.float() @ m.float().t()
+    if valid is not None:
+        s = s.masked_fill(valid[: m.shape[0]].to(s.device) == 0, float("-inf"))
+    # stable order: descending score, ascending index on ties
+    idx = torch.arange(m.shape[0], device=s.device).expand_as(s)
+    order = torch.argsort(s, dim=1, descending=True, stable=True)[:, :k]
+    return torch.gather(s, 1, order), torch.gather(idx, 1, order)

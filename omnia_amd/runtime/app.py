@@ -81,6 +81,16 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
         policy = PolicyBrokerClient(cfg.policy_broker_url) if cfg.policy_broker_url else None
         executor = OmniaExecutor(load_tools_config(cfg.tools_config_path),
                                  secrets_dir=cfg.tool_secrets_dir, policy=policy)
+    memory = None
+    if cfg.memory_enabled and cfg.memory_api_url:
+        from ..memory.retriever import HTTPMemoryRetriever
+        from ..memory.tools import memory_tools
+
+        ws = cfg.workspace_uid or cfg.workspace
+        memory = HTTPMemoryRetriever(cfg.memory_api_url, workspace=ws, agent=cfg.agent_name,
+                                     strategy=cfg.memory_strategy, deny_cel=cfg.memory_deny_cel,
+                                     limit=cfg.memory_limit)
+        executor.add_handler(memory_tools(memory.client, ws, cfg.agent_name))
     try:
         await executor.discover()
     except Exception as e:  # noqa: BLE001
@@ -90,12 +100,6 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
         from ..session.httpclient import SessionEventSink
 
         event_sink = SessionEventSink(cfg.session_api_url)
-    memory = None
-    if cfg.memory_enabled and cfg.memory_api_url:
-        from ..memory.retriever import HTTPMemoryRetriever
-
-        memory = HTTPMemoryRetriever(cfg.memory_api_url, workspace=cfg.workspace_uid or
-                                     cfg.workspace, agent=cfg.agent_name)
     evaluator = None
     if cfg.eval_enabled:
         from .evals import InlineEvaluator

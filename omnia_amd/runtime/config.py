@@ -39,6 +39,9 @@ class RuntimeConfig:
     session_api_url: str = ""
     memory_enabled: bool = False
     memory_api_url: str = ""
+    memory_strategy: str = "composite"  # keyword | semantic | composite
+    memory_deny_cel: str = ""
+    memory_limit: int = 10
     policy_broker_url: str = ""
     eval_enabled: bool = False
     tracing_enabled: bool = False
@@ -85,6 +88,9 @@ class RuntimeConfig:
         c.session_api_url = e.get("OMNIA_SESSION_API_URL", "")
         c.memory_enabled = e.get("OMNIA_MEMORY_ENABLED", "false").lower() == "true"
         c.memory_api_url = e.get("OMNIA_MEMORY_API_URL", "")
+        c.memory_strategy = e.get("OMNIA_MEMORY_STRATEGY", c.memory_strategy)
+        c.memory_deny_cel = e.get("OMNIA_MEMORY_DENY_CEL", "")
+        c.memory_limit = int(e.get("OMNIA_MEMORY_LIMIT", c.memory_limit))
         c.policy_broker_url = e.get("OMNIA_POLICY_BROKER_URL", "")
         c.eval_enabled = e.get("OMNIA_EVAL_ENABLED", "false").lower() == "true"
         c.tracing_enabled = e.get("OMNIA_TRACING_ENABLED", "false").lower() == "true"
@@ -123,6 +129,10 @@ class RuntimeConfig:
                 env[k] = v
         if self.memory_enabled:
             env["OMNIA_MEMORY_ENABLED"] = "true"
+            env["OMNIA_MEMORY_STRATEGY"] = self.memory_strategy
+            env["OMNIA_MEMORY_LIMIT"] = str(self.memory_limit)
+            if self.memory_deny_cel:
+                env["OMNIA_MEMORY_DENY_CEL"] = self.memory_deny_cel
         if self.eval_enabled:
             env["OMNIA_EVAL_ENABLED"] = "true"
         for k, v in self.engine.items():

@@ -54,6 +54,7 @@ class EngineConfig:
     tokenizer: str | None = None
     decode_part_size: int = 512
     pipeline: bool = True  # one-deep async decode scheduling
+    checkpoint: str | None = None  # HF safetensors dir (random init when None)
 
     @classmethod
     def from_env(cls, **kw) -> "EngineConfig":
@@ -67,6 +68,8 @@ class EngineConfig:
             "OMNIA_ENGINE_BLOCK_SIZE": ("block_size", int),
             "OMNIA_ENGINE_DEVICE": ("device", str),
             "OMNIA_ENGINE_SWAP_GIB": ("swap_gib", float),
+            "OMNIA_ENGINE_CHECKPOINT": ("checkpoint", str),
+            "OMNIA_ENGINE_USE_GRAPHS": ("use_graphs", lambda v: v.lower() != "false"),
         }
         for k, (f, t) in m.items():
             if k in env:
@@ -75,36 +78,56 @@ class EngineConfig:
 
 
 class LLMEngine:
-    def __init__(self, cfg: EngineConfig, model_cfg: ModelConfig | None = None):
+    def __init__(self, cfg: EngineConfig, model_cfg: ModelConfig | None = None,
+                 weights: dict | None = None):
         self.cfg = cfg
         self.model_cfg = model_cfg or resolve(cfg.model)
-        dev = torch.device(cfg.device if (cfg.device != "cuda" or torch.cuda.is_available())
-                           else "cpu")
-        if dev.type == "cuda" and dev.index is None:
-            dev = torch.device("cuda", torch.cuda.current_device())
+        if cfg.checkpoint and model_cfg is None:
+            from ..models.loader import config_from_hf
+
+            self.model_cfg = config_from_hf(cfg.checkpoint, cfg.model)
+        dev = self._pick_device(cfg)
         self.device = dev
         dtype = getattr(torch, cfg.dtype)
+        st = self._ensure_parallel(cfg, dev)
+        if st.tp_size > 1 and st.tp_rank != 0:
+            raise RuntimeError("TP ranks > 0 run omnia_amd.engine.tp.run_worker, not LLMEngine")
         if dev.type == "cuda":
             from ..ops.gemm_tuning import enable_tuned_gemms
 
             self.tuned_gemms = enable_tuned_gemms(dev.index or 0)
         t0 = time.perf_counter()
+        if weights is None and cfg.checkpoint:
+            from ..models.loader import load_hf_checkpoint
+
+            weights = load_hf_checkpoint(cfg.checkpoint, self.model_cfg, st.tp_size, st.tp_rank,
+                                         dev, dtype)
         self.model = build_model(self.model_cfg, device=dev, dtype=dtype, seed=cfg.seed,
-                                 decode_part_size=cfg.decode_part_size)
+                                 weights=weights, decode_part_size=cfg.decode_part_size)
         self.load_s = time.perf_counter() - t0
-        nb = cfg.num_blocks or self._size_kv_pool(dtype)
+        nb = cfg.num_blocks or self.kv_pool_blocks(cfg, self.model_cfg, self.model.tp, dev, dtype)
+        runner_cls = ModelRunner
+        if st.tp_size > 1:
+            from .tp import TPModelRunner, agree_num_blocks
+
+            nb = agree_num_blocks(nb, dev)
+            runner_cls = TPModelRunner
         self.kv = KVCache.allocate(self.model_cfg, nb, cfg.block_size, dev,
                                    tp_size=self.model.tp, dtype=dtype)
+        self.runner = runner_cls(self.model, self.kv, max_batch=cfg.max_batch,
+                                 max_model_len=cfg.max_model_len, use_graphs=cfg.use_graphs,
+                                 max_prefill_tokens=cfg.max_prefill_tokens)
         swap = None
         if cfg.swap_gib > 0 and dev.type == "cuda":
             swap = SwapSpace(self.kv, cfg.swap_gib)
+            if st.tp_size > 1:
+                from .tp import TPSwapProxy
+
+                swap = TPSwapProxy(swap, self.runner.chan)
         self.blocks = BlockManager(nb, cfg.block_size, swap=swap)
         self.scheduler = Scheduler(
             SchedulerConfig(max_batch=cfg.max_batch, max_prefill_tokens=cfg.max_prefill_tokens,
                             max_model_len=cfg.max_model_len), self.blocks)
-        self.runner = ModelRunner(self.model, self.kv, max_batch=cfg.max_batch,
-                                  max_model_len=cfg.max_model_len, use_graphs=cfg.use_graphs,
-                                  max_prefill_tokens=cfg.max_prefill_tokens)
         self.tokenizer = make_tokenizer(self.model_cfg, cfg.tokenizer)
         self.eos = set(self.tokenizer.eos_token_ids)
         self.seqs: dict[int, Sequence] = {}
@@ -113,24 +136,43 @@ class LLMEngine:
         self.inflight = None
         self.counters = {"prefill_tokens": 0, "decode_tokens": 0, "steps_prefill": 0,
                          "steps_decode": 0, "finished": 0}
-        log.info("engine ready: %s on %s, %d KV blocks x %d tokens, load %.1fs",
-                 self.model_cfg.name, dev, nb, cfg.block_size, self.load_s)
+        log.info("engine ready: %s on %s (tp=%d), %d KV blocks x %d tokens, load %.1fs",
+                 self.model_cfg.name, dev, st.tp_size, nb, cfg.block_size, self.load_s)
 
-    def _size_kv_pool(self, dtype) -> int:
-        cfg, mc = self.cfg, self.model_cfg
+    @staticmethod
+    def _pick_device(cfg: EngineConfig) -> torch.device:
+        dev = torch.device(cfg.device if (cfg.device != "cuda" or torch.cuda.is_available())
+                           else "cpu")
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        return dev
+
+    @staticmethod
+    def _ensure_parallel(cfg: EngineConfig, dev):
+        from ..parallel import state as pstate
+
+        st = pstate.get_state()
+        if cfg.tp > 1 and st.tp_size != cfg.tp:
+            st = pstate.init_distributed(tp_size=cfg.tp, device=dev.type)
+        return st
+
+    @staticmethod
+    def kv_pool_blocks(cfg: EngineConfig, mc: ModelConfig, tp: int, device, dtype) -> int:
         per_block = (mc.kv_bytes_per_token(torch.tensor([], dtype=dtype).element_size())
-                     // self.model.tp) * cfg.block_size
-        if self.device.type == "cuda":
+                     // tp) * cfg.block_size
+        if device.type == "cuda":
             torch.cuda.synchronize()
-            free, total = torch.cuda.mem_get_info(self.device)
+            free, total = torch.cuda.mem_get_info(device)
             # leave room for activations / graphs
             reserve = 6 * 2**30 + cfg.max_prefill_tokens * mc.hidden_size * 40
             budget = max(0, int(free * cfg.kv_fraction) - reserve)
         else:
             budget = 256 * 2**20
-        nb = max(16, budget // per_block)
-        # cap to what max_batch sequences of max_model_len could ever use (+ session cache)
-        return int(nb)
+        return int(max(16, budget // per_block))
+
+    def shutdown(self):
+        if hasattr(self.runner, "shutdown"):
+            self.runner.shutdown()
 
     # --------------------------------------------------------------- requests
     def add_request(self, prompt: list[int] | str, params: SamplingParams | None = None,

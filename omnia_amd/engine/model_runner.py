@@ -137,6 +137,17 @@ class ModelRunner:
         """chunks: (seq, n_new) -- prefill n_new uncached tokens of each seq.
 
         Returns {seq_id: sampled token} for sequences whose prompt completed."""
+        t, meta, sample_seqs = self._prefill_pack(chunks)
+        logits = self._prefill_forward(t, meta)
+        self.stats["prefill_steps"] += 1
+        if not sample_seqs:
+            return {}
+        toks = self._sample_eager(logits[: len(sample_seqs)], sample_seqs)
+        return {s.seq_id: t for s, t in zip(sample_seqs, toks)}
+
+    def _prefill_pack(self, chunks):
+        """Host-side batch assembly -> (packed int64 device tensor, meta, sampled seqs).
+        meta = (T, B, maxb, n_tiles, n_sample)."""
         ids, pos, slots, qsl, seq_lens, sample_rows, sample_seqs = [], [], [], [0], [], [], []
         bs = self.bs
         maxb = 1
@@ -158,7 +169,6 @@ class ModelRunner:
         for i, (s, _) in enumerate(chunks):
             bt[i, :len(s.blocks)] = s.blocks
         tseq, tq0 = ops.prefill_tiles([qsl[i + 1] - qsl[i] for i in range(B)])
-        dev = self.device
         # one pinned packed upload
         arr = np.concatenate([
             np.asarray(ids, np.int64), np.asarray(pos, np.int64), np.asarray(slots, np.int64),
@@ -167,8 +177,11 @@ class ModelRunner:
             bt.reshape(-1).astype(np.int64)])
         t = torch.from_numpy(arr)
         if self.is_gpu:
-            t = t.pin_memory().to(dev, non_blocking=True)
-        T = len(ids)
+            t = t.pin_memory().to(self.device, non_blocking=True)
+        return t, (len(ids), B, maxb, len(tseq), len(sample_rows)), sample_seqs
+
+    def _prefill_forward(self, t: torch.Tensor, meta) -> torch.Tensor:
+        T, B, maxb, n_tiles, n_sample = meta
         o = 0
 
         def take(n, dtype):
@@ -183,16 +196,11 @@ class ModelRunner:
             is_decode=False, num_seqs=B)
         fb.q_start_loc = take(B + 1, torch.int32)
         fb.seq_lens = take(B, torch.int32)
-        fb.tile_seq = take(len(tseq), torch.int32)
-        fb.tile_q0 = take(len(tq0), torch.int32)
-        fb.logits_indices = take(max(1, len(sample_rows)), torch.int64)
+        fb.tile_seq = take(n_tiles, torch.int32)
+        fb.tile_q0 = take(n_tiles, torch.int32)
+        fb.logits_indices = take(max(1, n_sample), torch.int64)
         fb.block_tables = take(B * maxb, torch.int32).view(B, maxb)
-        logits = self.model.forward(fb, self.kv)
-        self.stats["prefill_steps"] += 1
-        if not sample_seqs:
-            return {}
-        toks = self._sample_eager(logits[: len(sample_seqs)], sample_seqs)
-        return {s.seq_id: t for s, t in zip(sample_seqs, toks)}
+        return self.model.forward(fb, self.kv)
 
     def _sample_eager(self, logits, seqs: list[Sequence]) -> list[int]:
         n = len(seqs)
@@ -304,9 +312,8 @@ class ModelRunner:
         if st.event is not None:
             st.event.synchronize()  # host staging buffer free again
         self._decode_inputs(seqs, nrows, ncols, st)
-        g = self.graphs.get((nrows, ncols)) or self._capture(nrows, ncols)
-        g.replay()
-        self.stats["graph_replays"] += 1
+        self._before_replay(nrows, ncols)
+        self._replay(nrows, ncols)
         out_host[:n].copy_(self.out_tok[:n], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
@@ -314,6 +321,14 @@ class ModelRunner:
         for i, s in enumerate(seqs):
             s.slot = i
         return DecodeHandle(seqs, out_host, ev, n)
+
+    def _before_replay(self, nrows: int, ncols: int):
+        """Hook: TP runners broadcast the step inputs to their workers here."""
+
+    def _replay(self, nrows: int, ncols: int):
+        g = self.graphs.get((nrows, ncols)) or self._capture(nrows, ncols)
+        g.replay()
+        self.stats["graph_replays"] += 1
 
     @staticmethod
     def collect(h: "DecodeHandle") -> list[int]:
@@ -328,10 +343,17 @@ class ModelRunner:
         ncols = self._ctx_bucket(max(s.length for s in seqs))
         st = self.stage[0]
         self._decode_inputs(seqs, n, ncols, st)
-        fb = self._decode_fb(n, ncols)
-        logits = self.model.forward(fb, self.kv)
-        self.stats["eager_decodes"] += 1
+        self._before_eager(n, ncols)
+        logits = self._eager_forward(n, ncols)
         return self._sample_eager(logits, seqs)
+
+    def _before_eager(self, n: int, ncols: int):
+        """Hook: TP runners broadcast the eager-decode inputs here."""
+
+    def _eager_forward(self, n: int, ncols: int):
+        fb = self._decode_fb(n, ncols)
+        self.stats["eager_decodes"] += 1
+        return self.model.forward(fb, self.kv)
 
 
 PLACEHOLDER = -1

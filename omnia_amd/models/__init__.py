@@ -6,6 +6,8 @@ def build_model(cfg: ModelConfig, device="cpu", dtype=None, seed: int = 0, **kw)
     import torch
 
     dtype = dtype or torch.bfloat16
+    if kw.get("weights") is None:
+        kw.pop("weights", None)
     if cfg.arch == "llama":
         from .llama import LlamaModel
 

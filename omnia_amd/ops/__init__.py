@@ -13,6 +13,7 @@ import os
 import threading
 
 import torch
+import torch.nn.functional as F
 
 from . import reference as ref
 
@@ -246,3 +247,58 @@ def cosine_topk(q: torch.Tensor, m: torch.Tensor, k: int, valid: torch.Tensor | 
             i += n
         return torch.cat(vals), torch.cat(idxs)
     return ref.cosine_topk(q, m, k, valid)
+
+
+# ------------------------------------------------------------- MoE (K14)
+MOE_LIBRARY_ROWS = 1024  # mean rows/expert above which eager calls use hipBLASLt per expert
+
+
+def moe(x: torch.Tensor, router: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor,
+        k: int, n_experts: int, e_lo: int = 0, renorm: bool = True,
+        graph_safe: bool = True) -> torch.Tensor:
+    """Top-k MoE FFN over the local experts ``[e_lo, e_lo + w_gu.shape[0])``.
+
+    x [T, d] bf16, router [E, d], w_gu [E_loc, 2I, d] (gate ; up), w_down [E_loc, d, I].
+    Returns the local experts' weighted contribution [T, d] (all-reduce over the
+    EP group to complete it).  ``graph_safe`` keeps every shape static and the
+    whole path on device (hipGraph decode); otherwise large batches run each
+    expert's GEMMs on hipBLASLt after one host sync on the expert counts."""
+    e_hi = e_lo + w_gu.shape[0]
+    if not x.is_cuda:
+        return ref.moe(x, router, w_gu, w_down, k, e_lo, renorm).to(x.dtype)
+    kk = kernels()
+    T, d = x.shape
+    n = T * k
+    logits = F.linear(x, router)
+    ids = torch.empty(T, k, dtype=torch.int32, device=x.device)
+    wts = torch.empty(T, k, dtype=torch.float32, device=x.device)
+    kk.moe_topk(ids, wts, logits, k, renorm)
+    out = torch.empty_like(x)
+    if not graph_safe and n >= MOE_LIBRARY_ROWS * (e_hi - e_lo):
+        flat = ids.view(-1)
+        order = torch.argsort(flat, stable=True)
+        counts = torch.bincount(flat, minlength=n_experts).tolist()  # host sync (eager only)
+        xs = x.index_select(0, (order // k))
+        ys = torch.empty(n, d, dtype=x.dtype, device=x.device)
+        o = sum(counts[:e_lo])
+        for e in range(e_lo, e_hi):
+            c = counts[e]
+            if c:
+                h = F.linear(xs[o:o + c], w_gu[e - e_lo])
+                ys[o:o + c] = F.linear(silu_mul(h), w_down[e - e_lo])
+            o += c
+        Y = torch.empty(n, d, dtype=x.dtype, device=x.device)
+        Y.index_copy_(0, order, ys * wts.view(-1).index_select(0, order)[:, None].to(x.dtype))
+        kk.moe_combine(out, Y, ids, k, e_lo, e_hi)
+        return out
+    mb = kk.moe_max_blocks(n, e_hi - e_lo)
+    sorted_ids = torch.empty(mb * 64, dtype=torch.int32, device=x.device)
+    blk = torch.empty(mb, dtype=torch.int32, device=x.device)
+    nblk = torch.empty(1, dtype=torch.int32, device=x.device)
+    kk.moe_align(sorted_ids, blk, nblk, ids, n_experts, e_lo, e_hi)
+    act = torch.empty(mb * 64, w_down.shape[2], dtype=x.dtype, device=x.device)
+    kk.moe_gemm(0, act, x, w_gu, sorted_ids, blk, nblk, None, k, n, e_lo)
+    Y = torch.empty(n, d, dtype=x.dtype, device=x.device)
+    kk.moe_gemm(1, Y, act, w_down, sorted_ids, blk, nblk, wts.view(-1), k, n, e_lo)
+    kk.moe_combine(out, Y, ids, k, e_lo, e_hi)
+    return out

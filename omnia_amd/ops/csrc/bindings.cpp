@@ -37,6 +37,16 @@ int omnia_cosine_scores(float* scores, const float* q, int nq, const void* m, in
                         const uint8_t* valid, hipStream_t s);
 int omnia_topk(int* out_idx, float* out_val, const float* scores, int nq, int64_t N, int k,
                hipStream_t s);
+int omnia_moe_topk(int* ids, float* wts, const void* logits, int logits_bf16, int n_tok, int E,
+                   int k, int renorm, hipStream_t s);
+int omnia_moe_max_blocks(int n_assign, int n_experts);
+int omnia_moe_align(int* sorted, int* blk_expert, int* n_blocks, const int* ids, int n, int E,
+                    int e_lo, int e_hi, int max_blocks, hipStream_t s);
+int omnia_moe_gemm(int mode, void* out, const void* A, const void* W, const int* sorted,
+                   const int* blk_expert, const int* n_blocks, const float* route_w, int K,
+                   int N, int topk, int n_assign, int e_lo, int max_blocks, hipStream_t s);
+int omnia_moe_combine(void* out, const void* Y, const int* ids, int n_tok, int d, int topk,
+                      int e_lo, int e_hi, hipStream_t s);
 }
 
 namespace {
@@ -245,6 +255,75 @@ void topk(at::Tensor out_idx, at::Tensor out_val, at::Tensor scores, int64_t k) 
                       scores.data_ptr<float>(), nq, N, (int)k, cur_stream()), "topk");
 }
 
+// ---------------------------------------------------------------- MoE (K14)
+void moe_topk(at::Tensor ids, at::Tensor wts, at::Tensor logits, int64_t k, bool renorm) {
+  CHECK_GPU(logits); CHECK_I32(ids);
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits [T, E] contiguous");
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "logits bf16/fp32");
+  const int T = logits.size(0), E = logits.size(1);
+  TORCH_CHECK(E <= 64 && k >= 1 && k <= E, "E <= 64, 1 <= k <= E");
+  TORCH_CHECK(ids.numel() == (int64_t)T * k && wts.numel() == (int64_t)T * k &&
+              wts.scalar_type() == at::kFloat && ids.is_contiguous() && wts.is_contiguous(),
+              "ids/wts [T, k]");
+  CHECK_RC(omnia_moe_topk(ids.data_ptr<int>(), wts.data_ptr<float>(), logits.data_ptr(), bf, T,
+                          E, k, renorm, cur_stream()), "moe_topk");
+}
+
+int64_t moe_max_blocks(int64_t n_assign, int64_t n_experts) {
+  return omnia_moe_max_blocks(n_assign, n_experts);
+}
+
+void moe_align(at::Tensor sorted, at::Tensor blk_expert, at::Tensor n_blocks, at::Tensor ids,
+               int64_t E, int64_t e_lo, int64_t e_hi) {
+  CHECK_GPU(ids); CHECK_I32(ids); CHECK_I32(sorted); CHECK_I32(blk_expert); CHECK_I32(n_blocks);
+  const int n = ids.numel();
+  const int mb = blk_expert.numel();
+  TORCH_CHECK(mb >= omnia_moe_max_blocks(n, e_hi - e_lo), "blk_expert too small");
+  TORCH_CHECK(sorted.numel() == (int64_t)mb * 64, "sorted must hold max_blocks*64 rows");
+  TORCH_CHECK(E <= 256 && 0 <= e_lo && e_lo < e_hi && e_hi <= E, "expert range");
+  CHECK_RC(omnia_moe_align(sorted.data_ptr<int>(), blk_expert.data_ptr<int>(),
+                           n_blocks.data_ptr<int>(), ids.data_ptr<int>(), n, E, e_lo, e_hi, mb,
+                           cur_stream()), "moe_align");
+}
+
+void moe_gemm(int64_t mode, at::Tensor out, at::Tensor A, at::Tensor W, at::Tensor sorted,
+              at::Tensor blk_expert, at::Tensor n_blocks, c10::optional<at::Tensor> route_w,
+              int64_t topk, int64_t n_assign, int64_t e_lo) {
+  CHECK_GPU(A); CHECK_BF16(A); CHECK_BF16(W); CHECK_BF16(out);
+  TORCH_CHECK(A.is_contiguous() && W.is_contiguous() && out.is_contiguous(), "contiguous");
+  TORCH_CHECK(W.dim() == 3, "W [E_local, rows, K]");
+  const int K = W.size(2);
+  const int mb = blk_expert.numel();
+  TORCH_CHECK(A.size(-1) == K && K % 64 == 0, "K mismatch / K % 64");
+  int N;
+  if (mode == 0) {
+    N = W.size(1) / 2;
+    TORCH_CHECK(N % 32 == 0 && out.size(0) == (int64_t)mb * 64 && out.size(1) == N,
+                "act [max_blocks*64, I]");
+    TORCH_CHECK(A.size(0) * topk == n_assign, "x rows * topk == n_assign");
+  } else {
+    N = W.size(1);
+    TORCH_CHECK(N % 64 == 0 && out.size(0) == n_assign && out.size(1) == N, "Y [T*k, d]");
+    TORCH_CHECK(A.size(0) == (int64_t)mb * 64, "act rows");
+    TORCH_CHECK(route_w.has_value() && route_w->numel() == n_assign, "route weights");
+  }
+  CHECK_RC(omnia_moe_gemm((int)mode, out.data_ptr(), A.data_ptr(), W.data_ptr(),
+                          sorted.data_ptr<int>(), blk_expert.data_ptr<int>(),
+                          n_blocks.data_ptr<int>(), opt_ptr<float>(route_w), K, N, topk,
+                          n_assign, e_lo, mb, cur_stream()), "moe_gemm");
+}
+
+void moe_combine(at::Tensor out, at::Tensor Y, at::Tensor ids, int64_t topk, int64_t e_lo,
+                 int64_t e_hi) {
+  CHECK_GPU(Y); CHECK_BF16(Y); CHECK_BF16(out); CHECK_I32(ids);
+  const int T = out.size(0), d = out.size(1);
+  TORCH_CHECK(Y.size(0) == (int64_t)T * topk && Y.size(1) == d && ids.numel() == T * topk,
+              "Y [T*k, d]");
+  CHECK_RC(omnia_moe_combine(out.data_ptr(), Y.data_ptr(), ids.data_ptr<int>(), T, d, topk,
+                             e_lo, e_hi, cur_stream()), "moe_combine");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_omnia_kernels, m) {
@@ -260,5 +339,10 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("mean_pool_l2", &mean_pool_l2);
   m.def("cosine_scores", &cosine_scores);
   m.def("topk", &topk);
+  m.def("moe_topk", &moe_topk);
+  m.def("moe_max_blocks", &moe_max_blocks);
+  m.def("moe_align", &moe_align);
+  m.def("moe_gemm", &moe_gemm);
+  m.def("moe_combine", &moe_combine);
   m.attr("arch") = "gfx950";
 }

@@ -184,3 +184,33 @@ def cosine_topk(q: torch.Tensor, m: torch.Tensor, k: int, valid: torch.Tensor | 
     idx = torch.arange(m.shape[0], device=s.device).expand_as(s)
     order = torch.argsort(s, dim=1, descending=True, stable=True)[:, :k]
     return torch.gather(s, 1, order), torch.gather(idx, 1, order)
+
+
+def moe_route(logits: torch.Tensor, k: int, renorm: bool = True):
+    """softmax -> top-k (lowest index wins ties) -> optional renormalisation."""
+    p = torch.softmax(logits.float(), dim=-1)
+    # stable top-k: sort by (-p, index)
+    order = torch.argsort(-p, dim=-1, stable=True)[:, :k]
+    w = torch.gather(p, 1, order)
+    if renorm:
+        w = w / w.sum(-1, keepdim=True)
+    return order.to(torch.int32), w
+
+
+def moe(x: torch.Tensor, router: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor, k: int,
+        e_lo: int = 0, renorm: bool = True, ids=None, wts=None) -> torch.Tensor:
+    """fp32 oracle of the MoE FFN over the experts [e_lo, e_lo + w_gu.shape[0])."""
+    xf = x.float()
+    if ids is None:
+        ids, wts = moe_route(xf @ router.float().t(), k, renorm)
+    out = torch.zeros_like(xf)
+    n_loc = w_gu.shape[0]
+    inter = w_down.shape[2]
+    for t in range(x.shape[0]):
+        for j in range(k):
+            e = int(ids[t, j]) - e_lo
+            if 0 <= e < n_loc:
+                h = w_gu[e].float() @ xf[t]
+                a = torch.nn.functional.silu(h[:inter]) * h[inter:]
+                out[t] += float(wts[t, j]) * (w_down[e].float() @ a)
+    return out

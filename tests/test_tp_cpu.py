@@ -18,14 +18,16 @@ from omnia_amd.models.loader import shard_weights
 PROMPTS = [list(range(5, 70)), list(range(100, 130)), list(range(7, 200, 3))]
 
 
-def _cfg(tp):
-    return EngineConfig(model="tiny-llama", device="cpu", dtype="float32", tp=tp, num_blocks=64,
+def _cfg(tp, model="tiny-llama"):
+    return EngineConfig(model=model, device="cpu", dtype="float32", tp=tp, num_blocks=64,
                         block_size=32, max_batch=8, max_model_len=1024, max_prefill_tokens=64,
                         use_graphs=False)
 
 
-def _full_weights():
-    return LlamaModel(resolve("tiny-llama"), device="cpu", dtype=torch.float32, seed=3).w
+def _full_weights(model="tiny-llama"):
+    from omnia_amd.models import build_model
+
+    return build_model(resolve(model), device="cpu", dtype=torch.float32, seed=3).w
 
 
 def _generate(eng):
@@ -36,17 +38,17 @@ def _generate(eng):
     return out + [t2.output], t2.prefix_hit
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, model="tiny-llama"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from omnia_amd.engine import tp
     from omnia_amd.parallel import state as pstate
 
     try:
-        cfg = _cfg(world)
-        full = _full_weights()  # built before the TP state exists: the whole model
+        cfg = _cfg(world, model)
+        full = _full_weights(model)  # built before the TP state exists: the whole model
         pstate.init_distributed(tp_size=world, backend="gloo", device="cpu")
-        w = shard_weights(full, resolve("tiny-llama"), world, rank)
+        w = shard_weights(full, resolve(model), world, rank)
         eng = tp.start(cfg, weights=w)
         if eng is not None:
             res = _generate(eng)
@@ -67,12 +69,14 @@ def _free_port():
     return p
 
 
-def test_tp2_engine_matches_single_rank():
-    ref = _generate(LLMEngine(_cfg(1), weights=_full_weights()))
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])
+def test_tp2_engine_matches_single_rank(model):
+    """tiny-mixtral at TP=2 is expert parallel: 2 of 4 experts per rank."""
+    ref = _generate(LLMEngine(_cfg(1, model), weights=_full_weights(model)))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, model)) for r in range(2)]
     for p in procs:
         p.start()
     try:

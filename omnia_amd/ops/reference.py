@@ -198,8 +198,13 @@ def moe_route(logits: torch.Tensor, k: int, renorm: bool = True):
 
 
 def moe(x: torch.Tensor, router: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor, k: int,
-        e_lo: int = 0, renorm: bool = True, ids=None, wts=None) -> torch.Tensor:
-    """fp32 oracle of the MoE FFN over the experts [e_lo, e_lo + w_gu.shape[0])."""
+        e_lo: int = 0, renorm: bool = True, ids=None, wts=None,
+        act_dtype=None) -> torch.Tensor:
+    """fp32 oracle of the MoE FFN over the experts [e_lo, e_lo + w_gu.shape[0]).
+
+    ``ids``/``wts`` pin the routing (so near-tie top-k choices cannot flip between
+    implementations); ``act_dtype`` rounds the SwiGLU activation like a kernel
+    that stores it (bf16) between the two GEMMs."""
     xf = x.float()
     if ids is None:
         ids, wts = moe_route(xf @ router.float().t(), k, renorm)
@@ -212,5 +217,7 @@ def moe(x: torch.Tensor, router: torch.Tensor, w_gu: torch.Tensor, w_down: torch
             if 0 <= e < n_loc:
                 h = w_gu[e].float() @ xf[t]
                 a = torch.nn.functional.silu(h[:inter]) * h[inter:]
+                if act_dtype is not None:
+                    a = a.to(act_dtype).float()
                 out[t] += float(wts[t, j]) * (w_down[e].float() @ a)
     return out

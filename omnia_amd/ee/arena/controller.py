@@ -1,0 +1,144 @@
+"""ArenaJob reconciler (``ee/internal/controller/arenajob_controller.go``).
+
+Pending job -> resolve its ArenaSource (inline ``spec.config`` or ConfigMap-like
+data), partition scenarios x providers x trials into work items, enqueue, start
+``workers.replicas`` worker tasks ("pods" in single-node mode), then aggregate
+results, evaluate ``loadTest.thresholds`` and write ``status``
+(phase Running -> Succeeded / Failed, progress, per-metric verdicts)."""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+
+import yaml
+
+from ...operator.apistore import set_condition
+from .profile import LoadProfile
+from .queue import WorkItem
+from .stats import JobStats, evaluate
+from .worker import ArenaWorker
+
+log = logging.getLogger("omnia.arena.controller")
+
+
+def partition(job_name: str, scenarios: dict, providers: dict, trials: int = 1) -> list:
+    return [WorkItem(job_id=job_name, scenario_id=s, provider_id=p, config={"trial": t})
+            for t in range(max(1, trials)) for s in scenarios for p in providers]
+
+
+def load_arena_config(store, job: dict) -> dict:
+    spec = job["spec"]
+    ns = job["metadata"].get("namespace", "default")
+    src = store.get("ArenaSource", spec["sourceRef"]["name"], ns)
+    sspec = src.get("spec", {})
+    fname = spec.get("arenaFile") or "config.arena.yaml"
+    if sspec.get("type") == "configmap":
+        cm = store.get("ConfigMap", sspec["configMap"]["name"], ns)
+        return yaml.safe_load((cm.get("data") or {}).get(fname, "")) or {}
+    # git / oci / workspace sources are materialised on disk by the source syncer
+    path = (src.get("status") or {}).get("artifact", {}).get("path")
+    if not path:
+        raise RuntimeError(f"ArenaSource {ns}/{src['metadata']['name']} has no synced artifact")
+    import os
+
+    with open(os.path.join(path, fname)) as f:
+        return yaml.safe_load(f) or {}
+
+
+class ArenaJobController:
+    def __init__(self, store, queue, provider_objects: dict | None = None):
+        self.store = store
+        self.q = queue
+        self.provider_objects = provider_objects or {}
+        self.tasks: dict[str, asyncio.Task] = {}
+
+    async def reconcile(self, ns: str, name: str):
+        job = self.store.get("ArenaJob", name, ns)
+        phase = (job.get("status") or {}).get("phase", "")
+        if phase in ("Succeeded", "Failed", "Cancelled") or name in self.tasks:
+            return
+        if (job.get("spec") or {}).get("cancelled"):
+            self._status(job, "Cancelled")
+            return
+        self.tasks[name] = asyncio.create_task(self._run(job))
+
+    def _status(self, job, phase, **extra):
+        st = dict(job.get("status") or {})
+        st.update(phase=phase, **extra)
+        set_condition(st, "Complete" if phase in ("Succeeded", "Failed") else "Running",
+                      True, phase, extra.get("message", ""))
+        job["status"] = st
+        try:
+            self.store.update_status(job)
+        except Exception as e:  # noqa: BLE001
+            log.debug("status update failed: %s", e)
+
+    async def _run(self, job):
+        md, spec = job["metadata"], job["spec"]
+        cfg = load_arena_config(self.store, job)
+        scenarios = {s["id"]: s for s in cfg.get("scenarios", [])}
+        providers = {}
+        for p in cfg.get("providers", []):
+            p = dict(p)
+            if p.get("mode") == "direct":
+                p["object"] = self.provider_objects[p["id"]]
+            providers[p["id"]] = p
+        items = partition(md["name"], scenarios, providers, int(spec.get("trials") or 1))
+        await self.q.enqueue(items)
+        lt = spec.get("loadTest") or {}
+        ramp = lt.get("ramp") or {}
+        conc = int(lt.get("concurrency") or lt.get("vusPerWorker") or 4)
+        replicas = int((spec.get("workers") or {}).get("replicas") or 1)
+        self._status(job, "Running", progress={"total": len(items), "done": 0},
+                     startTime=time.time())
+        t0 = time.perf_counter()
+        budget = float(lt["budgetLimit"]) if lt.get("budgetLimit") else None
+        workers = [ArenaWorker(self.q, md["name"], scenarios, providers,
+                               LoadProfile(max(1, conc // replicas),
+                                           float(ramp.get("upSeconds") or 0),
+                                           float(ramp.get("downSeconds") or 0)),
+                               budget=budget / replicas if budget else None)
+                   for _ in range(replicas)]
+        await asyncio.gather(*(w.run() for w in workers))
+        wall = time.perf_counter() - t0
+        results = await self.q.results_of(md["name"])
+        turn_results = []
+        for r in results:  # per-turn timing drives latency/TTFT percentiles
+            for t in r.get("turns") or []:
+                turn_results.append({**t, "passed": r.get("passed"), "error": r.get("error")})
+        stats = JobStats.from_results(results, wall)
+        tstats = JobStats.from_results(turn_results, wall) if turn_results else stats
+        stats.latencies_ms, stats.ttfts_ms = tstats.latencies_ms, tstats.ttfts_ms
+        verdicts, ok = evaluate(lt.get("thresholds") or [], stats)
+        phase = "Succeeded" if ok and stats.errors < max(1, stats.total) else "Failed"
+        job = self.store.get("ArenaJob", md["name"], md.get("namespace", "default"))
+        self._status(job, phase, progress={"total": len(items), "done": len(results)},
+                     results=stats.to_json(), thresholds=[str(v) for v in verdicts],
+                     completionTime=time.time(), message="thresholds " + (
+                         "passed" if ok else "failed"))
+        return stats
+
+
+class ArenaJobReconciler:
+    """Manager adapter: the operator's reconcile loop is synchronous; jobs run as
+    tasks on the manager's event loop (one worker "pod" group per job)."""
+
+    kind = "ArenaJob"
+
+    def __init__(self, queue=None, provider_objects: dict | None = None):
+        from .queue import MemoryQueue
+
+        self.queue = queue or MemoryQueue()
+        self.provider_objects = provider_objects or {}
+        self.ctl = None
+
+    def reconcile(self, store, ns, name):
+        if self.ctl is None:
+            self.ctl = ArenaJobController(store, self.queue, self.provider_objects)
+        try:
+            store.get("ArenaJob", name, ns or "default")
+        except KeyError:
+            return None
+        asyncio.get_event_loop().create_task(self.ctl.reconcile(ns or "default", name))
+        return None

@@ -1,0 +1,76 @@
+"""Fleet mode: drive a deployed agent through its WebSocket facade and time it
+(``ee/pkg/arena/fleet/client.go:124-179``, ``fleet/provider.go``).
+
+TTFT = first ``chunk`` (or ``done`` when the agent does not stream) after the
+``message`` frame; turn latency = ``done`` arrival.  Client-side tools are
+answered with a canned result so tool loops complete."""
+from __future__ import annotations
+
+import json
+import time
+
+import aiohttp
+
+
+class FleetSession:
+    def __init__(self, url: str, agent: str = "", headers: dict | None = None,
+                 timeout_s: float = 120.0):
+        self.url = url
+        self.agent = agent
+        self.headers = headers or {}
+        self.timeout_s = timeout_s
+        self._http = None
+        self.ws = None
+        self.session_id = ""
+
+    async def __aenter__(self):
+        self._http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None))
+        url = self.url + (("&" if "?" in self.url else "?") + f"agent={self.agent}"
+                          if self.agent else "")
+        self.ws = await self._http.ws_connect(url, headers=self.headers, max_msg_size=0)
+        hello = await self.ws.receive_json(timeout=self.timeout_s)
+        if hello.get("type") != "connected":
+            raise RuntimeError(f"facade handshake failed: {hello}")
+        self.session_id = hello.get("session_id", "")
+        return self
+
+    async def __aexit__(self, *exc):
+        if self.ws is not None:
+            await self.ws.close()
+        if self._http is not None:
+            await self._http.close()
+
+    async def turn(self, content: str, metadata: dict | None = None,
+                   tool_result=lambda name, args: {"ok": True}) -> dict:
+        t0 = time.perf_counter()
+        await self.ws.send_json({"type": "message", "content": content,
+                                 "metadata": metadata or {}})
+        ttft, text, usage = None, [], {}
+        while True:
+            msg = await self.ws.receive(timeout=self.timeout_s)
+            if msg.type != aiohttp.WSMsgType.TEXT:
+                raise RuntimeError(f"unexpected websocket frame {msg.type}")
+            f = json.loads(msg.data)
+            t = f.get("type")
+            if t == "chunk":
+                if ttft is None:
+                    ttft = time.perf_counter() - t0
+                text.append(f.get("content", ""))
+            elif t == "tool_call":
+                tc = f["tool_call"]
+                await self.ws.send_json({"type": "tool_call_ack",
+                                         "tool_call_ack": {"call_id": tc["id"]}})
+                await self.ws.send_json({"type": "tool_result", "tool_result": {
+                    "call_id": tc["id"], "result": tool_result(tc.get("name"),
+                                                               tc.get("arguments"))}})
+            elif t == "done":
+                lat = time.perf_counter() - t0
+                if ttft is None:
+                    ttft = lat
+                final = f.get("content") or "".join(text)
+                usage = f.get("usage") or {}
+                return {"content": final, "ttft_ms": ttft * 1e3, "latency_ms": lat * 1e3,
+                        "usage": usage}
+            elif t == "error":
+                err = f.get("error") or {}
+                raise RuntimeError(f"{err.get('code')}: {err.get('message')}")

@@ -532,4 +532,7 @@ def default_reconcilers(gpu_count: int | None = None) -> list:
               "SkillSource", "SessionPrivacyPolicy", "RolloutAnalysis", "ArenaSource",
               "ArenaTemplateSource", "PromptPackSource", "ArenaDevSession"):
         rs.append(SimplePolicyReconciler(k))
+    from ..ee.arena.controller import ArenaJobReconciler
+
+    rs.append(ArenaJobReconciler())
     return rs

@@ -326,6 +326,12 @@ class MiniRedis:
             h[a[i]] = a[i + 1]
         return n
 
+    def c_hincrby(self, a):
+        h = self.data.setdefault(a[0], {})
+        v = int(h.get(a[1], b"0")) + int(a[2])
+        h[a[1]] = str(v).encode()
+        return v
+
     def c_hget(self, a):
         h = self.data.get(a[0]) if self._alive(a[0]) else None
         return None if not isinstance(h, dict) else h.get(a[1])

@@ -1,0 +1,164 @@
+"""Arena (load profile, queues incl. Redis Streams reclaim, VU pool over a real
+facade in fleet mode, thresholds, ArenaJob controller) and the eval worker
+(sampling, stream consumption, session-api write-back)."""
+import asyncio
+import json
+
+import pytest
+from aiohttp import web
+
+from omnia_amd.ee.arena.controller import ArenaJobController
+from omnia_amd.ee.arena.profile import LoadProfile
+from omnia_amd.ee.arena.queue import MemoryQueue, StreamQueue, WorkItem
+from omnia_amd.ee.arena.stats import JobStats, evaluate, metric
+from omnia_amd.ee.arena.worker import ArenaWorker
+from omnia_amd.ee.eval_worker import EvalWorker, fnv1a32, should_sample
+from omnia_amd.utils.resp import MiniRedis, RedisClient
+
+
+def test_load_profile_ramps():
+    p = LoadProfile(10, ramp_up_s=10, ramp_down_s=5)
+    assert p.allowed(0.0, 100) == 0 and p.allowed(5.0, 100) == 5 and p.allowed(20, 100) == 10
+    assert p.allowed(20, 10) == 5 and p.allowed(20, 0) == 1
+    assert LoadProfile(7).allowed(0, 0) == 7
+
+
+def test_stats_and_thresholds():
+    res = [{"passed": True, "latency_ms": 100 * i, "ttft_ms": 10 * i, "output_tokens": 10,
+            "cost": 0.01} for i in range(1, 11)]
+    res.append({"passed": False, "error": "boom"})
+    s = JobStats.from_results(res, wall_s=2.0)
+    assert s.total == 11 and s.errors == 1
+    assert metric(s, "latency_p50") == pytest.approx(0.55)
+    assert metric(s, "tokens_per_second") == pytest.approx(50.0)
+    v, ok = evaluate([{"metric": "latency_p95", "max": "2s"}, {"metric": "error_rate",
+                                                                "max": "0.2"},
+                      {"metric": "ttft_p50", "max": "40ms"}], s)
+    assert [x.passed for x in v] == [True, True, False] and not ok
+    v, ok = evaluate([{"metric": "latency_p99", "max": "not-a-duration"}], JobStats())
+    assert ok  # unavailable / unparseable pass, like the reference
+
+
+def test_stream_queue_reclaim_and_retry():
+    async def go():
+        red = await MiniRedis().start()
+        try:
+            q = StreamQueue(RedisClient(red.url))
+            await q.enqueue([WorkItem("j1", "s1", "p1"), WorkItem("j1", "s2", "p1",
+                                                                  max_attempts=1)])
+            a = await q.claim("j1", "w1", 10)
+            assert len(a) == 2 and (await q.progress("j1"))["processing"] == 2
+            # worker died: visibility timeout 0 -> both return (s2 has no attempts left)
+            assert await q.reclaim("j1", 0.0) == 1
+            b = await q.claim("j1", "w2", 10)
+            assert [i.scenario_id for i in b] == ["s1"] and b[0].attempt == 2
+            await q.complete(b[0], {"passed": True, "latency_ms": 5})
+            assert (await q.results_of("j1")) == [{"passed": True, "latency_ms": 5}]
+        finally:
+            await red.stop()
+
+    asyncio.run(go())
+
+
+async def _facade():
+    """Mock-provider runtime + WebSocket facade (fleet-mode target)."""
+    from omnia_amd.facade.runtime_client import InProcessRuntimeClient
+    from omnia_amd.facade.server import FacadeConfig, FacadeServer
+    from omnia_amd.runtime.app import build_runtime
+    from omnia_amd.runtime.config import RuntimeConfig
+
+    cfg = RuntimeConfig(provider={"type": "mock", "mock": {"scenarios": {
+        "default_response": "Hello there, friend"}}})
+    svc = await build_runtime(cfg)
+    fac = FacadeServer(FacadeConfig(), runtime_client=InProcessRuntimeClient(svc))
+    fac.port = await fac.start("127.0.0.1", 0)
+    return fac
+
+
+def test_arena_job_fleet_mode_end_to_end():
+    from omnia_amd.operator.apistore import APIStore
+
+    async def go():
+        fac = await _facade()
+        try:
+            url = f"http://127.0.0.1:{fac.port}/ws"
+            store = APIStore()
+            import yaml
+
+            arena = {
+                              "scenarios": [
+                                  {"id": "greet", "turns": [
+                                      {"user": "hi", "assertions": [
+                                          {"type": "contains", "params": {"value": "hello"}}]},
+                                      {"user": "again"}]},
+                                  {"id": "strict", "turns": [{"user": "x", "assertions": [
+                                      {"type": "contains", "params": {"value": "nope"}}]}]}],
+                              "providers": [{"id": "fleet", "mode": "fleet", "url": url}]}
+            store.create({"apiVersion": "v1", "kind": "ConfigMap",
+                          "metadata": {"name": "arena-cfg", "namespace": "default"},
+                          "data": {"config.arena.yaml": yaml.safe_dump(arena)}})
+            store.create({"apiVersion": "omnia.altairalabs.ai/v1alpha1", "kind": "ArenaSource",
+                          "metadata": {"name": "src", "namespace": "default"},
+                          "spec": {"type": "configmap", "interval": "5m",
+                                   "configMap": {"name": "arena-cfg"}}})
+            store.create({"apiVersion": "omnia.altairalabs.ai/v1alpha1", "kind": "ArenaJob",
+                          "metadata": {"name": "load1", "namespace": "default"},
+                          "spec": {"sourceRef": {"name": "src"}, "type": "loadtest",
+                                   "trials": 3, "loadTest": {
+                                       "concurrency": 4, "thresholds": [
+                                           {"metric": "latency_p50", "max": "5s"},
+                                           {"metric": "pass_rate", "min": "0.4"}]}}})
+            ctl = ArenaJobController(store, MemoryQueue())
+            await ctl.reconcile("default", "load1")
+            await ctl.tasks["load1"]
+            return store.get("ArenaJob", "load1", "default")["status"]
+        finally:
+            await fac.stop()
+
+    st = asyncio.run(go())
+    assert st["phase"] == "Succeeded", st
+    r = st["results"]
+    assert r["total"] == 6 and r["passed"] == 3 and r["pass_rate"] == 0.5
+    assert r["latency_p50"] > 0 and r["ttft_p50"] <= r["latency_p50"]
+    assert all("PASS" in t for t in st["thresholds"])
+
+
+def test_eval_worker_sampling_and_writeback():
+    assert fnv1a32("") == 0x811C9DC5 and fnv1a32("a") == 0xE40C292C
+    assert should_sample("s", "lightweight", 100) and not should_sample("s", "x", 0)
+    frac = sum(should_sample(f"s{i}", "extended", 10) for i in range(2000)) / 2000
+    assert 0.06 < frac < 0.14
+
+    class Sessions:
+        def __init__(self):
+            self.posted = []
+
+        async def get_messages(self, sid):
+            return [{"id": "m1", "role": "user", "content": "what is 2+2"},
+                    {"id": "m2", "role": "assistant", "content": "The answer is 4."}]
+
+        async def post_eval_results(self, results):
+            self.posted.extend(results)
+
+    async def go():
+        red = await MiniRedis().start()
+        try:
+            rc = RedisClient(red.url)
+            sess = Sessions()
+            defs = [{"id": "has4", "type": "contains", "params": {"value": "4"}},
+                    {"id": "short", "type": "max_length", "params": {"max": 5}},
+                    {"id": "judge", "type": "llm_judge"}]
+            w = EvalWorker(rc, sess, ["ns1"], lambda agent, ns: defs)
+            await w.setup()
+            for role, mid in (("user", "m1"), ("assistant", "m2")):
+                await rc.xadd("omnia:eval-events:ns1", {"event": json.dumps({
+                    "type": "message.appended", "sessionId": "sid", "namespace": "ns1",
+                    "agentName": "a", "messageId": mid, "role": role})})
+            assert await w.poll_once() == 2
+            return sess.posted, w.stats
+        finally:
+            await red.stop()
+
+    posted, stats = asyncio.run(go())
+    assert {(p["evalId"], p["passed"]) for p in posted} == {("has4", True), ("short", False)}
+    assert stats["skipped"] == 1  # the user message

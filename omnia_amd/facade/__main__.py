@@ -1,0 +1,30 @@
+"""``python -m omnia_amd.facade`` -- the facade container entrypoint.
+
+Dials the runtime sidecar over gRPC (retrying until ready), serves WebSocket /
+REST functions (+ A2A / MCP when enabled) and drains gracefully on SIGTERM
+(in-flight turns finish, new connections refused, ``omnia_facade_draining`` = 1)."""
+import asyncio
+import logging
+import os
+import signal
+
+from .app import build_facade, dial_runtime
+
+
+async def main():
+    logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO").upper())
+    env = dict(os.environ)
+    client = await dial_runtime(env.get("OMNIA_RUNTIME_ADDRESS", "127.0.0.1:9000"))
+    fac = build_facade(env, client)
+    await fac.start("0.0.0.0", int(env.get("OMNIA_FACADE_PORT", 8080)))
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(sig, stop.set)
+    await stop.wait()
+    await fac.drain()
+    await fac.stop()
+
+
+if __name__ == "__main__":
+    asyncio.run(main())

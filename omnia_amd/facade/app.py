@@ -1,0 +1,112 @@
+"""Facade process assembly from env (``cmd/agent/main.go:55-155``).
+
+``build_facade(env, runtime_client)`` is shared by the standalone binary
+(``python -m omnia_amd.facade``) and the single-node launcher.  Env contract
+(set by the operator's deployment builder):
+
+  OMNIA_AGENT_NAME / OMNIA_NAMESPACE / OMNIA_FACADE_PORT / OMNIA_RUNTIME_ADDRESS
+  OMNIA_MODE (agent|function), OMNIA_FACADE_TYPES (websocket,rest,a2a,mcp)
+  OMNIA_HANDLER_MODE (runtime|echo|demo), OMNIA_INPUT_SCHEMA / OMNIA_OUTPUT_SCHEMA
+  auth: OMNIA_AUTH_SHARED_TOKEN, OMNIA_AUTH_CLIENT_KEYS (json {id: sha256}),
+        OMNIA_OIDC_ISSUER / OMNIA_OIDC_AUDIENCE / OMNIA_OIDC_HS256_SECRET /
+        OMNIA_OIDC_JWKS_FILE, OMNIA_EDGE_TRUST=true, OMNIA_MGMT_PLANE_KEY,
+        OMNIA_AUTH_ALLOW_ANONYMOUS (default true when no validator is configured)
+  recording: OMNIA_SESSION_API_URL (+ OMNIA_RECORDING_WORKERS / _QUEUE)
+  limits: OMNIA_MAX_CONNECTIONS, OMNIA_MSG_RATE, OMNIA_MSG_BURST, OMNIA_DRAIN_TIMEOUT
+"""
+from __future__ import annotations
+
+import json
+import os
+
+from .auth import (AuthChain, ClientKeyValidator, EdgeTrustValidator, MgmtPlaneValidator,
+                   OIDCValidator, SharedTokenValidator)
+from .server import FacadeConfig, FacadeServer
+
+
+def auth_from_env(env) -> AuthChain:
+    vs = []
+    if env.get("OMNIA_MGMT_PLANE_KEY"):
+        vs.append(MgmtPlaneValidator(env["OMNIA_MGMT_PLANE_KEY"].encode()))
+    if env.get("OMNIA_AUTH_SHARED_TOKEN"):
+        vs.append(SharedTokenValidator(env["OMNIA_AUTH_SHARED_TOKEN"]))
+    if env.get("OMNIA_AUTH_CLIENT_KEYS"):
+        vs.append(ClientKeyValidator(json.loads(env["OMNIA_AUTH_CLIENT_KEYS"])))
+    if env.get("OMNIA_OIDC_ISSUER") or env.get("OMNIA_OIDC_HS256_SECRET"):
+        jwks = None
+        if env.get("OMNIA_OIDC_JWKS_FILE"):
+            with open(env["OMNIA_OIDC_JWKS_FILE"]) as f:
+                jwks = json.load(f)
+        hs = env.get("OMNIA_OIDC_HS256_SECRET")
+        vs.append(OIDCValidator(env.get("OMNIA_OIDC_ISSUER"), env.get("OMNIA_OIDC_AUDIENCE"),
+                                jwks=jwks, hs_key=hs.encode() if hs else None))
+    if env.get("OMNIA_EDGE_TRUST", "").lower() == "true":
+        vs.append(EdgeTrustValidator())
+    anon = env.get("OMNIA_AUTH_ALLOW_ANONYMOUS", "true" if not vs else "false").lower() == "true"
+    return AuthChain(vs, allow_anonymous=anon)
+
+
+def config_from_env(env) -> FacadeConfig:
+    funcs = {}
+    if env.get("OMNIA_MODE") == "function":
+        funcs["*"] = {"input_schema": json.loads(env.get("OMNIA_INPUT_SCHEMA", "null")),
+                      "output_schema": json.loads(env.get("OMNIA_OUTPUT_SCHEMA", "null"))}
+    c = FacadeConfig(agent=env.get("OMNIA_AGENT_NAME", "agent"),
+                     namespace=env.get("OMNIA_NAMESPACE", "default"),
+                     port=int(env.get("OMNIA_FACADE_PORT", 8080)), functions=funcs)
+    for k, f, t in (("OMNIA_MAX_CONNECTIONS", "max_connections", int),
+                    ("OMNIA_MSG_RATE", "msg_rate", float), ("OMNIA_MSG_BURST", "msg_burst", float),
+                    ("OMNIA_DRAIN_TIMEOUT", "drain_timeout_s", float),
+                    ("OMNIA_MEDIA_ENABLED", "media_enabled", lambda v: v.lower() == "true")):
+        if env.get(k):
+            setattr(c, f, t(env[k]))
+    return c
+
+
+def build_facade(env, runtime_client, recorder=None) -> FacadeServer:
+    handler = None
+    mode = env.get("OMNIA_HANDLER_MODE", "runtime")
+    if mode in ("echo", "demo"):
+        from .handlers import DemoHandler, EchoHandler
+
+        handler = EchoHandler() if mode == "echo" else DemoHandler()
+    if recorder is None and env.get("OMNIA_SESSION_API_URL"):
+        from ..session.httpclient import RecordingPool, SessionHTTPClient
+
+        recorder = RecordingPool(SessionHTTPClient(env["OMNIA_SESSION_API_URL"]),
+                                 workers=int(env.get("OMNIA_RECORDING_WORKERS", 100)),
+                                 queue=int(env.get("OMNIA_RECORDING_QUEUE", 1000)))
+    fac = FacadeServer(config_from_env(env), handler=handler, runtime_client=runtime_client,
+                       auth=auth_from_env(env), recorder=recorder)
+    types = set(filter(None, env.get("OMNIA_FACADE_TYPES", "").split(",")))
+    if "a2a" in types:
+        from .a2a import mount_a2a
+
+        mount_a2a(fac, runtime_client)
+    if "mcp" in types or env.get("OMNIA_MCP_ENABLED", "").lower() == "true":
+        from .mcp import mount_mcp
+
+        mount_mcp(fac, runtime_client)
+    return fac
+
+
+async def dial_runtime(address: str, attempts: int = 30, delay_s: float = 1.0):
+    """``runtime_dial.go:47-120``: wait for the runtime's gRPC channel to be ready."""
+    import asyncio
+
+    import grpc
+
+    from .runtime_client import GrpcRuntimeClient
+
+    client = GrpcRuntimeClient(address)
+    for i in range(attempts):
+        try:
+            await asyncio.wait_for(client.ch.channel_ready(), timeout=delay_s * 2)
+            return client
+        except (asyncio.TimeoutError, grpc.aio.AioRpcError):
+            await asyncio.sleep(delay_s)
+    raise RuntimeError(f"runtime at {address} not reachable after {attempts} attempts")
+
+
+def env() -> dict:
+    return dict(os.environ)

@@ -77,7 +77,6 @@ class LocalLauncher:
 
     async def _start_pod(self, dep: dict, pod: Pod):
         from ..facade.runtime_client import GrpcRuntimeClient, InProcessRuntimeClient
-        from ..facade.server import FacadeConfig, FacadeServer
         from ..runtime.app import build_runtime
         from ..runtime.config import RuntimeConfig
         from ..runtime.server import serve_grpc
@@ -99,31 +98,9 @@ class LocalLauncher:
             client = GrpcRuntimeClient(f"127.0.0.1:{gport}")
         else:
             client = InProcessRuntimeClient(svc)
-        fenv = _env(cs["facade"])
-        funcs = {}
-        if fenv.get("OMNIA_MODE") == "function":
-            funcs["*"] = {"input_schema": json.loads(fenv.get("OMNIA_INPUT_SCHEMA", "null")),
-                          "output_schema": json.loads(fenv.get("OMNIA_OUTPUT_SCHEMA",
-                                                               "null"))}
-        handler = None
-        mode = fenv.get("OMNIA_HANDLER_MODE", "runtime")
-        if mode in ("echo", "demo"):
-            from ..facade.handlers import DemoHandler, EchoHandler
+        from ..facade.app import build_facade
 
-            handler = EchoHandler() if mode == "echo" else DemoHandler()
-        fac = FacadeServer(FacadeConfig(agent=fenv.get("OMNIA_AGENT_NAME", "agent"),
-                                        namespace=fenv.get("OMNIA_NAMESPACE", "default"),
-                                        functions=funcs),
-                           handler=handler, runtime_client=client)
-        types = set(filter(None, fenv.get("OMNIA_FACADE_TYPES", "").split(",")))
-        if "a2a" in types:
-            from ..facade.a2a import mount_a2a
-
-            mount_a2a(fac, client)
-        if "mcp" in types:
-            from ..facade.mcp import mount_mcp
-
-            mount_mcp(fac, client)
+        fac = build_facade(_env(cs["facade"]), client)
         pod.port = await fac.start("127.0.0.1", 0)
         pod.facade = fac
 

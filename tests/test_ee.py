@@ -156,3 +156,67 @@ def test_broker_http_with_runtime_client_and_watcher():
             await runner.cleanup()
 
     asyncio.run(go())
+
+
+def test_privacy_api_consent_optout_and_dsar_fanout():
+    from omnia_amd.ee.privacy import FanoutEraser, PrivacyStore, build_app as privacy_app
+    from omnia_amd.memory.api import build_app as memory_app
+    from omnia_amd.memory.model import Memory
+    from omnia_amd.memory.service import MemoryService
+    from omnia_amd.memory.store import MemoryStore
+    from omnia_amd.session.api import build_app as session_app
+    from omnia_amd.session.model import Session
+    from omnia_amd.session.store import TieredSessionService
+
+    async def serve(app):
+        runner = web.AppRunner(app)
+        await runner.setup()
+        site = web.TCPSite(runner, "127.0.0.1", 0)
+        await site.start()
+        return runner, f"http://127.0.0.1:{site._server.sockets[0].getsockname()[1]}"
+
+    async def go():
+        ss = TieredSessionService()
+        for i in range(3):
+            ss.create(Session(id=f"s{i}", namespace="ns",
+                              virtual_user_id="alice" if i < 2 else "bob"))
+        ms = MemoryService(MemoryStore())
+        await ms.save(Memory(content="alice likes tea", scope={"workspace_id": "w",
+                                                               "virtual_user_id": "alice"}))
+        r1, s_url = await serve(session_app(ss))
+        r2, m_url = await serve(memory_app(ms, enterprise=True))
+        st = PrivacyStore()
+        r3, p_url = await serve(privacy_app(st, FanoutEraser(st, s_url, m_url, ["w"]), m_url))
+        try:
+            async with aiohttp.ClientSession() as s:
+                c = await (await s.get(f"{p_url}/api/v1/privacy/preferences/alice/consent")).json()
+                assert "memory:health" in c["denied"] and "memory:context" in c["defaults"]
+                r = await s.put(f"{p_url}/api/v1/privacy/preferences/alice/consent",
+                                json={"grants": ["memory:health"], "revocations": []})
+                assert "memory:health" in (await r.json())["grants"]
+                r = await s.put(f"{p_url}/api/v1/privacy/preferences/alice/consent",
+                                json={"grants": ["bogus"]})
+                assert r.status == 400
+                await s.post(f"{p_url}/api/v1/privacy/opt-out", json={"userId": "alice"})
+                p = await (await s.get(f"{p_url}/api/v1/privacy/preferences/alice")).json()
+                assert p["optedOut"]
+                r = await s.post(f"{p_url}/api/v1/privacy/deletion-request",
+                                 json={"virtualUserId": "alice", "reason": "gdpr"})
+                rid = (await r.json())["id"]
+                for _ in range(100):
+                    d = await (await s.get(
+                        f"{p_url}/api/v1/privacy/deletion-request/{rid}")).json()
+                    if d["status"] in ("completed", "failed"):
+                        break
+                    await asyncio.sleep(0.05)
+                assert d["status"] == "completed", d
+                assert d["sessionsDeleted"] == 2
+        finally:
+            for r in (r1, r2, r3):
+                await r.cleanup()
+        return ss, ms, st
+
+    ss, ms, st = asyncio.run(go())
+    assert ss.get("s2") is not None and ss.get("s0") is None
+    assert ms.store.list({"workspace_id": "w", "virtual_user_id": "alice"}) == []
+    assert any(e["type"] == "dsar.erasure" for e in st.audit())

@@ -17,7 +17,7 @@ out over own same she should so some such than that the their theirs them themse
 these they this those through to too under until up very was we were what when where which while
 who whom why will with you your yours yourself yourselves remind""".split())
 
-_TOKEN = re.compile(r'"[^"]*"|-?[\w\']+|\bOR\b', re.UNICODE)
+_TOKEN = re.compile(r'"[^"]*"|(?:(?<=\s)|^)-[^\s"]+|[^\s"]+', re.UNICODE)
 _WORD = re.compile(r"[\w]+", re.UNICODE)
 
 
@@ -40,8 +40,8 @@ def to_fts5(query: str) -> str:
             if words:
                 groups[-1].append('"' + " ".join(w.lower() for w in words) + '"')
             continue
-        neg = tok.startswith("-")
-        ts = _terms(tok.lstrip("-"))
+        neg = tok.startswith("-") and len(tok) > 1  # "-word" at a word start negates
+        ts = _terms(tok[1:] if neg else tok)
         if not ts:
             continue
         if neg:

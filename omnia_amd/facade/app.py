@@ -12,6 +12,7 @@
         OMNIA_OIDC_JWKS_FILE, OMNIA_EDGE_TRUST=true, OMNIA_MGMT_PLANE_KEY,
         OMNIA_AUTH_ALLOW_ANONYMOUS (default true when no validator is configured)
   recording: OMNIA_SESSION_API_URL (+ OMNIA_RECORDING_WORKERS / _QUEUE)
+  media: OMNIA_MEDIA_STORAGE=local|s3|gcs|azure (+ OMNIA_MEDIA_ROOT / _BUCKET / ...)
   limits: OMNIA_MAX_CONNECTIONS, OMNIA_MSG_RATE, OMNIA_MSG_BURST, OMNIA_DRAIN_TIMEOUT
 """
 from __future__ import annotations
@@ -76,8 +77,19 @@ def build_facade(env, runtime_client, recorder=None) -> FacadeServer:
         recorder = RecordingPool(SessionHTTPClient(env["OMNIA_SESSION_API_URL"]),
                                  workers=int(env.get("OMNIA_RECORDING_WORKERS", 100)),
                                  queue=int(env.get("OMNIA_RECORDING_QUEUE", 1000)))
-    fac = FacadeServer(config_from_env(env), handler=handler, runtime_client=runtime_client,
-                       auth=auth_from_env(env), recorder=recorder)
+    media = None
+    if env.get("OMNIA_MEDIA_STORAGE"):
+        from ..media import build_media_storage
+
+        media = build_media_storage(env)
+    cfg = config_from_env(env)
+    cfg.media_enabled = cfg.media_enabled or media is not None
+    fac = FacadeServer(cfg, handler=handler, runtime_client=runtime_client,
+                       auth=auth_from_env(env), recorder=recorder, media_store=media)
+    if media is not None:
+        from ..media import mount_media
+
+        mount_media(fac.app, media)
     types = set(filter(None, env.get("OMNIA_FACADE_TYPES", "").split(",")))
     if "a2a" in types:
         from .a2a import mount_a2a

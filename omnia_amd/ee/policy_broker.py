@@ -30,6 +30,7 @@ from aiohttp import web
 
 from ..observability import metrics as M
 from ..utils import cel
+from ..observability.logging import configure as configure_logging
 
 log = logging.getLogger("omnia.policy_broker")
 
@@ -294,7 +295,7 @@ def main(argv=None):
             app["watch"] = asyncio.create_task(w.run())
 
         app.on_startup.append(start)
-    logging.basicConfig(level=logging.INFO)
+    configure_logging()
     web.run_app(app, host=a.host, port=a.port)
 
 

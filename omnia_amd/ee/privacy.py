@@ -28,6 +28,7 @@ import time
 import uuid
 
 from aiohttp import web
+from ..observability.logging import configure as configure_logging
 
 log = logging.getLogger("omnia.privacy")
 
@@ -305,7 +306,7 @@ def main(argv=None):
     store = PrivacyStore(a.db)
     er = FanoutEraser(store, a.session_api, a.memory_api,
                       [w for w in a.workspaces.split(",") if w])
-    logging.basicConfig(level=logging.INFO)
+    configure_logging()
     web.run_app(build_app(store, er, a.memory_api), port=a.port)
 
 

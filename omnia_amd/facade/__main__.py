@@ -9,10 +9,11 @@ import os
 import signal
 
 from .app import build_facade, dial_runtime
+from ..observability.logging import configure as configure_logging
 
 
 async def main():
-    logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO").upper())
+    configure_logging()
     env = dict(os.environ)
     client = await dial_runtime(env.get("OMNIA_RUNTIME_ADDRESS", "127.0.0.1:9000"))
     fac = build_facade(env, client)

@@ -33,6 +33,7 @@ from ..observability import tracing
 from ..utils import jsonschema
 from ..utils.ratelimit import TokenBucket
 from . import protocol as P
+from ..observability import logging as logctx
 from .auth import AuthChain, AuthError
 from .handlers import PendingTools, RuntimeHandler, Writer
 
@@ -392,6 +393,8 @@ class _Connection:
         srv = self.srv
         labels = srv.labels
         t0 = time.perf_counter()
+        logctx.bind(session_id=self.session_id, agent=srv.cfg.agent,
+                    namespace=srv.cfg.namespace)
         M.REQUESTS_INFLIGHT.labels(*labels).inc()
         status = "ok"
         sid = msg.get("session_id") or self.session_id

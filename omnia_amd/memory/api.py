@@ -27,6 +27,7 @@ from .model import (META_ABOUT_KEY, META_ABOUT_KIND, META_CONSENT_CATEGORY, PII_
                     parse_time)
 from .service import MemoryService
 from .store import MultiTierRequest, NotFound
+from ..observability.logging import configure as configure_logging
 
 log = logging.getLogger("omnia.memory.api")
 
@@ -606,7 +607,7 @@ def main(argv=None):
 
     app.on_startup.append(start_workers)
     app.on_cleanup.append(stop_workers)
-    logging.basicConfig(level=logging.INFO)
+    configure_logging()
     web.run_app(app, host=a.host, port=a.port)
 
 

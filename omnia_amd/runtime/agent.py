@@ -27,6 +27,7 @@ from ..engine.sampling_params import SamplingParams
 from ..observability import metrics as M
 from ..observability import tracing
 from ..tools.executor import CallContext, OmniaExecutor
+from ..observability import logging as logctx
 from .chat import Message, ToolCallReq
 from .context_store import StoreUnavailable
 from .promptpack import PromptPack, run_validators
@@ -157,6 +158,7 @@ class Agent:
                        metadata: dict | None = None, ctx: CallContext | None = None,
                        variables: dict | None = None, persist: bool = True) -> TurnResult:
         t_start = time.perf_counter()
+        logctx.bind(session_id=session_id, agent=getattr(ctx, "agent", "") or "")
         M.PIPELINES_ACTIVE.inc()
         ctx = ctx or CallContext(session_id=session_id)
         res = TurnResult()

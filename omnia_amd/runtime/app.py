@@ -22,6 +22,7 @@ from .context_store import make_store
 from .promptpack import PackError, PromptPack
 from .providers import build_provider
 from .server import CAPABILITIES, RuntimeService, serve_grpc, serve_health
+from ..observability.logging import configure as configure_logging
 
 log = logging.getLogger("omnia.runtime")
 
@@ -130,8 +131,7 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
 
 async def run(cfg: RuntimeConfig | None = None):
     cfg = cfg or RuntimeConfig.from_env()
-    logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO").upper(),
-                        format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    configure_logging()
     if cfg.tracing_enabled:
         tracing.configure("omnia-runtime", cfg.tracing_endpoint or None, cfg.tracing_sample_rate)
     svc = await build_runtime(cfg)

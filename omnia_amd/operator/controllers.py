@@ -529,9 +529,12 @@ def default_reconcilers(gpu_count: int | None = None) -> list:
     rs = [PromptPackReconciler(), ProviderReconciler(gpu_count), ToolRegistryReconciler(),
           AgentRuntimeReconciler(gpu_count), WorkspaceReconciler()]
     for k in ("AgentPolicy", "ToolPolicy", "MemoryPolicy", "SessionRetentionPolicy",
-              "SkillSource", "SessionPrivacyPolicy", "RolloutAnalysis", "ArenaSource",
-              "ArenaTemplateSource", "PromptPackSource", "ArenaDevSession"):
+              "SessionPrivacyPolicy", "RolloutAnalysis", "ArenaDevSession"):
         rs.append(SimplePolicyReconciler(k))
+    from .sourcesync import SourceReconciler
+
+    for k in ("SkillSource", "ArenaSource", "ArenaTemplateSource", "PromptPackSource"):
+        rs.append(SourceReconciler(k))
     from ..ee.arena.controller import ArenaJobReconciler
 
     rs.append(ArenaJobReconciler())

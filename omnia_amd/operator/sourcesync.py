@@ -1,0 +1,291 @@
+"""Source sync: materialise PromptKit bundles / skills / arena configs from git,
+ConfigMaps, OCI artifacts or a workspace path into the workspace content tree
+(``internal/sourcesync/{git,oci,configmap,syncer}.go``, ``SyncToFilesystem``
+``syncer.go:92``).
+
+Layout: ``<root>/<namespace>/<kind>/<name>/<revision>/`` with a ``current``
+symlink swapped atomically after a successful sync, so readers never see a
+half-written tree.  Revisions: git commit sha, ConfigMap content hash, OCI
+manifest digest.  ``historyLimit`` old revisions are kept.
+
+* git: ``git`` CLI (clone --depth 1 of a branch/tag, or fetch + checkout of a
+  commit), optional sub-``path``; credentials from a Secret's ``username`` /
+  ``password`` (HTTPS) via ``GIT_ASKPASS``;
+* oci: OCI distribution API over HTTP(S) -- manifest, then each layer blob
+  (tar / tar+gzip) unpacked; anonymous bearer-token challenge supported;
+* configmap: every data key becomes a file.
+
+:class:`SourceReconciler` drives ArenaSource / SkillSource / PromptPackSource
+objects: sync every ``spec.interval`` (unless ``suspend``), write
+``status.artifact {path, revision}``, ``phase`` and a Ready condition.
+"""
+from __future__ import annotations
+
+import hashlib
+import io
+import logging
+import os
+import shutil
+import subprocess
+import tarfile
+import tempfile
+import time
+from pathlib import Path
+
+from .apistore import APIStore, set_condition
+
+log = logging.getLogger("omnia.sourcesync")
+
+
+class SyncError(RuntimeError):
+    pass
+
+
+def parse_duration(s: str | None, default: float = 300.0) -> float:
+    if not s:
+        return default
+    total, num = 0.0, ""
+    units = {"h": 3600, "m": 60, "s": 1}
+    for ch in s.strip():
+        if ch.isdigit() or ch == ".":
+            num += ch
+        elif ch in units and num:
+            total += float(num) * units[ch]
+            num = ""
+        else:
+            raise ValueError(f"bad duration {s!r}")
+    return total + (float(num) if num else 0.0)
+
+
+def _hash_tree(files: dict[str, bytes]) -> str:
+    h = hashlib.sha256()
+    for k in sorted(files):
+        h.update(k.encode() + b"\0" + files[k] + b"\0")
+    return "sha256:" + h.hexdigest()[:16]
+
+
+class SourceSyncer:
+    def __init__(self, root: str, history_limit: int = 5):
+        self.root = Path(root)
+        self.history = history_limit
+
+    def target(self, ns, kind, name) -> Path:
+        return self.root / ns / kind.lower() / name
+
+    # -------------------------------------------------------------- fetchers
+    def _git(self, spec: dict, secret: dict | None, timeout: float) -> tuple[str, Path, Path]:
+        g = spec["git"]
+        ref = g.get("ref") or {}
+        tmp = Path(tempfile.mkdtemp(prefix="omnia-git-"))
+        env = dict(os.environ, GIT_TERMINAL_PROMPT="0")
+        if secret and secret.get("password"):
+            ask = tmp.parent / (tmp.name + "-askpass.sh")
+            ask.write_text("#!/bin/sh\ncase \"$1\" in Username*) echo \"$GIT_USER\";; "
+                           "*) echo \"$GIT_PASS\";; esac\n")
+            ask.chmod(0o700)
+            env.update(GIT_ASKPASS=str(ask), GIT_USER=secret.get("username", "git"),
+                       GIT_PASS=secret["password"])
+
+        def git(*args, cwd=None):
+            r = subprocess.run(["git", *args], cwd=cwd, env=env, capture_output=True,
+                               text=True, timeout=timeout)
+            if r.returncode != 0:
+                raise SyncError(f"git {args[0]} failed: {r.stderr.strip()[:300]}")
+            return r.stdout.strip()
+
+        repo = tmp / "repo"
+        if ref.get("commit"):
+            git("init", "-q", str(repo))
+            git("remote", "add", "origin", g["url"], cwd=repo)
+            git("fetch", "-q", "--depth", "1", "origin", ref["commit"], cwd=repo)
+            git("checkout", "-q", "FETCH_HEAD", cwd=repo)
+        else:
+            br = ref.get("tag") or ref.get("branch")
+            args = ["clone", "-q", "--depth", "1"] + (["--branch", br] if br else [])
+            git(*args, g["url"], str(repo))
+        rev = git("rev-parse", "HEAD", cwd=repo)
+        src = repo / g["path"] if g.get("path") else repo
+        if not src.exists():
+            raise SyncError(f"path {g.get('path')!r} not found in repository")
+        shutil.rmtree(repo / ".git", ignore_errors=True)
+        return rev, src, tmp
+
+    def _configmap(self, store: APIStore, ns: str, spec: dict) -> tuple[str, dict]:
+        cm = store.try_get("ConfigMap", spec["configMap"]["name"], ns)
+        if cm is None:
+            raise SyncError(f"ConfigMap {spec['configMap']['name']} not found")
+        data = {k: v.encode() if isinstance(v, str) else v for k, v in
+                (cm.get("data") or {}).items()}
+        key = spec["configMap"].get("key")
+        if key:
+            data = {key: data[key]} if key in data else {}
+        return _hash_tree(data), data
+
+    def _oci(self, spec: dict, secret: dict | None, timeout: float) -> tuple[str, dict]:
+        import requests
+
+        url = spec["oci"]["url"].removeprefix("oci://")
+        host, _, rest = url.partition("/")
+        repo, _, tag = rest.partition(":")
+        tag = tag or "latest"
+        scheme = "http" if spec["oci"].get("insecure") else "https"
+        base = f"{scheme}://{host}/v2/{repo}"
+        headers = {"Accept": "application/vnd.oci.image.manifest.v1+json"}
+        auth = (secret.get("username"), secret.get("password")) if secret else None
+        r = requests.get(f"{base}/manifests/{tag}", headers=headers, auth=auth, timeout=timeout)
+        if r.status_code == 401 and "Bearer" in r.headers.get("WWW-Authenticate", ""):
+            chal = dict(kv.split("=", 1) for kv in r.headers["WWW-Authenticate"][7:]
+                        .replace('"', "").split(","))
+            tok = requests.get(chal["realm"], params={"service": chal.get("service"),
+                                                      "scope": chal.get("scope")},
+                               auth=auth, timeout=timeout).json()
+            headers["Authorization"] = "Bearer " + (tok.get("token") or tok.get("access_token"))
+            r = requests.get(f"{base}/manifests/{tag}", headers=headers, timeout=timeout)
+        if r.status_code >= 400:
+            raise SyncError(f"OCI manifest HTTP {r.status_code}")
+        digest = r.headers.get("Docker-Content-Digest") or \
+            "sha256:" + hashlib.sha256(r.content).hexdigest()
+        files: dict[str, bytes] = {}
+        for layer in r.json().get("layers", []):
+            b = requests.get(f"{base}/blobs/{layer['digest']}", headers=headers,
+                             timeout=timeout)
+            if b.status_code >= 400:
+                raise SyncError(f"OCI blob HTTP {b.status_code}")
+            mode = "r:gz" if "gzip" in layer.get("mediaType", "") else "r:*"
+            with tarfile.open(fileobj=io.BytesIO(b.content), mode=mode) as tf:
+                for m in tf.getmembers():
+                    if m.isfile() and not m.name.startswith("/") and ".." not in m.name:
+                        files[m.name] = tf.extractfile(m).read()
+        return digest, files
+
+    # -------------------------------------------------------------- sync
+    def sync(self, store: APIStore, obj: dict) -> dict:
+        md, spec = obj["metadata"], obj["spec"]
+        ns, kind, name = md.get("namespace", "default"), obj["kind"], md["name"]
+        timeout = parse_duration(spec.get("timeout"), 60.0)
+        secret = None
+        sref = ((spec.get("git") or spec.get("oci") or {}).get("secretRef") or {}).get("name")
+        if sref:
+            s = store.try_get("Secret", sref, ns)
+            if s is not None:
+                import base64
+
+                secret = {k: base64.b64decode(v).decode() for k, v in
+                          (s.get("data") or {}).items()}
+                secret.update(s.get("stringData") or {})
+        t = spec.get("type")
+        dest_root = self.target(ns, kind, name)
+        dest_root.mkdir(parents=True, exist_ok=True)
+        if t == "git":
+            rev, src, tmp = self._git(spec, secret, timeout)
+            short = rev[:12]
+            dest = dest_root / short
+            try:
+                if not dest.exists():
+                    shutil.copytree(src, dest)
+            finally:
+                shutil.rmtree(tmp, ignore_errors=True)
+                Path(str(tmp) + "-askpass.sh").unlink(missing_ok=True)
+        elif t in ("configmap", "oci"):
+            rev, files = (self._configmap(store, ns, spec) if t == "configmap"
+                          else self._oci(spec, secret, timeout))
+            short = rev.split(":")[-1][:12]
+            dest = dest_root / short
+            if not dest.exists():
+                tmp = dest_root / (short + ".tmp")
+                shutil.rmtree(tmp, ignore_errors=True)
+                for rel, data in files.items():
+                    p = (tmp / rel).resolve()
+                    if not str(p).startswith(str(tmp.resolve())):
+                        raise SyncError(f"path escapes artifact root: {rel}")
+                    p.parent.mkdir(parents=True, exist_ok=True)
+                    p.write_bytes(data)
+                tmp.mkdir(parents=True, exist_ok=True)
+                tmp.rename(dest)
+        elif t == "workspace":
+            p = Path(spec.get("workspace", {}).get("path", ""))
+            if not p.is_dir():
+                raise SyncError(f"workspace path {p} not found")
+            files = {str(f.relative_to(p)): f.read_bytes() for f in p.rglob("*") if f.is_file()}
+            rev = _hash_tree(files)
+            short = rev.split(":")[-1][:12]
+            dest = dest_root / short
+            if not dest.exists():
+                shutil.copytree(p, dest)
+        else:
+            raise SyncError(f"unsupported source type {t!r}")
+        target = dest / spec["targetPath"] if spec.get("targetPath") else dest
+        cur = dest_root / "current"
+        tmp_link = dest_root / ".current.tmp"
+        if tmp_link.is_symlink() or tmp_link.exists():
+            tmp_link.unlink()
+        tmp_link.symlink_to(dest.name)
+        os.replace(tmp_link, cur)
+        self._gc(dest_root, keep=dest.name, limit=int(spec.get("historyLimit") or self.history))
+        return {"path": str(target), "revision": rev,
+                "files": sum(1 for f in dest.rglob("*") if f.is_file())}
+
+    @staticmethod
+    def _gc(root: Path, keep: str, limit: int):
+        revs = sorted((d for d in root.iterdir() if d.is_dir() and not d.is_symlink()
+                       and not d.name.endswith(".tmp")), key=lambda d: d.stat().st_mtime)
+        for d in revs[:-max(1, limit)]:
+            if d.name != keep:
+                shutil.rmtree(d, ignore_errors=True)
+
+
+class SourceReconciler:
+    """ArenaSource / SkillSource / PromptPackSource reconciler."""
+
+    def __init__(self, kind: str, root: str | None = None):
+        self.kind = kind
+        self.syncer = SourceSyncer(root or os.environ.get("OMNIA_CONTENT_ROOT",
+                                                          tempfile.gettempdir() +
+                                                          "/omnia-content"))
+
+    def reconcile(self, store: APIStore, ns, name):
+        o = store.try_get(self.kind, name, ns)
+        if o is None:
+            return None
+        spec = o["spec"]
+        st = dict(o.get("status") or {})
+        interval = parse_duration(spec.get("interval"), 300.0)
+        if spec.get("suspend"):
+            st["phase"] = "Suspended"
+            set_condition(st, "Ready", False, "Suspended", "", o["metadata"]["generation"])
+        else:
+            try:
+                art = self.syncer.sync(store, o)
+                changed = (st.get("artifact") or {}).get("revision") != art["revision"]
+                st.update(phase="Ready", artifact=art, revision=art["revision"],
+                          lastSyncTime=time.time())
+                if self.kind == "SkillSource":
+                    st["skillCount"] = sum(1 for _ in Path(art["path"]).rglob("SKILL.md"))
+                if self.kind == "PromptPackSource" and changed:
+                    self._publish_pack(store, o, art)
+                set_condition(st, "Ready", True, "Synced", f"revision {art['revision']}",
+                              o["metadata"]["generation"])
+            except (SyncError, subprocess.TimeoutExpired, OSError, ValueError, KeyError) as e:
+                st["phase"] = "Failed"
+                set_condition(st, "Ready", False, "SyncFailed", str(e)[:300],
+                              o["metadata"]["generation"])
+        st["observedGeneration"] = o["metadata"]["generation"]
+        o["status"] = st
+        store.update_status(o)
+        return interval
+
+    @staticmethod
+    def _publish_pack(store: APIStore, src: dict, art: dict):
+        """PromptPackSource: a new revision becomes a ConfigMap the PromptPack
+        reconciler versions (``createVersionOnSync``)."""
+        ns = src["metadata"].get("namespace", "default")
+        pack = Path(art["path"])
+        data = {f.name: f.read_text() for f in pack.iterdir() if f.is_file() and
+                f.suffix in (".json", ".yaml", ".yml", ".md")}
+        name = f"{src['spec']['packName']}-{art['revision'].split(':')[-1][:8]}"
+        if store.try_get("ConfigMap", name, ns) is None:
+            store.create({"apiVersion": "v1", "kind": "ConfigMap",
+                          "metadata": {"name": name, "namespace": ns, "labels": {
+                              "omnia.altairalabs.ai/pack": src["spec"]["packName"]}},
+                          "data": data})
+

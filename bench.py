@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--max-prefill-tokens", type=int, default=16384)
     ap.add_argument("--temperature", type=float, default=0.0)
-    ap.add_argument("--path", choices=["engine", "runtime"], default="engine")
+    ap.add_argument("--path", choices=["engine", "runtime"], default="runtime",
+                    help="runtime = full AgentRuntime turn path (default); engine = engine only")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default="cuda")
     return ap.parse_args()

@@ -367,12 +367,23 @@ class LLMEngine:
 class GenEvent:
     text: str = ""
     token: int | None = None
+    n_tokens: int = 1  # tokens coalesced into this event
     finished: bool = False
     finish_reason: str | None = None
     prompt_tokens: int = 0
     output_tokens: int = 0
     cached_tokens: int = 0
     ttft: float | None = None
+
+
+class _Chan:
+    """Per-request delivery buffer (filled on the consumer's loop, drained whole)."""
+
+    __slots__ = ("items", "event")
+
+    def __init__(self):
+        self.items: list = []
+        self.event = asyncio.Event()
 
 
 class AsyncLLMEngine:
@@ -394,8 +405,9 @@ class AsyncLLMEngine:
 
     @staticmethod
     def _deliver(batch):
-        for q, ev in batch:
-            q.put_nowait(ev)
+        for ch, ev in batch:
+            ch.items.append(ev)
+            ch.event.set()
 
     def _flush(self):
         if self._outbox:
@@ -454,7 +466,7 @@ class AsyncLLMEngine:
     async def generate(self, prompt, params: SamplingParams | None = None,
                        session_id: str | None = None, request_id: str | None = None):
         loop = asyncio.get_running_loop()
-        q: asyncio.Queue = asyncio.Queue()
+        q = _Chan()
         holder = {}
 
         def on_token(s, tok, text):
@@ -477,12 +489,25 @@ class AsyncLLMEngine:
         self.submit(add)
         try:
             while True:
-                ev = await q.get()
-                if isinstance(ev, Exception):
-                    raise ev
-                yield ev
-                if ev.finished:
-                    return
+                await q.event.wait()
+                q.event.clear()
+                items, q.items = q.items, []
+                # adaptive coalescing: tokens that arrived while the consumer was busy
+                # are streamed as one chunk (one token per chunk when it keeps up)
+                text, last_tok, n = [], None, 0
+                for ev in items:
+                    if isinstance(ev, Exception):
+                        raise ev
+                    if ev.finished:
+                        if n:
+                            yield GenEvent(text="".join(text), token=last_tok, n_tokens=n)
+                        yield ev
+                        return
+                    text.append(ev.text)
+                    last_tok = ev.token
+                    n += 1
+                if n:
+                    yield GenEvent(text="".join(text), token=last_tok, n_tokens=n)
         finally:
             s = holder.get("seq")
             if s is not None and not s.is_finished:

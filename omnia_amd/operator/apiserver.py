@@ -33,7 +33,10 @@ def kind_of(plural: str) -> str:
 
 
 def build_app(store: APIStore) -> web.Application:
+    from .restapi import mount
+
     app = web.Application()
+    mount(app, store)  # specific routes first: the generic resource routes below are greedy
 
     def err(status, msg):
         return web.json_response({"kind": "Status", "status": "Failure", "message": msg,

@@ -137,6 +137,11 @@ class LLMEngine:
         self.inflight = None
         self.counters = {"prefill_tokens": 0, "decode_tokens": 0, "steps_prefill": 0,
                          "steps_decode": 0, "finished": 0}
+        # host-side time per phase of pipelined decode (diagnostics; bench reports it)
+        self.timing = {"schedule_s": 0.0, "launch_s": 0.0, "collect_wait_s": 0.0,
+                       "append_s": 0.0, "pipeline_breaks": 0, "gpu_starved_launches": 0}
+        self.step_trace = [] if os.environ.get("OMNIA_STEP_TRACE") else None
+        self.gpu_trace: list = []
         log.info("engine ready: %s on %s (tp=%d), %d KV blocks x %d tokens, load %.1fs",
                  self.model_cfg.name, dev, st.tp_size, nb, cfg.block_size, self.load_s)
 
@@ -219,10 +224,16 @@ class LLMEngine:
         h, self.inflight = self.inflight, None
         if h is None:
             return 0
+        t0 = time.perf_counter()
         toks = self.runner.collect(h)
         now = time.perf_counter()
         for sq, tok in zip(h.seqs, toks):
             self._append(sq, tok, now)
+        tm = self.timing
+        tm["collect_wait_s"] += now - t0
+        if self.step_trace is not None:
+            self.step_trace.append(("collect", h.kind, t0, now))
+        tm["append_s"] += time.perf_counter() - now
         return len(toks)
 
     def _steady(self) -> bool:
@@ -231,12 +242,58 @@ class LLMEngine:
                 self.blocks.num_free >= len(sch.running) + 1)
 
     def _step_pipelined(self) -> int:
-        if self.inflight is not None and not self._steady():
-            return self._flush_inflight()
-        plan = self.scheduler.schedule()
+        sch = self.scheduler
+        h0 = self.inflight
+        if h0 is not None:
+            if h0.kind == "decode" and not self._steady():
+                self.timing["pipeline_breaks"] += 1
+                return self._flush_inflight()
+            if h0.kind == "prefill" and not (sch.waiting or sch.partial):
+                # the next step decodes: it feeds the prefill's sampled tokens
+                return self._flush_inflight()
+        ts = time.perf_counter()
+        plan = sch.schedule()
+        if plan.kind == "prefill" and self.runner.can_pipeline_prefill(plan.prefill):
+            # prefill N+1 is assembled and enqueued while prefill N runs on the GPU;
+            # counters advance now, the completed prompts' tokens arrive at collect
+            t0 = time.perf_counter()
+            self.timing["schedule_s"] += t0 - ts
+            h = self.runner.launch_prefill(plan.prefill)
+            self.timing["launch_s"] += time.perf_counter() - t0
+            sch.on_prefill_done(plan.prefill, {})
+            n = self._flush_inflight()
+            self.inflight = h
+            ntok = sum(k for _, k in plan.prefill)
+            self.counters["prefill_tokens"] += ntok
+            self.counters["steps_prefill"] += 1
+            M.PREFILL_TOKENS.inc(ntok)
+            self.step_count += 1
+            return n
+        if h0 is not None and h0.kind == "prefill" and plan.kind != "prefill":
+            n0 = self._flush_inflight()
+            if plan.kind == "decode":
+                plan.decode = [sq for sq in plan.decode if not sq.is_finished]
+                if not plan.decode:
+                    return n0
+        else:
+            n0 = 0
         if plan.kind == "decode" and self.runner.can_pipeline(plan.decode):
             t0 = time.perf_counter()
+            self.timing["schedule_s"] += t0 - ts
+            if h0 is not None and h0.event.query():
+                self.timing["gpu_starved_launches"] += 1  # GPU drained before this launch
+            if self.step_trace is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             h = self.runner.launch_decode(plan.decode)
+            if self.step_trace is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                self.gpu_trace.append((e0, e1))
+            t1 = time.perf_counter()
+            self.timing["launch_s"] += t1 - t0
+            if self.step_trace is not None:
+                self.step_trace.append(("launch", "decode", t0, t1))
             for sq in plan.decode:
                 sq.num_cached = sq.length  # the fed token's KV is written by this step
                 sq.output.append(PLACEHOLDER)
@@ -248,8 +305,8 @@ class LLMEngine:
             M.BATCH_SIZE.observe(len(plan.decode))
             M.STEP_SECONDS.labels("decode").observe(time.perf_counter() - t0)
             self.step_count += 1
-            return n
-        n = self._flush_inflight()
+            return n0 + n
+        n = n0 + self._flush_inflight()
         if plan.kind == "idle":
             return n
         if plan.kind == "decode":
@@ -396,6 +453,16 @@ class AsyncLLMEngine:
         # wake-up after every GPU wait by up to 5 ms (a GPU bubble per decode step);
         # hand the GIL over faster.
         sys.setswitchinterval(float(os.environ.get("OMNIA_GIL_SWITCH_INTERVAL", "0.0005")))
+        # a cyclic-GC pass holds the GIL for its whole duration (tens of ms on a
+        # serving heap full of coroutines and protobuf frames): the engine thread
+        # stalls and the GPU drains.  Fewer, larger young-generation passes.
+        gct = os.environ.get("OMNIA_GC_THRESHOLD", "")
+        if gct:
+            import gc
+
+            gc.set_threshold(*[int(x) for x in gct.split(",")])
+            if os.environ.get("OMNIA_GC_FREEZE"):
+                gc.freeze()
         self.engine = engine
         self._inbox: list = []
         self._lock = threading.Lock()

@@ -27,6 +27,7 @@ class _Staging:
 
     def __init__(self, spec: dict, device, pin: bool, dev=None):
         self.event = None
+        self.nev = None
         self.off = {}
         o = 0
         for name, (dtype, n) in spec.items():
@@ -44,13 +45,42 @@ class _Staging:
             self.h[name] = self.host[o:o + n * es].view(dtype)
             self.d[name] = self.dev[o:o + n * es].view(dtype)
         self.np = {k: v.numpy() for k, v in self.h.items()}
+        nrows = spec["ids"][1]
+        self.row_seq: list = [None] * nrows  # sequence whose data each row holds
+        self.row_nb = [0] * nrows  # block-table entries already written for it
+
+    def native_event(self):
+        if self.nev is None:
+            self.nev = _NativeEvent(ops.kernels())
+        return self.nev
 
     def upload(self, nbytes: int | None = None):
         n = self.nbytes if nbytes is None else nbytes
         self.dev[:n].copy_(self.host[:n], non_blocking=True)
 
 
+class _NativeEvent:
+    """Reusable hipEvent (timing disabled) driven through the kernel extension;
+    ``synchronize`` only drops the GIL when the event has not completed yet."""
+
+    __slots__ = ("k", "h")
+
+    def __init__(self, k):
+        self.k = k
+        self.h = k.event_create()
+
+    def synchronize(self) -> int:
+        """Wait; returns ns spent re-taking the GIL after the event fired."""
+        return self.k.event_sync(self.h)
+
+    def query(self) -> bool:
+        return self.k.event_query(self.h)
+
+
 class ModelRunner:
+    # single-call native step launch; TP rank 0 broadcasts the uploaded staging
+    # buffer between the H2D copy and the replay, so it keeps the split path
+    fused_launch = True
     def __init__(self, model, kv: KVCache, max_batch: int = 256, max_model_len: int = 8192,
                  use_graphs: bool = True, max_prefill_tokens: int = 16384):
         self.model = model
@@ -82,10 +112,16 @@ class ModelRunner:
         self.logits_idx = torch.arange(B, dtype=torch.int64, device=self.device)
         self.out_tok = torch.zeros(B, dtype=torch.int32, device=self.device)
         self.out_hosts = [torch.zeros(B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        # prefill steps are pipelined too: two pinned token buffers + their events
+        self.pf_hosts = [torch.zeros(B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.pf_events = [None, None]
+        self.pf_flip = 0
         self.graphs: dict = {}
+        self.graph_exec: dict = {}  # (rows, cols) -> raw hipGraphExec_t for the fused launch
         self.graph_pool = None
         self.stats = {"graph_replays": 0, "eager_decodes": 0, "prefill_steps": 0,
-                      "captures": 0, "capture_s": 0.0}
+                      "captures": 0, "capture_s": 0.0,
+                      "gil_wait_s": 0.0}
 
     # ------------------------------------------------------------------ utils
     def _ctx_bucket(self, max_len: int) -> int:
@@ -95,21 +131,6 @@ class ModelRunner:
         while c < nb:
             c *= 2
         return min(c, self.max_blocks)
-
-    def _fill_sampling(self, st: _Staging, seqs: list[Sequence], n: int):
-        temp, topk, topp = st.np["temp"], st.np["top_k"], st.np["top_p"]
-        seeds, steps = st.np["seeds"], st.np["steps"]
-        for i, s in enumerate(seqs):
-            p = s.params
-            temp[i] = p.temperature
-            topk[i] = p.top_k
-            topp[i] = p.top_p
-            seeds[i] = p.seed if p.seed is not None else (s.seq_id * 7919 + 17)
-            steps[i] = len(s.output)
-        for i in range(len(seqs), n):
-            temp[i] = 0.0
-            topk[i] = 0
-            topp[i] = 1.0
 
     def _penalty_counts(self, seqs: list[Sequence], rows: int):
         if not any(s.params.needs_penalties for s in seqs):
@@ -137,6 +158,9 @@ class ModelRunner:
         """chunks: (seq, n_new) -- prefill n_new uncached tokens of each seq.
 
         Returns {seq_id: sampled token} for sequences whose prompt completed."""
+        if self.can_pipeline_prefill(chunks):
+            h = self.launch_prefill(chunks)
+            return {s.seq_id: t for s, t in zip(h.seqs, self.collect(h))}
         t, meta, sample_seqs = self._prefill_pack(chunks)
         logits = self._prefill_forward(t, meta)
         self.stats["prefill_steps"] += 1
@@ -145,43 +169,91 @@ class ModelRunner:
         toks = self._sample_eager(logits[: len(sample_seqs)], sample_seqs)
         return {s.seq_id: t for s, t in zip(sample_seqs, toks)}
 
-    def _prefill_pack(self, chunks):
+    def can_pipeline_prefill(self, chunks) -> bool:
+        return self.is_gpu and not any(s.params.needs_penalties for s, _ in chunks)
+
+    def launch_prefill(self, chunks: list[tuple[Sequence, int]]) -> "DecodeHandle":
+        """Enqueue one prefill step + on-device sampling of the completed prompts and
+        the D2H copy of their tokens; returns without waiting.  The sampling
+        parameters travel in the same packed upload as the batch metadata, so the
+        step issues no synchronous copies and the host can assemble step N+1 while
+        the GPU runs step N."""
+        t, meta, sample_seqs = self._prefill_pack(chunks, sampling=True)
+        logits = self._prefill_forward(t, meta)
+        self.stats["prefill_steps"] += 1
+        n = len(sample_seqs)
+        slot = self.pf_flip
+        self.pf_flip ^= 1
+        out_host = self.pf_hosts[slot]
+        ev = self.pf_events[slot]
+        if ev is not None:
+            ev.synchronize()  # the pinned token buffer of step N-2 has been read
+        if n:
+            o = meta[5]
+            temp = t[o:o + n].view(torch.float64).float()
+            top_k = t[o + n:o + 2 * n].int()
+            top_p = t[o + 2 * n:o + 3 * n].view(torch.float64).float()
+            seeds, steps = t[o + 3 * n:o + 4 * n], t[o + 4 * n:o + 5 * n]
+            tok = ops.sample(logits[:n], temp, top_k, top_p, seeds=seeds, steps=steps)
+            out_host[:n].copy_(tok, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pf_events[slot] = ev
+        return DecodeHandle(sample_seqs, out_host, ev, n, "prefill")
+
+    def _prefill_pack(self, chunks, sampling: bool = False):
         """Host-side batch assembly -> (packed int64 device tensor, meta, sampled seqs).
-        meta = (T, B, maxb, n_tiles, n_sample)."""
-        ids, pos, slots, qsl, seq_lens, sample_rows, sample_seqs = [], [], [], [0], [], [], []
+        meta = (T, B, maxb, n_tiles, n_sample[, sampling-params offset])."""
         bs = self.bs
-        maxb = 1
-        for s, n in chunks:
-            toks = s.all_tokens
-            start = s.num_cached
-            ids.extend(toks[start:start + n])
-            pos.extend(range(start, start + n))
-            blk = s.blocks
-            slots.extend(blk[p // bs] * bs + p % bs for p in range(start, start + n))
-            qsl.append(qsl[-1] + n)
-            seq_lens.append(start + n)
-            maxb = max(maxb, len(blk))
-            if start + n == s.length:
-                sample_rows.append(qsl[-1] - 1)
-                sample_seqs.append(s)
         B = len(chunks)
-        bt = np.zeros((B, maxb), dtype=np.int32)
-        for i, (s, _) in enumerate(chunks):
+        lens = np.fromiter((n for _, n in chunks), np.int64, B)
+        qsl = np.zeros(B + 1, np.int64)
+        np.cumsum(lens, out=qsl[1:])
+        T = int(qsl[-1])
+        maxb = max(1, max(len(s.blocks) for s, _ in chunks))
+        ids = np.empty(T, np.int64)
+        pos = np.empty(T, np.int64)
+        bt = np.zeros((B, maxb), dtype=np.int64)
+        seq_lens = np.empty(B, np.int64)
+        sample_rows, sample_seqs = [], []
+        for i, (s, n) in enumerate(chunks):
+            start = s.num_cached
+            q0 = int(qsl[i])
+            plen = len(s.prompt)
+            if start + n <= plen:
+                ids[q0:q0 + n] = s.prompt[start:start + n]
+            else:
+                ids[q0:q0 + n] = s.all_tokens[start:start + n]
+            pos[q0:q0 + n] = np.arange(start, start + n)
             bt[i, :len(s.blocks)] = s.blocks
-        tseq, tq0 = ops.prefill_tiles([qsl[i + 1] - qsl[i] for i in range(B)])
-        # one pinned packed upload
-        arr = np.concatenate([
-            np.asarray(ids, np.int64), np.asarray(pos, np.int64), np.asarray(slots, np.int64),
-            np.asarray(qsl, np.int64), np.asarray(seq_lens, np.int64), np.asarray(tseq, np.int64),
-            np.asarray(tq0, np.int64), np.asarray(sample_rows or [0], np.int64),
-            bt.reshape(-1).astype(np.int64)])
-        t = torch.from_numpy(arr)
+            seq_lens[i] = start + n
+            if start + n == s.length:
+                sample_rows.append(q0 + n - 1)
+                sample_seqs.append(s)
+        # slot of token p of row i = block_table[i][p // bs] * bs + p % bs
+        row = np.repeat(np.arange(B), lens)
+        slots = bt[row, pos // bs] * bs + pos % bs
+        tseq, tq0 = ops.prefill_tiles(lens.tolist())
+        parts = [ids, pos, slots, qsl, seq_lens, np.asarray(tseq, np.int64),
+                 np.asarray(tq0, np.int64), np.asarray(sample_rows or [0], np.int64),
+                 bt.reshape(-1)]
+        meta = (T, B, maxb, len(tseq), len(sample_rows))
+        if sampling and sample_seqs:
+            meta = meta + (sum(len(x) for x in parts),)
+            ps = [x.params for x in sample_seqs]
+            parts += [np.array([p.temperature for p in ps], np.float64).view(np.int64),
+                      np.array([p.top_k for p in ps], np.int64),
+                      np.array([p.top_p for p in ps], np.float64).view(np.int64),
+                      np.array([p.seed if p.seed is not None else x.seq_id * 7919 + 17
+                                for p, x in zip(ps, sample_seqs)], np.int64),
+                      np.array([len(x.output) for x in sample_seqs], np.int64)]
+        t = torch.from_numpy(np.concatenate(parts))
         if self.is_gpu:
             t = t.pin_memory().to(self.device, non_blocking=True)
-        return t, (len(ids), B, maxb, len(tseq), len(sample_rows)), sample_seqs
+        return t, meta, sample_seqs
 
     def _prefill_forward(self, t: torch.Tensor, meta) -> torch.Tensor:
-        T, B, maxb, n_tiles, n_sample = meta
+        T, B, maxb, n_tiles, n_sample = meta[:5]
         o = 0
 
         def take(n, dtype):
@@ -220,11 +292,19 @@ class ModelRunner:
         return tok.cpu().tolist()
 
     # ------------------------------------------------------------------ decode
-    def _decode_inputs(self, seqs: list[Sequence], nrows: int, ncols: int, st: "_Staging"):
+    def _decode_inputs(self, seqs: list[Sequence], nrows: int, ncols: int, st: "_Staging",
+                       upload: bool = True):
+        """Fill a host staging buffer for one decode step.  Each buffer remembers
+        which sequence occupied each row and how many block-table entries it
+        already holds, so steady-state steps only write what changed (positions,
+        slots, steps and newly allocated pages)."""
         n = len(seqs)
-        ids, pos, slots, lens = st.np["ids"], st.np["pos"], st.np["slots"], st.np["seq_lens"]
-        src = st.np["src"]
-        bt = st.np["bt"].reshape(self.max_batch, self.max_blocks)
+        npv = st.np
+        ids, pos, slots, lens, src = npv["ids"], npv["pos"], npv["slots"], npv["seq_lens"], \
+            npv["src"]
+        steps = npv["steps"]
+        bt = npv["bt"].reshape(self.max_batch, self.max_blocks)
+        row_seq, row_nb = st.row_seq, st.row_nb
         bs = self.bs
         for i, s in enumerate(seqs):
             p = s.length - 1
@@ -237,20 +317,49 @@ class ModelRunner:
                 src[i] = -1
                 ids[i] = last
             pos[i] = p
-            slots[i] = s.blocks[p // bs] * bs + p % bs
+            blocks = s.blocks
+            slots[i] = blocks[p // bs] * bs + p % bs
             lens[i] = p + 1
-            nb = len(s.blocks)
-            bt[i, :nb] = s.blocks
+            nb = len(blocks)
+            had = row_nb[i]
+            # same sequence in the same row with an unchanged block prefix (pages
+            # are only ever appended while a sequence runs; preemption / swap
+            # re-allocate them, which the endpoint check catches)
+            if row_seq[i] is s and 0 < had <= nb and bt[i, 0] == blocks[0] and \
+                    bt[i, had - 1] == blocks[had - 1]:
+                if nb > had:
+                    bt[i, had:nb] = blocks[had:nb]
+                    row_nb[i] = nb
+            else:
+                bt[i, :nb] = blocks
+                row_seq[i] = s
+                row_nb[i] = nb
+                self._fill_row_sampling(npv, i, s)
+            steps[i] = len(s.output)
         for i in range(n, nrows):  # padded rows -> null page, no KV write
-            ids[i] = 0
-            src[i] = -1
-            pos[i] = 0
-            slots[i] = -1
-            lens[i] = 1
-            bt[i, 0] = 0
-        self._fill_sampling(st, seqs, nrows)
+            if row_seq[i] is not _PAD:
+                ids[i] = 0
+                src[i] = -1
+                pos[i] = 0
+                slots[i] = -1
+                lens[i] = 1
+                bt[i, 0] = 0
+                npv["temp"][i] = 0.0
+                npv["top_k"][i] = 0
+                npv["top_p"][i] = 1.0
+                row_seq[i] = _PAD
+                row_nb[i] = 0
         # upload into the (single) device twin the graphs read from
-        self.dec.dev.copy_(st.host, non_blocking=True)
+        if upload:
+            self.dec.dev.copy_(st.host, non_blocking=True)
+
+    @staticmethod
+    def _fill_row_sampling(npv, i: int, s: Sequence):
+        p = s.params
+        npv["temp"][i] = p.temperature
+        npv["top_k"][i] = p.top_k
+        npv["top_p"][i] = p.top_p
+        npv["seeds"][i] = p.seed if p.seed is not None else (s.seq_id * 7919 + 17)
 
     def _decode_fb(self, nrows: int, ncols: int, ids=None) -> ForwardBatch:
         d = self.dec.d
@@ -291,6 +400,8 @@ class ModelRunner:
         torch.cuda.synchronize()
         self.out_tok.copy_(saved)
         self.graphs[(nrows, ncols)] = g
+        if self.fused_launch:
+            self.graph_exec[(nrows, ncols)] = int(g.raw_cuda_graph_exec())
         self.stats["captures"] += 1
         self.stats["capture_s"] += time.perf_counter() - t0
         return g
@@ -311,12 +422,23 @@ class ModelRunner:
         self.flip ^= 1
         if st.event is not None:
             st.event.synchronize()  # host staging buffer free again
-        self._decode_inputs(seqs, nrows, ncols, st)
-        self._before_replay(nrows, ncols)
-        self._replay(nrows, ncols)
-        out_host[:n].copy_(self.out_tok[:n], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        gx = self.graph_exec.get((nrows, ncols)) if self.fused_launch else None
+        if gx is not None:
+            # H2D + graph launch + D2H + event record in ONE native call: the GIL is
+            # held throughout instead of being dropped/re-taken around each enqueue
+            self._decode_inputs(seqs, nrows, ncols, st, upload=False)
+            ev = st.native_event()
+            ops.kernels().graph_launch_step(
+                gx, self.dec.dev.data_ptr(), st.host.data_ptr(), st.nbytes,
+                out_host.data_ptr(), self.out_tok.data_ptr(), 4 * n, ev.h)
+            self.stats["graph_replays"] += 1
+        else:
+            self._decode_inputs(seqs, nrows, ncols, st)
+            self._before_replay(nrows, ncols)
+            self._replay(nrows, ncols)
+            out_host[:n].copy_(self.out_tok[:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
         st.event = ev
         for i, s in enumerate(seqs):
             s.slot = i
@@ -330,9 +452,10 @@ class ModelRunner:
         g.replay()
         self.stats["graph_replays"] += 1
 
-    @staticmethod
-    def collect(h: "DecodeHandle") -> list[int]:
-        h.event.synchronize()
+    def collect(self, h: "DecodeHandle") -> list[int]:
+        gil_ns = h.event.synchronize()
+        if gil_ns:
+            self.stats["gil_wait_s"] += gil_ns * 1e-9
         return h.out_host[: h.n].tolist()
 
     def run_decode(self, seqs: list[Sequence]) -> list[int]:
@@ -357,12 +480,14 @@ class ModelRunner:
 
 
 PLACEHOLDER = -1
+_PAD = object()  # row_seq marker of a padded (null) row
 
 
 class DecodeHandle:
-    __slots__ = ("seqs", "out_host", "event", "n")
+    __slots__ = ("seqs", "out_host", "event", "n", "kind")
 
-    def __init__(self, seqs, out_host, event, n):
+    def __init__(self, seqs, out_host, event, n, kind="decode"):
+        self.kind = kind
         self.seqs = seqs
         self.out_host = out_host
         self.event = event

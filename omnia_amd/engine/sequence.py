@@ -49,13 +49,16 @@ class Sequence:
     slot: int = -1  # row in the last launched decode step
     n_real: int = 0  # output tokens whose value is known on the host
 
+    def __post_init__(self):
+        self._plen = len(self.prompt)
+
     @property
     def all_tokens(self) -> list[int]:
         return self.prompt + self.output
 
     @property
     def length(self) -> int:
-        return len(self.prompt) + len(self.output)
+        return self._plen + len(self.output)
 
     @property
     def num_uncached(self) -> int:

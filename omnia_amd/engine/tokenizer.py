@@ -113,6 +113,14 @@ class HFTokenizer:
         return self.tk.decode(list(ids), skip_special_tokens=skip_special)
 
 
+def _token_bytes_cached(tok, tid: int) -> bytes:
+    cache = tok.__dict__.setdefault("_tb_cache", {})
+    b = cache.get(tid)
+    if b is None:
+        b = cache[tid] = tok.token_bytes(tid)
+    return b
+
+
 class Detokenizer:
     """Incremental UTF-8-safe streaming detokeniser for one sequence."""
 
@@ -121,7 +129,14 @@ class Detokenizer:
         self.pending = bytearray()
 
     def push(self, tid: int) -> str:
-        self.pending.extend(self.tok.token_bytes(tid))
+        b = _token_bytes_cached(self.tok, tid)
+        if not self.pending:
+            # fast path: a token that is complete UTF-8 on its own (the common case)
+            try:
+                return b.decode("utf-8")
+            except UnicodeDecodeError:
+                pass
+        self.pending.extend(b)
         # emit the longest valid UTF-8 prefix
         for cut in range(len(self.pending), max(-1, len(self.pending) - 4), -1):
             try:

@@ -70,12 +70,14 @@ class TPChannel:
 class TPModelRunner(ModelRunner):
     """Rank-0 runner: broadcasts every step to the TP workers."""
 
+    fused_launch = False
+
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
         self.chan = TPChannel(self.device)
 
     def _prefill_forward(self, t, meta):
-        self.chan.send(PREFILL, *meta, t.numel(), payload=t)
+        self.chan.send(PREFILL, *meta[:5], t.numel(), payload=t)
         return super()._prefill_forward(t, meta)
 
     def _before_replay(self, nrows, ncols):

@@ -2,6 +2,7 @@
 // operand shapes/dtypes on the host BEFORE launching (a bad launch on the box
 // can take every GPU of the host down), then launches on the current HIP
 // stream so the calls are capturable into hipGraphs by the engine.
+#include <chrono>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
@@ -324,6 +325,59 @@ void moe_combine(at::Tensor out, at::Tensor Y, at::Tensor ids, int64_t topk, int
                              e_lo, e_hi, cur_stream()), "moe_combine");
 }
 
+// ------------------------------------------------- host step launch (no GIL churn)
+// One decode step = H2D staging copy + graph launch + D2H token copy + event
+// record, enqueued back to back on the current stream inside ONE Python call.
+// Each separate torch call would drop and re-take the GIL; with a busy asyncio
+// serving thread every re-take can wait a full switch interval, starving the
+// engine thread and idling the GPU between steps.
+void graph_launch_step(int64_t graph_exec, int64_t h2d_dst, int64_t h2d_src, int64_t h2d_bytes,
+                       int64_t d2h_dst, int64_t d2h_src, int64_t d2h_bytes, int64_t event) {
+  hipStream_t s = cur_stream();
+  if (h2d_bytes > 0)
+    TORCH_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(h2d_dst),
+                               reinterpret_cast<const void*>(h2d_src), h2d_bytes,
+                               hipMemcpyHostToDevice, s) == hipSuccess, "H2D staging copy");
+  TORCH_CHECK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(graph_exec), s) == hipSuccess,
+              "hipGraphLaunch");
+  if (d2h_bytes > 0)
+    TORCH_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(d2h_dst),
+                               reinterpret_cast<const void*>(d2h_src), d2h_bytes,
+                               hipMemcpyDeviceToHost, s) == hipSuccess, "D2H token copy");
+  if (event)
+    TORCH_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(event), s) == hipSuccess,
+                "hipEventRecord");
+}
+
+int64_t event_create() {
+  hipEvent_t e;
+  TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess,
+              "hipEventCreate");
+  return reinterpret_cast<int64_t>(e);
+}
+
+void event_destroy(int64_t e) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e)); }
+
+bool event_query(int64_t e) {
+  return hipEventQuery(reinterpret_cast<hipEvent_t>(e)) == hipSuccess;
+}
+
+// wait for an event; the GIL is released only if it has not completed yet.
+// Returns the nanoseconds spent re-acquiring the GIL after the event fired
+// (the serving thread's hold time -- a direct measure of GIL contention).
+int64_t event_sync(int64_t e) {
+  auto ev = reinterpret_cast<hipEvent_t>(e);
+  if (hipEventQuery(ev) == hipSuccess) return 0;
+  std::chrono::steady_clock::time_point done;
+  {
+    py::gil_scoped_release rel;
+    TORCH_CHECK(hipEventSynchronize(ev) == hipSuccess, "hipEventSynchronize");
+    done = std::chrono::steady_clock::now();
+  }
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now() - done).count();
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_omnia_kernels, m) {
@@ -344,5 +398,10 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("moe_align", &moe_align);
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
+  m.def("graph_launch_step", &graph_launch_step);
+  m.def("event_create", &event_create);
+  m.def("event_destroy", &event_destroy);
+  m.def("event_query", &event_query);
+  m.def("event_sync", &event_sync);
   m.attr("arch") = "gfx950";
 }

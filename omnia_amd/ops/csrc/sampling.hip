@@ -182,7 +182,9 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
   // ---- Gumbel-max draw among survivors
   const uint64_t seed = seeds ? seeds[row] : 0x5eedull;
   const uint64_t step = steps ? (uint64_t)steps[row] : 0ull;
-  const uint64_t rs = mix64(seed ^ (step * 0x9e3779b97f4a7c15ull) ^ ((uint64_t)row << 48));
+  // (seed, step) only -- never the batch row -- so a seeded request draws the
+  // same tokens whatever batch it lands in (pipelined vs synchronous, ragged finishes)
+  const uint64_t rs = mix64(seed ^ (step * 0x9e3779b97f4a7c15ull));
   float gbest = -INFINITY, xsel = -INFINITY;
   int gi = argm;
   for (int i = tid; i < vocab; i += kThreads) {

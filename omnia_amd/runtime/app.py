@@ -42,9 +42,32 @@ def shared_engine(engine_cfg: dict | None = None):
                 t = EngineConfig.__dataclass_fields__[k].type
                 kw[k] = (int(v) if "int" in str(t) else float(v) if "float" in str(t)
                          else (str(v).lower() == "true") if "bool" in str(t) else v)
-        eng = AsyncLLMEngine.from_config(EngineConfig.from_env(**kw))
+        cfg = EngineConfig.from_env(**kw)
+        eng = None
+        if _use_engine_process(cfg):
+            from ..engine.core_proc import EngineCoreClient
+
+            eng = EngineCoreClient(cfg)
+        if eng is None:
+            eng = AsyncLLMEngine.from_config(cfg)
         _ENGINES[key] = eng
     return eng
+
+
+def _use_engine_process(cfg) -> bool:
+    """Run the engine in its own engine-core process (``engine/core_proc.py``) so the
+    serving loop and the engine loop do not share a GIL.  ``OMNIA_ENGINE_PROC``:
+    ``1`` / ``0`` / ``auto`` (default: GPU, TP=1, and this process has not
+    initialised the GPU yet -- the core must be a fresh child)."""
+    import torch
+
+    mode = os.environ.get("OMNIA_ENGINE_PROC", "auto").lower()
+    if mode in ("0", "false", "no"):
+        return False
+    if mode in ("1", "true", "yes"):
+        return True
+    return (cfg.device == "cuda" and cfg.tp == 1 and torch.cuda.device_count() > 0
+            and not torch.cuda.is_initialized())
 
 
 def response_format_instruction(fmt: str, schema: dict | None) -> str:

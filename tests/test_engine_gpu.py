@@ -32,6 +32,27 @@ def test_pipelined_equals_synchronous_greedy():
     assert [len(x) for x in a] == max_toks
 
 
+def test_pipelined_chunked_prefill_equals_synchronous_sampled():
+    """Many small pipelined prefill steps (chunked prompts finishing in different
+    steps) + seeded sampling: identical to the synchronous engine and to eager."""
+    prompts = [list(range(5 + i, 5 + i + 30 + 23 * i)) for i in range(8)]
+
+    def run(temp=0.8, **kw):
+        e = eng(max_prefill_tokens=64, **kw)
+        seqs = [e.add_request(p, SamplingParams(temperature=temp, top_k=20, seed=100 + i,
+                                                max_tokens=6 + i, ignore_eos=True),
+                              session_id=f"c{i}") for i, p in enumerate(prompts)]
+        e.run_until_done()
+        return [s.output for s in seqs], e.runner.stats["prefill_steps"]
+
+    a, na = run(pipeline=True)
+    b, nb = run(pipeline=False)
+    assert a == b
+    assert na == nb and na > 5
+    g = [run(0.0, **kw)[0] for kw in (dict(pipeline=True), dict(use_graphs=False))]
+    assert g[0] == g[1]
+
+
 def test_decode_matches_fresh_prefill_on_gpu():
     e = eng()
     s = e.generate([list(range(3, 200))], SamplingParams(temperature=0, max_tokens=20,

@@ -133,6 +133,7 @@ class LLMEngine:
         self.eos = set(self.tokenizer.eos_token_ids)
         self.seqs: dict[int, Sequence] = {}
         self.detok: dict[int, Detokenizer] = {}
+        self._guided = None  # K13 grammar registry, built on the first guided request
         self.step_count = 0
         self.inflight = None
         self.counters = {"prefill_tokens": 0, "decode_tokens": 0, "steps_prefill": 0,
@@ -190,6 +191,12 @@ class LLMEngine:
         s = Sequence(prompt=list(prompt), params=params, session_id=session_id,
                      request_id=request_id or uuid.uuid4().hex, on_token=on_token,
                      on_finish=on_finish)
+        if params.guided:
+            if self._guided is None:
+                from .guided import GuidedRegistry
+
+                self._guided = GuidedRegistry(self.tokenizer)
+            s.guide = self._guided.matcher(params)  # raises SchemaError on bad schemas
         self.scheduler.add(s)
         self.seqs[s.seq_id] = s
         self.detok[s.seq_id] = Detokenizer(self.tokenizer)
@@ -360,14 +367,21 @@ class LLMEngine:
         nout = s.n_real
         p = s.params
         reason = None
-        if not p.ignore_eos and tok in self.eos and nout > p.min_tokens:
-            reason = FinishReason.STOP
-        elif tok in p.stop_token_ids:
-            reason = FinishReason.STOP
-        elif nout >= p.max_tokens:
-            reason = FinishReason.LENGTH
-        elif len(s.prompt) + nout >= self.cfg.max_model_len:
-            reason = FinishReason.LENGTH
+        if s.guide is not None:
+            ok = s.guide.accept(tok)
+            if not ok:
+                log.warning("seq %d: token %d rejected by its grammar", s.seq_id, tok)
+            if not ok or s.guide.m.finished:
+                reason = FinishReason.STOP  # the document is complete (EOS taken)
+        if reason is None:
+            if not p.ignore_eos and tok in self.eos and nout > p.min_tokens:
+                reason = FinishReason.STOP
+            elif tok in p.stop_token_ids:
+                reason = FinishReason.STOP
+            elif nout >= p.max_tokens:
+                reason = FinishReason.LENGTH
+            elif len(s.prompt) + nout >= self.cfg.max_model_len:
+                reason = FinishReason.LENGTH
         text = ""
         if s.on_token is not None or p.stop:
             if not (reason == FinishReason.STOP and tok in self.eos):

@@ -170,7 +170,8 @@ class ModelRunner:
         return {s.seq_id: t for s, t in zip(sample_seqs, toks)}
 
     def can_pipeline_prefill(self, chunks) -> bool:
-        return self.is_gpu and not any(s.params.needs_penalties for s, _ in chunks)
+        return self.is_gpu and not any(s.params.needs_penalties or s.guide is not None
+                                       for s, _ in chunks)
 
     def launch_prefill(self, chunks: list[tuple[Sequence, int]]) -> "DecodeHandle":
         """Enqueue one prefill step + on-device sampling of the completed prompts and
@@ -288,6 +289,17 @@ class ModelRunner:
         if pc is not None:
             kw = dict(counts=pc[0], freq_pen=pc[1]["freq"], pres_pen=pc[1]["pres"],
                       rep_pen=pc[1]["rep"])
+        if any(s.guide is not None for s in seqs):
+            from .guided import masks_for
+
+            words = (logits.shape[1] + 31) // 32
+            m = torch.from_numpy(masks_for([s.guide for s in seqs], words))
+            if self.is_gpu:
+                m = m.pin_memory().to(dev, non_blocking=True)
+            logits = logits[:n]
+            if not logits.is_contiguous() and logits.stride(1) != 1:
+                logits = logits.contiguous()
+            ops.apply_token_mask(logits, m)
         tok = ops.sample(logits, temp, top_k, top_p, seeds=seeds, steps=steps, **kw)
         return tok.cpu().tolist()
 
@@ -407,7 +419,9 @@ class ModelRunner:
         return g
 
     def can_pipeline(self, seqs: list[Sequence]) -> bool:
-        return self.use_graphs and not any(s.params.needs_penalties for s in seqs)
+        # penalties need host token counts, grammars the previous token: synchronous
+        return self.use_graphs and not any(s.params.needs_penalties or s.guide is not None
+                                           for s in seqs)
 
     def launch_decode(self, seqs: list[Sequence]) -> "DecodeHandle":
         """Enqueue one decode step (graph replay) without waiting for it."""

@@ -22,10 +22,17 @@ class SamplingParams:
     stop_token_ids: list[int] = field(default_factory=list)
     ignore_eos: bool = False
     logprobs: bool = False
+    # K13 guided decoding: JSON-schema-constrained output / any JSON object
+    json_schema: dict | None = None
+    json_object: bool = False
 
     @property
     def greedy(self) -> bool:
         return self.temperature <= 0.0
+
+    @property
+    def guided(self) -> bool:
+        return self.json_schema is not None or self.json_object
 
     @property
     def needs_penalties(self) -> bool:
@@ -56,10 +63,18 @@ class SamplingParams:
             "frequency_penalty": "frequency_penalty", "presence_penalty": "presence_penalty",
             "repetition_penalty": "repetition_penalty", "seed": "seed", "stop": "stop",
             "ignore_eos": "ignore_eos", "min_tokens": "min_tokens", "logprobs": "logprobs",
+            "json_schema": "json_schema", "json_object": "json_object",
         }
         for k, v in d.items():
             if k in mapping and v is not None:
                 kw[mapping[k]] = v
+        rf = d.get("response_format")
+        if isinstance(rf, dict):  # OpenAI-style response_format
+            if rf.get("type") == "json_object":
+                kw["json_object"] = True
+            elif rf.get("type") == "json_schema":
+                js = rf.get("json_schema") or {}
+                kw["json_schema"] = js.get("schema", js) if isinstance(js, dict) else None
         if isinstance(kw.get("stop"), str):
             kw["stop"] = [kw["stop"]]
         for f in ("temperature", "top_p", "frequency_penalty", "presence_penalty",

@@ -48,6 +48,7 @@ class Sequence:
     text_tail: str = ""  # recent decoded text for stop-string matching
     slot: int = -1  # row in the last launched decode step
     n_real: int = 0  # output tokens whose value is known on the host
+    guide: object = None  # K13 grammar matcher (engine/guided.py) for constrained output
 
     def __post_init__(self):
         self._plen = len(self.prompt)

@@ -202,6 +202,15 @@ def sample(logits, temperature, top_k=None, top_p=None, seeds=None, steps=None, 
     return r
 
 
+def apply_token_mask(logits: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """K13: in place, logits[r, v] = -inf where bit v of int32 ``mask[r]`` is clear."""
+    if logits.is_cuda:
+        kernels().apply_token_mask(logits, mask.to(device=logits.device, dtype=torch.int32)
+                                   .contiguous())
+        return logits
+    return ref.apply_token_mask(logits, mask)
+
+
 # ------------------------------------------------------------- memory tier (K17 / K18)
 def mean_pool_l2(hidden: torch.Tensor, cu_seqlens: torch.Tensor) -> torch.Tensor:
     """[T, D] bf16 hidden states + [B+1] int32 offsets -> [B, D] fp32 unit vectors."""

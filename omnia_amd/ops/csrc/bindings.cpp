@@ -27,6 +27,8 @@ int omnia_prefill_attention(void* out, const void* q, const void* k_cache, const
                             const int* seq_lens, const int* tile_seq, const int* tile_q0,
                             int n_tiles, int hq, int hkv, int head_dim, int block_size,
                             int64_t q_stride, int64_t out_stride, float scale, hipStream_t s);
+int omnia_apply_token_mask(void* logits, int logits_is_bf16, int rows, int64_t row_stride,
+                           int vocab, const uint32_t* mask, int words, hipStream_t s);
 int omnia_sample(int* out_tok, float* out_logprob, const void* logits, int logits_is_bf16,
                  int rows, int64_t row_stride, int vocab, const float* temperature,
                  const int* top_k, const float* top_p, const uint64_t* seeds,
@@ -202,6 +204,21 @@ void sample(at::Tensor out_tok, c10::optional<at::Tensor> out_logprob, at::Tenso
                         opt_ptr<uint64_t>(seeds), opt_ptr<int64_t>(steps), opt_ptr<int>(counts),
                         opt_ptr<float>(freq_pen), opt_ptr<float>(pres_pen),
                         opt_ptr<float>(rep_pen), cur_stream()), "sample");
+}
+
+// K13: grammar mask -> -inf logits (mask int32 [rows, ceil(V/32)], bit v = allowed)
+void apply_token_mask(at::Tensor logits, at::Tensor mask) {
+  CHECK_GPU(logits); CHECK_GPU(mask); CHECK_I32(mask);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V]");
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat,
+              "logits bf16/f32");
+  const int rows = logits.size(0), vocab = logits.size(1), words = (vocab + 31) / 32;
+  TORCH_CHECK(mask.dim() == 2 && mask.size(0) == rows && mask.size(1) == words &&
+              mask.is_contiguous(), "mask int32 [B, ceil(V/32)] contiguous");
+  CHECK_RC(omnia_apply_token_mask(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, rows,
+                                  logits.stride(0), vocab,
+                                  reinterpret_cast<const uint32_t*>(mask.data_ptr<int>()), words,
+                                  cur_stream()), "apply_token_mask");
 }
 
 // K17: out[b] = normalize(mean(hidden[cu[b]:cu[b+1]]))   fp32
@@ -398,6 +415,7 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("moe_align", &moe_align);
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
+  m.def("apply_token_mask", &apply_token_mask);
   m.def("graph_launch_step", &graph_launch_step);
   m.def("event_create", &event_create);
   m.def("event_destroy", &event_destroy);

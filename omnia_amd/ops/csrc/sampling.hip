@@ -239,3 +239,41 @@ extern "C" int omnia_sample(int* out_tok, float* out_logprob, const void* logits
                                                    rep_pen);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- K13 token mask
+// logits[row, v] = -inf where bit v of mask[row] is clear (grammar-constrained rows;
+// unconstrained rows carry all-ones masks).  One thread per (row, 32-token word):
+// a 64-wide wave covers 2048 vocabulary entries with one mask load per lane.
+namespace {
+template <typename T>
+__global__ void __launch_bounds__(256)
+apply_token_mask_kernel(T* __restrict__ logits, int64_t row_stride, int vocab,
+                        const uint32_t* __restrict__ mask, int words) {
+  const int row = blockIdx.y;
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= words) return;
+  const uint32_t m = mask[(int64_t)row * words + w];
+  if (m == 0xffffffffu) return;
+  T* lr = logits + (int64_t)row * row_stride + (int64_t)w * 32;
+  const int n = min(32, vocab - w * 32);
+  for (int i = 0; i < n; ++i)
+    if (!((m >> i) & 1u)) {
+      if constexpr (sizeof(T) == 2) lr[i] = (T)0xff80u;  // bf16 -inf
+      else lr[i] = -INFINITY;
+    }
+}
+}  // namespace
+
+extern "C" int omnia_apply_token_mask(void* logits, int logits_is_bf16, int rows,
+                                      int64_t row_stride, int vocab, const uint32_t* mask,
+                                      int words, hipStream_t s) {
+  if (rows == 0) return 0;
+  dim3 grid((words + 255) / 256, rows);
+  if (logits_is_bf16)
+    apply_token_mask_kernel<uint16_t><<<grid, 256, 0, s>>>((uint16_t*)logits, row_stride, vocab,
+                                                           mask, words);
+  else
+    apply_token_mask_kernel<float><<<grid, 256, 0, s>>>((float*)logits, row_stride, vocab, mask,
+                                                        words);
+  return (int)hipGetLastError();
+}

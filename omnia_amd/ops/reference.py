@@ -221,3 +221,12 @@ def moe(x: torch.Tensor, router: torch.Tensor, w_gu: torch.Tensor, w_down: torch
                     a = a.to(act_dtype).float()
                 out[t] += float(wts[t, j]) * (w_down[e].float() @ a)
     return out
+
+
+def apply_token_mask(logits: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """fp32 reference of K13: unpack the int32 bit rows and fill -inf where clear."""
+    B, V = logits.shape
+    bits = (mask.to(torch.int64).unsqueeze(-1) >> torch.arange(32, device=mask.device)) & 1
+    allow = bits.reshape(B, -1)[:, :V].to(torch.bool).to(logits.device)
+    logits.masked_fill_(~allow, float("-inf"))
+    return logits

@@ -103,7 +103,10 @@ class Agent:
         return {"messages": [self._system_message(variables).to_dict()], "turn": 0,
                 "created": time.time()}
 
-    def params(self, overrides: dict | None = None) -> SamplingParams:
+    def params(self, overrides: dict | None = None, guided: bool = False) -> SamplingParams:
+        """Sampling params for a turn.  ``guided``: enforce the function-mode response
+        format in the engine (K13 grammar masks; ignored by remote/mock providers) --
+        only on tool-free turns, where the whole answer is the JSON document."""
         d = {}
         dd = self.cfg.defaults or {}
         for k_src, k in (("temperature", "temperature"), ("topP", "top_p"),
@@ -112,6 +115,11 @@ class Agent:
                 d[k] = dd[k_src]
         d.update(self.prompt.parameters or {})
         d.update(overrides or {})
+        if guided and self.cfg.response_format in ("json", "json_schema"):
+            if self.cfg.response_format == "json_schema" and self.cfg.response_schema:
+                d.setdefault("json_schema", self.cfg.response_schema)
+            else:
+                d.setdefault("json_object", True)
         return SamplingParams.from_dict(d)
 
     def _count(self, m: Message) -> int:
@@ -184,7 +192,8 @@ class Agent:
             if self.executor is not None and policy.tool_choice != "none":
                 tools = self.pack.tool_specs(self.prompt, self.executor.specs())
             params = self.params((metadata or {}).get("parameters")
-                                 if isinstance((metadata or {}).get("parameters"), dict) else None)
+                                 if isinstance((metadata or {}).get("parameters"), dict) else None,
+                                 guided=not tools)
             max_rounds = self.cfg.max_rounds or policy.max_rounds
             text_acc: list[str] = []
             calls_total = 0

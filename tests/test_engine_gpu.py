@@ -93,3 +93,27 @@ def test_llama3_8b_shapes_one_step():
     assert e.runner.stats["graph_replays"] > 0
     del e
     torch.cuda.empty_cache()
+
+
+def test_guided_json_mixed_with_pipelined_batch():
+    """Grammar-constrained requests (synchronous steps with GPU token masks) share
+    the engine with ordinary requests; every guided output is schema-valid JSON."""
+    import json
+
+    from omnia_amd.utils import jsonschema as js
+
+    schema = {"type": "object", "properties": {"n": {"type": "integer"},
+                                               "tag": {"enum": ["x", "yy"]}},
+              "required": ["n", "tag"]}
+    e = eng()
+    guided = [e.add_request(list(range(20, 60 + i)), SamplingParams(
+        temperature=0.9, seed=i, max_tokens=200, json_schema=schema)) for i in range(4)]
+    free = [e.add_request(list(range(30, 70)), SamplingParams(temperature=0, max_tokens=20,
+                                                              ignore_eos=True))
+            for _ in range(3)]
+    e.run_until_done()
+    for s in guided:
+        assert s.finish_reason.value == "stop"
+        js.validate(json.loads(e.tokenizer.decode(s.output)), schema)
+    assert all(len(s.output) == 20 for s in free)
+    assert free[0].output == free[1].output == free[2].output

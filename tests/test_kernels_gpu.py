@@ -194,3 +194,22 @@ def test_sample_penalties():
     tok = ops.sample(logits, temp, counts=counts, freq_pen=freq, pres_pen=pres).cpu()
     assert tok.tolist() == [20, 10]
     assert int(counts[0, 20]) == 1 and int(counts[1, 10]) == 1
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("V", [1000, 128256])
+def test_apply_token_mask_matches_reference(dtype, V):
+    g = torch.Generator().manual_seed(5)
+    B, W = 5, (V + 31) // 32
+    logits = torch.randn(B, V, generator=g).to(dtype)
+    mask = torch.randint(-2**31, 2**31 - 1, (B, W), generator=g, dtype=torch.int64).to(torch.int32)
+    mask[2] = -1  # an unconstrained row stays untouched
+    want = ref.apply_token_mask(logits.float().clone(), mask)
+    got = ops.apply_token_mask(logits.cuda(), mask.cuda()).float().cpu()
+    assert torch.equal(torch.isinf(got), torch.isinf(want))
+    fin = torch.isfinite(want)
+    assert torch.equal(got[fin], want[fin])
+    # masked greedy sampling picks the best ALLOWED token
+    tok = ops.sample(ops.apply_token_mask(logits.cuda(), mask.cuda()),
+                     torch.zeros(B, device="cuda"))
+    assert torch.equal(tok.cpu().long(), want.argmax(-1))

@@ -313,6 +313,11 @@ class OpenAICompatProvider(Provider):
             body["user"] = session_id
         if tools:
             body["tools"] = [{"type": "function", "function": t} for t in tools]
+        elif params.json_schema is not None:
+            body["response_format"] = {"type": "json_schema", "json_schema": {
+                "name": "response", "schema": params.json_schema, "strict": True}}
+        elif params.json_object:
+            body["response_format"] = {"type": "json_object"}
         usage = Usage()
         calls: dict[int, dict] = {}
         finish = ""

@@ -1,9 +1,12 @@
 """Llama-3 family forward on the engine's paged KV cache (TP-aware).
 
 Per layer (T tokens, hidden d):
-    fused_add_rmsnorm -> QKV GEMM (hipBLASLt) -> RoPE + paged KV write (HIP) ->
+    fused_add_rmsnorm -> QKV GEMM -> RoPE + paged KV write (HIP) ->
     paged attention (HIP prefill / decode) -> O GEMM [-> TP all-reduce] ->
-    fused_add_rmsnorm -> gate_up GEMM -> SwiGLU (HIP) -> down GEMM [-> all-reduce]
+    fused_add_rmsnorm -> gate_up GEMM + SwiGLU -> down GEMM [-> all-reduce]
+GEMMs go through :func:`omnia_amd.ops.linear`: the hand MFMA decode kernel
+(``ops/csrc/gemm.hip``, SwiGLU fused in its epilogue) on the shapes where the
+MI355X sweep measured it faster, tuned hipBLASLt everywhere else.
 Weights are kept in their natural [out, in] layout so ``F.linear`` maps onto a
 single hipBLASLt GEMM; column-parallel shards (QKV, gate_up) and row-parallel
 shards (O, down) follow Megatron.  The reference has no model code at all
@@ -87,6 +90,7 @@ class LlamaModel:
                                         cfg.rope_scaling, device=self.device)
         self.w = weights if weights is not None else self._random_weights(seed)
         self._ws = {}
+        ops.dgemm_prepare(self.device)  # split-K workspace, before any graph capture
 
     # ------------------------------------------------------------ weights
     def _random_weights(self, seed: int) -> dict:
@@ -147,14 +151,13 @@ class LlamaModel:
 
     # ------------------------------------------------------------ forward
     def mlp(self, layer: dict, h: torch.Tensor) -> torch.Tensor:
-        gu = F.linear(h, layer["gate_up"])
-        a = ops.silu_mul(gu)
-        return F.linear(a, layer["down"])
+        a = ops.linear_silu(h, layer["gate_up"])  # SwiGLU fused into decode GEMMs
+        return ops.linear(a, layer["down"])
 
     def attention(self, li: int, h: torch.Tensor, fb: ForwardBatch, kv: KVCache) -> torch.Tensor:
         T = h.shape[0]
         D = self.cfg.head_dim
-        qkv = F.linear(h, self.w["layers"][li]["qkv"])
+        qkv = ops.linear(h, self.w["layers"][li]["qkv"])
         q = qkv[:, : self.hq * D]
         k = qkv[:, self.hq * D: (self.hq + self.hkv) * D]
         v = qkv[:, (self.hq + self.hkv) * D:]
@@ -169,7 +172,7 @@ class LlamaModel:
         else:
             o = ops.prefill_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.q_start_loc,
                                       fb.seq_lens, self.scale, fb.tile_seq, fb.tile_q0)
-        out = F.linear(o.view(T, self.hq * D), self.w["layers"][li]["o"])
+        out = ops.linear(o.view(T, self.hq * D), self.w["layers"][li]["o"])
         return pstate.tp_all_reduce(out)
 
     def decode_part(self, batch: int, max_ctx: int) -> int:
@@ -211,7 +214,7 @@ class LlamaModel:
         return h
 
     def logits(self, h: torch.Tensor) -> torch.Tensor:
-        lg = F.linear(h, self.w["lm_head"])
+        lg = ops.linear(h, self.w["lm_head"])
         return pstate.tp_all_gather_lastdim(lg) if self.tp > 1 else lg
 
     def forward(self, fb: ForwardBatch, kv: KVCache) -> torch.Tensor:

@@ -93,6 +93,126 @@ def rope_kv(q, k, v, positions, cos_sin, k_cache, v_cache, slots, hq, hkv, block
         ref.write_kv(k_cache, v_cache, kr, v.reshape(T, hkv, D), slots)
 
 
+# ------------------------------------------------------- decode GEMM (K3/K8/K9/K10)
+DGEMM_MAX_M = 256
+_DGEMM_WS_FLOATS = 16 << 20  # 64 MiB of split-K slabs per device
+_DGEMM_CNT = 8192
+_dgemm_ws: dict = {}
+_dgemm_table: dict | None = None
+_dgemm_on = os.environ.get("OMNIA_DGEMM", "1") != "0"
+_dgemm_force = os.environ.get("OMNIA_DGEMM", "") == "force"
+
+
+def dgemm_prepare(device) -> None:
+    """Allocate the split-K workspace + zeroed tile counters for ``device``.
+
+    Call eagerly (model init) so nothing is allocated while a hipGraph captures."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _dgemm_ws:
+        _dgemm_ws[key] = (torch.empty(_DGEMM_WS_FLOATS, dtype=torch.float32, device=dev),
+                          torch.zeros(_DGEMM_CNT, dtype=torch.int32, device=dev))
+
+
+def _dgemm_tuned() -> dict:
+    global _dgemm_table
+    if _dgemm_table is None:
+        import json
+
+        p = os.path.join(os.path.dirname(__file__), "tuned", "dgemm_mi355x.json")
+        tab = {}
+        if os.path.exists(p):
+            with open(p) as f:
+                for k, v in json.load(f).items():
+                    tab[k] = tuple(v)
+        _dgemm_table = tab
+    return _dgemm_table
+
+
+DGEMM_BUCKETS = (8, 32, 64, 128, 256)
+
+
+def dgemm_bucket(M: int) -> int:
+    for b in DGEMM_BUCKETS:
+        if M <= b:
+            return b
+    return 0
+
+
+def dgemm_config(M: int, N: int, K: int, mode: int, force: bool | None = None
+                 ) -> tuple[int, int, int] | None:
+    """(wm, wn, splits) for a decode GEMM, or None to use hipBLASLt.
+
+    Dispatch is measured, not assumed: ``ops/tuned/dgemm_mi355x.json`` (written
+    by ``scripts/dgemm_sweep.py`` on an MI355X, keyed ``mode:Mbucket:N:K``) lists
+    the shapes where the hand kernel beat the tuned hipBLASLt solution; every
+    other shape stays on the library.  ``force`` (or ``OMNIA_DGEMM=force``) uses
+    the heuristic config for any covered shape (tests, sweeps)."""
+    if M < 1 or M > DGEMM_MAX_M or K % 64:
+        return None
+    wm = 1 if M <= 64 else 2 if M <= 128 else 4
+    hit = _dgemm_tuned().get(f"{mode}:{dgemm_bucket(M)}:{N}:{K}")
+    if hit is not None:
+        return (wm, hit[1], hit[2]) if hit[0] == wm else hit
+    if not (force if force is not None else _dgemm_force):
+        return None
+    wn = 2
+    cols = 64 * wn if mode == 0 else 32 * wn
+    if N % cols:
+        wn = 1
+        cols = 64 if mode == 0 else 32
+        if N % cols:
+            return None
+    tiles = N // cols
+    s = 1
+    while (tiles * s < 256 and s < 8 and K % (64 * s * 2) == 0
+           and N * (s * 2) * 64 * wm * (1 if mode == 0 else 2) <= _DGEMM_WS_FLOATS):
+        s *= 2
+    return wm, wn, s
+
+
+def _dgemm(mode: int, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None):
+    if not (_dgemm_on and x.is_cuda and x.dim() == 2 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and w.is_contiguous()):
+        return None
+    M, K = x.shape
+    N = w.shape[0] if mode == 0 else w.shape[0] // 2
+    cfg = dgemm_config(M, N, K, mode)
+    if cfg is None:
+        return None
+    key = x.device.index if x.device.index is not None else torch.cuda.current_device()
+    if key not in _dgemm_ws:
+        dgemm_prepare(x.device)
+    ws, cnt = _dgemm_ws[key]
+    x = x.contiguous()
+    out = x.new_empty(M, N) if out is None else out
+    wm, wn, s = cfg
+    kernels().dgemm(mode, out, x, w, ws, cnt, s, wm, wn)
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``x @ w.T`` (w in [out, in] layout).  Decode-sized GPU batches (M <= 256)
+    run the hand MFMA kernel (gemm.hip); larger batches (prefill) hipBLASLt."""
+    r = _dgemm(0, x, w, out)
+    if r is not None:
+        return r
+    if out is not None:
+        return torch.mm(x, w.t(), out=out)
+    return F.linear(x, w)
+
+
+def linear_silu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
+    """``silu(x Wg^T) * (x Wu^T)`` with ``w_gu = [Wg; Wu]``: the SwiGLU MLP's first
+    half.  Decode batches fuse the activation into the GEMM epilogue."""
+    r = _dgemm(1, x, w_gu, None)
+    if r is not None:
+        return r
+    return silu_mul(F.linear(x, w_gu))
+
+
 def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None):
     inter = x.shape[-1] // 2
     if x.is_cuda:

@@ -50,6 +50,9 @@ int omnia_moe_gemm(int mode, void* out, const void* A, const void* W, const int*
                    int N, int topk, int n_assign, int e_lo, int max_blocks, hipStream_t s);
 int omnia_moe_combine(void* out, const void* Y, const int* ids, int n_tok, int d, int topk,
                       int e_lo, int e_hi, hipStream_t s);
+int omnia_dgemm(int mode, void* out, const void* X, const void* W, float* ws, int* cnt, int M,
+                int N, int K, int S, int wm, int wn, int ldo, int64_t ws_floats, int cnt_len,
+                hipStream_t s);
 }
 
 namespace {
@@ -342,6 +345,27 @@ void moe_combine(at::Tensor out, at::Tensor Y, at::Tensor ids, int64_t topk, int
                              e_lo, e_hi, cur_stream()), "moe_combine");
 }
 
+// decode projection GEMM: mode 0 out[M,N] = x W^T (W [N,K]); mode 1 out[M,I] =
+// silu(x Wg^T) * (x Wu^T) with W = [Wg; Wu] ([2I, K]).  Shapes are validated
+// here AND in omnia_dgemm before anything is launched.
+void dgemm(int64_t mode, at::Tensor out, at::Tensor x, at::Tensor W, at::Tensor ws, at::Tensor cnt,
+           int64_t splits, int64_t wm, int64_t wn) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(W); CHECK_BF16(out);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_cuda(), "ws fp32");
+  CHECK_I32(cnt);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && out.dim() == 2, "2-D operands");
+  TORCH_CHECK(x.is_contiguous() && W.is_contiguous() && out.stride(1) == 1, "contiguous");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(W.size(1) == K, "K mismatch");
+  const int N = mode == 0 ? W.size(0) : W.size(0) / 2;
+  TORCH_CHECK(mode == 0 || W.size(0) % 2 == 0, "gate_up rows even");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N, "out shape");
+  CHECK_RC(omnia_dgemm((int)mode, out.data_ptr(), x.data_ptr(), W.data_ptr(),
+                       ws.data_ptr<float>(), cnt.data_ptr<int>(), M, N, K, (int)splits, (int)wm,
+                       (int)wn, (int)out.stride(0), ws.numel(), (int)cnt.numel(), cur_stream()),
+           "dgemm");
+}
+
 // ------------------------------------------------- host step launch (no GIL churn)
 // One decode step = H2D staging copy + graph launch + D2H token copy + event
 // record, enqueued back to back on the current stream inside ONE Python call.
@@ -415,6 +439,7 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("moe_align", &moe_align);
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
+  m.def("dgemm", &dgemm);
   m.def("apply_token_mask", &apply_token_mask);
   m.def("graph_launch_step", &graph_launch_step);
   m.def("event_create", &event_create);

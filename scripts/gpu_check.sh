@@ -3,7 +3,7 @@
 # crash/timeout (anything other than a clean pass/fail exit).
 mkdir -p gpurun_out
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
-timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "gpu tests rc=$rc"; tail -3 gpurun_out/gpu_tests.log
 ok $rc || exit $rc
 timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1

@@ -50,6 +50,16 @@ int omnia_moe_gemm(int mode, void* out, const void* A, const void* W, const int*
                    int N, int topk, int n_assign, int e_lo, int max_blocks, hipStream_t s);
 int omnia_moe_combine(void* out, const void* Y, const int* ids, int n_tok, int d, int topk,
                       int e_lo, int e_hi, hipStream_t s);
+int omnia_ipc_handle_size();
+int omnia_ipc_alloc(void** ptr, int64_t bytes);
+int omnia_ipc_free(void* ptr);
+int omnia_ipc_get_handle(void* ptr, void* handle_out);
+int omnia_ipc_open(const void* handle, void** ptr);
+int omnia_ipc_close(void* ptr);
+int omnia_ar_blocks();
+int omnia_ar_max_ranks();
+int omnia_ar_oneshot(void* out, const void* in, void* const* regions, int* epochs, int* err,
+                     int64_t n, int64_t slot_bytes, int rank, int world, hipStream_t s);
 int omnia_dgemm(int mode, void* out, const void* X, const void* W, float* ws, int* cnt, int M,
                 int N, int K, int S, int wm, int wn, int ldo, int64_t ws_floats, int cnt_len,
                 hipStream_t s);
@@ -366,6 +376,43 @@ void dgemm(int64_t mode, at::Tensor out, at::Tensor x, at::Tensor W, at::Tensor 
            "dgemm");
 }
 
+// ------------------------------------------------- one-shot IPC all-reduce (K16)
+int64_t ipc_alloc(int64_t bytes) {
+  void* p = nullptr;
+  CHECK_RC(omnia_ipc_alloc(&p, bytes), "ipc_alloc");
+  return reinterpret_cast<int64_t>(p);
+}
+void ipc_free(int64_t ptr) { CHECK_RC(omnia_ipc_free(reinterpret_cast<void*>(ptr)), "ipc_free"); }
+py::bytes ipc_get_handle(int64_t ptr) {
+  std::string h(omnia_ipc_handle_size(), '\0');
+  CHECK_RC(omnia_ipc_get_handle(reinterpret_cast<void*>(ptr), &h[0]), "ipc_get_handle");
+  return py::bytes(h);
+}
+int64_t ipc_open(py::bytes handle) {
+  std::string h = handle;
+  TORCH_CHECK((int)h.size() == omnia_ipc_handle_size(), "bad IPC handle size");
+  void* p = nullptr;
+  CHECK_RC(omnia_ipc_open(h.data(), &p), "ipc_open");
+  return reinterpret_cast<int64_t>(p);
+}
+void ipc_close(int64_t ptr) { CHECK_RC(omnia_ipc_close(reinterpret_cast<void*>(ptr)), "ipc_close"); }
+
+// regions: int64 CPU tensor [world] of region base pointers (own + opened peers)
+void ar_oneshot(at::Tensor out, at::Tensor in, at::Tensor regions, at::Tensor epochs,
+                at::Tensor err, int64_t slot_bytes, int64_t rank) {
+  CHECK_GPU(in); CHECK_BF16(in); CHECK_BF16(out); CHECK_I32(epochs); CHECK_I32(err);
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel(), "contig");
+  TORCH_CHECK(regions.device().is_cpu() && regions.scalar_type() == at::kLong, "regions cpu i64");
+  TORCH_CHECK(epochs.numel() >= omnia_ar_blocks(), "epochs per block");
+  const int world = regions.numel();
+  TORCH_CHECK(world <= omnia_ar_max_ranks(), "world too large");
+  std::vector<void*> regs(world);
+  for (int p = 0; p < world; ++p) regs[p] = reinterpret_cast<void*>(regions.data_ptr<int64_t>()[p]);
+  CHECK_RC(omnia_ar_oneshot(out.data_ptr(), in.data_ptr(), regs.data(), epochs.data_ptr<int>(),
+                            err.data_ptr<int>(), in.numel(), slot_bytes, (int)rank, world,
+                            cur_stream()), "ar_oneshot");
+}
+
 // ------------------------------------------------- host step launch (no GIL churn)
 // One decode step = H2D staging copy + graph launch + D2H token copy + event
 // record, enqueued back to back on the current stream inside ONE Python call.
@@ -440,6 +487,14 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
   m.def("dgemm", &dgemm);
+  m.def("ipc_alloc", &ipc_alloc);
+  m.def("ipc_free", &ipc_free);
+  m.def("ipc_get_handle", &ipc_get_handle);
+  m.def("ipc_open", &ipc_open);
+  m.def("ipc_close", &ipc_close);
+  m.def("ar_oneshot", &ar_oneshot);
+  m.def("ar_blocks", &omnia_ar_blocks);
+  m.def("ar_max_ranks", &omnia_ar_max_ranks);
   m.def("apply_token_mask", &apply_token_mask);
   m.def("graph_launch_step", &graph_launch_step);
   m.def("event_create", &event_create);

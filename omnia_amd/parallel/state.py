@@ -95,6 +95,12 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, device: str |
             g = dist.new_group(ranks) if len(ranks) > 1 else None
             if rank in ranks:
                 st.dp_group = g
+        if use_gpu and tp_size > 1 and os.environ.get("OMNIA_CUSTOM_AR", "0") == "1":
+            # one-shot IPC all-reduce for decode-size TP collectives (opt-in until
+            # validated on a full 8-GPU node; RCCL stays the default and the oracle)
+            from .custom_allreduce import CustomAllReduce
+
+            st.custom_ar = CustomAllReduce(st.tp_group)
     set_state(st)
     return st
 

@@ -37,14 +37,29 @@ def shared_engine(engine_cfg: dict | None = None):
     eng = _ENGINES.get(key)
     if eng is None:
         kw = {}
-        for k, v in (engine_cfg or {}).items():
+        ecfg = dict(engine_cfg or {})
+        # data-parallel replicas on this node: one engine-core process per GPU,
+        # sessions pinned by the rendezvous router (parallel/router.py)
+        n_rep = int(ecfg.pop("replicas", 0) or ecfg.pop("dp", 0) or
+                    os.environ.get("OMNIA_ENGINE_REPLICAS", "1"))
+        for k, v in ecfg.items():
             if k in EngineConfig.__dataclass_fields__:
                 t = EngineConfig.__dataclass_fields__[k].type
                 kw[k] = (int(v) if "int" in str(t) else float(v) if "float" in str(t)
                          else (str(v).lower() == "true") if "bool" in str(t) else v)
         cfg = EngineConfig.from_env(**kw)
         eng = None
-        if _use_engine_process(cfg):
+        if n_rep > 1:
+            from ..engine.core_proc import EngineCoreClient
+            from ..parallel.router import ReplicatedEngine
+
+            if cfg.device == "cuda":
+                reps = [EngineCoreClient(cfg, device_index=i * max(1, cfg.tp))
+                        for i in range(n_rep)]
+            else:
+                reps = [AsyncLLMEngine.from_config(cfg) for _ in range(n_rep)]
+            eng = ReplicatedEngine(reps)
+        elif _use_engine_process(cfg):
             from ..engine.core_proc import EngineCoreClient
 
             eng = EngineCoreClient(cfg)

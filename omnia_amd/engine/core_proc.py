@@ -97,6 +97,8 @@ class _Core:
         self.fin_out: list = []
         self.frames = _Frames()
         self.stop = False
+        self.faults: list = []
+        self.fatal = False
 
     # -- engine callbacks (engine thread == this thread)
     def _on_token(self, s, tok, text):
@@ -156,6 +158,11 @@ class _Core:
 
                 torch.cuda.synchronize(eng.device)
             return True
+        if name == "health":
+            now = time.monotonic()
+            recent = [t for t in self.faults if now - t < 60.0]
+            storm = len(recent) >= int(os.environ.get("OMNIA_ENGINE_MAX_FAULTS", "3"))
+            return {"healthy": not (self.fatal or storm), "faults": len(self.faults)}
         if name == "stats":
             return {"timing": dict(eng.timing), "counters": dict(eng.counters),
                     "runner": {k: v for k, v in eng.runner.stats.items()},
@@ -203,7 +210,13 @@ class _Core:
                     eng.step()
                 except Exception as e:  # noqa: BLE001
                     log.exception("engine step failed")
-                    self._fail_all(e)
+                    self.faults.append(time.monotonic())
+                    try:
+                        eng.recover(e)  # fail live seqs, drop resident KV, keep serving
+                    except Exception:  # noqa: BLE001
+                        log.exception("engine recovery failed")
+                        self._fail_all(e)
+                        self.fatal = True
             if self.tok_out or self.fin_out:
                 toks = [[rid, "".join(e[0]), e[1], e[2]] for rid, e in self.tok_out.items()]
                 fins, self.fin_out = self.fin_out, []
@@ -441,6 +454,19 @@ class EngineCoreClient:
 
     def stats(self) -> dict:
         return self.call("stats")
+
+    def health(self, timeout: float | None = None) -> bool:
+        """False when the core died, reports a fault storm, or cannot answer within
+        ``OMNIA_CORE_HEALTH_TIMEOUT_S`` (a hung GPU step blocks its loop) -- the
+        cross-process form of the in-process engine watchdog."""
+        if self._closed or self.error is not None or self.proc.poll() is not None:
+            return False
+        t = float(os.environ.get("OMNIA_CORE_HEALTH_TIMEOUT_S", "30")) if timeout is None \
+            else timeout
+        try:
+            return bool(self.call("health", timeout=t).get("healthy"))
+        except Exception:  # noqa: BLE001 - timeout / broken pipe
+            return False
 
     def shutdown(self, timeout: float = 30.0):
         if self._closed:

@@ -25,6 +25,7 @@ from ..models import build_model
 from ..models.config import ModelConfig, resolve
 from ..models.llama import KVCache
 from ..observability import metrics as M
+from ..utils import failpoints
 from .kv_manager import BlockManager
 from .model_runner import ModelRunner
 from .sampling_params import SamplingParams
@@ -220,9 +221,40 @@ class LLMEngine:
         output -- before step N's tokens are pulled to the host and processed,
         so host work (scheduling, detokenisation, streaming, stop checks)
         overlaps the GPU instead of idling it."""
+        if failpoints.active():
+            failpoints.hit("engine.step")
+            failpoints.hit("engine.prefill" if self.scheduler.waiting else "engine.decode_step")
+            if failpoints.triggered("engine.hang"):
+                time.sleep(float(os.environ.get("OMNIA_FAILPOINT_HANG_S", "5")))
         if self.cfg.pipeline and self.runner.use_graphs:
             return self._step_pipelined()
         return self._step_sync()
+
+    def recover(self, err: Exception) -> int:
+        """Engine-fault recovery (SURVEY §5.3 [design]): fail every live sequence
+        with ERROR (the runtime answers the turn with an ``ENGINE_FAULT`` error),
+        discard the in-flight pipelined step and ALL resident session KV (it may
+        hold half-written pages), so the next turn of each session re-prefills
+        from its transcript -- the transcript stays authoritative, as in the
+        reference's resume path.  Returns the number of sequences failed."""
+        self.inflight = None
+        self.counters["faults"] = self.counters.get("faults", 0) + 1
+        M.ENGINE_FAULTS.labels(type(err).__name__).inc()
+        n = 0
+        for s in list(self.seqs.values()):
+            self.scheduler.abort(s.seq_id)
+            s.finish_reason = FinishReason.ERROR
+            self._finalize(s)
+            n += 1
+        for sid in list(self.blocks.sessions.keys()):
+            self.blocks.drop_session(sid)
+        if self.device.type == "cuda":
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:  # noqa: BLE001 - a dead context stays dead; health says so
+                log.exception("device sync after fault failed")
+        log.error("engine fault (%s): failed %d sequences, dropped resident KV", err, n)
+        return n
 
     def has_work(self) -> bool:
         return self.inflight is not None or self.scheduler.has_work()
@@ -483,9 +515,34 @@ class AsyncLLMEngine:
         self._wake = threading.Event()
         self._stop = False
         self._outbox: dict = {}  # loop -> [(queue, event)] flushed once per engine step
+        self.error: Exception | None = None
+        self.healthy = True
+        self._fault_times: list = []
+        self._step_t0 = None
+        self.step_timeout = float(os.environ.get("OMNIA_STEP_TIMEOUT_S", "120"))
         self._thread = threading.Thread(target=self._loop, name="omnia-engine", daemon=True)
         self._thread.start()
-        self.error: Exception | None = None
+        self._watchdog = threading.Thread(target=self._watch, name="omnia-engine-watchdog",
+                                          daemon=True)
+        self._watchdog.start()
+
+    def _watch(self):
+        """Step watchdog: a GPU step that never returns (hung kernel, lost peer in
+        a collective) cannot be interrupted from Python, so the watchdog flips
+        ``healthy`` off -- readiness fails, the replica router re-homes the
+        engine's sessions and the orchestrator restarts the pod."""
+        while not self._stop:
+            t0 = self._step_t0
+            if t0 is not None and self.healthy and time.monotonic() - t0 > self.step_timeout:
+                self.healthy = False
+                self.error = TimeoutError(f"engine step exceeded {self.step_timeout:.0f}s")
+                M.ENGINE_FAULTS.labels("StepTimeout").inc()
+                log.error("engine watchdog: step running for >%.0fs, marking unhealthy",
+                          self.step_timeout)
+            time.sleep(min(1.0, max(0.05, self.step_timeout / 10)))
+
+    def health(self) -> bool:
+        return self.healthy and self._thread.is_alive()
 
     def _emit(self, loop, q, ev):
         self._outbox.setdefault(loop, []).append((q, ev))
@@ -526,12 +583,24 @@ class AsyncLLMEngine:
                 except Exception as e:  # surface to the submitter
                     log.exception("engine request failed: %s", e)
             if eng.has_work():
+                self._step_t0 = time.monotonic()
                 try:
                     eng.step()
                 except Exception as e:
                     log.exception("engine step failed")
                     self.error = e
-                    self._fail_all(e)
+                    self._fault_times.append(time.monotonic())
+                    try:
+                        eng.recover(e)
+                    except Exception:  # noqa: BLE001
+                        log.exception("engine recovery failed")
+                        self._fail_all(e)
+                        self.healthy = False
+                    recent = [t for t in self._fault_times if time.monotonic() - t < 60.0]
+                    self._fault_times = recent
+                    if len(recent) >= int(os.environ.get("OMNIA_ENGINE_MAX_FAULTS", "3")):
+                        self.healthy = False  # fault storm: stop advertising readiness
+                self._step_t0 = None
                 self._flush()
             else:
                 self._flush()

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import asyncio
 
+from ..utils import failpoints
 from ..api.proto import runtime_v1 as pb
 
 
@@ -87,6 +88,7 @@ class GrpcRuntimeClient:
         """Dial with retry (cmd/agent/runtime_dial.go:47-112)."""
         for _ in range(attempts):
             try:
+                failpoints.hit("runtime.dial")
                 h = await self.health(timeout=2.0)
                 if h.healthy:
                     return True

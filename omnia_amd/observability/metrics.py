@@ -95,6 +95,8 @@ PREFILL_TOKENS = Counter("omnia_engine_prefill_tokens_total", "Prefilled tokens"
 DECODE_TOKENS = Counter("omnia_engine_decode_tokens_total", "Decoded tokens", registry=REGISTRY)
 BATCH_SIZE = Histogram("omnia_engine_batch_size", "Decode batch size",
                        buckets=(1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024), registry=REGISTRY)
+ENGINE_FAULTS = Counter("omnia_engine_faults_total", "Engine step faults (recovered or fatal)",
+                        ["type"], registry=REGISTRY)
 KV_UTIL = Gauge("omnia_engine_kv_utilization", "Fraction of KV pages in use", registry=REGISTRY)
 ENGINE_WAITING = Gauge("omnia_engine_requests_waiting", "Queued requests", registry=REGISTRY)
 KV_HIT_TOKENS = Counter("omnia_engine_kv_hit_tokens_total", "Prompt tokens served from session KV",

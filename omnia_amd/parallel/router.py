@@ -105,6 +105,17 @@ class ReplicatedEngine:
         finally:
             self.router.release(r)
 
+    def health(self) -> bool:
+        """Probe every replica, pull dead ones out of routing; healthy while any
+        replica can serve (its sessions re-home to the survivors)."""
+        alive = False
+        for i, rep in enumerate(self.replicas):
+            h = getattr(rep, "health", None)
+            ok = bool(h()) if callable(h) else True
+            self.router.mark(i, ok)
+            alive = alive or ok
+        return alive
+
     def drop_session(self, session_id: str):
         for rep in self.replicas:
             rep.drop_session(session_id)

@@ -25,13 +25,14 @@ from dataclasses import dataclass, field
 
 from ..engine.sampling_params import SamplingParams
 from ..observability import metrics as M
+from ..utils import failpoints
 from ..observability import tracing
 from ..tools.executor import CallContext, OmniaExecutor
 from ..observability import logging as logctx
 from .chat import Message, ToolCallReq
 from .context_store import StoreUnavailable
 from .promptpack import PromptPack, run_validators
-from .providers import Provider, ProviderEvent, Usage
+from .providers import Provider, ProviderError, ProviderEvent, Usage
 
 log = logging.getLogger("omnia.runtime.agent")
 
@@ -206,6 +207,7 @@ class Agent:
                 t_llm = time.perf_counter()
                 status = "ok"
                 try:
+                    failpoints.hit("provider.stream")
                     async for ev in self.provider.stream(window, tools, params, session_id,
                                                          metadata):
                         if ev.type == "text" and ev.text:
@@ -215,7 +217,8 @@ class Agent:
                         elif ev.type == "tool_calls":
                             round_calls.extend(ev.tool_calls)
                         elif ev.type == "error":
-                            raise RuntimeError(ev.text or "provider error")
+                            raise ProviderError(ev.text or "provider error",
+                                                ev.code or "PROVIDER_ERROR")
                         elif ev.type == "done":
                             if ev.usage:
                                 res.usage += ev.usage

@@ -44,6 +44,16 @@ class ProviderEvent:
     usage: Usage | None = None
     finish_reason: str = ""
     ttft: float | None = None
+    code: str = ""  # error events: machine code surfaced in the runtime Error frame
+
+
+class ProviderError(RuntimeError):
+    """A provider failure with a client-visible code (``ENGINE_FAULT``,
+    ``PROVIDER_ERROR``...).  The message stays generic on the wire."""
+
+    def __init__(self, message: str = "provider error", code: str = "PROVIDER_ERROR"):
+        super().__init__(message)
+        self.code = code
 
 
 @dataclass
@@ -154,7 +164,7 @@ class LocalEngineProvider(Provider):
                 elif text:
                     yield ProviderEvent("text", text=text)
                 if ev.finish_reason == "error":
-                    yield ProviderEvent("error", text="engine error")
+                    yield ProviderEvent("error", text="engine fault", code="ENGINE_FAULT")
                 yield ProviderEvent("done", usage=usage, finish_reason=ev.finish_reason or "",
                                     ttft=ev.ttft if ev.ttft is not None else ttft)
                 return
@@ -163,6 +173,13 @@ class LocalEngineProvider(Provider):
         if self.embedder is None:
             raise NotImplementedError("no embedding model configured")
         return await self.embedder.embed(texts)
+
+    async def health(self) -> bool:
+        h = getattr(self.engine, "health", None)
+        if not callable(h):
+            return True
+        # an engine-core health call is a blocking round trip: keep it off the loop
+        return bool(await asyncio.get_running_loop().run_in_executor(None, h))
 
 
 # ===================================================================== mock

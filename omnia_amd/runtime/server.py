@@ -28,6 +28,7 @@ from ..observability import metrics as M
 from ..observability import tracing
 from ..tools.executor import CallContext
 from .agent import Agent, TurnIO
+from .providers import ProviderError
 from .chat import ToolCallReq
 from .context_store import StoreUnavailable
 
@@ -222,6 +223,12 @@ class RuntimeService:
         try:
             res = await self.agent.run_turn(sid, content, io, parts=parts, metadata=metadata,
                                             ctx=ctx)
+        except ProviderError as e:  # coded provider failure (e.g. ENGINE_FAULT)
+            log.error("turn failed for session %s: %s (%s)", sid, e, e.code)
+            tracing.end_span(span, error=True)
+            await stream.send(pb.ServerMessage(error=pb.Error(code=e.code,
+                                                              message=GENERIC_ERROR)))
+            return
         except Exception:  # noqa: BLE001 - never leak provider details
             log.exception("turn failed for session %s", sid)
             tracing.end_span(span, error=True)

@@ -21,6 +21,7 @@ import time
 from collections import OrderedDict
 from pathlib import Path
 
+from ..utils import failpoints
 from .model import (EvalResult, Message, ProviderCall, RuntimeEvent, Session, ToolCall,
                     STATUS_ACTIVE)
 
@@ -373,6 +374,7 @@ class TieredSessionService:
         return s
 
     async def append_message(self, sid: str, m: Message) -> Message:
+        failpoints.hit("session.write")
         s = self._get_session_only(sid)
         if s is None:
             raise KeyError(sid)

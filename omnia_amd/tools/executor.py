@@ -27,6 +27,7 @@ from pathlib import Path
 
 import yaml
 
+from ..utils import failpoints
 from ..observability import metrics as M
 from ..utils import jmespath
 from .resilience import (CircuitBreaker, CircuitOpen, PermanentError, RetryPolicy,
@@ -655,6 +656,7 @@ class OmniaExecutor:
             if not br.allow():
                 raise CircuitOpen(f"circuit open for tool {name}")
             try:
+                failpoints.hit("tool.call")
                 res = await asyncio.wait_for(h.call(tool, args, ctx), h.timeout + 1)
             except Exception:
                 br.record(False)

@@ -139,3 +139,25 @@ def test_expert_parallel_all_to_all_gloo():
         assert status == "ok", val
         assert val < 1e-4, (rank, val)
         assert stats["sent_rows"] > 0 and stats["recv_rows"] > 0
+
+
+def test_replicated_engine_health_rehomes_sessions():
+    class Rep:
+        def __init__(self):
+            self.ok = True
+            self.engine = None
+
+        def health(self):
+            return self.ok
+
+    reps = [Rep(), Rep(), Rep()]
+    eng = ReplicatedEngine(reps)
+    home = {f"s{i}": eng.replica_for(f"s{i}") for i in range(300)}
+    reps[1].ok = False
+    assert eng.health() is True
+    for sid, r in home.items():
+        now = eng.replica_for(sid)
+        assert now != 1 and (r == 1 or now == r)
+    for r in reps:
+        r.ok = False
+    assert eng.health() is False

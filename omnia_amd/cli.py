@@ -173,6 +173,11 @@ def main(argv=None):
     p.add_argument("--port", type=int, default=8090)
     p.add_argument("-f", "--filename", action="append", default=[])
     p.add_argument("--no-engine", action="store_true")
+    p.add_argument("--leader-elect", action="store_true",
+                   help="cluster mode: run reconcilers only while holding the Lease")
+    p.add_argument("--enterprise", action="store_true", help="also run the EE controllers")
+    p = sp.add_parser("chart", help="write the Helm chart + kustomize bases (deploy/)")
+    p.add_argument("--out", default="deploy")
     p = sp.add_parser("apply")
     p.add_argument("-f", "--filename", action="append", required=True)
     p.add_argument("-n", "--namespace", default="default")
@@ -202,6 +207,11 @@ def main(argv=None):
         cmd_delete(a)
     elif a.cmd == "crds":
         cmd_crds(a)
+    elif a.cmd == "chart":
+        from .operator import chart
+
+        for rel in chart.write(a.out):
+            print(f"{a.out}/{rel}")
     elif a.cmd == "conformance":
         from .runtime import conformance
 

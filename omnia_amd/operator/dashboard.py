@@ -1,0 +1,131 @@
+"""Operator dashboard (minimal).
+
+The reference dashboard is a ~124K-line Next.js app (``dashboard/``): workspace
+resource browser, agent status, session viewer, a WebSocket console to an
+agent's facade, arena and consent UIs.  This is the serving-side core of it as
+one dependency-free page plus a small aiohttp backend:
+
+* ``GET /api/resources/{plural}`` proxies the operator REST API (K8s-style);
+* ``GET /api/sessions`` proxies session-api search (``/api/v1/sessions``);
+* ``GET /api/overview`` -- AgentRuntime phase / replicas / engine summary;
+* ``/`` -- the page: resource tables, session list, and a chat console that
+  opens ``ws://<facade>/ws?agent=...`` directly from the browser (the
+  reference proxies through the dashboard's mgmt-plane twin; here the facade's
+  own auth chain applies).
+Run: ``python -m omnia_amd.operator.dashboard --port 3000 --api http://operator:8090``.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+
+import aiohttp
+from aiohttp import web
+
+from ..api import crds
+
+PAGE = """<!doctype html><html><head><meta charset="utf-8"><title>Omnia (MI355X)</title>
+<style>body{font:14px system-ui;margin:24px;color:#222}table{border-collapse:collapse;margin:8px 0}
+td,th{border:1px solid #ccc;padding:4px 8px}th{background:#f3f3f3}#log{height:240px;overflow:auto;
+border:1px solid #ccc;padding:6px;white-space:pre-wrap}</style></head><body>
+<h1>Omnia &mdash; MI355X agent platform</h1>
+<h2>Agents</h2><table id="agents"><tr><th>namespace</th><th>name</th><th>phase</th>
+<th>replicas</th><th>provider</th></tr></table>
+<h2>Resources</h2><select id="kind"></select><table id="res"></table>
+<h2>Sessions</h2><table id="sess"><tr><th>id</th><th>agent</th><th>messages</th></tr></table>
+<h2>Console</h2><input id="ws" size="40" value="ws://127.0.0.1:8080/ws">
+<button onclick="conn()">connect</button><br><input id="msg" size="60">
+<button onclick="send()">send</button><div id="log"></div>
+<script>
+const KINDS=__KINDS__;let sock;
+async function j(u){const r=await fetch(u);return r.json()}
+async function agents(){const o=await j('/api/overview');const t=document.getElementById('agents');
+ for(const a of o.agents){const r=t.insertRow();for(const v of [a.namespace,a.name,a.phase,a.replicas,a.provider])
+ r.insertCell().textContent=v??''}}
+async function res(){const k=document.getElementById('kind').value;const o=await j('/api/resources/'+k);
+ const t=document.getElementById('res');t.innerHTML='<tr><th>namespace</th><th>name</th><th>phase</th></tr>';
+ for(const it of (o.items||[])){const r=t.insertRow();r.insertCell().textContent=it.metadata.namespace||'';
+ r.insertCell().textContent=it.metadata.name;r.insertCell().textContent=(it.status||{}).phase||''}}
+async function sess(){const o=await j('/api/sessions');const t=document.getElementById('sess');
+ for(const s of (o.sessions||[])){const r=t.insertRow();for(const v of [s.id,s.agent_name,s.message_count])
+ r.insertCell().textContent=v}}
+function log(x){const l=document.getElementById('log');l.textContent+=x+'\\n';l.scrollTop=1e9}
+function conn(){sock=new WebSocket(document.getElementById('ws').value);
+ sock.onmessage=e=>{const m=JSON.parse(e.data);log(m.type+': '+(m.content||m.error?.message||''))}}
+function send(){sock.send(JSON.stringify({type:'message',content:document.getElementById('msg').value}))}
+const sel=document.getElementById('kind');for(const k of KINDS){const o=document.createElement('option');
+ o.value=k;o.textContent=k;sel.appendChild(o)};sel.onchange=res;agents();res();sess();
+</script></body></html>"""
+
+
+def build_app(api: str, session_api: str = "") -> web.Application:
+    app = web.Application()
+    plurals = sorted(k.plural for k in crds.KINDS.values())
+
+    async def _get(url):
+        async with aiohttp.ClientSession() as s:
+            async with s.get(url, timeout=aiohttp.ClientTimeout(total=10)) as r:
+                return r.status, await r.json(content_type=None)
+
+    async def page(_):
+        return web.Response(text=PAGE.replace("__KINDS__", json.dumps(plurals)),
+                            content_type="text/html")
+
+    async def resources(request):
+        plural = request.match_info["plural"]
+        if plural not in plurals:
+            return web.json_response({"error": "unknown resource"}, status=404)
+        st, body = await _get(f"{api}/apis/{crds.GROUP}/{crds.VERSION}/{plural}")
+        return web.json_response(body, status=st)
+
+    async def sessions(request):
+        if not session_api:
+            return web.json_response({"sessions": []})
+        st, body = await _get(f"{session_api}/api/v1/sessions?limit="
+                              f"{int(request.query.get('limit', 50))}")
+        return web.json_response(body, status=st)
+
+    async def overview(_):
+        st, body = await _get(f"{api}/apis/{crds.GROUP}/{crds.VERSION}/agentruntimes")
+        out = []
+        for it in (body or {}).get("items", []):
+            spec, status = it.get("spec", {}), it.get("status", {})
+            provs = spec.get("providers") or []
+            out.append({"namespace": it["metadata"].get("namespace"),
+                        "name": it["metadata"]["name"], "phase": status.get("phase"),
+                        "replicas": (status.get("replicas") or {}).get("ready"),
+                        "provider": ",".join(p.get("providerRef", {}).get("name", "")
+                                             for p in provs)})
+        return web.json_response({"agents": out})
+
+    async def healthz(_):
+        return web.json_response({"status": "ok"})
+
+    app.router.add_get("/", page)
+    app.router.add_get("/api/resources/{plural}", resources)
+    app.router.add_get("/api/sessions", sessions)
+    app.router.add_get("/api/overview", overview)
+    app.router.add_get("/healthz", healthz)
+    return app
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("omnia-dashboard")
+    ap.add_argument("--port", type=int, default=3000)
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--api", default="http://127.0.0.1:8090")
+    ap.add_argument("--session-api", default="")
+    a = ap.parse_args(argv)
+
+    async def run():
+        runner = web.AppRunner(build_app(a.api, a.session_api))
+        await runner.setup()
+        await web.TCPSite(runner, a.host, a.port).start()
+        await asyncio.Event().wait()
+
+    asyncio.run(run())
+
+
+if __name__ == "__main__":
+    main()

@@ -128,7 +128,8 @@ def cmd_crds(a):
                              sort_keys=False))
 
 
-async def serve(port: int, manifests: list[str], engine: bool, host: str = "127.0.0.1"):
+async def serve(port: int, manifests: list[str], engine: bool, host: str = "127.0.0.1",
+                enterprise: bool = False, leader_elect: bool = True):
     from aiohttp import web
 
     from .operator.apiserver import build_app
@@ -136,6 +137,11 @@ async def serve(port: int, manifests: list[str], engine: bool, host: str = "127.
     from .operator.manager import Manager, new_store
 
     store = new_store()
+    if enterprise:
+        from .operator.manager import license_validator_for, set_license_validator
+
+        set_license_validator(license_validator_for(
+            store, os.environ.get("OMNIA_LICENSE_PUBLIC_KEY") or None))
     gpus = None
     try:
         import torch
@@ -143,7 +149,7 @@ async def serve(port: int, manifests: list[str], engine: bool, host: str = "127.
         gpus = torch.cuda.device_count()
     except Exception:  # noqa: BLE001
         pass
-    mgr = Manager(store, gpu_count=gpus, leader_elect=True)
+    mgr = Manager(store, gpu_count=gpus, leader_elect=leader_elect)
     await mgr.start()
     factory = None
     if engine:
@@ -198,7 +204,8 @@ def main(argv=None):
     p.add_argument("--session-api", default="")
     a = ap.parse_args(argv)
     if a.cmd == "serve":
-        asyncio.run(serve(a.port, a.filename, not a.no_engine))
+        asyncio.run(serve(a.port, a.filename, not a.no_engine, enterprise=a.enterprise,
+                          leader_elect=True))
     elif a.cmd == "apply":
         cmd_apply(a)
     elif a.cmd == "get":

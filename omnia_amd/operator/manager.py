@@ -23,8 +23,43 @@ log = logging.getLogger("omnia.operator.manager")
 
 
 # ------------------------------------------------------------------ webhooks
+_LICENSE = None  # ee.license.Validator when the manager runs with --enterprise
+
+
+def set_license_validator(v) -> None:
+    global _LICENSE
+    _LICENSE = v
+
+
+def license_validator_for(store: APIStore, public_key_pem: str | None):
+    """Validator reading Secret ``omnia-license`` (key ``license``) from ``store``."""
+    import base64
+
+    from ..ee import license as lic
+
+    def read():
+        for ns in (os.environ.get("OMNIA_NAMESPACE", "omnia-system"), "default"):
+            try:
+                sec = store.get("Secret", lic.SECRET_NAME, ns)
+            except Exception:  # noqa: BLE001
+                continue
+            data = (sec.get("data") or {}).get(lic.SECRET_KEY)
+            if data:
+                return base64.b64decode(data).decode()
+            sd = (sec.get("stringData") or {}).get(lic.SECRET_KEY)
+            if sd:
+                return sd
+        return os.environ.get("OMNIA_LICENSE")
+
+    return lic.Validator(public_key_pem, secret_reader=read)
+
+
 def agentruntime_webhook(obj, old):
     errs = []
+    if _LICENSE is not None:
+        from ..ee import license as lic
+
+        errs += lic.gate_agentruntime(obj["spec"], _LICENSE.get_or_default())
     for f in ("inputSchema", "outputSchema"):
         sch = obj["spec"].get(f)
         if sch is not None:

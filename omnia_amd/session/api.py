@@ -54,8 +54,20 @@ class MemoryPublisher:
 
 def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400.0,
               tokens: dict | None = None, allowed_namespaces: set | None = None,
-              redactor=None, optout=None) -> web.Application:
+              redactor=None, optout=None, audit_logger=None) -> web.Application:
+    """``audit_logger`` (EE, :class:`omnia_amd.ee.audit.AuditLogger`): record
+    session created/accessed/searched/deleted events and serve them at
+    ``/api/v1/audit/sessions`` (reference session-api audit wiring)."""
     limiter = KeyedLimiter(rate, burst)
+
+    def audit(request, event, **kw):
+        if audit_logger is None:
+            return
+        from ..ee.audit import Entry
+
+        audit_logger.log_event(Entry(event, ipAddress=request.remote or "",
+                                     userAgent=request.headers.get("User-Agent", ""),
+                                     userId=request.headers.get("x-omnia-user-id", ""), **kw))
 
     @web.middleware
     async def guard(request, handler):
@@ -90,6 +102,8 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         if optout is not None and optout(s):
             return web.Response(status=204)
         s = svc.create(s)
+        audit(request, "session_created", sessionId=s.id, agentName=s.agent_name,
+              namespace=s.namespace)
         return web.json_response(s.to_json(), status=201)
 
     async def list_sessions(request):
@@ -107,10 +121,13 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         q = request.query
         rows = svc.warm.list_sessions(namespace=q.get("namespace"), agent=q.get("agent"),
                                       q=q.get("q", ""), limit=int(q.get("limit", 50)))
+        audit(request, "session_searched", query=q.get("q", ""), resultCount=len(rows),
+              namespace=q.get("namespace") or "")
         return web.json_response({"sessions": [s.to_json() for s in rows]})
 
     async def get(request):
         sid = request.match_info["id"]
+        audit(request, "session_accessed", sessionId=sid)
         try:
             v = svc.get(sid, with_messages=False)
         except TierError:
@@ -227,7 +244,10 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
 
     async def delete(request):
         sid = request.match_info["id"]
-        return web.Response(status=204) if svc.delete(sid) else nf(sid)
+        if svc.delete(sid):
+            audit(request, "session_deleted", sessionId=sid)
+            return web.Response(status=204)
+        return nf(sid)
 
     async def bulk_delete(request):
         ns = request.query.get("namespace")
@@ -250,6 +270,10 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         return web.json_response({"sessions_deleted": n, "errors": []})
 
     r.add_get("/healthz", healthz)
+    if audit_logger is not None:
+        from ..ee.audit import mount_routes
+
+        mount_routes(app, audit_logger)
     r.add_post("/api/v1/sessions", create)
     r.add_get("/api/v1/sessions", list_sessions)
     r.add_delete("/api/v1/sessions", bulk_delete)
@@ -291,6 +315,9 @@ def main(argv=None):
     ap.add_argument("--cold-dir", default="")
     ap.add_argument("--redis-url", default="")
     ap.add_argument("--ttl", type=float, default=24 * 3600)
+    ap.add_argument("--audit-db", default="", help="EE: enable the audit log (SQLite path)")
+    ap.add_argument("--audit-retention-days", type=int, default=0)
+    ap.add_argument("--audit-hub", default="", help="EE: privacy-api URL to forward audit to")
     a = ap.parse_args(argv)
     cold = ColdArchive(LocalBlobStore(a.cold_dir)) if a.cold_dir else None
     pub = None
@@ -299,7 +326,34 @@ def main(argv=None):
 
         pub = StreamPublisher(RedisClient(a.redis_url))
     svc = TieredSessionService(HotCache(), WarmStore(a.db), cold, a.ttl, pub)
-    web.run_app(build_app(svc), port=a.port)
+    audit_logger = None
+    app_kw = {}
+    if a.audit_db:
+        from ..ee.audit import AuditLogger, Forwarder
+
+        audit_logger = AuditLogger(a.audit_db, retention_days=a.audit_retention_days)
+        app_kw["audit_logger"] = audit_logger
+    app = build_app(svc, **app_kw)
+    if audit_logger is not None and a.audit_hub:
+        fw = Forwarder(audit_logger, a.audit_hub)
+
+        async def forward_loop(_app):
+            async def loop():
+                import asyncio
+
+                while True:
+                    await fw.drain_once()
+                    audit_logger.delete_expired()
+                    await asyncio.sleep(10)
+
+            import asyncio
+
+            task = asyncio.create_task(loop())
+            yield
+            task.cancel()
+
+        app.cleanup_ctx.append(forward_loop)
+    web.run_app(app, port=a.port)
 
 
 if __name__ == "__main__":

@@ -74,6 +74,12 @@ class _WSWriter(Writer):
                 await self.ws.send_str(json.dumps(msg, separators=(",", ":")))
                 M.MESSAGES_SENT.labels(*self.labels).inc()
 
+    async def write_bytes(self, data: bytes) -> None:
+        async with self.lock:
+            if not self.ws.closed:
+                await self.ws.send_bytes(data)
+                M.MESSAGES_SENT.labels(*self.labels).inc()
+
 
 class FacadeServer:
     def __init__(self, cfg: FacadeConfig, handler=None, runtime_client=None,
@@ -87,6 +93,8 @@ class FacadeServer:
         self.connections = 0
         self.draining = False
         self.sessions: set = set()
+        self.audio_sessions = 0
+        self._caps: tuple[float, list] | None = None
         self.labels = (cfg.agent, cfg.namespace)
         self._conn_done = asyncio.Event()
         self.app = web.Application(client_max_size=cfg.max_message_bytes)
@@ -98,6 +106,19 @@ class FacadeServer:
         r.add_get("/readyz", self.readyz)
         r.add_get("/metrics", self.metrics)
         self.runner = None
+
+    async def duplex_available(self) -> bool:
+        """True when the runtime advertises ``duplex_audio`` (cached 30 s)."""
+        if self.client is None:
+            return False
+        now = time.monotonic()
+        if self._caps is None or now - self._caps[0] > 30.0:
+            try:
+                h = await self.client.health(timeout=2.0)
+                self._caps = (now, list(h.capabilities))
+            except Exception:  # noqa: BLE001
+                self._caps = (now, [])
+        return pb.CAP_DUPLEX_AUDIO in self._caps[1]
 
     # ---------------------------------------------------------------- health
     async def healthz(self, request):
@@ -269,6 +290,27 @@ class _Connection:
         self.media_bucket = TokenBucket(srv.cfg.media_rate, srv.cfg.media_burst)
         self.tasks: set = set()
         self.session_ensured = False
+        self.audio = None  # _AudioSession while a duplex call is up
+
+    async def on_audio(self, fr: dict):
+        if self.audio is None:
+            if self.srv.audio_sessions >= self.srv.cfg.max_audio_sessions:
+                M.RATE_LIMITED.labels("audio").inc()
+                await self.writer.write(P.error(self.session_id, P.E_RATE_LIMITED,
+                                                "audio session limit reached"))
+                return
+            self.audio = _AudioSession(self)
+            try:
+                await self.audio.start(fr.get("meta") or {})
+            except Exception as e:  # noqa: BLE001
+                self.audio = None
+                await self.writer.write(P.error(self.session_id, P.E_INVALID_MESSAGE,
+                                                f"audio session start failed: {e}"))
+                return
+        await self.audio.frame(fr)
+        if fr["flags"] & P.FLAG_LAST and not (fr["flags"] & P.FLAG_CHUNKED):
+            await self.audio.wait_closed()
+            self.audio = None
 
     async def read_loop(self):
         labels = self.srv.labels
@@ -302,6 +344,17 @@ class _Connection:
             await asyncio.gather(t, return_exceptions=True)
 
     async def on_binary(self, data: bytes):
+        try:
+            peek = P.decode_frame(data)
+        except ValueError as e:
+            await self.writer.write(P.error(self.session_id, P.E_INVALID_MESSAGE, str(e)))
+            return
+        # media-chunk frames are a duplex audio call when the runtime speaks it
+        # (reference: BinaryMessageTypeMediaChunk -> audio session); uploads stay uploads
+        if peek["type"] == P.TYPE_MEDIA_CHUNK and (self.audio is not None or
+                                                  await self.srv.duplex_available()):
+            await self.on_audio(peek)
+            return
         if not self.srv.cfg.media_enabled or self.srv.media is None:
             await self.writer.write(P.error(self.session_id, P.E_MEDIA_NOT_ENABLED,
                                             "media uploads are not enabled"))
@@ -434,3 +487,76 @@ class _Connection:
             M.REQUESTS_TOTAL.labels(*labels, status).inc()
             M.REQUEST_DURATION.labels(*labels).observe(time.perf_counter() - t0)
             tracing.end_span(span, error=status != "ok")
+
+
+class _AudioSession:
+    """One duplex call over the runtime's Converse stream (reference
+    ``internal/facade/audio_session.go``): DuplexStart from the first frame's
+    metadata, every inbound media-chunk frame -> AudioInputChunk, and the
+    runtime's frames relayed back (audio as binary media-chunk frames)."""
+
+    def __init__(self, conn: "_Connection"):
+        self.c = conn
+        self.stream = None
+        self.relay = None
+        self.media_seq = 0
+
+    async def start(self, meta: dict):
+        c = self.c
+        md = {"x-omnia-session-id": c.session_id, "x-omnia-agent-name": c.srv.cfg.agent}
+        self.stream = await c.srv.client.open(md)
+        await self.stream.send(pb.ClientMessage(session_id=c.session_id, duplex_start=pb.DuplexStart(
+            codec=meta.get("codec") or "pcm", sample_rate=int(meta.get("sample_rate") or 16000),
+            channels=int(meta.get("channels") or 1),
+            system_instruction=meta.get("system_instruction", ""))))
+        c.srv.audio_sessions += 1
+        self.relay = asyncio.get_running_loop().create_task(self._relay())
+
+    async def frame(self, fr: dict):
+        await self.stream.send(pb.ClientMessage(audio_input=pb.AudioInputChunk(
+            data=fr["payload"], sequence=fr["seq"],
+            is_last=bool(fr["flags"] & P.FLAG_LAST) and not (fr["flags"] & P.FLAG_CHUNKED))))
+
+    async def _relay(self):
+        c, sid, w = self.c, self.c.session_id, self.c.writer
+        try:
+            while True:
+                resp = await self.stream.recv()
+                if resp is None:
+                    return
+                kind = resp.WhichOneof("message")
+                if kind == "runtime_hello":
+                    m = resp.runtime_hello.media
+                    await w.write(P.server_msg(P.SESSION_CONFIG, sid, media={
+                        "codec": m.codec, "sample_rate": m.sample_rate, "channels": m.channels},
+                        capabilities=list(resp.runtime_hello.capabilities)))
+                elif kind == "chunk":
+                    await w.write(P.chunk(sid, resp.chunk.content, resp.chunk.role))
+                elif kind == "media_chunk":
+                    mc = resp.media_chunk
+                    fl = P.FLAG_LAST if mc.is_last else 0
+                    await w.write_bytes(P.encode_frame(
+                        P.TYPE_MEDIA_CHUNK, bytes(mc.data),
+                        {"session_id": sid, "mime_type": mc.mime_type}, mc.sequence,
+                        mc.media_id.encode()[:12], fl))
+                elif kind == "interruption":
+                    await w.write(P.server_msg(P.INTERRUPT, sid))
+                elif kind == "done":
+                    d = resp.done
+                    await w.write(P.done(sid, d.final_content, None, {
+                        "input_tokens": d.usage.input_tokens,
+                        "output_tokens": d.usage.output_tokens}))
+                elif kind == "error":
+                    await w.write(P.error(sid, resp.error.code or P.E_INTERNAL,
+                                          resp.error.message))
+                    return
+        finally:
+            c.srv.audio_sessions -= 1
+            await self.stream.close()
+
+    async def wait_closed(self, timeout: float = 120.0):
+        if self.relay is not None:
+            try:
+                await asyncio.wait_for(self.relay, timeout)
+            except asyncio.TimeoutError:
+                self.relay.cancel()

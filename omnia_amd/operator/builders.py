@@ -85,6 +85,8 @@ def runtime_config(ar: dict, pack: dict, providers: list[dict], registry: dict |
         extra_providers=[dict(p["spec"], name=p["metadata"]["name"]) for p in providers
                          if p is not llm],
         tools_config_path="/etc/omnia/tools")
+    if (spec.get("duplex") or {}).get("enabled"):
+        c.duplex = dict(spec["duplex"])
     d = pspec.get("defaults") or {}
     c.context_window = int(d.get("contextWindow", 0) or 0)
     c.truncation = d.get("truncationStrategy", "sliding")

@@ -110,7 +110,17 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
             engine = shared_engine(cfg.engine)
         provider = build_provider(cfg.provider or {"type": "mock"}, engine=engine)
     extra = {}
+    audio = {}
     for p in cfg.extra_providers:
+        role = (p.get("role") or "").lower()
+        if role in ("stt", "tts"):
+            from .duplex import build_audio_provider
+
+            try:
+                audio[role] = build_audio_provider(p, role)
+            except ValueError as e:
+                log.warning("%s provider skipped: %s", role, e)
+            continue
         try:
             extra[p.get("role", p.get("name", "extra"))] = build_provider(p, engine=engine)
         except ValueError as e:
@@ -164,7 +174,17 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
     M.RUNTIME_INFO.info({"agent": cfg.agent_name, "namespace": cfg.namespace,
                          "promptpack": pack.id, "promptpack_version": pack.version,
                          "provider": provider.type, "contract_version": "1.3.0"})
-    return RuntimeService(agent, capabilities=list(CAPABILITIES), invoke_agent=invoke_agent)
+    duplex = None
+    if "stt" in audio and "tts" in audio:
+        from .duplex import DuplexConfig
+
+        dcfg = cfg.duplex or {}
+        aud = dcfg.get("audio") or {}
+        duplex = DuplexConfig(audio["stt"], audio["tts"],
+                              sample_rate=int(aud.get("sampleRate", 16000)),
+                              codec=aud.get("codec", "pcm"), channels=int(aud.get("channels", 1)))
+    return RuntimeService(agent, capabilities=list(CAPABILITIES), invoke_agent=invoke_agent,
+                          duplex=duplex)
 
 
 async def run(cfg: RuntimeConfig | None = None):

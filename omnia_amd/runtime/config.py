@@ -31,7 +31,8 @@ class RuntimeConfig:
     context_url: str = ""
     context_ttl_s: int = 24 * 3600
     provider: dict = field(default_factory=lambda: {"type": "mock"})
-    extra_providers: list = field(default_factory=list)
+    extra_providers: list = field(default_factory=list)  # embedding / stt / tts / judge roles
+    duplex: dict = field(default_factory=dict)  # AgentRuntime spec.duplex (audio params)
     context_window: int = 0
     truncation: str = "sliding"
     tools_config_path: str = "/etc/omnia/tools"
@@ -79,6 +80,10 @@ class RuntimeConfig:
                       "baseURL": e.get("OMNIA_PROVIDER_BASE_URL", "")}
         if e.get("OMNIA_PROVIDER_JSON"):
             c.provider.update(json.loads(e["OMNIA_PROVIDER_JSON"]))
+        if e.get("OMNIA_EXTRA_PROVIDERS_JSON"):
+            c.extra_providers = json.loads(e["OMNIA_EXTRA_PROVIDERS_JSON"])
+        if e.get("OMNIA_DUPLEX_JSON"):
+            c.duplex = json.loads(e["OMNIA_DUPLEX_JSON"])
         if e.get("OMNIA_MOCK_CONFIG"):
             c.provider.setdefault("mock", {})["path"] = e["OMNIA_MOCK_CONFIG"]
         c.context_window = int(e.get("OMNIA_CONTEXT_WINDOW", "0") or 0)
@@ -117,6 +122,10 @@ class RuntimeConfig:
         }
         if self.context_url:
             env["OMNIA_CONTEXT_URL"] = self.context_url
+        if self.extra_providers:
+            env["OMNIA_EXTRA_PROVIDERS_JSON"] = json.dumps(self.extra_providers)
+        if self.duplex:
+            env["OMNIA_DUPLEX_JSON"] = json.dumps(self.duplex)
         if self.output_format:
             env["OMNIA_OUTPUT_FORMAT"] = self.output_format
         if self.output_schema is not None:

@@ -120,10 +120,15 @@ class _GrpcTurnIO(TurnIO):
 
 class RuntimeService:
     def __init__(self, agent: Agent, capabilities: list[str] | None = None,
-                 invoke_agent: Agent | None = None):
+                 invoke_agent: Agent | None = None, duplex=None):
         self.agent = agent
         self.invoke_agent = invoke_agent or agent
         self.capabilities = list(capabilities or CAPABILITIES)
+        self.duplex = duplex  # DuplexConfig when STT + TTS providers are configured
+        if duplex is not None:
+            for c in (pb.CAP_DUPLEX_AUDIO, pb.CAP_INTERRUPTION):
+                if c not in self.capabilities:
+                    self.capabilities.append(c)
         self.ready = True
         self.active_streams = 0
 
@@ -184,9 +189,16 @@ class RuntimeService:
                 if msg is None:
                     return
                 if msg.HasField("duplex_start"):
-                    await stream.send(pb.ServerMessage(error=pb.Error(
-                        code="DUPLEX_UNSUPPORTED",
-                        message="this runtime does not advertise duplex_audio")))
+                    if self.duplex is None:
+                        await stream.send(pb.ServerMessage(error=pb.Error(
+                            code="DUPLEX_UNSUPPORTED",
+                            message="this runtime does not advertise duplex_audio")))
+                        return
+                    from .duplex import DuplexSession
+
+                    sid = msg.session_id or md.get("x-omnia-session-id") or uuid.uuid4().hex
+                    await DuplexSession(self.agent, self.duplex, stream, sid,
+                                        identity_from_metadata(md, sid)).run(msg)
                     return
                 if not hello_sent:
                     await stream.send(pb.ServerMessage(runtime_hello=pb.RuntimeHello(

@@ -155,7 +155,7 @@ def dgemm_config(M: int, N: int, K: int, mode: int, force: bool | None = None
     wm = 1 if M <= 64 else 2 if M <= 128 else 4
     hit = _dgemm_tuned().get(f"{mode}:{dgemm_bucket(M)}:{N}:{K}")
     if hit is not None:
-        return (wm, hit[1], hit[2]) if hit[0] == wm else hit
+        return tuple(hit)
     if not (force if force is not None else _dgemm_force):
         return None
     wn = 2
@@ -168,7 +168,8 @@ def dgemm_config(M: int, N: int, K: int, mode: int, force: bool | None = None
     tiles = N // cols
     s = 1
     while (tiles * s < 256 and s < 8 and K % (64 * s * 2) == 0
-           and N * (s * 2) * 64 * wm * (1 if mode == 0 else 2) <= _DGEMM_WS_FLOATS):
+           and N * (s * 2) * 64 * wm * ((M + 64 * wm - 1) // (64 * wm))
+           * (1 if mode == 0 else 2) <= _DGEMM_WS_FLOATS):
         s *= 2
     return wm, wn, s
 

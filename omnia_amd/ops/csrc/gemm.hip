@@ -6,8 +6,9 @@
 // Why a hand kernel here: at M = 256 a GEMM is neither HBM- nor MFMA-bound by
 // itself -- the per-CU load path is the limit (every column tile re-reads the
 // whole x slab from L2).  The design answers that directly:
-//   * ONE M tile covers the whole batch (BM = 64*WM rows, WM in {1,2,4}), so
-//     every weight byte is streamed from HBM exactly once;
+//   * BM = 64*WM rows per tile (WM in {1,2,4}); with WM covering the batch
+//     every weight byte is streamed from HBM exactly once, with smaller WM the
+//     row tiles of one column tile run adjacently so the re-read hits L2;
 //   * wide column tiles (BN = 64*WN) keep the FLOP per staged byte high
 //     (BM*BN/(BM+BN) = 85 at 256x128);
 //   * split-K over S slices fills the 256 CUs when N/BN is small (QKV, O,
@@ -51,7 +52,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void dgemm_kernel(
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * BUF];
 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = bid / S, split = bid - tile * S;  // a tile's slices are adjacent
+  // block order: (column tile, row tile, k slice) -- a tile's slices and the row
+  // tiles that share its weight columns are adjacent, i.e. on one XCD's L2
+  const int mtiles = (M + BM - 1) / BM;
+  const int ntile = bid / (S * mtiles);
+  const int rem = bid - ntile * S * mtiles;
+  const int mt = rem / S, split = rem - mt * S;
+  const int tile = ntile * mtiles + mt;  // counter / slab index
+  const int m0 = mt * BM;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wn = w - wm * WN;
   const int Kb = K / S;
@@ -62,7 +70,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void dgemm_kernel(
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
     const int c = tid + i * NT, row = c >> 3, ch = c & 7;
-    const int r = row < M ? row : M - 1;  // rows past the batch recompute the last row
+    const int r = m0 + row < M ? m0 + row : M - 1;  // rows past the batch: clamped
     a_src[i] = X + (int64_t)r * K + kbeg + ch * 8;
     a_off[i] = swz(row, ch);
   }
@@ -73,10 +81,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void dgemm_kernel(
     const int c = tid + i * NT, row = c >> 3, ch = c & 7;
     int64_t wrow;
     if (MODE == 0) {
-      wrow = (int64_t)tile * BN + row;
+      wrow = (int64_t)ntile * BN + row;
     } else {
       const int wc = row >> 6, rr = row & 63;
-      const int64_t col0 = (int64_t)tile * (32 * WN) + wc * 32;
+      const int64_t col0 = (int64_t)ntile * (32 * WN) + wc * 32;
       wrow = rr < 32 ? col0 + rr : (int64_t)N + col0 + (rr - 32);
     }
     b_src[i] = W + wrow * K + kbeg + ch * 8;
@@ -129,22 +137,27 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void dgemm_kernel(
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
     }
   };
+  // Branch-free load/store schedule: every iteration issues its prefetch (the
+  // k offset is clamped at the tail, re-reading the last slice harmlessly) and
+  // writes its staging buffer, so hipcc can count vmcnt across the loop instead
+  // of draining every outstanding load before the next prefetch (which had
+  // serialised the k-steps on the full memory latency).
+  const int klast = (nk - 1) * 64;
   gload(ra0, rb0, 0);
-  if (nk > 1) gload(ra1, rb1, 64);
+  gload(ra1, rb1, min(64, klast));
   lstore(ra0, rb0, 0);
   __syncthreads();
-  // unrolled by two so each register set is static: even k-steps own set 0
   for (int kt = 0; kt < nk; kt += 2) {
-    if (kt + 2 < nk) gload(ra0, rb0, (kt + 2) * 64);
+    gload(ra0, rb0, min((kt + 2) * 64, klast));
     compute(0);
-    if (kt + 1 < nk) lstore(ra1, rb1, 1);
+    lstore(ra1, rb1, 1);
     __syncthreads();
-    if (kt + 1 >= nk) break;
-    if (kt + 3 < nk) gload(ra1, rb1, (kt + 3) * 64);
-    compute(1);
-    if (kt + 2 < nk) lstore(ra0, rb0, 0);
+    gload(ra1, rb1, min((kt + 3) * 64, klast));
+    if (kt + 1 < nk) compute(1);
+    lstore(ra0, rb0, 0);
     __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   if (S > 1) {
     // ---- in-launch split-K combine (release -> ticket -> acquire) ----
@@ -199,17 +212,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void dgemm_kernel(
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = wm * 64 + 16 * i + 4 * fq + r;
+      const int row = m0 + wm * 64 + 16 * i + 4 * fq + r;
       if (row >= M) continue;
       bf16_t* orow = out + (int64_t)row * ldo;
       if (MODE == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          orow[(int64_t)tile * BN + wn * 64 + 16 * j + fr] = f2bf(acc[i][j][r]);
+          orow[(int64_t)ntile * BN + wn * 64 + 16 * j + fr] = f2bf(acc[i][j][r]);
       } else {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
-          orow[(int64_t)tile * (32 * WN) + wn * 32 + 16 * jj + fr] =
+          orow[(int64_t)ntile * (32 * WN) + wn * 32 + 16 * jj + fr] =
               f2bf(silu(acc[i][jj][r]) * acc[i][jj + 2][r]);
       }
     }
@@ -220,7 +233,7 @@ template <int WM, int WN, int MODE>
 int launch(bf16_t* out, const bf16_t* X, const bf16_t* W, float* ws, int* cnt, int M, int N,
            int K, int S, int ldo, hipStream_t s) {
   const int cols = MODE == 0 ? 64 * WN : 32 * WN;
-  const int tiles = N / cols;
+  const int tiles = (N / cols) * ((M + 64 * WM - 1) / (64 * WM));
   dgemm_kernel<WM, WN, MODE><<<tiles * S, 64 * WM * WN, 0, s>>>(out, X, W, ws, cnt, M, N, K, S,
                                                                  ldo);
   return (int)hipGetLastError();
@@ -249,11 +262,11 @@ int omnia_dgemm(int mode, void* out, const void* X, const void* W, float* ws, in
                 int N, int K, int S, int wm, int wn, int ldo, int64_t ws_floats, int cnt_len,
                 hipStream_t s) {
   if (mode != 0 && mode != 1) return -1;
-  if (M < 1 || M > 64 * wm) return -2;
+  if (M < 1 || M > 256) return -2;
   if (S < 1 || K % (64 * S)) return -3;
   const int cols = mode == 0 ? 64 * wn : 32 * wn;
   if (N % cols) return -4;
-  const int tiles = N / cols;
+  const int tiles = (N / cols) * ((M + 64 * wm - 1) / (64 * wm));
   if (S > 1) {
     if (tiles > cnt_len) return -5;
     if ((int64_t)tiles * S * (64 * wm) * (64 * wn) > ws_floats) return -6;

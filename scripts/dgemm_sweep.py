@@ -78,16 +78,17 @@ def main():
                     ops.silu_mul(y)
 
             t_lib = timeit(lib, a.iters)
-            wm = 1 if M <= 64 else 2 if M <= 128 else 4
+            wm_max = 1 if M <= 64 else 2 if M <= 128 else 4
             res = []
-            for wn in (1, 2, 4):
-                if wm * wn > 8:
-                    continue
+            for wm, wn in [(a, b) for a in (1, 2, 4) for b in (1, 2, 4)
+                           if a <= wm_max and a * b <= 8]:
+                mt = (M + 64 * wm - 1) // (64 * wm)
                 cols = 64 * wn if mode == 0 else 32 * wn
                 if N % cols:
                     continue
                 for s in (1, 2, 4, 8):
-                    if K % (64 * s) or (s > 1 and (N // cols) * s * 64 * wm * 64 * wn > ws.numel()):
+                    if K % (64 * s) or (s > 1 and mt * (N // cols) * s * 64 * wm * 64 * wn
+                                        > ws.numel()):
                         continue
                     out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
                     kk.dgemm(mode, out, x, Ws[0], ws, cnt, s, wm, wn)
@@ -108,8 +109,8 @@ def main():
                 gbs = wbytes / (t * 1e-6) / 1e9
                 rows.append((name, M, t_lib, t, wn_, s_, gbs, wbytes / (t_lib * 1e-6) / 1e9))
                 print(f"{name:13s} M={M:3d}  lib {t_lib:8.1f} us ({rows[-1][7]:6.0f} GB/s)  "
-                      f"dgemm {t:8.1f} us ({gbs:6.0f} GB/s) wn={wn_} S={s_}  "
-                      f"x{t_lib / t:5.2f}  top3={[(round(r[0], 1), r[2], r[3]) for r in res[:3]]}",
+                      f"dgemm {t:8.1f} us ({gbs:6.0f} GB/s) wm={wm_} wn={wn_} S={s_}  "
+                      f"x{t_lib / t:5.2f}  top3={[(round(r[0], 1), r[1], r[2], r[3]) for r in res[:3]]}",
                       flush=True)
         del Ws
         torch.cuda.empty_cache()

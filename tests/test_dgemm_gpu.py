@@ -101,3 +101,10 @@ def test_rejects_bad_shapes():
     o = torch.empty(16, 128, device=DEV, dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         ops.kernels().dgemm(0, o, x, w, ws, cnt, 2, 1, 2)  # K % (64*S)
+
+
+@pytest.mark.parametrize("wm,S,M", [(1, 1, 256), (2, 2, 200), (1, 4, 130), (2, 1, 129)])
+def test_multiple_row_tiles(wm, S, M):
+    for mode in (0, 1):
+        o, r = _run(mode, M, 512, 1024, S, wm, 2)
+        _check(o, r)

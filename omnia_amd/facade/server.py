@@ -433,10 +433,15 @@ class _Connection:
             self.session_id = sid
         if not self.session_ensured and srv.recorder is not None:
             try:
+                from ..operator.authz import pseudonymize_id
+
+                # recorded sessions carry the pseudonym, never the raw user id
+                # (pkg/identity: facade ingestion and dashboard queries agree)
                 await srv.recorder.ensure_session(self.session_id, srv.cfg.agent,
                                                   srv.cfg.namespace,
-                                                  {"user": self.ident.end_user or
-                                                   self.ident.subject})
+                                                  {"user": pseudonymize_id(
+                                                      self.ident.end_user or
+                                                      self.ident.subject or "")})
             except Exception as e:  # noqa: BLE001
                 log.warning("session ensure failed: %s", e)
         self.session_ensured = True

@@ -9,6 +9,8 @@ single-node operator).  Paths follow the K8s conventions:
 """
 from __future__ import annotations
 
+import os
+
 import json
 
 from aiohttp import web
@@ -35,7 +37,20 @@ def kind_of(plural: str) -> str:
 def build_app(store: APIStore) -> web.Application:
     from .restapi import mount
 
-    app = web.Application()
+    middlewares = []
+    jwks_path = os.environ.get("OMNIA_DASHBOARD_JWKS_FILE", "")
+    if jwks_path:
+        # dashboard-minted identity tokens guard the workspace content API (C18 authz)
+        import json
+
+        from .authz import IdentityVerifier, authz_middleware
+
+        with open(jwks_path) as f:
+            jwks = json.load(f)
+        middlewares.append(authz_middleware(IdentityVerifier(
+            jwks, issuer=os.environ.get("OMNIA_DASHBOARD_ISSUER", ""),
+            audience=os.environ.get("OMNIA_DASHBOARD_AUDIENCE", "")), store))
+    app = web.Application(middlewares=middlewares)
     mount(app, store)  # specific routes first: the generic resource routes below are greedy
 
     def err(status, msg):

@@ -395,10 +395,21 @@ class AgentRuntimeReconciler:
             store.delete("Deployment", name + "-candidate", ns)
         st["rollout"] = ros
         active = ros["phase"] == "Progressing"
+        from . import rollout_routing
+
+        traffic = rollout_routing.apply(store, ar, int(ros["weight"]), active)
+        ros["traffic"] = traffic
+        if traffic["trafficRoutingMode"] == "replica-weighted" and active:
+            cand = store.try_get("Deployment", name + "-candidate", ns)
+            if cand is not None and cand["spec"].get("replicas") != traffic["candidateReplicas"]:
+                cand["spec"]["replicas"] = traffic["candidateReplicas"]
+                store.apply(cand)
         set_condition(st, "RolloutActive", active, ros["phase"], f"weight={ros['weight']}",
                       md["generation"])
-        set_condition(st, "TrafficRouting", True, "WeightedService", f"candidate={ros['weight']}%",
-                      md["generation"])
+        set_condition(st, "TrafficRouting", not traffic.get("degraded"),
+                      {"mesh": "MeshWeighted", "external": "IstioPatched"}.get(
+                          traffic["trafficRoutingMode"], "ReplicaWeighted"),
+                      f"candidate={traffic['deliveredWeight']}%", md["generation"])
         return 1.0 if active else None
 
     def _analysis(self, store, ns, a):

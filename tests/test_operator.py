@@ -280,3 +280,68 @@ def test_canary_rollout_steps_and_promotion():
     assert "candidate" in seen and 20 in seen
     assert a["status"]["rollout"]["phase"] == "Promoted" and a["status"]["rollout"]["weight"] == 100
     assert cand is None  # candidate folded into stable after promotion
+
+
+def test_rollout_traffic_routing_modes(monkeypatch):
+    from omnia_amd.operator import rollout_routing as RR
+
+    assert RR.resolve_mode(None, False) == ("replica-weighted", False)
+    assert RR.resolve_mode({"mode": "mesh"}, False) == ("replica-weighted", True)
+    assert RR.resolve_mode({"istio": {"virtualService": {"name": "v"}}}, True) == \
+        ("external", False)
+    assert RR.split_replicas(4, 20) == (3, 1) and RR.split_replicas(4, 60) == (1, 3)
+    assert RR.split_replicas(3, 0) == (3, 0) and RR.split_replicas(3, 100) == (0, 3)
+
+    def run(routing, mesh):
+        if mesh:
+            monkeypatch.setenv("OMNIA_MESH_ENABLED", "1")
+        else:
+            monkeypatch.delenv("OMNIA_MESH_ENABLED", raising=False)
+        docs = load_manifests([ECHO])
+        for d in docs:
+            if d["kind"] == "AgentRuntime":
+                d["spec"]["rollout"] = {"candidate": {"promptPackVersion": "1.0.0"},
+                                        "steps": [{"setWeight": 30}, {"pause": {"duration": "1h"}}],
+                                        "trafficRouting": routing}
+                d["spec"].setdefault("runtime", {})["replicas"] = 4
+        extra = []
+        if routing.get("istio"):
+            extra = [{"apiVersion": RR.ISTIO_API, "kind": "VirtualService",
+                      "metadata": {"name": "echo-vs", "namespace": "default"},
+                      "spec": {"http": [{"name": "primary", "route": [
+                          {"destination": {"host": "echo", "subset": "stable"}, "weight": 100},
+                          {"destination": {"host": "echo", "subset": "canary"}, "weight": 0}]}]}},
+                     {"apiVersion": RR.ISTIO_API, "kind": "DestinationRule",
+                      "metadata": {"name": "echo-dr", "namespace": "default"}, "spec": {}}]
+
+        async def go():
+            store, mgr, _ = await _run_operator(docs + extra)
+            for _ in range(60):
+                ro = store.get("AgentRuntime", "echo")["status"].get("rollout") or {}
+                if ro.get("weight") == 30 and ro.get("traffic"):
+                    break
+                await asyncio.sleep(0.1)
+            await mgr.settle(timeout=5)
+            out = (store.get("AgentRuntime", "echo")["status"]["rollout"],
+                   store.try_get("VirtualService", "echo-rollout"),
+                   store.try_get("VirtualService", "echo-vs"),
+                   store.try_get("DestinationRule", "echo-dr"),
+                   store.try_get("Deployment", "echo-candidate"))
+            await mgr.stop()
+            return out
+
+        return asyncio.run(go())
+
+    ro, owned, _, _, cand = run({"mode": "mesh"}, True)
+    assert ro["traffic"]["trafficRoutingMode"] == "mesh"
+    w = [r["weight"] for r in owned["spec"]["http"][0]["route"]]
+    assert w == [70, 30]
+    ro, owned, _, _, cand = run({}, False)
+    assert ro["traffic"]["trafficRoutingMode"] == "replica-weighted" and owned is None
+    assert ro["traffic"]["candidateReplicas"] == 2 and cand["spec"]["replicas"] == 2
+    ro, _, vs, dr, _ = run({"istio": {"virtualService": {"name": "echo-vs", "routes": ["primary"]},
+                                      "destinationRule": {"name": "echo-dr"}}}, False)
+    assert ro["traffic"]["trafficRoutingMode"] == "external"
+    assert [r["weight"] for r in vs["spec"]["http"][0]["route"]] == [70, 30]
+    assert dr["spec"]["trafficPolicy"]["loadBalancer"]["consistentHash"]["httpHeaderName"] == \
+        "x-omnia-session-id"

@@ -8,6 +8,7 @@ results, evaluate ``loadTest.thresholds`` and write ``status``
 from __future__ import annotations
 
 import asyncio
+import json
 import logging
 import time
 
@@ -44,6 +45,40 @@ def load_arena_config(store, job: dict) -> dict:
 
     with open(os.path.join(path, fname)) as f:
         return yaml.safe_load(f) or {}
+
+
+def write_dataset(records: list[dict], fmt: str, path: str | None, job: str) -> dict:
+    """Serialise datagen records as json / jsonl / csv (``DataGenSettings.format``)."""
+    import csv
+    import io
+    import os
+
+    records = sorted(records, key=lambda r: str(r.get("id")))
+    fmt = (fmt or "jsonl").lower()
+    if fmt == "json":
+        body = json.dumps(records, indent=1)
+    elif fmt == "csv":
+        buf = io.StringIO()
+        w = csv.DictWriter(buf, fieldnames=["id", "scenario", "input", "output", "variables"])
+        w.writeheader()
+        for r in records:
+            w.writerow({**{k: r.get(k) for k in ("id", "scenario", "input", "output")},
+                        "variables": json.dumps(r.get("variables") or {})})
+        body = buf.getvalue()
+    elif fmt == "jsonl":
+        body = "".join(json.dumps(r) + "\n" for r in records)
+    else:
+        raise ValueError(f"unsupported datagen format {fmt!r}")
+    out = {"records": len(records), "format": fmt}
+    if path:
+        os.makedirs(path, exist_ok=True)
+        fn = os.path.join(path, f"{job}.{fmt}")
+        with open(fn, "w") as f:
+            f.write(body)
+        out["path"] = fn
+    else:
+        out["inline"] = body
+    return out
 
 
 class ArenaJobController:
@@ -83,8 +118,14 @@ class ArenaJobController:
             p = dict(p)
             if p.get("mode") == "direct":
                 p["object"] = self.provider_objects[p["id"]]
+            if p.get("persona"):
+                p["persona_object"] = self.provider_objects[p["persona"]]
             providers[p["id"]] = p
-        items = partition(md["name"], scenarios, providers, int(spec.get("trials") or 1))
+        job_type = spec.get("type", "evaluation")
+        trials = int(spec.get("trials") or 1)
+        if job_type == "datagen":
+            trials = int((spec.get("dataGen") or {}).get("count") or 100)
+        items = partition(md["name"], scenarios, providers, trials)
         await self.q.enqueue(items)
         lt = spec.get("loadTest") or {}
         ramp = lt.get("ramp") or {}
@@ -98,7 +139,8 @@ class ArenaJobController:
                                LoadProfile(max(1, conc // replicas),
                                            float(ramp.get("upSeconds") or 0),
                                            float(ramp.get("downSeconds") or 0)),
-                               budget=budget / replicas if budget else None)
+                               budget=budget / replicas if budget else None,
+                               job_type=job_type)
                    for _ in range(replicas)]
         await asyncio.gather(*(w.run() for w in workers))
         wall = time.perf_counter() - t0
@@ -111,12 +153,18 @@ class ArenaJobController:
         tstats = JobStats.from_results(turn_results, wall) if turn_results else stats
         stats.latencies_ms, stats.ttfts_ms = tstats.latencies_ms, tstats.ttfts_ms
         verdicts, ok = evaluate(lt.get("thresholds") or [], stats)
+        dataset = None
+        if job_type == "datagen":
+            dataset = write_dataset([r["record"] for r in results if r.get("record")],
+                                    (spec.get("dataGen") or {}).get("format", "jsonl"),
+                                    (spec.get("output") or {}).get("path"), md["name"])
         phase = "Succeeded" if ok and stats.errors < max(1, stats.total) else "Failed"
         job = self.store.get("ArenaJob", md["name"], md.get("namespace", "default"))
         self._status(job, phase, progress={"total": len(items), "done": len(results)},
                      results=stats.to_json(), thresholds=[str(v) for v in verdicts],
                      completionTime=time.time(), message="thresholds " + (
-                         "passed" if ok else "failed"))
+                         "passed" if ok else "failed"),
+                     **({"dataset": dataset} if dataset else {}))
         return stats
 
 

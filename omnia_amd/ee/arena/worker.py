@@ -71,6 +71,109 @@ async def run_direct(item: WorkItem, scenario: dict, provider: dict) -> dict:
     return _summarise(turns)
 
 
+async def _complete(prov, msgs, params, sid, source: str, calls: list) -> tuple[str, float, float]:
+    """One provider call -> (text, ttft_s, latency_s), recorded in ``calls``."""
+    t0 = time.perf_counter()
+    ttft, text, usage = None, [], None
+    async for ev in prov.stream(msgs, [], params, session_id=sid):
+        if ev.type == "text":
+            if ttft is None:
+                ttft = time.perf_counter() - t0
+            text.append(ev.text)
+        elif ev.type == "error":
+            raise RuntimeError(ev.text)
+        elif ev.type == "done":
+            usage = ev.usage
+    lat = time.perf_counter() - t0
+    calls.append({"source": source, "provider": getattr(prov, "name", ""),
+                  "model": getattr(prov, "model", ""), "latency_ms": lat * 1e3,
+                  "output_tokens": getattr(usage, "output_tokens", 0) if usage else 0})
+    return "".join(text), (ttft or lat), lat
+
+
+async def run_selfplay(item: WorkItem, scenario: dict, provider: dict) -> dict:
+    """Self-play (reference ``selfplay_capture.go`` + PromptKit personas): a
+    persona model plays the USER -- it sees the conversation with roles swapped
+    and its persona prompt (goals, constraints, style) as system -- against the
+    agent under test, for ``max_turns`` exchanges or until the persona emits
+    ``[DONE]``.  Provider calls are tagged ``agent`` / ``selfplay``."""
+    from ...engine.sampling_params import SamplingParams
+    from ...runtime.chat import Message
+
+    sp = scenario.get("self_play") or {}
+    agent, persona = provider["object"], provider["persona_object"]
+    params = SamplingParams(**(provider.get("params") or {"temperature": 0.0,
+                                                         "max_tokens": 128}))
+    pp = sp.get("persona") or {}
+    persona_sys = pp.get("system_prompt") or (
+        f"You are role-playing a user. {pp.get('description', '')} Goals: "
+        f"{'; '.join(pp.get('goals') or [])}. Constraints: "
+        f"{'; '.join(pp.get('constraints') or [])}. Style: {pp.get('style', 'concise')}. "
+        "Reply with only the user's next message, or [DONE] when the goals are met.")
+    sid = f"arena-sp-{item.id}"
+    agent_msgs = [Message("system", scenario.get("system", "You are a helpful assistant."))]
+    persona_msgs = [Message("system", persona_sys)]
+    opener = sp.get("opening_message") or (scenario.get("turns") or [{}])[0].get("user")
+    calls, turns = [], []
+    user = opener
+    for i in range(int(sp.get("max_turns", 4))):
+        if user is None:
+            user, _, _ = await _complete(persona, persona_msgs, params, sid + "-u",
+                                         "selfplay", calls)
+        user = user.strip()
+        if not user or "[DONE]" in user:
+            break
+        agent_msgs.append(Message("user", user))
+        persona_msgs.append(Message("assistant", user))
+        reply, ttft, lat = await _complete(agent, agent_msgs, params, sid, "agent", calls)
+        agent_msgs.append(Message("assistant", reply))
+        persona_msgs.append(Message("user", reply))  # roles swapped for the persona
+        turns.append({"user": user, "content": reply, "ttft_ms": ttft * 1e3,
+                      "latency_ms": lat * 1e3, "usage": {},
+                      "assertions": [evaluate(a, user, reply)
+                                     for a in sp.get("assertions", [])]})
+        user = None
+    out = _summarise(turns)
+    out["transcript"] = [{"user": t["user"], "assistant": t["content"]} for t in turns]
+    out["provider_calls"] = calls
+    return out
+
+
+def _render(template: str, variables: dict) -> str:
+    for k, v in variables.items():
+        template = template.replace("{{" + k + "}}", str(v)).replace("{{ " + k + " }}", str(v))
+    return template
+
+
+async def run_datagen(item: WorkItem, scenario: dict, provider: dict) -> dict:
+    """Data generation (ArenaJob type ``datagen``): render the scenario's prompt
+    template with variables sampled deterministically per item, run it through
+    the provider, return the (input, output) record."""
+    import random
+
+    from ...engine.sampling_params import SamplingParams
+    from ...runtime.chat import Message
+
+    rng = random.Random(f"{item.job_id}:{item.id}")
+    choices = scenario.get("variables") or {}
+    variables = {k: (rng.choice(v) if isinstance(v, list) and v else v)
+                 for k, v in choices.items()}
+    prompt = _render(scenario.get("prompt") or (scenario.get("turns") or [{}])[0].get(
+        "user", ""), variables)
+    params = SamplingParams(**(provider.get("params") or {"temperature": 0.7,
+                                                         "max_tokens": 128}))
+    msgs = [Message("system", scenario.get("system", "You generate training data.")),
+            Message("user", prompt)]
+    calls: list = []
+    text, ttft, lat = await _complete(provider["object"], msgs, params, f"dg-{item.id}",
+                                      "datagen", calls)
+    return {"passed": True, "latency_ms": lat * 1e3, "ttft_ms": ttft * 1e3,
+            "turns": [{"latency_ms": lat * 1e3, "ttft_ms": ttft * 1e3}],
+            "output_tokens": calls[0]["output_tokens"], "cost": 0.0, "assertions": [],
+            "record": {"id": item.id, "scenario": item.scenario_id, "variables": variables,
+                       "input": prompt, "output": text}}
+
+
 def _summarise(turns: list[dict]) -> dict:
     checks = [a for t in turns for a in t["assertions"] if not a.get("skipped")]
     out_tok = sum(int((t.get("usage") or {}).get("output_tokens") or
@@ -88,7 +191,8 @@ def _summarise(turns: list[dict]) -> dict:
 class ArenaWorker:
     def __init__(self, queue, job_id: str, scenarios: dict, providers: dict,
                  profile: LoadProfile, budget: float | None = None,
-                 consumer: str | None = None, visibility_s: float = 300.0):
+                 consumer: str | None = None, visibility_s: float = 300.0,
+                 job_type: str = "evaluation"):
         self.q = queue
         self.job = job_id
         self.scenarios = scenarios
@@ -97,6 +201,7 @@ class ArenaWorker:
         self.budget = budget
         self.consumer = consumer or f"worker-{os.getpid()}-{uuid.uuid4().hex[:6]}"
         self.visibility_s = visibility_s
+        self.job_type = job_type
         self.spent = 0.0
         self.active = 0
         self.done = 0
@@ -105,7 +210,12 @@ class ArenaWorker:
         scen = self.scenarios[item.scenario_id]
         prov = self.providers[item.provider_id]
         try:
-            fn = run_fleet if prov.get("mode", "fleet") == "fleet" else run_direct
+            if self.job_type == "datagen":
+                fn = run_datagen
+            elif scen.get("self_play"):
+                fn = run_selfplay
+            else:
+                fn = run_fleet if prov.get("mode", "fleet") == "fleet" else run_direct
             res = await fn(item, scen, prov)
             res.update(scenario=item.scenario_id, provider=item.provider_id,
                        attempt=item.attempt)

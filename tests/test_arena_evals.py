@@ -162,3 +162,95 @@ def test_eval_worker_sampling_and_writeback():
     posted, stats = asyncio.run(go())
     assert {(p["evalId"], p["passed"]) for p in posted} == {("has4", True), ("short", False)}
     assert stats["skipped"] == 1  # the user message
+
+
+class _Echo:
+    """Direct-mode provider: echoes a transform of the last user message."""
+
+    def __init__(self, name, fn):
+        self.name, self.model, self.fn = name, name + "-model", fn
+
+    async def stream(self, msgs, tools, params, session_id=None, metadata=None):
+        from omnia_amd.runtime.providers import ProviderEvent, Usage
+
+        last = [m for m in msgs if m.role == "user"][-1].content
+        yield ProviderEvent("text", text=self.fn(last, msgs))
+        yield ProviderEvent("done", usage=Usage(input_tokens=1, output_tokens=2))
+
+
+def _job_store(arena, spec):
+    import yaml
+
+    from omnia_amd.operator.apistore import APIStore
+
+    store = APIStore()
+    store.create({"apiVersion": "v1", "kind": "ConfigMap",
+                  "metadata": {"name": "arena-cfg", "namespace": "default"},
+                  "data": {"config.arena.yaml": yaml.safe_dump(arena)}})
+    store.create({"apiVersion": "omnia.altairalabs.ai/v1alpha1", "kind": "ArenaSource",
+                  "metadata": {"name": "src", "namespace": "default"},
+                  "spec": {"type": "configmap", "interval": "5m",
+                           "configMap": {"name": "arena-cfg"}}})
+    store.create({"apiVersion": "omnia.altairalabs.ai/v1alpha1", "kind": "ArenaJob",
+                  "metadata": {"name": "j", "namespace": "default"},
+                  "spec": {"sourceRef": {"name": "src"}, **spec}})
+    return store
+
+
+def test_arena_datagen_job(tmp_path):
+    import json
+
+    arena = {"scenarios": [{"id": "faq", "prompt": "Write a question about {{topic}}.",
+                            "variables": {"topic": ["GPUs", "HBM", "xGMI"]}}],
+             "providers": [{"id": "gen", "mode": "direct"}]}
+    gen = _Echo("gen", lambda u, m: "Q: " + u)
+
+    async def go():
+        store = _job_store(arena, {"type": "datagen", "dataGen": {"count": 6, "format": "jsonl"},
+                                   "output": {"path": str(tmp_path)}})
+        ctl = ArenaJobController(store, MemoryQueue(), provider_objects={"gen": gen})
+        await ctl.reconcile("default", "j")
+        await ctl.tasks["j"]
+        return store.get("ArenaJob", "j", "default")["status"]
+
+    st = asyncio.run(go())
+    assert st["phase"] == "Succeeded" and st["dataset"]["records"] == 6
+    lines = [json.loads(x) for x in open(st["dataset"]["path"])]
+    assert len(lines) == 6
+    assert all(r["output"] == "Q: " + r["input"] for r in lines)
+    assert {r["variables"]["topic"] for r in lines} <= {"GPUs", "HBM", "xGMI"}
+    assert all("{{" not in r["input"] for r in lines)
+
+
+def test_arena_selfplay_persona():
+    turns = {"n": 0}
+
+    def persona_fn(last, msgs):
+        turns["n"] += 1
+        return "[DONE]" if turns["n"] > 2 else f"follow-up {turns['n']} about {last[:10]}"
+
+    agent = _Echo("agent", lambda u, m: "answer to " + u)
+    persona = _Echo("persona", persona_fn)
+    arena = {"scenarios": [{"id": "sp", "self_play": {
+        "opening_message": "hello, I need help with my bill",
+        "persona": {"description": "an annoyed customer", "goals": ["get a refund"]},
+        "max_turns": 6,
+        "assertions": [{"type": "contains", "params": {"value": "answer"}}]}}],
+        "providers": [{"id": "agent", "mode": "direct", "persona": "persona"}]}
+
+    async def go():
+        store = _job_store(arena, {"type": "evaluation"})
+        ctl = ArenaJobController(store, MemoryQueue(),
+                                 provider_objects={"agent": agent, "persona": persona})
+        await ctl.reconcile("default", "j")
+        await ctl.tasks["j"]
+        res = await ctl.q.results_of("j")
+        return store.get("ArenaJob", "j", "default")["status"], res
+
+    st, res = asyncio.run(go())
+    assert st["phase"] == "Succeeded", st
+    r = res[0]
+    assert [t["user"] for t in r["transcript"]][0] == "hello, I need help with my bill"
+    assert len(r["transcript"]) == 3  # opener + 2 persona turns, then [DONE]
+    assert {c["source"] for c in r["provider_calls"]} == {"agent", "selfplay"}
+    assert r["passed"]

@@ -194,6 +194,208 @@ class VaultTransitKMS:
         pass
 
 
+# ------------------------------------------------------------------ cloud KMS (REST, no SDKs)
+def sigv4_headers(method: str, url: str, body: bytes, region: str, service: str,
+                  access_key: str, secret_key: str, session_token: str = "",
+                  extra: dict | None = None, now=None) -> dict:
+    """AWS Signature V4 Authorization header for a request (header form)."""
+    import datetime as dt
+    import hashlib
+    import hmac
+    import urllib.parse
+
+    u = urllib.parse.urlsplit(url)
+    t = now or dt.datetime.now(dt.timezone.utc)
+    amz_date, day = t.strftime("%Y%m%dT%H%M%SZ"), t.strftime("%Y%m%d")
+    hdrs = {"host": u.netloc, "x-amz-date": amz_date, **{k.lower(): v for k, v in
+                                                         (extra or {}).items()}}
+    if session_token:
+        hdrs["x-amz-security-token"] = session_token
+    signed = ";".join(sorted(hdrs))
+    canon_h = "".join(f"{k}:{hdrs[k].strip()}\n" for k in sorted(hdrs))
+    creq = "\n".join([method, u.path or "/", u.query, canon_h, signed,
+                      hashlib.sha256(body).hexdigest()])
+    scope = f"{day}/{region}/{service}/aws4_request"
+    sts = "\n".join(["AWS4-HMAC-SHA256", amz_date, scope,
+                     hashlib.sha256(creq.encode()).hexdigest()])
+
+    def h(k, m):
+        return hmac.new(k, m.encode(), hashlib.sha256).digest()
+
+    k = h(h(h(h(("AWS4" + secret_key).encode(), day), region), service), "aws4_request")
+    sig = hmac.new(k, sts.encode(), hashlib.sha256).hexdigest()
+    out = {k2: v for k2, v in hdrs.items() if k2 != "host"}
+    out["Authorization"] = (f"AWS4-HMAC-SHA256 Credential={access_key}/{scope}, "
+                            f"SignedHeaders={signed}, Signature={sig}")
+    return out
+
+
+class _WrappingKMS:
+    """Common envelope logic: a fresh DEK per record, wrapped by the cloud key."""
+
+    key_id = "kms"
+
+    def _wrap(self, dek: bytes) -> tuple[bytes, str]:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def _unwrap(self, edk: bytes) -> bytes:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def encrypt(self, plaintext: bytes) -> EncryptOutput:
+        dek = os.urandom(32)
+        edk, ver = self._wrap(dek)
+        return EncryptOutput(_pack(self.key_id, ver, edk, seal(dek, plaintext)), self.key_id,
+                             ver)
+
+    def decrypt(self, blob: bytes) -> bytes:
+        kid, _ver, edk, body = _unpack(blob)
+        if kid != self.key_id:
+            raise ValueError(f"envelope sealed under key {kid!r}, not {self.key_id!r}")
+        return open_(self._unwrap(edk), body)
+
+    def close(self):
+        pass
+
+    @staticmethod
+    def _post(url: str, body: dict, headers: dict, timeout: float = 10.0) -> dict:
+        import requests
+
+        r = requests.post(url, data=json.dumps(body).encode(), headers=headers, timeout=timeout)
+        if r.status_code >= 400:
+            raise RuntimeError(f"KMS {url}: HTTP {r.status_code} {r.text[:200]}")
+        return r.json() if r.text else {}
+
+
+class AWSKMS(_WrappingKMS):
+    """AWS KMS ``TrentService`` JSON API (Encrypt / Decrypt / DescribeKey /
+    RotateKeyOnDemand), SigV4-signed; credentials from the env like the SDK."""
+
+    def __init__(self, key_id: str, region: str, access_key: str = "", secret_key: str = "",
+                 session_token: str = "", endpoint: str = ""):
+        self.arn, self.region = key_id, region
+        self.ak = access_key or os.environ.get("AWS_ACCESS_KEY_ID", "")
+        self.sk = secret_key or os.environ.get("AWS_SECRET_ACCESS_KEY", "")
+        self.st = session_token or os.environ.get("AWS_SESSION_TOKEN", "")
+        self.url = endpoint or f"https://kms.{region}.amazonaws.com/"
+        self.key_id = f"aws-kms:{key_id}"
+
+    def _call(self, op: str, body: dict) -> dict:
+        raw = json.dumps(body).encode()
+        extra = {"content-type": "application/x-amz-json-1.1",
+                 "x-amz-target": f"TrentService.{op}"}
+        h = sigv4_headers("POST", self.url, raw, self.region, "kms", self.ak, self.sk, self.st,
+                          extra)
+        h.update({"Content-Type": extra["content-type"], "X-Amz-Target": extra["x-amz-target"]})
+        return self._post(self.url, body, h)
+
+    def _wrap(self, dek):
+        d = self._call("Encrypt", {"KeyId": self.arn, "Plaintext": base64.b64encode(dek).decode()})
+        return base64.b64decode(d["CiphertextBlob"]), "aws"
+
+    def _unwrap(self, edk):
+        d = self._call("Decrypt", {"KeyId": self.arn,
+                                   "CiphertextBlob": base64.b64encode(edk).decode()})
+        return base64.b64decode(d["Plaintext"])
+
+    def key_metadata(self) -> KeyMetadata:
+        d = self._call("DescribeKey", {"KeyId": self.arn}).get("KeyMetadata", {})
+        return KeyMetadata(self.key_id, "aws", created_at=float(d.get("CreationDate") or 0))
+
+    def rotate(self) -> tuple[str, str]:
+        self._call("RotateKeyOnDemand", {"KeyId": self.arn})
+        return "aws", "aws"  # AWS keeps backing-key versions internal; blobs self-describe
+
+
+class GCPKMS(_WrappingKMS):
+    """Cloud KMS REST (``:encrypt`` / ``:decrypt`` on a CryptoKey); OAuth bearer
+    from ``GOOGLE_OAUTH_ACCESS_TOKEN`` or the metadata server."""
+
+    def __init__(self, key_name: str, token: str = "",
+                 endpoint: str = "https://cloudkms.googleapis.com"):
+        self.name, self.base = key_name, endpoint.rstrip("/")
+        self.token = token
+        self.key_id = f"gcp-kms:{key_name.rsplit('/', 1)[-1]}"
+
+    def _bearer(self) -> str:
+        if self.token or os.environ.get("GOOGLE_OAUTH_ACCESS_TOKEN"):
+            return self.token or os.environ["GOOGLE_OAUTH_ACCESS_TOKEN"]
+        import requests
+
+        r = requests.get("http://metadata.google.internal/computeMetadata/v1/instance/"
+                         "service-accounts/default/token", headers={"Metadata-Flavor": "Google"},
+                         timeout=5)
+        r.raise_for_status()
+        return r.json()["access_token"]
+
+    def _call(self, verb: str, body: dict) -> dict:
+        return self._post(f"{self.base}/v1/{self.name}:{verb}", body,
+                          {"Authorization": f"Bearer {self._bearer()}",
+                           "Content-Type": "application/json"})
+
+    def _wrap(self, dek):
+        d = self._call("encrypt", {"plaintext": base64.b64encode(dek).decode()})
+        return base64.b64decode(d["ciphertext"]), d.get("name", "").rsplit("/", 1)[-1] or "1"
+
+    def _unwrap(self, edk):
+        d = self._call("decrypt", {"ciphertext": base64.b64encode(edk).decode()})
+        return base64.b64decode(d["plaintext"])
+
+    def key_metadata(self) -> KeyMetadata:
+        return KeyMetadata(self.key_id, "primary")
+
+    def rotate(self) -> tuple[str, str]:
+        return "primary", "primary"  # rotation is a CryptoKey schedule on the GCP side
+
+
+class AzureKeyVaultKMS(_WrappingKMS):
+    """Key Vault ``wrapkey`` / ``unwrapkey`` (RSA-OAEP-256) REST; bearer from
+    ``AZURE_ACCESS_TOKEN`` or the instance metadata service (workload identity)."""
+
+    def __init__(self, vault_url: str, key_name: str, key_version: str = "", token: str = "",
+                 api_version: str = "7.4"):
+        self.vault, self.name, self.ver = vault_url.rstrip("/"), key_name, key_version
+        self.token, self.api = token, api_version
+        self.key_id = f"azure-kv:{key_name}"
+
+    def _bearer(self) -> str:
+        if self.token or os.environ.get("AZURE_ACCESS_TOKEN"):
+            return self.token or os.environ["AZURE_ACCESS_TOKEN"]
+        import requests
+
+        r = requests.get("http://169.254.169.254/metadata/identity/oauth2/token",
+                         params={"api-version": "2018-02-01",
+                                 "resource": "https://vault.azure.net"},
+                         headers={"Metadata": "true"}, timeout=5)
+        r.raise_for_status()
+        return r.json()["access_token"]
+
+    def _call(self, path: str, body: dict) -> dict:
+        return self._post(f"{self.vault}/keys/{path}?api-version={self.api}", body,
+                          {"Authorization": f"Bearer {self._bearer()}",
+                           "Content-Type": "application/json"})
+
+    def _wrap(self, dek):
+        path = f"{self.name}/{self.ver}/wrapkey" if self.ver else f"{self.name}/wrapkey"
+        d = self._call(path, {"alg": "RSA-OAEP-256", "value": base64.urlsafe_b64encode(
+            dek).rstrip(b"=").decode()})
+        kver = d.get("kid", "").rstrip("/").rsplit("/", 1)[-1] or self.ver or "current"
+        return (kver.encode() + b"|" + base64.urlsafe_b64decode(d["value"] + "=" * (
+            -len(d["value"]) % 4))), kver
+
+    def _unwrap(self, edk):
+        kver, wrapped = edk.split(b"|", 1)
+        d = self._call(f"{self.name}/{kver.decode()}/unwrapkey",
+                       {"alg": "RSA-OAEP-256",
+                        "value": base64.urlsafe_b64encode(wrapped).rstrip(b"=").decode()})
+        return base64.urlsafe_b64decode(d["value"] + "=" * (-len(d["value"]) % 4))
+
+    def key_metadata(self) -> KeyMetadata:
+        return KeyMetadata(self.key_id, self.ver or "current")
+
+    def rotate(self) -> tuple[str, str]:
+        return self.ver or "current", self.ver or "current"  # versions are created in Azure
+
+
 def build_provider(cfg: dict):
     """``ProviderConfig``-shaped dict -> provider (``config.go``)."""
     t = (cfg.get("type") or cfg.get("providerType") or "local").lower()
@@ -203,8 +405,15 @@ def build_provider(cfg: dict):
         return VaultTransitKMS(cfg["address"], cfg.get("keyName", "omnia"),
                                cfg.get("token") or os.environ.get("VAULT_TOKEN", ""),
                                cfg.get("mount", "transit"))
-    if t in ("aws-kms", "awskms", "gcp-kms", "gcpkms", "azure-keyvault", "azurekeyvault"):
-        raise ProviderUnavailable(f"{t} needs its vendor SDK, which is not installed")
+    if t in ("aws-kms", "awskms"):
+        return AWSKMS(cfg["keyID"], cfg.get("region", os.environ.get("AWS_REGION", "us-east-1")),
+                      endpoint=cfg.get("endpoint", ""))
+    if t in ("gcp-kms", "gcpkms"):
+        return GCPKMS(cfg["keyID"], endpoint=cfg.get("endpoint",
+                                                     "https://cloudkms.googleapis.com"))
+    if t in ("azure-keyvault", "azurekeyvault"):
+        return AzureKeyVaultKMS(cfg["vaultURL"], cfg.get("keyName") or cfg["keyID"],
+                                cfg.get("keyVersion", ""))
     raise ValueError(f"unknown KMS provider type {t!r}")
 
 

@@ -272,7 +272,11 @@ def decode_attention(q, k_cache, v_cache, block_tables, seq_lens, scale, part_si
     return r
 
 
-def prefill_tiles(q_lens: list[int], tile: int = 64) -> tuple[list[int], list[int]]:
+PREFILL_Q_TILE = int(os.environ.get("OMNIA_PREFILL_Q_TILE", "128"))  # 64 | 128 query rows
+
+
+def prefill_tiles(q_lens: list[int], tile: int | None = None) -> tuple[list[int], list[int]]:
+    tile = tile or PREFILL_Q_TILE
     seqs, q0s = [], []
     for s, n in enumerate(q_lens):
         for q0 in range(0, n, tile):
@@ -282,17 +286,19 @@ def prefill_tiles(q_lens: list[int], tile: int = 64) -> tuple[list[int], list[in
 
 
 def prefill_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, scale,
-                      tile_seq=None, tile_q0=None, out=None):
+                      tile_seq=None, tile_q0=None, out=None, heads_per_wave: int = 0,
+                      q_tile: int | None = None):
     """q: [T, Hq, D] new tokens of several sequences (varlen, causal w/ cached prefix)."""
     if q.is_cuda:
         if tile_seq is None:
             qsl = q_start_loc.cpu().tolist()
-            s, q0 = prefill_tiles([qsl[i + 1] - qsl[i] for i in range(len(qsl) - 1)])
+            s, q0 = prefill_tiles([qsl[i + 1] - qsl[i] for i in range(len(qsl) - 1)], q_tile)
             tile_seq = torch.tensor(s, dtype=torch.int32, device=q.device)
             tile_q0 = torch.tensor(q0, dtype=torch.int32, device=q.device)
         out = torch.empty_like(q) if out is None else out
         kernels().prefill_attention(out, q, k_cache, v_cache, block_tables, q_start_loc,
-                                    seq_lens, tile_seq, tile_q0, scale)
+                                    seq_lens, tile_seq, tile_q0, scale, heads_per_wave,
+                                    q_tile or PREFILL_Q_TILE)
         return out
     r = ref.paged_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, scale)
     if out is not None:

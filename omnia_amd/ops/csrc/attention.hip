@@ -16,6 +16,8 @@
 //           S^T = K.Q^T so each lane owns one query row (softmax row stats are
 //           lane-local + 2 shuffles), P^T reused in-register as the B operand of
 //           O^T = V^T.P^T with V^T fragments from ds_read_b64_tr_b16.
+#include <stdlib.h>
+
 #include "common.h"
 
 using namespace omnia;
@@ -212,9 +214,14 @@ __device__ __forceinline__ int vswz(int row, int ch) {
   return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
 }
 
-// grid: (Hq, n_tiles)   block: 256 (4 waves x 16 query rows)
-template <int BS>
-__global__ __launch_bounds__(256) void prefill_attn_kernel(
+// grid: (Hq / HP, n_tiles)   block: 64*NW (NW waves x 16 query rows = a 16*NW-row
+// query tile; every staged 64-key K/V tile feeds all NW waves)
+// GQA head packing: each wave carries HP query heads of the same KV head for its
+// 16 rows, so every K / V fragment read from LDS (and every K / V tile staged
+// from HBM) feeds HP heads' MFMAs -- HP x fewer LDS bytes per FLOP and HP x
+// fewer K/V tile loads than one head per block.
+template <int BS, int HP, int NW>
+__global__ __launch_bounds__(64 * NW) void prefill_attn_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ q_start_loc, const int* __restrict__ seq_lens,
@@ -224,10 +231,10 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   char* Kl = lds;
   char* Vl = lds + 64 * 256;
 
-  const int h = blockIdx.x, tile = blockIdx.y;
-  const int hq = gridDim.x;
+  const int h0 = blockIdx.x * HP, tile = blockIdx.y;
+  const int hq = gridDim.x * HP;
   const int G = hq / hkv;
-  const int kvh = h / G;
+  const int kvh = h0 / G;
   const int s = tile_seq[tile], q0 = tile_q0[tile];
   const int qs = q_start_loc[s], qlen = q_start_loc[s + 1] - qs;
   const int ctx = seq_lens[s];
@@ -241,29 +248,36 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   const bool row_ok = qr < qlen;
   const int qr_c = row_ok ? qr : qlen - 1;
   const int qpos = off + qr_c;
-  short8 qf[4];
-  {
-    const bf16_t* qrow = q + (int64_t)(qs + qr_c) * q_stride + h * D;
+  short8 qf[HP][4];
+#pragma unroll
+  for (int hh = 0; hh < HP; ++hh) {
+    const bf16_t* qrow = q + (int64_t)(qs + qr_c) * q_stride + (h0 + hh) * D;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
-      qf[kk] = *reinterpret_cast<const short8*>(qrow + kk * 32 + 8 * g4);
+      qf[hh][kk] = *reinterpret_cast<const short8*>(qrow + kk * 32 + 8 * g4);
   }
 
-  const int last_row = min(q0 + 63, qlen - 1);
+  const int last_row = min(q0 + 16 * NW - 1, qlen - 1);
   const int kv_end = off + last_row + 1;  // keys [0, kv_end)
   const int ntiles = (kv_end + 63) / 64;
   const int min_qpos = off + q0;
 
-  float m_run = -INFINITY, l_run = 0.f;
-  float4v o[8];
+  float m_run[HP], l_run[HP];
+  float4v o[HP][8];
 #pragma unroll
-  for (int mb = 0; mb < 8; ++mb) o[mb] = float4v{0.f, 0.f, 0.f, 0.f};
+  for (int hh = 0; hh < HP; ++hh) {
+    m_run[hh] = -INFINITY;
+    l_run[hh] = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) o[hh][mb] = float4v{0.f, 0.f, 0.f, 0.f};
+  }
 
-  short8 kreg[4], vreg[4];
+  constexpr int NCH = 16 / NW;  // 16-B chunks per thread per 64x128 tile
+  short8 kreg[NCH], vreg[NCH];
   auto gload = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = i * 256 + tid;
+    for (int i = 0; i < NCH; ++i) {
+      const int c = i * 64 * NW + tid;
       const int row = c >> 4, ch = c & 15;
       const int key = t * 64 + row;
       if (key < kv_end) {
@@ -278,8 +292,8 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   };
   auto lwrite = [&]() {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = i * 256 + tid;
+    for (int i = 0; i < NCH; ++i) {
+      const int c = i * 64 * NW + tid;
       const int row = c >> 4, ch = c & 15;
       *reinterpret_cast<short8*>(Kl + row * 256 + 16 * kswz(row, ch)) = kreg[i];
       *reinterpret_cast<short8*>(Vl + row * 256 + 16 * vswz(row, ch)) = vreg[i];
@@ -293,63 +307,67 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   for (int t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) gload(t + 1);
     const int k0 = t * 64;
-    // ---- S^T = K . Q^T
-    float4v sacc[4];
+    // ---- S^T = K . Q^T  (each K fragment feeds HP heads)
+    float4v sacc[HP][4];
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
-      sacc[nb] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int hh = 0; hh < HP; ++hh) sacc[hh][nb] = float4v{0.f, 0.f, 0.f, 0.f};
       const int row = nb * 16 + c16;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         short8 a = *reinterpret_cast<const short8*>(Kl + row * 256 + 16 * kswz(row, kk * 4 + g4));
-        sacc[nb] = mfma16(a, qf[kk], sacc[nb]);
+#pragma unroll
+        for (int hh = 0; hh < HP; ++hh) sacc[hh][nb] = mfma16(a, qf[hh][kk], sacc[hh][nb]);
       }
     }
     const bool need_mask = (k0 + 63 > min_qpos) || (k0 + 63 >= ctx);
-    float mloc = -INFINITY;
+    short8 pb[HP][2];
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb)
+    for (int hh = 0; hh < HP; ++hh) {
+      float mloc = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = sacc[nb][r] * scale_log2;
-        if (need_mask) {
-          const int key = k0 + nb * 16 + g4 * 4 + r;
-          if (key > qpos) v = -INFINITY;
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = sacc[hh][nb][r] * scale_log2;
+          if (need_mask) {
+            const int key = k0 + nb * 16 + g4 * 4 + r;
+            if (key > qpos) v = -INFINITY;
+          }
+          sacc[hh][nb][r] = v;
+          mloc = fmaxf(mloc, v);
         }
-        sacc[nb][r] = v;
-        mloc = fmaxf(mloc, v);
-      }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float m_new = fmaxf(m_run, mloc);
-    const float alpha = exp2f(m_run - m_new);
-    float lsum = 0.f;
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float m_new = fmaxf(m_run[hh], mloc);
+      const float alpha = exp2f(m_run[hh] - m_new);
+      float lsum = 0.f;
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb)
+      for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(sacc[nb][r] - m_new);
-        sacc[nb][r] = p;
-        lsum += p;
-      }
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-    l_run = l_run * alpha + lsum;
-    m_run = m_new;
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(sacc[hh][nb][r] - m_new);
+          sacc[hh][nb][r] = p;
+          lsum += p;
+        }
+      lsum += __shfl_xor(lsum, 16, 64);
+      lsum += __shfl_xor(lsum, 32, 64);
+      l_run[hh] = l_run[hh] * alpha + lsum;
+      m_run[hh] = m_new;
 #pragma unroll
-    for (int mb = 0; mb < 8; ++mb) o[mb] *= alpha;
-
-    // ---- P^T as B operand (k order permuted consistently with the V^T reads)
-    short8 pb[2];
+      for (int mb = 0; mb < 8; ++mb) o[hh][mb] *= alpha;
+      // ---- P^T as B operand (k order permuted consistently with the V^T reads)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pb[ks][j] = (short)f2bf(sacc[2 * ks][j]);
-        pb[ks][4 + j] = (short)f2bf(sacc[2 * ks + 1][j]);
+        for (int j = 0; j < 4; ++j) {
+          pb[hh][ks][j] = (short)f2bf(sacc[hh][2 * ks][j]);
+          pb[hh][ks][4 + j] = (short)f2bf(sacc[hh][2 * ks + 1][j]);
+        }
       }
     }
-    // ---- O^T += V^T . P^T
+    // ---- O^T += V^T . P^T  (each V^T fragment feeds HP heads)
     const int qq = c16 >> 2, pp = c16 & 3;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -364,7 +382,8 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
         v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (__attribute__((address_space(3))) v4s*)(Vl + r2 * 256 + 16 * vswz(r2, ch) + 8 * (pp & 1)));
         short8 a = short8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[mb] = mfma16(a, pb[ks], o[mb]);
+#pragma unroll
+        for (int hh = 0; hh < HP; ++hh) o[hh][mb] = mfma16(a, pb[hh][ks], o[hh][mb]);
       }
     }
     __syncthreads();
@@ -375,14 +394,17 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   }
 
   if (row_ok) {
-    const float inv = 1.f / l_run;
-    bf16_t* orow = out + (int64_t)(qs + qr) * out_stride + h * D;
 #pragma unroll
-    for (int mb = 0; mb < 8; ++mb) {
-      uint2v pk;
-      pk[0] = pack_bf2(o[mb][0] * inv, o[mb][1] * inv);
-      pk[1] = pack_bf2(o[mb][2] * inv, o[mb][3] * inv);
-      *reinterpret_cast<uint2v*>(orow + mb * 16 + g4 * 4) = pk;
+    for (int hh = 0; hh < HP; ++hh) {
+      const float inv = 1.f / l_run[hh];
+      bf16_t* orow = out + (int64_t)(qs + qr) * out_stride + (h0 + hh) * D;
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        uint2v pk;
+        pk[0] = pack_bf2(o[hh][mb][0] * inv, o[hh][mb][1] * inv);
+        pk[1] = pack_bf2(o[hh][mb][2] * inv, o[hh][mb][3] * inv);
+        *reinterpret_cast<uint2v*>(orow + mb * 16 + g4 * 4) = pk;
+      }
     }
   }
 }
@@ -431,21 +453,36 @@ int omnia_prefill_attention(void* out, const void* q, const void* k_cache, const
                             const int* block_tables, int bt_stride, const int* q_start_loc,
                             const int* seq_lens, const int* tile_seq, const int* tile_q0,
                             int n_tiles, int hq, int hkv, int head_dim, int block_size,
-                            int64_t q_stride, int64_t out_stride, float scale, hipStream_t s) {
+                            int64_t q_stride, int64_t out_stride, float scale, int hp_req, int q_tile, hipStream_t s) {
   if (head_dim != 128) return -1;
   if (hq % hkv) return -2;
   if (n_tiles == 0) return 0;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(hq, n_tiles), block(256);
-#define OMNIA_PRE(BB)                                                                        \
-  prefill_attn_kernel<BB><<<grid, block, 0, s>>>(                                            \
+  // heads per wave (GQA packing) and waves per block (query tile = 16 * nw rows)
+  const int G = hq / hkv;
+  static const int env_hp = getenv("OMNIA_PREFILL_HP") ? atoi(getenv("OMNIA_PREFILL_HP")) : 0;
+  int hp = hp_req > 0 ? hp_req : env_hp > 0 ? env_hp : 1;
+  if (hp != 1 && hp != 2 && hp != 4) return -5;
+  if (G % hp) hp = 1;
+  const int nw = q_tile / 16;
+  if (q_tile != 64 && q_tile != 128) return -6;
+  if (nw == 8 && hp != 1) return -7;
+  dim3 grid(hq / hp, n_tiles), block(64 * nw);
+#define OMNIA_PRE(BB, HH, NN)                                                                \
+  prefill_attn_kernel<BB, HH, NN><<<grid, block, 0, s>>>(                                    \
       (bf16_t*)out, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache,        \
       block_tables, bt_stride, q_start_loc, seq_lens, tile_seq, tile_q0, hkv, q_stride,      \
       out_stride, scale_log2)
-  if (block_size == 16) OMNIA_PRE(16);
-  else if (block_size == 32) OMNIA_PRE(32);
-  else if (block_size == 64) OMNIA_PRE(64);
+#define OMNIA_PRE_HP(BB)                              \
+  if (nw == 8) OMNIA_PRE(BB, 1, 8);                   \
+  else if (hp == 4) OMNIA_PRE(BB, 4, 4);              \
+  else if (hp == 2) OMNIA_PRE(BB, 2, 4);              \
+  else OMNIA_PRE(BB, 1, 4);
+  if (block_size == 16) { OMNIA_PRE_HP(16) }
+  else if (block_size == 32) { OMNIA_PRE_HP(32) }
+  else if (block_size == 64) { OMNIA_PRE_HP(64) }
   else return -3;
+#undef OMNIA_PRE_HP
 #undef OMNIA_PRE
   return (int)hipGetLastError();
 }

@@ -26,7 +26,8 @@ int omnia_prefill_attention(void* out, const void* q, const void* k_cache, const
                             const int* block_tables, int bt_stride, const int* q_start_loc,
                             const int* seq_lens, const int* tile_seq, const int* tile_q0,
                             int n_tiles, int hq, int hkv, int head_dim, int block_size,
-                            int64_t q_stride, int64_t out_stride, float scale, hipStream_t s);
+                            int64_t q_stride, int64_t out_stride, float scale, int hp,
+                            int q_tile, hipStream_t s);
 int omnia_apply_token_mask(void* logits, int logits_is_bf16, int rows, int64_t row_stride,
                            int vocab, const uint32_t* mask, int words, hipStream_t s);
 int omnia_sample(int* out_tok, float* out_logprob, const void* logits, int logits_is_bf16,
@@ -178,7 +179,8 @@ void decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tens
 
 void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                        at::Tensor block_tables, at::Tensor q_start_loc, at::Tensor seq_lens,
-                       at::Tensor tile_seq, at::Tensor tile_q0, double scale) {
+                       at::Tensor tile_seq, at::Tensor tile_q0, double scale, int64_t hp,
+                       int64_t q_tile) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_BF16(k_cache);
   CHECK_I32(block_tables); CHECK_I32(q_start_loc); CHECK_I32(seq_lens); CHECK_I32(tile_seq);
   CHECK_I32(tile_q0);
@@ -192,7 +194,8 @@ void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Ten
                                    block_tables.stride(0), q_start_loc.data_ptr<int>(),
                                    seq_lens.data_ptr<int>(), tile_seq.data_ptr<int>(),
                                    tile_q0.data_ptr<int>(), tile_seq.numel(), q.size(1), hkv, D,
-                                   bs, q.stride(0), out.stride(0), (float)scale, cur_stream()),
+                                   bs, q.stride(0), out.stride(0), (float)scale, (int)hp,
+                                   (int)q_tile, cur_stream()),
            "prefill_attention");
 }
 
@@ -476,7 +479,10 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("silu_mul", &silu_mul);
   m.def("embedding", &embedding);
   m.def("decode_attention", &decode_attention);
-  m.def("prefill_attention", &prefill_attention);
+  m.def("prefill_attention", &prefill_attention, py::arg("out"), py::arg("q"),
+        py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("q_start_loc"),
+        py::arg("seq_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("scale"),
+        py::arg("hp") = 0, py::arg("q_tile") = 64);
   m.def("sample", &sample);
   m.def("mean_pool_l2", &mean_pool_l2);
   m.def("cosine_scores", &cosine_scores);

@@ -121,9 +121,11 @@ def test_decode_attention(hq, hkv, bs):
 
 
 @pytest.mark.parametrize("bs", [16, 32])
-def test_prefill_attention(bs):
+@pytest.mark.parametrize("hq,hkv,hp,qt", [(32, 8, 1, 64), (32, 8, 2, 64), (32, 8, 4, 64),
+                                          (64, 8, 4, 64), (8, 8, 0, 64), (32, 8, 1, 128),
+                                          (8, 8, 1, 128)])
+def test_prefill_attention(bs, hq, hkv, hp, qt):
     torch.manual_seed(4)
-    hq, hkv = 32, 8
     # (new tokens, cached prefix) per sequence: ragged + page-boundary edges
     specs = [(1, 0), (64, 0), (100, 37), (257, 0), (5, 600), (130, 64)]
     lens = [q + c for q, c in specs]
@@ -136,7 +138,7 @@ def test_prefill_attention(bs):
     qsl = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
     sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
     scale = 1 / math.sqrt(128)
-    out = ops.prefill_attention(q, kc, vc, bt, qsl, sl, scale)
+    out = ops.prefill_attention(q, kc, vc, bt, qsl, sl, scale, heads_per_wave=hp, q_tile=qt)
     exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), qsl.cpu(), sl.cpu(), scale)
     _close(out.cpu(), exp, 0.03, 0.02)
 

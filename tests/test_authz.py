@@ -32,7 +32,9 @@ def test_roles_basic():
 
 @pytest.mark.skipif(not os.path.exists(REF_CASES), reason="reference fixture not mounted")
 def test_reference_parity_cases():
-    for c in json.load(open(REF_CASES)):
+    with open(REF_CASES) as f:
+        cases = json.load(f)
+    for c in cases:
         got = A.compute_role(c.get("roleBindings") or [], c.get("directGrants") or [],
                              c.get("anonymousAccess"), c.get("userGroups") or [],
                              c.get("userIdentity", ""), c.get("anonymous", False))

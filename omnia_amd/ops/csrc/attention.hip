@@ -35,7 +35,11 @@ constexpr int D = 128;
 
 // ============================================================== decode
 // grid: (B, Hkv, max_parts)   block: 256 (4 waves)
-template <int G, int BS>
+// UG: 16-key groups whose K loads one wave issues before its first MFMA (and,
+// for UG > 1, the first V batch is issued ahead of the softmax) -- the memory-
+// level parallelism of one workgroup, which at short contexts (one workgroup
+// streams a whole ~600-token context) sets the kernel's speed, not HBM.
+template <int G, int BS, int UG>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
@@ -74,30 +78,55 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   }
   __syncthreads();
 
-  // ---- phase 1: scores. each wave takes 16-key groups round-robin.
+  // ---- phase 1: scores. each wave takes 16-key groups round-robin, UG per
+  // pass with all their K loads in flight before the first MFMA (groups past
+  // the end re-read the last key: branch-free, hits in cache).
   const int ngroups = (n + 15) / 16;
-  for (int grp = w; grp < ngroups; grp += 4) {
-    const int key = grp * 16 + (lane & 15);      // this lane's A-row key
-    const int kk_ = min(key, n - 1);
-    const int tok = p0 + kk_;
-    const bf16_t* krow = kc + (((int64_t)pages[kk_ / BS] * hkv + kvh) * BS + (tok % BS)) * D;
-    short8 a[4];
+  for (int grp0 = w; grp0 < ngroups; grp0 += 4 * UG) {
+    short8 a[UG][4];
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-      a[kk] = *reinterpret_cast<const short8*>(krow + kk * 32 + 8 * (lane >> 4));
-    float4v acc = {0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < UG; ++u) {
+      const int key = (grp0 + 4 * u) * 16 + (lane & 15);  // this lane's A-row key
+      const int kk_ = min(key, n - 1);
+      const int tok = p0 + kk_;
+      const bf16_t* krow = kc + (((int64_t)pages[kk_ / BS] * hkv + kvh) * BS + (tok % BS)) * D;
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) acc = mfma16(a[kk], qf[kk], acc);
-    // acc[r] = S^T[key grp*16 + 4*(lane>>4) + r][head lane&15]
-    const int g = lane & 15;
-    if (g < G) {
+      for (int kk = 0; kk < 4; ++kk)
+        a[u][kk] = *reinterpret_cast<const short8*>(krow + kk * 32 + 8 * (lane >> 4));
+    }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kidx = grp * 16 + 4 * (lane >> 4) + r;
-        if (kidx < n) scores[g * part_size + kidx] = acc[r] * scale_log2;
+    for (int u = 0; u < UG; ++u) {
+      const int grp = grp0 + 4 * u;
+      if (grp >= ngroups) break;
+      float4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) acc = mfma16(a[u][kk], qf[kk], acc);
+      // acc[r] = S^T[key grp*16 + 4*(lane>>4) + r][head lane&15]
+      const int g = lane & 15;
+      if (g < G) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kidx = grp * 16 + 4 * (lane >> 4) + r;
+          if (kidx < n) scores[g * part_size + kidx] = acc[r] * scale_log2;
+        }
       }
     }
   }
+  // first V batch of phase 3 in flight across the softmax (plain loads survive
+  // the barriers); lane = (token sub-index tg = lane>>4, dim chunk ch = lane&15)
+  const int tg = lane >> 4, ch = lane & 15;
+  constexpr int U = 4;
+  short8 vv[U];
+  auto vload = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = min(base + u * 16 + tg, n - 1);
+      const int tok = p0 + t;
+      vv[u] = *reinterpret_cast<const short8*>(
+          vc + (((int64_t)pages[t / BS] * hkv + kvh) * BS + (tok % BS)) * D + ch * 8);
+    }
+  };
+  if (UG > 1) vload(w * 4);
   __syncthreads();
 
   // ---- phase 2: softmax per head (wave w handles heads w, w+4)
@@ -125,27 +154,21 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-  const int tg = lane >> 4, ch = lane & 15;
-  constexpr int U = 4;
   for (int base = w * 4; base < n; base += 16 * U) {
-    short8 vv[U];
-    int ti[U];
+    if (UG == 1) vload(base);
+    short8 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = vv[u];
+    if (UG > 1) vload(base + 16 * U);  // next batch (clamped past the end)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      ti[u] = base + u * 16 + tg;
-      const int t = min(ti[u], n - 1);
-      const int tok = p0 + t;
-      vv[u] = *reinterpret_cast<const short8*>(
-          vc + (((int64_t)pages[t / BS] * hkv + kvh) * BS + (tok % BS)) * D + ch * 8);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (ti[u] < n) {
+      const int ti = base + u * 16 + tg;
+      if (ti < n) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-          const float p = scores[g * part_size + ti[u]];
+          const float p = scores[g * part_size + ti];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[g][j] += p * bf2f((uint16_t)vv[u][j]);
+          for (int j = 0; j < 8; ++j) acc[g][j] += p * bf2f((uint16_t)cur[u][j]);
         }
       }
     }
@@ -426,11 +449,18 @@ int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void*
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(B, hkv, max_parts), block(256);
   const size_t lds = 64 + (size_t)G * part_size * 4 + 4 * G * D * 4 + (part_size / block_size) * 4;
-#define OMNIA_DEC(GG, BB)                                                                     \
-  decode_attn_kernel<GG, BB><<<grid, block, lds, s>>>(                                        \
+  // OMNIA_DECODE_UG=1 selects the single-group schedule (A/B measurements)
+  static const int ug = [] {
+    const char* e = getenv("OMNIA_DECODE_UG");
+    return e && atoi(e) == 1 ? 1 : 4;
+  }();
+#define OMNIA_DEC_UG(GG, BB, UU)                                                               \
+  decode_attn_kernel<GG, BB, UU><<<grid, block, lds, s>>>(                                    \
       (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, (const bf16_t*)k_cache,               \
       (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, hkv, q_stride, part_size,   \
       max_parts, scale_log2)
+#define OMNIA_DEC(GG, BB) \
+  do { if (ug == 1) OMNIA_DEC_UG(GG, BB, 1); else OMNIA_DEC_UG(GG, BB, 4); } while (0)
 #define OMNIA_DEC_BS(GG)                                \
   if (block_size == 16) OMNIA_DEC(GG, 16);              \
   else if (block_size == 32) OMNIA_DEC(GG, 32);         \
@@ -443,6 +473,7 @@ int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void*
   else return -4;
 #undef OMNIA_DEC_BS
 #undef OMNIA_DEC
+#undef OMNIA_DEC_UG
   if (max_parts > 1)
     decode_reduce_kernel<<<B * hq, 128, 0, s>>>((bf16_t*)out, part_o, part_ml, seq_lens, hq,
                                                 part_size, max_parts);

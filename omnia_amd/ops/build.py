@@ -107,6 +107,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         futs = [ex.submit(_compile_hip, s, headers) for s in hip_srcs]
         futs.append(ex.submit(_compile_bindings, CSRC / "bindings.cpp", incs))
         objs = [f.result() for f in futs]
+    for stale in set(BUILD.glob("*.o")) - set(objs):  # superseded source versions
+        stale.unlink()
     tlib = tdir / "lib"
     stamp = _hash(objs, ["link"])
     stamp_file = BUILD / "link.stamp"

@@ -219,6 +219,12 @@ def build_audio_provider(spec: dict, role: str, sample_rate: int = 16000):
         return OpenAIAudio(spec.get("baseURL") or "https://api.openai.com/v1",
                            spec.get("model", ""), spec.get("apiKey"),
                            (spec.get("audio") or {}).get("voice", "alloy"))
+    if role == "tts":
+        from .vendors import build_tts_provider
+
+        tts = build_tts_provider(spec, spec.get("apiKey"))
+        if tts is not None:
+            return tts
     raise ValueError(f"unsupported {role} provider type {t!r}")
 
 

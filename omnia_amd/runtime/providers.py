@@ -5,8 +5,10 @@ The reference builds a PromptKit ``providers.Provider`` from the Provider CRD
 and every call leaves the pod.  Here the default is **local**: the in-node
 MI355X engine (:class:`LocalEngineProvider`).  Remote OpenAI-compatible
 endpoints (``openai`` / ``vllm`` / ``ollama`` types) and Anthropic's Messages
-API (``claude``) remain available, and ``mock`` reproduces the reference's
-scenario-driven mock provider for tests (``internal/runtime/scenario.go``).
+API (``claude``) remain available, the other vendor types and the bedrock /
+vertex / azure platforms are in :mod:`.vendors`, and ``mock`` reproduces the
+reference's scenario-driven mock provider for tests
+(``internal/runtime/scenario.go``).
 """
 from __future__ import annotations
 
@@ -492,6 +494,12 @@ def build_provider(spec: dict, engine=None, secrets: dict | None = None) -> Prov
                             path=(spec.get("mock") or {}).get("path"),
                             scenarios=(spec.get("mock") or {}).get("scenarios"),
                             pricing=pricing, defaults=defaults)
+    from .vendors import build_vendor_provider
+
+    vendor = build_vendor_provider(spec, key, secrets,
+                                   {"pricing": pricing, "defaults": defaults})
+    if vendor is not None:
+        return vendor
     if t in ("openai", "vllm", "ollama", "openrouter", "azure"):
         base = spec.get("baseURL") or {"openai": "https://api.openai.com/v1",
                                        "ollama": "http://127.0.0.1:11434",

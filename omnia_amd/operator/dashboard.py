@@ -6,12 +6,19 @@ agent's facade, arena and consent UIs.  This is the serving-side core of it as
 one dependency-free page plus a small aiohttp backend:
 
 * ``GET /api/resources/{plural}`` proxies the operator REST API (K8s-style);
-* ``GET /api/sessions`` proxies session-api search (``/api/v1/sessions``);
+* ``GET /api/sessions`` proxies session-api search (``/api/v1/sessions``) and
+  ``GET /api/sessions/{id}/messages`` one session's transcript;
 * ``GET /api/overview`` -- AgentRuntime phase / replicas / engine summary;
+* ``GET /api/arena/jobs`` -- ArenaJobs with type, phase and result summary;
+* ``GET /api/consent/{user}`` -- the privacy API's consent record (read-only);
 * ``/`` -- the page: resource tables, session list, and a chat console that
   opens ``ws://<facade>/ws?agent=...`` directly from the browser (the
   reference proxies through the dashboard's mgmt-plane twin; here the facade's
   own auth chain applies).
+
+Every ``/api/*`` route is read-only.  With ``--oidc-jwks-file`` the API
+requires an IdP-issued bearer JWT (RS256, issuer / audience checked) -- the
+dashboard holds no credentials of its own to lend to callers.
 Run: ``python -m omnia_amd.operator.dashboard --port 3000 --api http://operator:8090``.
 """
 from __future__ import annotations
@@ -19,6 +26,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import urllib.parse
 
 import aiohttp
 from aiohttp import web
@@ -34,6 +42,11 @@ border:1px solid #ccc;padding:6px;white-space:pre-wrap}</style></head><body>
 <th>replicas</th><th>provider</th></tr></table>
 <h2>Resources</h2><select id="kind"></select><table id="res"></table>
 <h2>Sessions</h2><table id="sess"><tr><th>id</th><th>agent</th><th>messages</th></tr></table>
+<pre id="msgs"></pre>
+<h2>Arena</h2><table id="arena"><tr><th>namespace</th><th>name</th><th>type</th><th>phase</th>
+<th>result</th></tr></table>
+<h2>Consent</h2><input id="cuser" placeholder="user id"><button onclick="consent()">lookup</button>
+<pre id="cons"></pre>
 <h2>Console</h2><input id="ws" size="40" value="ws://127.0.0.1:8080/ws">
 <button onclick="conn()">connect</button><br><input id="msg" size="60">
 <button onclick="send()">send</button><div id="log"></div>
@@ -47,20 +60,54 @@ async function res(){const k=document.getElementById('kind').value;const o=await
  const t=document.getElementById('res');t.innerHTML='<tr><th>namespace</th><th>name</th><th>phase</th></tr>';
  for(const it of (o.items||[])){const r=t.insertRow();r.insertCell().textContent=it.metadata.namespace||'';
  r.insertCell().textContent=it.metadata.name;r.insertCell().textContent=(it.status||{}).phase||''}}
+async function msgs(id){const o=await j('/api/sessions/'+encodeURIComponent(id)+'/messages');
+ document.getElementById('msgs').textContent=(o.messages||[]).map(m=>m.role+': '+m.content).join('\\n')}
 async function sess(){const o=await j('/api/sessions');const t=document.getElementById('sess');
  for(const s of (o.sessions||[])){const r=t.insertRow();for(const v of [s.id,s.agent_name,s.message_count])
- r.insertCell().textContent=v}}
+ r.insertCell().textContent=v;r.onclick=()=>msgs(s.id)}}
+async function arena(){const o=await j('/api/arena/jobs');const t=document.getElementById('arena');
+ for(const a of o.jobs){const r=t.insertRow();for(const v of [a.namespace,a.name,a.type,a.phase,
+ JSON.stringify(a.result||{})])r.insertCell().textContent=v??''}}
+async function consent(){const u=document.getElementById('cuser').value;
+ document.getElementById('cons').textContent=JSON.stringify(
+ await j('/api/consent/'+encodeURIComponent(u)),null,1)}
 function log(x){const l=document.getElementById('log');l.textContent+=x+'\\n';l.scrollTop=1e9}
 function conn(){sock=new WebSocket(document.getElementById('ws').value);
  sock.onmessage=e=>{const m=JSON.parse(e.data);log(m.type+': '+(m.content||m.error?.message||''))}}
 function send(){sock.send(JSON.stringify({type:'message',content:document.getElementById('msg').value}))}
 const sel=document.getElementById('kind');for(const k of KINDS){const o=document.createElement('option');
- o.value=k;o.textContent=k;sel.appendChild(o)};sel.onchange=res;agents();res();sess();
+ o.value=k;o.textContent=k;sel.appendChild(o)};sel.onchange=res;agents();res();sess();arena();
 </script></body></html>"""
 
 
-def build_app(api: str, session_api: str = "") -> web.Application:
-    app = web.Application()
+def oidc_middleware(jwks: dict, issuer: str = "", audience: str = ""):
+    """401 on ``/api/*`` without a valid IdP bearer token."""
+    from ..facade.auth import AuthError, bearer, jwt_decode
+
+    @web.middleware
+    async def mw(request, handler):
+        if request.path.startswith("/api/"):
+            tok = bearer(request.headers)
+            if not tok:
+                return web.json_response({"error": "missing bearer token"}, status=401)
+            try:
+                claims = jwt_decode(tok, jwks=jwks, issuer=issuer or None,
+                                    audience=audience or None)
+            except AuthError:
+                return web.json_response({"error": "invalid token"}, status=401)
+            if "exp" not in claims:
+                return web.json_response({"error": "token without exp"}, status=401)
+        return await handler(request)
+
+    return mw
+
+
+def build_app(api: str, session_api: str = "", privacy_api: str = "",
+              oidc: dict | None = None) -> web.Application:
+    """``oidc``: ``{"jwks": {...}, "issuer": ..., "audience": ...}`` gates the API."""
+    mws = [oidc_middleware(oidc["jwks"], oidc.get("issuer", ""), oidc.get("audience", ""))] \
+        if oidc else []
+    app = web.Application(middlewares=mws)
     plurals = sorted(k.plural for k in crds.KINDS.values())
 
     async def _get(url):
@@ -86,6 +133,31 @@ def build_app(api: str, session_api: str = "") -> web.Application:
                               f"{int(request.query.get('limit', 50))}")
         return web.json_response(body, status=st)
 
+    async def session_messages(request):
+        if not session_api:
+            return web.json_response({"messages": []})
+        sid = urllib.parse.quote(request.match_info["id"], safe="")
+        st, body = await _get(f"{session_api}/api/v1/sessions/{sid}/messages")
+        return web.json_response(body, status=st)
+
+    async def arena_jobs(_):
+        st, body = await _get(f"{api}/apis/{crds.GROUP}/{crds.VERSION}/arenajobs")
+        jobs = []
+        for it in (body or {}).get("items", []):
+            spec, status = it.get("spec", {}), it.get("status", {})
+            jobs.append({"namespace": it["metadata"].get("namespace"),
+                         "name": it["metadata"]["name"], "type": spec.get("type"),
+                         "phase": status.get("phase"),
+                         "result": status.get("result") or status.get("results")})
+        return web.json_response({"jobs": jobs})
+
+    async def consent(request):
+        if not privacy_api:
+            return web.json_response({"error": "privacy api not configured"}, status=404)
+        user = urllib.parse.quote(request.match_info["user"], safe="")
+        st, body = await _get(f"{privacy_api}/api/v1/privacy/preferences/{user}/consent")
+        return web.json_response(body, status=st)
+
     async def overview(_):
         st, body = await _get(f"{api}/apis/{crds.GROUP}/{crds.VERSION}/agentruntimes")
         out = []
@@ -106,6 +178,9 @@ def build_app(api: str, session_api: str = "") -> web.Application:
     app.router.add_get("/api/resources/{plural}", resources)
     app.router.add_get("/api/sessions", sessions)
     app.router.add_get("/api/overview", overview)
+    app.router.add_get("/api/sessions/{id}/messages", session_messages)
+    app.router.add_get("/api/arena/jobs", arena_jobs)
+    app.router.add_get("/api/consent/{user}", consent)
     app.router.add_get("/healthz", healthz)
     return app
 
@@ -116,10 +191,18 @@ def main(argv=None):
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--api", default="http://127.0.0.1:8090")
     ap.add_argument("--session-api", default="")
+    ap.add_argument("--privacy-api", default="")
+    ap.add_argument("--oidc-jwks-file", default="", help="IdP JWKS; gates /api/* when set")
+    ap.add_argument("--oidc-issuer", default="")
+    ap.add_argument("--oidc-audience", default="")
     a = ap.parse_args(argv)
+    oidc = None
+    if a.oidc_jwks_file:
+        with open(a.oidc_jwks_file) as f:
+            oidc = {"jwks": json.load(f), "issuer": a.oidc_issuer, "audience": a.oidc_audience}
 
     async def run():
-        runner = web.AppRunner(build_app(a.api, a.session_api))
+        runner = web.AppRunner(build_app(a.api, a.session_api, a.privacy_api, oidc))
         await runner.setup()
         await web.TCPSite(runner, a.host, a.port).start()
         await asyncio.Event().wait()

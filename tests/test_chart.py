@@ -8,6 +8,7 @@
 import asyncio
 import glob
 import importlib
+import json
 import os
 import re
 
@@ -88,5 +89,96 @@ def test_dashboard_proxies_operator_api():
         finally:
             await dash.close()
             await api.close()
+
+    asyncio.run(run())
+
+
+def _rsa_jwk(seed=7):
+    import base64
+    import random
+
+    rng = random.Random(seed)
+
+    def prime(bits):
+        while True:
+            c = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+            if all(pow(a, c - 1, c) == 1 for a in (2, 3, 5, 7, 11, 13, 17, 19, 23)):
+                return c
+    e = 65537
+    while True:
+        p, q = prime(512), prime(512)
+        phi = (p - 1) * (q - 1)
+        if p != q and phi % e:
+            break
+    n, d = p * q, pow(e, -1, (p - 1) * (q - 1))
+
+    def b64(i):
+        return base64.urlsafe_b64encode(i.to_bytes((i.bit_length() + 7) // 8, "big")
+                                        ).rstrip(b"=").decode()
+    return {"kty": "RSA", "kid": "idp", "n": b64(n), "e": b64(e)}, n, d
+
+
+def _rs256(claims, n, d, kid="idp"):
+    import base64
+
+    from omnia_amd.ee.license import rs256_sign
+
+    def enc(b):
+        return base64.urlsafe_b64encode(b).rstrip(b"=").decode()
+    h = enc(json.dumps({"alg": "RS256", "kid": kid}).encode())
+    p = enc(json.dumps(claims).encode())
+    return f"{h}.{p}.{enc(rs256_sign(f'{h}.{p}'.encode(), n, d))}"
+
+
+def test_dashboard_views_and_oidc_gate():
+    import time
+
+    from aiohttp import web
+    from aiohttp.test_utils import TestClient, TestServer
+
+    from omnia_amd.operator.apiserver import build_app as api_app
+    from omnia_amd.operator.apistore import APIStore
+    from omnia_amd.operator.dashboard import build_app
+
+    pub, n, d = _rsa_jwk()
+
+    async def run():
+        store = APIStore()
+        store.apply({"apiVersion": crds.API_VERSION, "kind": "ArenaJob",
+                     "metadata": {"name": "lt", "namespace": "default"},
+                     "spec": {"type": "loadtest", "sourceRef": {"name": "s"}}})
+        api = TestServer(api_app(store))
+        await api.start_server()
+        side = web.Application()
+        side.router.add_get("/api/v1/sessions/{id}/messages", lambda r: web.json_response(
+            {"messages": [{"role": "user", "content": "hi " + r.match_info["id"]}]}))
+        side.router.add_get("/api/v1/privacy/preferences/{u}/consent", lambda r: web.json_response(
+            {"userId": r.match_info["u"], "grants": ["analytics"]}))
+        sides = TestServer(side)
+        await sides.start_server()
+        sbase = str(sides.make_url("")).rstrip("/")
+        dash = TestClient(TestServer(build_app(
+            str(api.make_url("")).rstrip("/"), session_api=sbase, privacy_api=sbase,
+            oidc={"jwks": {"keys": [pub]}, "issuer": "https://idp", "audience": "dash"})))
+        await dash.start_server()
+        try:
+            assert (await dash.get("/")).status == 200  # the page itself is public
+            assert (await dash.get("/api/arena/jobs")).status == 401
+            bad = _rs256({"iss": "https://other", "aud": "dash", "exp": time.time() + 60}, n, d)
+            r = await dash.get("/api/arena/jobs", headers={"Authorization": f"Bearer {bad}"})
+            assert r.status == 401
+            tok = _rs256({"iss": "https://idp", "aud": "dash", "sub": "u1",
+                          "exp": time.time() + 60}, n, d)
+            h = {"Authorization": f"Bearer {tok}"}
+            jobs = (await (await dash.get("/api/arena/jobs", headers=h)).json())["jobs"]
+            assert [(j["name"], j["type"]) for j in jobs] == [("lt", "loadtest")]
+            m = await (await dash.get("/api/sessions/s%201/messages", headers=h)).json()
+            assert m["messages"][0]["content"] == "hi s 1"
+            c = await (await dash.get("/api/consent/alice", headers=h)).json()
+            assert c == {"userId": "alice", "grants": ["analytics"]}
+        finally:
+            await dash.close()
+            await api.close()
+            await sides.close()
 
     asyncio.run(run())

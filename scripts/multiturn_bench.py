@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Multi-turn agent conversations on one MI355X: session-resident KV vs
+re-prefilling the whole history every turn.
+
+The reference's agents are stateless towards their provider: each turn re-sends
+the full conversation, and the remote model re-prefills it
+(``internal/runtime/conversation.go``).  The in-node engine keeps each session's
+KV resident between turns (keyed by ``session_id``), so turn k only prefills
+the new user message.
+
+S sessions run T turns in lock-step. Each turn appends ``--user-len`` synthetic
+tokens and generates ``--gen-len`` (ignore_eos). The whole workload runs twice:
+* ``resident``: requests carry their session_id, so the prefix comes from the
+  cache;
+* ``stateless``: requests carry no session id, so the full history is
+  re-prefilled.
+
+Per turn it reports wall time, mean TTFT, and the prompt tokens that were
+actually prefilled versus served from the cache.
+Llama-3-8B architecture, random-init bf16 weights, synthetic token ids.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(eng, S, T, user_len, gen_len, resident, seed):
+    from omnia_amd.engine.sampling_params import SamplingParams
+
+    rng = random.Random(seed)
+    params = SamplingParams(temperature=0.0, max_tokens=gen_len, ignore_eos=True)
+    hist = [[] for _ in range(S)]
+    sids = [f"mt-{seed}-{i}" for i in range(S)] if resident else None
+    turns = []
+    for t in range(T):
+        prompts = []
+        for i in range(S):
+            hist[i] = hist[i] + [rng.randrange(1000, 100000) for _ in range(user_len)]
+            prompts.append(list(hist[i]))
+        t0 = time.perf_counter()
+        seqs = eng.generate(prompts, params, session_ids=sids)
+        wall = time.perf_counter() - t0
+        ttft = [s.ttft() for s in seqs if s.ttft() is not None]
+        cached = sum(s.prefix_hit for s in seqs)
+        total = sum(len(p) for p in prompts)
+        for i, s in enumerate(seqs):
+            hist[i] = hist[i] + list(s.output[:gen_len])
+        turns.append({"turn": t + 1, "history_tokens": total // S, "wall_s": round(wall, 3),
+                      "mean_ttft_ms": round(1e3 * sum(ttft) / len(ttft), 1) if ttft else None,
+                      "prefilled_tokens": total - cached, "cached_tokens": cached})
+        print(json.dumps({"mode": "resident" if resident else "stateless", **turns[-1]}),
+              flush=True)
+    if resident:
+        for sid in sids:
+            eng.drop_session(sid)
+    return turns
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sessions", type=int, default=128)
+    ap.add_argument("--turns", type=int, default=4)
+    ap.add_argument("--user-len", type=int, default=256)
+    ap.add_argument("--gen-len", type=int, default=128)
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    import torch
+
+    from omnia_amd.engine.engine import EngineConfig, LLMEngine
+
+    eng = LLMEngine(EngineConfig(model=a.model, device="cuda" if torch.cuda.is_available()
+                                 else "cpu", max_batch=max(256, a.sessions)))
+    run(eng, 8, 1, 32, 8, True, 99)  # warm-up: graphs, tuned GEMMs
+    res = {m: run(eng, a.sessions, a.turns, a.user_len, a.gen_len, m == "resident", 1)
+           for m in ("resident", "stateless")}
+    r, s = res["resident"], res["stateless"]
+    summary = {"sessions": a.sessions, "turns": a.turns, "user_len": a.user_len,
+               "gen_len": a.gen_len,
+               "total_wall_s": {"resident": round(sum(x["wall_s"] for x in r), 3),
+                                "stateless": round(sum(x["wall_s"] for x in s), 3)},
+               "last_turn_ttft_ms": {"resident": r[-1]["mean_ttft_ms"],
+                                     "stateless": s[-1]["mean_ttft_ms"]},
+               "prefilled_tokens": {"resident": sum(x["prefilled_tokens"] for x in r),
+                                    "stateless": sum(x["prefilled_tokens"] for x in s)}}
+    print(json.dumps({"summary": summary}), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"summary": summary, "turns": res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -21,9 +21,10 @@ for m in models:
     cfg = resolve(m)
     shapes += gemm_tuning.decode_shapes(cfg, batches=tuple(batches + prefill))
 seen = set()
+vocab = {resolve(m).vocab_size for m in models}
 for (M, N, K) in shapes:
-    if (M, N, K) in seen:
-        continue
+    if (M, N, K) in seen or (M in prefill and N in vocab):
+        continue  # the LM head only sees the last token of each prefill
     seen.add((M, N, K))
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)

@@ -64,3 +64,23 @@ def test_ring_attention_matches_dense(world, causal):
     assert all(p.exitcode == 0 for p in procs)
     err = q.get(timeout=5)
     assert err < 1e-4, err
+
+
+@pytest.mark.gpu
+def test_block_merge_on_gpu_bf16():
+    """The per-block product + LSE merge on the MI355X (bf16 operands through
+    hipBLASLt, fp32 statistics) against dense fp32 attention."""
+    torch.manual_seed(1)
+    T, Hq, Hkv, D = 1024, 32, 8, 128
+    dev = "cuda"
+    q = torch.randn(T, Hq, D, device=dev, dtype=torch.bfloat16)
+    k = torch.randn(T, Hkv, D, device=dev, dtype=torch.bfloat16)
+    v = torch.randn(T, Hkv, D, device=dev, dtype=torch.bfloat16)
+    pos = torch.arange(T, device=dev)
+    scale = D ** -0.5
+    h = T // 2
+    o1, l1 = cp._block(q, k[:h], v[:h], pos, pos[:h], scale, True, 256)
+    o2, l2 = cp._block(q, k[h:], v[h:], pos, pos[h:], scale, True, 256)
+    o, _ = cp._merge(o1, l1, o2, l2)
+    ref = cp.reference_attention(q.float(), k.float(), v.float(), scale=scale)
+    assert (o - ref).abs().max().item() < 3e-2

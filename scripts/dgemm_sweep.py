@@ -27,6 +27,9 @@ SHAPES = [
     # Llama-3-70B TP=8 shards
     ("70b_qkv_tp8", 0, 1280, 8192), ("70b_o_tp8", 0, 8192, 1024),
     ("70b_gu_tp8", 1, 3584, 8192), ("70b_down_tp8", 0, 8192, 3584),
+    # Llama-3-70B on one GPU (TP=1)
+    ("70b_qkv", 0, 10240, 8192), ("70b_o", 0, 8192, 8192), ("70b_gu", 1, 28672, 8192),
+    ("70b_down", 0, 8192, 28672), ("70b_lm_head", 0, 128256, 8192),
 ]
 
 

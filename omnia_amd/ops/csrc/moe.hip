@@ -134,14 +134,12 @@ __global__ __launch_bounds__(256) void moe_gemm_kernel(
   const bf16_t* a_src[2];
   const bf16_t* b_src[2];
   int a_lds[2], b_lds[2];
-  bool a_ok[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int c = tid + i * 256;  // 0..511
     const int row = c >> 3, ch = c & 7;
     const int flat = sorted[mb * BM + row];
-    a_ok[i] = flat < n_assign;
-    const int64_t arow = MODE == 0 ? (a_ok[i] ? flat / topk : 0) : (int64_t)mb * BM + row;
+    const int64_t arow = MODE == 0 ? (flat < n_assign ? flat / topk : 0) : (int64_t)mb * BM + row;
     a_src[i] = A + arow * K + ch * 8;
     a_lds[i] = swz(row, ch);
     int wrow;
@@ -152,16 +150,18 @@ __global__ __launch_bounds__(256) void moe_gemm_kernel(
     b_src[i] = We + (int64_t)wrow * K + ch * 8;
     b_lds[i] = swz(row, ch);
   }
-  short8 ra[2], rb[2];
-  const short8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto gload = [&](int k0) {
+  // Rows past the expert's assignments read row 0 of A (valid memory) and are
+  // dropped in the epilogue, so every load is unconditional.  Two k-tiles of
+  // loads in flight in a register ring with clamped k offsets (branch-free, so
+  // hipcc counts vmcnt across the loop instead of draining it each k-step).
+  auto gload = [&](short8* ra, short8* rb, int k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      ra[i] = (MODE == 1 || a_ok[i]) ? *reinterpret_cast<const short8*>(a_src[i] + k0) : zero;
-      rb[i] = *reinterpret_cast<const short8*>(b_src[i] + k0);
+      ra[i] = *reinterpret_cast<const short8*>(a_src[i] + k0);
+      rb[i] = __builtin_nontemporal_load(reinterpret_cast<const short8*>(b_src[i] + k0));
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](const short8* ra, const short8* rb, int buf) {
     bf16_t* As = lds + buf * (2 * BM * 64);
     bf16_t* Bs = As + BM * 64;
 #pragma unroll
@@ -176,13 +176,9 @@ __global__ __launch_bounds__(256) void moe_gemm_kernel(
   for (int j = 0; j < 4; ++j) acc[j] = {0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / 64;
-  gload(0);
-  lstore(0);
-  __syncthreads();
   const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload((kt + 1) * 64);
-    const bf16_t* As = lds + (kt & 1) * (2 * BM * 64);
+  auto compute = [&](int buf) {
+    const bf16_t* As = lds + buf * (2 * BM * 64);
     const bf16_t* Bs = As + BM * 64;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -193,9 +189,24 @@ __global__ __launch_bounds__(256) void moe_gemm_kernel(
         acc[j] = mfma16(a, b, acc[j]);
       }
     }
-    if (kt + 1 < nk) lstore((kt + 1) & 1);
+  };
+  const int klast = (nk - 1) * 64;
+  short8 ra0[2], rb0[2], ra1[2], rb1[2];
+  gload(ra0, rb0, 0);
+  gload(ra1, rb1, min(64, klast));
+  lstore(ra0, rb0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    gload(ra0, rb0, min((kt + 2) * 64, klast));
+    compute(0);
+    lstore(ra1, rb1, 1);
+    __syncthreads();
+    gload(ra1, rb1, min((kt + 3) * 64, klast));
+    if (kt + 1 < nk) compute(1);
+    lstore(ra0, rb0, 0);
     __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // epilogue: lane holds rows 16w + 4*fq + r, columns 16*j + fr
 #pragma unroll

@@ -59,6 +59,7 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
     const float* __restrict__ pres_pen, const float* __restrict__ rep_pen) {
   __shared__ float red_f[kThreads / 64];
   __shared__ int red_i[kThreads / 64];
+  __shared__ float red_z[kThreads / 64];
   __shared__ int hist[256];
   __shared__ float hmass[256];
   __shared__ uint32_t sh_prefix, sh_mask;
@@ -76,31 +77,52 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
   c.rep = rep_pen ? rep_pen[row] : 1.f;
   c.inv_t = greedy ? 1.f : 1.f / temp;
 
-  // ---- pass A: max (+ argmax)
-  float best = -INFINITY;
+  // ---- pass A: max, argmax and the partition function in ONE sweep (online
+  // rescaling of the running sum), with 16-B loads when the row layout allows
+  // (bf16 logits, no penalty table): the greedy path reads each logit once.
+  float best = -INFINITY, z = 0.f;
   int besti = 0;
-  for (int i = tid; i < vocab; i += kThreads) {
-    const float x = value_at<T>(lr, i, c);
-    if (x > best) { best = x; besti = i; }
-  }
+  auto visit = [&](float x, int i) {
+    if (x == -INFINITY) return;  // masked token: no mass
+    if (x > best) {
+      z = z * __expf(best - x) + 1.f;  // exp(-inf) = 0 on the first hit
+      best = x;
+      besti = i;
+    } else {
+      z += __expf(x - best);
+    }
+  };
+  const bool vec = sizeof(T) == 2 && c.counts == nullptr && (row_stride % 8) == 0 &&
+                   (vocab % 8) == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0;
+  if (vec) {
+    const short8* lv = reinterpret_cast<const short8*>(lr);
+    for (int ch = tid; ch < vocab / 8; ch += kThreads) {
+      const short8 v = lv[ch];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ob = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(besti, o, 64);
-    if (ob > best || (ob == best && oi < besti)) { best = ob; besti = oi; }
+      for (int j = 0; j < 8; ++j) visit(bf2f((uint16_t)v[j]) * c.inv_t, ch * 8 + j);
+    }
+  } else {
+    for (int i = tid; i < vocab; i += kThreads) visit(value_at<T>(lr, i, c), i);
   }
-  if (lane == 0) { red_f[wid] = best; red_i[wid] = besti; }
+  auto merge = [&](float ob, int oi, float oz) {
+    const float m = fmaxf(best, ob);
+    const float nz = (best == -INFINITY ? 0.f : z * __expf(best - m)) +
+                     (ob == -INFINITY ? 0.f : oz * __expf(ob - m));
+    if (ob > best || (ob == best && oi < besti)) besti = oi;
+    best = m;
+    z = nz;
+  };
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    merge(__shfl_xor(best, o, 64), __shfl_xor(besti, o, 64), __shfl_xor(z, o, 64));
+  if (lane == 0) { red_f[wid] = best; red_i[wid] = besti; red_z[wid] = z; }
   __syncthreads();
-  float M = red_f[0];
-  int argm = red_i[0];
-  for (int i = 1; i < kThreads / 64; ++i)
-    if (red_f[i] > M || (red_f[i] == M && red_i[i] < argm)) { M = red_f[i]; argm = red_i[i]; }
-  __syncthreads();
-
-  // ---- pass B: partition function of the (temperature-scaled) distribution
-  float z = 0.f;
-  for (int i = tid; i < vocab; i += kThreads) z += __expf(value_at<T>(lr, i, c) - M);
-  const float Z = block_sum(z, red_f);
+  best = red_f[0];
+  besti = red_i[0];
+  z = red_z[0];
+  for (int i = 1; i < kThreads / 64; ++i) merge(red_f[i], red_i[i], red_z[i]);
+  const float M = best, Z = z;
+  const int argm = besti;
   __syncthreads();
 
   if (greedy) {

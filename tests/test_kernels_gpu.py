@@ -152,6 +152,32 @@ def test_sample_greedy_matches_argmax():
     assert torch.equal(tok16.long().cpu(), logits.bfloat16().float().argmax(-1).cpu())
 
 
+def test_sample_bf16_vector_path_logprob_and_masked():
+    """bf16 rows take the fused one-pass max/argmax/partition sweep (16-B
+    loads): token, log-prob and -inf (grammar-masked) entries vs fp32 torch."""
+    torch.manual_seed(11)
+    B, V = 9, 128256
+    logits = (torch.randn(B, V, device=DEV) * 4).bfloat16()
+    logits[0, :1000] = float("-inf")
+    logits[1, 5] = 30.0
+    logits[2, 7] = 25.0
+    logits[2, 9] = 25.0  # tie -> lowest index, like argmax
+    temp = torch.zeros(B, device=DEV)
+    lp = torch.empty(B, device=DEV)
+    tok = ops.sample(logits, temp, out_logprob=lp).long().cpu()
+    f = logits.float().cpu()
+    assert torch.equal(tok, f.argmax(-1))
+    exp_lp = torch.log_softmax(f, -1)[torch.arange(B), tok]
+    assert (lp.cpu() - exp_lp).abs().max() < 1e-3
+    # temperature path (same fused sweep feeds its max / partition function)
+    temp = torch.full((B,), 0.9, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV)
+    tok = ops.sample(logits, temp, seeds=seeds, steps=seeds, out_logprob=lp).long().cpu()
+    exp_lp = torch.log_softmax(f / 0.9, -1)[torch.arange(B), tok]
+    assert (lp.cpu() - exp_lp).abs().max() < 1e-3
+    assert bool(torch.isfinite(f[torch.arange(B), tok]).all())
+
+
 def test_sample_topk_topp_support():
     torch.manual_seed(5)
     B, V = 6, 32000

@@ -141,6 +141,12 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
                                      limit=cfg.memory_limit)
         executor.add_handler(memory_tools(memory.client, ws, cfg.agent_name))
     try:
+        from .skills import attach_skills
+
+        attach_skills(executor)  # OMNIA_PROMPTPACK_MANIFEST_PATH; no-op without skills
+    except (OSError, ValueError) as e:
+        log.error("skill manifest load failed: %s", e)
+    try:
         await executor.discover()
     except Exception as e:  # noqa: BLE001
         log.warning("tool discovery failed: %s", e)

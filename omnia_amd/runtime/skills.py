@@ -1,0 +1,158 @@
+"""PromptPack skills in the runtime (reference
+``internal/runtime/skills/manifest.go`` and ``server.go`` ``WithSkillManifest``).
+
+The PromptPack reconciler writes a skill manifest (``OMNIA_PROMPTPACK_MANIFEST_PATH``):
+``{"version", "skills": [{"mount_as", "content_path", "name"}], "config":
+{"max_active", "selector"}}``. Each entry is a directory that holds a
+``SKILL.md`` with YAML front matter (``name``, ``description``) followed by the
+skill's instructions. An empty path or a missing file means no skills; a
+malformed file is an error.
+
+The agent sees each skill's catalog line (name, mount path, description) in the
+server-side tool descriptions. It activates a skill to receive its
+instructions and reads the skill's bundled resources on demand:
+* ``skill__activate`` returns the instructions. At most ``max_active`` skills
+  are active at once; the oldest is dropped first.
+* ``skill__deactivate`` removes a skill from the active set.
+* ``skill__read_resource`` reads a file inside the skill directory. The path is
+  confined to the directory.
+
+These are server-side tools of a :class:`SkillsHandler`, so they go through the
+executor's policy, circuit-breaker and metrics path like any other tool. They
+are never sent to the facade.
+"""
+from __future__ import annotations
+
+import json
+import os
+from collections import OrderedDict
+from dataclasses import dataclass, field
+
+import yaml
+
+from ..tools.executor import CallContext, Handler, ToolDef
+
+
+@dataclass
+class ManifestEntry:
+    mount_as: str
+    content_path: str
+    name: str = ""
+
+
+@dataclass
+class Manifest:
+    version: str = ""
+    skills: list = field(default_factory=list)
+    max_active: int = 0
+    selector: str = ""
+
+
+def read_manifest(path: str | None) -> Manifest:
+    if not path or not os.path.exists(path):
+        return Manifest()
+    with open(path) as f:
+        try:
+            raw = json.load(f)
+        except json.JSONDecodeError as e:
+            raise ValueError(f"parse skill manifest {path}: {e}") from e
+    cfg = raw.get("config") or {}
+    return Manifest(version=raw.get("version", ""),
+                    skills=[ManifestEntry(s.get("mount_as", ""), s.get("content_path", ""),
+                                          s.get("name", "")) for s in raw.get("skills") or []],
+                    max_active=int(cfg.get("max_active") or 0), selector=cfg.get("selector", ""))
+
+
+@dataclass
+class Skill:
+    name: str
+    description: str
+    mount_as: str
+    root: str
+    instructions: str
+
+
+def load_skill(entry: ManifestEntry) -> Skill:
+    with open(os.path.join(entry.content_path, "SKILL.md")) as f:
+        text = f.read()
+    meta, body = {}, text
+    if text.startswith("---"):
+        end = text.find("\n---", 3)
+        if end != -1:
+            meta = yaml.safe_load(text[3:end]) or {}
+            body = text[end + 4:].lstrip("\n")
+    return Skill(name=str(meta.get("name") or entry.name or os.path.basename(entry.content_path)),
+                 description=str(meta.get("description", "")), mount_as=entry.mount_as,
+                 root=os.path.realpath(entry.content_path), instructions=body)
+
+
+class SkillsHandler(Handler):
+    type = "skills"
+
+    def __init__(self, manifest: Manifest, workflow_prefix: str = ""):
+        super().__init__({"name": "skills"})
+        self.skills: dict[str, Skill] = {}
+        for e in manifest.skills:
+            s = load_skill(e)
+            if workflow_prefix and not s.mount_as.startswith(workflow_prefix):
+                continue  # workflow scoping by mount path
+            self.skills[s.name] = s
+        self.max_active = manifest.max_active
+        self.active: "OrderedDict[str, None]" = OrderedDict()
+
+    def catalog(self) -> str:
+        return "\n".join(f"- {s.name} ({s.mount_as}): {s.description}"
+                         for s in self.skills.values())
+
+    async def discover(self) -> list[ToolDef]:
+        if not self.skills:
+            return []
+        names = sorted(self.skills)
+        one = {"type": "object", "properties": {"name": {"type": "string", "enum": names}},
+               "required": ["name"]}
+        res = {"type": "object", "properties": {"name": {"type": "string", "enum": names},
+                                                "path": {"type": "string"}},
+               "required": ["name", "path"]}
+        cat = self.catalog()
+        return [ToolDef("skill__activate", "Activate a skill and receive its instructions. "
+                        "Available skills:\n" + cat, one, self.name, self.type),
+                ToolDef("skill__deactivate", "Deactivate an active skill.", one, self.name,
+                        self.type),
+                ToolDef("skill__read_resource", "Read a file bundled with a skill.", res,
+                        self.name, self.type)]
+
+    async def call(self, tool: ToolDef, args: dict, ctx: CallContext) -> str:
+        s = self.skills.get(args.get("name", ""))
+        if s is None:
+            raise KeyError(f"unknown skill {args.get('name')!r}")
+        if tool.name == "skill__activate":
+            self.active.pop(s.name, None)
+            self.active[s.name] = None
+            dropped = []
+            while self.max_active and len(self.active) > self.max_active:
+                dropped.append(self.active.popitem(last=False)[0])
+            return json.dumps({"skill": s.name, "instructions": s.instructions,
+                               "active": list(self.active), "deactivated": dropped})
+        if tool.name == "skill__deactivate":
+            self.active.pop(s.name, None)
+            return json.dumps({"skill": s.name, "active": list(self.active)})
+        if tool.name == "skill__read_resource":
+            p = os.path.realpath(os.path.join(s.root, args.get("path", "")))
+            if os.path.commonpath([p, s.root]) != s.root or not os.path.isfile(p):
+                raise PermissionError("resource outside the skill directory or missing")
+            with open(p, errors="replace") as f:
+                return json.dumps({"skill": s.name, "path": args["path"],
+                                   "content": f.read(256 * 1024)})
+        raise KeyError(tool.name)
+
+
+def attach_skills(executor, manifest_path: str | None = None, workflow_prefix: str = ""):
+    """Add the manifest's skills to an executor (no-op without a manifest)."""
+    path = manifest_path if manifest_path is not None else \
+        os.environ.get("OMNIA_PROMPTPACK_MANIFEST_PATH", "")
+    m = read_manifest(path)
+    if not m.skills:
+        return None
+    h = SkillsHandler(m, workflow_prefix)
+    executor.add_handler(h)
+    return h

@@ -149,6 +149,10 @@ class Scheduler:
         if self.running:
             # every running seq needs a slot for its next token
             for s in list(self.running):
+                # a sequence preempted earlier in this pass holds no pages and
+                # must not allocate any (that would cascade preemptions)
+                if s not in self.running:
+                    continue
                 while True:
                     try:
                         self._ensure_blocks(s, s.length)
@@ -156,8 +160,6 @@ class Scheduler:
                     except OutOfBlocks:
                         if not self._preempt_one(protect=s):
                             raise
-                if s not in self.running:
-                    continue
             return StepPlan("decode", [], list(self.running))
         return StepPlan("idle", [], [])
 

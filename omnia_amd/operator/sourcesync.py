@@ -57,6 +57,38 @@ def parse_duration(s: str | None, default: float = 300.0) -> float:
     return total + (float(num) if num else 0.0)
 
 
+def _confined_copytree(src: Path, dest: Path) -> None:
+    """Copy ``src`` to ``dest`` keeping symlinks as links (never following them,
+    as ``internal/sourcesync/dir.go`` does with Readlink/Symlink), then drop every
+    link whose target resolves outside the copied tree, so a synced repo cannot
+    smuggle operator-host files (service-account tokens, ...) into the content
+    tree that skills and packs later read."""
+    shutil.copytree(src, dest, symlinks=True)
+    root = dest.resolve()
+    for p in sorted(dest.rglob("*"), key=lambda q: len(q.parts), reverse=True):
+        if p.is_symlink():
+            try:
+                tgt = (p.parent / os.readlink(p)).resolve()
+            except OSError:
+                tgt = None
+            if tgt is None or not (tgt == root or str(tgt).startswith(str(root) + os.sep)):
+                log.warning("source sync: dropping symlink %s escaping the tree", p)
+                p.unlink()
+
+
+def _workspace_files(p: Path) -> dict[str, bytes]:
+    """Content map for hashing a workspace tree; symlinks contribute their link
+    text, never the bytes of what they point at."""
+    out: dict[str, bytes] = {}
+    for f in p.rglob("*"):
+        rel = str(f.relative_to(p))
+        if f.is_symlink():
+            out[rel] = b"link:" + os.readlink(f).encode()
+        elif f.is_file():
+            out[rel] = f.read_bytes()
+    return out
+
+
 def _hash_tree(files: dict[str, bytes]) -> str:
     h = hashlib.sha256()
     for k in sorted(files):
@@ -104,7 +136,10 @@ class SourceSyncer:
             args = ["clone", "-q", "--depth", "1"] + (["--branch", br] if br else [])
             git(*args, g["url"], str(repo))
         rev = git("rev-parse", "HEAD", cwd=repo)
-        src = repo / g["path"] if g.get("path") else repo
+        src = (repo / g["path"]).resolve() if g.get("path") else repo
+        rr = repo.resolve()
+        if src != rr and not str(src).startswith(str(rr) + os.sep):
+            raise SyncError(f"path {g.get('path')!r} escapes the repository")
         if not src.exists():
             raise SyncError(f"path {g.get('path')!r} not found in repository")
         shutil.rmtree(repo / ".git", ignore_errors=True)
@@ -182,7 +217,7 @@ class SourceSyncer:
             dest = dest_root / short
             try:
                 if not dest.exists():
-                    shutil.copytree(src, dest)
+                    _confined_copytree(src, dest)
             finally:
                 shutil.rmtree(tmp, ignore_errors=True)
                 Path(str(tmp) + "-askpass.sh").unlink(missing_ok=True)
@@ -206,12 +241,11 @@ class SourceSyncer:
             p = Path(spec.get("workspace", {}).get("path", ""))
             if not p.is_dir():
                 raise SyncError(f"workspace path {p} not found")
-            files = {str(f.relative_to(p)): f.read_bytes() for f in p.rglob("*") if f.is_file()}
-            rev = _hash_tree(files)
+            rev = _hash_tree(_workspace_files(p))
             short = rev.split(":")[-1][:12]
             dest = dest_root / short
             if not dest.exists():
-                shutil.copytree(p, dest)
+                _confined_copytree(p, dest)
         else:
             raise SyncError(f"unsupported source type {t!r}")
         target = dest / spec["targetPath"] if spec.get("targetPath") else dest

@@ -144,7 +144,7 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
         from .skills import attach_skills
 
         attach_skills(executor)  # OMNIA_PROMPTPACK_MANIFEST_PATH; no-op without skills
-    except (OSError, ValueError) as e:
+    except (OSError, ValueError) as e:  # unreadable/malformed manifest: serve without skills
         log.error("skill manifest load failed: %s", e)
     try:
         await executor.discover()

@@ -24,6 +24,7 @@ are never sent to the facade.
 from __future__ import annotations
 
 import json
+import logging
 import os
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -31,6 +32,12 @@ from dataclasses import dataclass, field
 import yaml
 
 from ..tools.executor import CallContext, Handler, ToolDef
+
+log = logging.getLogger("omnia.runtime.skills")
+
+# active-skill sets of this many conversations are kept; the least recently
+# used conversation's set is forgotten first
+MAX_TRACKED_SESSIONS = 10000
 
 
 @dataclass
@@ -79,7 +86,12 @@ def load_skill(entry: ManifestEntry) -> Skill:
     if text.startswith("---"):
         end = text.find("\n---", 3)
         if end != -1:
-            meta = yaml.safe_load(text[3:end]) or {}
+            try:
+                meta = yaml.safe_load(text[3:end]) or {}
+            except yaml.YAMLError as e:
+                raise ValueError(f"skill {entry.content_path}: bad front matter: {e}") from e
+            if not isinstance(meta, dict):
+                raise ValueError(f"skill {entry.content_path}: front matter is not a mapping")
             body = text[end + 4:].lstrip("\n")
     return Skill(name=str(meta.get("name") or entry.name or os.path.basename(entry.content_path)),
                  description=str(meta.get("description", "")), mount_as=entry.mount_as,
@@ -92,13 +104,37 @@ class SkillsHandler(Handler):
     def __init__(self, manifest: Manifest, workflow_prefix: str = ""):
         super().__init__({"name": "skills"})
         self.skills: dict[str, Skill] = {}
+        self.load_errors: list[str] = []
         for e in manifest.skills:
-            s = load_skill(e)
+            try:
+                s = load_skill(e)
+            except (OSError, ValueError) as err:
+                # one bad skill is logged and skipped; the rest still serve
+                log.error("skill %s skipped: %s", e.content_path or e.mount_as, err)
+                self.load_errors.append(str(err))
+                continue
             if workflow_prefix and not s.mount_as.startswith(workflow_prefix):
                 continue  # workflow scoping by mount path
+            if s.name in self.skills:
+                log.error("duplicate skill name %r (%s and %s): keeping the first",
+                          s.name, self.skills[s.name].mount_as, s.mount_as)
+                self.load_errors.append(f"duplicate skill {s.name}")
+                continue
             self.skills[s.name] = s
         self.max_active = manifest.max_active
-        self.active: "OrderedDict[str, None]" = OrderedDict()
+        # per-conversation active sets (PromptKit keeps the active set per
+        # conversation): session id -> ordered active skill names
+        self._active: "OrderedDict[str, OrderedDict[str, None]]" = OrderedDict()
+
+    def active(self, session_id: str) -> "OrderedDict[str, None]":
+        cur = self._active.get(session_id)
+        if cur is None:
+            cur = self._active[session_id] = OrderedDict()
+            while len(self._active) > MAX_TRACKED_SESSIONS:
+                self._active.popitem(last=False)
+        else:
+            self._active.move_to_end(session_id)
+        return cur
 
     def catalog(self) -> str:
         return "\n".join(f"- {s.name} ({s.mount_as}): {s.description}"
@@ -125,17 +161,18 @@ class SkillsHandler(Handler):
         s = self.skills.get(args.get("name", ""))
         if s is None:
             raise KeyError(f"unknown skill {args.get('name')!r}")
+        active = self.active(ctx.session_id or "")
         if tool.name == "skill__activate":
-            self.active.pop(s.name, None)
-            self.active[s.name] = None
+            active.pop(s.name, None)
+            active[s.name] = None
             dropped = []
-            while self.max_active and len(self.active) > self.max_active:
-                dropped.append(self.active.popitem(last=False)[0])
+            while self.max_active and len(active) > self.max_active:
+                dropped.append(active.popitem(last=False)[0])
             return json.dumps({"skill": s.name, "instructions": s.instructions,
-                               "active": list(self.active), "deactivated": dropped})
+                               "active": list(active), "deactivated": dropped})
         if tool.name == "skill__deactivate":
-            self.active.pop(s.name, None)
-            return json.dumps({"skill": s.name, "active": list(self.active)})
+            active.pop(s.name, None)
+            return json.dumps({"skill": s.name, "active": list(active)})
         if tool.name == "skill__read_resource":
             p = os.path.realpath(os.path.join(s.root, args.get("path", "")))
             if os.path.commonpath([p, s.root]) != s.root or not os.path.isfile(p):

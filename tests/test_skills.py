@@ -74,3 +74,42 @@ def test_workflow_scoping(tmp_path):
                            S.ManifestEntry("logistics/shipping", str(b))])
     h = S.SkillsHandler(m, workflow_prefix="billing/")
     assert list(h.skills) == ["refunds"]
+
+
+def test_active_sets_are_per_session(tmp_path):
+    """Two conversations activating skills do not evict each other."""
+    from omnia_amd.tools.executor import CallContext
+
+    dirs = [_skill(tmp_path, n, n, n) for n in ("a", "b", "c")]
+    m = S.Manifest(max_active=1, skills=[S.ManifestEntry(f"x/{d.name}", str(d)) for d in dirs])
+
+    async def run():
+        ex = OmniaExecutor()
+        ex.add_handler(S.SkillsHandler(m))
+        await ex.discover()
+        s1, s2 = CallContext(session_id="s1"), CallContext(session_id="s2")
+        r, _ = await ex.execute("skill__activate", {"name": "a"}, s1)
+        r, _ = await ex.execute("skill__activate", {"name": "b"}, s2)
+        assert json.loads(r)["active"] == ["b"] and json.loads(r)["deactivated"] == []
+        r, _ = await ex.execute("skill__deactivate", {"name": "c"}, s1)
+        assert json.loads(r)["active"] == ["a"]
+
+    asyncio.run(run())
+
+
+def test_bad_and_duplicate_skills_are_skipped(tmp_path):
+    good = _skill(tmp_path, "good", "g", "ok")
+    dup = tmp_path / "dup"
+    dup.mkdir()
+    (dup / "SKILL.md").write_text("---\nname: good\n---\nsecond\n")
+    bad = tmp_path / "bad"
+    bad.mkdir()
+    (bad / "SKILL.md").write_text("---\nname: [unclosed\n---\nx\n")
+    lst = tmp_path / "lst"
+    lst.mkdir()
+    (lst / "SKILL.md").write_text("---\n- a\n- b\n---\nx\n")
+    m = S.Manifest(skills=[S.ManifestEntry(f"m/{d.name}", str(d))
+                           for d in (good, dup, bad, lst, tmp_path / "missing")])
+    h = S.SkillsHandler(m)
+    assert list(h.skills) == ["good"] and h.skills["good"].instructions.startswith("ok")
+    assert len(h.load_errors) == 4

@@ -94,3 +94,36 @@ def test_syncer_history_gc(tmp_path):
     revs = [d for d in (tmp_path / "default" / "arenasource" / "x").iterdir()
             if d.is_dir() and not d.is_symlink()]
     assert len(revs) == 2
+
+
+def test_symlinks_escaping_the_tree_are_dropped(tmp_path):
+    """A synced tree keeps in-tree links as links and drops links to host files
+    (copytree followed symlinks and copied e.g. SA tokens in)."""
+    secret = tmp_path / "host-secret"
+    secret.write_text("TOKEN")
+    ws = tmp_path / "ws"
+    (ws / "skills").mkdir(parents=True)
+    (ws / "skills" / "SKILL.md").write_text("# s\n")
+    (ws / "leak.txt").symlink_to(secret)
+    (ws / "ok.md").symlink_to("skills/SKILL.md")
+    s = SourceSyncer(str(tmp_path / "content"))
+    out = s.sync(APIStore(), {"kind": "SkillSource",
+                              "metadata": {"name": "w", "namespace": "default"},
+                              "spec": {"type": "workspace", "workspace": {"path": str(ws)}}})
+    from pathlib import Path
+
+    dest = Path(out["path"])
+    assert not (dest / "leak.txt").exists() and not (dest / "leak.txt").is_symlink()
+    assert (dest / "ok.md").is_symlink() and (dest / "ok.md").read_text() == "# s\n"
+
+
+def test_git_path_traversal_rejected(tmp_path, repo):
+    store = APIStore()
+    store.create({"apiVersion": "omnia.altairalabs.ai/v1alpha1", "kind": "SkillSource",
+                  "metadata": {"name": "t", "namespace": "default"},
+                  "spec": {"type": "git", "interval": "1m",
+                           "git": {"url": str(repo), "path": "../../.."}}})
+    rec = SourceReconciler("SkillSource", str(tmp_path / "content"))
+    rec.reconcile(store, "default", "t")
+    st = store.get("SkillSource", "t", "default")["status"]
+    assert st["phase"] == "Failed" and "escapes" in st["conditions"][0]["message"]

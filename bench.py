@@ -2,32 +2,44 @@
 """Headline benchmark: streamed tokens/sec + p50 turn latency of an AgentRuntime
 serving Llama-3-8B (BASELINE.json metric) on 1/2/4/8 MI355X GPUs.
 
-One process per GPU (torchrun), each rank an independent engine replica
-(DP = N, weak scaling: per-GPU concurrency is fixed as N grows).  A "step" is
-one wave of C concurrent agent turns per GPU: each turn submits a fresh
-synthetic ``--prompt-len``-token message (no KV prefix reuse across waves) and
-streams ``--gen-len`` tokens with ignore_eos, exactly the reference's arena
-load-test definitions (``ee/pkg/arena/fleet/client.go:124-157``): TTFT = first
-streamed token, turn latency = done.  Weights are random-init bf16 of the exact
-Llama-3-8B architecture (no checkpoints offline); data is synthetic.
+One rank process per GPU (DP = N replicas, weak scaling: per-GPU concurrency is
+fixed as N grows).  ``--gpus N`` without a torchrun environment spawns the N
+rank processes itself (the parent never touches a GPU); under
+``torch.distributed.run`` the world size must equal ``--gpus``.
 
-``--path runtime`` (default) drives every turn through the omnia.runtime.v1
-Converse handler (agent loop + PromptPack rendering + chunk framing) with the
-engine in its own engine-core process (``omnia_amd.engine.core_proc``, the
-production layout); ``--inproc`` runs it as a thread of the serving process and
-``--path engine`` calls the engine directly.
+A "step" is one wave of C concurrent agent turns per GPU.  Every turn sends a
+fresh synthetic message whose rendered prompt (PromptPack system prompt + Llama-3
+chat template + user text) is exactly ``--prompt-len`` tokens and streams
+``--gen-len`` tokens with ignore_eos.  Timing follows the reference's arena load
+tester (``ee/pkg/arena/fleet/client.go:124-157``): TTFT = first streamed frame,
+turn latency = ``done``, tokens = ``done.usage.output_tokens``.  Weights are
+random-init bf16 of the exact Llama-3-8B architecture; data is synthetic.
+
+Paths (``--path``):
+  ws       (default) the production pod: every turn is a real WebSocket
+           connection to the facade process, which calls the runtime process
+           over gRPC; the runtime renders the pack, tokenizes and streams from
+           its engine-core child on this rank's GPU (``operator/pods.py``).
+  runtime  the runtime's Converse handler in-process (no sockets), engine-core
+           child process.
+  engine   the engine API directly.
+``--arrival poisson --rate R`` replaces the closed-loop waves by an open-loop
+stream of ``steps x C`` turns per GPU arriving at R turns/s and reports TTFT and
+inter-token latency percentiles.
 """
 from __future__ import annotations
 
 import argparse
+import asyncio
 import json
 import os
+import random
+import socket
 import statistics
+import subprocess
 import sys
+import tempfile
 import time
-
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -35,7 +47,7 @@ sys.path.insert(0, ROOT)
 BASELINE_METRIC = "streamed tokens/sec + p50 turn latency, AgentRuntime Llama-3-8B at 1/2/4/8 GPU"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -46,156 +58,358 @@ def parse():
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--max-prefill-tokens", type=int, default=16384)
     ap.add_argument("--temperature", type=float, default=0.0)
-    ap.add_argument("--path", choices=["engine", "runtime"], default="runtime",
-                    help="runtime = full AgentRuntime turn path (default); engine = engine only")
+    ap.add_argument("--path", choices=["ws", "runtime", "engine"], default="ws")
+    ap.add_argument("--stream-interval-ms", type=float, default=0.0,
+                    help="runtime text-delta coalescing window (0 = one frame per token)")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica")
+    ap.add_argument("--arrival", choices=["closed", "poisson"], default="closed")
+    ap.add_argument("--rate", type=float, default=0.0, help="poisson: turns/s per replica")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--inproc", action="store_true",
-                    help="runtime path: run the engine as a thread of the serving process "
-                         "instead of its own engine-core process")
-    ap.add_argument("--device", default="cuda")
-    return ap.parse_args()
+                    help="runtime path: engine as a thread of the serving process")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--pod-timeout", type=float, default=900.0)
+    return ap.parse_args(argv)
 
 
-def main():
-    a = parse()
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # device_count() does not initialise the GPU: the engine-core child must be
-    # started before this process touches it
-    use_gpu = a.device == "cuda" and torch.cuda.device_count() > 0
-    proc = a.path == "runtime" and not a.inproc
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    from omnia_amd.engine.engine import AsyncLLMEngine, EngineConfig, LLMEngine
-    from omnia_amd.engine.sampling_params import SamplingParams
 
-    C = a.concurrency
-    cfg = EngineConfig(model=a.model, device="cuda" if use_gpu else "cpu",
-                       max_batch=max(C, 1), max_model_len=max(2048, a.prompt_len + a.gen_len + 64),
-                       max_prefill_tokens=a.max_prefill_tokens, use_graphs=not a.no_graphs,
-                       seed=rank)
-    eng = client = None
-    if proc:
-        from omnia_amd.engine.core_proc import EngineCoreClient
+def spawn_ranks(a) -> int:
+    """``--gpus N`` outside torchrun: start N rank processes of this script (the
+    torchrun env contract) and return the first failing exit code.  Nothing in
+    this process initialises a GPU."""
+    port = _free_port()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    for p in procs:
+        p.wait()
+        if p.returncode and not rc:
+            rc = p.returncode
+    return rc
 
-        client = EngineCoreClient(cfg, device_index=local if use_gpu else None)
-        if ws > 1:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo")  # host-side result aggregation only
-        model_cfg = client.engine.model_cfg
-    else:
-        if use_gpu:
-            torch.cuda.set_device(local)
-        if ws > 1:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("nccl" if use_gpu else "gloo")
-        eng = LLMEngine(cfg)
-        model_cfg = eng.model_cfg
-    vocab = model_cfg.vocab_size
-    params = SamplingParams(temperature=a.temperature, max_tokens=a.gen_len, ignore_eos=True,
-                            top_p=1.0)
-    g = torch.Generator().manual_seed(1234 + rank)
 
-    runtime = None
-    if a.path == "runtime":
-        from omnia_amd.runtime.bench_driver import RuntimeBenchDriver
+def pct(v, q):
+    if not v:
+        return None
+    v = sorted(v)
+    return v[min(len(v) - 1, int(round(q * (len(v) - 1))))]
 
-        runtime = RuntimeBenchDriver(client if proc else AsyncLLMEngine(eng), params)
 
-    def one_wave(step: int):
-        lo = min(1000, vocab // 4)
-        prompts = torch.randint(lo, vocab - lo, (C, a.prompt_len), generator=g).tolist()
-        if runtime is not None:
-            return runtime.run_wave(prompts, step)
-        seqs = [eng.add_request(p, params, session_id=f"r{rank}-s{step}-{i}")
+# ============================================================== WebSocket path
+class WSDriver:
+    """Runs this rank's agent pod (facade + runtime + engine-core processes) and
+    drives turns through its WebSocket endpoint."""
+
+    SYSTEM = "You are a benchmark agent."
+
+    def __init__(self, a, rank: int, local: int, use_gpu: bool, world: int):
+        from omnia_amd.operator.pods import ProcessPod
+        from omnia_amd.runtime.promptpack import PromptPack
+
+        self.a = a
+        self.rank = rank
+        self.leader = rank % a.tp == 0
+        self.tmp = tempfile.mkdtemp(prefix=f"omnia-bench-r{rank}-")
+        self.rng = random.Random(1234 + rank)
+        self.pod = None
+        self.overhead = self._template_overhead()
+        if a.prompt_len <= self.overhead:
+            raise SystemExit(f"--prompt-len {a.prompt_len} must exceed the chat-template "
+                             f"overhead of {self.overhead} tokens")
+        if not self.leader:
+            return
+        pack = PromptPack.minimal(self.SYSTEM).data
+        pack["prompts"]["default"]["parameters"] = {
+            "max_tokens": a.gen_len, "ignore_eos": True, "temperature": a.temperature,
+            "top_p": 1.0}
+        pack_path = os.path.join(self.tmp, "pack.json")
+        with open(pack_path, "w") as f:
+            json.dump(pack, f)
+        C = a.concurrency
+        renv = {
+            "OMNIA_AGENT_NAME": f"bench-{rank}", "OMNIA_PROVIDER_TYPE": "local",
+            "OMNIA_PROMPTPACK_PATH": pack_path, "OMNIA_TOOLS_CONFIG_PATH": "",
+            "OMNIA_STREAM_INTERVAL_MS": a.stream_interval_ms,
+            "OMNIA_ENGINE_MODEL": a.model, "OMNIA_ENGINE_DEVICE": "cuda" if use_gpu else "cpu",
+            "OMNIA_ENGINE_MAX_BATCH": max(C, 1),
+            "OMNIA_ENGINE_MAX_MODEL_LEN": max(2048, a.prompt_len + a.gen_len + 64),
+            "OMNIA_ENGINE_MAX_PREFILL_TOKENS": a.max_prefill_tokens,
+            "OMNIA_ENGINE_USE_GRAPHS": "false" if a.no_graphs else "true",
+            "OMNIA_ENGINE_SEED": rank, "OMNIA_ENGINE_PROC": "1" if use_gpu and a.tp == 1 else "0",
+            "OMNIA_ENGINE_TP": a.tp,
+        }
+        fenv = {"OMNIA_AGENT_NAME": f"bench-{rank}", "OMNIA_MAX_CONNECTIONS": 4 * C + 64,
+                "OMNIA_MSG_RATE": 1000, "OMNIA_MSG_BURST": 1000}
+        devs = list(range(local, local + a.tp)) if use_gpu else None
+        self.pod = ProcessPod(f"bench-r{rank}", renv, fenv, device_index=devs,
+                              log_dir=os.path.join(self.tmp, "logs"), tp=a.tp)
+        self.pod.start(timeout_s=a.pod_timeout)
+        self.loop = asyncio.new_event_loop()
+        self.http = self.loop.run_until_complete(self._mk_http())
+
+    async def _mk_http(self):
+        import aiohttp
+
+        return aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None),
+                                     connector=aiohttp.TCPConnector(limit=0))
+
+    def _template_overhead(self) -> int:
+        """Tokens the runtime adds around the user text (system prompt + chat
+        template), with the engine's tokenizer (byte-level for random-init)."""
+        from omnia_amd.engine.tokenizer import make_tokenizer
+        from omnia_amd.models.config import resolve
+        from omnia_amd.runtime.chat import Message, render_llama3
+
+        self.tok = make_tokenizer(resolve(self.a.model))
+        base = render_llama3([Message("system", self.SYSTEM), Message("user", "")])
+        return len(self.tok.encode(base))
+
+    def _content(self) -> str:
+        n = self.a.prompt_len - self.overhead
+        # printable ASCII, one byte token each; fresh per turn (no cross-turn prefix reuse)
+        return "".join(self.rng.choice("abcdefghijklmnopqrstuvwxyz ,.") for _ in range(n))
+
+    async def _turn(self, content: str):
+        from omnia_amd.ee.arena.fleet import FleetSession
+
+        async with FleetSession(self.pod.ws_url, http=self.http, timeout_s=600) as fs:
+            r = await fs.turn(content)
+        u = r["usage"] or {}
+        return (r["ttft_ms"] / 1e3, r["latency_ms"] / 1e3, int(u.get("output_tokens", 0)),
+                int(u.get("input_tokens", 0)), r["chunk_times_s"])
+
+    async def _wave(self):
+        return await asyncio.gather(*(self._turn(self._content())
+                                      for _ in range(self.a.concurrency)))
+
+    def wave(self, step: int):
+        if self.pod is None:
+            return []
+        res = self.loop.run_until_complete(self._wave())
+        if step < 0:
+            ins = {r[3] for r in res}
+            if ins != {self.a.prompt_len}:
+                raise SystemExit(f"prompt length mismatch: runtime saw {sorted(ins)[:4]} "
+                                 f"tokens, expected {self.a.prompt_len}")
+        return res
+
+    async def _open_loop(self, n: int, rate: float):
+        rng = random.Random(99 + self.rank)
+        tasks = []
+        t = time.perf_counter()
+        for _ in range(n):
+            tasks.append(asyncio.ensure_future(self._turn(self._content())))
+            t += rng.expovariate(rate)
+            d = t - time.perf_counter()
+            if d > 0:
+                await asyncio.sleep(d)
+        return await asyncio.gather(*tasks)
+
+    def open_loop(self, n: int, rate: float):
+        if self.pod is None:
+            return []
+        return self.loop.run_until_complete(self._open_loop(n, rate))
+
+    def close(self):
+        if self.pod is not None:
+            self.loop.run_until_complete(self.http.close())
+            self.pod.stop()
+            self.pod = None
+
+
+# ============================================================== in-process paths
+class LocalDriver:
+    def __init__(self, a, rank: int, local: int, use_gpu: bool, world: int):
+        import torch
+        import torch.distributed as dist
+
+        from omnia_amd.engine.engine import AsyncLLMEngine, EngineConfig, LLMEngine
+        from omnia_amd.engine.sampling_params import SamplingParams
+
+        self.a = a
+        self.rank = rank
+        self.proc = a.path == "runtime" and not a.inproc
+        self.use_gpu = use_gpu
+        C = a.concurrency
+        cfg = EngineConfig(model=a.model, device="cuda" if use_gpu else "cpu",
+                           max_batch=max(C, 1),
+                           max_model_len=max(2048, a.prompt_len + a.gen_len + 64),
+                           max_prefill_tokens=a.max_prefill_tokens, use_graphs=not a.no_graphs,
+                           seed=rank)
+        self.cfg = cfg
+        self.eng = self.client = None
+        if self.proc:
+            from omnia_amd.engine.core_proc import EngineCoreClient
+
+            self.client = EngineCoreClient(cfg, device_index=local if use_gpu else None)
+            model_cfg = self.client.engine.model_cfg
+        else:
+            if use_gpu:
+                torch.cuda.set_device(local)
+            self.eng = LLMEngine(cfg)
+            model_cfg = self.eng.model_cfg
+        self.vocab = model_cfg.vocab_size
+        self.params = SamplingParams(temperature=a.temperature, max_tokens=a.gen_len,
+                                     ignore_eos=True, top_p=1.0)
+        self.g = torch.Generator().manual_seed(1234 + rank)
+        self.runtime = None
+        if a.path == "runtime":
+            from omnia_amd.runtime.bench_driver import RuntimeBenchDriver
+
+            self.runtime = RuntimeBenchDriver(self.client if self.proc else AsyncLLMEngine(self.eng),
+                                              self.params)
+
+    def wave(self, step: int):
+        import torch
+
+        a = self.a
+        lo = min(1000, self.vocab // 4)
+        prompts = torch.randint(lo, self.vocab - lo, (a.concurrency, a.prompt_len),
+                                generator=self.g).tolist()
+        if self.runtime is not None:
+            return [(t, l, n, a.prompt_len, []) for t, l, n in self.runtime.run_wave(prompts, step)]
+        eng = self.eng
+        seqs = [eng.add_request(p, self.params, session_id=f"r{self.rank}-s{step}-{i}")
                 for i, p in enumerate(prompts)]
         eng.run_until_done()
         for s in seqs:
             eng.drop_session(s.session_id)  # fresh prompts next wave: no prefix reuse
-        return [(s.ttft(), s.latency(), len(s.output)) for s in seqs]
+        return [(s.ttft(), s.latency(), len(s.output), a.prompt_len, []) for s in seqs]
+
+    def sync(self):
+        import torch
+
+        if self.proc:
+            self.client.synchronize()  # torch.cuda.synchronize() in the GPU-owning process
+        elif self.use_gpu:
+            torch.cuda.synchronize()
+
+    def engine_stats(self) -> dict:
+        if self.proc:
+            return self.client.stats()
+        eng = self.eng
+        return {"timing": dict(eng.timing), "counters": dict(eng.counters),
+                "runner": dict(eng.runner.stats), "kv_blocks": eng.blocks.num_blocks,
+                "block_size": self.cfg.block_size}
+
+    def reset_timing(self):
+        if self.proc:
+            self.client.call("reset_timing")
+        else:
+            for k in self.eng.timing:
+                self.eng.timing[k] = 0.0
+            self.eng.runner.stats["gil_wait_s"] = 0.0
+
+    def close(self):
+        if self.runtime is not None:
+            self.runtime.close()
+        elif self.client is not None:
+            self.client.shutdown()
+
+
+# ============================================================== main
+def main():
+    a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a))
+    import torch
+    import torch.distributed as dist
+
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but the launcher started {ws} ranks")
+    if a.gpus % a.tp:
+        raise SystemExit(f"--gpus {a.gpus} is not a multiple of --tp {a.tp}")
+    if a.tp > 1 and a.path != "ws":
+        raise SystemExit("--tp > 1 is served by the ws path (one TP pod per replica)")
+    # device_count() does not initialise the GPU: engine children start before any HIP call
+    use_gpu = a.device == "cuda" and torch.cuda.device_count() > 0
+    host_only = a.path == "ws" or (a.path == "runtime" and not a.inproc)
+    if ws > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # result aggregation only: host-side gloo whenever this process owns no GPU work
+        dist.init_process_group("gloo" if (host_only or not use_gpu) else "nccl")
+
+    drv = WSDriver(a, rank, local, use_gpu, ws) if a.path == "ws" else \
+        LocalDriver(a, rank, local, use_gpu, ws)
+    try:
+        run(a, drv, ws, rank, use_gpu, host_only)
+    finally:
+        drv.close()
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run(a, drv, ws, rank, use_gpu, host_only):
+    import torch
+    import torch.distributed as dist
 
     def sync():
-        if proc:
-            client.synchronize()  # torch.cuda.synchronize() in the GPU-owning process
-        elif use_gpu:
-            torch.cuda.synchronize()
+        if isinstance(drv, LocalDriver):
+            drv.sync()
         if ws > 1:
             dist.barrier()
 
-    def engine_stats() -> dict:
-        if proc:
-            return client.stats()
-        return {"timing": dict(eng.timing), "counters": dict(eng.counters),
-                "runner": dict(eng.runner.stats), "kv_blocks": eng.blocks.num_blocks,
-                "block_size": cfg.block_size}
-
-    def reset_timing():
-        if proc:
-            client.call("reset_timing")
-        else:
-            for k in eng.timing:
-                eng.timing[k] = 0.0
-            eng.runner.stats["gil_wait_s"] = 0.0
-
-    gc_pauses = None
-    if os.environ.get("OMNIA_STEP_TRACE"):
-        import gc
-
-        gc_pauses = {0: [0, 0.0], 1: [0, 0.0], 2: [0, 0.0]}
-        _gc_t = {}
-
-        def _gc_cb(phase, info):
-            if phase == "start":
-                _gc_t["t"] = time.perf_counter()
-            else:
-                e = gc_pauses[info["generation"]]
-                e[0] += 1
-                e[1] += time.perf_counter() - _gc_t.get("t", time.perf_counter())
-
-        gc.callbacks.append(_gc_cb)
     for w in range(a.warmup):
-        one_wave(-1 - w)
+        drv.wave(-1 - w)
+    if isinstance(drv, LocalDriver):
+        drv.reset_timing()
     sync()
-    reset_timing()
     t0 = time.perf_counter()
     results = []
-    for k in range(a.steps):
-        results.extend(one_wave(k))
+    if a.arrival == "poisson":
+        if a.rate <= 0:
+            raise SystemExit("--arrival poisson needs --rate > 0 (turns/s per replica)")
+        results = drv.open_loop(a.steps * a.concurrency, a.rate) if a.path == "ws" else []
+    else:
+        for k in range(a.steps):
+            results.extend(drv.wave(k))
     sync()
     elapsed = time.perf_counter() - t0
-    if gc_pauses is not None:
-        print("[gc]", {g: (n, round(t * 1e3, 1)) for g, (n, t) in gc_pauses.items()},
-              file=sys.stderr)
-    if eng is not None and eng.step_trace is not None and rank == 0:
-        import json as _json
-
-        gt = eng.gpu_trace
-        gpu = [(a.elapsed_time(b), (gt[i - 1][1].elapsed_time(a) if i else 0.0))
-               for i, (a, b) in enumerate(gt)]
-        with open(os.environ["OMNIA_STEP_TRACE"], "w") as f:
-            _json.dump({"host": eng.step_trace, "gpu_ms_and_gap": gpu}, f)
 
     out_tokens = sum(r[2] for r in results)
     ttfts = [r[0] for r in results if r[0] is not None]
     lats = [r[1] for r in results if r[1] is not None]
-    stats = torch.tensor([elapsed, float(out_tokens)], dtype=torch.float64)
+    # inter-token latency: mean gap per turn (TPOT) and every gap between frames
+    tpot = [(r[1] - r[0]) / (r[2] - 1) for r in results if r[2] > 1 and r[0] is not None]
+    gaps = []
+    for r in results:
+        ct = r[4]
+        gaps.extend(ct[i] - ct[i - 1] for i in range(1, len(ct)))
+    my_rate = out_tokens / elapsed if elapsed > 0 else 0.0
     if ws > 1:
-        t = stats.clone().cuda() if (use_gpu and not proc) else stats.clone()
-        mx = t.clone()
+        stats = torch.tensor([elapsed, float(out_tokens)], dtype=torch.float64)
+        if not (host_only or not use_gpu):
+            stats = stats.cuda()
+        mx, sm = stats.clone(), stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed = float(mx[0])
-        out_tokens = float(sm[1])
+        elapsed, out_tokens = float(mx[0]), float(sm[1])
         gathered = [None] * ws
-        dist.all_gather_object(gathered, (ttfts, lats))
-        ttfts = [x for gg in gathered for x in gg[0]]
-        lats = [x for gg in gathered for x in gg[1]]
+        dist.all_gather_object(gathered, (ttfts, lats, tpot, gaps[:20000], round(my_rate, 2)))
+        ttfts = [x for g in gathered for x in g[0]]
+        lats = [x for g in gathered for x in g[1]]
+        tpot = [x for g in gathered for x in g[2]]
+        gaps = [x for g in gathered for x in g[3]]
+        per_rank = [g[4] for g in gathered]
+    else:
+        per_rank = [round(my_rate, 2)]
     value = out_tokens / elapsed
-    st = engine_stats()
-    if runtime is not None:
-        runtime.close()
+    st = drv.engine_stats() if isinstance(drv, LocalDriver) else None
     if rank == 0:
+        ms = lambda x: round(1000 * x, 2) if x is not None else None  # noqa: E731
         rec = {
             "metric": BASELINE_METRIC,
             "value": round(value, 2),
@@ -208,39 +422,43 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (random prompt token ids, random-init weights of the named "
-                    "architecture, ignore_eos)",
-            "p50_turn_latency_ms": round(1000 * statistics.median(lats), 2) if lats else None,
-            "p95_turn_latency_ms": round(1000 * sorted(lats)[int(0.95 * (len(lats) - 1))], 2)
-            if lats else None,
-            "p50_ttft_ms": round(1000 * statistics.median(ttfts), 2) if ttfts else None,
+            "data": "synthetic (random text prompts of exactly prompt_len tokens after the "
+                    "chat template, random-init weights of the named architecture, ignore_eos)",
+            "world_size": ws,
+            "per_rank_tokens_per_s": per_rank,
+            "p50_turn_latency_ms": ms(statistics.median(lats)) if lats else None,
+            "p95_turn_latency_ms": ms(pct(lats, 0.95)),
+            "p50_ttft_ms": ms(statistics.median(ttfts)) if ttfts else None,
+            "p95_ttft_ms": ms(pct(ttfts, 0.95)),
+            "p50_tpot_ms": ms(pct(tpot, 0.5)),
+            "p95_tpot_ms": ms(pct(tpot, 0.95)),
+            "p95_frame_gap_ms": ms(pct(gaps, 0.95)),
+            "turns": len(lats),
             "config": {
                 "model": a.model,
-                "global_batch": C * ws,
+                "global_batch": a.concurrency * (ws // a.tp),
                 "seq_len": a.prompt_len + a.gen_len,
                 "prompt_len": a.prompt_len,
                 "gen_len": a.gen_len,
-                "concurrency_per_gpu": C,
-                "parallelism": f"dp{ws}",
+                "concurrency_per_replica": a.concurrency,
+                "parallelism": f"dp{ws // a.tp}" + (f"-tp{a.tp}" if a.tp > 1 else ""),
                 "path": a.path,
-                "engine_process": proc,
-                "tp": 1,
+                "arrival": a.arrival if a.arrival == "closed" else f"poisson@{a.rate}/s",
+                "stream_interval_ms": a.stream_interval_ms,
+                "tp": a.tp,
                 "hip_graphs": not a.no_graphs,
             },
-            "engine": {
-                "kv_blocks": st["kv_blocks"],
-                "block_size": st["block_size"],
+        }
+        if st is not None:
+            rec["engine"] = {
+                "kv_blocks": st["kv_blocks"], "block_size": st["block_size"],
                 "prefill_steps": st["counters"]["steps_prefill"],
                 "decode_steps": st["counters"]["steps_decode"],
                 "graph_captures": st["runner"]["captures"],
                 "host_timing_s": {**{k: round(v, 3) for k, v in st["timing"].items()},
                                   "gil_wait_s": round(st["runner"]["gil_wait_s"], 3)},
-            },
-        }
+            }
         print(json.dumps(rec), flush=True)
-    if ws > 1:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

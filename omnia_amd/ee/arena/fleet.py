@@ -13,21 +13,28 @@ import aiohttp
 
 
 class FleetSession:
+    """One virtual user's WebSocket conversation.  ``http``: a shared
+    :class:`aiohttp.ClientSession` (load generators open hundreds of sessions
+    through one connector); otherwise the session owns its own."""
+
     def __init__(self, url: str, agent: str = "", headers: dict | None = None,
-                 timeout_s: float = 120.0):
+                 timeout_s: float = 120.0, http: aiohttp.ClientSession | None = None):
         self.url = url
         self.agent = agent
         self.headers = headers or {}
         self.timeout_s = timeout_s
+        self._shared = http
         self._http = None
         self.ws = None
         self.session_id = ""
 
     async def __aenter__(self):
-        self._http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None))
+        if self._shared is None:
+            self._http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None))
+        http = self._shared or self._http
         url = self.url + (("&" if "?" in self.url else "?") + f"agent={self.agent}"
                           if self.agent else "")
-        self.ws = await self._http.ws_connect(url, headers=self.headers, max_msg_size=0)
+        self.ws = await http.ws_connect(url, headers=self.headers, max_msg_size=0)
         hello = await self.ws.receive_json(timeout=self.timeout_s)
         if hello.get("type") != "connected":
             raise RuntimeError(f"facade handshake failed: {hello}")
@@ -46,6 +53,7 @@ class FleetSession:
         await self.ws.send_json({"type": "message", "content": content,
                                  "metadata": metadata or {}})
         ttft, text, usage = None, [], {}
+        stamps = []  # arrival time of every streamed chunk (inter-token latency)
         while True:
             msg = await self.ws.receive(timeout=self.timeout_s)
             if msg.type != aiohttp.WSMsgType.TEXT:
@@ -53,8 +61,10 @@ class FleetSession:
             f = json.loads(msg.data)
             t = f.get("type")
             if t == "chunk":
+                now = time.perf_counter()
                 if ttft is None:
-                    ttft = time.perf_counter() - t0
+                    ttft = now - t0
+                stamps.append(now - t0)
                 text.append(f.get("content", ""))
             elif t == "tool_call":
                 tc = f["tool_call"]
@@ -70,7 +80,7 @@ class FleetSession:
                 final = f.get("content") or "".join(text)
                 usage = f.get("usage") or {}
                 return {"content": final, "ttft_ms": ttft * 1e3, "latency_ms": lat * 1e3,
-                        "usage": usage}
+                        "usage": usage, "chunk_times_s": stamps}
             elif t == "error":
                 err = f.get("error") or {}
                 raise RuntimeError(f"{err.get('code')}: {err.get('message')}")

@@ -1,0 +1,201 @@
+"""Agent pods as OS processes on this node (the single-node kubelet's pod model).
+
+An AgentRuntime pod is two containers (``internal/controller/deployment_builder.go``):
+the runtime (``python -m omnia_amd.runtime``: gRPC :9000, health :9001, which in
+turn starts its engine-core child on the pod's GPU) and the facade
+(``python -m omnia_amd.facade``: WebSocket/REST on :8080, dialing the runtime
+over gRPC).  :class:`ProcessPod` runs exactly those two entrypoints as child
+processes with the container env the operator built, on free local ports:
+
+* the pod's GPU is pinned with ``HIP_VISIBLE_DEVICES`` (the kubelet's device
+  plugin equivalent), so the runtime's engine sees it as ``cuda:0``;
+* each container gets its own process group; stopping the pod sends SIGTERM to
+  the group (graceful drain in both entrypoints) and SIGKILL after a grace
+  period, so the engine-core grandchild never outlives its runtime;
+* readiness = runtime ``/readyz`` (engine loaded and healthy), then facade
+  ``/readyz``; the facade is started only once the runtime is ready (the
+  reference's facade retries its dial instead, ``cmd/agent/runtime_dial.go``).
+
+Nothing here touches the GPU itself, so a parent that will later fork GPU
+workers (the bench, the operator) stays safe.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import signal
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+import urllib.error
+import urllib.request
+
+log = logging.getLogger("omnia.pods")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _get(url: str, timeout: float = 2.0) -> tuple[int, dict]:
+    try:
+        with urllib.request.urlopen(url, timeout=timeout) as r:
+            return r.status, json.loads(r.read() or b"{}")
+    except urllib.error.HTTPError as e:
+        return e.code, {}
+    except (OSError, ValueError):
+        return 0, {}
+
+
+class PodFailed(RuntimeError):
+    pass
+
+
+class ProcessPod:
+    def __init__(self, name: str, runtime_env: dict, facade_env: dict,
+                 device_index: int | list | None = None, log_dir: str | None = None,
+                 python: str = sys.executable, tp: int = 1):
+        self.name = name
+        self.runtime_env = dict(runtime_env)
+        self.facade_env = dict(facade_env)
+        if isinstance(device_index, int):
+            device_index = [device_index]
+        self.devices = list(device_index) if device_index is not None else None
+        self.tp = tp
+        self.log_dir = log_dir or tempfile.mkdtemp(prefix=f"omnia-pod-{name}-")
+        os.makedirs(self.log_dir, exist_ok=True)
+        self.python = python
+        self.grpc_port = self.health_port = self.facade_port = None
+        self.runtime: subprocess.Popen | None = None
+        self.facade: subprocess.Popen | None = None
+        self._logs = []
+
+    # ------------------------------------------------------------ lifecycle
+    def _spawn(self, module: str, env: dict, tag: str, launcher: list | None = None
+               ) -> subprocess.Popen:
+        full = dict(os.environ)
+        full.update({k: str(v) for k, v in env.items()})
+        full["PYTHONPATH"] = ROOT + os.pathsep + full.get("PYTHONPATH", "")
+        full.setdefault("PYTHONUNBUFFERED", "1")
+        if self.devices is not None:
+            full["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in self.devices)
+            full.pop("CUDA_VISIBLE_DEVICES", None)
+            full.pop("ROCR_VISIBLE_DEVICES", None)
+        # a pod is never a torchrun rank itself
+        for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                  "TORCHELASTIC_RUN_ID"):
+            if k not in env:
+                full.pop(k, None)
+        path = os.path.join(self.log_dir, f"{tag}.log")
+        f = open(path, "wb")
+        self._logs.append(f)
+        return subprocess.Popen([self.python] + (launcher or []) + ["-m", module], env=full,
+                                stdout=f, stderr=subprocess.STDOUT, cwd=ROOT,
+                                start_new_session=True)
+
+    def start_runtime(self):
+        self.grpc_port = int(self.runtime_env.get("OMNIA_GRPC_PORT") or free_port())
+        self.health_port = int(self.runtime_env.get("OMNIA_HEALTH_PORT") or free_port())
+        env = {**self.runtime_env, "OMNIA_GRPC_PORT": self.grpc_port,
+               "OMNIA_HEALTH_PORT": self.health_port}
+        launcher = None
+        if self.tp > 1:
+            # one runtime process per GPU of the pod; TP rank 0 serves gRPC
+            # (``omnia_amd/runtime/__main__.py``); torchrun's agent itself never
+            # touches a GPU, it only starts the ranks
+            env["OMNIA_ENGINE_TP"] = self.tp
+            launcher = ["-m", "torch.distributed.run", "--nnodes=1",
+                        f"--nproc-per-node={self.tp}", "--master-addr=127.0.0.1",
+                        f"--master-port={free_port()}"]
+        self.runtime = self._spawn("omnia_amd.runtime", env, "runtime", launcher)
+
+    def start_facade(self):
+        self.facade_port = int(self.facade_env.get("OMNIA_FACADE_PORT") or free_port())
+        env = {**self.facade_env, "OMNIA_FACADE_PORT": self.facade_port,
+               "OMNIA_RUNTIME_ADDRESS": f"127.0.0.1:{self.grpc_port}"}
+        self.facade = self._spawn("omnia_amd.facade", env, "facade")
+
+    def log_tail(self, tag: str, n: int = 4000) -> str:
+        try:
+            with open(os.path.join(self.log_dir, f"{tag}.log"), "rb") as f:
+                f.seek(0, 2)
+                f.seek(max(0, f.tell() - n))
+                return f.read().decode(errors="replace")
+        except OSError:
+            return ""
+
+    def _wait(self, proc, url: str, tag: str, deadline: float):
+        while time.monotonic() < deadline:
+            if proc.poll() is not None:
+                raise PodFailed(f"pod {self.name}: {tag} exited with {proc.returncode}:\n"
+                                + self.log_tail(tag))
+            st, body = _get(url)
+            if st == 200:
+                return
+            time.sleep(0.25)
+        raise PodFailed(f"pod {self.name}: {tag} not ready after timeout:\n" + self.log_tail(tag))
+
+    def start(self, timeout_s: float = 600.0) -> "ProcessPod":
+        deadline = time.monotonic() + timeout_s
+        self.start_runtime()
+        try:
+            self._wait(self.runtime, f"http://127.0.0.1:{self.health_port}/readyz", "runtime",
+                       deadline)
+            self.start_facade()
+            self._wait(self.facade, f"http://127.0.0.1:{self.facade_port}/readyz", "facade",
+                       deadline)
+        except BaseException:
+            self.stop()
+            raise
+        log.info("pod %s ready: ws://127.0.0.1:%d/ws (runtime gRPC :%d)", self.name,
+                 self.facade_port, self.grpc_port)
+        return self
+
+    @property
+    def ws_url(self) -> str:
+        return f"ws://127.0.0.1:{self.facade_port}/ws"
+
+    @property
+    def endpoint(self) -> str:
+        return f"127.0.0.1:{self.facade_port}"
+
+    def alive(self) -> bool:
+        return all(p is not None and p.poll() is None for p in (self.runtime, self.facade))
+
+    def stop(self, grace_s: float = 15.0):
+        procs = [p for p in (self.facade, self.runtime) if p is not None]
+        for p in procs:  # facade first: it drains in-flight turns against the runtime
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+            try:
+                p.wait(timeout=grace_s)
+            except subprocess.TimeoutExpired:
+                pass
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)  # stragglers incl. the engine-core child
+            except ProcessLookupError:
+                pass
+            try:
+                p.wait(timeout=5)
+            except subprocess.TimeoutExpired:
+                pass
+        for f in self._logs:
+            f.close()
+        self._logs.clear()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()

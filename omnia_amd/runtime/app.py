@@ -190,7 +190,7 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
                               sample_rate=int(aud.get("sampleRate", 16000)),
                               codec=aud.get("codec", "pcm"), channels=int(aud.get("channels", 1)))
     return RuntimeService(agent, capabilities=list(CAPABILITIES), invoke_agent=invoke_agent,
-                          duplex=duplex)
+                          duplex=duplex, stream_interval_s=cfg.stream_interval_ms / 1000.0)
 
 
 async def run(cfg: RuntimeConfig | None = None):

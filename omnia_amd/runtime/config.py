@@ -48,6 +48,7 @@ class RuntimeConfig:
     tracing_enabled: bool = False
     tracing_endpoint: str = ""
     tracing_sample_rate: float = 1.0
+    stream_interval_ms: float = 0.0  # Converse text-delta coalescing window (0 = per delta)
     grpc_port: int = 9000
     health_port: int = 9001
     engine: dict = field(default_factory=dict)
@@ -101,6 +102,7 @@ class RuntimeConfig:
         c.tracing_enabled = e.get("OMNIA_TRACING_ENABLED", "false").lower() == "true"
         c.tracing_endpoint = e.get("OMNIA_TRACING_ENDPOINT", "")
         c.tracing_sample_rate = float(e.get("OMNIA_TRACING_SAMPLE_RATE", "1.0"))
+        c.stream_interval_ms = float(e.get("OMNIA_STREAM_INTERVAL_MS", "0") or 0)
         c.grpc_port = int(e.get("OMNIA_GRPC_PORT", c.grpc_port))
         c.health_port = int(e.get("OMNIA_HEALTH_PORT", c.health_port))
         c.engine = {k[len("OMNIA_ENGINE_"):].lower(): v for k, v in e.items()
@@ -122,6 +124,8 @@ class RuntimeConfig:
         }
         if self.context_url:
             env["OMNIA_CONTEXT_URL"] = self.context_url
+        if self.stream_interval_ms:
+            env["OMNIA_STREAM_INTERVAL_MS"] = str(self.stream_interval_ms)
         if self.extra_providers:
             env["OMNIA_EXTRA_PROVIDERS_JSON"] = json.dumps(self.extra_providers)
         if self.duplex:

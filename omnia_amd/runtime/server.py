@@ -86,16 +86,58 @@ class QueueStream(Stream):
 
 
 class _GrpcTurnIO(TurnIO):
-    def __init__(self, stream: Stream, pending_msgs: list):
+    """Turn output onto the Converse stream.
+
+    ``interval_s`` > 0 coalesces text deltas: the first delta of a turn goes out
+    at once (TTFT is unaffected), later deltas are sent at most once per
+    interval as one Chunk with their concatenated text (a timer flushes a
+    partial buffer, so no text waits longer than the interval).  Every other
+    frame (tool calls, Done, Error) first flushes the buffer, so frame order is
+    the order of the deltas.  ``interval_s`` = 0 sends one Chunk per delta
+    (the reference's behaviour, ``internal/runtime/server.go:742-760``)."""
+
+    def __init__(self, stream: Stream, pending_msgs: list, interval_s: float = 0.0):
         self.stream = stream
         self.pending = pending_msgs
         self.nchunks = 0
+        self.interval = interval_s
+        self.buf: list[str] = []
+        self.last = -1e9
+        self.timer = None
+        self.lock = asyncio.Lock()
 
     async def chunk(self, text: str) -> None:
-        self.nchunks += 1
-        await self.stream.send(pb.ServerMessage(chunk=pb.Chunk(content=text)))
+        if self.interval <= 0:
+            self.nchunks += 1
+            await self.stream.send(pb.ServerMessage(chunk=pb.Chunk(content=text)))
+            return
+        self.buf.append(text)
+        wait = self.interval - (time.monotonic() - self.last)
+        if wait <= 0:
+            await self.flush()
+        elif self.timer is None:
+            self.timer = asyncio.get_running_loop().call_later(wait, self._on_timer)
+
+    def _on_timer(self):
+        self.timer = None
+        if self.buf:
+            asyncio.ensure_future(self.flush())
+
+    async def flush(self) -> None:
+        async with self.lock:
+            if self.timer is not None:
+                self.timer.cancel()
+                self.timer = None
+            if not self.buf:
+                return
+            text = "".join(self.buf)
+            self.buf.clear()
+            self.last = time.monotonic()
+            self.nchunks += 1
+            await self.stream.send(pb.ServerMessage(chunk=pb.Chunk(content=text)))
 
     async def client_tool_calls(self, calls: list[ToolCallReq], meta: dict) -> dict:
+        await self.flush()
         for c in calls:
             m = meta.get(c.id, {})
             await self.stream.send(pb.ServerMessage(tool_call=pb.ToolCall(
@@ -120,8 +162,10 @@ class _GrpcTurnIO(TurnIO):
 
 class RuntimeService:
     def __init__(self, agent: Agent, capabilities: list[str] | None = None,
-                 invoke_agent: Agent | None = None, duplex=None):
+                 invoke_agent: Agent | None = None, duplex=None, stream_interval_s: float = 0.0):
         self.agent = agent
+        # text-delta coalescing window of Converse streams (OMNIA_STREAM_INTERVAL_MS)
+        self.stream_interval_s = stream_interval_s
         self.invoke_agent = invoke_agent or agent
         self.capabilities = list(capabilities or CAPABILITIES)
         self.duplex = duplex  # DuplexConfig when STT + TTS providers are configured
@@ -228,20 +272,23 @@ class RuntimeService:
         metadata = dict(msg.metadata)
         if msg.consent_grants:
             metadata["consent_grants"] = ",".join(msg.consent_grants)
-        io = _GrpcTurnIO(stream, pending)
+        io = _GrpcTurnIO(stream, pending, self.stream_interval_s)
         tp = tracing.parse_traceparent(md.get("traceparent"))
         span = tracing.start_span("omnia.runtime.message", {"session.id": sid},
                                   trace_id=tracing.session_trace_id(sid), link=tp)
         try:
             res = await self.agent.run_turn(sid, content, io, parts=parts, metadata=metadata,
                                             ctx=ctx)
+            await io.flush()
         except ProviderError as e:  # coded provider failure (e.g. ENGINE_FAULT)
+            await io.flush()
             log.error("turn failed for session %s: %s (%s)", sid, e, e.code)
             tracing.end_span(span, error=True)
             await stream.send(pb.ServerMessage(error=pb.Error(code=e.code,
                                                               message=GENERIC_ERROR)))
             return
         except Exception:  # noqa: BLE001 - never leak provider details
+            await io.flush()
             log.exception("turn failed for session %s", sid)
             tracing.end_span(span, error=True)
             await stream.send(pb.ServerMessage(error=pb.Error(code="INTERNAL_ERROR",

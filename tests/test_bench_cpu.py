@@ -1,0 +1,40 @@
+"""bench.py contract on CPU: the WebSocket pod path (facade + runtime processes),
+``--gpus N`` spawning N rank processes itself, and the aggregated JSON line."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, timeout=300):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu",
+                        "--model", "tiny-llama", "--prompt-len", "96", "--gen-len", "6",
+                        "--warmup", "1", *args], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_ws_path_two_ranks_spawned_by_bench():
+    rec = _bench("--gpus", "2", "--concurrency", "3", "--steps", "2")
+    assert rec["n_gpus"] == 2 and rec["world_size"] == 2
+    assert len(rec["per_rank_tokens_per_s"]) == 2 and all(v > 0 for v in
+                                                          rec["per_rank_tokens_per_s"])
+    assert rec["config"]["path"] == "ws" and rec["config"]["parallelism"] == "dp2"
+    assert rec["turns"] == 2 * 2 * 3
+    # every turn streamed gen_len tokens: value = tokens / elapsed of the slowest rank
+    tokens = 2 * 2 * 3 * 6
+    assert abs(rec["value"] - tokens / (rec["ms_per_step"] * rec["steps"] / 1000)) < 1.0
+
+
+def test_open_loop_poisson_reports_latency_percentiles():
+    rec = _bench("--concurrency", "4", "--steps", "1", "--arrival", "poisson", "--rate", "40",
+                 "--stream-interval-ms", "0")
+    assert rec["config"]["arrival"].startswith("poisson")
+    assert rec["turns"] == 4 and rec["p95_tpot_ms"] is not None and rec["p95_ttft_ms"]

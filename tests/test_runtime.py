@@ -248,3 +248,34 @@ def test_local_engine_provider_end_to_end_cpu():
         assert eng.engine.blocks.stats["prefix_hit_tokens"] > 0
     finally:
         eng.shutdown()
+
+
+def test_stream_interval_coalesces_chunks():
+    """OMNIA_STREAM_INTERVAL_MS: the first delta goes out at once, later deltas are
+    merged per window, the text is complete and ends before Done."""
+    words = " ".join(f"w{i}" for i in range(30))
+
+    async def run(interval):
+        prov = MockProvider(scenarios={"default_response": words}, delay_s=0.004)
+        agent = Agent(PromptPack.minimal("sys"), prov, MemoryContextStore(), None, AgentConfig())
+        svc = RuntimeService(agent, stream_interval_s=interval)
+        st = QueueStream({"x-omnia-session-id": "s"})
+        task = asyncio.ensure_future(svc.converse(st))
+        await st.inbox.put(pb.ClientMessage(session_id="s", content="hi"))
+        chunks = []
+        while True:
+            f = await st.outbox.get()
+            k = f.WhichOneof("message")
+            if k == "chunk":
+                chunks.append(f.chunk.content)
+            elif k == "done":
+                break
+        st.close()
+        await task
+        return chunks
+
+    per_delta = _run_sync(run(0.0))
+    merged = _run_sync(run(0.03))
+    assert len(per_delta) == 30 and "".join(per_delta) == words
+    assert "".join(merged) == words and merged[0] == "w0"
+    assert 2 <= len(merged) < 15

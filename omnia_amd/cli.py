@@ -156,7 +156,9 @@ async def serve(port: int, manifests: list[str], engine: bool, host: str = "127.
         from .runtime.app import shared_engine
 
         factory = shared_engine
-    launcher = LocalLauncher(store, engine_factory=factory)
+    # every replica is a pod of OS processes with its own GPU(s)
+    launcher = LocalLauncher(store, engine_factory=factory, mode="process",
+                             gpu_count=gpus or 0)
     launcher.start()
     for d in load_manifests(manifests):
         try:

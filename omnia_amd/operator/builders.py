@@ -139,12 +139,14 @@ def config_hash(*parts) -> str:
 
 
 def deployment(ar: dict, rc: RuntimeConfig, pack_cm: str, track: str = "stable",
-               replicas: int | None = None, extra_hash=None) -> dict:
+               replicas: int | None = None, extra_hash=None,
+               facade_extra: dict | None = None) -> dict:
     spec, md = ar["spec"], ar["metadata"]
     rt = spec.get("runtime") or {}
     po = spec.get("podOverrides") or {}
     name = md["name"] + ("" if track == "stable" else "-candidate")
     fenv = facade_env(ar)
+    fenv.update(facade_extra or {})
     renv = rc.to_env()
     for e in rt.get("extraEnv") or []:
         renv[e["name"]] = e.get("value", "")

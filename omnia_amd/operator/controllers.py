@@ -15,6 +15,7 @@ from ..api import crds
 from ..models.config import REGISTRY as MODEL_REGISTRY
 from ..runtime.promptpack import PackError, PromptPack
 from . import builders as B
+from .chart import COMPONENTS
 from .apistore import APIStore, NotFound, get_condition, owner_ref, set_condition
 
 log = logging.getLogger("omnia.operator")
@@ -187,6 +188,18 @@ class ToolRegistryReconciler:
 
 
 # ===================================================================== AgentRuntime
+def workspace_service_group(store: APIStore, ns: str, group: str) -> dict | None:
+    """The ServiceGroupStatus of the Workspace that owns namespace ``ns``
+    (``resolveSessionURLForWorkspace``, ``internal/controller/eval_worker.go:434``)."""
+    for ws in store.list("Workspace"):
+        if ((ws.get("spec") or {}).get("namespace") or {}).get("name") != ns:
+            continue
+        for sg in (ws.get("status") or {}).get("services") or []:
+            if sg.get("name") == group:
+                return {**sg, "_workspace": ws["metadata"]["name"]}
+    return None
+
+
 class AgentRuntimeReconciler:
     kind = "AgentRuntime"
 
@@ -276,6 +289,20 @@ class AgentRuntimeReconciler:
         set_condition(st, "CapabilitiesSatisfied", cap_ok,
                       "CapabilitiesSatisfied" if cap_ok else "CapabilitiesMissing",
                       "" if cap_ok else "insufficient GPUs for engine.tp", gen)
+        # ---- workspace service group: session-api / memory-api endpoints
+        facade_extra = {}
+        sg = workspace_service_group(store, ns, spec.get("serviceGroup") or "default")
+        if sg is not None:
+            if sg.get("sessionURL"):
+                rc.session_api_url = sg["sessionURL"]
+                facade_extra["OMNIA_SESSION_API_URL"] = sg["sessionURL"]
+            if rc.memory_enabled and sg.get("memoryURL"):
+                rc.memory_api_url = sg["memoryURL"]
+            if not rc.workspace:
+                rc.workspace = sg.get("_workspace", "")
+        elif spec.get("serviceGroup"):
+            set_condition(st, "ServiceGroupReady", False, "NotFound",
+                          f"service group {spec['serviceGroup']!r} not found", gen)
         # ---- owned objects
         store.apply(B.tools_configmap(ar, registry))
         pack_cm = pack["spec"]["source"].get("configMapRef", {}).get("name", "")
@@ -285,7 +312,8 @@ class AgentRuntimeReconciler:
             if cur is not None:
                 replicas = cur["spec"].get("replicas")
         dep = B.deployment(ar, rc, pack_cm, "stable", replicas,
-                           extra_hash=[pack["spec"]["version"], (registry or {}).get("spec")])
+                           extra_hash=[pack["spec"]["version"], (registry or {}).get("spec")],
+                           facade_extra=facade_extra)
         store.apply(dep)
         store.apply(B.service(ar))
         want_r = dep["spec"]["replicas"]
@@ -472,36 +500,66 @@ class WorkspaceReconciler:
                          "spec": {"accessModes": stor.get("accessModes", ["ReadWriteMany"]),
                                   "resources": {"requests": {"storage": stor.get("size",
                                                                                  "10Gi")}}}})
-        groups = {}
+        groups = []
         for sg in spec.get("services") or [{"name": "default"}]:
             g = sg.get("name", "default")
+            if sg.get("mode") == "external":
+                ext = sg.get("external") or {}
+                groups.append({"name": g, "sessionURL": ext.get("sessionURL", ""),
+                               "memoryURL": ext.get("memoryURL", ""), "ready": True})
+                continue
+            urls = {}
+            ready = True
             for svc in ("session-api", "memory-api"):
                 dn = f"{svc}-{name}-{g}"
+                cmd, _, _ = COMPONENTS[svc]
+                cfg = sg.get("session" if svc == "session-api" else "memory") or {}
+                args = list(cmd[3:]) + ["--port", "8080"]
+                redis = (cfg.get("redis") or sg.get("redis") or {}).get("url")
+                if redis:
+                    args += ["--redis-url" if svc == "session-api" else "--redis", redis]
                 store.apply({"apiVersion": "apps/v1", "kind": "Deployment",
                              "metadata": {"name": dn, "namespace": nsname,
                                           "labels": {"omnia.altairalabs.ai/component": svc,
-                                                     "omnia.altairalabs.ai/service-group": g},
+                                                     "omnia.altairalabs.ai/service-group": g,
+                                                     "omnia.altairalabs.ai/workspace": name},
                                           "ownerReferences": own},
-                             "spec": {"replicas": 1, "selector": {"matchLabels": {
-                                 "app": dn}}, "template": {"metadata": {"labels": {"app": dn}},
-                                                           "spec": {"containers": [{
-                                                               "name": svc,
-                                                               "image": f"omnia-{svc}"}]}}}})
+                             "spec": {"replicas": int(cfg.get("replicas", 1)),
+                                      "selector": {"matchLabels": {"app": dn}},
+                                      "template": {"metadata": {"labels": {"app": dn}},
+                                                   "spec": {"containers": [{
+                                                       "name": svc, "image": f"omnia-{svc}",
+                                                       "command": cmd[:3], "args": args,
+                                                       "ports": [{"name": "http",
+                                                                  "containerPort": 8080}],
+                                                       "readinessProbe": {"httpGet": {
+                                                           "path": "/healthz",
+                                                           "port": 8080}}}]}}}})
                 store.apply({"apiVersion": "v1", "kind": "Service",
                              "metadata": {"name": dn, "namespace": nsname,
                                           "ownerReferences": own},
                              "spec": {"selector": {"app": dn},
                                       "ports": [{"name": "http", "port": 8080}]}})
-            groups[g] = {"sessionURL": f"http://session-api-{name}-{g}.{nsname}:8080",
-                         "memoryURL": f"http://memory-api-{name}-{g}.{nsname}:8080"}
-        st["serviceGroups"] = groups
+                urls[svc] = f"http://{dn}.{nsname}:8080"
+                dep = store.try_get("Deployment", dn, nsname) or {}
+                if not (dep.get("status") or {}).get("readyReplicas"):
+                    ready = False
+            groups.append({"name": g, "sessionURL": urls["session-api"],
+                           "memoryURL": urls["memory-api"], "ready": ready})
+        # ServiceGroupStatus list (workspace_types.go:825)
+        st["services"] = groups
+        st.pop("serviceGroups", None)
+        all_ready = all(g["ready"] for g in groups)
         st["namespace"] = nsname
         st["phase"] = "Ready"
-        set_condition(st, "Ready", True, "Reconciled", "", ws["metadata"]["generation"])
-        st["observedGeneration"] = ws["metadata"]["generation"]
+        gen = ws["metadata"]["generation"]
+        set_condition(st, "Ready", True, "Reconciled", "", gen)
+        set_condition(st, "ServicesReady", all_ready,
+                      "AllServicesReady" if all_ready else "ServicesPending", "", gen)
+        st["observedGeneration"] = gen
         ws["status"] = st
         store.update_status(ws)
-        return None
+        return None if all_ready else 5.0  # re-check service readiness
 
 
 # ===================================================================== policies

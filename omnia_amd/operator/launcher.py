@@ -6,10 +6,20 @@ For every Deployment labelled ``app.kubernetes.io/managed-by=omnia-operator``
 and ``omnia.altairalabs.ai/component=agent`` it materialises the pod's mounts
 (PromptPack / tools ConfigMaps -> files), builds the runtime from the runtime
 container's env (``RuntimeConfig.from_env``) and the facade from the facade
-container's env, starts them in-process (one shared GPU engine per model) on
-free local ports, and writes back ``status.readyReplicas`` and the Service's
-``status.endpoint``.  Pod template changes (config-hash annotation) restart the
-pod; replicas=0 (scale-to-zero / capability gate) stops it.
+container's env, and starts them on free local ports.  Two pod models:
+
+* ``mode="process"`` (``omnia serve``): every replica is a real pod of OS
+  processes (:class:`~omnia_amd.operator.pods.ProcessPod`: ``python -m
+  omnia_amd.runtime`` + ``python -m omnia_amd.facade``), ``spec.replicas`` of
+  them; local-engine runtimes get their own GPU(s) from a node device
+  allocator (``OMNIA_ENGINE_TP`` GPUs each), like the device plugin would.
+* ``mode="inproc"``: one in-process runtime + facade per Deployment (tests;
+  one shared engine per model).
+
+It writes back ``status.readyReplicas`` and the Service's ``status.endpoint``
+(``status.endpoints`` lists every ready replica).  Pod template changes
+(config-hash annotation) restart the pods; replicas=0 (scale-to-zero /
+capability gate) stops them.
 """
 from __future__ import annotations
 
@@ -47,12 +57,53 @@ class Pod:
             await self.grpc.stop(0)
 
 
+class DeviceAllocator:
+    """GPUs of this node handed to pods (first-fit contiguous ranges, so a TP
+    group sits on neighbouring xGMI peers)."""
+
+    def __init__(self, count: int):
+        self.count = count
+        self.owner: list = [None] * count
+
+    def take(self, who, n: int) -> list[int] | None:
+        for start in range(0, self.count - n + 1):
+            if all(o is None for o in self.owner[start:start + n]):
+                for i in range(start, start + n):
+                    self.owner[i] = who
+                return list(range(start, start + n))
+        return None
+
+    def release(self, who):
+        self.owner = [None if o == who else o for o in self.owner]
+
+
+class _ProcReplica:
+    """One replica of a Deployment in process mode."""
+
+    def __init__(self, key, index, template_hash, pod, devices):
+        self.key = key
+        self.index = index
+        self.hash = template_hash
+        self.pod = pod
+        self.devices = devices
+        self.port = None
+        self.ready = False
+
+    async def stop(self):
+        await asyncio.get_running_loop().run_in_executor(None, self.pod.stop)
+
+
 class LocalLauncher:
-    def __init__(self, store: APIStore, engine_factory=None, use_grpc: bool = False):
+    def __init__(self, store: APIStore, engine_factory=None, use_grpc: bool = False,
+                 mode: str = "inproc", gpu_count: int = 0):
         self.store = store
         self.pods: dict[tuple, Pod] = {}
+        self.replicas: dict[tuple, list] = {}  # process mode: key -> [_ProcReplica]
+        self.services: dict[tuple, tuple] = {}  # (ns, name) -> (ServiceProcess, hash)
         self.engine_factory = engine_factory  # fn(engine_cfg) -> AsyncLLMEngine
         self.use_grpc = use_grpc
+        self.mode = mode
+        self.devices = DeviceAllocator(gpu_count)
         self.task = None
 
     def _materialise(self, dep: dict, pod: Pod):
@@ -104,18 +155,148 @@ class LocalLauncher:
         pod.port = await fac.start("127.0.0.1", 0)
         pod.facade = fac
 
+    # ------------------------------------------------------------ service pods
+    SERVICE_COMPONENTS = ("session-api", "memory-api")
+
+    async def _sync_services(self):
+        """Workspace session-api / memory-api Deployments as service processes."""
+        loop = asyncio.get_running_loop()
+        want = {}
+        for d in self.store.list("Deployment"):
+            comp = d["metadata"].get("labels", {}).get(B.LABEL_COMPONENT)
+            if comp in self.SERVICE_COMPONENTS and (d["spec"].get("replicas", 1) or 0) > 0:
+                want[(d["metadata"]["namespace"], d["metadata"]["name"])] = d
+        for key in list(self.services):
+            sp, h = self.services[key]
+            d = want.get(key)
+            if d is None or not sp.alive() or h != B.config_hash(d["spec"]["template"]):
+                self.services.pop(key)
+                await loop.run_in_executor(None, sp.stop)
+        for key, d in want.items():
+            if key not in self.services:
+                from .pods import ServiceProcess
+
+                c = d["spec"]["template"]["spec"]["containers"][0]
+                if not c.get("command"):
+                    continue
+                sp = ServiceProcess(key[1], c, tempfile.mkdtemp(prefix=f"omnia-{key[1]}-"))
+                try:
+                    await loop.run_in_executor(None, sp.start)
+                except Exception:  # noqa: BLE001
+                    log.exception("service %s/%s failed to start", *key)
+                    continue
+                self.services[key] = (sp, B.config_hash(d["spec"]["template"]))
+            sp = self.services[key][0]
+            st = d.get("status") or {}
+            if st.get("readyReplicas") != 1:
+                d["status"] = {**st, "replicas": 1, "readyReplicas": 1, "availableReplicas": 1,
+                               "observedGeneration": d["metadata"]["generation"]}
+                d["metadata"].pop("resourceVersion", None)
+                self.store.update_status(d)
+            svc = self.store.try_get("Service", key[1], key[0])
+            if svc is not None and (svc.get("status") or {}).get("endpoint") != sp.endpoint:
+                svc["status"] = {**(svc.get("status") or {}), "endpoint": sp.endpoint}
+                svc["metadata"].pop("resourceVersion", None)
+                self.store.update_status(svc)
+
+    # ------------------------------------------------------------ process mode
+    def _pod_envs(self, dep: dict, workdir: str) -> tuple[dict, dict]:
+        import types
+
+        paths = self._materialise(dep, types.SimpleNamespace(dir=workdir))
+        cs = {c["name"]: c for c in dep["spec"]["template"]["spec"]["containers"]}
+        renv = _env(cs["runtime"])
+        renv["OMNIA_PROMPTPACK_PATH"] = paths.get("/etc/omnia/pack", renv.get(
+            "OMNIA_PROMPTPACK_PATH", ""))
+        renv["OMNIA_TOOLS_CONFIG_PATH"] = paths.get("/etc/omnia/tools", "")
+        from .pods import resolve_service_urls
+
+        return (resolve_service_urls(renv, self._service_endpoint),
+                resolve_service_urls(_env(cs["facade"]), self._service_endpoint))
+
+    def _service_endpoint(self, name: str, ns: str) -> str | None:
+        svc = self.store.try_get("Service", name, ns)
+        return ((svc or {}).get("status") or {}).get("endpoint")
+
+    def _start_replica(self, dep: dict, key, index: int, thash) -> _ProcReplica:
+        from .pods import ProcessPod
+
+        workdir = tempfile.mkdtemp(prefix=f"omnia-{key[1]}-{index}-")
+        renv, fenv = self._pod_envs(dep, workdir)
+        rc_provider = (json.loads(renv.get("OMNIA_PROVIDER_JSON", "{}") or "{}").get("type")
+                       or renv.get("OMNIA_PROVIDER_TYPE", "mock"))
+        devices = None
+        who = (key, index)
+        if rc_provider in ("local", "engine", "omnia", "rocm") and self.devices.count:
+            tp = int(renv.get("OMNIA_ENGINE_TP", "1") or 1)
+            devices = self.devices.take(who, tp)
+            if devices is None:
+                raise RuntimeError(f"no {tp} free GPU(s) for {key[0]}/{key[1]} replica {index}")
+        for k in ("OMNIA_GRPC_PORT", "OMNIA_HEALTH_PORT"):
+            renv.pop(k, None)
+        fenv.pop("OMNIA_FACADE_PORT", None)
+        pod = ProcessPod(f"{key[1]}-{index}", renv, fenv, device_index=devices,
+                         log_dir=os.path.join(workdir, "logs"),
+                         tp=int(renv.get("OMNIA_ENGINE_TP", "1") or 1))
+        try:
+            pod.start(timeout_s=float(os.environ.get("OMNIA_POD_START_TIMEOUT", "900")))
+        except Exception:
+            self.devices.release(who)
+            raise
+        r = _ProcReplica(key, index, thash, pod, devices)
+        r.port = pod.facade_port
+        r.ready = True
+        return r
+
+    async def _sync_process(self, d: dict, key, replicas: int, thash) -> int:
+        loop = asyncio.get_running_loop()
+        cur = self.replicas.setdefault(key, [])
+        # template change: replace every replica
+        stale = [r for r in cur if r.hash != thash or not r.pod.alive()]
+        for r in stale:
+            cur.remove(r)
+            await r.stop()
+            self.devices.release((key, r.index))
+        while len(cur) > replicas:
+            r = cur.pop()
+            await r.stop()
+            self.devices.release((key, r.index))
+        used = {r.index for r in cur}
+        for i in range(replicas):
+            if len(cur) >= replicas:
+                break
+            if i in used:
+                continue
+            try:
+                r = await loop.run_in_executor(None, self._start_replica, d, key, i, thash)
+            except Exception:  # noqa: BLE001
+                log.exception("pod %s/%s replica %d failed to start", key[0], key[1], i)
+                continue
+            cur.append(r)
+        cur.sort(key=lambda r: r.index)
+        return sum(1 for r in cur if r.ready)
+
     async def sync(self):
         """One pass: converge running pods to the Deployments."""
         deps = [d for d in self.store.list("Deployment")
                 if d["metadata"].get("labels", {}).get(B.LABEL_MANAGED_BY) == "omnia-operator"
                 and d["metadata"].get("labels", {}).get(B.LABEL_COMPONENT) == "agent"]
         live = set()
+        if self.mode == "process":
+            await self._sync_services()
         for d in deps:
             ns, name = d["metadata"]["namespace"], d["metadata"]["name"]
             replicas = d["spec"].get("replicas", 1)
             thash = d["spec"]["template"]["metadata"].get("annotations", {}).get(
                 B.ANN_CONFIG_HASH)
             key = (ns, name)
+            if self.mode == "process":
+                want_n = int(replicas or 0)
+                if want_n > 0:
+                    live.add(key)
+                ready = await self._sync_process(d, key, want_n, thash)
+                self._write_status(d, ready, name, ns, key)
+                continue
             pod = self.pods.get(key)
             if replicas and replicas > 0:
                 live.add(key)
@@ -151,6 +332,30 @@ class LocalLauncher:
         for key in list(self.pods):
             if key not in live:
                 await self.pods.pop(key).stop()
+        for key in list(self.replicas):
+            if key not in live:
+                for r in self.replicas.pop(key):
+                    await r.stop()
+                    self.devices.release((key, r.index))
+
+    def _write_status(self, d: dict, ready: int, name: str, ns: str, key):
+        st = d.get("status") or {}
+        want = {"replicas": ready, "readyReplicas": ready, "availableReplicas": ready,
+                "observedGeneration": d["metadata"]["generation"]}
+        if any(st.get(k) != v for k, v in want.items()):
+            d["status"] = {**st, **want}
+            d["metadata"].pop("resourceVersion", None)
+            self.store.update_status(d)
+        track = d["metadata"].get("labels", {}).get(B.LABEL_TRACK, "stable")
+        svc = self.store.try_get("Service", name, ns) if track == "stable" else None
+        reps = [r for r in self.replicas.get(key, []) if r.ready]
+        if svc is not None and reps:
+            eps = [f"127.0.0.1:{r.port}" for r in reps]
+            cur = svc.get("status") or {}
+            if cur.get("endpoint") != eps[0] or cur.get("endpoints") != eps:
+                svc["status"] = {**cur, "endpoint": eps[0], "endpoints": eps}
+                svc["metadata"].pop("resourceVersion", None)
+                self.store.update_status(svc)
 
     async def run(self, interval: float = 0.2):
         q = self.store.watch("Deployment")
@@ -179,3 +384,11 @@ class LocalLauncher:
         for p in list(self.pods.values()):
             await p.stop()
         self.pods.clear()
+        for key, reps in list(self.replicas.items()):
+            for r in reps:
+                await r.stop()
+                self.devices.release((key, r.index))
+        self.replicas.clear()
+        for sp, _ in self.services.values():
+            sp.stop()
+        self.services.clear()

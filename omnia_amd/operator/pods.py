@@ -85,9 +85,15 @@ class ProcessPod:
         full["PYTHONPATH"] = ROOT + os.pathsep + full.get("PYTHONPATH", "")
         full.setdefault("PYTHONUNBUFFERED", "1")
         if self.devices is not None:
-            full["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in self.devices)
+            # indices are relative to what this process sees: map them through an
+            # inherited visibility list (a launcher may have restricted it)
+            vis = next((os.environ[k] for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+                        if os.environ.get(k)), None)
+            phys = [x.strip() for x in vis.split(",")] if vis else None
+            devs = [phys[d] if phys is not None and d < len(phys) else str(d)
+                    for d in self.devices]
+            full["HIP_VISIBLE_DEVICES"] = ",".join(devs)
             full.pop("CUDA_VISIBLE_DEVICES", None)
-            full.pop("ROCR_VISIBLE_DEVICES", None)
         # a pod is never a torchrun rank itself
         for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
                   "TORCHELASTIC_RUN_ID"):
@@ -199,3 +205,100 @@ class ProcessPod:
 
     def __exit__(self, *exc):
         self.stop()
+
+
+class ServiceProcess:
+    """A single-container service pod (workspace session-api / memory-api,
+    ``internal/controller/workspace_services.go``) as one OS process: the
+    container's ``command`` + ``args`` with its port rebound to a free local port
+    and ``/data`` mapped into a per-pod directory."""
+
+    def __init__(self, name: str, container: dict, workdir: str,
+                 python: str = sys.executable):
+        self.name = name
+        self.container = container
+        self.workdir = workdir
+        self.python = python
+        self.port = None
+        self.proc: subprocess.Popen | None = None
+        self._log = None
+
+    def argv(self) -> list[str]:
+        cmd = list(self.container.get("command") or []) + list(self.container.get("args") or [])
+        if cmd and cmd[0] in ("python", "python3"):
+            cmd[0] = self.python
+        out, i = [], 0
+        data = os.path.join(self.workdir, "data")
+        os.makedirs(data, exist_ok=True)
+        while i < len(cmd):
+            a = cmd[i]
+            if a == "--port" and i + 1 < len(cmd):
+                out += ["--port", str(self.port)]
+                i += 2
+                continue
+            out.append(a.replace("/data/", data + "/") if a.startswith("/data/") else a)
+            i += 1
+        if "--port" not in out:
+            out += ["--port", str(self.port)]
+        return out
+
+    def start(self, timeout_s: float = 60.0) -> "ServiceProcess":
+        self.port = free_port()
+        env = dict(os.environ)
+        env.update({e["name"]: str(e.get("value", "")) for e in self.container.get("env", [])})
+        env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+        os.makedirs(self.workdir, exist_ok=True)
+        self._log = open(os.path.join(self.workdir, "service.log"), "wb")
+        self.proc = subprocess.Popen(self.argv(), env=env, stdout=self._log,
+                                     stderr=subprocess.STDOUT, cwd=ROOT, start_new_session=True)
+        path = ((self.container.get("readinessProbe") or {}).get("httpGet") or {}).get(
+            "path", "/healthz")
+        deadline = time.monotonic() + timeout_s
+        while time.monotonic() < deadline:
+            if self.proc.poll() is not None:
+                raise PodFailed(f"service {self.name} exited with {self.proc.returncode}")
+            if _get(f"http://127.0.0.1:{self.port}{path}")[0] == 200:
+                return self
+            time.sleep(0.2)
+        self.stop()
+        raise PodFailed(f"service {self.name} not ready")
+
+    @property
+    def endpoint(self) -> str:
+        return f"127.0.0.1:{self.port}"
+
+    def alive(self) -> bool:
+        return self.proc is not None and self.proc.poll() is None
+
+    def stop(self, grace_s: float = 10.0):
+        if self.proc is not None and self.proc.poll() is None:
+            try:
+                os.killpg(self.proc.pid, signal.SIGTERM)
+                self.proc.wait(timeout=grace_s)
+            except (ProcessLookupError, subprocess.TimeoutExpired):
+                try:
+                    os.killpg(self.proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+        if self._log is not None:
+            self._log.close()
+            self._log = None
+
+
+_SVC_URL = None
+
+
+def resolve_service_urls(env: dict, lookup) -> dict:
+    """Cluster DNS for a single node: rewrite ``http://<svc>.<ns>[.svc...]:<port>``
+    in env values to the local endpoint ``lookup(svc, ns)`` returns (or leave it)."""
+    import re
+
+    global _SVC_URL
+    if _SVC_URL is None:
+        _SVC_URL = re.compile(r"(https?://)([a-z0-9-]+)\.([a-z0-9-]+)(?:\.svc[.a-z0-9-]*)?:\d+")
+
+    def sub(m):
+        ep = lookup(m.group(2), m.group(3))
+        return f"{m.group(1)}{ep}" if ep else m.group(0)
+
+    return {k: _SVC_URL.sub(sub, v) if isinstance(v, str) else v for k, v in env.items()}

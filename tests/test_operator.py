@@ -244,9 +244,15 @@ def test_workspace_reconcile():
     store = asyncio.run(go())
     w = store.get("Workspace", "team-a", None)
     assert w["status"]["phase"] == "Ready"
-    assert set(w["status"]["serviceGroups"]) == {"default", "gold"}
+    groups = {g["name"]: g for g in w["status"]["services"]}
+    assert set(groups) == {"default", "gold"}
+    assert groups["gold"]["sessionURL"] == "http://session-api-team-a-gold.team-a:8080"
+    assert not groups["gold"]["ready"]  # no launcher ran the service pods
+    assert get_condition(w, "ServicesReady")["status"] == "False"
     assert store.get("Namespace", "team-a", None)
-    assert store.get("Deployment", "session-api-team-a-gold", "team-a")
+    dep = store.get("Deployment", "session-api-team-a-gold", "team-a")
+    c = dep["spec"]["template"]["spec"]["containers"][0]
+    assert c["command"][-1] == "omnia_amd.session.api" and "--port" in c["args"]
     assert store.get("NetworkPolicy", "workspace-team-a-isolation", "team-a")
 
 
@@ -345,3 +351,106 @@ def test_rollout_traffic_routing_modes(monkeypatch):
     assert [r["weight"] for r in vs["spec"]["http"][0]["route"]] == [70, 30]
     assert dr["spec"]["trafficPolicy"]["loadBalancer"]["consistentHash"]["httpHeaderName"] == \
         "x-omnia-session-id"
+
+
+def test_process_pods_honour_replicas():
+    """Process pod model (omnia serve): each replica is facade + runtime OS
+    processes on its own ports; the Service lists every ready endpoint."""
+    docs = load_manifests([ECHO])
+    for d in docs:
+        if d["kind"] == "AgentRuntime":
+            d["spec"]["runtime"] = {"replicas": 2}
+
+    async def go():
+        store = new_store()
+        mgr = Manager(store)
+        await mgr.start()
+        launcher = LocalLauncher(store, mode="process")
+        launcher.start()
+        try:
+            for d in docs:
+                store.apply(d)
+            await mgr.settle(timeout=15, quiet=0.4)
+            eps = []
+            for _ in range(400):
+                svc = store.try_get("Service", "echo")
+                eps = ((svc or {}).get("status") or {}).get("endpoints") or []
+                if len(eps) == 2:
+                    break
+                await asyncio.sleep(0.1)
+            codes = []
+            async with aiohttp.ClientSession() as s:
+                for ep in eps:
+                    r = await s.get(f"http://{ep}/healthz")
+                    codes.append(r.status)
+            pids = [r.pod.runtime.pid for r in launcher.replicas[("default", "echo")]]
+            dep = store.get("Deployment", "echo")
+            return eps, codes, pids, dep["status"].get("readyReplicas")
+        finally:
+            await launcher.stop()
+            await mgr.stop()
+
+    eps, codes, pids, ready = asyncio.run(go())
+    assert len(eps) == 2 and len(set(eps)) == 2 and codes == [200, 200]
+    assert len(set(pids)) == 2 and ready == 2
+
+
+def test_process_mode_workspace_services_record_sessions():
+    """Workspace service group -> session-api process; an agent in the
+    workspace namespace gets its URL (local DNS) and the facade records turns."""
+    from omnia_amd.ee.arena.fleet import FleetSession
+
+    ws = {"apiVersion": crds.API_VERSION, "kind": "Workspace", "metadata": {"name": "team-b"},
+          "spec": {"displayName": "Team B", "namespace": {"name": "team-b"},
+                   "services": [{"name": "default"}]}}
+    docs = [ws] + load_manifests([ECHO])
+    for d in docs[1:]:
+        d["metadata"]["namespace"] = "team-b"
+        if d["kind"] == "AgentRuntime":
+            d["spec"] = {"facades": [{"type": "websocket"}], "promptPackRef": {"name": "echo-pack"},
+                         "providers": [{"providerRef": {"name": "echo-mock"}}]}
+
+    async def go():
+        store = new_store()
+        mgr = Manager(store)
+        await mgr.start()
+        launcher = LocalLauncher(store, mode="process")
+        launcher.start()
+        try:
+            for d in docs:
+                store.apply(d)
+            ep = None
+            for _ in range(600):
+                w = store.get("Workspace", "team-b", None)
+                svc = store.try_get("Service", "echo", "team-b")
+                ep = ((svc or {}).get("status") or {}).get("endpoint")
+                sgs = (w.get("status") or {}).get("services") or []
+                if ep and sgs and sgs[0]["ready"]:
+                    break
+                await asyncio.sleep(0.1)
+            dep = store.get("Deployment", "echo", "team-b")
+            fac = [c for c in dep["spec"]["template"]["spec"]["containers"]
+                   if c["name"] == "facade"][0]
+            url = {e["name"]: e["value"] for e in fac["env"]}["OMNIA_SESSION_API_URL"]
+            async with FleetSession(f"ws://{ep}/ws") as fs:
+                await fs.turn("hello")
+                sid = fs.session_id
+            sess_ep = store.get("Service", "session-api-team-b-default", "team-b")["status"][
+                "endpoint"]
+            rows = []
+            async with aiohttp.ClientSession() as s:
+                for _ in range(50):
+                    r = await s.get(f"http://{sess_ep}/api/v1/sessions/{sid}/messages")
+                    if r.status == 200:
+                        rows = (await r.json()).get("messages", [])
+                        if len(rows) >= 2:
+                            break
+                    await asyncio.sleep(0.1)
+            return url, rows
+        finally:
+            await launcher.stop()
+            await mgr.stop()
+
+    url, rows = asyncio.run(go())
+    assert url == "http://session-api-team-b-default.team-b:8080"
+    assert [m["role"] for m in rows][:2] == ["user", "assistant"]

@@ -122,6 +122,24 @@ class ModelRunner:
         self.stats = {"graph_replays": 0, "eager_decodes": 0, "prefill_steps": 0,
                       "captures": 0, "capture_s": 0.0,
                       "gil_wait_s": 0.0}
+        # correctness tap (tests): fp32 copies of every sampled logits row
+        self.logit_tap: list | None = None
+        self._tap = None
+
+    def enable_logit_tap(self):
+        """Record ``(seq_ids, fp32 logits rows)`` for every step, for whole-model
+        correctness checks against ``ops.reference.dense_forward``.  The decode
+        graphs capture one extra copy into a tap buffer, so they are re-captured.
+        Needs the synchronous (non-pipelined) engine loop."""
+        self.logit_tap = []
+        self._tap = torch.zeros(self.max_batch, self.vocab, dtype=torch.float32,
+                                device=self.device)
+        self.graphs.clear()
+        self.graph_exec.clear()
+
+    def _tap_rows(self, seqs, rows):
+        if self.logit_tap is not None:
+            self.logit_tap.append(([s.seq_id for s in seqs], rows.float().cpu()))
 
     # ------------------------------------------------------------------ utils
     def _ctx_bucket(self, max_len: int) -> int:
@@ -166,6 +184,7 @@ class ModelRunner:
         self.stats["prefill_steps"] += 1
         if not sample_seqs:
             return {}
+        self._tap_rows(sample_seqs, logits[: len(sample_seqs)])
         toks = self._sample_eager(logits[: len(sample_seqs)], sample_seqs)
         return {s.seq_id: t for s, t in zip(sample_seqs, toks)}
 
@@ -190,6 +209,7 @@ class ModelRunner:
         if ev is not None:
             ev.synchronize()  # the pinned token buffer of step N-2 has been read
         if n:
+            self._tap_rows(sample_seqs, logits[:n])
             o = meta[5]
             temp = t[o:o + n].view(torch.float64).float()
             top_k = t[o + n:o + 2 * n].int()
@@ -390,6 +410,8 @@ class ModelRunner:
                           d["ids"][:nrows])
         fb = self._decode_fb(nrows, ncols, ids)
         logits = self.model.forward(fb, self.kv)
+        if self._tap is not None:
+            self._tap[:nrows].copy_(logits)
         ops.sample(logits, d["temp"][:nrows], d["top_k"][:nrows], d["top_p"][:nrows],
                    seeds=d["seeds"][:nrows], steps=d["steps"][:nrows],
                    out=self.out_tok[:nrows])
@@ -470,6 +492,8 @@ class ModelRunner:
         gil_ns = h.event.synchronize()
         if gil_ns:
             self.stats["gil_wait_s"] += gil_ns * 1e-9
+        if self._tap is not None and h.kind == "decode":
+            self._tap_rows(h.seqs, self._tap[: h.n])
         return h.out_host[: h.n].tolist()
 
     def run_decode(self, seqs: list[Sequence]) -> list[int]:
@@ -482,6 +506,7 @@ class ModelRunner:
         self._decode_inputs(seqs, n, ncols, st)
         self._before_eager(n, ncols)
         logits = self._eager_forward(n, ncols)
+        self._tap_rows(seqs, logits[:n])
         return self._sample_eager(logits, seqs)
 
     def _before_eager(self, n: int, ncols: int):

@@ -230,3 +230,46 @@ def apply_token_mask(logits: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     allow = bits.reshape(B, -1)[:, :V].to(torch.bool).to(logits.device)
     logits.masked_fill_(~allow, float("-inf"))
     return logits
+
+
+def dense_forward(cfg, w: dict, tokens: list[int]) -> torch.Tensor:
+    """fp32 whole-model oracle: dense causal forward of ONE sequence.
+
+    Independent of the engine's paged-KV / batching machinery (no block tables,
+    no slots, no chunking, no graphs): embedding -> per layer RMSNorm, QKV,
+    RoPE, causal GQA softmax attention, O, residual, RMSNorm, SwiGLU MLP (or
+    top-k MoE), residual -> final norm -> LM head.  ``w`` holds the model's
+    weights in its natural [out, in] layout (``LlamaModel.w``, any device /
+    dtype; computed in fp32 on the CPU).  Returns fp32 logits [T, vocab].
+    """
+    f = lambda t: t.detach().to("cpu", torch.float32)  # noqa: E731
+    T = len(tokens)
+    D, hq, hkv = cfg.head_dim, cfg.num_heads, cfg.num_kv_heads
+    ids = torch.tensor(tokens, dtype=torch.long)
+    pos = torch.arange(T)
+    cs = rope_cos_sin(max(T, 1), D, cfg.rope_theta, cfg.rope_scaling)
+    x = f(w["embed"])[ids]
+    causal = torch.ones(T, T, dtype=torch.bool).tril()
+    scale = 1.0 / math.sqrt(D)
+    for layer in w["layers"]:
+        h = rmsnorm(x, f(layer["in_norm"]), cfg.rms_eps)
+        qkv = h @ f(layer["qkv"]).t()
+        q = qkv[:, : hq * D].view(T, hq, D)
+        k = qkv[:, hq * D: (hq + hkv) * D].view(T, hkv, D)
+        v = qkv[:, (hq + hkv) * D:].view(T, hkv, D)
+        q, k = apply_rope(q, pos, cs), apply_rope(k, pos, cs)
+        g = hq // hkv
+        kk, vv = k.repeat_interleave(g, dim=1), v.repeat_interleave(g, dim=1)
+        s = torch.einsum("qhd,khd->hqk", q, kk) * scale
+        s = s.masked_fill(~causal[None], float("-inf"))
+        o = torch.einsum("hqk,khd->qhd", torch.softmax(s, dim=-1), vv).reshape(T, hq * D)
+        x = x + o @ f(layer["o"]).t()
+        h = rmsnorm(x, f(layer["post_norm"]), cfg.rms_eps)
+        if "router" in layer:
+            m = moe(h, f(layer["router"]), f(layer["experts_gate_up"]),
+                    f(layer["experts_down"]), cfg.experts_per_token)
+        else:
+            m = silu_mul(h @ f(layer["gate_up"]).t()) @ f(layer["down"]).t()
+        x = x + m
+    x = rmsnorm(x, f(w["final_norm"]), cfg.rms_eps)
+    return x @ f(w["lm_head"]).t()

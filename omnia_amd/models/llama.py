@@ -43,6 +43,15 @@ class ForwardBatch:
     num_seqs: int = 0
 
 
+class Parts:
+    """fp32 split-K partial slabs [S, M, N] of a projection (wgemm.hip MODE 2)."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t: torch.Tensor):
+        self.t = t
+
+
 @dataclass
 class KVCache:
     k: list  # per layer [NB, Hkv_local, BS, D]
@@ -150,19 +159,74 @@ class LlamaModel:
         return n
 
     # ------------------------------------------------------------ forward
-    def mlp(self, layer: dict, h: torch.Tensor) -> torch.Tensor:
-        a = ops.linear_silu(h, layer["gate_up"])  # SwiGLU fused into decode GEMMs
-        return ops.linear(a, layer["down"])
+    # Projections return either a bf16 tensor (library / gemm.hip path, not yet
+    # TP-reduced) or :class:`Parts` (fp32 split-K slabs of the weight-streaming
+    # kernel, wgemm.hip), which the NEXT kernel reduces while doing its own work:
+    # QKV parts -> splitk_rope_kv (RoPE + paged KV write), O / down parts ->
+    # splitk_add_rmsnorm (residual add + RMSNorm), gate_up parts -> splitk_swiglu.
+    def _wcfg(self, M: int, N: int, K: int, mode: int, is_decode: bool):
+        if not is_decode or self.device.type != "cuda":
+            return None
+        return ops.wgemm_config(M, N, K, mode)
 
-    def attention(self, li: int, h: torch.Tensor, fb: ForwardBatch, kv: KVCache) -> torch.Tensor:
+    def _parts(self, tag, S: int, M: int, N: int) -> torch.Tensor:
+        key = ("parts", tag, S, M, N)
+        buf = self._ws.get(key)
+        if buf is None:
+            buf = torch.empty(S, M, N, dtype=torch.float32, device=self.device)
+            self._ws[key] = buf
+        return buf
+
+    def _proj(self, tag, x: torch.Tensor, w: torch.Tensor, is_decode: bool):
+        """Plain projection: Parts on the weight-streaming path, else bf16."""
+        M, K = x.shape
+        cfg = self._wcfg(M, w.shape[0], K, 0, is_decode)
+        if cfg is None:
+            return ops.linear(x, w)
+        nw, nwaves, S = cfg
+        return Parts(ops.wgemm(2, x, w, S, nw, nwaves, out=self._parts(tag, S, M, w.shape[0])))
+
+    def add_norm(self, x, residual: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        """residual += x (TP-reduced); returns RMSNorm(residual) * w."""
+        eps = self.cfg.rms_eps
+        if isinstance(x, Parts):
+            if self.tp == 1:
+                return ops.splitk_add_rmsnorm(x.t, residual, w, eps)
+            x = ops.splitk_reduce(x.t)
+        if self.tp > 1:
+            x = pstate.tp_all_reduce(x)
+        ops.fused_add_rmsnorm(x, residual, w, eps)
+        return x
+
+    def mlp(self, layer: dict, h: torch.Tensor, is_decode: bool = False):
+        M, K = h.shape
+        I2 = layer["gate_up"].shape[0]
+        cfg = self._wcfg(M, I2 // 2, K, 1, is_decode)
+        if cfg is None:
+            a = ops.linear_silu(h, layer["gate_up"])  # SwiGLU fused into decode GEMMs
+        else:
+            nw, nwaves, S = cfg
+            if S == 1:
+                a = ops.wgemm(1, h, layer["gate_up"], 1, nw, nwaves)
+            else:
+                a = ops.splitk_swiglu(ops.wgemm(2, h, layer["gate_up"], S, nw, nwaves,
+                                                out=self._parts("gu", S, M, I2)))
+        return self._proj("down", a, layer["down"], is_decode)
+
+    def attention(self, li: int, h: torch.Tensor, fb: ForwardBatch, kv: KVCache):
         T = h.shape[0]
         D = self.cfg.head_dim
-        qkv = ops.linear(h, self.w["layers"][li]["qkv"])
-        q = qkv[:, : self.hq * D]
-        k = qkv[:, self.hq * D: (self.hq + self.hkv) * D]
-        v = qkv[:, (self.hq + self.hkv) * D:]
-        ops.rope_kv(q, k, v, fb.positions, self.cos_sin, kv.k[li], kv.v[li], fb.slots, self.hq,
-                    self.hkv, kv.block_size)
+        wqkv = self.w["layers"][li]["qkv"]
+        qkv = self._proj("qkv", h, wqkv, fb.is_decode)
+        if isinstance(qkv, Parts):
+            q = ops.splitk_rope_kv(qkv.t, fb.positions, self.cos_sin, kv.k[li], kv.v[li],
+                                   fb.slots, self.hq, self.hkv, kv.block_size)
+        else:
+            q = qkv[:, : self.hq * D]
+            k = qkv[:, self.hq * D: (self.hq + self.hkv) * D]
+            v = qkv[:, (self.hq + self.hkv) * D:]
+            ops.rope_kv(q, k, v, fb.positions, self.cos_sin, kv.k[li], kv.v[li], fb.slots,
+                        self.hq, self.hkv, kv.block_size)
         q3 = q.view(T, self.hq, D)
         if fb.is_decode:
             part = self.decode_part(T, fb.block_tables.shape[1] * kv.block_size)
@@ -172,8 +236,7 @@ class LlamaModel:
         else:
             o = ops.prefill_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.q_start_loc,
                                       fb.seq_lens, self.scale, fb.tile_seq, fb.tile_q0)
-        out = ops.linear(o.view(T, self.hq * D), self.w["layers"][li]["o"])
-        return pstate.tp_all_reduce(out)
+        return self._proj("o", o.view(T, self.hq * D), self.w["layers"][li]["o"], fb.is_decode)
 
     def decode_part(self, batch: int, max_ctx: int) -> int:
         """Split-K partition length: as long as possible (fewer partials to merge,
@@ -201,17 +264,16 @@ class LlamaModel:
 
     def hidden_states(self, fb: ForwardBatch, kv: KVCache) -> torch.Tensor:
         cfg = self.cfg
-        eps = cfg.rms_eps
         residual = self.embed(fb.input_ids)
-        h = ops.rmsnorm(residual, self.w["layers"][0]["in_norm"], eps)
+        h = ops.rmsnorm(residual, self.w["layers"][0]["in_norm"], cfg.rms_eps)
+        m = None
         for li, layer in enumerate(self.w["layers"]):
             if li > 0:
-                ops.fused_add_rmsnorm(h, residual, layer["in_norm"], eps)
-            h = self.attention(li, h, fb, kv)
-            ops.fused_add_rmsnorm(h, residual, layer["post_norm"], eps)
-            h = pstate.tp_all_reduce(self.mlp(layer, h)) if self.tp > 1 else self.mlp(layer, h)
-        ops.fused_add_rmsnorm(h, residual, self.w["final_norm"], eps)
-        return h
+                h = self.add_norm(m, residual, layer["in_norm"])
+            a = self.attention(li, h, fb, kv)
+            h = self.add_norm(a, residual, layer["post_norm"])
+            m = self.mlp(layer, h, fb.is_decode)
+        return self.add_norm(m, residual, self.w["final_norm"])
 
     def logits(self, h: torch.Tensor) -> torch.Tensor:
         lg = ops.linear(h, self.w["lm_head"])

@@ -40,7 +40,7 @@ class MixtralModel(LlamaModel):
             "experts_down": _init((E, d, I), 0.02 / math.sqrt(2 * cfg.num_layers), dev, dt, g),
         }
 
-    def mlp(self, layer: dict, h: torch.Tensor) -> torch.Tensor:
+    def mlp(self, layer: dict, h: torch.Tensor, is_decode: bool = False) -> torch.Tensor:
         return ops.moe(h, layer["router"], layer["experts_gate_up"], layer["experts_down"],
                        self.cfg.experts_per_token, self.cfg.num_experts, self.e_lo,
                        graph_safe=self.graph_safe or h.shape[0] < 64)

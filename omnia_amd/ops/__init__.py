@@ -194,6 +194,103 @@ def _dgemm(mode: int, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None
     return out
 
 
+# ------------------------------------------ weight-streaming decode GEMM (wgemm.hip)
+WGEMM_MAX_M = 256
+
+
+_wgemm_table: dict | None = None
+_wgemm_on = os.environ.get("OMNIA_WGEMM", "1") != "0"
+WGEMM_BUCKETS = (16, 32, 64, 128, 256)
+
+
+def wgemm_config(M: int, N: int, K: int, mode: int) -> tuple[int, int, int] | None:
+    """(nw, nwaves, splits) of the weight-streaming kernel for a decode projection,
+    or None to keep the library / gemm.hip path.  ``mode`` 0 = plain projection
+    (its split-K slabs are reduced by the consumer kernel), 1 = gate_up + SwiGLU.
+    Measured dispatch: ``ops/tuned/wgemm_mi355x.json`` (scripts/wgemm_sweep.py +
+    scripts/wgemm_table.py) lists only the shapes where it won on an MI355X."""
+    global _wgemm_table
+    if not _wgemm_on or M < 1 or M > WGEMM_MAX_M:
+        return None
+    if _wgemm_table is None:
+        import json
+
+        p = os.path.join(os.path.dirname(__file__), "tuned", "wgemm_mi355x.json")
+        _wgemm_table = {}
+        if os.path.exists(p):
+            with open(p) as f:
+                _wgemm_table = {k: tuple(v) for k, v in json.load(f).items()}
+    b = next(x for x in WGEMM_BUCKETS if M <= x)
+    return _wgemm_table.get(f"{mode}:{b}:{N}:{K}")
+
+
+def wgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, nw: int = 2,
+          nwaves: int = 4, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Decode GEMM with W streamed HBM -> MFMA registers (``csrc/wgemm.hip``).
+
+    mode 0: bf16 ``x @ w.T``; mode 1: bf16 ``silu(x Wg^T) * (x Wu^T)`` with
+    ``w = [Wg; Wu]``; mode 2: fp32 split-K partial slabs ``[splits, M, N]`` whose
+    sum is ``x @ w.T`` (reduced by the consumer kernel)."""
+    M, K = x.shape
+    N = w.shape[0] // 2 if mode == 1 else w.shape[0]
+    if out is None:
+        out = (torch.empty(splits, M, N, dtype=torch.float32, device=x.device) if mode == 2
+               else x.new_empty(M, N))
+    kernels().wgemm(mode, out, x.contiguous(), w, splits, nw, nwaves)
+    return out
+
+
+def splitk_add_rmsnorm(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+    """``residual += bf16(sum_s parts[s])`` in place; returns ``RMSNorm(residual) * w``."""
+    if parts.is_cuda:
+        out = residual.new_empty(residual.shape) if out is None else out
+        kernels().splitk_add_rmsnorm(out, parts, residual, w, eps)
+        return out
+    o, r = ref.fused_add_rmsnorm(parts.sum(0).to(residual.dtype), residual, w, eps)
+    residual.copy_(r)
+    return o
+
+
+def splitk_rope_kv(parts, positions, cos_sin, k_cache, v_cache, slots, hq, hkv, block_size,
+                   q: torch.Tensor | None = None) -> torch.Tensor:
+    """QKV split-K partials -> RoPE'd q ``[T, hq*D]`` (returned); RoPE'd k and v
+    written to the paged cache at ``slots``."""
+    T = parts.shape[1]
+    D = 128
+    if parts.is_cuda:
+        q = torch.empty(T, hq * D, dtype=k_cache.dtype, device=parts.device) if q is None else q
+        kernels().splitk_rope_kv(q, parts, positions, cos_sin, k_cache, v_cache, slots, hq, hkv,
+                                 block_size)
+        return q
+    qkv = parts.sum(0).to(k_cache.dtype)
+    qq = qkv[:, : hq * D].reshape(T, hq, D)
+    kk = qkv[:, hq * D:(hq + hkv) * D].reshape(T, hkv, D)
+    vv = qkv[:, (hq + hkv) * D:].reshape(T, hkv, D)
+    qq = ref.apply_rope(qq, positions, cos_sin)
+    kk = ref.apply_rope(kk, positions, cos_sin)
+    ref.write_kv(k_cache, v_cache, kk, vv, slots)
+    return qq.reshape(T, hq * D)
+
+
+def splitk_swiglu(parts: torch.Tensor) -> torch.Tensor:
+    S, M, N2 = parts.shape
+    if parts.is_cuda:
+        out = torch.empty(M, N2 // 2, dtype=torch.bfloat16, device=parts.device)
+        kernels().splitk_swiglu(out, parts)
+        return out
+    return ref.silu_mul(parts.sum(0).to(torch.bfloat16))
+
+
+def splitk_reduce(parts: torch.Tensor) -> torch.Tensor:
+    S, M, N = parts.shape
+    if parts.is_cuda:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=parts.device)
+        kernels().splitk_reduce(out, parts)
+        return out
+    return parts.sum(0).to(torch.bfloat16)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """``x @ w.T`` (w in [out, in] layout).  Decode-sized GPU batches (M <= 256)
     run the hand MFMA kernel (gemm.hip); larger batches (prefill) hipBLASLt."""

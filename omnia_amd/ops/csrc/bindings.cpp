@@ -61,6 +61,15 @@ int omnia_ar_blocks();
 int omnia_ar_max_ranks();
 int omnia_ar_oneshot(void* out, const void* in, void* const* regions, int* epochs, int* err,
                      int64_t n, int64_t slot_bytes, int rank, int world, hipStream_t s);
+int omnia_splitk_add_rmsnorm(void* out, const float* parts, void* residual, const void* w, int S,
+                             int M, int d, float eps, hipStream_t s);
+int omnia_splitk_rope_kv(void* q, const float* parts, int S, int T, const int* positions,
+                         const float* cos_sin, void* k_cache, void* v_cache, const int64_t* slots,
+                         int hq, int hkv, int head_dim, int block_size, hipStream_t s);
+int omnia_splitk_swiglu(void* out, const float* parts, int S, int M, int inter, hipStream_t s);
+int omnia_splitk_reduce(void* out, const float* parts, int S, int64_t n, hipStream_t s);
+int omnia_wgemm(int mode, void* out, const void* X, const void* W, int M, int N, int K, int S,
+                int nw, int nwaves, int ldo, hipStream_t s);
 int omnia_dgemm(int mode, void* out, const void* X, const void* W, float* ws, int* cnt, int M,
                 int N, int K, int S, int wm, int wn, int ldo, int64_t ws_floats, int cnt_len,
                 hipStream_t s);
@@ -379,6 +388,97 @@ void dgemm(int64_t mode, at::Tensor out, at::Tensor x, at::Tensor W, at::Tensor 
            "dgemm");
 }
 
+// weight-streaming decode GEMM (wgemm.hip): mode 0 bf16 out[M,N] = x W^T; mode 1
+// SwiGLU bf16 out[M,I] from W = [Wg; Wu]; mode 2 fp32 split-K slabs out[S,M,N].
+void wgemm(int64_t mode, at::Tensor out, at::Tensor x, at::Tensor W, int64_t splits, int64_t nw,
+           int64_t nwaves) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(W);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2, "2-D operands");
+  TORCH_CHECK(x.is_contiguous() && W.is_contiguous(), "contiguous x / W");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(W.size(1) == K, "K mismatch");
+  TORCH_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");
+  TORCH_CHECK(mode != 1 || W.size(0) % 2 == 0, "gate_up rows even");
+  const int N = mode == 1 ? W.size(0) / 2 : W.size(0);
+  int ldo;
+  if (mode == 2) {
+    TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_cuda() && out.is_contiguous(),
+                "mode 2: fp32 contiguous slabs");
+    TORCH_CHECK(out.dim() == 3 && out.size(0) == splits && out.size(1) == M && out.size(2) == N,
+                "mode 2: out [S, M, N]");
+    ldo = N;
+  } else {
+    CHECK_BF16(out);
+    TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N && out.stride(1) == 1,
+                "out [M, N]");
+    ldo = out.stride(0);
+  }
+  CHECK_RC(omnia_wgemm((int)mode, out.data_ptr(), x.data_ptr(), W.data_ptr(), M, N, K,
+                       (int)splits, (int)nw, (int)nwaves, ldo, cur_stream()),
+           "wgemm");
+}
+
+// ------------------------------------------------- split-K consumers (splitk.hip)
+static void check_parts(const at::Tensor& p) {
+  TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat && p.is_contiguous() && p.dim() == 3,
+              "parts: contiguous fp32 [S, M, N]");
+  TORCH_CHECK(p.size(0) >= 1 && p.size(0) <= 16, "1 <= S <= 16");
+}
+
+void splitk_add_rmsnorm(at::Tensor out, at::Tensor parts, at::Tensor residual, at::Tensor w,
+                        double eps) {
+  check_parts(parts);
+  CHECK_BF16(out); CHECK_BF16(residual); CHECK_BF16(w);
+  const int M = parts.size(1), d = parts.size(2);
+  TORCH_CHECK(residual.is_contiguous() && residual.size(0) == M && residual.size(1) == d,
+              "residual [M, d]");
+  TORCH_CHECK(out.is_contiguous() && out.size(0) == M && out.size(1) == d, "out [M, d]");
+  TORCH_CHECK(w.numel() == d, "w [d]");
+  CHECK_RC(omnia_splitk_add_rmsnorm(out.data_ptr(), parts.data_ptr<float>(), residual.data_ptr(),
+                                    w.data_ptr(), parts.size(0), M, d, (float)eps, cur_stream()),
+           "splitk_add_rmsnorm");
+}
+
+void splitk_rope_kv(at::Tensor q, at::Tensor parts, at::Tensor positions, at::Tensor cos_sin,
+                    at::Tensor k_cache, at::Tensor v_cache, at::Tensor slots, int64_t hq,
+                    int64_t hkv, int64_t block_size) {
+  check_parts(parts);
+  CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_I32(positions);
+  const int T = parts.size(1);
+  TORCH_CHECK(parts.size(2) == (hq + 2 * hkv) * 128, "parts N = (hq + 2 hkv) * 128");
+  TORCH_CHECK(q.is_contiguous() && q.size(0) == T && q.size(1) == hq * 128, "q [T, hq*128]");
+  TORCH_CHECK(positions.numel() == T && slots.numel() == T, "positions / slots [T]");
+  TORCH_CHECK(slots.scalar_type() == at::kLong, "slots int64");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == 128, "cos_sin");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == hkv && k_cache.size(2) == block_size &&
+              k_cache.size(3) == 128 && k_cache.is_contiguous() && v_cache.is_contiguous(),
+              "cache [NB, Hkv, BS, 128]");
+  CHECK_RC(omnia_splitk_rope_kv(q.data_ptr(), parts.data_ptr<float>(), parts.size(0), T,
+                                positions.data_ptr<int>(), cos_sin.data_ptr<float>(),
+                                k_cache.data_ptr(), v_cache.data_ptr(),
+                                slots.data_ptr<int64_t>(), hq, hkv, 128, block_size,
+                                cur_stream()),
+           "splitk_rope_kv");
+}
+
+void splitk_swiglu(at::Tensor out, at::Tensor parts) {
+  check_parts(parts);
+  CHECK_BF16(out);
+  const int M = parts.size(1), I = parts.size(2) / 2;
+  TORCH_CHECK(parts.size(2) % 2 == 0 && out.is_contiguous() && out.size(0) == M &&
+              out.size(1) == I, "out [M, I] for parts [S, M, 2I]");
+  CHECK_RC(omnia_splitk_swiglu(out.data_ptr(), parts.data_ptr<float>(), parts.size(0), M, I,
+                               cur_stream()), "splitk_swiglu");
+}
+
+void splitk_reduce(at::Tensor out, at::Tensor parts) {
+  check_parts(parts);
+  CHECK_BF16(out);
+  TORCH_CHECK(out.is_contiguous() && out.numel() == parts.size(1) * parts.size(2), "out [M, N]");
+  CHECK_RC(omnia_splitk_reduce(out.data_ptr(), parts.data_ptr<float>(), parts.size(0),
+                               out.numel(), cur_stream()), "splitk_reduce");
+}
+
 // ------------------------------------------------- one-shot IPC all-reduce (K16)
 int64_t ipc_alloc(int64_t bytes) {
   void* p = nullptr;
@@ -493,6 +593,11 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
   m.def("dgemm", &dgemm);
+  m.def("wgemm", &wgemm);
+  m.def("splitk_add_rmsnorm", &splitk_add_rmsnorm);
+  m.def("splitk_rope_kv", &splitk_rope_kv);
+  m.def("splitk_swiglu", &splitk_swiglu);
+  m.def("splitk_reduce", &splitk_reduce);
   m.def("ipc_alloc", &ipc_alloc);
   m.def("ipc_free", &ipc_free);
   m.def("ipc_get_handle", &ipc_get_handle);

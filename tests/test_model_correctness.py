@@ -134,3 +134,29 @@ def test_gpu_llama3_8b_shaped_large_batch_decode():
     frac, worst = _check(mc, eng.model.w, sample, eng.runner.logit_tap, 0.04)
     print(f"llama-3-8b-2l B=160: worst rel err {worst:.4f}")
     assert frac == 1.0
+
+
+@pytest.fixture
+def forced_wgemm(monkeypatch):
+    """Route every decode projection through wgemm + the split-K consumers."""
+    from omnia_amd import ops
+
+    def cfg(M, N, K, mode):
+        if M > 256:
+            return None
+        S = 2 if K % 256 == 0 else 1
+        if mode == 1:
+            return (2, 2, S)
+        return (1, 2, S)
+
+    monkeypatch.setattr(ops, "wgemm_config", cfg)
+
+
+@pytest.mark.gpu
+def test_gpu_fused_splitk_decode_path_matches_dense_oracle(forced_wgemm):
+    """QKV -> splitk_rope_kv, O / down -> splitk_add_rmsnorm, gate_up split-K ->
+    splitk_swiglu, all inside the captured decode graphs."""
+    for mc in (resolve("tiny-llama"),
+               resolve("llama-3-8b").replace(name="llama-3-8b-2l", num_layers=2)):
+        frac, worst = _gate("cuda", mc, chunk=64, rel_tol=0.04)
+        print(f"{mc.name} fused split-K decode: worst rel err {worst:.4f}")

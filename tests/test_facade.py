@@ -57,9 +57,15 @@ def test_ws_turn_over_real_grpc_and_recording():
                     assert hello["connected"]["capabilities"]["protocol_version"] == 1
                     await ws.send_json({"type": "message", "content": "hi"})
                     frames = await _recv_until(ws)
-            await rec.join()
             sid = hello["session_id"]
-            v = svc.get(sid)
+            # recording is asynchronous (recording pool): the assistant record is
+            # submitted after the done frame reaches the client
+            for _ in range(100):
+                await rec.join()
+                v = svc.get(sid)
+                if v is not None and len(v[1]) >= 2:
+                    break
+                await asyncio.sleep(0.02)
             return hello, frames, v
         finally:
             await fac.stop()

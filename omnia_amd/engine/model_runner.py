@@ -199,7 +199,8 @@ class ModelRunner:
         step issues no synchronous copies and the host can assemble step N+1 while
         the GPU runs step N."""
         t, meta, sample_seqs = self._prefill_pack(chunks, sampling=True)
-        logits = self._prefill_forward(t, meta)
+        tp = self.model.tp > 1
+        logits = self._prefill_forward(t, meta, gather=not tp)
         self.stats["prefill_steps"] += 1
         n = len(sample_seqs)
         slot = self.pf_flip
@@ -209,18 +210,36 @@ class ModelRunner:
         if ev is not None:
             ev.synchronize()  # the pinned token buffer of step N-2 has been read
         if n:
-            self._tap_rows(sample_seqs, logits[:n])
-            o = meta[5]
-            temp = t[o:o + n].view(torch.float64).float()
-            top_k = t[o + n:o + 2 * n].int()
-            top_p = t[o + 2 * n:o + 3 * n].view(torch.float64).float()
-            seeds, steps = t[o + 3 * n:o + 4 * n], t[o + 4 * n:o + 5 * n]
-            tok = ops.sample(logits[:n], temp, top_k, top_p, seeds=seeds, steps=steps)
+            if tp:
+                tok = self._prefill_tp_sample(t, meta, logits)
+            else:
+                self._tap_rows(sample_seqs, logits[:n])
+                temp, top_k, top_p, seeds, steps = self._prefill_sampling(t, meta)
+                tok = ops.sample(logits[:n], temp, top_k, top_p, seeds=seeds, steps=steps)
             out_host[:n].copy_(tok, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self.pf_events[slot] = ev
         return DecodeHandle(sample_seqs, out_host, ev, n, "prefill")
+
+    @staticmethod
+    def _prefill_sampling(t, meta):
+        """(temperature, top_k, top_p, seeds=, steps=) of the sampled rows, sliced
+        from the packed prefill upload."""
+        n, o = meta[4], meta[5]
+        return (t[o:o + n].view(torch.float64).float(), t[o + n:o + 2 * n].int(),
+                t[o + 2 * n:o + 3 * n].view(torch.float64).float(),
+                t[o + 3 * n:o + 4 * n], t[o + 4 * n:o + 5 * n])
+
+    def _prefill_tp_sample(self, t, meta, local_logits):
+        """TP: the distributed sampler (every rank runs it: it is a collective)."""
+        from ..parallel import state as pstate
+        from ..parallel.tp_sampling import tp_sample
+
+        n = meta[4]
+        temp, top_k, top_p, seeds, steps = self._prefill_sampling(t, meta)
+        return tp_sample(local_logits[:n], self.model.vocab_start, temp, top_k, top_p,
+                         seeds=seeds, steps=steps, group=pstate.get_state().tp_group)
 
     def _prefill_pack(self, chunks, sampling: bool = False):
         """Host-side batch assembly -> (packed int64 device tensor, meta, sampled seqs).
@@ -273,7 +292,7 @@ class ModelRunner:
             t = t.pin_memory().to(self.device, non_blocking=True)
         return t, meta, sample_seqs
 
-    def _prefill_forward(self, t: torch.Tensor, meta) -> torch.Tensor:
+    def _prefill_forward(self, t: torch.Tensor, meta, gather: bool = True) -> torch.Tensor:
         T, B, maxb, n_tiles, n_sample = meta[:5]
         o = 0
 
@@ -293,7 +312,7 @@ class ModelRunner:
         fb.tile_q0 = take(n_tiles, torch.int32)
         fb.logits_indices = take(max(1, n_sample), torch.int64)
         fb.block_tables = take(B * maxb, torch.int32).view(B, maxb)
-        return self.model.forward(fb, self.kv)
+        return self.model.forward(fb, self.kv, gather)
 
     def _sample_eager(self, logits, seqs: list[Sequence]) -> list[int]:
         n = len(seqs)
@@ -409,6 +428,16 @@ class ModelRunner:
         ids = torch.where(src >= 0, self.out_tok.index_select(0, src.clamp(min=0)),
                           d["ids"][:nrows])
         fb = self._decode_fb(nrows, ncols, ids)
+        if self.model.tp > 1:
+            # vocab-parallel LM head + distributed sampler: no full-vocab gather
+            from ..parallel import state as pstate
+            from ..parallel.tp_sampling import tp_sample
+
+            local = self.model.forward(fb, self.kv, gather=False)
+            tp_sample(local, self.model.vocab_start, d["temp"][:nrows], d["top_k"][:nrows],
+                      d["top_p"][:nrows], seeds=d["seeds"][:nrows], steps=d["steps"][:nrows],
+                      out=self.out_tok[:nrows], group=pstate.get_state().tp_group)
+            return
         logits = self.model.forward(fb, self.kv)
         if self._tap is not None:
             self._tap[:nrows].copy_(logits)

@@ -5,12 +5,14 @@ weights and of the KV cache (``Hkv / tp`` heads per page, same page ids on every
 rank).  Only TP-rank 0 runs the scheduler, the block manager and the runtime;
 each step it broadcasts the step's packed inputs to the other ranks over the TP
 group (RCCL on GPU, gloo on CPU) and every rank then executes the same forward,
-meeting in the per-layer all-reduces.  Decode inputs are broadcast straight from
-rank 0's device staging buffer into the workers' (one small collective per
-step, stream-ordered before the graph replay), so the workers' captured graphs
-read identical inputs.  Sampling runs redundantly on every rank over identical
-all-gathered logits, which keeps the device-side token feedback of the
-pipelined decode consistent without any extra traffic.
+meeting in the per-layer all-reduces (IPC one-/two-shot kernels with the
+residual add + RMSNorm fused in, ``parallel/custom_allreduce.py``).  Decode
+inputs are broadcast straight from rank 0's device staging buffer into the
+workers' (one small collective per step, stream-ordered before the graph
+replay), so the workers' captured graphs read identical inputs.  Sampling is
+distributed (``parallel/tp_sampling.py``): each rank reduces its vocab slice to
+candidates, only those are all-gathered, and every rank picks the same token,
+which keeps the device-side token feedback of pipelined decode consistent.
 
 Commands (int64 header of 16 words, then an optional payload):
 ``PREFILL (T,B,maxb,tiles,nsample,len)``, ``DECODE (nrows,ncols)``,
@@ -76,9 +78,11 @@ class TPModelRunner(ModelRunner):
         super().__init__(*a, **kw)
         self.chan = TPChannel(self.device)
 
-    def _prefill_forward(self, t, meta):
-        self.chan.send(PREFILL, *meta[:5], t.numel(), payload=t)
-        return super()._prefill_forward(t, meta)
+    def _prefill_forward(self, t, meta, gather: bool = True):
+        # header: T, B, maxb, tiles, n_sample, payload len, gather flag, sampling offset
+        self.chan.send(PREFILL, *meta[:5], t.numel(), int(gather),
+                       meta[5] if len(meta) > 5 else 0, payload=t)
+        return super()._prefill_forward(t, meta, gather)
 
     def _before_replay(self, nrows, ncols):
         self.chan.send(DECODE, nrows, ncols, payload=self.dec.dev)
@@ -106,10 +110,13 @@ class TPWorker(ModelRunner):
             if cmd == STOP:
                 return
             if cmd == PREFILL:
-                T, B, maxb, tiles, ns, n = h[1:7]
+                T, B, maxb, tiles, ns, n, gather, so = h[1:9]
                 t = torch.empty(n, dtype=torch.int64, device=self.device)
                 self.chan.recv_into(t)
-                ModelRunner._prefill_forward(self, t, (T, B, maxb, tiles, ns))
+                meta = (T, B, maxb, tiles, ns, so)
+                lg = ModelRunner._prefill_forward(self, t, meta, bool(gather))
+                if not gather and ns:
+                    self._prefill_tp_sample(t, meta, lg)  # collective: mirror rank 0
             elif cmd == DECODE:
                 self.chan.recv_into(self.dec.dev)
                 self._replay(h[1], h[2])

@@ -194,7 +194,7 @@ class LlamaModel:
                 return ops.splitk_add_rmsnorm(x.t, residual, w, eps)
             x = ops.splitk_reduce(x.t)
         if self.tp > 1:
-            x = pstate.tp_all_reduce(x)
+            return pstate.tp_all_reduce_add_rmsnorm(x, residual, w, eps)
         ops.fused_add_rmsnorm(x, residual, w, eps)
         return x
 
@@ -275,11 +275,14 @@ class LlamaModel:
             m = self.mlp(layer, h, fb.is_decode)
         return self.add_norm(m, residual, self.w["final_norm"])
 
-    def logits(self, h: torch.Tensor) -> torch.Tensor:
+    def logits(self, h: torch.Tensor, gather: bool = True) -> torch.Tensor:
+        """LM head.  Under TP the result is this rank's vocab slice unless
+        ``gather`` (the distributed sampler, parallel/tp_sampling.py, needs
+        only the slice)."""
         lg = ops.linear(h, self.w["lm_head"])
-        return pstate.tp_all_gather_lastdim(lg) if self.tp > 1 else lg
+        return pstate.tp_all_gather_lastdim(lg) if (self.tp > 1 and gather) else lg
 
-    def forward(self, fb: ForwardBatch, kv: KVCache) -> torch.Tensor:
+    def forward(self, fb: ForwardBatch, kv: KVCache, gather: bool = True) -> torch.Tensor:
         h = self.hidden_states(fb, kv)
         sel = h.index_select(0, fb.logits_indices)
-        return self.logits(sel)
+        return self.logits(sel, gather)

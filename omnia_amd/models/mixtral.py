@@ -45,7 +45,7 @@ class MixtralModel(LlamaModel):
                        self.cfg.experts_per_token, self.cfg.num_experts, self.e_lo,
                        graph_safe=self.graph_safe or h.shape[0] < 64)
 
-    def forward(self, fb, kv):
+    def forward(self, fb, kv, gather: bool = True):
         # decode batches are captured into hipGraphs: keep the MoE path sync-free
         self.graph_safe = fb.is_decode
-        return super().forward(fb, kv)
+        return super().forward(fb, kv, gather)

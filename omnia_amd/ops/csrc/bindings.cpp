@@ -68,6 +68,10 @@ int omnia_splitk_rope_kv(void* q, const float* parts, int S, int T, const int* p
                          int hq, int hkv, int head_dim, int block_size, hipStream_t s);
 int omnia_splitk_swiglu(void* out, const float* parts, int S, int M, int inter, hipStream_t s);
 int omnia_splitk_reduce(void* out, const float* parts, int S, int64_t n, hipStream_t s);
+int64_t omnia_ar_region_bytes(int64_t slot_bytes);
+int omnia_ar_twoshot(void* out, const void* in, void* residual, const void* w,
+                     void* const* regions, int* epochs, int* err, int M, int d,
+                     int64_t slot_bytes, int rank, int world, float eps, hipStream_t s);
 int omnia_wgemm(int mode, void* out, const void* X, const void* W, int M, int N, int K, int S,
                 int nw, int nwaves, int ldo, hipStream_t s);
 int omnia_dgemm(int mode, void* out, const void* X, const void* W, float* ws, int* cnt, int M,
@@ -516,6 +520,33 @@ void ar_oneshot(at::Tensor out, at::Tensor in, at::Tensor regions, at::Tensor ep
                             cur_stream()), "ar_oneshot");
 }
 
+// two-shot (reduce-scatter + all-gather) over the same IPC regions; with w the
+// fused residual add + RMSNorm variant (residual updated in place)
+void ar_twoshot(at::Tensor out, at::Tensor in, c10::optional<at::Tensor> residual,
+                c10::optional<at::Tensor> w, at::Tensor regions, at::Tensor epochs, at::Tensor err,
+                int64_t slot_bytes, int64_t rank, double eps) {
+  CHECK_GPU(in); CHECK_BF16(in); CHECK_BF16(out); CHECK_I32(epochs); CHECK_I32(err);
+  TORCH_CHECK(in.dim() == 2 && in.is_contiguous() && out.is_contiguous() &&
+              out.sizes() == in.sizes(), "in/out contiguous [M, d]");
+  TORCH_CHECK(regions.device().is_cpu() && regions.scalar_type() == at::kLong, "regions cpu i64");
+  TORCH_CHECK(epochs.numel() >= omnia_ar_blocks(), "epochs per block");
+  const bool norm = w.has_value() && w->defined();
+  if (norm) {
+    TORCH_CHECK(residual.has_value() && residual->defined(), "NORM needs the residual");
+    CHECK_BF16((*residual)); CHECK_BF16((*w));
+    TORCH_CHECK(residual->sizes() == in.sizes() && residual->is_contiguous(), "residual [M, d]");
+    TORCH_CHECK(w->numel() == in.size(1), "w [d]");
+  }
+  const int world = regions.numel();
+  TORCH_CHECK(world <= omnia_ar_max_ranks(), "world too large");
+  std::vector<void*> regs(world);
+  for (int p = 0; p < world; ++p) regs[p] = reinterpret_cast<void*>(regions.data_ptr<int64_t>()[p]);
+  CHECK_RC(omnia_ar_twoshot(out.data_ptr(), in.data_ptr(), opt_ptr<void>(residual),
+                            opt_ptr<void>(w), regs.data(), epochs.data_ptr<int>(),
+                            err.data_ptr<int>(), in.size(0), in.size(1), slot_bytes, (int)rank,
+                            world, (float)eps, cur_stream()), "ar_twoshot");
+}
+
 // ------------------------------------------------- host step launch (no GIL churn)
 // One decode step = H2D staging copy + graph launch + D2H token copy + event
 // record, enqueued back to back on the current stream inside ONE Python call.
@@ -594,6 +625,8 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("moe_combine", &moe_combine);
   m.def("dgemm", &dgemm);
   m.def("wgemm", &wgemm);
+  m.def("ar_twoshot", &ar_twoshot);
+  m.def("ar_region_bytes", &omnia_ar_region_bytes);
   m.def("splitk_add_rmsnorm", &splitk_add_rmsnorm);
   m.def("splitk_rope_kv", &splitk_rope_kv);
   m.def("splitk_swiglu", &splitk_swiglu);

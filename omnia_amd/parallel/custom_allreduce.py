@@ -9,6 +9,13 @@ directly (kernel + protocol in ``ops/csrc/comm.hip``).  Messages above
 ``max_bytes`` (prefill) go to RCCL, which is also this op's correctness oracle
 in the tests.
 
+Above ``oneshot_max`` (256 KiB) the one-shot read volume ((world-1) x n per
+rank) loses to a two-shot reduce-scatter + all-gather (2 (world-1)/world x n),
+so 2-D messages switch to the two-shot kernel.  ``all_reduce_add_rmsnorm``
+fuses the decoder's residual add + RMSNorm into the two-shot reduce (the rank
+that owns a row chunk normalises it; everyone gathers output and residual), so
+a tensor-parallel layer boundary is one kernel instead of all-reduce + norm.
+
 Handles are exchanged once over the TP group (any backend: gloo on CPU tests,
 RCCL on the node); the per-call path is one kernel launch with no host sync, so
 it is captured into the engine's decode hipGraphs.
@@ -22,7 +29,8 @@ import torch.distributed as dist
 class CustomAllReduce:
     """One-shot all-reduce for bf16 tensors of at most ``max_bytes``."""
 
-    def __init__(self, group=None, device=None, max_bytes: int = 8 << 20):
+    def __init__(self, group=None, device=None, max_bytes: int = 8 << 20,
+                 oneshot_max: int = 256 << 10):
         from .. import ops
 
         self.k = ops.kernels()
@@ -34,9 +42,9 @@ class CustomAllReduce:
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
         self.slot_bytes = (max_bytes + 15) // 16 * 16
-        flag_bytes = self.k.ar_blocks() * self.k.ar_max_ranks() * 4
+        self.oneshot_max = oneshot_max
         with torch.cuda.device(self.device):
-            self.base = self.k.ipc_alloc(2 * self.slot_bytes + flag_bytes)
+            self.base = self.k.ipc_alloc(self.k.ar_region_bytes(self.slot_bytes))
             handle = self.k.ipc_get_handle(self.base)
             if self.world > 1:
                 handles = [None] * self.world
@@ -63,10 +71,32 @@ class CustomAllReduce:
         return (not self.closed and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
                 and n % 8 == 0 and 2 * n <= self.max_bytes)
 
-    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        """In place when ``out`` is None (same contract as ``dist.all_reduce``)."""
+    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None,
+                   algo: str | None = None) -> torch.Tensor:
+        """In place when ``out`` is None (same contract as ``dist.all_reduce``).
+        ``algo``: "oneshot" / "twoshot" / None (by size: two-shot above
+        ``oneshot_max`` for 2-D tensors)."""
         out = x if out is None else out
-        self.k.ar_oneshot(out, x, self.regions, self.epochs, self.err, self.slot_bytes, self.rank)
+        if algo is None:
+            algo = "twoshot" if (x.dim() == 2 and 2 * x.numel() > self.oneshot_max) else "oneshot"
+        if algo == "twoshot":
+            self.k.ar_twoshot(out, x, None, None, self.regions, self.epochs, self.err,
+                              self.slot_bytes, self.rank, 0.0)
+        else:
+            self.k.ar_oneshot(out, x, self.regions, self.epochs, self.err, self.slot_bytes,
+                              self.rank)
+        return out
+
+    def can_fuse_norm(self, x: torch.Tensor) -> bool:
+        return (self.should_use(x) and x.dim() == 2 and x.shape[1] % 8 == 0
+                and 4 * x.numel() <= self.slot_bytes)
+
+    def all_reduce_add_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                               eps: float, out: torch.Tensor | None = None) -> torch.Tensor:
+        """``residual += allreduce(x)`` (bf16, in place); returns ``RMSNorm(residual) * w``."""
+        out = x if out is None else out
+        self.k.ar_twoshot(out, x, residual, w, self.regions, self.epochs, self.err,
+                          self.slot_bytes, self.rank, eps)
         return out
 
     def check(self) -> None:

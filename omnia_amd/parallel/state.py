@@ -95,9 +95,9 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, device: str |
             g = dist.new_group(ranks) if len(ranks) > 1 else None
             if rank in ranks:
                 st.dp_group = g
-        if use_gpu and tp_size > 1 and os.environ.get("OMNIA_CUSTOM_AR", "0") == "1":
-            # one-shot IPC all-reduce for decode-size TP collectives (opt-in until
-            # validated on a full 8-GPU node; RCCL stays the default and the oracle)
+        if use_gpu and tp_size > 1 and os.environ.get("OMNIA_CUSTOM_AR", "1") == "1":
+            # one-/two-shot IPC all-reduce for decode-size TP collectives (RCCL for
+            # prefill-size messages and as the correctness oracle in the tests)
             from .custom_allreduce import CustomAllReduce
 
             st.custom_ar = CustomAllReduce(st.tp_group)
@@ -112,6 +112,22 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     if st.custom_ar is not None and x.is_cuda and st.custom_ar.should_use(x):
         return st.custom_ar.all_reduce(x)
     dist.all_reduce(x, group=st.tp_group)
+    return x
+
+
+def tp_all_reduce_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                              eps: float) -> torch.Tensor:
+    """TP layer boundary: ``residual += allreduce(x)``; returns RMSNorm(residual) * w.
+    One fused IPC kernel for decode-size messages, RCCL + the fused add-norm
+    kernel otherwise."""
+    st = _STATE
+    from .. import ops
+
+    if st.tp_size > 1 and st.custom_ar is not None and x.is_cuda and \
+            st.custom_ar.can_fuse_norm(x):
+        return st.custom_ar.all_reduce_add_rmsnorm(x, residual, w, eps)
+    x = tp_all_reduce(x)
+    ops.fused_add_rmsnorm(x, residual, w, eps)
     return x
 
 

@@ -1,0 +1,67 @@
+"""Tensor-parallel sampling without gathering the vocabulary.
+
+Under TP the LM head is vocab-parallel: rank r holds logits for its V/tp slice.
+Gathering the full [B, V] logits every decode step moves B x V x 2 bytes
+(64 MB at B = 256, V = 128256) into every rank; instead each rank reduces its
+slice to a few candidates and only those are exchanged (B x tp x (2K + 2)
+floats, 0.5 MB at K = 64, tp = 8):
+
+* greedy rows (temperature 0): the global argmax is the argmax of the ranks'
+  local top-1s -- exact;
+* pure temperature rows (no top-k / top-p): Gumbel-max -- every rank adds
+  independent Gumbel noise to its logits / T and keeps the local winner; the
+  arg-max of the winners is an exact sample from softmax(logits / T) over the
+  whole vocabulary;
+* top-k / top-p rows: the fused sampler runs over the union of the ranks'
+  local top-K logits (K = 64): exact for top_k <= K; top-p is taken inside that
+  candidate set (exact whenever the nucleus has <= K tokens per rank).
+Every rank computes the same final token from the same gathered candidates,
+which keeps the device-side token feedback of pipelined decode consistent.
+Penalised / grammar-constrained rows keep the full gather (the runner routes
+them to the eager path).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+
+def tp_sample(local_logits: torch.Tensor, vocab_start: int, temperature: torch.Tensor,
+              top_k: torch.Tensor, top_p: torch.Tensor, seeds: torch.Tensor | None = None,
+              steps: torch.Tensor | None = None, out: torch.Tensor | None = None, group=None,
+              K: int = 64, generator: torch.Generator | None = None) -> torch.Tensor:
+    B, Vl = local_logits.shape
+    W = dist.get_world_size(group)
+    K = min(K, Vl)
+    lf = local_logits.float()
+    cv, ci = torch.topk(lf, K, dim=1)
+    t = temperature.float().clamp(min=1e-6)[:, None]
+    u = torch.rand(B, Vl, device=lf.device, generator=generator).clamp_(1e-10, 1.0 - 1e-7)
+    gv, gi = (lf / t - torch.log(-torch.log(u))).max(dim=1)
+    pack = torch.cat([cv, (ci + vocab_start).float(), gv[:, None],
+                      (gi + vocab_start).float()[:, None]], dim=1).contiguous()
+    if pack.is_cuda:
+        allp = torch.empty(W * B, pack.shape[1], dtype=pack.dtype, device=pack.device)
+        dist.all_gather_into_tensor(allp, pack, group=group)
+        allp = allp.view(W, B, -1)
+    else:
+        parts = [torch.empty_like(pack) for _ in range(W)]
+        dist.all_gather(parts, pack, group=group)
+        allp = torch.stack(parts)
+    cand_v = allp[:, :, :K].permute(1, 0, 2).reshape(B, W * K)
+    cand_i = allp[:, :, K:2 * K].permute(1, 0, 2).reshape(B, W * K).long()
+    gum_v = allp[:, :, 2 * K].t()  # [B, W]
+    gum_i = allp[:, :, 2 * K + 1].t().long()
+    greedy = cand_i.gather(1, cand_v.argmax(dim=1, keepdim=True))[:, 0]
+    gumbel = gum_i.gather(1, gum_v.argmax(dim=1, keepdim=True))[:, 0]
+    filt_local = ops.sample(cand_v.to(local_logits.dtype).contiguous(), temperature,
+                            top_k, top_p, seeds=seeds, steps=steps).long()
+    filtered = cand_i.gather(1, filt_local.clamp(0, W * K - 1)[:, None])[:, 0]
+    use_filter = (top_k > 0) | (top_p < 1.0)
+    tok = torch.where(temperature <= 0, greedy, torch.where(use_filter, filtered, gumbel))
+    if out is None:
+        return tok.to(torch.int32)
+    out.copy_(tok)
+    return out

@@ -38,3 +38,12 @@ def test_open_loop_poisson_reports_latency_percentiles():
                  "--stream-interval-ms", "0")
     assert rec["config"]["arrival"].startswith("poisson")
     assert rec["turns"] == 4 and rec["p95_tpot_ms"] is not None and rec["p95_ttft_ms"]
+
+
+def test_tp2_pod_serves_over_ws():
+    """--tp K: one TP pod per K ranks (torchrun'd runtime ranks, TP-rank 0 serves
+    gRPC), the other bench ranks only join the aggregation (CPU, gloo)."""
+    rec = _bench("--gpus", "2", "--tp", "2", "--concurrency", "2", "--steps", "1")
+    assert rec["config"]["parallelism"] == "dp1-tp2" and rec["n_gpus"] == 2
+    assert rec["turns"] == 2 and rec["per_rank_tokens_per_s"][1] == 0.0
+    assert rec["value"] > 0

@@ -1,0 +1,74 @@
+"""Distributed TP sampling (parallel/tp_sampling.py) with gloo, world 2 and 4:
+greedy equals the full-vocab argmax, pure temperature sampling follows
+softmax(logits / T) over the WHOLE vocabulary (Gumbel-max), top-k draws stay in
+the global top-k, and every rank picks the same token."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from omnia_amd.parallel.tp_sampling import tp_sample
+
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        V, B = 64 * world, 4000
+        g = torch.Generator().manual_seed(0)
+        base = torch.randn(V, generator=g) * 1.5
+        L = base.repeat(B, 1)
+        sl = V // world
+        local = L[:, rank * sl:(rank + 1) * sl].contiguous()
+        gen = torch.Generator().manual_seed(100 + rank)
+        zeros = torch.zeros(B, dtype=torch.int32)
+        ones = torch.ones(B)
+        res = {}
+        res["greedy"] = tp_sample(local, rank * sl, torch.zeros(B), zeros, ones,
+                                  generator=gen, K=8)
+        res["temp"] = tp_sample(local, rank * sl, ones, zeros, ones, generator=gen, K=8)
+        res["topk"] = tp_sample(local, rank * sl, ones, torch.full((B,), 3, dtype=torch.int32),
+                                ones, seeds=torch.arange(B), steps=torch.zeros(B, dtype=torch.int64),
+                                generator=gen, K=8)
+        q.put(("ok", rank, {k: v.tolist() for k, v in res.items()}, base.tolist()))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put(("err", rank, traceback.format_exc(), None))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tp_sample_matches_full_vocab(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(30)
+    for st, rank, val, _ in res:
+        assert st == "ok", val
+    outs = {r: v for _, r, v, _ in res}
+    base = torch.tensor(res[0][3])
+    for k in ("greedy", "temp", "topk"):
+        assert all(outs[r][k] == outs[0][k] for r in outs), f"ranks disagree on {k}"
+    assert set(outs[0]["greedy"]) == {int(base.argmax())}
+    top3 = set(base.topk(3).indices.tolist())
+    assert set(outs[0]["topk"]) <= top3 and len(set(outs[0]["topk"])) >= 2
+    # Gumbel-max: empirical frequencies follow softmax over the whole vocabulary
+    p = torch.softmax(base, 0)
+    freq = torch.bincount(torch.tensor(outs[0]["temp"]), minlength=base.numel()).float() / 4000
+    assert (freq - p).abs().max() < 0.03

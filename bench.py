@@ -64,6 +64,8 @@ def parse(argv=None):
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica")
     ap.add_argument("--arrival", choices=["closed", "poisson"], default="closed")
     ap.add_argument("--rate", type=float, default=0.0, help="poisson: turns/s per replica")
+    ap.add_argument("--mixed-budget", type=int, default=0,
+                    help="engine mixed steps: decode rows + <= N prefill tokens per forward")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--inproc", action="store_true",
                     help="runtime path: engine as a thread of the serving process")
@@ -145,7 +147,7 @@ class WSDriver:
             "OMNIA_ENGINE_MAX_PREFILL_TOKENS": a.max_prefill_tokens,
             "OMNIA_ENGINE_USE_GRAPHS": "false" if a.no_graphs else "true",
             "OMNIA_ENGINE_SEED": rank, "OMNIA_ENGINE_PROC": "1" if use_gpu and a.tp == 1 else "0",
-            "OMNIA_ENGINE_TP": a.tp,
+            "OMNIA_ENGINE_TP": a.tp, "OMNIA_ENGINE_MIXED_BUDGET": a.mixed_budget,
         }
         fenv = {"OMNIA_AGENT_NAME": f"bench-{rank}", "OMNIA_MAX_CONNECTIONS": 4 * C + 64,
                 "OMNIA_MSG_RATE": 1000, "OMNIA_MSG_BURST": 1000}
@@ -244,7 +246,7 @@ class LocalDriver:
                            max_batch=max(C, 1),
                            max_model_len=max(2048, a.prompt_len + a.gen_len + 64),
                            max_prefill_tokens=a.max_prefill_tokens, use_graphs=not a.no_graphs,
-                           seed=rank)
+                           seed=rank, mixed_budget=a.mixed_budget)
         self.cfg = cfg
         self.eng = self.client = None
         if self.proc:
@@ -445,6 +447,7 @@ def run(a, drv, ws, rank, use_gpu, host_only):
                 "path": a.path,
                 "arrival": a.arrival if a.arrival == "closed" else f"poisson@{a.rate}/s",
                 "stream_interval_ms": a.stream_interval_ms,
+                "mixed_budget": a.mixed_budget,
                 "tp": a.tp,
                 "hip_graphs": not a.no_graphs,
             },

@@ -56,6 +56,9 @@ class EngineConfig:
     tokenizer: str | None = None
     decode_part_size: int = 512
     pipeline: bool = True  # one-deep async decode scheduling
+    # >0: mixed steps (running sequences' decode rows + <= this many prefill tokens
+    # in one forward) bound inter-token latency under arrivals; 0: separate steps
+    mixed_budget: int = 0
     checkpoint: str | None = None  # HF safetensors dir (random init when None)
 
     @classmethod
@@ -72,6 +75,7 @@ class EngineConfig:
             "OMNIA_ENGINE_SWAP_GIB": ("swap_gib", float),
             "OMNIA_ENGINE_CHECKPOINT": ("checkpoint", str),
             "OMNIA_ENGINE_USE_GRAPHS": ("use_graphs", lambda v: v.lower() != "false"),
+            "OMNIA_ENGINE_MIXED_BUDGET": ("mixed_budget", int),
         }
         for k, (f, t) in m.items():
             if k in env:
@@ -129,7 +133,11 @@ class LLMEngine:
         self.blocks = BlockManager(nb, cfg.block_size, swap=swap)
         self.scheduler = Scheduler(
             SchedulerConfig(max_batch=cfg.max_batch, max_prefill_tokens=cfg.max_prefill_tokens,
-                            max_model_len=cfg.max_model_len), self.blocks)
+                            max_model_len=cfg.max_model_len,
+                            # mixed steps run on the TP-rank-0-only eager path: TP keeps
+                            # separate prefill / decode steps
+                            mixed_budget=cfg.mixed_budget if self.model.tp == 1 else 0),
+            self.blocks)
         self.tokenizer = make_tokenizer(self.model_cfg, cfg.tokenizer)
         self.eos = set(self.tokenizer.eos_token_ids)
         self.seqs: dict[int, Sequence] = {}
@@ -308,6 +316,13 @@ class LLMEngine:
             M.PREFILL_TOKENS.inc(ntok)
             self.step_count += 1
             return n
+        if plan.kind == "mixed":
+            # decode rows need their real last tokens: drain the in-flight step
+            n0 = self._flush_inflight()
+            plan.decode = [sq for sq in plan.decode if not sq.is_finished]
+            if not plan.decode:
+                plan.kind = "prefill"
+            return n0 + self._run_plan(plan)
         if h0 is not None and h0.kind == "prefill" and plan.kind != "prefill":
             n0 = self._flush_inflight()
             if plan.kind == "decode":
@@ -362,7 +377,17 @@ class LLMEngine:
 
     def _run_plan(self, plan) -> int:
         t0 = time.perf_counter()
-        if plan.kind == "prefill":
+        if plan.kind == "mixed":
+            toks, sampled = self.runner.run_mixed(plan.decode, plan.prefill)
+            done = self.scheduler.on_decode_done(plan.decode, toks)
+            done += self.scheduler.on_prefill_done(plan.prefill, sampled)
+            ntok = sum(n for _, n in plan.prefill)
+            self.counters["prefill_tokens"] += ntok
+            self.counters["decode_tokens"] += len(toks)
+            self.counters["steps_mixed"] = self.counters.get("steps_mixed", 0) + 1
+            M.PREFILL_TOKENS.inc(ntok)
+            M.DECODE_TOKENS.inc(len(toks))
+        elif plan.kind == "prefill":
             sampled = self.runner.run_prefill(plan.prefill)
             done = self.scheduler.on_prefill_done(plan.prefill, sampled)
             ntok = sum(n for _, n in plan.prefill)

@@ -314,6 +314,81 @@ class ModelRunner:
         fb.block_tables = take(B * maxb, torch.int32).view(B, maxb)
         return self.model.forward(fb, self.kv, gather)
 
+    # ------------------------------------------------------------------ mixed
+    def run_mixed(self, dseqs: list[Sequence], chunks: list[tuple[Sequence, int]]
+                  ) -> tuple[list[int], dict[int, int]]:
+        """One forward over the running sequences' next tokens (decode rows,
+        first) and prefill chunks.  Returns (tokens of ``dseqs``, {seq_id: token}
+        of the prompts this step completed)."""
+        bs = self.bs
+        Bd, B = len(dseqs), len(chunks)
+        lens = np.fromiter((n for _, n in chunks), np.int64, B)
+        qsl = np.zeros(B + 1, np.int64)
+        np.cumsum(lens, out=qsl[1:])
+        Tp = int(qsl[-1])
+        T = Bd + Tp
+        ids = np.empty(T, np.int64)
+        pos = np.empty(T, np.int64)
+        slots = np.empty(T, np.int64)
+        mbd = self._ctx_bucket(max(s.length for s in dseqs))
+        dbt = np.zeros((Bd, mbd), np.int64)
+        dlen = np.empty(Bd, np.int64)
+        for i, s in enumerate(dseqs):
+            p = s.length - 1
+            ids[i] = s.output[-1] if s.output else s.prompt[-1]
+            pos[i] = p
+            slots[i] = s.blocks[p // bs] * bs + p % bs
+            dbt[i, :len(s.blocks)] = s.blocks
+            dlen[i] = p + 1
+        maxb = max(1, max(len(s.blocks) for s, _ in chunks))
+        bt = np.zeros((B, maxb), np.int64)
+        seq_lens = np.empty(B, np.int64)
+        sample_rows, sample_seqs = list(range(Bd)), list(dseqs)
+        for i, (s, n) in enumerate(chunks):
+            start, q0 = s.num_cached, Bd + int(qsl[i])
+            src = s.prompt if start + n <= len(s.prompt) else s.all_tokens
+            ids[q0:q0 + n] = src[start:start + n]
+            pos[q0:q0 + n] = np.arange(start, start + n)
+            bt[i, :len(s.blocks)] = s.blocks
+            seq_lens[i] = start + n
+            blk = bt[i][pos[q0:q0 + n] // bs]
+            slots[q0:q0 + n] = blk * bs + pos[q0:q0 + n] % bs
+            if start + n == s.length:
+                sample_rows.append(q0 + n - 1)
+                sample_seqs.append(s)
+        tseq, tq0 = ops.prefill_tiles(lens.tolist())
+        parts = [ids, pos, slots, qsl, seq_lens, np.asarray(tseq, np.int64),
+                 np.asarray(tq0, np.int64), np.asarray(sample_rows, np.int64), bt.reshape(-1),
+                 dbt.reshape(-1), dlen]
+        t = torch.from_numpy(np.concatenate(parts))
+        if self.is_gpu:
+            t = t.pin_memory().to(self.device, non_blocking=True)
+        o = 0
+
+        def take(n, dtype):
+            nonlocal o
+            v = t[o:o + n]
+            o += n
+            return v.to(dtype)
+
+        fb = ForwardBatch(input_ids=take(T, torch.int32), positions=take(T, torch.int32),
+                          slots=take(T, torch.int64), block_tables=None, seq_lens=None,
+                          logits_indices=None, is_decode=False, num_seqs=B)
+        fb.q_start_loc = take(B + 1, torch.int32)
+        fb.seq_lens = take(B, torch.int32)
+        fb.tile_seq = take(len(tseq), torch.int32)
+        fb.tile_q0 = take(len(tq0), torch.int32)
+        fb.logits_indices = take(len(sample_rows), torch.int64)
+        fb.block_tables = take(B * maxb, torch.int32).view(B, maxb)
+        fb.dec_block_tables = take(Bd * mbd, torch.int32).view(Bd, mbd)
+        fb.dec_seq_lens = take(Bd, torch.int32)
+        fb.num_decode = Bd
+        logits = self.model.forward(fb, self.kv)
+        self.stats["mixed_steps"] = self.stats.get("mixed_steps", 0) + 1
+        self._tap_rows(sample_seqs, logits)
+        toks = self._sample_eager(logits, sample_seqs)
+        return toks[:Bd], {s.seq_id: tk for s, tk in zip(sample_seqs[Bd:], toks[Bd:])}
+
     def _sample_eager(self, logits, seqs: list[Sequence]) -> list[int]:
         n = len(seqs)
         dev = self.device

@@ -1,10 +1,15 @@
 """Continuous-batching scheduler with chunked prefill and session-affine KV.
 
-Each engine step is either a PREFILL step (new/partially-prefilled sequences,
-packed up to ``max_prefill_tokens`` new tokens -- long prompts are chunked) or a
-DECODE step over every running sequence.  Prefill has priority while the
-running set is below ``max_batch`` so TTFT stays low; decode steps are the
-hipGraph-captured hot loop.  When the KV pool runs dry, idle session caches are
+Each engine step is a PREFILL step (new/partially-prefilled sequences, packed
+up to ``max_prefill_tokens`` new tokens -- long prompts are chunked), a DECODE
+step over every running sequence (the hipGraph-captured hot loop), or -- with
+``mixed_budget`` > 0 -- a MIXED step: every running sequence's next token plus
+prefill chunks of at most ``mixed_budget`` tokens in ONE forward (the decode
+rows ride in the prefill GEMMs, and running sequences never stall behind a
+whole prefill chunk: the step time, i.e. their inter-token latency, is bounded
+by the budget).  Without running sequences prefill uses the full
+``max_prefill_tokens`` (throughput); prefill has priority while the running set
+is below ``max_batch`` so TTFT stays low.  When the KV pool runs dry, idle session caches are
 evicted first (LRU, optionally to host DRAM), then the youngest running
 sequence is preempted (its pages are freed and it is re-queued for recompute).
 """
@@ -24,11 +29,12 @@ class SchedulerConfig:
     max_prefill_tokens: int = 16384
     max_model_len: int = 8192
     prefill_chunk: int = 8192  # max new tokens of ONE sequence per prefill step
+    mixed_budget: int = 0  # >0: co-schedule decode rows with <= this many prefill tokens
 
 
 @dataclass
 class StepPlan:
-    kind: str  # "prefill" | "decode" | "idle"
+    kind: str  # "prefill" | "decode" | "mixed" | "idle"
     prefill: list  # [(seq, n_new)]
     decode: list  # [seq]
 
@@ -106,8 +112,24 @@ class Scheduler:
     # ------------------------------------------------------------ planning
     def schedule(self) -> StepPlan:
         cfg = self.cfg
+        if cfg.mixed_budget > 0 and self.running and (self.partial or self.waiting):
+            decode = self._decode_rows()
+            chunks = self._prefill_chunks(cfg.mixed_budget)
+            if chunks and decode:
+                return StepPlan("mixed", chunks, decode)
+            if chunks:
+                return StepPlan("prefill", chunks, [])
+            return StepPlan("decode", [], decode) if decode else StepPlan("idle", [], [])
+        chunks = self._prefill_chunks(cfg.max_prefill_tokens)
+        if chunks:
+            return StepPlan("prefill", chunks, [])
+        if self.running:
+            return StepPlan("decode", [], self._decode_rows())
+        return StepPlan("idle", [], [])
+
+    def _prefill_chunks(self, budget: int) -> list:
+        cfg = self.cfg
         chunks: list[tuple[Sequence, int]] = []
-        budget = cfg.max_prefill_tokens
         # continue chunked prompts first
         for s in list(self.partial):
             n = min(s.num_uncached, cfg.prefill_chunk, budget)
@@ -144,24 +166,23 @@ class Scheduler:
             budget -= n
             if n < s.num_uncached:
                 self.partial.append(s)
-        if chunks:
-            return StepPlan("prefill", chunks, [])
-        if self.running:
-            # every running seq needs a slot for its next token
-            for s in list(self.running):
-                # a sequence preempted earlier in this pass holds no pages and
-                # must not allocate any (that would cascade preemptions)
-                if s not in self.running:
-                    continue
-                while True:
-                    try:
-                        self._ensure_blocks(s, s.length)
-                        break
-                    except OutOfBlocks:
-                        if not self._preempt_one(protect=s):
-                            raise
-            return StepPlan("decode", [], list(self.running))
-        return StepPlan("idle", [], [])
+        return chunks
+
+    def _decode_rows(self) -> list:
+        # every running seq needs a slot for its next token
+        for s in list(self.running):
+            # a sequence preempted earlier in this pass holds no pages and
+            # must not allocate any (that would cascade preemptions)
+            if s not in self.running:
+                continue
+            while True:
+                try:
+                    self._ensure_blocks(s, s.length)
+                    break
+                except OutOfBlocks:
+                    if not self._preempt_one(protect=s):
+                        raise
+        return list(self.running)
 
     # ------------------------------------------------------------ results
     def on_prefill_done(self, chunks, sampled: dict[int, int]) -> list[tuple[Sequence, int]]:

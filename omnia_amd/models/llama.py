@@ -41,6 +41,12 @@ class ForwardBatch:
     tile_seq: torch.Tensor | None = None  # int32 [n_tiles] (prefill)
     tile_q0: torch.Tensor | None = None
     num_seqs: int = 0
+    # mixed step: the first ``num_decode`` tokens are decode rows (one token of a
+    # running sequence each, attended by the decode kernel over dec_*), the rest
+    # are prefill chunks described by q_start_loc / seq_lens / block_tables
+    num_decode: int = 0
+    dec_block_tables: torch.Tensor | None = None  # int32 [Bd, max_blocks]
+    dec_seq_lens: torch.Tensor | None = None  # int32 [Bd]
 
 
 class Parts:
@@ -233,6 +239,23 @@ class LlamaModel:
             ws = self._decode_ws(T, fb.block_tables.shape[1], kv.block_size, h.device, part)
             o = ops.decode_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.seq_lens,
                                      self.scale, part_size=part, workspace=ws)
+        elif fb.num_decode:
+            # mixed step: decode rows on the split-K decode kernel (K/V read once per
+            # GQA group), prefill chunks on the flash prefill kernel, one output
+            Bd = fb.num_decode
+            o = torch.empty_like(q3) if q3.is_contiguous() else torch.empty(
+                T, self.hq, D, dtype=q3.dtype, device=q3.device)
+            mb = fb.dec_block_tables.shape[1]
+            part = self.decode_part(Bd, mb * kv.block_size)
+            ws = self._decode_ws(1 << max(0, Bd - 1).bit_length(), mb, kv.block_size, h.device,
+                                 part)  # pow2 rows: few workspace shapes across mixed steps
+            ops.decode_attention(q3[:Bd], kv.k[li], kv.v[li], fb.dec_block_tables,
+                                 fb.dec_seq_lens, self.scale, part_size=part, workspace=ws,
+                                 out=o[:Bd])
+            if T > Bd:
+                ops.prefill_attention(q3[Bd:], kv.k[li], kv.v[li], fb.block_tables,
+                                      fb.q_start_loc, fb.seq_lens, self.scale, fb.tile_seq,
+                                      fb.tile_q0, out=o[Bd:])
         else:
             o = ops.prefill_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.q_start_loc,
                                       fb.seq_lens, self.scale, fb.tile_seq, fb.tile_q0)

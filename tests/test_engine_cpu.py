@@ -120,3 +120,26 @@ def test_model_param_count():
     assert abs(LLAMA3_8B.num_params() / 1e9 - 8.03) < 0.05
     assert abs(LLAMA3_70B.num_params() / 1e9 - 70.6) < 0.2
     assert LLAMA3_8B.kv_bytes_per_token() == 128 * 1024
+
+
+def test_mixed_steps_match_separate_steps():
+    """Mixed decode+prefill steps (mixed_budget) produce the same greedy tokens
+    as separate prefill / decode steps, with staggered arrivals."""
+    from omnia_amd.engine.engine import EngineConfig, LLMEngine
+    from omnia_amd.engine.sampling_params import SamplingParams
+
+    outs = {}
+    for budget in (0, 48):
+        eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", num_blocks=256,
+                                     block_size=16, max_batch=8, max_model_len=1024,
+                                     max_prefill_tokens=256, mixed_budget=budget, seed=1))
+        p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+        first = [eng.add_request(list(range(10, 90)), p), eng.add_request(list(range(5, 40)), p)]
+        for _ in range(4):
+            eng.step()
+        later = [eng.add_request(list(range(100, 230)), p), eng.add_request([7] * 61, p)]
+        eng.run_until_done()
+        outs[budget] = [s.output for s in first + later]
+        if budget:
+            assert eng.counters.get("steps_mixed", 0) >= 2
+    assert outs[0] == outs[48]

@@ -160,3 +160,26 @@ def test_gpu_fused_splitk_decode_path_matches_dense_oracle(forced_wgemm):
                resolve("llama-3-8b").replace(name="llama-3-8b-2l", num_layers=2)):
         frac, worst = _gate("cuda", mc, chunk=64, rel_tol=0.04)
         print(f"{mc.name} fused split-K decode: worst rel err {worst:.4f}")
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_steps_match_dense_oracle():
+    """Mixed decode + prefill steps (split decode / prefill attention in one
+    forward) with staggered arrivals, against the dense oracle."""
+    mc = resolve("llama-3-8b").replace(name="llama-3-8b-2l", num_layers=2)
+    eng = LLMEngine(EngineConfig(model=mc.name, device="cuda", num_blocks=512, block_size=16,
+                                 max_batch=8, max_model_len=1024, max_prefill_tokens=256,
+                                 pipeline=False, seed=9, mixed_budget=40), model_cfg=mc)
+    eng.runner.enable_logit_tap()
+    rng = random.Random(3)
+    V = mc.vocab_size
+    p = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
+    seqs = [eng.add_request([rng.randrange(10, V - 10) for _ in range(n)], p) for n in (70, 33)]
+    for _ in range(3):
+        eng.step()
+    seqs += [eng.add_request([rng.randrange(10, V - 10) for _ in range(n)], p) for n in (120, 9)]
+    eng.run_until_done()
+    assert eng.counters.get("steps_mixed", 0) >= 3
+    frac, worst = _check(mc, eng.model.w, seqs, eng.runner.logit_tap, 0.04)
+    print(f"mixed steps: {eng.counters['steps_mixed']}, worst rel err {worst:.4f}")
+    assert frac == 1.0

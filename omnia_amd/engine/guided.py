@@ -73,6 +73,18 @@ def compile_schema(schema: dict | None) -> tuple[list[dict], int]:
             memo[ref] = idx
             nodes[idx] = nodes[build(defs[name], depth + 1)].copy()
             return idx
+        if "x-omnia-tool-union" in s:
+            # Llama-3 tool call {"name": <tool>, "parameters": <that tool's schema>}:
+            # a tagged object, the matched name selects the parameters grammar
+            tools = s["x-omnia-tool-union"]
+            if not tools:
+                raise SchemaError("tool union needs at least one tool")
+            name_node = add({"kind": LITERALS, "literals": [_lit(t["name"]) for t in tools]})
+            params = [build(t.get("parameters") or {"type": "object"}, depth + 1)
+                      for t in tools]
+            return add({"kind": OBJECT, "props": [(_lit("name"), name_node, True),
+                                                  (_lit("parameters"), params[0], True)],
+                        "tag_children": params})
         if "const" in s:
             return add({"kind": LITERALS, "literals": [_lit(s["const"])]})
         if "enum" in s:
@@ -189,6 +201,10 @@ class GuidedRegistry:
         return g
 
     def matcher(self, params) -> "Guide":
+        if getattr(params, "tool_grammar", None) is not None:
+            g = Guide(self, self.nat.JsonMatcher(self.grammar(
+                {"x-omnia-tool-union": params.tool_grammar})))
+            return g if params.tool_choice == "required" else TriggeredGuide(g)
         schema = params.json_schema if params.json_schema is not None else None
         return Guide(self, self.nat.JsonMatcher(self.grammar(schema)))
 
@@ -212,6 +228,55 @@ class Guide:
     @property
     def complete(self) -> bool:
         return self.m.is_complete()
+
+
+class TriggeredGuide:
+    """tool_choice "auto" on the local engine: the model is free until it opens
+    a JSON object (its first non-space bytes are ``{``); from then on the
+    tool-call grammar holds, so a call it starts is always a valid call of a
+    declared tool with schema-valid arguments.  Text answers stay unconstrained."""
+
+    __slots__ = ("g", "active", "off", "seen")
+
+    def __init__(self, g: Guide):
+        self.g = g
+        self.active = False
+        self.off = False
+        self.seen = b""
+
+    @property
+    def m(self):
+        return self.g.m if self.active else _Unfinished
+
+    def fill(self, row: np.ndarray) -> None:
+        if self.active:
+            self.g.fill(row)
+        else:
+            row[:] = np.uint32(0xFFFFFFFF)
+
+    def accept(self, tid: int) -> bool:
+        if self.active:
+            return self.g.accept(tid)
+        if self.off:
+            return True
+        b = self.g.reg.table[tid] if tid < len(self.g.reg.table) else b""
+        lead = (self.seen + b).lstrip()
+        if not lead:
+            self.seen += b
+            return True
+        if lead[:1] == b"{":
+            self.active = True
+            return self.g.m.accept_bytes(lead)
+        self.off = True  # a text answer: never constrain this turn
+        return True
+
+    @property
+    def complete(self) -> bool:
+        return self.g.complete if self.active else False
+
+
+class _Unfinished:
+    finished = False
 
 
 def masks_for(guides: list, words: int) -> np.ndarray:

@@ -25,6 +25,11 @@ class SamplingParams:
     # K13 guided decoding: JSON-schema-constrained output / any JSON object
     json_schema: dict | None = None
     json_object: bool = False
+    # tool calling on the in-node engine: [{"name", "parameters"}] of the offered
+    # tools; "required" constrains the whole answer to one valid Llama-3 tool call,
+    # "auto" only once the model opens a JSON object (engine/guided.py)
+    tool_grammar: list | None = None
+    tool_choice: str = "auto"
 
     @property
     def greedy(self) -> bool:
@@ -32,7 +37,7 @@ class SamplingParams:
 
     @property
     def guided(self) -> bool:
-        return self.json_schema is not None or self.json_object
+        return self.json_schema is not None or self.json_object or bool(self.tool_grammar)
 
     @property
     def needs_penalties(self) -> bool:

@@ -46,6 +46,9 @@ struct Node {
   int min_len = 0, max_len = -1;  // K_STRING
   std::vector<std::string> literals;  // K_LITERALS (enum / const / true,false / null)
   std::vector<int> children;          // K_UNION
+  // tagged object (tool-call union): props[0]'s value is an enum whose matched
+  // literal i selects tag_children[i] as the value schema of props[1]
+  std::vector<int> tag_children;
 };
 
 enum FK : uint8_t { F_VALUE = 0, F_OBJ, F_ARR, F_STR, F_NUM, F_LIT };
@@ -199,6 +202,18 @@ class Grammar {
         }
         p.phase = O_COLON;
       } else if (p.phase == O_VAL) {
+        const Node& nd = nodes[p.node];
+        if (!nd.tag_children.empty() && p.a == 0 && done.kind == F_LIT) {
+          // remember which tag literal the discriminator matched (F_OBJ frames do
+          // not use `alive` otherwise)
+          const Node& ln = nodes[done.node];
+          p.alive = 0;
+          for (int i = 0; i < (int)ln.literals.size() && i < 64; ++i)
+            if (((done.alive >> i) & 1) && (int)ln.literals[i].size() == done.a) {
+              p.alive = (uint64_t)i;
+              break;
+            }
+        }
         p.phase = O_AFTER;
       }
     } else if (p.kind == F_ARR) {
@@ -308,6 +323,10 @@ class Grammar {
               if (f.b < 0) return REJECT;
               f.a = f.b;
               child = nd.props[f.b].child;
+              if (!nd.tag_children.empty() && f.b == 1) {
+                if (f.alive >= nd.tag_children.size()) return REJECT;
+                child = nd.tag_children[f.alive];
+              }
             } else {
               child = nd.kind == K_OBJECT ? nd.items : 0;
             }
@@ -615,10 +634,25 @@ std::shared_ptr<Grammar> make_grammar(std::shared_ptr<Vocab> v, const py::list& 
     if (d.contains("literals")) n.literals = d["literals"].cast<std::vector<std::string>>();
     if (n.literals.size() > 64) throw std::invalid_argument("at most 64 enum values");
     if (d.contains("children")) n.children = d["children"].cast<std::vector<int>>();
+    if (d.contains("tag_children")) {
+      n.tag_children = d["tag_children"].cast<std::vector<int>>();
+      if (n.props.size() < 2) throw std::invalid_argument("tagged object needs 2 properties");
+    }
     g->nodes.push_back(std::move(n));
   }
   if (g->nodes.empty() || g->nodes[0].kind != K_ANY)
     throw std::invalid_argument("node 0 must be the ANY node");
+  const int nn = (int)g->nodes.size();
+  for (const Node& n : g->nodes) {  // every child reference in range
+    auto bad = [nn](int i) { return i < 0 || i >= nn; };
+    for (const Prop& p : n.props)
+      if (bad(p.child)) throw std::invalid_argument("property child out of range");
+    for (int c : n.children)
+      if (bad(c)) throw std::invalid_argument("union child out of range");
+    for (int c : n.tag_children)
+      if (bad(c)) throw std::invalid_argument("tag child out of range");
+    if (bad(n.items)) throw std::invalid_argument("items node out of range");
+  }
   return g;
 }
 

@@ -16,6 +16,8 @@ Reference behaviour (``internal/runtime/message.go:40-431``, PromptKit pipeline)
 """
 from __future__ import annotations
 
+import dataclasses
+
 import asyncio
 import json
 import logging
@@ -200,6 +202,18 @@ class Agent:
             calls_total = 0
             while True:
                 window = await self._truncate(msgs, self.cfg.context_window)
+                if tools and getattr(self.provider, "type", "") == "local" \
+                        and policy.tool_choice in ("auto", "required"):
+                    # the in-node engine enforces tool calls with a grammar.  "required"
+                    # forces a valid call of an offered tool on every round until
+                    # max_rounds tool rounds have run; the round after that is free
+                    # ("auto") so the agent answers instead of hitting the round cap
+                    params = dataclasses.replace(
+                        params, tool_grammar=[{"name": t["name"],
+                                               "parameters": t.get("parameters")
+                                               or {"type": "object"}} for t in tools],
+                        tool_choice=policy.tool_choice if res.rounds < max_rounds
+                        else "auto")
                 round_text: list[str] = []
                 round_calls: list[ToolCallReq] = []
                 span_llm = tracing.start_span("genai.chat", {

@@ -163,3 +163,65 @@ def test_response_format_mapping():
         "type": "json_schema", "json_schema": {"name": "x", "schema": {"type": "integer"}}}})
     assert p.json_schema == {"type": "integer"} and p.guided
     assert SamplingParams.from_dict({"response_format": {"type": "json_object"}}).json_object
+
+
+TOOLS = [
+    {"name": "get_weather", "parameters": {"type": "object", "properties": {
+        "city": {"type": "string", "maxLength": 12}, "unit": {"enum": ["C", "F"]}},
+        "required": ["city"]}},
+    {"name": "get_time", "parameters": {"type": "object", "properties": {
+        "tz": {"type": "integer"}}, "required": ["tz"]}},
+    {"name": "ping", "parameters": {"type": "object"}},
+]
+
+
+def _tool_schema_of(name):
+    return next(t["parameters"] for t in TOOLS if t["name"] == name)
+
+
+def test_tool_union_random_walks_are_valid_calls(reg):
+    """The tagged tool-call grammar: every completed document is a call of a
+    declared tool whose parameters validate against THAT tool's schema."""
+    rng = random.Random(5)
+    seen = set()
+    for _ in range(30):
+        text = _walk(reg, {"x-omnia-tool-union": TOOLS}, rng)
+        call = json.loads(text)
+        assert set(call) == {"name", "parameters"}
+        js.validate(call["parameters"], _tool_schema_of(call["name"]))
+        seen.add(call["name"])
+    assert len(seen) >= 2
+
+
+def test_tool_union_rejects_wrong_parameters(reg):
+    class P:
+        json_schema = {"x-omnia-tool-union": TOOLS}
+        json_object = False
+
+    ok = b'{"name":"get_time","parameters":{"tz":3}}'
+    bad = b'{"name":"get_time","parameters":{"city":"x"}}'
+    assert reg.matcher(P).m.accept_bytes(ok)
+    assert not reg.matcher(P).m.accept_bytes(bad)
+    assert not reg.matcher(P).m.accept_bytes(b'{"name":"nope"')
+
+
+def test_engine_forced_tool_call_and_auto_trigger():
+    """tool_choice=required on the local engine always yields a parseable call of
+    an offered tool; "auto" leaves text answers free."""
+    from omnia_amd.runtime.chat import parse_tool_calls
+
+    e = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", num_blocks=256, block_size=32,
+                               max_batch=8, max_model_len=1024))
+    req = [e.add_request(list(range(10, 40 + i)), SamplingParams(
+        temperature=t, seed=i, max_tokens=400, tool_grammar=TOOLS, tool_choice="required"))
+        for i, t in enumerate([0.0, 0.9, 1.3])]
+    auto = e.add_request(list(range(10, 30)), SamplingParams(
+        temperature=0.0, max_tokens=6, ignore_eos=True, tool_grammar=TOOLS, tool_choice="auto"))
+    e.run_until_done()
+    names = {t["name"] for t in TOOLS}
+    for s in req:
+        text = e.tokenizer.decode(s.output)
+        rest, calls = parse_tool_calls(text, names)
+        assert s.finish_reason.value == "stop" and len(calls) == 1, text
+        js.validate(calls[0].arguments, _tool_schema_of(calls[0].name))
+    assert len(auto.output) == 6

@@ -118,7 +118,8 @@ def cmd_delete(a):
 
     kind = crds.resolve_kind(a.kind)
     st, out = _http("DELETE", a.server + _path(kind, a.namespace, a.name))
-    print(f"{kind.lower()}/{a.name} {'deleted' if out and out.get('deleted') else 'not found'}")
+    ok = bool(out) and (out.get("deleted") or out.get("status") == "Success")
+    print(f"{kind.lower()}/{a.name} {'deleted' if ok else 'not found'}")
 
 
 def cmd_crds(a):
@@ -173,6 +174,30 @@ async def serve(port: int, manifests: list[str], engine: bool, host: str = "127.
     await asyncio.Event().wait()
 
 
+async def run_operator(kubeconfig: str | None, in_cluster: bool, leader_elect: bool,
+                       namespace: str, enterprise: bool, gpus: int | None) -> None:
+    """Real-cluster mode: the same reconcilers against a kube-apiserver
+    (``cmd/main.go:400-660``); pods are run by the kubelet, not a launcher."""
+    from .operator.kube import KubeClient, KubeConfig
+    from .operator.manager import Manager, license_validator_for, set_license_validator
+
+    cfg = KubeConfig.in_cluster() if in_cluster else (
+        KubeConfig.from_kubeconfig(kubeconfig) if kubeconfig else KubeConfig.auto())
+    client = KubeClient(cfg)
+    if enterprise:
+        set_license_validator(license_validator_for(
+            client, os.environ.get("OMNIA_LICENSE_PUBLIC_KEY") or None))
+    mgr = Manager(client, gpu_count=gpus, leader_elect=leader_elect, namespace=namespace)
+    await mgr.start()
+    print(f"omnia operator reconciling against {cfg.server} (leader={mgr.is_leader})",
+          flush=True)
+    try:
+        await asyncio.gather(*mgr.tasks)
+    finally:
+        await mgr.stop()
+        client.close()
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser("omnia")
     ap.add_argument("--server", default=os.environ.get("OMNIA_SERVER", "http://127.0.0.1:8090"))
@@ -184,6 +209,14 @@ def main(argv=None):
     p.add_argument("--leader-elect", action="store_true",
                    help="cluster mode: run reconcilers only while holding the Lease")
     p.add_argument("--enterprise", action="store_true", help="also run the EE controllers")
+    p = sp.add_parser("operator", help="run the controllers against a real kube-apiserver")
+    p.add_argument("--kubeconfig", default=None)
+    p.add_argument("--in-cluster", action="store_true")
+    p.add_argument("--leader-elect", action="store_true")
+    p.add_argument("--namespace", default=os.environ.get("OMNIA_NAMESPACE", "omnia-system"))
+    p.add_argument("--enterprise", action="store_true")
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs per node for the capability gate (default: unchecked)")
     p = sp.add_parser("chart", help="write the Helm chart + kustomize bases (deploy/)")
     p.add_argument("--out", default="deploy")
     p = sp.add_parser("apply")
@@ -208,6 +241,9 @@ def main(argv=None):
     if a.cmd == "serve":
         asyncio.run(serve(a.port, a.filename, not a.no_engine, enterprise=a.enterprise,
                           leader_elect=True))
+    elif a.cmd == "operator":
+        asyncio.run(run_operator(a.kubeconfig, a.in_cluster, a.leader_elect, a.namespace,
+                                 a.enterprise, a.gpus))
     elif a.cmd == "apply":
         cmd_apply(a)
     elif a.cmd == "get":

@@ -13,6 +13,7 @@ Namespace, Lease...) are stored as-is.
 from __future__ import annotations
 
 import asyncio
+import collections
 import copy
 import datetime as _dt
 import itertools
@@ -28,6 +29,10 @@ class NotFound(KeyError):
 
 class Conflict(Exception):
     pass
+
+
+class Gone(Exception):
+    """The requested resourceVersion is older than the retained watch history."""
 
 
 class Invalid(ValueError):
@@ -72,20 +77,36 @@ def match_labels(labels: dict, selector: dict | None) -> bool:
 
 
 class APIStore:
-    def __init__(self, webhooks: dict | None = None):
+    def __init__(self, webhooks: dict | None = None, history: int = 10000):
         self.objs: dict[tuple, dict] = {}
         self.rv = itertools.count(1)
+        self.last_rv = 0
         self.lock = threading.RLock()
         self.watchers: list[tuple] = []  # (kind or None, loop, queue)
         self.webhooks = webhooks or {}  # kind -> fn(obj, old) -> list[str] errors
+        # bounded event history (etcd's compaction window): a watch may resume
+        # from any resourceVersion still inside it, older ones get 410 Gone
+        self.history: collections.deque = collections.deque(maxlen=history)
+        self.compacted_rv = 0
 
     # ------------------------------------------------------------ helpers
     @staticmethod
     def key(kind: str, ns: str | None, name: str) -> tuple:
         return (kind, ns if is_namespaced(kind) else "", name)
 
+    def _next_rv(self) -> str:
+        self.last_rv = next(self.rv)
+        return str(self.last_rv)
+
+    def current_rv(self) -> str:
+        return str(self.last_rv)
+
     def _notify(self, etype: str, obj: dict):
         ev = (etype, copy.deepcopy(obj))
+        with self.lock:
+            if len(self.history) == self.history.maxlen:
+                self.compacted_rv = self.history[0][0]
+            self.history.append((int(obj["metadata"].get("resourceVersion") or 0), ev))
         for kind, loop, q in list(self.watchers):
             if kind is None or kind == obj["kind"]:
                 try:
@@ -97,6 +118,15 @@ class APIStore:
         q: asyncio.Queue = asyncio.Queue()
         self.watchers.append((kind, asyncio.get_running_loop(), q))
         return q
+
+    def events_since(self, rv: int, kind: str | None = None) -> list[tuple]:
+        """Events with resourceVersion > rv, or Gone if rv was compacted away."""
+        with self.lock:
+            if rv < self.compacted_rv:
+                raise Gone(f"too old resource version: {rv} ({self.compacted_rv})")
+            return sorted(((r, copy.deepcopy(ev)) for r, ev in self.history
+                           if r > rv and (kind is None or ev[1]["kind"] == kind)),
+                          key=lambda x: x[0])
 
     def unwatch(self, q):
         self.watchers = [w for w in self.watchers if w[2] is not q]
@@ -128,7 +158,7 @@ class APIStore:
             if k in self.objs:
                 raise Conflict(f"{kind} {md['name']} already exists")
             md["uid"] = str(uuid.uuid4())
-            md["resourceVersion"] = str(next(self.rv))
+            md["resourceVersion"] = self._next_rv()
             md["generation"] = 1
             md["creationTimestamp"] = now_ts()
             obj.setdefault("status", {})
@@ -188,7 +218,7 @@ class APIStore:
                         new["metadata"]["generation"] = cur["metadata"]["generation"] + 1
             if _same(new, cur):
                 return copy.deepcopy(cur)  # no-op write: no new resourceVersion, no event
-            new["metadata"]["resourceVersion"] = str(next(self.rv))
+            new["metadata"]["resourceVersion"] = self._next_rv()
             if new["metadata"].get("deletionTimestamp") and not new["metadata"].get(
                     "finalizers"):
                 self.objs.pop(k, None)
@@ -235,7 +265,7 @@ class APIStore:
             if cur["metadata"].get("finalizers"):
                 if not cur["metadata"].get("deletionTimestamp"):
                     cur["metadata"]["deletionTimestamp"] = now_ts()
-                    cur["metadata"]["resourceVersion"] = str(next(self.rv))
+                    cur["metadata"]["resourceVersion"] = self._next_rv()
                     out = copy.deepcopy(cur)
                 else:
                     return True
@@ -243,6 +273,7 @@ class APIStore:
             else:
                 self.objs.pop(k)
                 out = copy.deepcopy(cur)
+                out["metadata"]["resourceVersion"] = self._next_rv()
                 gone = True
         self._notify("DELETED" if gone else "MODIFIED", out)
         if gone:

@@ -107,6 +107,13 @@ class Manager:
         self.stats = {"reconciles": 0, "errors": 0}
         self._idle = None
         self._gens: dict = {}
+        self.lease = None
+        self.lease_duration_s = 15
+        self.processing: set = set()
+        self.dirty: set = set()
+        # a remote apiserver client blocks on HTTP: reconcile off the event loop
+        self.threaded = not isinstance(store, APIStore)
+        self.is_leader = False
 
     def enqueue(self, kind: str, ns: str | None, name: str, after: float = 0.0):
         key = (kind, ns or "", name)
@@ -170,28 +177,41 @@ class Manager:
     async def _acquire_lease(self) -> bool:
         if not self.leader_elect:
             return True
-        name = "omnia-operator-leader"
-        now = time.time()
-        lease = self.store.try_get("Lease", name, self.lease_ns)
-        if lease is None:
-            self.store.create({"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
-                               "metadata": {"name": name, "namespace": self.lease_ns},
-                               "spec": {"holderIdentity": self.identity, "renewTime": now,
-                                        "leaseDurationSeconds": 15}})
-            return True
-        sp = lease["spec"]
-        if sp["holderIdentity"] == self.identity or now - sp["renewTime"] > \
-                sp["leaseDurationSeconds"]:
-            lease["spec"] = {**sp, "holderIdentity": self.identity, "renewTime": now}
-            self.store.update(lease)
-            return True
-        return False
+        if self.lease is None:
+            from .kube import LeaseLock
+
+            self.lease = LeaseLock(self.store, "omnia-operator-leader", self.lease_ns,
+                                   self.identity, lease_duration_s=self.lease_duration_s,
+                                   renew_deadline_s=self.lease_duration_s * 2 / 3,
+                                   retry_period_s=self.lease_duration_s / 7.5)
+        return await asyncio.to_thread(self.lease.try_acquire_or_renew)
+
+    async def _renew_loop(self):
+        """Renew every retry period; a leader that cannot renew within the
+        renew deadline stops reconciling (client-go ``OnStoppedLeading``)."""
+        while True:
+            await asyncio.sleep(self.lease.retry_period_s)
+            ok = False
+            try:
+                ok = await asyncio.to_thread(self.lease.try_acquire_or_renew)
+            except Exception:  # noqa: BLE001 - apiserver blip: deadline decides
+                log.warning("lease renewal failed", exc_info=True)
+            if not ok and not self.lease.holds():
+                log.error("lost leader lease %s; stopping", self.identity)
+                self.is_leader = False
+                for t in self.tasks:
+                    if t is not asyncio.current_task():
+                        t.cancel()
+                return
 
     async def _watch_loop(self, q):
         try:
             while True:
                 etype, obj = await q.get()
-                self._map(etype, obj)
+                if self.threaded:
+                    await asyncio.to_thread(self._map, etype, obj)
+                else:
+                    self._map(etype, obj)
         finally:
             self.store.unwatch(q)
 
@@ -212,8 +232,15 @@ class Manager:
             r = self.reconcilers.get(kind)
             if r is None:
                 continue
+            if key in self.processing:
+                self.dirty.add(key)  # never reconcile one key concurrently
+                continue
+            self.processing.add(key)
             try:
-                after = r.reconcile(self.store, ns or None, name)
+                if self.threaded:
+                    after = await asyncio.to_thread(r.reconcile, self.store, ns or None, name)
+                else:
+                    after = r.reconcile(self.store, ns or None, name)
                 self.stats["reconciles"] += 1
                 if after:
                     self.enqueue(kind, ns, name, after)
@@ -221,16 +248,27 @@ class Manager:
                 self.stats["errors"] += 1
                 log.exception("reconcile %s %s/%s failed", kind, ns, name)
                 self.enqueue(kind, ns, name, 1.0)
+            finally:
+                self.processing.discard(key)
+                if key in self.dirty:
+                    self.dirty.discard(key)
+                    self.enqueue(kind, ns, name)
 
     async def start(self, workers: int = 4):
         self.queue = asyncio.Queue()
         while not await self._acquire_lease():
-            await asyncio.sleep(2)
+            await asyncio.sleep(self.lease.retry_period_s if self.lease else 2)
+        self.is_leader = True
         q = self.store.watch(None)  # register before listing: no missed events
-        for o in [o for kind in self.reconcilers for o in self.store.list(kind)]:
-            self._map("ADDED", o)
+        if isinstance(self.store, APIStore):
+            # in-memory store: its watch has no initial LIST; a KubeClient
+            # reflector delivers the initial LIST as ADDED events itself
+            for o in [o for kind in self.reconcilers for o in self.store.list(kind)]:
+                self._map("ADDED", o)
         self.tasks = [asyncio.ensure_future(self._watch_loop(q)),
                       asyncio.ensure_future(self._timer_loop())]
+        if self.lease is not None:
+            self.tasks.append(asyncio.ensure_future(self._renew_loop()))
         self.tasks += [asyncio.ensure_future(self._worker()) for _ in range(workers)]
 
     async def settle(self, timeout: float = 10.0, quiet: float = 0.2) -> None:
@@ -238,7 +276,8 @@ class Manager:
         t0 = time.monotonic()
         calm = None
         while time.monotonic() - t0 < timeout:
-            busy = not self.queue.empty() or bool(self.pending) or any(
+            busy = not self.queue.empty() or bool(self.pending) or bool(
+                self.processing) or any(
                 t <= time.monotonic() + quiet for t in self.delayed.values())
             if busy:
                 calm = None
@@ -252,3 +291,6 @@ class Manager:
         for t in self.tasks:
             t.cancel()
         await asyncio.gather(*self.tasks, return_exceptions=True)
+        if self.lease is not None and self.is_leader:
+            await asyncio.to_thread(self.lease.release)  # ReleaseOnCancel
+        self.is_leader = False

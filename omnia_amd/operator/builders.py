@@ -128,6 +128,15 @@ def facade_env(ar: dict) -> dict:
         env["OMNIA_INPUT_SCHEMA"] = json.dumps(spec["inputSchema"])
     if spec.get("outputSchema") is not None:
         env["OMNIA_OUTPUT_SCHEMA"] = json.dumps(spec["outputSchema"])
+    ea = spec.get("externalAuth") or {}
+    oidc = ea.get("oidc") or {}
+    if oidc:
+        env["OMNIA_OIDC_ISSUER"] = oidc.get("issuer", "")
+        if oidc.get("audience"):
+            env["OMNIA_OIDC_AUDIENCE"] = oidc["audience"]
+        env["OMNIA_OIDC_JWKS_FILE"] = "/etc/omnia/oidc/jwks.json"
+    if (ea.get("edgeTrust") or {}).get("enabled"):
+        env["OMNIA_EDGE_TRUST"] = "true"
     return env
 
 
@@ -140,7 +149,8 @@ def config_hash(*parts) -> str:
 
 def deployment(ar: dict, rc: RuntimeConfig, pack_cm: str, track: str = "stable",
                replicas: int | None = None, extra_hash=None,
-               facade_extra: dict | None = None) -> dict:
+               facade_extra: dict | None = None, sidecars: list | None = None,
+               sa_name: str | None = None) -> dict:
     spec, md = ar["spec"], ar["metadata"]
     rt = spec.get("runtime") or {}
     po = spec.get("podOverrides") or {}
@@ -192,12 +202,21 @@ def deployment(ar: dict, rc: RuntimeConfig, pack_cm: str, track: str = "stable",
     volumes = [{"name": "promptpack-config", "configMap": {"name": pack_cm}},
                {"name": "tools-config", "configMap": {"name": md["name"] + "-tools"}},
                {"name": "pack-cache", "emptyDir": {}}, *(rt.get("volumes") or [])]
+    if (spec.get("externalAuth") or {}).get("oidc"):
+        # the operator-mirrored JWKS Secret (agentruntime_oidc_jwks.go); optional so
+        # the pod starts before the first fetch lands (OIDC tokens 401 until then)
+        volumes.append({"name": "oidc-jwks", "secret": {
+            "secretName": f"agent-{md['name']}-oidc-jwks", "optional": True}})
+        containers[0].setdefault("volumeMounts", []).append(
+            {"name": "oidc-jwks", "mountPath": "/etc/omnia/oidc", "readOnly": True})
+    containers += list(sidecars or [])
     labels = {**pod_labels(ar, track), **(po.get("labels") or {})}
     ann = {ANN_CONFIG_HASH: config_hash(fenv, renv, extra_hash),
            **(po.get("annotations") or {}), **(spec.get("extraPodAnnotations") or {})}
     pod_spec = {"containers": containers, "volumes": volumes,
                 "terminationGracePeriodSeconds": 45,
-                "serviceAccountName": po.get("serviceAccountName") or md["name"] + "-facade"}
+                "serviceAccountName": sa_name or po.get("serviceAccountName") or
+                md["name"] + "-facade"}
     for f in ("nodeSelector", "tolerations", "affinity"):
         v = po.get(f) or rt.get(f)
         if v:

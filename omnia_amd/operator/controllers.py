@@ -15,6 +15,7 @@ from ..api import crds
 from ..models.config import REGISTRY as MODEL_REGISTRY
 from ..runtime.promptpack import PackError, PromptPack
 from . import builders as B
+from . import subresources as SR
 from .chart import COMPONENTS
 from .apistore import APIStore, NotFound, get_condition, owner_ref, set_condition
 
@@ -107,8 +108,9 @@ class PromptPackReconciler:
 class ProviderReconciler:
     kind = "Provider"
 
-    def __init__(self, gpu_count: int | None = None):
+    def __init__(self, gpu_count: int | None = None, cfg: SR.OperatorConfig | None = None):
         self.gpu_count = gpu_count
+        self.cfg = cfg or SR.OperatorConfig.from_env()
 
     def reconcile(self, store: APIStore, ns: str, name: str):
         pv = store.try_get("Provider", name, ns)
@@ -149,6 +151,22 @@ class ProviderReconciler:
         set_condition(st, "ModelValid", model_ok, "Valid" if model_ok else "Invalid", model_msg,
                       gen)
         ok = cred_ok and model_ok
+        # endpoint liveness (provider_controller.go:135-161): any HTTP response
+        # is reachable; a connection failure makes the provider Unavailable
+        url = SR.provider_health_url(spec) if cred_ok else ""
+        if url:
+            err = SR.check_endpoint_health(url, self.cfg)
+            if err is not None:
+                set_condition(st, "EndpointReachable", False, "EndpointUnreachable",
+                              f"health check failed: {err}"[:300], gen)
+                st["phase"] = "Unavailable"
+                set_condition(st, "Ready", False, "EndpointUnreachable", err[:300], gen)
+                st["observedGeneration"] = gen
+                pv["status"] = st
+                store.update_status(pv)
+                return SR.HEALTH_REQUEUE_S
+            set_condition(st, "EndpointReachable", True, "EndpointReachable",
+                          "health check passed", gen)
         st["phase"] = "Ready" if ok else "Error"
         set_condition(st, "Ready", ok, "Ready" if ok else "NotReady", cred_msg or model_msg, gen)
         st["observedGeneration"] = gen
@@ -159,32 +177,132 @@ class ProviderReconciler:
 
 # ===================================================================== ToolRegistry
 class ToolRegistryReconciler:
+    """Validate handlers, resolve endpoints, build ``discoveredTools`` and,
+    when ``spec.probe.enabled``, TCP-probe them on an interval
+    (``internal/controller/toolregistry_controller.go:55-346``,
+    ``toolregistry_probe.go:53-155``).  Phase: Ready (all available) /
+    Degraded (some) / Failed (none, or a handler failed validation)."""
+
     kind = "ToolRegistry"
+
+    def __init__(self, cfg: SR.OperatorConfig | None = None):
+        self.cfg = cfg or SR.OperatorConfig.from_env()
+
+    @staticmethod
+    def validate_handler(h: dict) -> str | None:
+        from ..tools.resilience import RetryPolicy
+
+        t = h.get("type")
+        cfgk = {"http": "httpConfig", "grpc": "grpcConfig", "mcp": "mcpConfig",
+                "openapi": "openAPIConfig"}.get(t)
+        if t not in ("http", "grpc", "mcp", "openapi", "client"):
+            return f"unknown handler type: {t}"
+        conf = h.get(cfgk) if cfgk else None
+        if t in ("http", "grpc") and conf is None and not h.get("endpoint"):
+            return f"{cfgk} is required for {t} handlers"
+        if t in ("http", "grpc", "client") and not h.get("tool"):
+            return f"tool definition is required for {t} handlers"
+        if t == "mcp":
+            if conf is None and not h.get("endpoint"):
+                return "mcpConfig is required for mcp handlers"
+            tr = (conf or {}).get("transport", "streamable-http" if h.get("endpoint") else "")
+            if tr in ("sse", "streamable-http") and not ((conf or {}).get("endpoint") or
+                                                          h.get("endpoint")):
+                return f"endpoint is required for mcp handlers with {tr} transport"
+            if tr == "stdio" and not (conf or {}).get("command"):
+                return "command is required for mcp handlers with stdio transport"
+        if t == "openapi" and conf is None:
+            return "openAPIConfig is required for openapi handlers"
+        for rp in [(conf or {}).get("retryPolicy"), h.get("retryPolicy")]:
+            if not rp:
+                continue
+            try:
+                p = RetryPolicy.from_cfg(rp)
+            except (TypeError, ValueError) as e:
+                return f"invalid retryPolicy: {e}"
+            if p.max_attempts < 1:
+                return "retryPolicy.maxAttempts must be >= 1"
+            if p.multiplier < 1:
+                return "retryPolicy.backoffMultiplier must be >= 1"
+            if p.max_backoff < p.initial_backoff:
+                return "retryPolicy.maxBackoff must be >= initialBackoff"
+        return None
+
+    @staticmethod
+    def resolve_endpoint(h: dict) -> str:
+        t = h.get("type")
+        conf = h.get({"http": "httpConfig", "grpc": "grpcConfig", "mcp": "mcpConfig",
+                      "openapi": "openAPIConfig"}.get(t, ""), None) or {}
+        if t in ("http", "grpc"):
+            return conf.get("endpoint") or h.get("endpoint", "")
+        if t == "mcp":
+            if conf.get("endpoint") or h.get("endpoint"):
+                return conf.get("endpoint") or h["endpoint"]
+            return f"stdio://{conf.get('command', '')}"
+        if t == "openapi":
+            return conf.get("specURL") or conf.get("baseURL") or h.get("endpoint", "")
+        return "client://browser"
 
     def reconcile(self, store: APIStore, ns: str, name: str):
         tr = store.try_get("ToolRegistry", name, ns)
         if tr is None:
             return None
         st = tr.get("status") or {}
-        tools = []
+        gen = tr["metadata"]["generation"]
+        now = SR._rfc3339(time.time())
+        tools, errors = [], []
         for h in tr["spec"].get("handlers", []):
+            err = self.validate_handler(h)
+            if err:
+                errors.append(f"handler {h.get('name')!r}: {err}")
+                continue
+            ep = self.resolve_endpoint(h)
             t = h.get("tool")
-            if t:
-                tools.append({"name": t["name"], "description": t.get("description", ""),
-                              "handlerName": h["name"], "handlerType": h["type"],
-                              "status": "Available"})
-            else:
-                tools.append({"name": h["name"] + ".*", "handlerName": h["name"],
-                              "handlerType": h["type"], "status": "Discoverable"})
+            if t and h["type"] in ("http", "grpc", "client"):
+                d = {"name": t["name"], "handlerName": h["name"],
+                     "description": t.get("description", ""), "endpoint": ep,
+                     "status": "Available", "lastChecked": now}
+                if t.get("inputSchema") is not None:
+                    d["inputSchema"] = t["inputSchema"]
+                if t.get("outputSchema") is not None:
+                    d["outputSchema"] = t["outputSchema"]
+                tools.append(d)
+            else:  # self-describing (mcp / openapi): discovered at runtime
+                tools.append({"name": h["name"], "handlerName": h["name"],
+                              "description": f"Self-describing {h['type']} handler (tools "
+                                             "discovered at runtime)",
+                              "endpoint": ep, "status": "Available", "lastChecked": now})
+        probe = tr["spec"].get("probe") or {}
+        if probe.get("enabled"):
+            from ..runtime.context_store import parse_ttl
+
+            SR.probe_tools(tools, float(parse_ttl(probe.get("timeout", "5s")) or
+                                        SR.PROBE_TIMEOUT_S), self.cfg.dial)
         st["discoveredTools"] = tools
-        st["toolCount"] = len(tools)
-        st["phase"] = "Ready"
-        set_condition(st, "Ready", True, "HandlersValid", "", tr["metadata"]["generation"])
-        st["observedGeneration"] = tr["metadata"]["generation"]
+        st["discoveredToolsCount"] = st["toolCount"] = len(tools)
+        st["lastDiscoveryTime"] = now
+        avail = sum(1 for t in tools if t["status"] == "Available")
+        if errors:
+            st["phase"] = "Failed"
+            set_condition(st, "HandlersValid", False, "ValidationFailed",
+                          f"Handler validation errors: {errors}"[:1000], gen)
+        else:
+            st["phase"] = "Failed" if not tools or avail == 0 else (
+                "Ready" if avail == len(tools) else "Degraded")
+            set_condition(st, "HandlersValid", True, "HandlersValid",
+                          "All handlers validated successfully", gen)
+        set_condition(st, "ToolsDiscovered", True, "ToolsDiscovered",
+                      f"Discovered {len(tools)} tool(s) from "
+                      f"{len(tr['spec'].get('handlers', []))} handler(s)", gen)
+        set_condition(st, "Ready", st["phase"] == "Ready", st["phase"], "", gen)
+        st["observedGeneration"] = gen
         tr["status"] = st
         store.update_status(tr)
-        probe = tr["spec"].get("probe") or {}
-        return 60.0 if probe.get("enabled") else None
+        if probe.get("enabled"):
+            from ..runtime.context_store import parse_ttl
+
+            return float(parse_ttl(probe.get("interval", "60s")) or SR.PROBE_INTERVAL_S)
+        return None
 
 
 # ===================================================================== AgentRuntime
@@ -203,8 +321,9 @@ def workspace_service_group(store: APIStore, ns: str, group: str) -> dict | None
 class AgentRuntimeReconciler:
     kind = "AgentRuntime"
 
-    def __init__(self, gpu_count: int | None = None):
+    def __init__(self, gpu_count: int | None = None, cfg: SR.OperatorConfig | None = None):
         self.gpu_count = gpu_count
+        self.cfg = cfg or SR.OperatorConfig.from_env()
 
     def _fail(self, store, ar, st, cond, reason, msg, phase=PENDING):
         set_condition(st, cond, False, reason, msg, ar["metadata"]["generation"])
@@ -220,6 +339,8 @@ class AgentRuntimeReconciler:
             return None
         md = ar["metadata"]
         if md.get("deletionTimestamp"):
+            # the departing agent no longer holds its group's eval worker
+            SR.reconcile_eval_workers(store, ns, self.cfg)
             md["finalizers"] = [f for f in md.get("finalizers", []) if f != B.FINALIZER]
             store.update(ar)
             return None
@@ -304,6 +425,11 @@ class AgentRuntimeReconciler:
             set_condition(st, "ServiceGroupReady", False, "NotFound",
                           f"service group {spec['serviceGroup']!r} not found", gen)
         # ---- owned objects
+        sa_name = SR.reconcile_facade_rbac(store, ar, self.cfg)
+        sidecars = []
+        if self.cfg.policy_broker_image:
+            sidecars.append(SR.policy_broker_container(ar, self.cfg))
+            rc.policy_broker_url = f"http://127.0.0.1:{SR.POLICY_BROKER_PORT}"
         store.apply(B.tools_configmap(ar, registry))
         pack_cm = pack["spec"]["source"].get("configMapRef", {}).get("name", "")
         a = ((spec.get("runtime") or {}).get("autoscaling") or {})
@@ -313,9 +439,22 @@ class AgentRuntimeReconciler:
                 replicas = cur["spec"].get("replicas")
         dep = B.deployment(ar, rc, pack_cm, "stable", replicas,
                            extra_hash=[pack["spec"]["version"], (registry or {}).get("spec")],
-                           facade_extra=facade_extra)
+                           facade_extra=facade_extra, sidecars=sidecars, sa_name=sa_name)
         store.apply(dep)
         store.apply(B.service(ar))
+        route = SR.reconcile_facade_route(store, ar, self.cfg)
+        if route is not None:
+            st["externalURL"] = f"https://{route['host']}"
+        else:
+            st.pop("externalURL", None)
+        workers = SR.reconcile_eval_workers(store, ns, self.cfg)
+        if (spec.get("evals") or {}).get("enabled"):
+            grp = spec.get("serviceGroup") or "default"
+            set_condition(st, "EvalWorkerReady", True,
+                          "WorkerDeployed" if grp in workers else "InlineEvals",
+                          f"arena-eval-worker-{grp}" if grp in workers else
+                          "evaluated inline by the runtime", gen)
+        jwks_after = SR.reconcile_oidc_jwks(store, ar, st, self.cfg)
         want_r = dep["spec"]["replicas"]
         if want_r and want_r > 1:
             store.apply(B.pdb(ar))
@@ -362,6 +501,8 @@ class AgentRuntimeReconciler:
         store.update_status(ar)
         if not dep_ok:
             return 2.0
+        if jwks_after is not None:
+            requeue = min(requeue, jwks_after) if requeue else jwks_after
         return requeue
 
     # ---------------------------------------------------------------- rollout
@@ -594,9 +735,12 @@ class SimplePolicyReconciler:
         return None
 
 
-def default_reconcilers(gpu_count: int | None = None) -> list:
-    rs = [PromptPackReconciler(), ProviderReconciler(gpu_count), ToolRegistryReconciler(),
-          AgentRuntimeReconciler(gpu_count), WorkspaceReconciler()]
+def default_reconcilers(gpu_count: int | None = None,
+                        cfg: SR.OperatorConfig | None = None) -> list:
+    cfg = cfg or SR.OperatorConfig.from_env()
+    rs = [PromptPackReconciler(), ProviderReconciler(gpu_count, cfg),
+          ToolRegistryReconciler(cfg), AgentRuntimeReconciler(gpu_count, cfg),
+          WorkspaceReconciler()]
     for k in ("AgentPolicy", "ToolPolicy", "MemoryPolicy", "SessionRetentionPolicy",
               "SessionPrivacyPolicy", "RolloutAnalysis", "ArenaDevSession"):
         rs.append(SimplePolicyReconciler(k))

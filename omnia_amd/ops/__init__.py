@@ -200,11 +200,13 @@ WGEMM_MAX_M = 256
 
 _wgemm_table: dict | None = None
 _wgemm_on = os.environ.get("OMNIA_WGEMM", "1") != "0"
-WGEMM_BUCKETS = (16, 32, 64, 128, 256)
+WGEMM_BUCKETS = (16, 32, 64, 128, 192, 256)
 
 
 def wgemm_config(M: int, N: int, K: int, mode: int) -> tuple[int, int, int] | None:
-    """(nw, nwaves, splits) of the weight-streaming kernel for a decode projection,
+    """(nw, nwaves, splits) of the weight-streaming kernel for a decode projection
+    (nwaves == 0 selects the wide-batch 32x32x16 kernel, wgemm_wide.hip, with nw
+    32-column tiles per wave),
     or None to keep the library / gemm.hip path.  ``mode`` 0 = plain projection
     (its split-K slabs are reduced by the consumer kernel), 1 = gate_up + SwiGLU.
     Measured dispatch: ``ops/tuned/wgemm_mi355x.json`` (scripts/wgemm_sweep.py +
@@ -221,7 +223,10 @@ def wgemm_config(M: int, N: int, K: int, mode: int) -> tuple[int, int, int] | No
             with open(p) as f:
                 _wgemm_table = {k: tuple(v) for k, v in json.load(f).items()}
     b = next(x for x in WGEMM_BUCKETS if M <= x)
-    return _wgemm_table.get(f"{mode}:{b}:{N}:{K}")
+    cfg = _wgemm_table.get(f"{mode}:{b}:{N}:{K}")
+    if cfg is None and b == 192:  # the 192 bucket only lists its own wins
+        cfg = _wgemm_table.get(f"{mode}:256:{N}:{K}")
+    return cfg
 
 
 def wgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, nw: int = 2,
@@ -231,12 +236,27 @@ def wgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, nw: int 
     mode 0: bf16 ``x @ w.T``; mode 1: bf16 ``silu(x Wg^T) * (x Wu^T)`` with
     ``w = [Wg; Wu]``; mode 2: fp32 split-K partial slabs ``[splits, M, N]`` whose
     sum is ``x @ w.T`` (reduced by the consumer kernel)."""
+    if nwaves == 0:  # table code for the wide-batch kernel: nw = 32-col tiles per wave
+        return wgemm_wide(mode, x, w, splits, nw, out)
     M, K = x.shape
     N = w.shape[0] // 2 if mode == 1 else w.shape[0]
     if out is None:
         out = (torch.empty(splits, M, N, dtype=torch.float32, device=x.device) if mode == 2
                else x.new_empty(M, N))
     kernels().wgemm(mode, out, x.contiguous(), w, splits, nw, nwaves)
+    return out
+
+
+def wgemm_wide(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, wt: int = 2,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """Wide-batch (128 < M <= 256) weight-streaming decode GEMM on 32x32x16 MFMA
+    (``csrc/wgemm_wide.hip``); same modes and outputs as :func:`wgemm`."""
+    M, K = x.shape
+    N = w.shape[0] // 2 if mode == 1 else w.shape[0]
+    if out is None:
+        out = (torch.empty(splits, M, N, dtype=torch.float32, device=x.device) if mode == 2
+               else x.new_empty(M, N))
+    kernels().wgemm_wide(mode, out, x.contiguous(), w, splits, wt)
     return out
 
 

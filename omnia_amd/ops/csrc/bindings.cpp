@@ -74,6 +74,8 @@ int omnia_ar_twoshot(void* out, const void* in, void* residual, const void* w,
                      int64_t slot_bytes, int rank, int world, float eps, hipStream_t s);
 int omnia_wgemm(int mode, void* out, const void* X, const void* W, int M, int N, int K, int S,
                 int nw, int nwaves, int ldo, hipStream_t s);
+int omnia_wgemm_wide(int mode, void* out, const void* X, const void* W, int M, int N, int K,
+                     int S, int wt, int ldo, hipStream_t s);
 int omnia_dgemm(int mode, void* out, const void* X, const void* W, float* ws, int* cnt, int M,
                 int N, int K, int S, int wm, int wn, int ldo, int64_t ws_floats, int cnt_len,
                 hipStream_t s);
@@ -422,6 +424,36 @@ void wgemm(int64_t mode, at::Tensor out, at::Tensor x, at::Tensor W, int64_t spl
            "wgemm");
 }
 
+// wide-batch weight-streaming decode GEMM (wgemm_wide.hip, 128 < M <= 256):
+// same modes / out shapes as wgemm; wt = 32-column MFMA tiles per wave (1 or 2)
+void wgemm_wide(int64_t mode, at::Tensor out, at::Tensor x, at::Tensor W, int64_t splits,
+                int64_t wt) {
+  CHECK_BF16(x); CHECK_BF16(W);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2, "2-D operands");
+  TORCH_CHECK(x.is_contiguous() && W.is_contiguous(), "contiguous x / W");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(W.size(1) == K, "K mismatch");
+  TORCH_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");
+  TORCH_CHECK(mode != 1 || W.size(0) % 2 == 0, "gate_up rows even");
+  const int N = mode == 1 ? W.size(0) / 2 : W.size(0);
+  int ldo;
+  if (mode == 2) {
+    TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_cuda() && out.is_contiguous(),
+                "mode 2: fp32 contiguous slabs");
+    TORCH_CHECK(out.dim() == 3 && out.size(0) == splits && out.size(1) == M && out.size(2) == N,
+                "mode 2: out [S, M, N]");
+    ldo = N;
+  } else {
+    CHECK_BF16(out);
+    TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N && out.stride(1) == 1,
+                "out [M, N]");
+    ldo = out.stride(0);
+  }
+  CHECK_RC(omnia_wgemm_wide((int)mode, out.data_ptr(), x.data_ptr(), W.data_ptr(), M, N, K,
+                            (int)splits, (int)wt, ldo, cur_stream()),
+           "wgemm_wide");
+}
+
 // ------------------------------------------------- split-K consumers (splitk.hip)
 static void check_parts(const at::Tensor& p) {
   TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat && p.is_contiguous() && p.dim() == 3,
@@ -625,6 +657,7 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("moe_combine", &moe_combine);
   m.def("dgemm", &dgemm);
   m.def("wgemm", &wgemm);
+  m.def("wgemm_wide", &wgemm_wide);
   m.def("ar_twoshot", &ar_twoshot);
   m.def("ar_region_bytes", &omnia_ar_region_bytes);
   m.def("splitk_add_rmsnorm", &splitk_add_rmsnorm);

@@ -47,8 +47,55 @@ def load_arena_config(store, job: dict) -> dict:
         return yaml.safe_load(f) or {}
 
 
-def write_dataset(records: list[dict], fmt: str, path: str | None, job: str) -> dict:
-    """Serialise datagen records as json / jsonl / csv (``DataGenSettings.format``)."""
+def output_location(output: dict | None) -> dict | None:
+    """``spec.output`` (``ee/api/v1alpha1/arenajob_types.go:197-257``) -> where a
+    job's artefacts go: ``pvc`` = ``<OMNIA_PVC_ROOT>/<claimName>/<subPath>`` (the
+    claim's mount point on this node), ``s3`` = bucket + prefix (+ endpoint)."""
+    import os
+
+    if not output:
+        return None
+    if output.get("type") == "pvc":
+        pvc = output.get("pvc") or {}
+        root = os.environ.get("OMNIA_PVC_ROOT", "/var/lib/omnia/pvc")
+        return {"type": "pvc", "path": os.path.join(root, pvc.get("claimName", ""),
+                                                     pvc.get("subPath", ""))}
+    if output.get("type") == "s3":
+        return {"type": "s3", **(output.get("s3") or {})}
+    return None
+
+
+def put_s3_object(loc: dict, key: str, body: bytes, creds: dict) -> str:
+    """PUT ``body`` at ``s3://bucket/prefix/key`` with a SigV4-presigned URL
+    (``media.sigv4_presign``); a custom ``endpoint`` (MinIO, Ceph) is path-style."""
+    import urllib.parse
+    import urllib.request
+
+    from ...media import sigv4_presign
+
+    ep = loc.get("endpoint") or ""
+    prefix = (loc.get("prefix") or "").strip("/")
+    obj = "/".join(p for p in (prefix, key) if p)
+    if ep:
+        u = urllib.parse.urlsplit(ep if "://" in ep else "https://" + ep)
+        host, scheme, path = u.netloc, u.scheme, f"/{loc['bucket']}/{obj}"
+    else:
+        host = f"{loc['bucket']}.s3.{loc.get('region') or 'us-east-1'}.amazonaws.com"
+        scheme, path = "https", f"/{obj}"
+    url = sigv4_presign("PUT", host, path, loc.get("region") or "us-east-1", "s3",
+                        creds.get("access_key", ""), creds.get("secret_key", ""),
+                        scheme=scheme)
+    req = urllib.request.Request(url, data=body, method="PUT")
+    with urllib.request.urlopen(req, timeout=30) as r:
+        if r.status >= 300:
+            raise OSError(f"S3 PUT {r.status}")
+    return f"s3://{loc['bucket']}/{obj}"
+
+
+def write_dataset(records: list[dict], fmt: str, output: dict | None, job: str,
+                  creds: dict | None = None) -> dict:
+    """Serialise datagen records as json / jsonl / csv (``DataGenSettings.format``)
+    into ``spec.output`` (a PVC directory or an S3 object); inline when unset."""
     import csv
     import io
     import os
@@ -70,18 +117,35 @@ def write_dataset(records: list[dict], fmt: str, path: str | None, job: str) -> 
     else:
         raise ValueError(f"unsupported datagen format {fmt!r}")
     out = {"records": len(records), "format": fmt}
-    if path:
-        os.makedirs(path, exist_ok=True)
-        fn = os.path.join(path, f"{job}.{fmt}")
+    loc = output_location(output)
+    if loc is not None and loc["type"] == "pvc":
+        os.makedirs(loc["path"], exist_ok=True)
+        fn = os.path.join(loc["path"], f"{job}.{fmt}")
         with open(fn, "w") as f:
             f.write(body)
         out["path"] = fn
+        out["url"] = "file://" + fn
+    elif loc is not None and loc["type"] == "s3":
+        out["url"] = put_s3_object(loc, f"{job}.{fmt}", body.encode(), creds or {})
     else:
         out["inline"] = body
     return out
 
 
 class ArenaJobController:
+    def _s3_creds(self, output: dict | None, ns: str) -> dict:
+        """Access keys for an s3 output from its secretRef (AWS-style key names)."""
+        import base64
+
+        ref = ((output or {}).get("s3") or {}).get("secretRef") or {}
+        sec = self.store.try_get("Secret", ref.get("name", ""), ns) if ref else None
+        if sec is None:
+            return {}
+        data = {k: base64.b64decode(v).decode() for k, v in (sec.get("data") or {}).items()}
+        data.update(sec.get("stringData") or {})
+        return {"access_key": data.get("AWS_ACCESS_KEY_ID") or data.get("access-key", ""),
+                "secret_key": data.get("AWS_SECRET_ACCESS_KEY") or data.get("secret-key", "")}
+
     def __init__(self, store, queue, provider_objects: dict | None = None):
         self.store = store
         self.q = queue
@@ -157,7 +221,9 @@ class ArenaJobController:
         if job_type == "datagen":
             dataset = write_dataset([r["record"] for r in results if r.get("record")],
                                     (spec.get("dataGen") or {}).get("format", "jsonl"),
-                                    (spec.get("output") or {}).get("path"), md["name"])
+                                    spec.get("output"), md["name"],
+                                    self._s3_creds(spec.get("output"),
+                                                   md.get("namespace", "default")))
         phase = "Succeeded" if ok and stats.errors < max(1, stats.total) else "Failed"
         job = self.store.get("ArenaJob", md["name"], md.get("namespace", "default"))
         self._status(job, phase, progress={"total": len(items), "done": len(results)},

@@ -199,7 +199,8 @@ def _hmac(key: bytes, msg: str) -> bytes:
 def sigv4_presign(method: str, host: str, path: str, region: str, service: str,
                   access_key: str, secret_key: str, expires_s: int = 900, now=None,
                   algo: str = "AWS4-HMAC-SHA256", prefix: str = "AWS4",
-                  req_type: str = "aws4_request", header_prefix: str = "X-Amz") -> str:
+                  req_type: str = "aws4_request", header_prefix: str = "X-Amz",
+                  scheme: str = "https") -> str:
     """Query-string presigned URL (AWS SigV4; GCS V4 HMAC uses the same scheme with
     the ``GOOG4`` names)."""
     t = now or dt.datetime.now(dt.timezone.utc)
@@ -220,7 +221,7 @@ def sigv4_presign(method: str, host: str, path: str, region: str, service: str,
     k = _hmac(k, service)
     k = _hmac(k, req_type)
     sig = hmac.new(k, sts.encode(), hashlib.sha256).hexdigest()
-    return f"https://{host}{canon_path}?{canon_q}&{header_prefix}-Signature={sig}"
+    return f"{scheme}://{host}{canon_path}?{canon_q}&{header_prefix}-Signature={sig}"
 
 
 class S3MediaStorage(_Base):

@@ -265,9 +265,18 @@ def build_app(store: APIStore, token: str | None = None,
             store.unwatch(q)
         return resp
 
+    def json_ok(obj, status=200):
+        headers = {}
+        if store.warnings:  # Warn-mode pruning surfaces as HTTP Warning headers
+            headers["Warning"] = ", ".join(f'299 - "{w}"' for w in store.warnings[:10])
+        return web.json_response(obj, status=status, headers=headers)
+
     async def handle(request):
         if not authed(request):
             return err(401, "Unauthorized", "Unauthorized")
+        fv = request.query.get("fieldValidation") or None
+        if fv not in (None, "Strict", "Warn", "Ignore"):
+            return err(400, "BadRequest", f"invalid fieldValidation {fv!r}")
         mi = request.match_info
         try:
             kind = kind_of(mi["plural"])
@@ -298,13 +307,13 @@ def build_app(store: APIStore, token: str | None = None,
                 body.setdefault("kind", kind)
                 if ns:
                     body.setdefault("metadata", {})["namespace"] = ns
-                return web.json_response(store.create(body), status=201)
+                return json_ok(store.create(body, fv), status=201)
             if request.method == "PUT":
                 body = await request.json()
                 body.setdefault("kind", kind)
                 if sub == "status":
                     return web.json_response(store.update_status(body))
-                return web.json_response(store.update(body))
+                return json_ok(store.update(body, field_validation=fv))
             if request.method == "PATCH":
                 ctype = request.headers.get("Content-Type", "").split(";")[0].strip()
                 raw = await request.read()
@@ -321,7 +330,7 @@ def build_app(store: APIStore, token: str | None = None,
                         cur["status"] = merge_patch(cur.get("status") or {},
                                                     body.get("status") or {})
                         return web.json_response(store.update_status(cur))
-                    return web.json_response(store.apply(body))
+                    return json_ok(store.apply(body, fv))
                 patch = json.loads(raw or b"{}")
                 cur = store.get(kind, name, ns)
                 if ctype == "application/json-patch+json":
@@ -340,7 +349,7 @@ def build_app(store: APIStore, token: str | None = None,
                     new["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
                 if sub == "status":
                     return web.json_response(store.update_status(new))
-                return web.json_response(store.update(new))
+                return json_ok(store.update(new, field_validation=fv))
             if request.method == "DELETE":
                 existed = store.delete(kind, name, ns)
                 if not existed:

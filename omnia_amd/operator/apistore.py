@@ -77,7 +77,8 @@ def match_labels(labels: dict, selector: dict | None) -> bool:
 
 
 class APIStore:
-    def __init__(self, webhooks: dict | None = None, history: int = 10000):
+    def __init__(self, webhooks: dict | None = None, history: int = 10000,
+                 field_validation: str = "Strict"):
         self.objs: dict[tuple, dict] = {}
         self.rv = itertools.count(1)
         self.last_rv = 0
@@ -87,6 +88,9 @@ class APIStore:
         # bounded event history (etcd's compaction window): a watch may resume
         # from any resourceVersion still inside it, older ones get 410 Gone
         self.history: collections.deque = collections.deque(maxlen=history)
+        # default fieldValidation for writes that do not pass one (kubectl: Strict)
+        self.field_validation = field_validation
+        self.warnings: list[str] = []  # last write's warnings (Warn mode pruning)
         self.compacted_rv = 0
 
     # ------------------------------------------------------------ helpers
@@ -131,10 +135,12 @@ class APIStore:
     def unwatch(self, q):
         self.watchers = [w for w in self.watchers if w[2] is not q]
 
-    def _admit(self, obj: dict, old: dict | None):
+    def _admit(self, obj: dict, old: dict | None, field_validation: str | None = None):
         kind = obj.get("kind")
+        self.warnings = []
         if kind in crds.KINDS:
-            errs = crds.validate_object(obj)
+            errs = crds.validate_object(obj, old, field_validation or self.field_validation,
+                                        self.warnings)
             hook = self.webhooks.get(kind)
             if hook is not None and not errs:
                 errs += hook(obj, old) or []
@@ -142,7 +148,7 @@ class APIStore:
                 raise Invalid(errs)
 
     # ------------------------------------------------------------ CRUD
-    def create(self, obj: dict) -> dict:
+    def create(self, obj: dict, field_validation: str | None = None) -> dict:
         obj = copy.deepcopy(obj)
         md = obj.setdefault("metadata", {})
         if not md.get("name") and md.get("generateName"):
@@ -152,7 +158,7 @@ class APIStore:
             md.setdefault("namespace", "default")
         else:
             md.pop("namespace", None)
-        self._admit(obj, None)
+        self._admit(obj, None, field_validation)
         with self.lock:
             k = self.key(kind, md.get("namespace"), md["name"])
             if k in self.objs:
@@ -188,7 +194,8 @@ class APIStore:
         return sorted(out, key=lambda o: (o["metadata"].get("namespace", ""),
                                           o["metadata"]["name"]))
 
-    def update(self, obj: dict, subresource: str | None = None) -> dict:
+    def update(self, obj: dict, subresource: str | None = None,
+               field_validation: str | None = None) -> dict:
         obj = copy.deepcopy(obj)
         kind, md = obj["kind"], obj["metadata"]
         with self.lock:
@@ -213,7 +220,7 @@ class APIStore:
                                                                         "spec")} != \
                         {k2: v for k2, v in cur.items() if k2 not in ("metadata", "status",
                                                                       "spec")}:
-                    self._admit(new, cur)
+                    self._admit(new, cur, field_validation)
                     if new.get("spec") != cur.get("spec"):
                         new["metadata"]["generation"] = cur["metadata"]["generation"] + 1
             if _same(new, cur):
@@ -237,12 +244,12 @@ class APIStore:
     def update_status(self, obj: dict) -> dict:
         return self.update(obj, subresource="status")
 
-    def apply(self, obj: dict) -> dict:
+    def apply(self, obj: dict, field_validation: str | None = None) -> dict:
         """Create-or-update (server-side-apply-lite): spec/labels/annotations/data win."""
         md = obj.get("metadata", {})
         cur = self.try_get(obj["kind"], md.get("name"), md.get("namespace", "default"))
         if cur is None:
-            return self.create(obj)
+            return self.create(obj, field_validation)
         new = copy.deepcopy(cur)
         for k, v in obj.items():
             if k in ("metadata", "status"):
@@ -254,7 +261,7 @@ class APIStore:
         new["metadata"].pop("resourceVersion", None)
         if new == cur:
             return cur
-        return self.update(new)
+        return self.update(new, field_validation=field_validation)
 
     def delete(self, kind: str, name: str, ns: str | None = "default") -> bool:
         with self.lock:

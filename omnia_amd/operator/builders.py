@@ -288,7 +288,7 @@ def scaled_object(ar: dict, a: dict, prometheus: str = "http://prometheus:9090")
             "serverAddress": prometheus,
             "query": (f'sum(omnia_agent_connections_active{{agent="{md["name"]}",'
                       f'namespace="{md["namespace"]}"}})'),
-            "threshold": str(k.get("threshold", KEDA_DEFAULT_THRESHOLD))}}]
+            "threshold": str(k.get("connectionThreshold") or KEDA_DEFAULT_THRESHOLD)}}]
     return {"apiVersion": "keda.sh/v1alpha1", "kind": "ScaledObject",
             "metadata": {"name": md["name"], "namespace": md["namespace"],
                          "ownerReferences": [owner_ref(ar)]},

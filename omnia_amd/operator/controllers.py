@@ -523,9 +523,14 @@ class AgentRuntimeReconciler:
         ros = st.get("rollout") or {"currentStep": 0, "weight": 0, "phase": "Progressing",
                                     "stepStarted": time.time()}
         cand_ar = json.loads(json.dumps(ar))
-        if cand_spec.get("promptPackVersion"):
-            cand_ar["spec"]["promptPackRef"] = {"name": spec["promptPackRef"]["name"],
-                                                "version": cand_spec["promptPackVersion"]}
+        # candidate overrides (rollout_types.go:71-91): a promptPackRef (pinned
+        # version or track), provider refs and/or a tool registry
+        if cand_spec.get("promptPackRef"):
+            cand_ar["spec"]["promptPackRef"] = dict(cand_spec["promptPackRef"])
+        if cand_spec.get("providerRefs"):
+            cand_ar["spec"]["providers"] = list(cand_spec["providerRefs"])
+        if cand_spec.get("toolRegistryRef"):
+            cand_ar["spec"]["toolRegistryRef"] = dict(cand_spec["toolRegistryRef"])
         cand_pack = resolve_promptpack(store, ns, cand_ar["spec"]["promptPackRef"]) or pack
         steps = ro.get("steps") or [{"setWeight": 100}]
         if ros["phase"] == "Progressing":

@@ -243,8 +243,10 @@ class KubeClient:
     """APIStore-compatible client of a real kube-apiserver."""
 
     def __init__(self, cfg: KubeConfig, field_manager: str = FIELD_MANAGER,
-                 timeout: float = 30.0, watch_timeout_s: int = 300):
+                 timeout: float = 30.0, watch_timeout_s: int = 300,
+                 field_validation: str = "Strict"):
         self.cfg = cfg
+        self.field_validation = field_validation  # what kubectl sends
         self.field_manager = field_manager
         self.timeout = timeout
         self.watch_timeout_s = watch_timeout_s
@@ -325,13 +327,16 @@ class KubeClient:
         ns = md.get("namespace") or ("default" if resource_of(kind)[2] else None)
         if resource_of(kind)[2]:
             md["namespace"] = ns
-        return self._with_type(kind, self._request("POST", resource_path(kind, ns), obj))
+        return self._with_type(kind, self._request(
+            "POST", resource_path(kind, ns), obj,
+            query={"fieldValidation": self.field_validation}))
 
     def update(self, obj: dict, subresource: str | None = None) -> dict:
         kind, md = obj["kind"], obj["metadata"]
         obj = self._with_type(kind, copy.deepcopy(obj))
         return self._with_type(kind, self._request(
-            "PUT", resource_path(kind, md.get("namespace"), md["name"], subresource), obj))
+            "PUT", resource_path(kind, md.get("namespace"), md["name"], subresource), obj,
+            query={"fieldValidation": self.field_validation}))
 
     def update_status(self, obj: dict) -> dict:
         return self.update(obj, subresource="status")
@@ -343,7 +348,7 @@ class KubeClient:
                  "json": "application/json-patch+json",
                  "strategic": "application/strategic-merge-patch+json",
                  "apply": "application/apply-patch+yaml"}[patch_type]
-        query = {"fieldManager": self.field_manager}
+        query = {"fieldManager": self.field_manager, "fieldValidation": self.field_validation}
         if patch_type == "apply" and force:
             query["force"] = "true"
         return self._with_type(kind, self._request(

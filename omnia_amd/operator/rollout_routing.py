@@ -86,10 +86,10 @@ def patch_route_weights(vs: dict, routes: list[str], stable: str, cand: str, wei
     return hit
 
 
-def patch_destination_rule(dr: dict, sticky: bool) -> None:
+def patch_destination_rule(dr: dict, sticky: bool, header: str = SESSION_HEADER) -> None:
     tp = dr.setdefault("spec", {}).setdefault("trafficPolicy", {})
     if sticky:
-        tp["loadBalancer"] = {"consistentHash": {"httpHeaderName": SESSION_HEADER}}
+        tp["loadBalancer"] = {"consistentHash": {"httpHeaderName": header}}
     else:
         tp.pop("loadBalancer", None)
 
@@ -134,9 +134,10 @@ def apply(store, ar: dict, weight: int, active: bool) -> dict:
             status["message"] = f"VirtualService {vref.get('name')!r} not found"
         dr = store.try_get("DestinationRule", dref.get("name", ""), ns)
         if dr is not None:
-            sticky = bool(((spec.get("rollout") or {}).get("stickySessions") or {})
-                          .get("enabled", True)) and active
-            patch_destination_rule(dr, sticky)
+            # spec.rollout.stickySession.hashOn (rollout_types.go:150): the header a
+            # session's requests hash on, so one conversation stays on one track
+            ss = (spec.get("rollout") or {}).get("stickySession") or {}
+            patch_destination_rule(dr, active, ss.get("hashOn") or SESSION_HEADER)
             store.apply(dr)
     else:
         total = int((spec.get("runtime") or {}).get("replicas", 1) or 1)

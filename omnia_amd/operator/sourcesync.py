@@ -149,11 +149,16 @@ class SourceSyncer:
         cm = store.try_get("ConfigMap", spec["configMap"]["name"], ns)
         if cm is None:
             raise SyncError(f"ConfigMap {spec['configMap']['name']} not found")
-        data = {k: v.encode() if isinstance(v, str) else v for k, v in
-                (cm.get("data") or {}).items()}
-        key = spec["configMap"].get("key")
-        if key:
-            data = {key: data[key]} if key in data else {}
+        # every key becomes a file (Data wins over BinaryData); "__" in a key is a
+        # path separator, the dashboard deploy route's encoding of nested files
+        # (internal/sourcesync/configmap.go:124-199)
+        import base64
+
+        data = {k: base64.b64decode(v) for k, v in (cm.get("binaryData") or {}).items()}
+        data.update({k: v.encode() if isinstance(v, str) else v for k, v in
+                     (cm.get("data") or {}).items()})
+        data = {k.replace("__", "/"): v for k, v in sorted(data.items())
+                if ".." not in k.replace("__", "/").split("/")}
         return _hash_tree(data), data
 
     def _oci(self, spec: dict, secret: dict | None, timeout: float) -> tuple[str, dict]:

@@ -115,7 +115,9 @@ class Agent:
         for k_src, k in (("temperature", "temperature"), ("topP", "top_p"),
                          ("maxTokens", "max_tokens")):
             if dd.get(k_src) is not None:
-                d[k] = dd[k_src]
+                # Provider CRD carries temperature / topP as decimal strings
+                v = dd[k_src]
+                d[k] = int(v) if k == "max_tokens" else float(v)
         d.update(self.prompt.parameters or {})
         d.update(overrides or {})
         if guided and self.cfg.response_format in ("json", "json_schema"):

@@ -106,8 +106,10 @@ def test_arena_job_fleet_mode_end_to_end():
                           "spec": {"sourceRef": {"name": "src"}, "type": "loadtest",
                                    "trials": 3, "loadTest": {
                                        "concurrency": 4, "thresholds": [
-                                           {"metric": "latency_p50", "max": "5s"},
-                                           {"metric": "pass_rate", "min": "0.4"}]}}})
+                                           {"metric": "latency_p50", "operator": "<=",
+                                            "value": "5s"},
+                                           {"metric": "pass_rate", "operator": ">=",
+                                            "value": "0.4"}]}}})
             ctl = ArenaJobController(store, MemoryQueue())
             await ctl.reconcile("default", "load1")
             await ctl.tasks["load1"]
@@ -197,9 +199,10 @@ def _job_store(arena, spec):
     return store
 
 
-def test_arena_datagen_job(tmp_path):
+def test_arena_datagen_job(tmp_path, monkeypatch):
     import json
 
+    monkeypatch.setenv("OMNIA_PVC_ROOT", str(tmp_path))
     arena = {"scenarios": [{"id": "faq", "prompt": "Write a question about {{topic}}.",
                             "variables": {"topic": ["GPUs", "HBM", "xGMI"]}}],
              "providers": [{"id": "gen", "mode": "direct"}]}
@@ -207,7 +210,8 @@ def test_arena_datagen_job(tmp_path):
 
     async def go():
         store = _job_store(arena, {"type": "datagen", "dataGen": {"count": 6, "format": "jsonl"},
-                                   "output": {"path": str(tmp_path)}})
+                                   "output": {"type": "pvc", "pvc": {
+                                       "claimName": "arena-out", "subPath": "gen"}}})
         ctl = ArenaJobController(store, MemoryQueue(), provider_objects={"gen": gen})
         await ctl.reconcile("default", "j")
         await ctl.tasks["j"]
@@ -215,6 +219,7 @@ def test_arena_datagen_job(tmp_path):
 
     st = asyncio.run(go())
     assert st["phase"] == "Succeeded" and st["dataset"]["records"] == 6
+    assert st["dataset"]["path"] == str(tmp_path / "arena-out" / "gen" / "j.jsonl")
     lines = [json.loads(x) for x in open(st["dataset"]["path"])]
     assert len(lines) == 6
     assert all(r["output"] == "Q: " + r["input"] for r in lines)
@@ -254,3 +259,43 @@ def test_arena_selfplay_persona():
     assert len(r["transcript"]) == 3  # opener + 2 persona turns, then [DONE]
     assert {c["source"] for c in r["provider_calls"]} == {"agent", "selfplay"}
     assert r["passed"]
+
+
+def test_arena_output_to_s3_compatible_endpoint():
+    """spec.output.type s3 with a custom endpoint: a SigV4-presigned PUT lands the
+    dataset in the bucket (fake S3 endpoint, path-style)."""
+    import http.server
+    import threading
+    import urllib.parse
+
+    from omnia_amd.ee.arena.controller import write_dataset
+
+    got = {}
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_PUT(self):  # noqa: N802
+            n = int(self.headers.get("Content-Length", 0))
+            u = urllib.parse.urlsplit(self.path)
+            got["path"], got["query"] = u.path, urllib.parse.parse_qs(u.query)
+            got["body"] = self.rfile.read(n)
+            self.send_response(200)
+            self.end_headers()
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.HTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        out = write_dataset([{"id": 1, "input": "a", "output": "b"}], "jsonl",
+                            {"type": "s3", "s3": {"bucket": "arena", "prefix": "runs/x",
+                                                  "region": "eu-west-1",
+                                                  "endpoint": f"http://127.0.0.1:"
+                                                              f"{srv.server_address[1]}"}},
+                            "job1", {"access_key": "AKID", "secret_key": "s3cr3t"})
+    finally:
+        srv.shutdown()
+    assert out["url"] == "s3://arena/runs/x/job1.jsonl"
+    assert got["path"] == "/arena/runs/x/job1.jsonl"
+    assert got["query"]["X-Amz-Credential"][0].startswith("AKID/")
+    assert "X-Amz-Signature" in got["query"] and got["body"].startswith(b'{"id": 1')

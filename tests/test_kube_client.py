@@ -153,7 +153,7 @@ def test_crd_admission_and_status_subresource(srv):
         c.create({"apiVersion": crds.API_VERSION, "kind": "Provider",
                   "metadata": {"name": "bad", "namespace": "default"},
                   "spec": {"type": "claude", "role": "embedding"}})
-    assert any("does not support role" in e for e in ei.value.errors)
+    assert any("requires type in" in e for e in ei.value.errors)
     pv = c.create({"apiVersion": crds.API_VERSION, "kind": "Provider",
                    "metadata": {"name": "m", "namespace": "default"},
                    "spec": {"type": "mock"}})

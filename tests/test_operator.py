@@ -20,6 +20,11 @@ ECHO = os.path.join(ROOT, "examples", "echo-function", "manifests.yaml")
 AGENT = os.path.join(ROOT, "examples", "llama3-8b-agent", "manifests.yaml")
 
 
+# a managed service group needs its memory + session databases (workspace_types.go:634)
+DB = {"memory": {"database": {"secretRef": {"name": "memory-db"}}},
+      "session": {"database": {"secretRef": {"name": "session-db"}}}}
+
+
 def ar(name="a", **spec):
     base = {"facades": [{"type": "websocket"}], "promptPackRef": {"name": "p"}}
     base.update(spec)
@@ -42,11 +47,11 @@ def test_agentruntime_cel_rules():
     st = new_store()
     with pytest.raises(Invalid, match="inputSchema is required"):
         st.create(ar(mode="function", facades=[{"type": "rest"}]))
-    with pytest.raises(Invalid, match="only allowed when mode is function"):
+    with pytest.raises(Invalid, match="only valid when spec.mode is .function."):
         st.create(ar(inputSchema={"type": "object"}))
-    with pytest.raises(Invalid, match="at most once"):
+    with pytest.raises(Invalid, match="must not contain duplicate facade types"):
         st.create(ar(facades=[{"type": "websocket"}, {"type": "websocket"}]))
-    with pytest.raises(Invalid, match="function mode requires exactly one rest"):
+    with pytest.raises(Invalid, match="requires exactly one .rest. facade"):
         st.create(ar(mode="function", facades=[{"type": "mcp"}], inputSchema={},
                      outputSchema={}))
     with pytest.raises(Invalid, match="does not compile"):
@@ -60,9 +65,9 @@ def test_provider_role_type_matrix():
     st = new_store()
     bad = {"apiVersion": crds.API_VERSION, "kind": "Provider",
            "metadata": {"name": "x"}, "spec": {"type": "claude", "role": "embedding"}}
-    with pytest.raises(Invalid, match="does not support role"):
+    with pytest.raises(Invalid, match="role 'embedding' requires type in"):
         st.create(bad)
-    with pytest.raises(Invalid, match="baseURL is required"):
+    with pytest.raises(Invalid, match="spec.model is required"):
         st.create({**bad, "spec": {"type": "vllm"}})
     with pytest.raises(Invalid, match="engine.model"):
         st.create({**bad, "spec": {"type": "local"}})
@@ -234,7 +239,7 @@ def test_workspace_reconcile():
     ws = {"apiVersion": crds.API_VERSION, "kind": "Workspace", "metadata": {"name": "team-a"},
           "spec": {"displayName": "Team A", "namespace": {"name": "team-a"},
                    "networkPolicy": {"isolate": True}, "storage": {"enabled": True},
-                   "services": [{"name": "default"}, {"name": "gold"}]}}
+                   "services": [{"name": "default", **DB}, {"name": "gold", **DB}]}}
 
     async def go():
         store, mgr, _ = await _run_operator([ws])
@@ -260,7 +265,8 @@ def test_canary_rollout_steps_and_promotion():
     docs = load_manifests([ECHO])
     for d in docs:
         if d["kind"] == "AgentRuntime":
-            d["spec"]["rollout"] = {"candidate": {"promptPackVersion": "1.0.0"},
+            d["spec"]["rollout"] = {"candidate": {"promptPackRef": {"name": "echo-pack",
+                                                                    "version": "1.0.0"}},
                                     "steps": [{"setWeight": 20}, {"pause": {"duration": "1s"}},
                                               {"setWeight": 100}]}
 
@@ -306,7 +312,8 @@ def test_rollout_traffic_routing_modes(monkeypatch):
         docs = load_manifests([ECHO])
         for d in docs:
             if d["kind"] == "AgentRuntime":
-                d["spec"]["rollout"] = {"candidate": {"promptPackVersion": "1.0.0"},
+                d["spec"]["rollout"] = {"candidate": {"promptPackRef": {"name": "echo-pack",
+                                                                    "version": "1.0.0"}},
                                         "steps": [{"setWeight": 30}, {"pause": {"duration": "1h"}}],
                                         "trafficRouting": routing}
                 d["spec"].setdefault("runtime", {})["replicas"] = 4
@@ -402,13 +409,13 @@ def test_process_mode_workspace_services_record_sessions():
 
     ws = {"apiVersion": crds.API_VERSION, "kind": "Workspace", "metadata": {"name": "team-b"},
           "spec": {"displayName": "Team B", "namespace": {"name": "team-b"},
-                   "services": [{"name": "default"}]}}
+                   "services": [{"name": "default", **DB}]}}
     docs = [ws] + load_manifests([ECHO])
     for d in docs[1:]:
         d["metadata"]["namespace"] = "team-b"
         if d["kind"] == "AgentRuntime":
             d["spec"] = {"facades": [{"type": "websocket"}], "promptPackRef": {"name": "echo-pack"},
-                         "providers": [{"providerRef": {"name": "echo-mock"}}]}
+                         "providers": [{"name": "llm", "providerRef": {"name": "echo-mock"}}]}
 
     async def go():
         store = new_store()

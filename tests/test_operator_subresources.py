@@ -82,7 +82,7 @@ def test_facade_rbac_objects_and_effective_sa():
     # podOverrides SA wins and the binding follows it; client keys widen secrets
     def mut(d):
         d["spec"]["podOverrides"] = {"serviceAccountName": "wi-sa"}
-        d["spec"]["externalAuth"] = {"clientKeys": {"secretSelector": {}}}
+        d["spec"]["externalAuth"] = {"clientKeys": {"defaultRole": "viewer"}}
 
     store, r = setup_store(mut)
     reconcile(store, r)
@@ -193,7 +193,9 @@ def test_eval_worker_per_service_group_and_cleanup():
     store.apply({"apiVersion": crds.API_VERSION, "kind": "Workspace", "metadata": {"name": "w"},
                  "spec": {"displayName": "W", "namespace": {"name": "default"},
                           "services": [{"name": "default",
-                                        "session": {"redis": {"url": "redis://grp:6379"}}}]}})
+                                        "memory": {"database": {"secretRef": {"name": "m"}}},
+                                        "session": {"database": {"secretRef": {"name": "s"}},
+                                                    "redis": {"url": "redis://grp:6379"}}}]}})
     reconcile(store, r)
     dep = store.get("Deployment", "arena-eval-worker-default")
     env = {e["name"]: e["value"] for e in dep["spec"]["template"]["spec"]["containers"][0]["env"]}
@@ -218,7 +220,10 @@ def test_inline_evaluating_framework_needs_no_worker_unless_group_opts_in():
         "InlineEvals"
     store.apply({"apiVersion": crds.API_VERSION, "kind": "Workspace", "metadata": {"name": "w"},
                  "spec": {"displayName": "W", "namespace": {"name": "default"},
-                          "services": [{"name": "default", "evalWorker": {
+                          "services": [{"name": "default", "mode": "external",
+                                        "external": {"sessionURL": "http://s:8080",
+                                                     "memoryURL": "http://m:8080"},
+                                        "evalWorker": {
                               "enabled": True, "podOverrides": {"serviceAccountName": "wi"}}}]}})
     reconcile(store, r)
     dep = store.get("Deployment", "arena-eval-worker-default")
@@ -317,7 +322,7 @@ def test_toolregistry_validation_probe_and_phases():
     assert st["phase"] == "Degraded" and st["discoveredToolsCount"] == 4
     # an invalid retry policy fails validation
     tr = store.get("ToolRegistry", "reg")
-    tr["spec"]["handlers"][0]["httpConfig"]["retryPolicy"] = {"initialBackoff": "5s",
+    tr["spec"]["handlers"][0]["httpConfig"]["retryPolicy"] = {"maxAttempts": 3, "initialBackoff": "5s",
                                                              "maxBackoff": "1s"}
     store.update(tr)
     rr.reconcile(store, "default", "reg")
@@ -350,7 +355,7 @@ def test_provider_endpoint_health():
                  "stringData": {"api-key": "x"}})
     store.apply({"apiVersion": crds.API_VERSION, "kind": "Provider",
                  "metadata": {"name": "o", "namespace": "default"},
-                 "spec": {"type": "ollama", "baseURL": "http://o:11434"}})
+                 "spec": {"type": "ollama", "model": "llama3", "baseURL": "http://o:11434"}})
     seen = []
 
     def unauthorized(url, timeout):

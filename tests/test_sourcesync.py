@@ -37,7 +37,7 @@ def test_git_skillsource_reconcile_and_revisions(tmp_path, repo):
     store.create({"apiVersion": "omnia.altairalabs.ai/v1alpha1", "kind": "SkillSource",
                   "metadata": {"name": "sk", "namespace": "default"},
                   "spec": {"type": "git", "interval": "5m",
-                           "git": {"url": str(repo), "ref": {"branch": "main"},
+                           "git": {"url": "file://" + str(repo), "ref": {"branch": "main"},
                                    "path": "skills"}}})
     rec = SourceReconciler("SkillSource", str(tmp_path / "content"))
     assert rec.reconcile(store, "default", "sk") == 300
@@ -69,7 +69,7 @@ def test_configmap_and_bad_git(tmp_path):
     for name, spec in (("a", {"type": "configmap", "interval": "1m",
                               "configMap": {"name": "cfg"}}),
                        ("b", {"type": "git", "interval": "1m",
-                              "git": {"url": str(tmp_path / "missing")}})):
+                              "git": {"url": "file://" + str(tmp_path / "missing")}})):
         store.create({"apiVersion": "omnia.altairalabs.ai/v1alpha1", "kind": "ArenaSource",
                       "metadata": {"name": name, "namespace": "default"}, "spec": spec})
     rec = SourceReconciler("ArenaSource", str(tmp_path / "c"))
@@ -122,7 +122,7 @@ def test_git_path_traversal_rejected(tmp_path, repo):
     store.create({"apiVersion": "omnia.altairalabs.ai/v1alpha1", "kind": "SkillSource",
                   "metadata": {"name": "t", "namespace": "default"},
                   "spec": {"type": "git", "interval": "1m",
-                           "git": {"url": str(repo), "path": "../../.."}}})
+                           "git": {"url": "file://" + str(repo), "path": "../../.."}}})
     rec = SourceReconciler("SkillSource", str(tmp_path / "content"))
     rec.reconcile(store, "default", "t")
     st = store.get("SkillSource", "t", "default")["status"]

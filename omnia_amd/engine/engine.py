@@ -60,6 +60,10 @@ class EngineConfig:
     # in one forward) bound inter-token latency under arrivals; 0: separate steps
     mixed_budget: int = 0
     checkpoint: str | None = None  # HF safetensors dir (random init when None)
+    # MoE expert parallelism: "tp" = experts sharded over the TP group (EP inside
+    # TP); "a2a" = data-parallel attention replicas + token all-to-all to the
+    # experts' ranks, every rank stepping in lockstep (engine/ep.py)
+    ep_mode: str = "tp"
 
     @classmethod
     def from_env(cls, **kw) -> "EngineConfig":
@@ -76,6 +80,7 @@ class EngineConfig:
             "OMNIA_ENGINE_CHECKPOINT": ("checkpoint", str),
             "OMNIA_ENGINE_USE_GRAPHS": ("use_graphs", lambda v: v.lower() != "false"),
             "OMNIA_ENGINE_MIXED_BUDGET": ("mixed_budget", int),
+            "OMNIA_ENGINE_EP_MODE": ("ep_mode", str),
         }
         for k, (f, t) in m.items():
             if k in env:
@@ -109,10 +114,18 @@ class LLMEngine:
             weights = load_hf_checkpoint(cfg.checkpoint, self.model_cfg, st.tp_size, st.tp_rank,
                                          dev, dtype)
         self.model = build_model(self.model_cfg, device=dev, dtype=dtype, seed=cfg.seed,
-                                 weights=weights, decode_part_size=cfg.decode_part_size)
+                                 weights=weights, decode_part_size=cfg.decode_part_size,
+                                 ep_mode=cfg.ep_mode)
         self.load_s = time.perf_counter() - t0
         nb = cfg.num_blocks or self.kv_pool_blocks(cfg, self.model_cfg, self.model.tp, dev, dtype)
         runner_cls = ModelRunner
+        # DP-attention + EP: every forward is a collective of the EP group
+        self.ep_lockstep = cfg.ep_mode == "a2a" and st.world_size > 1
+        self._ep_active = 0
+        if self.ep_lockstep:
+            from .ep import EPModelRunner
+
+            runner_cls = EPModelRunner
         if st.tp_size > 1:
             from .tp import TPModelRunner, agree_num_blocks
 
@@ -170,6 +183,8 @@ class LLMEngine:
         st = pstate.get_state()
         if cfg.tp > 1 and st.tp_size != cfg.tp:
             st = pstate.init_distributed(tp_size=cfg.tp, device=dev.type)
+        elif cfg.ep_mode == "a2a" and st.world_size == 1 and pstate.env_world()[0] > 1:
+            st = pstate.init_distributed(tp_size=1, device=dev.type)
         return st
 
     @staticmethod
@@ -234,6 +249,10 @@ class LLMEngine:
             failpoints.hit("engine.prefill" if self.scheduler.waiting else "engine.decode_step")
             if failpoints.triggered("engine.hang"):
                 time.sleep(float(os.environ.get("OMNIA_FAILPOINT_HANG_S", "5")))
+        if self.ep_lockstep:
+            from .ep import run_ep_step
+
+            return run_ep_step(self)
         if self.cfg.pipeline and self.runner.use_graphs:
             return self._step_pipelined()
         return self._step_sync()
@@ -474,6 +493,13 @@ class LLMEngine:
 
     def run_until_done(self, max_steps: int = 10**9) -> None:
         n = 0
+        if self.ep_lockstep:  # step until the whole EP group is idle
+            while n < max_steps:
+                self.step()
+                n += 1
+                if not self._ep_active:
+                    return
+            return
         while self.has_work() and n < max_steps:
             self.step()
             n += 1
@@ -488,6 +514,8 @@ class LLMEngine:
             for s in seqs:
                 if s.is_finished:
                     finished.add(s.seq_id)
+        if self.ep_lockstep:
+            self.run_until_done()  # keep serving the group's all-to-alls until all idle
         return seqs
 
 
@@ -607,7 +635,7 @@ class AsyncLLMEngine:
                     fn()
                 except Exception as e:  # surface to the submitter
                     log.exception("engine request failed: %s", e)
-            if eng.has_work():
+            if eng.has_work() or eng.ep_lockstep:
                 self._step_t0 = time.monotonic()
                 try:
                     eng.step()
@@ -627,6 +655,9 @@ class AsyncLLMEngine:
                         self.healthy = False  # fault storm: stop advertising readiness
                 self._step_t0 = None
                 self._flush()
+                if eng.ep_lockstep and not eng._ep_active:
+                    self._wake.wait(0.001)  # group idle: keep the lockstep cadence cheap
+                    self._wake.clear()
             else:
                 self._flush()
                 self._wake.wait(0.05)

@@ -1,0 +1,150 @@
+"""Lockstep execution of DP-attention + EP replicas (``EngineConfig.ep_mode="a2a"``).
+
+Every rank is a full engine (its own scheduler, KV and batch) for attention,
+but each Mixtral MoE layer is a collective: tokens go to their experts' rank and
+back (:mod:`omnia_amd.parallel.expert`).  So every rank must execute the same
+sequence of forwards with the same all-to-all shapes, whatever its own load:
+
+1. each step every rank publishes ``[active, tokens, eager, rows, cols]`` and the
+   group all-reduces it (MAX) -- one small collective per step;
+2. nobody active -> everybody idles;
+3. anyone needs an eager forward (a prefill / mixed step, or a decode that
+   cannot replay a graph -- penalties, grammars) -> EVERY rank runs eagerly with
+   the all-to-all capacity set by the step-global token count: prefill ranks
+   prefill, decoding ranks decode eagerly, idle ranks run one padded row;
+4. otherwise every rank replays the decode graph of the agreed ``(rows, cols)``
+   bucket (idle ranks with all rows padded), so graph captures -- which run the
+   collectives too -- happen on all ranks together.
+
+The runner is used with synchronous engine steps (no one-deep pipelining: a
+step's collective shape depends on every rank's schedule).
+"""
+from __future__ import annotations
+
+import bisect
+
+import torch
+import torch.distributed as dist
+
+from ..parallel import state as pstate
+from .model_runner import ModelRunner
+
+
+class EPModelRunner(ModelRunner):
+    """ModelRunner whose every forward is agreed across the EP group."""
+
+    fused_launch = False
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        st = pstate.get_state()
+        self.group = st.dp_group
+        self.ep = st.dp_size
+        self.desc = torch.zeros(5, dtype=torch.int64, device=self.device)
+        self.ep_stats = {"steps": 0, "eager_steps": 0, "graph_steps": 0, "idle_fill": 0}
+
+    # ------------------------------------------------------------ agreement
+    def agree(self, active: int, tokens: int, eager: int, rows: int, cols: int) -> list[int]:
+        if self.ep == 1:
+            return [active, tokens, eager, rows, cols]
+        self.desc.copy_(torch.tensor([active, tokens, eager, rows, cols], dtype=torch.int64))
+        dist.all_reduce(self.desc, op=dist.ReduceOp.MAX, group=self.group)
+        return self.desc.tolist()
+
+    def bucket(self, n: int) -> int:
+        return self.buckets[bisect.bisect_left(self.buckets, max(1, n))]
+
+    def describe(self, plan) -> tuple[int, int, int, int, int]:
+        if plan.kind == "idle":
+            return 0, 0, 0, 0, 0
+        if plan.kind in ("prefill", "mixed"):
+            n = sum(k for _, k in plan.prefill) + len(plan.decode or [])
+            return 1, n, 1, 0, 0
+        seqs = plan.decode
+        eager = 0 if self.use_graphs and self.can_pipeline(seqs) else 1
+        cols = self._ctx_bucket(max(s.length for s in seqs))
+        return 1, len(seqs), eager, self.bucket(len(seqs)), cols
+
+    # ------------------------------------------------------------ forwards
+    def ep_eager_decode(self, seqs) -> list[int]:
+        n = len(seqs)
+        ncols = self._ctx_bucket(max(s.length for s in seqs))
+        self._decode_inputs(seqs, n, ncols, self.stage[0])
+        logits = self._eager_forward(n, ncols)
+        self._tap_rows(seqs, logits[:n])
+        return self._sample_eager(logits, seqs)
+
+    def ep_idle_forward(self):
+        """One padded row through the whole model: this rank still serves the
+        MoE all-to-alls of a step in which it has no tokens of its own."""
+        ncols = self._ctx_bucket(1)
+        self._decode_inputs([], 1, ncols, self.stage[0])
+        self._eager_forward(1, ncols)
+        self.ep_stats["idle_fill"] += 1
+
+    def ep_graph_decode(self, seqs, nrows: int, ncols: int) -> list[int]:
+        n = len(seqs)
+        self._decode_inputs(seqs, nrows, ncols, self.stage[0])
+        self._replay(nrows, ncols)
+        for i, s in enumerate(seqs):
+            s.slot = i
+        if n == 0:
+            self.ep_stats["idle_fill"] += 1
+            torch.cuda.current_stream().synchronize()
+            return []
+        return self.out_tok[:n].tolist()
+
+
+def run_ep_step(engine) -> int:
+    """One lockstep engine step (see module docstring).  Returns tokens produced."""
+    from . import engine as E
+
+    runner: EPModelRunner = engine.runner
+    model = runner.model
+    plan = engine.scheduler.schedule()
+    active, tokens, eager, rows, cols = runner.agree(*runner.describe(plan))
+    engine._ep_active = active
+    if not active:
+        return 0
+    runner.ep_stats["steps"] += 1
+    done = []
+    if eager:
+        runner.ep_stats["eager_steps"] += 1
+        model.ep_tokens = tokens  # a2a capacity = step-global max tokens x k
+        try:
+            if plan.kind == "idle":
+                runner.ep_idle_forward()
+            elif plan.kind == "prefill":
+                sampled = runner.run_prefill(plan.prefill)
+                done = engine.scheduler.on_prefill_done(plan.prefill, sampled)
+                engine.counters["prefill_tokens"] += sum(n for _, n in plan.prefill)
+                engine.counters["steps_prefill"] += 1
+            elif plan.kind == "mixed":
+                toks, sampled = runner.run_mixed(plan.decode, plan.prefill)
+                done = engine.scheduler.on_decode_done(plan.decode, toks)
+                done += engine.scheduler.on_prefill_done(plan.prefill, sampled)
+                engine.counters["prefill_tokens"] += sum(n for _, n in plan.prefill)
+                engine.counters["decode_tokens"] += len(toks)
+            else:
+                toks = runner.ep_eager_decode(plan.decode)
+                done = engine.scheduler.on_decode_done(plan.decode, toks)
+                engine.counters["decode_tokens"] += len(toks)
+                engine.counters["steps_decode"] += 1
+        finally:
+            model.ep_tokens = 0
+    else:
+        runner.ep_stats["graph_steps"] += 1
+        seqs = plan.decode if plan.kind == "decode" else []
+        toks = runner.ep_graph_decode(seqs, rows, cols)
+        if seqs:
+            done = engine.scheduler.on_decode_done(seqs, toks)
+            engine.counters["decode_tokens"] += len(toks)
+            engine.counters["steps_decode"] += 1
+    import time
+
+    now = time.perf_counter()
+    for s, tok in done:
+        engine._append(s, tok, now)
+    engine.step_count += 1
+    E.M.KV_UTIL.set(engine.blocks.utilization())
+    return len(done)

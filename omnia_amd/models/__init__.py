@@ -11,6 +11,7 @@ def build_model(cfg: ModelConfig, device="cpu", dtype=None, seed: int = 0, **kw)
     if cfg.arch == "llama":
         from .llama import LlamaModel
 
+        kw.pop("ep_mode", None)
         return LlamaModel(cfg, device=device, dtype=dtype, seed=seed, **kw)
     if cfg.arch == "mixtral":
         from .mixtral import MixtralModel

@@ -100,6 +100,7 @@ class LlamaModel:
             raise ValueError("vocab not divisible by tp")
         self.vocab_start = self.tpr * self.vocab_local
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.seed = seed
         self.decode_part_size = decode_part_size
         self.cos_sin = ref.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
                                         cfg.rope_scaling, device=self.device)
@@ -123,18 +124,18 @@ class LlamaModel:
         }
         w["lm_head"] = w["embed"] if cfg.tie_embeddings else _init((self.vocab_local, d), 0.02,
                                                                    dev, dt, g)
-        for _ in range(cfg.num_layers):
+        for li in range(cfg.num_layers):
             layer = {
                 "in_norm": torch.ones(d, dtype=dt, device=dev),
                 "post_norm": torch.ones(d, dtype=dt, device=dev),
                 "qkv": _init(((self.hq + 2 * self.hkv) * D, d), 0.02, dev, dt, g),
                 "o": _init((d, self.hq * D), 0.02 / math.sqrt(2 * cfg.num_layers), dev, dt, g),
             }
-            layer.update(self._random_mlp(g))
+            layer.update(self._random_mlp(g, li))
             w["layers"].append(layer)
         return w
 
-    def _random_mlp(self, g) -> dict:
+    def _random_mlp(self, g, li: int = 0) -> dict:
         cfg, dev, dt, d = self.cfg, self.device, self.dtype, self.cfg.hidden_size
         return {
             "gate_up": _init((2 * self.inter, d), 0.02, dev, dt, g),

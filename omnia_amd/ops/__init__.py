@@ -506,6 +506,39 @@ def cosine_topk(q: torch.Tensor, m: torch.Tensor, k: int, valid: torch.Tensor | 
 MOE_LIBRARY_ROWS = 1024  # mean rows/expert above which eager calls use hipBLASLt per expert
 
 
+def moe_rows(rows: torch.Tensor, eids: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor,
+             e_lo: int, n_experts: int) -> torch.Tensor:
+    """Expert FFN of each row under its own expert id (the receive side of an
+    expert-parallel all-to-all): ``y[r] = down_e(silu(gate_e x) * up_e x)`` with
+    ``e = eids[r]`` for local experts ``[e_lo, e_lo + w_gu.shape[0])``; rows whose
+    id is outside that range (padding, ``-1``) are left unwritten.  Static shapes
+    and no host sync (hipGraph-safe): the grouped MFMA kernels with top-1 routing."""
+    R, d = rows.shape
+    e_hi = e_lo + w_gu.shape[0]
+    if not rows.is_cuda:
+        y = rows.new_zeros(R, w_down.shape[1])
+        local = (eids.long() - e_lo)
+        ok = (local >= 0) & (local < w_gu.shape[0])
+        li = local.clamp(0, w_gu.shape[0] - 1)
+        h = torch.bmm(w_gu.index_select(0, li).float(), rows.float()[:, :, None])[:, :, 0]
+        a = ref.silu_mul(h)
+        o = torch.bmm(w_down.index_select(0, li).float(), a[:, :, None])[:, :, 0]
+        return torch.where(ok[:, None], o.to(rows.dtype), y)
+    kk = kernels()
+    ids = eids.to(torch.int32).view(R, 1).contiguous()
+    mb = kk.moe_max_blocks(R, e_hi - e_lo)
+    sorted_ids = torch.empty(mb * 64, dtype=torch.int32, device=rows.device)
+    blk = torch.empty(mb, dtype=torch.int32, device=rows.device)
+    nblk = torch.empty(1, dtype=torch.int32, device=rows.device)
+    kk.moe_align(sorted_ids, blk, nblk, ids, n_experts, e_lo, e_hi)
+    act = torch.empty(mb * 64, w_down.shape[2], dtype=rows.dtype, device=rows.device)
+    kk.moe_gemm(0, act, rows, w_gu, sorted_ids, blk, nblk, None, 1, R, e_lo)
+    y = torch.empty(R, w_down.shape[1], dtype=rows.dtype, device=rows.device)
+    ones = torch.ones(R, dtype=torch.float32, device=rows.device)
+    kk.moe_gemm(1, y, act, w_down, sorted_ids, blk, nblk, ones, 1, R, e_lo)
+    return y
+
+
 def moe(x: torch.Tensor, router: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor,
         k: int, n_experts: int, e_lo: int = 0, renorm: bool = True,
         graph_safe: bool = True) -> torch.Tensor:

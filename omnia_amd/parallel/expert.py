@@ -1,23 +1,40 @@
-"""Expert parallelism with token all-to-all (SURVEY §2.3 EP row, K15).
+"""Expert parallelism with token all-to-all (SURVEY §2.3 EP row, K15; BASELINE
+config 5 "expert all-to-all over xGMI").
 
-Two EP layouts exist in the engine:
+Two EP layouts exist in the engine (``EngineConfig.ep_mode``):
 
-* **EP inside TP** (the default, :mod:`omnia_amd.models.mixtral`): attention is
-  tensor-parallel, so every rank already holds every token; each rank runs only
-  its experts and the all-reduce that dense TP needs anyway combines them.  No
-  extra collective.
-* **DP-attention + EP** (this module): ranks hold DIFFERENT tokens (data-parallel
-  attention, e.g. one replica per GPU), and the expert FFN is sharded E/ep per
-  rank.  Tokens travel to their experts' rank and back: dispatch all-to-all ->
-  local grouped expert FFN -> combine all-to-all -> weighted sum.  On an 8-GPU
-  MI355X node every rank talks to every peer over its own xGMI link, so the
-  all-to-all is one hop per pair (RCCL ``alltoall`` over the full mesh).
+* ``"tp"`` -- **EP inside TP** (:mod:`omnia_amd.models.mixtral`, the default):
+  attention is tensor-parallel, so every rank already holds every token; each
+  rank runs only its experts and the all-reduce that dense TP needs anyway
+  combines them.  No extra collective.
+* ``"a2a"`` -- **DP attention + EP** (this module): every rank is its own
+  data-parallel replica for attention (its own batch, KV, scheduler) and the
+  expert FFN is sharded E/ep per rank.  Each MoE layer sends every (token, slot)
+  assignment to the rank owning its expert, runs the local grouped expert GEMMs
+  on what arrives, and sends the results back to be weighted and summed.
 
-Wire format per direction: one ``all_to_all_single`` of the counts, then one of
-the rows ([n, d] activations) with the (expert, slot) metadata riding in a
-second small all-to-all.  Summation order of the combine is fixed (slot order
-per token), so the result is identical to the single-rank oracle up to the
-GEMM's own rounding.
+The all-to-all is **fixed-capacity and sync-free**, so the whole MoE layer is
+static-shaped and hipGraph-capturable:
+
+* send buffer ``[ep, C, d]``: assignment ``(t, j)`` for rank ``r`` lands at slot
+  ``r*C + pos`` where ``pos`` is its rank among rank-``r`` assignments -- a
+  device-side one-hot cumsum, no ``.tolist()``, no host round trip;
+* an expert-id slab ``[ep, C]`` (padding = -1) rides in a second all-to-all;
+* ``dist.all_to_all_single`` with equal splits (RCCL over xGMI: each rank talks
+  to each peer over its own link, one hop per pair);
+* the receive side runs :func:`omnia_amd.ops.moe_rows` -- the grouped MFMA
+  expert kernels with top-1 routing over the received rows; padding rows are
+  skipped by ``moe_align`` (no per-expert Python loop);
+* the combine all-to-all returns results to the same slots; the source gathers
+  its ``r*C + pos`` rows and sums them in fixed slot order, so outputs match the
+  single-rank oracle up to GEMM rounding.
+
+Capacity ``C`` must be the same on every rank of a step (it is a collective's
+shape); the engine passes the step-global token count (``ForwardBatch.ep_tokens``)
+so ``C = T_global * k`` is lossless.  The price of static shapes is padding
+bandwidth: each rank moves ``ep * C * d`` bytes per direction, of which only
+``T*k*d`` are real -- measured and documented against EP-inside-TP in
+``docs/PARALLELISM.md``.
 """
 from __future__ import annotations
 
@@ -28,19 +45,16 @@ import torch.nn.functional as F
 from ..ops import reference as ref
 
 
-def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group):
-    dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
-                           input_split_sizes=in_splits, group=group)
-    return out
-
-
-def expert_ffn(x: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor) -> torch.Tensor:
-    """SwiGLU FFN of one expert: down(silu(gate x) * up x); w_gu [2I, d], w_down [d, I]."""
-    from .. import ops
-
-    if x.shape[0] == 0:
-        return x.new_zeros(0, w_down.shape[0])
-    return ops.linear(ops.linear_silu(x, w_gu), w_down)
+def dispatch_slots(ids: torch.Tensor, e_local: int, ep: int, cap: int) -> torch.Tensor:
+    """Send-buffer slot ``rank * cap + pos`` of every (token, slot) assignment,
+    ``pos`` = its order among the assignments for ``rank`` (stable)."""
+    flat = ids.reshape(-1).long()
+    dest = torch.div(flat, e_local, rounding_mode="floor")
+    # one-hot by comparison (F.one_hot validates its input with a host sync,
+    # which a captured decode graph cannot contain)
+    onehot = (dest[:, None] == torch.arange(ep, device=dest.device)[None, :]).to(torch.int32)
+    pos = onehot.cumsum(0).gather(1, dest[:, None])[:, 0].long() - 1
+    return dest * cap + pos
 
 
 class ExpertParallelMoE:
@@ -61,46 +75,48 @@ class ExpertParallelMoE:
         if self.e_local * self.ep != self.n_experts:
             raise ValueError("experts must split evenly over the EP group")
         self.renorm = renorm
-        self.stats = {"sent_rows": 0, "recv_rows": 0}
+        self.stats = {"calls": 0, "rows_sent": 0, "bytes_sent": 0}
 
     def route(self, x: torch.Tensor):
+        if x.is_cuda:
+            from .. import ops
+
+            T = x.shape[0]
+            ids = torch.empty(T, self.k, dtype=torch.int32, device=x.device)
+            wts = torch.empty(T, self.k, dtype=torch.float32, device=x.device)
+            ops.kernels().moe_topk(ids, wts, F.linear(x, self.router), self.k, self.renorm)
+            return ids, wts
         return ref.moe_route(F.linear(x.float(), self.router.float()), self.k, self.renorm)
 
-    def __call__(self, x: torch.Tensor, ids=None, wts=None) -> torch.Tensor:
+    def _a2a(self, t: torch.Tensor) -> torch.Tensor:
+        if self.ep == 1:
+            return t
+        out = torch.empty_like(t)
+        dist.all_to_all_single(out, t, group=self.group)
+        return out
+
+    def __call__(self, x: torch.Tensor, ids=None, wts=None, tokens: int = 0) -> torch.Tensor:
+        """``tokens``: the step-global max token count across the EP group (sets
+        the capacity; defaults to this rank's own T, correct for a lone call)."""
+        from .. import ops
+
         T, d = x.shape
+        k = self.k
         if ids is None:
             ids, wts = self.route(x)
-        flat_e = ids.reshape(-1).long()                       # [T*k]
-        dest = flat_e // self.e_local                         # owning rank per assignment
-        order = torch.argsort(dest, stable=True)               # grouped by rank, stable
-        send_counts = torch.bincount(dest, minlength=self.ep)
-        rows = x.index_select(0, order // self.k)             # token row per assignment
-        meta = flat_e.index_select(0, order).to(torch.int64)  # expert id per row
-        if self.ep > 1:
-            recv_counts = torch.empty_like(send_counts)
-            dist.all_to_all_single(recv_counts, send_counts, group=self.group)
-            ins, outs = send_counts.tolist(), recv_counts.tolist()
-            r_rows = _a2a(rows.new_empty(sum(outs), d), rows.contiguous(), outs, ins, self.group)
-            r_meta = _a2a(meta.new_empty(sum(outs)), meta, outs, ins, self.group)
-        else:
-            ins = outs = [int(send_counts.sum())]
-            r_rows, r_meta = rows, meta
-        self.stats["sent_rows"] += int(sum(ins))
-        self.stats["recv_rows"] += int(sum(outs))
-        # local grouped expert FFN (rows of one expert are processed together)
-        y = r_rows.new_empty(r_rows.shape[0], d)
-        local = r_meta - self.rank * self.e_local
-        for e in range(self.e_local):
-            idx = (local == e).nonzero(as_tuple=True)[0]
-            if idx.numel():
-                y.index_copy_(0, idx, expert_ffn(r_rows.index_select(0, idx), self.w_gu[e],
-                                                 self.w_down[e]).to(y.dtype))
-        # combine: send results back along the reverse splits
-        back = _a2a(y.new_empty(rows.shape[0], d), y, ins, outs, self.group) \
-            if self.ep > 1 else y
-        per_assign = torch.empty_like(back)
-        per_assign.index_copy_(0, order, back)                 # back to (token, slot) order
-        w = wts.reshape(-1).to(torch.float32)
-        contrib = per_assign.float() * w[:, None]
-        out = contrib.view(T, self.k, d).sum(dim=1)            # fixed slot order
+        cap = max(1, max(tokens, T) * k)
+        slot = dispatch_slots(ids, self.e_local, self.ep, cap)         # [T*k]
+        send = x.new_zeros(self.ep * cap, d)
+        send.index_copy_(0, slot, x.repeat_interleave(k, dim=0))
+        meta = torch.full((self.ep * cap,), -1, dtype=torch.int32, device=x.device)
+        meta.index_copy_(0, slot, ids.reshape(-1).to(torch.int32))
+        recv, rmeta = self._a2a(send), self._a2a(meta)
+        y = ops.moe_rows(recv, rmeta, self.w_gu, self.w_down, self.rank * self.e_local,
+                         self.n_experts)
+        back = self._a2a(y)
+        got = back.index_select(0, slot).float().view(T, k, d)
+        out = (got * wts.to(torch.float32).view(T, k, 1)).sum(dim=1)  # fixed slot order
+        self.stats["calls"] += 1
+        self.stats["rows_sent"] += self.ep * cap
+        self.stats["bytes_sent"] += self.ep * cap * d * x.element_size()
         return out.to(x.dtype)

@@ -19,10 +19,10 @@ from omnia_amd.models.config import resolve
 from omnia_amd.ops import reference as ref
 
 
-def _engine(device, mc, chunk):
+def _engine(device, mc, chunk, **kw):
     eng = LLMEngine(EngineConfig(model=mc.name, device=device, num_blocks=512, block_size=16,
                                  max_batch=8, max_model_len=1024, max_prefill_tokens=chunk,
-                                 pipeline=False, seed=3), model_cfg=mc)
+                                 pipeline=False, seed=3, **kw), model_cfg=mc)
     eng.runner.enable_logit_tap()
     return eng
 
@@ -65,10 +65,10 @@ def _check(mc, w, seqs, tap, rel_tol, min_pass=1.0):
     return ok / total, worst
 
 
-def _gate(device, mc, chunk, rel_tol, min_pass=1.0, router_scale=None):
+def _gate(device, mc, chunk, rel_tol, min_pass=1.0, router_scale=None, **kw):
     rng = random.Random(7)
     torch.manual_seed(0)
-    eng = _engine(device, mc, chunk)
+    eng = _engine(device, mc, chunk, **kw)
     w = eng.model.w
     if router_scale is not None:  # sharpen routing so bf16 vs fp32 top-k cannot tie
         for layer in w["layers"]:
@@ -113,6 +113,22 @@ def test_gpu_tiny_mixtral_matches_dense_oracle():
     frac, worst = _gate("cuda", resolve("tiny-mixtral"), chunk=64, rel_tol=0.04,
                         min_pass=0.97, router_scale=30.0)
     print(f"tiny-mixtral: {frac:.3f} rows within tol, worst rel err {worst:.4f}")
+
+
+def test_cpu_mixtral_a2a_expert_parallel_path_matches_dense_oracle():
+    """ep_mode a2a (DP attention + EP) on one rank: the dispatch -> row-routed
+    expert FFN -> combine path of every MoE layer against the dense oracle."""
+    _gate("cpu", resolve("tiny-mixtral"), chunk=64, rel_tol=0.04, min_pass=0.97,
+          router_scale=30.0, ep_mode="a2a")
+
+
+@pytest.mark.gpu
+def test_gpu_tiny_mixtral_a2a_expert_parallel_path_matches_dense_oracle():
+    """Same on the GPU: the static-capacity dispatch / combine and the row-routed
+    grouped MFMA expert kernels (ops.moe_rows) inside captured decode graphs."""
+    frac, worst = _gate("cuda", resolve("tiny-mixtral"), chunk=64, rel_tol=0.04,
+                        min_pass=0.97, router_scale=30.0, ep_mode="a2a")
+    print(f"tiny-mixtral a2a EP: {frac:.3f} rows within tol, worst rel err {worst:.4f}")
 
 
 @pytest.mark.gpu

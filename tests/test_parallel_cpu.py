@@ -114,7 +114,8 @@ def _ep_worker(rank, world, port, q):
         moe = ExpertParallelMoE(router, w_gu[rank * el:(rank + 1) * el],
                                 w_down[rank * el:(rank + 1) * el], k)
         ids, wts = moe.route(x)
-        got = moe(x, ids, wts)
+        # capacity is a collective shape: every rank passes the step-global max T
+        got = moe(x, ids, wts, tokens=max(len(t) for t in xs))
         want = ref.moe(x, router, w_gu, w_down, k, ids=ids, wts=wts)
         q.put(("ok", rank, float((got - want).abs().max()), moe.stats))
         dist.barrier()
@@ -125,11 +126,12 @@ def _ep_worker(rank, world, port, q):
         q.put(("err", rank, traceback.format_exc(), None))
 
 
-def test_expert_parallel_all_to_all_gloo():
+@pytest.mark.parametrize("world", [2, 4])
+def test_expert_parallel_all_to_all_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ep_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_ep_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
@@ -138,7 +140,7 @@ def test_expert_parallel_all_to_all_gloo():
     for status, rank, val, stats in res:
         assert status == "ok", val
         assert val < 1e-4, (rank, val)
-        assert stats["sent_rows"] > 0 and stats["recv_rows"] > 0
+        assert stats["calls"] == 1 and stats["rows_sent"] == world * (13 + 7 * (world - 1)) * 2
 
 
 def test_replicated_engine_health_rehomes_sessions():

@@ -73,8 +73,9 @@ def _text_of(message: dict) -> str:
 
 class A2AServer:
     def __init__(self, runtime_client, name: str, description: str = "", base_url: str = "",
-                 task_store=None, metadata: dict | None = None):
+                 task_store=None, metadata: dict | None = None, skills: list | None = None):
         self.client = runtime_client
+        self.skills = skills
         self.name = name
         self.description = description or f"Omnia agent {name}"
         self.base_url = base_url
@@ -84,7 +85,7 @@ class A2AServer:
 
     async def card(self, request):
         url = self.base_url or f"http://{request.host}/a2a"
-        return web.json_response(agent_card(self.name, self.description, url))
+        return web.json_response(agent_card(self.name, self.description, url, self.skills))
 
     async def _run(self, message: dict, emit=None) -> dict:
         tid = message.get("taskId") or str(uuid.uuid4())
@@ -200,7 +201,25 @@ class A2AServer:
         return err(-32601, f"method {method} not found")
 
 
+def pack_card_skills(path: str | None) -> list | None:
+    """Card skills of a multi-agent PromptPack (one per ``agents.members``
+    entry); None for plain packs or an unreadable pack."""
+    if not path:
+        return None
+    from ..runtime.promptpack import PackError, PromptPack
+    from ..runtime.workflow import card_skills
+
+    try:
+        pack = PromptPack.load(path)
+    except (OSError, PackError):
+        return None
+    return card_skills(pack) or None
+
+
 def mount_a2a(facade, runtime_client, path: str = "/a2a", **kw) -> A2AServer:
+    import os
+
+    kw.setdefault("skills", pack_card_skills(os.environ.get("OMNIA_PROMPTPACK_PATH")))
     srv = A2AServer(runtime_client, facade.cfg.agent, **kw)
     facade.app.router.add_get("/.well-known/agent.json", srv.card)
     facade.app.router.add_get("/.well-known/agent-card.json", srv.card)

@@ -10,6 +10,9 @@ Reference behaviour (``internal/runtime/message.go:40-431``, PromptKit pipeline)
   * ``tool_policy.max_rounds`` (default 5) and ``max_tool_calls_per_turn``
     (default 10) bound the loop; ``tool_choice: none`` hides tools;
   * the turn ends with Done{final_content, usage{input, output, cost}}.
+  * workflow / multi-agent packs (:mod:`.workflow`): the active prompt follows
+    the conversation's workflow state; transitions and member-agent calls are
+    runtime-internal server-side tools.
   * context window: ``ProviderDefaults.contextWindow`` + ``truncationStrategy``
     (sliding = drop oldest, summarize = fold oldest turns into a summary,
     custom = warn and fall back to sliding) (``agentruntime_types.go:417-476``).
@@ -33,8 +36,10 @@ from ..tools.executor import CallContext, OmniaExecutor
 from ..observability import logging as logctx
 from .chat import Message, ToolCallReq
 from .context_store import StoreUnavailable
-from .promptpack import PromptPack, run_validators
+from .promptpack import Prompt, PromptPack, run_validators
 from .providers import Provider, ProviderError, ProviderEvent, Usage
+from .workflow import (AGENT_TOOL_PREFIX, ARTIFACT_TOOL, TRANSITION_TOOL, Workflow, WorkflowError,
+                       member_tool_specs, scope_skill_specs, scoped_skill_names)
 
 log = logging.getLogger("omnia.runtime.agent")
 
@@ -49,6 +54,9 @@ class TurnResult:
     violations: list = field(default_factory=list)
     ttft: float | None = None
     finish_reason: str = ""
+    workflow: dict | None = None  # the conversation's workflow snapshot after the turn
+    transitions: list = field(default_factory=list)
+    composition: list | None = None  # step trace when a composition state ran
 
 
 @dataclass
@@ -61,6 +69,16 @@ class AgentConfig:
     response_format: str = ""  # "" | text | json | json_schema (function mode)
     response_schema: dict | None = None
     max_rounds: int | None = None
+
+
+class _CollectIO:
+    """TurnIO of a member-agent sub-turn: text is collected, client tools refused."""
+
+    async def chunk(self, text: str) -> None:
+        pass
+
+    async def client_tool_calls(self, calls, meta):
+        raise RuntimeError("client tools are not available to member agents")
 
 
 class TurnIO:
@@ -81,7 +99,8 @@ def _approx_tokens(text: str) -> int:
 class Agent:
     def __init__(self, pack: PromptPack, provider: Provider, store, executor: OmniaExecutor | None,
                  cfg: AgentConfig | None = None, extra_providers: dict | None = None,
-                 memory=None, event_sink=None, evaluator=None, tokenizer=None):
+                 memory=None, event_sink=None, evaluator=None, tokenizer=None,
+                 graph: bool = True):
         self.pack = pack
         self.provider = provider
         self.store = store
@@ -92,21 +111,120 @@ class Agent:
         self.event_sink = event_sink  # async record(kind, session_id, payload)
         self.evaluator = evaluator
         self.tokenizer = tokenizer
-        self.prompt = pack.prompt(self.cfg.prompt_name)
+        # workflow / multi-agent packs open at their declared entry
+        # (pack_entry.go:54-86); ``graph=False`` is a member agent's view
+        self.workflow = Workflow(pack.workflow) if graph and pack.workflow else None
+        self.multi_agent = bool(graph and pack.agents)
+        if graph and (pack.workflow or pack.agents):
+            self.prompt = pack.prompts[pack.entry()]
+        else:
+            self.prompt = pack.prompt(self.cfg.prompt_name)
+        self._members: dict[str, Agent] = {}
 
     # ------------------------------------------------------------ state
-    def _system_message(self, variables: dict | None) -> Message:
+    def _skills(self):
+        h = self.executor.handlers.get("skills") if self.executor is not None else None
+        return h if getattr(h, "type", "") == "skills" else None
+
+    def _system_message(self, variables: dict | None, prompt: Prompt | None = None) -> Message:
+        from .skills import preloaded_instructions
+
         vs = {**self.cfg.variables, **(variables or {})}
-        return Message("system", self.pack.render_system(self.prompt, vs))
+        return Message("system", self.pack.render_system(prompt or self.prompt, vs)
+                       + preloaded_instructions(self._skills()))
+
+    def _active_prompt(self, snap: dict | None) -> Prompt:
+        if self.workflow is not None and snap is not None:
+            key = self.workflow.prompt_key(snap)  # None in a composition state
+            return self.pack.prompts[key] if key else self.prompt
+        return self.prompt
+
+    def _tools(self, prompt: Prompt, snap: dict | None) -> list[dict]:
+        if prompt.tool_policy.tool_choice == "none":
+            return []
+        if snap is not None and snap.get("exhausted") == "max_tool_calls":
+            return []  # the workflow's tool-call budget is spent
+        tools = []
+        if self.executor is not None:
+            tools = self.pack.tool_specs(prompt, self.executor.specs())
+            if self.workflow is not None and snap is not None:
+                sk = self._skills()
+                tools = scope_skill_specs(tools, self.workflow.skill_scope(snap),
+                                          sk.skills if sk else {})
+        if self.workflow is not None and snap is not None:
+            if self.workflow.model_can_fire(snap):
+                tools.append(self.workflow.tool_spec(snap))
+            art = self.workflow.artifact_spec(snap)
+            if art is not None:
+                tools.append(art)
+        if self.multi_agent and self.pack.key_of(prompt) == self.pack.agents["entry"]:
+            tools += member_tool_specs(self.pack)
+        return tools
+
+    async def _enter_state(self, session_id: str, snap: dict, rec: dict, msgs: list[Message],
+                           variables: dict | None, user: Message | None) -> list[Message]:
+        """Switch the context to the state just entered (``rec``)."""
+        if rec.get("budget_exhausted"):  # stopped where it stands
+            await self._completed(session_id, snap)
+            return msgs
+        system = self._system_message(variables, self._active_prompt(snap))
+        if self.workflow.persistence(rec["to_state"]) == "transient":
+            msgs = [system] + ([user] if user is not None else [])
+        else:
+            if msgs and msgs[0].role == "system":
+                msgs[0] = system
+            else:
+                msgs.insert(0, system)
+        span = tracing.start_span("omnia.workflow.transition", {
+            "workflow.from_state": rec["from_state"], "workflow.to_state": rec["to_state"],
+            "workflow.event": rec["event"], "workflow.prompt_task": rec["prompt_task"]})
+        tracing.end_span(span)
+        await self._emit(session_id, "workflow.transitioned", rec)
+        if snap["completed"]:
+            await self._completed(session_id, snap)
+        return msgs
+
+    async def _completed(self, session_id: str, snap: dict):
+        ev = {"final_state": snap["state"], "transition_count": snap["transitions"]}
+        if snap.get("exhausted"):
+            ev["budget_exhausted"] = snap["exhausted"]
+        await self._emit(session_id, "workflow.completed", ev)
+
+    async def _run_composition(self, name: str, session_id: str, content: str, io, ctx,
+                               metadata: dict, res: TurnResult) -> str:
+        from .composition import CompositionRunner, result_text
+
+        runner = CompositionRunner(self, name, session_id, io, ctx, metadata, res)
+        span = tracing.start_span("omnia.workflow.composition", {"composition.name": name})
+        try:
+            out, _ = await runner.run(content)
+        finally:
+            res.composition = runner.trace
+            tracing.end_span(span, {"composition.steps": len(runner.trace)})
+            await self._emit(session_id, "workflow.composition",
+                             {"composition": name, "steps": runner.trace})
+        return result_text(out)
+
+    async def _emit(self, session_id: str, kind: str, payload: dict):
+        if self.event_sink is None:
+            return
+        try:
+            await self.event_sink.record(session_id, kind, payload)
+        except Exception as e:  # noqa: BLE001
+            log.debug("event sink failed: %s", e)
 
     async def load_state(self, session_id: str) -> dict | None:
         return await self.store.load(session_id)
 
     async def new_state(self, variables=None) -> dict:
-        return {"messages": [self._system_message(variables).to_dict()], "turn": 0,
-                "created": time.time()}
+        st = {"messages": [self._system_message(variables).to_dict()], "turn": 0,
+              "created": time.time()}
+        if self.workflow is not None:
+            st["workflow"] = self.workflow.initial()
+        return st
 
-    def params(self, overrides: dict | None = None, guided: bool = False) -> SamplingParams:
+    def params(self, overrides: dict | None = None, guided: bool = False,
+               prompt: Prompt | None = None) -> SamplingParams:
         """Sampling params for a turn.  ``guided``: enforce the function-mode response
         format in the engine (K13 grammar masks; ignored by remote/mock providers) --
         only on tool-free turns, where the whole answer is the JSON document."""
@@ -118,7 +236,7 @@ class Agent:
                 # Provider CRD carries temperature / topP as decimal strings
                 v = dd[k_src]
                 d[k] = int(v) if k == "max_tokens" else float(v)
-        d.update(self.prompt.parameters or {})
+        d.update((prompt or self.prompt).parameters or {})
         d.update(overrides or {})
         if guided and self.cfg.response_format in ("json", "json_schema"):
             if self.cfg.response_format == "json_schema" and self.cfg.response_schema:
@@ -183,6 +301,20 @@ class Agent:
                 state = await self.new_state(variables)
             msgs = [Message.from_dict(d) for d in state["messages"]]
             user = Message("user", content, parts=parts or [])
+            snap = None
+            if self.workflow is not None:
+                snap = state.setdefault("workflow", self.workflow.initial())
+                if self.workflow.check_time(snap):
+                    await self._completed(session_id, snap)
+                ev = (metadata or {}).get("workflow_event")
+                if ev:  # caller-driven transition (orchestration external / hybrid)
+                    if not self.workflow.caller_can_fire(snap):
+                        raise WorkflowError(f"state {snap['state']!r} does not accept "
+                                            f"caller events")
+                    rec = self.workflow.fire(snap, ev)
+                    res.transitions.append(rec)
+                    msgs = await self._enter_state(session_id, snap, rec, msgs, variables, None)
+            prompt = self._active_prompt(snap)
             if self.memory is not None:
                 try:
                     mem = await self.memory.retrieve(session_id, content, ctx)
@@ -192,17 +324,24 @@ class Agent:
                 if mem:
                     msgs.append(Message("system", f"Relevant memories:\n{mem}"))
             msgs.append(user)
-            policy = self.prompt.tool_policy
-            tools = []
-            if self.executor is not None and policy.tool_choice != "none":
-                tools = self.pack.tool_specs(self.prompt, self.executor.specs())
-            params = self.params((metadata or {}).get("parameters")
-                                 if isinstance((metadata or {}).get("parameters"), dict) else None,
-                                 guided=not tools)
+            overrides = (metadata or {}).get("parameters") \
+                if isinstance((metadata or {}).get("parameters"), dict) else None
+            policy = prompt.tool_policy
+            tools = self._tools(prompt, snap)
+            params = self.params(overrides, guided=not tools, prompt=prompt)
             max_rounds = self.cfg.max_rounds or policy.max_rounds
             text_acc: list[str] = []
             calls_total = 0
             while True:
+                comp = self.workflow.composition(snap) if snap is not None else None
+                if comp:  # a composition state answers the turn with its step graph
+                    text = await self._run_composition(comp, session_id, content, io, ctx,
+                                                       metadata or {}, res)
+                    await io.chunk(text)
+                    text_acc.append(text)
+                    msgs.append(Message("assistant", text))
+                    res.rounds += 1
+                    break
                 window = await self._truncate(msgs, self.cfg.context_window)
                 if tools and getattr(self.provider, "type", "") == "local" \
                         and policy.tool_choice in ("auto", "required"):
@@ -263,16 +402,28 @@ class Agent:
                 budget = policy.max_tool_calls_per_turn - calls_total
                 allowed = round_calls[:max(0, budget)]
                 calls_total += len(round_calls)
-                results = await self._run_tools(allowed, io, ctx, metadata or {})
+                results = await self._run_tools(allowed, io, ctx, metadata or {}, snap, res)
                 for c in round_calls:
                     r = results.get(c.id) or {"result_json": json.dumps(
                         {"error": "max_tool_calls_per_turn exceeded"}), "is_error": True}
                     msgs.append(Message("tool", r["result_json"], tool_call_id=c.id, name=c.name))
                 res.tool_calls = calls_total
+                if snap is not None and self.workflow.count_tool_calls(snap, len(allowed)):
+                    await self._completed(session_id, snap)
+                    tools = []
+                    params = self.params(overrides, guided=True, prompt=prompt)
+                rec = results.get("__transition__")
+                if rec is not None:  # the model moved the workflow: new prompt from here on
+                    msgs = await self._enter_state(session_id, snap, rec, msgs, variables, user)
+                    prompt = self._active_prompt(snap)
+                    policy = prompt.tool_policy
+                    tools = self._tools(prompt, snap)
+                    params = self.params(overrides, guided=not tools, prompt=prompt)
             res.content = "".join(text_acc) if not msgs[-1].content else msgs[-1].content
             if res.rounds > 1:
                 res.content = msgs[-1].content or "".join(text_acc)
-            res.violations = run_validators(self.prompt, res.content)
+            res.violations = run_validators(prompt, res.content)
+            res.workflow = json.loads(json.dumps(snap)) if snap is not None else None
             for v in res.violations:
                 M.VALIDATIONS.labels(v.split(":")[0], "fail").inc()
             res.cost = self.provider.pricing.cost(res.usage)
@@ -294,7 +445,7 @@ class Agent:
                 await self._record(session_id, content, res)
             if self.evaluator is not None:
                 asyncio.get_running_loop().create_task(
-                    self.evaluator.on_turn(session_id, content, res, self.prompt))
+                    self.evaluator.on_turn(session_id, content, res, prompt))
             return res
         finally:
             M.PIPELINES_ACTIVE.dec()
@@ -304,8 +455,28 @@ class Agent:
                                     "gen_ai.usage.cost": res.cost})
 
     async def _run_tools(self, calls: list[ToolCallReq], io: TurnIO, ctx: CallContext,
-                         metadata: dict) -> dict[str, dict]:
+                         metadata: dict, snap: dict | None = None,
+                         res: TurnResult | None = None) -> dict[str, dict]:
         out: dict[str, dict] = {}
+        internal = [c for c in calls if c.name in (TRANSITION_TOOL, ARTIFACT_TOOL)
+                    or (self.multi_agent and c.name.startswith(AGENT_TOOL_PREFIX))]
+        calls = [c for c in calls if all(c is not i for i in internal)]
+        for c in internal:
+            out[c.id] = await self._run_internal(c, ctx, snap, res, out)
+        if self.executor is None:
+            for c in calls:
+                out[c.id] = {"result_json": json.dumps({"error": f"unknown tool {c.name}"}),
+                             "is_error": True}
+            return out
+        if snap is not None and self.workflow is not None and self.workflow.skill_scope(snap):
+            sk = self._skills()
+            allowed = scoped_skill_names(self.workflow.skill_scope(snap), sk.skills if sk else {})
+            for c in calls:
+                if c.name.startswith("skill__") and (c.arguments or {}).get("name") not in allowed:
+                    out[c.id] = {"result_json": json.dumps(
+                        {"error": f"skill not available in state {snap['state']!r}"}),
+                        "is_error": True}
+            calls = [c for c in calls if c.id not in out]
         server = [c for c in calls if not self.executor.is_client_tool(c.name)]
         client = [c for c in calls if self.executor.is_client_tool(c.name)]
 
@@ -332,6 +503,66 @@ class Agent:
                 else:
                     out[c.id] = {"result_json": r.get("result_json", "null"), "is_error": False}
         return out
+
+    async def _run_internal(self, c: ToolCallReq, ctx: CallContext, snap: dict | None,
+                            res: TurnResult | None, out: dict) -> dict:
+        args = c.arguments if isinstance(c.arguments, dict) else {}
+        if c.name == ARTIFACT_TOOL:
+            if self.workflow is None or snap is None:
+                return {"result_json": json.dumps({"error": "no workflow"}), "is_error": True}
+            try:
+                r = self.workflow.put_artifact(snap, str(args.get("name", "")),
+                                               args.get("content", ""))
+            except WorkflowError as e:
+                return {"result_json": json.dumps({"error": str(e)}), "is_error": True}
+            return {"result_json": json.dumps(r), "is_error": False}
+        if c.name == TRANSITION_TOOL:
+            if self.workflow is None or snap is None:
+                return {"result_json": json.dumps({"error": "no workflow"}), "is_error": True}
+            if "__transition__" in out:
+                return {"result_json": json.dumps(
+                    {"error": "one transition per round; already moved to "
+                              f"{snap['state']!r}"}), "is_error": True}
+            if not self.workflow.model_can_fire(snap):
+                return {"result_json": json.dumps(
+                    {"error": f"state {snap['state']!r} is not model-orchestrated"}),
+                    "is_error": True}
+            try:
+                rec = self.workflow.fire(snap, str(args.get("event", "")))
+            except WorkflowError as e:
+                return {"result_json": json.dumps({"error": str(e)}), "is_error": True}
+            out["__transition__"] = rec
+            if res is not None:
+                res.transitions.append(rec)
+            return {"result_json": json.dumps({"transitioned": True, **rec,
+                                               "completed": snap["completed"]}),
+                    "is_error": False}
+        member = c.name[len(AGENT_TOOL_PREFIX):]
+        if member not in (self.pack.agents or {}).get("members", {}) or \
+                member == self.pack.agents["entry"]:
+            return {"result_json": json.dumps({"error": f"unknown agent {member!r}"}),
+                    "is_error": True}
+        sub = self._members.get(member)
+        if sub is None:
+            sub = Agent(self.pack, self.provider, self.store, self.executor,
+                        dataclasses.replace(self.cfg, prompt_name=member), self.extra,
+                        self.memory, self.event_sink, None, self.tokenizer, graph=False)
+            sub.prompt = self.pack.prompts[member]
+            self._members[member] = sub
+        sid = f"{ctx.session_id or ''}/agent/{member}"
+        span = tracing.start_span("omnia.agent.delegate", {"agent.member": member})
+        try:
+            r = await sub.run_turn(sid, str(args.get("message", "")), _CollectIO(),
+                                   ctx=dataclasses.replace(ctx, session_id=sid))
+        except Exception as e:  # noqa: BLE001 - a failing member is a tool error
+            tracing.end_span(span, error=True)
+            return {"result_json": json.dumps({"agent": member, "error": str(e)}),
+                    "is_error": True}
+        tracing.end_span(span)
+        if res is not None:
+            res.usage += r.usage
+        return {"result_json": json.dumps({"agent": member, "content": r.content}),
+                "is_error": False}
 
     async def _record(self, session_id: str, user: str, res: TurnResult):
         try:

@@ -143,7 +143,8 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
     try:
         from .skills import attach_skills
 
-        attach_skills(executor)  # OMNIA_PROMPTPACK_MANIFEST_PATH; no-op without skills
+        # OMNIA_PROMPTPACK_MANIFEST_PATH + the pack's own skills; no-op without either
+        attach_skills(executor, pack=pack)
     except (OSError, ValueError) as e:  # unreadable/malformed manifest: serve without skills
         log.error("skill manifest load failed: %s", e)
     try:
@@ -171,7 +172,7 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
     if cfg.mode == "function" or cfg.output_format:
         prompt = agent.prompt
         instr = response_format_instruction(cfg.output_format or "json", cfg.output_schema)
-        fpack = PromptPack(json.loads(json.dumps(pack.data)))
+        fpack = PromptPack(json.loads(json.dumps(pack.data)), base_dir=pack.base_dir)
         for p in fpack.prompts.values():
             if p.id == prompt.id:
                 p.system_template = p.system_template + instr

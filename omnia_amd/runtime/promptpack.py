@@ -9,6 +9,23 @@ max_tool_calls_per_turn=10, blocklist), ``parameters`` (sampling) and
 ``validators`` (banned_words, max_length, min_length, regex_match, json_schema,
 pii_detection).  Templates use ``{{variable}}`` substitution and
 ``{{fragment_name}}`` / ``{{> fragment_name}}`` fragments (resolved first).
+
+Graph sections (``promptpack.schema.json:200-216``, ``$defs`` WorkflowConfig /
+AgentsConfig / SkillSource at ``:1211-1404``):
+
+* ``workflow`` -- a state machine over the prompts: ``entry`` state, ``states``
+  {name: {prompt_task, on_event {event: target}, persistence, orchestration,
+  skills}}; executed by :mod:`omnia_amd.runtime.workflow`;
+* ``agents`` -- multi-agent packs: ``entry`` prompt key plus ``members``
+  {prompt key: A2A card metadata}; the entry agent delegates to members;
+* ``skills`` -- pack-level skill sources (a path, ``{path, preload}`` or an
+  inline ``{name, description, instructions}``).
+
+Cross-references the JSON schema cannot express (entry exists, every
+``prompt_task`` / member is a prompt, every ``on_event`` target is a state) are
+checked on load.  The entry prompt resolves like ``internal/runtime/
+pack_entry.go:54-86``: workflow.entry, then agents.entry, then a sole prompt,
+then the configured/"default" name.
 The compiled pack lives at ``/etc/omnia/pack/pack.json`` in reconciled pods
 (``internal/controller/constants.go:103-127``).
 """
@@ -84,8 +101,101 @@ PACK_SCHEMA = {
                     "additionalProperties": {"$ref": "#/$defs/Prompt"}},
         "fragments": {"type": "object", "additionalProperties": {"type": "string"}},
         "tools": {"type": "object", "additionalProperties": {"$ref": "#/$defs/Tool"}},
+        "workflow": {"$ref": "#/$defs/WorkflowConfig"},
+        "agents": {"$ref": "#/$defs/AgentsConfig"},
+        "skills": {"type": "array", "items": {"$ref": "#/$defs/SkillSource"}},
+        "compositions": {"type": "object",
+                         "additionalProperties": {"$ref": "#/$defs/Composition"}},
     },
     "$defs": {
+        "WorkflowConfig": {
+            "type": "object", "required": ["version", "entry", "states"],
+            "additionalProperties": False,
+            "properties": {"version": {"type": "integer", "minimum": 1},
+                           "entry": {"type": "string"},
+                           "states": {"type": "object", "minProperties": 1,
+                                      "additionalProperties": {"$ref": "#/$defs/WorkflowState"}},
+                           "engine": {"type": "object", "properties": {"budget": {
+                               "type": "object", "properties": {
+                                   "max_total_visits": {"type": "integer", "minimum": 1},
+                                   "max_tool_calls": {"type": "integer", "minimum": 1},
+                                   "max_wall_time_sec": {"type": "number",
+                                                         "exclusiveMinimum": 0}}}}}}},
+        # the published schema file predates PromptKit 1.5; compiled packs in
+        # the reference's own samples also carry terminal / max_visits /
+        # on_max_visits / artifacts and composition states
+        # (config/samples/omnia_v1alpha1_promptpack_deep_research.yaml:383-455,
+        # ..._doc_analysis.yaml), so those are part of the accepted shape
+        "WorkflowState": {
+            "type": "object", "additionalProperties": False,
+            "properties": {"prompt_task": {"type": "string"},
+                           "description": {"type": "string"},
+                           "on_event": {"type": "object",
+                                        "additionalProperties": {"type": "string"}},
+                           "persistence": {"enum": ["transient", "persistent"]},
+                           "orchestration": {"enum": ["internal", "external", "hybrid",
+                                                      "composition"]},
+                           "composition": {"type": "string"},
+                           "skills": {"type": "string"},
+                           "terminal": {"type": "boolean"},
+                           "max_visits": {"type": "integer", "minimum": 1},
+                           "on_max_visits": {"type": "string"},
+                           "artifacts": {"type": "object", "additionalProperties": {
+                               "type": "object",
+                               "properties": {"type": {"type": "string"},
+                                              "mode": {"enum": ["append", "replace"]},
+                                              "description": {"type": "string"}}}}}},
+        "Composition": {
+            "type": "object", "required": ["steps"],
+            "properties": {"version": {"type": "integer", "minimum": 1},
+                           "description": {"type": "string"},
+                           "steps": {"type": "array", "minItems": 1,
+                                     "items": {"$ref": "#/$defs/Step"}}}},
+        "Step": {
+            "type": "object", "required": ["id", "kind"],
+            "properties": {"id": {"type": "string", "minLength": 1},
+                           "kind": {"enum": ["prompt", "parallel", "tool", "branch", "agent"]},
+                           "prompt_task": {"type": "string"},
+                           "tool": {"type": "string"},
+                           "args": {"type": "object"},
+                           "depends_on": {"type": "array", "items": {"type": "string"}},
+                           "branches": {"type": "array", "minItems": 1,
+                                        "items": {"$ref": "#/$defs/Step"}},
+                           "reduce": {"type": "object", "properties": {
+                               "strategy": {"enum": ["barrier"]},
+                               "into": {"type": "string"}}},
+                           "predicate": {"type": "object", "required": ["path", "op"],
+                                         "properties": {"path": {"type": "string"},
+                                                        "op": {"enum": [
+                                                            "equals", "not_equals", "contains",
+                                                            "exists", "gt", "gte", "lt", "lte",
+                                                            "in"]}}},
+                           "then": {"type": "string"}, "else": {"type": "string"},
+                           "tools": {"type": "array", "items": {"type": "string"}},
+                           "termination": {"type": "object", "properties": {
+                               "max_steps": {"type": "integer", "minimum": 1}}}}},
+        "AgentsConfig": {
+            "type": "object", "required": ["entry", "members"], "additionalProperties": False,
+            "properties": {"entry": {"type": "string"},
+                           "members": {"type": "object", "minProperties": 1,
+                                       "additionalProperties": {"$ref": "#/$defs/AgentDef"}}}},
+        "AgentDef": {
+            "type": "object", "additionalProperties": False,
+            "properties": {"description": {"type": "string"},
+                           "tags": {"type": "array", "items": {"type": "string"}},
+                           "input_modes": {"type": "array", "items": {"type": "string"}},
+                           "output_modes": {"type": "array", "items": {"type": "string"}}}},
+        "SkillSource": {"oneOf": [{"type": "string"}, {"$ref": "#/$defs/SkillPathSource"},
+                                  {"$ref": "#/$defs/InlineSkill"}]},
+        "SkillPathSource": {
+            "type": "object", "required": ["path"], "additionalProperties": False,
+            "properties": {"path": {"type": "string"}, "preload": {"type": "boolean"}}},
+        "InlineSkill": {
+            "type": "object", "required": ["name", "description", "instructions"],
+            "additionalProperties": False,
+            "properties": {"name": {"type": "string", "minLength": 1},
+                           "description": {"type": "string", "minLength": 1},
+                           "instructions": {"type": "string", "minLength": 1}}},
         "Prompt": {
             "type": "object",
             "required": ["id", "name", "version", "system_template"],
@@ -118,11 +228,12 @@ PACK_SCHEMA = {
 
 
 class PromptPack:
-    def __init__(self, data: dict):
+    def __init__(self, data: dict, base_dir: str | Path | None = None):
         errs = jsonschema.Validator(PACK_SCHEMA).errors(data)
         if errs:
             raise PackError("invalid pack: " + "; ".join(str(e) for e in errs[:5]))
         self.data = data
+        self.base_dir = Path(base_dir) if base_dir is not None else None
         self.id = data["id"]
         self.name = data["name"]
         self.version = data["version"]
@@ -137,6 +248,98 @@ class PromptPack:
                 tool_policy=ToolPolicy.from_dict(p.get("tool_policy")),
                 parameters=dict(p.get("parameters", {})),
                 validators=list(p.get("validators", [])), evals=list(p.get("evals", [])), raw=p)
+        self.workflow: dict | None = data.get("workflow")
+        self.agents: dict | None = data.get("agents")
+        self.skill_sources: list = list(data.get("skills", []))
+        self.compositions: dict = dict(data.get("compositions", {}))
+        self._check_graph()
+
+    def _check_graph(self):
+        """Cross-references of the workflow / agents sections."""
+        errs = []
+        wf = self.workflow
+        if wf:
+            states = wf["states"]
+            if wf["entry"] not in states:
+                errs.append(f"workflow.entry {wf['entry']!r} is not a state")
+            for name, st in states.items():
+                if st.get("orchestration") == "composition":
+                    if st.get("composition") not in self.compositions:
+                        errs.append(f"workflow state {name!r}: composition "
+                                    f"{st.get('composition')!r} is not defined")
+                elif st.get("prompt_task") not in self.prompts:
+                    errs.append(f"workflow state {name!r}: prompt_task "
+                                f"{st.get('prompt_task')!r} is not a prompt")
+                for ev, target in (st.get("on_event") or {}).items():
+                    if target not in states:
+                        errs.append(f"workflow state {name!r}: event {ev!r} targets "
+                                    f"unknown state {target!r}")
+                if st.get("on_max_visits") and st["on_max_visits"] not in states:
+                    errs.append(f"workflow state {name!r}: on_max_visits targets unknown "
+                                f"state {st['on_max_visits']!r}")
+        for cname, comp in self.compositions.items():
+            errs += self._check_composition(cname, comp)
+        ag = self.agents
+        if ag:
+            if ag["entry"] not in ag["members"]:
+                errs.append(f"agents.entry {ag['entry']!r} is not a member")
+            for key in ag["members"]:
+                if key not in self.prompts:
+                    errs.append(f"agents member {key!r} is not a prompt")
+        if errs:
+            raise PackError("invalid pack: " + "; ".join(errs[:5]))
+
+    def _check_composition(self, cname: str, comp: dict) -> list[str]:
+        errs, ids = [], []
+        top = [s["id"] for s in comp["steps"]]
+
+        def walk(step):
+            ids.append(step["id"])
+            k = step["kind"]
+            where = f"composition {cname!r} step {step['id']!r}"
+            if k in ("prompt", "agent") and step.get("prompt_task") not in self.prompts:
+                errs.append(f"{where}: prompt_task {step.get('prompt_task')!r} is not a prompt")
+            if k == "tool" and not step.get("tool"):
+                errs.append(f"{where}: tool step needs 'tool'")
+            if k == "parallel" and not step.get("branches"):
+                errs.append(f"{where}: parallel step needs 'branches'")
+            if k == "branch":
+                if "predicate" not in step or "then" not in step:
+                    errs.append(f"{where}: branch step needs 'predicate' and 'then'")
+                for tgt in (step.get("then"), step.get("else")):
+                    if tgt is not None and tgt not in top:
+                        errs.append(f"{where}: branch target {tgt!r} is not a step")
+            for d in step.get("depends_on") or []:
+                if d not in top:
+                    errs.append(f"{where}: depends_on {d!r} is not a step")
+            for b in step.get("branches") or []:
+                walk(b)
+
+        for st in comp["steps"]:
+            walk(st)
+        dup = sorted({i for i in ids if ids.count(i) > 1})
+        if dup:
+            errs.append(f"composition {cname!r}: duplicate step ids {dup}")
+        return errs
+
+    def entry(self, fallback: str = "default") -> str:
+        """Prompt key the runtime opens the pack at (``pack_entry.go:54-86``).
+        A workflow whose entry state runs a composition opens at the first
+        prompt (the composition's own steps name theirs)."""
+        if self.workflow:
+            st = self.workflow["states"][self.workflow["entry"]]
+            return st.get("prompt_task") or next(iter(self.prompts))
+        if self.agents:
+            return self.agents["entry"]
+        if len(self.prompts) == 1:
+            return next(iter(self.prompts))
+        return fallback
+
+    def key_of(self, prompt: "Prompt") -> str:
+        for k, p in self.prompts.items():
+            if p is prompt:
+                return k
+        return prompt.id
 
     @classmethod
     def load(cls, path: str | Path) -> "PromptPack":
@@ -144,7 +347,7 @@ class PromptPack:
         if p.is_dir():
             p = p / "pack.json"
         try:
-            return cls(json.loads(p.read_text()))
+            return cls(json.loads(p.read_text()), base_dir=p.parent)
         except json.JSONDecodeError as e:
             raise PackError(f"pack.json is not valid JSON: {e}") from e
 
@@ -163,8 +366,9 @@ class PromptPack:
                 if p.id == name or p.name == name:
                     return p
             raise PackError(f"prompt {name!r} not in pack {self.id}")
-        if "default" in self.prompts:
-            return self.prompts["default"]
+        key = self.entry()
+        if key in self.prompts:
+            return self.prompts[key]
         return next(iter(self.prompts.values()))
 
     # ------------------------------------------------------------ rendering

@@ -20,6 +20,13 @@ instructions and reads the skill's bundled resources on demand:
 These are server-side tools of a :class:`SkillsHandler`, so they go through the
 executor's policy, circuit-breaker and metrics path like any other tool. They
 are never sent to the facade.
+
+Pack-level ``skills`` (``promptpack.schema.json:210-216``, ``$defs.SkillSource``)
+join the manifest's: a string or ``{path, preload}`` names a skill directory
+(relative to the pack file) or a directory of skill directories; an inline
+``{name, description, instructions}`` is a skill without resources.  Skills
+marked ``preload`` are active from the first turn: their instructions are part
+of the system prompt (:func:`preloaded_instructions`).
 """
 from __future__ import annotations
 
@@ -77,6 +84,7 @@ class Skill:
     mount_as: str
     root: str
     instructions: str
+    preload: bool = False
 
 
 def load_skill(entry: ManifestEntry) -> Skill:
@@ -101,10 +109,16 @@ def load_skill(entry: ManifestEntry) -> Skill:
 class SkillsHandler(Handler):
     type = "skills"
 
-    def __init__(self, manifest: Manifest, workflow_prefix: str = ""):
+    def __init__(self, manifest: Manifest, workflow_prefix: str = "",
+                 extra: list[Skill] | None = None):
         super().__init__({"name": "skills"})
         self.skills: dict[str, Skill] = {}
         self.load_errors: list[str] = []
+        for s in extra or []:
+            if s.name in self.skills:
+                self.load_errors.append(f"duplicate skill {s.name}")
+                continue
+            self.skills[s.name] = s
         for e in manifest.skills:
             try:
                 s = load_skill(e)
@@ -174,6 +188,8 @@ class SkillsHandler(Handler):
             active.pop(s.name, None)
             return json.dumps({"skill": s.name, "active": list(active)})
         if tool.name == "skill__read_resource":
+            if not s.root:
+                raise PermissionError(f"inline skill {s.name!r} has no resources")
             p = os.path.realpath(os.path.join(s.root, args.get("path", "")))
             if os.path.commonpath([p, s.root]) != s.root or not os.path.isfile(p):
                 raise PermissionError("resource outside the skill directory or missing")
@@ -183,13 +199,57 @@ class SkillsHandler(Handler):
         raise KeyError(tool.name)
 
 
-def attach_skills(executor, manifest_path: str | None = None, workflow_prefix: str = ""):
-    """Add the manifest's skills to an executor (no-op without a manifest)."""
+def pack_skills(pack) -> list[Skill]:
+    """Skills declared in the pack's own ``skills`` list."""
+    out: list[Skill] = []
+    base = str(pack.base_dir) if getattr(pack, "base_dir", None) else os.getcwd()
+    for src in getattr(pack, "skill_sources", []) or []:
+        if isinstance(src, dict) and "instructions" in src:
+            out.append(Skill(name=src["name"], description=src["description"],
+                             mount_as=f"inline/{src['name']}", root="",
+                             instructions=src["instructions"], preload=True))
+            continue
+        path, preload = (src, False) if isinstance(src, str) else \
+            (src["path"], bool(src.get("preload", False)))
+        if path.startswith("@"):
+            log.warning("skill package reference %s needs the PromptPack reconciler's "
+                        "manifest; skipped", path)
+            continue
+        root = path if os.path.isabs(path) else os.path.normpath(os.path.join(base, path))
+        dirs = [root] if os.path.isfile(os.path.join(root, "SKILL.md")) else sorted(
+            os.path.join(root, d) for d in (os.listdir(root) if os.path.isdir(root) else [])
+            if os.path.isfile(os.path.join(root, d, "SKILL.md")))
+        if not dirs:
+            log.error("pack skill source %s holds no SKILL.md", path)
+        for d in dirs:
+            rel = os.path.relpath(d, base)
+            try:
+                s = load_skill(ManifestEntry(mount_as=rel, content_path=d))
+            except (OSError, ValueError) as err:
+                log.error("pack skill %s skipped: %s", d, err)
+                continue
+            s.preload = preload
+            out.append(s)
+    return out
+
+
+def preloaded_instructions(handler: "SkillsHandler | None") -> str:
+    if handler is None:
+        return ""
+    pre = [s for s in handler.skills.values() if s.preload]
+    return "".join(f"\n\n## Skill: {s.name}\n{s.instructions}" for s in pre)
+
+
+def attach_skills(executor, manifest_path: str | None = None, workflow_prefix: str = "",
+                  pack=None):
+    """Add the manifest's and the pack's skills to an executor (no-op without
+    either)."""
     path = manifest_path if manifest_path is not None else \
         os.environ.get("OMNIA_PROMPTPACK_MANIFEST_PATH", "")
     m = read_manifest(path)
-    if not m.skills:
+    extra = pack_skills(pack) if pack is not None else []
+    if not m.skills and not extra:
         return None
-    h = SkillsHandler(m, workflow_prefix)
+    h = SkillsHandler(m, workflow_prefix, extra=extra)
     executor.add_handler(h)
     return h

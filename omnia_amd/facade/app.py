@@ -6,6 +6,7 @@
 
   OMNIA_AGENT_NAME / OMNIA_NAMESPACE / OMNIA_FACADE_PORT / OMNIA_RUNTIME_ADDRESS
   OMNIA_MODE (agent|function), OMNIA_FACADE_TYPES (websocket,rest,a2a,mcp)
+  OMNIA_GRACE_WINDOW_SECONDS / OMNIA_ROUTE_REDIS_URL / POD_IP (realtime blip-resume)
   OMNIA_HANDLER_MODE (runtime|echo|demo), OMNIA_INPUT_SCHEMA / OMNIA_OUTPUT_SCHEMA
   auth: OMNIA_AUTH_SHARED_TOKEN, OMNIA_AUTH_CLIENT_KEYS (json {id: sha256}),
         OMNIA_OIDC_ISSUER / OMNIA_OIDC_AUDIENCE / OMNIA_OIDC_HS256_SECRET /
@@ -61,6 +62,13 @@ def config_from_env(env) -> FacadeConfig:
                     ("OMNIA_MEDIA_ENABLED", "media_enabled", lambda v: v.lower() == "true")):
         if env.get(k):
             setattr(c, f, t(env[k]))
+    try:  # cmd/agent/websocket.go:218-225: positive integer seconds, default 15
+        g = int(env.get("OMNIA_GRACE_WINDOW_SECONDS", "") or 0)
+    except ValueError:
+        g = 0
+    if g > 0:
+        c.grace_window_s = float(g)
+    c.pod_addr = f"{env.get('POD_IP', '')}:{c.port}"
     return c
 
 
@@ -84,8 +92,11 @@ def build_facade(env, runtime_client, recorder=None) -> FacadeServer:
         media = build_media_storage(env)
     cfg = config_from_env(env)
     cfg.media_enabled = cfg.media_enabled or media is not None
+    from .realtime import route_store_from_env
+
     fac = FacadeServer(cfg, handler=handler, runtime_client=runtime_client,
-                       auth=auth_from_env(env), recorder=recorder, media_store=media)
+                       auth=auth_from_env(env), recorder=recorder, media_store=media,
+                       routes=route_store_from_env(env))  # OMNIA_ROUTE_REDIS_URL
     if media is not None:
         from ..media import mount_media
 

@@ -15,6 +15,12 @@ client-supplied foreign session id triggers the HasConversation resume probe
 (NOT_FOUND -> SESSION_EXPIRED, UNAVAILABLE -> INTERNAL_ERROR), the trace id is
 derived from the session UUID, and SIGTERM drains: no new upgrades, live
 sessions get ``drain_timeout`` to finish.
+
+Realtime blip-resume (:mod:`.realtime`): a connection that drops without a
+``hangup`` while a duplex audio call is up parks the call for
+``grace_window_s``; ``?resume=<session>`` from the same owner takes it back
+(``connected.resumed = true``) and replays what the runtime said meanwhile.
+Draining still admits such resume upgrades and waits for live + parked calls.
 """
 from __future__ import annotations
 
@@ -36,6 +42,7 @@ from . import protocol as P
 from ..observability import logging as logctx
 from .auth import AuthChain, AuthError
 from .handlers import PendingTools, RuntimeHandler, Writer
+from .realtime import NoopRouteStore, RealtimeRegistry
 
 log = logging.getLogger("omnia.facade")
 
@@ -58,6 +65,8 @@ class FacadeConfig:
     binary_frames: bool = True
     media_enabled: bool = False
     drain_timeout_s: float = 30.0
+    grace_window_s: float = 15.0  # OMNIA_GRACE_WINDOW_SECONDS
+    pod_addr: str = ""  # POD_IP:port, the route hint of parked calls
     functions: dict = field(default_factory=dict)  # name -> {"input_schema", "output_schema"}
     allowed_origins: list = field(default_factory=list)  # [] = any
 
@@ -83,7 +92,8 @@ class _WSWriter(Writer):
 
 class FacadeServer:
     def __init__(self, cfg: FacadeConfig, handler=None, runtime_client=None,
-                 auth: AuthChain | None = None, recorder=None, media_store=None):
+                 auth: AuthChain | None = None, recorder=None, media_store=None,
+                 routes=None):
         self.cfg = cfg
         self.client = runtime_client
         self.handler = handler or (RuntimeHandler(runtime_client) if runtime_client else None)
@@ -97,6 +107,10 @@ class FacadeServer:
         self._caps: tuple[float, list] | None = None
         self.labels = (cfg.agent, cfg.namespace)
         self._conn_done = asyncio.Event()
+        self._bg: set = set()
+        self.routes = routes or NoopRouteStore()
+        self.parked = RealtimeRegistry(self.routes, cfg.pod_addr, cfg.grace_window_s,
+                                       self._park_expired)
         self.app = web.Application(client_max_size=cfg.max_message_bytes)
         r = self.app.router
         r.add_get("/ws", self.ws_handler)
@@ -119,6 +133,19 @@ class FacadeServer:
             except Exception:  # noqa: BLE001
                 self._caps = (now, [])
         return pb.CAP_DUPLEX_AUDIO in self._caps[1]
+
+    async def _park_expired(self, session_id: str, persisted: bool):
+        # parking skipped completion (the call might resume); expiry is where it
+        # definitively did not -- complete only a session that was recorded
+        if persisted and self.recorder is not None:
+            try:
+                await self.recorder.close_session(session_id)
+            except Exception as e:  # noqa: BLE001
+                log.warning("completing expired parked session %s failed: %s", session_id, e)
+
+    @staticmethod
+    def _owner(ident) -> str:
+        return getattr(ident, "end_user", "") or getattr(ident, "subject", "") or ""
 
     # ---------------------------------------------------------------- health
     async def healthz(self, request):
@@ -156,7 +183,8 @@ class FacadeServer:
 
     # ---------------------------------------------------------------- websocket
     async def ws_handler(self, request):
-        if self.draining:
+        resume = request.query.get("resume")
+        if self.draining and not resume:  # draining still admits realtime reattach
             return web.Response(status=503, text="draining")
         if self.connections >= self.cfg.max_connections:
             return web.Response(status=503, text="too many connections")
@@ -174,12 +202,17 @@ class FacadeServer:
         M.CONNECTIONS_ACTIVE.labels(*self.labels).inc()
         M.CONNECTIONS_TOTAL.labels(*self.labels).inc()
         binary = request.query.get("binary", "false").lower() == "true" and self.cfg.binary_frames
-        resume = request.query.get("resume")
+        owner = self._owner(ident)
+        parked = await self.parked.take(resume, owner) if resume else None
         session_id = resume or str(uuid.uuid4())
         writer = _WSWriter(ws, self.labels)
         await writer.write(P.connected(session_id, binary, self.cfg.max_message_bytes,
                                        resumed=bool(resume)))
         conn = _Connection(self, ws, writer, ident, request, session_id)
+        if parked is not None:  # blip-resume: the live call continues on this socket
+            conn.audio = parked
+            conn.session_ensured = parked.persisted
+            await parked.attach(conn)
         try:
             await conn.read_loop()
         finally:
@@ -189,7 +222,24 @@ class FacadeServer:
                 t.cancel()
             if self.connections == 0:
                 self._conn_done.set()
+            audio, conn.audio = conn.audio, None
+            if audio is not None:
+                # aiohttp cancels the handler when the peer drops: release the
+                # call in a task of its own so parking completes regardless
+                if not (conn.hung_up or audio.finished):
+                    audio.detach(persisted=conn.session_ensured)
+                t = asyncio.get_running_loop().create_task(
+                    self._release_audio(conn, audio, owner))
+                self._bg.add(t)
+                t.add_done_callback(self._bg.discard)
+                await asyncio.shield(t)
         return ws
+
+    async def _release_audio(self, conn, audio, owner: str):
+        if conn.hung_up or audio.finished:
+            await audio.close()
+        else:  # dropped mid-call: park it for a reconnect
+            await self.parked.park(conn.session_id, owner, audio, conn.session_ensured)
 
     # ---------------------------------------------------------------- function mode
     async def function_handler(self, request):
@@ -260,18 +310,31 @@ class FacadeServer:
         await site.start()
         return site._server.sockets[0].getsockname()[1]
 
-    async def drain(self):
-        """SIGTERM: stop upgrades, give live sessions drain_timeout (drain.go:51-92)."""
+    async def drain(self) -> int:
+        """SIGTERM: stop new upgrades (resume reattach still admitted), give live
+        connections and realtime calls -- active or parked -- drain_timeout
+        (drain.go:40-104).  Returns the realtime calls still live at the end."""
         self.draining = True
         M.DRAINING.set(1)
-        if self.connections:
-            self._conn_done.clear()
-            try:
-                await asyncio.wait_for(self._conn_done.wait(), self.cfg.drain_timeout_s)
-            except asyncio.TimeoutError:
-                pass
+        M.REALTIME_DRAINING.set(1)
+        t0 = time.monotonic()
+        initial = self.audio_sessions
+        deadline = t0 + self.cfg.drain_timeout_s
+        reason = "all_drained"
+        while self.connections or self.audio_sessions or len(self.parked):
+            if time.monotonic() >= deadline:
+                reason = "deadline"
+                break
+            await asyncio.sleep(0.05)
+        remaining = self.audio_sessions
+        M.REALTIME_DRAIN_DURATION.labels(reason).observe(time.monotonic() - t0)
+        M.REALTIME_DRAINED.inc(max(0, initial - remaining))
+        M.REALTIME_FORCE_ENDED.inc(remaining)
+        M.REALTIME_DRAINING.set(0)
+        return remaining
 
     async def stop(self):
+        await self.parked.close_all()
         if self.runner is not None:
             await self.runner.cleanup()
 
@@ -291,6 +354,7 @@ class _Connection:
         self.tasks: set = set()
         self.session_ensured = False
         self.audio = None  # _AudioSession while a duplex call is up
+        self.hung_up = False
 
     async def on_audio(self, fr: dict):
         if self.audio is None:
@@ -329,6 +393,7 @@ class _Connection:
                                                     f"invalid message: {e}"))
                     continue
                 if await self.on_message(msg) == "hangup":
+                    self.hung_up = True
                     await self.ws.close()
                     break
             elif m.type == WSMsgType.BINARY:
@@ -500,11 +565,48 @@ class _AudioSession:
     metadata, every inbound media-chunk frame -> AudioInputChunk, and the
     runtime's frames relayed back (audio as binary media-chunk frames)."""
 
+    MAX_BUFFERED = 4096  # frames held for a reconnect while parked
+
     def __init__(self, conn: "_Connection"):
         self.c = conn
+        self.srv = conn.srv
+        self.session_id = conn.session_id
         self.stream = None
         self.relay = None
         self.media_seq = 0
+        self.persisted = False
+        self.finished = False
+        self.buffer: list = []  # (is_bytes, payload) produced while parked
+
+    # ---------------------------------------------------------------- park / resume
+    def detach(self, persisted: bool = False):
+        self.c = None
+        self.persisted = persisted
+
+    async def attach(self, conn: "_Connection"):
+        self.c = conn
+        pending, self.buffer = self.buffer, []
+        for is_bytes, payload in pending:
+            await (conn.writer.write_bytes(payload) if is_bytes else conn.writer.write(payload))
+
+    async def _out(self, msg):
+        c = self.c
+        if c is None or c.ws.closed:
+            if len(self.buffer) < self.MAX_BUFFERED:
+                self.buffer.append((isinstance(msg, bytes), msg))
+            return
+        await (c.writer.write_bytes(msg) if isinstance(msg, bytes) else c.writer.write(msg))
+
+    async def close(self):
+        # the relay's exit releases the call's slot and closes the stream
+        if self.relay is not None and not self.relay.done():
+            self.relay.cancel()
+            await asyncio.gather(self.relay, return_exceptions=True)
+        elif self.stream is not None:
+            try:
+                await self.stream.close()
+            except Exception:  # noqa: BLE001
+                pass
 
     async def start(self, meta: dict):
         c = self.c
@@ -523,7 +625,7 @@ class _AudioSession:
             is_last=bool(fr["flags"] & P.FLAG_LAST) and not (fr["flags"] & P.FLAG_CHUNKED))))
 
     async def _relay(self):
-        c, sid, w = self.c, self.c.session_id, self.c.writer
+        sid, out = self.session_id, self._out
         try:
             while True:
                 resp = await self.stream.recv()
@@ -532,32 +634,39 @@ class _AudioSession:
                 kind = resp.WhichOneof("message")
                 if kind == "runtime_hello":
                     m = resp.runtime_hello.media
-                    await w.write(P.server_msg(P.SESSION_CONFIG, sid, media={
+                    await out(P.server_msg(P.SESSION_CONFIG, sid, media={
                         "codec": m.codec, "sample_rate": m.sample_rate, "channels": m.channels},
                         capabilities=list(resp.runtime_hello.capabilities)))
                 elif kind == "chunk":
-                    await w.write(P.chunk(sid, resp.chunk.content, resp.chunk.role))
+                    await out(P.chunk(sid, resp.chunk.content, resp.chunk.role))
                 elif kind == "media_chunk":
                     mc = resp.media_chunk
                     fl = P.FLAG_LAST if mc.is_last else 0
-                    await w.write_bytes(P.encode_frame(
+                    await out(P.encode_frame(
                         P.TYPE_MEDIA_CHUNK, bytes(mc.data),
                         {"session_id": sid, "mime_type": mc.mime_type}, mc.sequence,
                         mc.media_id.encode()[:12], fl))
                 elif kind == "interruption":
-                    await w.write(P.server_msg(P.INTERRUPT, sid))
+                    await out(P.server_msg(P.INTERRUPT, sid))
                 elif kind == "done":
                     d = resp.done
-                    await w.write(P.done(sid, d.final_content, None, {
+                    await out(P.done(sid, d.final_content, None, {
                         "input_tokens": d.usage.input_tokens,
                         "output_tokens": d.usage.output_tokens}))
                 elif kind == "error":
-                    await w.write(P.error(sid, resp.error.code or P.E_INTERNAL,
-                                          resp.error.message))
+                    await out(P.error(sid, resp.error.code or P.E_INTERNAL,
+                                      resp.error.message))
                     return
         finally:
-            c.srv.audio_sessions -= 1
-            await self.stream.close()
+            self.finished = True
+            self.srv.audio_sessions -= 1
+            try:
+                await self.stream.close()
+            except Exception:  # noqa: BLE001
+                pass
+            if self.c is None and sid in self.srv.parked.parked:
+                # the runtime ended the call while it was parked: nothing to resume
+                asyncio.get_running_loop().create_task(self.srv.parked.expire(sid))
 
     async def wait_closed(self, timeout: float = 120.0):
         if self.relay is not None:

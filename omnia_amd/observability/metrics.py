@@ -38,6 +38,23 @@ RECORDING_DROPPED = Counter("omnia_facade_recording_dropped_total",
 RATE_LIMITED = Counter("omnia_facade_rate_limited_total", "Messages rejected by rate limit",
                        ["kind"], registry=REGISTRY)
 DRAINING = Gauge("omnia_facade_draining", "1 while the facade drains", registry=REGISTRY)
+# realtime blip-resume + drain (internal/agent/metrics.go:298-340)
+REALTIME_PARKED = Counter("omnia_facade_realtime_sessions_parked_total",
+                          "Realtime sessions parked after a client disconnect", registry=REGISTRY)
+REALTIME_REATTACHED = Counter("omnia_facade_realtime_reattach_total",
+                              "Clients reattached to a parked realtime session",
+                              registry=REGISTRY)
+REALTIME_PARK_EXPIRED = Counter("omnia_facade_realtime_park_expired_total",
+                                "Parked realtime sessions that expired unclaimed",
+                                registry=REGISTRY)
+REALTIME_DRAINING = Gauge("omnia_facade_realtime_draining", "1 while realtime calls drain",
+                          registry=REGISTRY)
+REALTIME_DRAIN_DURATION = Histogram("omnia_facade_realtime_drain_duration_seconds",
+                                    "Drain duration", ["reason"], registry=REGISTRY)
+REALTIME_DRAINED = Counter("omnia_facade_realtime_calls_drained_total",
+                           "Realtime calls that finished during drain", registry=REGISTRY)
+REALTIME_FORCE_ENDED = Counter("omnia_facade_realtime_calls_force_ended_total",
+                               "Realtime calls still live when drain ended", registry=REGISTRY)
 A2A_REQUESTS = Counter("omnia_a2a_requests_total", "A2A JSON-RPC requests", ["method", "status"],
                        registry=REGISTRY)
 MCP_REQUESTS = Counter("omnia_mcp_requests_total", "MCP requests", ["method", "status"],

@@ -137,6 +137,11 @@ def facade_env(ar: dict) -> dict:
         env["OMNIA_OIDC_JWKS_FILE"] = "/etc/omnia/oidc/jwks.json"
     if (ea.get("edgeTrust") or {}).get("enabled"):
         env["OMNIA_EDGE_TRUST"] = "true"
+    # blip-resume route hints share the Redis of a Redis context store
+    # (internal/controller/deployment_builder_env.go:147-162)
+    ctx = spec.get("context") or {}
+    if ctx.get("type") == "redis" and (ctx.get("storeRef") or {}).get("url"):
+        env["OMNIA_ROUTE_REDIS_URL"] = ctx["storeRef"]["url"]
     return env
 
 

@@ -16,6 +16,8 @@ F = descriptor_pb2.FieldDescriptorProto
 _TYPES = {
     "string": F.TYPE_STRING, "bytes": F.TYPE_BYTES, "bool": F.TYPE_BOOL, "int32": F.TYPE_INT32,
     "uint32": F.TYPE_UINT32, "int64": F.TYPE_INT64, "float": F.TYPE_FLOAT, "double": F.TYPE_DOUBLE,
+    "uint64": F.TYPE_UINT64, "fixed32": F.TYPE_FIXED32, "fixed64": F.TYPE_FIXED64,
+    "sfixed64": F.TYPE_SFIXED64,
 }
 
 POOL = descriptor_pool.DescriptorPool()
@@ -31,7 +33,7 @@ def _field(msg, name, number, typ, repeated=False, oneof=None, package=""):
         f.type = _TYPES[typ]
     elif typ.startswith("enum:"):
         f.type = F.TYPE_ENUM
-        f.type_name = f".{package}.{typ[5:]}"
+        f.type_name = typ[5:] if typ[5:].startswith(".") else f".{package}.{typ[5:]}"
     else:
         f.type = F.TYPE_MESSAGE
         f.type_name = typ if typ.startswith(".") else f".{package}.{typ}"
@@ -40,12 +42,16 @@ def _field(msg, name, number, typ, repeated=False, oneof=None, package=""):
     return f
 
 
-def build_file(name: str, package: str, messages: dict, enums: dict, services: dict) -> dict:
-    """messages: {Msg: [(field, num, type, opts...)]}; map fields as ("map", k, v)."""
+def build_file(name: str, package: str, messages: dict, enums: dict, services: dict,
+               deps: tuple = ()) -> dict:
+    """messages: {Msg: [(field, num, type, opts...)]}; map fields as ("map", k, v);
+    a type name with a leading "." is fully qualified (another package, listed in
+    ``deps`` by file name).  Nested messages are written "Outer.Inner"."""
     fd = descriptor_pb2.FileDescriptorProto()
     fd.name = name
     fd.package = package
     fd.syntax = "proto3"
+    fd.dependency.extend(deps)
     for ename, values in enums.items():
         e = fd.enum_type.add()
         e.name = ename
@@ -53,9 +59,16 @@ def build_file(name: str, package: str, messages: dict, enums: dict, services: d
             v = e.value.add()
             v.name = vname
             v.number = vnum
+    tops: dict = {}
     for mname, fields in messages.items():
-        m = fd.message_type.add()
-        m.name = mname
+        if "." in mname:  # nested message (declared after its parent)
+            outer, inner = mname.split(".", 1)
+            m = tops[outer].nested_type.add()
+            m.name = inner
+        else:
+            m = fd.message_type.add()
+            m.name = mname
+            tops[mname] = m
         oneofs: dict[str, int] = {}
         for spec in fields:
             fname, num, typ = spec[0], spec[1], spec[2]

@@ -12,6 +12,7 @@ EE middleware hooks for PII redaction and privacy opt-out.
 from __future__ import annotations
 
 import argparse
+import os
 import asyncio
 import json
 import logging
@@ -318,6 +319,12 @@ def main(argv=None):
     ap.add_argument("--audit-db", default="", help="EE: enable the audit log (SQLite path)")
     ap.add_argument("--audit-retention-days", type=int, default=0)
     ap.add_argument("--audit-hub", default="", help="EE: privacy-api URL to forward audit to")
+    ap.add_argument("--otlp-enabled", action="store_true",
+                    default=os.environ.get("OTLP_ENABLED", "").lower() == "true")
+    ap.add_argument("--otlp-grpc-port", type=int,
+                    default=int(os.environ.get("OTLP_GRPC_PORT", 4317)))
+    ap.add_argument("--otlp-http-port", type=int,
+                    default=int(os.environ.get("OTLP_HTTP_PORT", 4318)))
     a = ap.parse_args(argv)
     cold = ColdArchive(LocalBlobStore(a.cold_dir)) if a.cold_dir else None
     pub = None
@@ -353,6 +360,20 @@ def main(argv=None):
             task.cancel()
 
         app.cleanup_ctx.append(forward_loop)
+    if a.otlp_enabled:
+        async def otlp_servers(_app):
+            from .otlp import Transformer, build_otlp_app, serve_otlp_grpc
+
+            tr = Transformer(svc)
+            runner = web.AppRunner(build_otlp_app(tr))
+            await runner.setup()
+            await web.TCPSite(runner, "0.0.0.0", a.otlp_http_port).start()
+            grpc_srv, _ = await serve_otlp_grpc(tr, a.otlp_grpc_port)
+            yield
+            await grpc_srv.stop(1)
+            await runner.cleanup()
+
+        app.cleanup_ctx.append(otlp_servers)
     web.run_app(app, port=a.port)
 
 

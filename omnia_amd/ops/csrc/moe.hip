@@ -44,9 +44,12 @@ __global__ __launch_bounds__(256) void moe_topk_kernel(int* __restrict__ ids,
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= n_tok) return;
-  const float x = lane < E ? ld<T>(logits + (int64_t)t * E + lane) : -INFINITY;
+  float x = lane < E ? ld<T>(logits + (int64_t)t * E + lane) : -INFINITY;
+  if (!(x == x)) x = -INFINITY;  // NaN logits (e.g. a padded row) never win a slot
   const float m = wave_max(x);
-  const float p = lane < E ? __expf(x - m) : 0.f;
+  // an all -inf row (padding) routes uniformly instead of producing NaN weights
+  const bool flat = !(m > -INFINITY);
+  const float p = lane < E ? (flat ? 1.f : __expf(x - m)) : 0.f;
   const float total = wave_sum(p);
   bool taken = false;
   int my_slot = -1;
@@ -54,9 +57,10 @@ __global__ __launch_bounds__(256) void moe_topk_kernel(int* __restrict__ ids,
   for (int j = 0; j < k; ++j) {
     const float v = taken ? -INFINITY : x;
     const float vm = wave_max(v);
-    const uint64_t b = __ballot(v == vm && lane < E);
+    // only untaken experts compete, so every slot gets a distinct valid id in [0, E)
+    const uint64_t b = __ballot(!taken && v == vm && lane < E);
     const int first = __ffsll((unsigned long long)b) - 1;  // lowest index wins ties
-    const float pj = __expf(vm - m);
+    const float pj = flat ? 1.f : __expf(vm - m);
     if (lane == first) {
       taken = true;
       my_slot = j;

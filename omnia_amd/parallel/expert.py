@@ -104,6 +104,9 @@ class ExpertParallelMoE:
         k = self.k
         if ids is None:
             ids, wts = self.route(x)
+        # a slot index outside the send buffer would be an out-of-bounds device
+        # write; routing always yields [0, E), the clamp keeps it so for any input
+        ids = ids.clamp(0, self.n_experts - 1)
         cap = max(1, max(tokens, T) * k)
         slot = dispatch_slots(ids, self.e_local, self.ep, cap)         # [T*k]
         send = x.new_zeros(self.ep * cap, d)

@@ -27,6 +27,27 @@ def test_moe_topk_matches_reference(T, E, k):
     torch.testing.assert_close(w.cpu(), rw, atol=1e-5, rtol=1e-5)
 
 
+def test_moe_topk_nan_and_padding_rows_route_to_valid_distinct_experts():
+    """A NaN row (e.g. a padded decode row) or an all -inf row must still yield k
+    distinct ids in [0, E) and finite weights: the expert-parallel dispatch turns
+    ids into send-buffer slots, so a -1 there would be an out-of-bounds write."""
+    E, k = 8, 2
+    logits = torch.randn(6, E)
+    logits[1] = float("nan")
+    logits[2] = float("-inf")
+    logits[3, :5] = float("nan")  # partially NaN: the finite experts win
+    ids = torch.full((6, k), -7, dtype=torch.int32, device="cuda")
+    w = torch.empty(6, k, dtype=torch.float32, device="cuda")
+    ops.kernels().moe_topk(ids, w, logits.cuda(), k, True)
+    ids, w = ids.cpu(), w.cpu()
+    assert ((ids >= 0) & (ids < E)).all() and (ids[:, 0] != ids[:, 1]).all()
+    assert torch.isfinite(w).all()
+    assert set(ids[3].tolist()) <= {5, 6, 7}
+    torch.testing.assert_close(w[1], torch.full((k,), 1.0 / k))
+    rid, rw = ref.moe_route(logits[[0, 4, 5]], k)
+    assert torch.equal(ids[[0, 4, 5]], rid)
+
+
 @pytest.mark.parametrize("T,d,I,E,k,e_lo,e_n", [
     (1, 256, 256, 8, 2, 0, 8), (13, 512, 256, 8, 2, 0, 8), (256, 512, 512, 8, 2, 0, 8),
     (100, 256, 256, 8, 2, 4, 4),  # expert-parallel shard: experts 4..7 only

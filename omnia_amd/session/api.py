@@ -314,6 +314,13 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=8300)
     ap.add_argument("--db", default=":memory:")
     ap.add_argument("--cold-dir", default="")
+    # cmd/session-api/main.go:120-155: object-store cold archive (env fallbacks)
+    ap.add_argument("--cold-backend", default=os.environ.get("COLD_BACKEND", ""),
+                    help="s3 | gcs | azure")
+    ap.add_argument("--cold-bucket", default=os.environ.get("COLD_BUCKET", ""))
+    ap.add_argument("--cold-region", default=os.environ.get("COLD_REGION", ""))
+    ap.add_argument("--cold-endpoint", default=os.environ.get("COLD_ENDPOINT", ""))
+    ap.add_argument("--cold-prefix", default=os.environ.get("COLD_PREFIX", "sessions/"))
     ap.add_argument("--redis-url", default="")
     ap.add_argument("--ttl", type=float, default=24 * 3600)
     ap.add_argument("--audit-db", default="", help="EE: enable the audit log (SQLite path)")
@@ -327,6 +334,11 @@ def main(argv=None):
                     default=int(os.environ.get("OTLP_HTTP_PORT", 4318)))
     a = ap.parse_args(argv)
     cold = ColdArchive(LocalBlobStore(a.cold_dir)) if a.cold_dir else None
+    if a.cold_backend and a.cold_bucket:
+        from .blobstores import build_cold_blobstore
+
+        cold = ColdArchive(build_cold_blobstore(a.cold_backend, a.cold_bucket, a.cold_region,
+                                                a.cold_endpoint, a.cold_prefix))
     pub = None
     if a.redis_url:
         from ..utils.resp import RedisClient

@@ -344,7 +344,18 @@ def main(argv=None):
         from ..utils.resp import RedisClient
 
         pub = StreamPublisher(RedisClient(a.redis_url))
-    svc = TieredSessionService(HotCache(), WarmStore(a.db), cold, a.ttl, pub)
+    if a.db.startswith(("postgres://", "postgresql://")):
+        warm = WarmStore.postgres(a.db)  # weekly-partitioned tables (sqldialect.py)
+        from .sqldialect import PartitionManager
+
+        def _pg(sql):
+            with warm.lock:
+                return warm._run(sql, ())
+
+        PartitionManager(_pg, warm.d).ensure_ahead(2)
+    else:
+        warm = WarmStore(a.db)
+    svc = TieredSessionService(HotCache(), warm, cold, a.ttl, pub)
     audit_logger = None
     app_kw = {}
     if a.audit_db:

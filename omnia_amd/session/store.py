@@ -1,7 +1,8 @@
 """Tiered session storage: hot -> warm -> cold (``internal/session/providers``).
 
   hot   in-process LRU with TTL, or Redis (RESP) -- recent sessions + messages
-  warm  SQLite (stand-in for the reference's partitioned Postgres tables)
+  warm  SQL over a dialect (:mod:`.sqldialect`): SQLite in-process, or the
+        reference's weekly-partitioned Postgres tables when a driver is present
   cold  Parquet files (pyarrow) in a blob store (local dir / memory), one file
         per archived batch plus a JSON manifest (``cold/provider.go``)
 
@@ -80,56 +81,62 @@ class HotCache:
 
 
 # ===================================================================== warm
-_SCHEMA = """
-CREATE TABLE IF NOT EXISTS sessions (id TEXT PRIMARY KEY, namespace TEXT, agent TEXT,
-    workspace TEXT, status TEXT, created REAL, updated REAL, expires REAL, user TEXT,
-    doc TEXT);
-CREATE INDEX IF NOT EXISTS sessions_ns ON sessions(namespace, agent, created);
-CREATE TABLE IF NOT EXISTS messages (id TEXT PRIMARY KEY, session_id TEXT, seq INTEGER,
-    ts REAL, role TEXT, content TEXT, doc TEXT);
-CREATE INDEX IF NOT EXISTS messages_sid ON messages(session_id, seq);
-CREATE TABLE IF NOT EXISTS tool_calls (id TEXT PRIMARY KEY, session_id TEXT, created REAL,
-    name TEXT, status TEXT, doc TEXT);
-CREATE TABLE IF NOT EXISTS provider_calls (id TEXT PRIMARY KEY, session_id TEXT,
-    created REAL, provider TEXT, model TEXT, input INTEGER, output INTEGER, cost REAL,
-    doc TEXT);
-CREATE TABLE IF NOT EXISTS events (id TEXT PRIMARY KEY, session_id TEXT, created REAL,
-    type TEXT, doc TEXT);
-CREATE TABLE IF NOT EXISTS eval_results (id TEXT PRIMARY KEY, session_id TEXT,
-    created REAL, eval_id TEXT, passed INTEGER, score REAL, doc TEXT);
-CREATE TABLE IF NOT EXISTS provider_usage (id INTEGER PRIMARY KEY AUTOINCREMENT,
-    workspace TEXT, created REAL, doc TEXT);
-"""
-
-
 class WarmStore:
-    def __init__(self, path: str = ":memory:"):
-        self.db = sqlite3.connect(path, check_same_thread=False)
-        self.db.executescript(_SCHEMA)
+    """The warm tier over a DB-API connection and a SQL dialect
+    (:mod:`.sqldialect`): SQLite by default, Postgres with weekly partitions when
+    a driver and DSN are given (:meth:`postgres`)."""
+
+    def __init__(self, path: str = ":memory:", dialect=None, conn=None, schema_dialect=None):
+        from .sqldialect import SQLiteDialect
+
+        self.d = dialect or SQLiteDialect()
+        self.db = conn if conn is not None else sqlite3.connect(path, check_same_thread=False)
         self.lock = threading.Lock()
         self.fail = False
+        for stmt in (schema_dialect or self.d).schema():
+            self._run(stmt, ())
 
-    def _x(self, sql, args=(), many=False):
+    @classmethod
+    def postgres(cls, dsn: str) -> "WarmStore":
+        from .sqldialect import connect_postgres
+
+        conn, dialect = connect_postgres(dsn)
+        return cls(dialect=dialect, conn=conn)
+
+    def _run(self, sql, args):
+        cur = self.db.cursor()
+        try:
+            cur.execute(sql, tuple(args))
+            rows = cur.fetchall() if cur.description else []
+        finally:
+            cur.close()
+        self.db.commit()
+        return rows
+
+    def _x(self, sql, args=()):
         if self.fail:
             raise TierError("warm tier unavailable")
         with self.lock:
-            cur = self.db.executemany(sql, args) if many else self.db.execute(sql, args)
-            self.db.commit()
-            return cur.fetchall()
+            return self._run(self.d.q(sql), args)
+
+    def _upsert(self, table, args):
+        if self.fail:
+            raise TierError("warm tier unavailable")
+        with self.lock:
+            return self._run(self.d.upsert(table), args)
 
     def put_session(self, s: Session):
-        self._x("INSERT OR REPLACE INTO sessions VALUES (?,?,?,?,?,?,?,?,?,?)",
-                (s.id, s.namespace, s.agent_name, s.workspace_name, s.status, s.created_at,
-                 s.updated_at, s.expires_at, s.virtual_user_id, json.dumps(s.to_json())))
+        self._upsert("sessions", (s.id, s.namespace, s.agent_name, s.workspace_name, s.status,
+                                  s.created_at, s.updated_at, s.expires_at, s.virtual_user_id,
+                                  json.dumps(s.to_json())))
 
     def get_session(self, sid: str) -> Session | None:
         r = self._x("SELECT doc FROM sessions WHERE id=?", (sid,))
         return Session.from_json(json.loads(r[0][0])) if r else None
 
     def add_message(self, sid: str, m: Message):
-        self._x("INSERT OR REPLACE INTO messages VALUES (?,?,?,?,?,?,?)",
-                (m.id, sid, m.sequence_num, m.timestamp, m.role, m.content,
-                 json.dumps(m.to_json())))
+        self._upsert("messages", (m.id, sid, m.sequence_num, m.timestamp, m.role, m.content,
+                                  json.dumps(m.to_json())))
 
     def messages(self, sid: str, limit: int = 1000, offset: int = 0) -> list[Message]:
         r = self._x("SELECT doc FROM messages WHERE session_id=? ORDER BY seq, ts LIMIT ? "
@@ -139,19 +146,17 @@ class WarmStore:
     def add(self, table: str, obj, sid: str):
         d = obj.to_json()
         if table == "tool_calls":
-            self._x("INSERT OR REPLACE INTO tool_calls VALUES (?,?,?,?,?,?)",
-                    (obj.id, sid, obj.created_at, obj.name, obj.status, json.dumps(d)))
+            self._upsert("tool_calls", (obj.id, sid, obj.created_at, obj.name, obj.status,
+                                        json.dumps(d)))
         elif table == "provider_calls":
-            self._x("INSERT OR REPLACE INTO provider_calls VALUES (?,?,?,?,?,?,?,?,?)",
-                    (obj.id, sid, obj.created_at, obj.provider, obj.model, obj.input_tokens,
-                     obj.output_tokens, obj.cost_usd, json.dumps(d)))
+            self._upsert("provider_calls", (obj.id, sid, obj.created_at, obj.provider,
+                                            obj.model, obj.input_tokens, obj.output_tokens,
+                                            obj.cost_usd, json.dumps(d)))
         elif table == "events":
-            self._x("INSERT OR REPLACE INTO events VALUES (?,?,?,?,?)",
-                    (obj.id, sid, obj.created_at, obj.type, json.dumps(d)))
+            self._upsert("events", (obj.id, sid, obj.created_at, obj.type, json.dumps(d)))
         elif table == "eval_results":
-            self._x("INSERT OR REPLACE INTO eval_results VALUES (?,?,?,?,?,?,?)",
-                    (obj.id, sid, obj.created_at, obj.eval_id, int(obj.passed), obj.score,
-                     json.dumps(d)))
+            self._upsert("eval_results", (obj.id, sid, obj.created_at, obj.eval_id,
+                                          int(obj.passed), obj.score, json.dumps(d)))
 
     def list_rows(self, table: str, sid: str) -> list[dict]:
         return [json.loads(x[0]) for x in self._x(
@@ -162,7 +167,7 @@ class WarmStore:
         sql = "SELECT doc FROM sessions WHERE 1=1"
         args: list = []
         for col, v in (("namespace", namespace), ("agent", agent), ("status", status),
-                       ("user", user)):
+                       ('"user"', user)):
             if v:
                 sql += f" AND {col}=?"
                 args.append(v)

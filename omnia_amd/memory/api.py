@@ -577,6 +577,8 @@ def main(argv=None):
     ap.add_argument("--ingest-chunk-overlap", type=int, default=40)
     ap.add_argument("--redis", default="", help="host:port for omnia:memory-events streams")
     ap.add_argument("--reembed-interval", type=float, default=5.0)
+    ap.add_argument("--policy-file", default="",
+                    help="MemoryPolicy spec (JSON; the operator's memory-policy-<name> ConfigMap)")
     a = ap.parse_args(argv)
     from .embedding import build_embedder
     from .store import MemoryStore
@@ -588,18 +590,22 @@ def main(argv=None):
     if a.redis:
         from ..utils.resp import RedisClient
 
-        host, _, port = a.redis.partition(":")
-        rc = RedisClient(host, int(port or 6379))
+        url = a.redis if "://" in a.redis else f"redis://{a.redis}"
+        rc = RedisClient(url)
 
         async def pub(stream, ev):
             await rc.xadd(stream, {"event": json.dumps(ev)}, maxlen=100_000)
 
+    policy = None
+    if a.policy_file:
+        with open(a.policy_file) as f:
+            policy = json.load(f)
     svc = MemoryService(MemoryStore(a.db), emb, publisher=pub, enterprise=a.enterprise)
     app = build_app(svc, a.enterprise, a.ingest_chunk_size, a.ingest_chunk_overlap)
 
     async def start_workers(app):
         app["workers"] = [asyncio.create_task(ReembedWorker(svc, a.reembed_interval).run()),
-                          asyncio.create_task(RetentionWorker(svc).run())]
+                          asyncio.create_task(RetentionWorker(svc, policy=policy).run())]
 
     async def stop_workers(app):
         for t in app.get("workers", []):

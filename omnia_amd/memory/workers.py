@@ -42,10 +42,25 @@ class ReembedWorker:
 
 
 class RetentionWorker:
-    def __init__(self, svc, interval: float = 300.0, forgotten_grace_s: float = 30 * 86400):
+    """``policy``: a MemoryPolicy spec (the operator's ``memory-policy-<name>``
+    ConfigMap); its tier rules run first (:mod:`.retention`), then expiry and the
+    purge of rows forgotten longer than the soft-delete grace."""
+
+    def __init__(self, svc, interval: float = 300.0, forgotten_grace_s: float = 30 * 86400,
+                 policy: dict | None = None):
         self.svc, self.interval, self.grace = svc, interval, forgotten_grace_s
+        self.policy = policy
+        self.last_stats: dict = {}
+        if policy:
+            from .retention import grace_seconds
+
+            self.grace = grace_seconds(policy, forgotten_grace_s / 86400.0)
 
     def run_once(self) -> int:
+        if self.policy:
+            from .retention import apply_memory_policy
+
+            self.last_stats = apply_memory_policy(self.svc.store, self.policy)
         obs = self.svc.store.expire() + self.svc.store.purge_forgotten(self.grace)
         self.svc._drop_vectors(obs)
         return len(obs)

@@ -92,6 +92,9 @@ class APIStore:
         self.field_validation = field_validation
         self.warnings: list[str] = []  # last write's warnings (Warn mode pruning)
         self.compacted_rv = 0
+        # third-party API kinds this "cluster" serves, e.g. Istio's
+        # ("security.istio.io/v1", "AuthorizationPolicy") -- discovery stand-in
+        self.served: set[tuple[str, str]] = set()
 
     # ------------------------------------------------------------ helpers
     @staticmethod
@@ -101,6 +104,9 @@ class APIStore:
     def _next_rv(self) -> str:
         self.last_rv = next(self.rv)
         return str(self.last_rv)
+
+    def serves(self, api_version: str, kind: str) -> bool:
+        return kind in crds.KINDS or (api_version, kind) in self.served
 
     def current_rv(self) -> str:
         return str(self.last_rv)

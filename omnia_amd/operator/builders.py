@@ -54,7 +54,9 @@ def pod_labels(ar: dict, track: str = "stable") -> dict:
             LABEL_COMPONENT: "agent", LABEL_MODE: ar["spec"].get("mode", "agent")}
 
 
-def tools_configmap(ar: dict, registry: dict | None) -> dict:
+def tools_configmap(ar: dict, registry: dict | None, tool_access: list | None = None) -> dict:
+    """The runtime's tool config: the registry's handlers, the registry name and
+    the compiled AgentPolicy tool access (``operator/policies.py``)."""
     handlers = []
     for h in (registry or {}).get("spec", {}).get("handlers", []):
         e = {k: v for k, v in h.items() if k in ("name", "type", "endpoint", "tool", "httpConfig",
@@ -65,7 +67,10 @@ def tools_configmap(ar: dict, registry: dict | None) -> dict:
             "metadata": {"name": ar["metadata"]["name"] + "-tools",
                          "namespace": ar["metadata"]["namespace"],
                          "labels": pod_labels(ar), "ownerReferences": [owner_ref(ar)]},
-            "data": {"tools.yaml": yaml.safe_dump({"handlers": handlers}, sort_keys=True)}}
+            "data": {"tools.yaml": yaml.safe_dump(
+                {"handlers": handlers,
+                 **({"registry": registry["metadata"]["name"]} if registry else {}),
+                 **({"toolAccess": tool_access} if tool_access else {})}, sort_keys=True)}}
 
 
 def runtime_config(ar: dict, pack: dict, providers: list[dict], registry: dict | None) -> RuntimeConfig:

@@ -11,6 +11,8 @@ import json
 import logging
 import time
 
+import yaml
+
 from ..api import crds
 from ..models.config import REGISTRY as MODEL_REGISTRY
 from ..runtime.promptpack import PackError, PromptPack
@@ -430,7 +432,10 @@ class AgentRuntimeReconciler:
         if self.cfg.policy_broker_image:
             sidecars.append(SR.policy_broker_container(ar, self.cfg))
             rc.policy_broker_url = f"http://127.0.0.1:{SR.POLICY_BROKER_PORT}"
-        store.apply(B.tools_configmap(ar, registry))
+        from .policies import compile_tool_access
+
+        store.apply(B.tools_configmap(ar, registry, compile_tool_access(
+            store.list("AgentPolicy", ns), name)))
         pack_cm = pack["spec"]["source"].get("configMapRef", {}).get("name", "")
         a = ((spec.get("runtime") or {}).get("autoscaling") or {})
         if a.get("enabled") and replicas is None:
@@ -664,6 +669,33 @@ class WorkspaceReconciler:
                 redis = (cfg.get("redis") or sg.get("redis") or {}).get("url")
                 if redis:
                     args += ["--redis-url" if svc == "session-api" else "--redis", redis]
+                volumes, mounts = [], []
+                pref = (cfg.get("policyRef") or {}).get("name")
+                if pref:
+                    # the cluster-scoped policy, copied next to the service so the pod
+                    # can mount it (the operator's own copy lives in its namespace)
+                    pkind = "SessionRetentionPolicy" if svc == "session-api" \
+                        else "MemoryPolicy"
+                    pol = store.try_get(pkind, pref, None)
+                    if pol is not None:
+                        if svc == "session-api":
+                            from .policies import resolved_retention
+
+                            fname, body = "retention.yaml", yaml.safe_dump(
+                                resolved_retention(pol["spec"]), sort_keys=True)
+                            args += ["--retention-config", f"/etc/omnia/policy/{fname}"]
+                        else:
+                            fname, body = "policy.json", json.dumps(pol["spec"],
+                                                                    sort_keys=True)
+                            args += ["--policy-file", f"/etc/omnia/policy/{fname}"]
+                        store.apply({"apiVersion": "v1", "kind": "ConfigMap",
+                                     "metadata": {"name": f"{dn}-policy", "namespace": nsname,
+                                                  "ownerReferences": own},
+                                     "data": {fname: body}})
+                        volumes = [{"name": "policy",
+                                    "configMap": {"name": f"{dn}-policy"}}]
+                        mounts = [{"name": "policy", "mountPath": "/etc/omnia/policy",
+                                   "readOnly": True}]
                 store.apply({"apiVersion": "apps/v1", "kind": "Deployment",
                              "metadata": {"name": dn, "namespace": nsname,
                                           "labels": {"omnia.altairalabs.ai/component": svc,
@@ -678,9 +710,11 @@ class WorkspaceReconciler:
                                                        "command": cmd[:3], "args": args,
                                                        "ports": [{"name": "http",
                                                                   "containerPort": 8080}],
+                                                       "volumeMounts": mounts,
                                                        "readinessProbe": {"httpGet": {
                                                            "path": "/healthz",
-                                                           "port": 8080}}}]}}}})
+                                                           "port": 8080}}}],
+                                                       "volumes": volumes}}}})
                 store.apply({"apiVersion": "v1", "kind": "Service",
                              "metadata": {"name": dn, "namespace": nsname,
                                           "ownerReferences": own},
@@ -710,8 +744,10 @@ class WorkspaceReconciler:
 
 # ===================================================================== policies
 class SimplePolicyReconciler:
-    """AgentPolicy / ToolPolicy / MemoryPolicy / SessionRetentionPolicy /
-    SkillSource / Arena*: admission already validated; mark Active and count."""
+    """ToolPolicy (enforced by the policy broker) / SessionPrivacyPolicy /
+    RolloutAnalysis / ArenaDevSession: admission already validated; mark Active
+    and count.  AgentPolicy / MemoryPolicy / SessionRetentionPolicy have their
+    own reconcilers (``operator/policies.py``)."""
 
     def __init__(self, kind: str):
         self.kind = kind
@@ -746,8 +782,12 @@ def default_reconcilers(gpu_count: int | None = None,
     rs = [PromptPackReconciler(), ProviderReconciler(gpu_count, cfg),
           ToolRegistryReconciler(cfg), AgentRuntimeReconciler(gpu_count, cfg),
           WorkspaceReconciler()]
-    for k in ("AgentPolicy", "ToolPolicy", "MemoryPolicy", "SessionRetentionPolicy",
-              "SessionPrivacyPolicy", "RolloutAnalysis", "ArenaDevSession"):
+    from .policies import (AgentPolicyReconciler, MemoryPolicyReconciler,
+                           SessionRetentionPolicyReconciler)
+
+    rs += [AgentPolicyReconciler(cfg.istio), MemoryPolicyReconciler(cfg.namespace),
+           SessionRetentionPolicyReconciler(cfg.namespace)]
+    for k in ("ToolPolicy", "SessionPrivacyPolicy", "RolloutAnalysis", "ArenaDevSession"):
         rs.append(SimplePolicyReconciler(k))
     from .sourcesync import SourceReconciler
 

@@ -298,6 +298,19 @@ class KubeClient:
         obj.setdefault("apiVersion", gv)
         return obj
 
+    def serves(self, api_version: str, kind: str) -> bool:
+        """API discovery: is ``kind`` served under ``api_version`` (cached)?"""
+        cache = self.__dict__.setdefault("_served", {})
+        key = (api_version, kind)
+        if key not in cache:
+            path = ("/api/" if "/" not in api_version else "/apis/") + api_version
+            try:
+                doc = self._request("GET", path)
+                cache[key] = any(r.get("kind") == kind for r in doc.get("resources", []))
+            except Exception:  # noqa: BLE001 - 404: group/version not installed
+                cache[key] = False
+        return cache[key]
+
     def get(self, kind: str, name: str, ns: str | None = "default") -> dict:
         return self._with_type(kind, self._request("GET", resource_path(kind, ns, name)))
 

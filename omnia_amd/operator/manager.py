@@ -159,6 +159,11 @@ class Manager:
                     hit = True
                 if hit:
                     self.enqueue("AgentRuntime", ns, ar["metadata"]["name"])
+        if kind == "AgentPolicy":  # the matched agents' tool config carries the policy
+            sel = set(((obj.get("spec") or {}).get("selector") or {}).get("agents") or [])
+            for ar in self.store.list("AgentRuntime", ns):
+                if not sel or ar["metadata"]["name"] in sel:
+                    self.enqueue("AgentRuntime", ns, ar["metadata"]["name"])
         if kind == "ConfigMap":
             for pp in self.store.list("PromptPack", ns):
                 if (pp["spec"]["source"].get("configMapRef") or {}).get("name") == md["name"]:

@@ -94,6 +94,8 @@ class OperatorConfig:
     eval_worker_image: str = "ghcr.io/omnia-mi355x/omnia-eval-worker:latest"
     workspace_reader_rbac: bool = False
     session_redis_url: str = ""
+    namespace: str = "omnia-system"  # the operator's own namespace (policy ConfigMaps)
+    istio: bool | None = None  # None: discover AuthorizationPolicy support from the API
     http_get: object = field(default=_http_get, repr=False)  # (url, timeout) -> (status, body)
     clock: object = field(default=time.time, repr=False)
     dial: object = field(default=None, repr=False)  # (host, port, timeout) -> None | raises
@@ -111,7 +113,11 @@ class OperatorConfig:
                                            cls.eval_worker_image),
                    workspace_reader_rbac=e.get("OMNIA_WORKSPACE_READER_RBAC", "").lower()
                    in ("1", "true"),
-                   session_redis_url=e.get("OMNIA_SESSION_REDIS_URL", ""))
+                   session_redis_url=e.get("OMNIA_SESSION_REDIS_URL", ""),
+                   namespace=e.get("POD_NAMESPACE", "") or e.get("OMNIA_OPERATOR_NAMESPACE",
+                                                                 "omnia-system"),
+                   istio={"true": True, "1": True, "false": False, "0": False}.get(
+                       e.get("OMNIA_ISTIO_ENABLED", "").lower()))
 
     @property
     def exposure_configured(self) -> bool:

@@ -326,6 +326,10 @@ def main(argv=None):
     ap.add_argument("--audit-db", default="", help="EE: enable the audit log (SQLite path)")
     ap.add_argument("--audit-retention-days", type=int, default=0)
     ap.add_argument("--audit-hub", default="", help="EE: privacy-api URL to forward audit to")
+    ap.add_argument("--retention-config", default="",
+                    help="retention.yaml of a SessionRetentionPolicy: hot-cache sizing and "
+                         "an in-process compaction loop with its warm/cold retention")
+    ap.add_argument("--compaction-interval", type=float, default=3600.0)
     ap.add_argument("--otlp-enabled", action="store_true",
                     default=os.environ.get("OTLP_ENABLED", "").lower() == "true")
     ap.add_argument("--otlp-grpc-port", type=int,
@@ -355,7 +359,18 @@ def main(argv=None):
         PartitionManager(_pg, warm.d).ensure_ahead(2)
     else:
         warm = WarmStore(a.db)
-    svc = TieredSessionService(HotCache(), warm, cold, a.ttl, pub)
+    retention = {}
+    if a.retention_config:
+        import yaml
+
+        from ..operator.policies import retention_from_config
+
+        with open(a.retention_config) as f:
+            retention = retention_from_config(yaml.safe_load(f) or {})
+    hot = HotCache(max_sessions=retention.get("hot_max_sessions", 10000),
+                   ttl_s=retention.get("hot_ttl_s", 3600),
+                   max_messages=retention.get("hot_max_messages", 200))
+    svc = TieredSessionService(hot, warm, cold, a.ttl, pub)
     audit_logger = None
     app_kw = {}
     if a.audit_db:
@@ -383,6 +398,27 @@ def main(argv=None):
             task.cancel()
 
         app.cleanup_ctx.append(forward_loop)
+    if retention:
+        async def compaction_loop(_app):
+            from .compaction import CompactionConfig, CompactionEngine
+
+            eng = CompactionEngine(warm, cold, hot, CompactionConfig(
+                retention.get("warm_retention_s", 7 * 86400),
+                retention.get("cold_retention_s", 365 * 86400)))
+
+            async def loop():
+                while True:
+                    await asyncio.sleep(a.compaction_interval)
+                    try:
+                        await asyncio.to_thread(eng.run)
+                    except Exception as e:  # noqa: BLE001
+                        logging.getLogger("omnia.session").warning("compaction failed: %s", e)
+
+            task = asyncio.create_task(loop())
+            yield
+            task.cancel()
+
+        app.cleanup_ctx.append(compaction_loop)
     if a.otlp_enabled:
         async def otlp_servers(_app):
             from .otlp import Transformer, build_otlp_app, serve_otlp_grpc

@@ -110,10 +110,22 @@ def main(argv=None):
     ap.add_argument("--warm-retention", type=float, default=7 * 86400)
     ap.add_argument("--cold-retention", type=float, default=365 * 86400)
     ap.add_argument("--dry-run", action="store_true")
+    ap.add_argument("--retention-config", default="",
+                    help="retention.yaml of a SessionRetentionPolicy (operator ConfigMap "
+                         "retention-policy-<name>); overrides the two retention flags")
     a = ap.parse_args(argv)
+    warm_s, cold_s = a.warm_retention, a.cold_retention
+    if a.retention_config:
+        import yaml
+
+        from ..operator.policies import retention_from_config
+
+        with open(a.retention_config) as f:
+            r = retention_from_config(yaml.safe_load(f) or {})
+        warm_s, cold_s = r.get("warm_retention_s", warm_s), r.get("cold_retention_s", cold_s)
     cold = ColdArchive(LocalBlobStore(a.cold_dir)) if a.cold_dir else None
     eng = CompactionEngine(WarmStore(a.db), cold, None, CompactionConfig(
-        a.warm_retention, a.cold_retention, dry_run=a.dry_run))
+        warm_s, cold_s, dry_run=a.dry_run))
     print(eng.run())
 
 

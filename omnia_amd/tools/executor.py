@@ -590,6 +590,50 @@ class PolicyBrokerClient:
         return d
 
 
+# ===================================================================== AgentPolicy
+class ToolAccess:
+    """In-node enforcement of the AgentPolicies selecting this agent
+    (compiled by ``operator/policies.compile_tool_access``; the mesh form is the
+    Istio AuthorizationPolicies keyed on ``X-Omnia-Tool-Name: registry/tool``).
+
+    Enforcing policies: a denylist match denies; when any allowlist applies, a
+    tool must match one of them.  Permissive policies evaluate the same way but
+    only record the decision (audit).  Tools outside the agent's ToolRegistry
+    (skills, memory tools, workflow tools) are not registry tools and are not
+    subject to tool-access rules, as in the reference."""
+
+    def __init__(self, policies: list[dict] | None, registry: str = ""):
+        self.policies = list(policies or [])
+        self.registry = registry
+        self.audit: list[dict] = []
+
+    @staticmethod
+    def _decide(policies, key: str):
+        allow_lists = [p for p in policies if p["mode"] == "allowlist"]
+        for p in policies:
+            if p["mode"] == "denylist" and any(key in {f"{r['registry']}/{t}" for t in r["tools"]}
+                                               for r in p["rules"]):
+                return False, p["policy"]
+        if allow_lists and not any(key in {f"{r['registry']}/{t}" for t in r["tools"]}
+                                   for p in allow_lists for r in p["rules"]):
+            return False, allow_lists[0]["policy"]
+        return True, ""
+
+    def check(self, tool: str) -> tuple[bool, str]:
+        if not self.policies or not self.registry:
+            return True, ""
+        key = f"{self.registry}/{tool}"
+        ok, by = self._decide([p for p in self.policies if p.get("enforce", True)], key)
+        if not ok:
+            M.TOOLPOLICY_DECISIONS.labels("deny").inc()
+            return False, by
+        would, pby = self._decide([p for p in self.policies if not p.get("enforce", True)], key)
+        if not would:  # permissive: audit only
+            self.audit.append({"tool": key, "policy": pby, "decision": "would-deny"})
+            log.info("AgentPolicy %s (permissive) would deny tool %s", pby, key)
+        return True, ""
+
+
 # ===================================================================== executor
 class OmniaExecutor:
     def __init__(self, config: dict | None = None, secrets_dir: str | None = None,
@@ -610,6 +654,9 @@ class OmniaExecutor:
             self.handlers[e["name"]] = cls(e, secrets_dir)
         self._client_cfg = {e["name"]: e.get("clientConfig") or {}
                             for e in (config or {}).get("handlers", []) if e.get("type") == "client"}
+        self.registry_handlers = {e["name"] for e in (config or {}).get("handlers", [])}
+        self.access = ToolAccess((config or {}).get("toolAccess"),
+                                 (config or {}).get("registry", ""))
 
     def add_handler(self, h: Handler):
         self.handlers[h.name] = h
@@ -645,6 +692,11 @@ class OmniaExecutor:
         t0 = time.perf_counter()
         status = "ok"
         try:
+            if tool.handler in self.registry_handlers:
+                ok, by = self.access.check(name)
+                if not ok:
+                    raise PolicyDenied(f"tool {self.access.registry}/{name} denied by "
+                                       f"AgentPolicy {by}")
             if self.policy is not None:
                 d = await self.policy.decide(tool, args, ctx)
                 if not d.get("allow"):

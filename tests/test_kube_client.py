@@ -268,7 +268,7 @@ def test_manager_reconciles_through_kube_client(srv):
             for d in docs:
                 await asyncio.to_thread(c.apply, d)
             ar = None
-            for _ in range(100):
+            for _ in range(300):  # generous: reconciles go through HTTP on a loaded box
                 await asyncio.sleep(0.1)
                 ar = srv.store.try_get("AgentRuntime", "echo", "default")
                 dep = srv.store.try_get("Deployment", "echo", "default")
@@ -283,7 +283,7 @@ def test_manager_reconciles_through_kube_client(srv):
             cur = await asyncio.to_thread(c.get, "AgentRuntime", "echo", "default")
             cur["spec"]["runtime"] = {"replicas": 3}
             await asyncio.to_thread(c.update, cur)
-            for _ in range(100):
+            for _ in range(300):
                 await asyncio.sleep(0.1)
                 if srv.store.get("Deployment", "echo", "default")["spec"]["replicas"] == 3:
                     break

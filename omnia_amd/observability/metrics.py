@@ -55,6 +55,19 @@ REALTIME_DRAINED = Counter("omnia_facade_realtime_calls_drained_total",
                            "Realtime calls that finished during drain", registry=REGISTRY)
 REALTIME_FORCE_ENDED = Counter("omnia_facade_realtime_calls_force_ended_total",
                                "Realtime calls still live when drain ended", registry=REGISTRY)
+# canary rollouts (internal/controller/rollout_metrics.go:22-28)
+ROLLOUT_ACTIVE = Gauge("omnia_rollout_active", "1 while a rollout is in flight",
+                       ["namespace", "agent"], registry=REGISTRY)
+ROLLOUT_STEPS = Counter("omnia_rollout_step_transitions_total", "Rollout step transitions",
+                        ["namespace", "agent", "step_type"], registry=REGISTRY)
+ROLLOUT_PROMOTIONS = Counter("omnia_rollout_promotions_total", "Rollout promotions",
+                             ["namespace", "agent"], registry=REGISTRY)
+ROLLOUT_ROLLBACKS = Counter("omnia_rollout_rollbacks_total", "Rollout rollbacks",
+                            ["namespace", "agent", "reason"], registry=REGISTRY)
+ROLLOUT_WEIGHT = Gauge("omnia_rollout_traffic_weight", "Traffic weight per track",
+                       ["namespace", "agent", "track"], registry=REGISTRY)
+ROLLOUT_ANALYSIS = Counter("omnia_rollout_analysis_runs_total", "Rollout analysis runs",
+                           ["namespace", "agent", "template", "outcome"], registry=REGISTRY)
 A2A_REQUESTS = Counter("omnia_a2a_requests_total", "A2A JSON-RPC requests", ["method", "status"],
                        registry=REGISTRY)
 MCP_REQUESTS = Counter("omnia_mcp_requests_total", "MCP requests", ["method", "status"],

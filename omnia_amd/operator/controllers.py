@@ -323,9 +323,11 @@ def workspace_service_group(store: APIStore, ns: str, group: str) -> dict | None
 class AgentRuntimeReconciler:
     kind = "AgentRuntime"
 
-    def __init__(self, gpu_count: int | None = None, cfg: SR.OperatorConfig | None = None):
+    def __init__(self, gpu_count: int | None = None, cfg: SR.OperatorConfig | None = None,
+                 rollout_engine=None):
         self.gpu_count = gpu_count
         self.cfg = cfg or SR.OperatorConfig.from_env()
+        self.rollout_engine = rollout_engine  # injectable clock / HTTP for tests
 
     def _fail(self, store, ar, st, cond, reason, msg, phase=PENDING):
         set_condition(st, cond, False, reason, msg, ar["metadata"]["generation"])
@@ -512,95 +514,15 @@ class AgentRuntimeReconciler:
 
     # ---------------------------------------------------------------- rollout
     def _rollout(self, store, ar, st, rc, pack_cm, pack):
-        """Canary rollout (``internal/controller/rollout.go:73-851``): candidate
-        Deployment + setWeight/pause/analysis steps; promote on completion,
-        roll back on a failed analysis."""
-        spec, md = ar["spec"], ar["metadata"]
-        ro = spec.get("rollout") or {}
-        ns, name = md["namespace"], md["name"]
-        cand_spec = ro.get("candidate")
-        if not cand_spec:
-            store.delete("Deployment", name + "-candidate", ns)
-            if st.get("rollout"):
-                st.pop("rollout")
-            set_condition(st, "RolloutActive", False, "NoRollout", "", md["generation"])
-            return None
-        ros = st.get("rollout") or {"currentStep": 0, "weight": 0, "phase": "Progressing",
-                                    "stepStarted": time.time()}
-        cand_ar = json.loads(json.dumps(ar))
-        # candidate overrides (rollout_types.go:71-91): a promptPackRef (pinned
-        # version or track), provider refs and/or a tool registry
-        if cand_spec.get("promptPackRef"):
-            cand_ar["spec"]["promptPackRef"] = dict(cand_spec["promptPackRef"])
-        if cand_spec.get("providerRefs"):
-            cand_ar["spec"]["providers"] = list(cand_spec["providerRefs"])
-        if cand_spec.get("toolRegistryRef"):
-            cand_ar["spec"]["toolRegistryRef"] = dict(cand_spec["toolRegistryRef"])
-        cand_pack = resolve_promptpack(store, ns, cand_ar["spec"]["promptPackRef"]) or pack
-        steps = ro.get("steps") or [{"setWeight": 100}]
-        if ros["phase"] == "Progressing":
-            store.apply(B.deployment(cand_ar, rc, cand_pack["spec"]["source"]["configMapRef"][
-                "name"], "candidate", 1, extra_hash=[cand_pack["spec"]["version"]]))
-            i = ros["currentStep"]
-            if i >= len(steps):
-                ros["phase"] = "Promoted"
-                ros["weight"] = 100
-                ros["promotedVersion"] = cand_pack["spec"]["version"]
-            else:
-                stp = steps[i]
-                if "setWeight" in stp:
-                    ros["weight"] = stp["setWeight"]
-                    ros["currentStep"] = i + 1
-                    ros["stepStarted"] = time.time()
-                elif "pause" in stp:
-                    from ..runtime.context_store import parse_ttl
+        """Canary rollout engine (:mod:`.rollout`, ``internal/controller/
+        rollout.go:73-851``)."""
+        from .rollout import RolloutEngine
 
-                    dur = parse_ttl((stp["pause"] or {}).get("duration", "0s")) or 0
-                    if time.time() - ros["stepStarted"] >= dur:
-                        ros["currentStep"] = i + 1
-                        ros["stepStarted"] = time.time()
-                elif "analysis" in stp:
-                    verdict = self._analysis(store, ns, stp["analysis"])
-                    if verdict is False:
-                        ros["phase"] = "RolledBack"
-                        ros["weight"] = 0
-                    elif verdict is True:
-                        ros["currentStep"] = i + 1
-                        ros["stepStarted"] = time.time()
-        if ros["phase"] == "Promoted":
-            store.delete("Deployment", name + "-candidate", ns)
-        if ros["phase"] == "RolledBack" and (ro.get("rollback") or {}).get("mode",
-                                                                            "automatic") != "manual":
-            store.delete("Deployment", name + "-candidate", ns)
-        st["rollout"] = ros
-        active = ros["phase"] == "Progressing"
-        from . import rollout_routing
-
-        traffic = rollout_routing.apply(store, ar, int(ros["weight"]), active)
-        ros["traffic"] = traffic
-        if traffic["trafficRoutingMode"] == "replica-weighted" and active:
-            cand = store.try_get("Deployment", name + "-candidate", ns)
-            if cand is not None and cand["spec"].get("replicas") != traffic["candidateReplicas"]:
-                cand["spec"]["replicas"] = traffic["candidateReplicas"]
-                store.apply(cand)
-        set_condition(st, "RolloutActive", active, ros["phase"], f"weight={ros['weight']}",
-                      md["generation"])
-        set_condition(st, "TrafficRouting", not traffic.get("degraded"),
-                      {"mesh": "MeshWeighted", "external": "IstioPatched"}.get(
-                          traffic["trafficRoutingMode"], "ReplicaWeighted"),
-                      f"candidate={traffic['deliveredWeight']}%", md["generation"])
-        return 1.0 if active else None
-
-    def _analysis(self, store, ns, a):
-        ra = store.try_get("RolloutAnalysis", (a or {}).get("templateName", ""), ns)
-        if ra is None:
-            return None
-        res = (ra.get("status") or {}).get("result")
-        if res == "Failed":
-            return False
-        if res == "Successful":
-            return True
-        return None
+        ns = ar["metadata"]["namespace"]
+        eng = self.rollout_engine or RolloutEngine()
+        return eng.reconcile(store, ar, st, rc, pack,
+                             lambda ref: resolve_promptpack(store, ns, ref),
+                             lambda pack_name: packs_for(store, ns, pack_name))
 
 
 # ===================================================================== Workspace

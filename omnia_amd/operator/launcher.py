@@ -188,7 +188,8 @@ class LocalLauncher:
                 self.services[key] = (sp, B.config_hash(d["spec"]["template"]))
             sp = self.services[key][0]
             st = d.get("status") or {}
-            if st.get("readyReplicas") != 1:
+            if st.get("readyReplicas") != 1 or \
+                    st.get("observedGeneration") != d["metadata"]["generation"]:
                 d["status"] = {**st, "replicas": 1, "readyReplicas": 1, "availableReplicas": 1,
                                "observedGeneration": d["metadata"]["generation"]}
                 d["metadata"].pop("resourceVersion", None)

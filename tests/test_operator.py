@@ -261,6 +261,25 @@ def test_workspace_reconcile():
     assert store.get("NetworkPolicy", "workspace-team-a-isolation", "team-a")
 
 
+def _fake_kubelet(store):
+    """Marks every Deployment rolled out (ready replicas, observed generation),
+    as the Deployment controller + kubelet would."""
+    async def loop():
+        while True:
+            for d in store.list("Deployment"):
+                st = d.get("status") or {}
+                want = d["spec"].get("replicas", 1)
+                if st.get("observedGeneration") != d["metadata"]["generation"] or \
+                        st.get("readyReplicas") != want:
+                    d["status"] = {"replicas": want, "readyReplicas": want,
+                                   "updatedReplicas": want, "availableReplicas": want,
+                                   "observedGeneration": d["metadata"]["generation"]}
+                    d["metadata"].pop("resourceVersion", None)
+                    store.update_status(d)
+            await asyncio.sleep(0.05)
+    return asyncio.ensure_future(loop())
+
+
 def test_canary_rollout_steps_and_promotion():
     docs = load_manifests([ECHO])
     for d in docs:
@@ -271,27 +290,39 @@ def test_canary_rollout_steps_and_promotion():
                                               {"setWeight": 100}]}
 
     async def go():
-        store, mgr, _ = await _run_operator(docs)
+        store = new_store()
+        kubelet = _fake_kubelet(store)
+        mgr = Manager(store)
+        await mgr.start()
+        for d in docs:
+            store.apply(d)
         seen = []
-        for _ in range(60):
+        for _ in range(100):
             c = store.try_get("Deployment", "echo-candidate")
             if c is not None:
                 seen.append(c["metadata"]["labels"]["omnia.altairalabs.ai/track"])
             ro = store.get("AgentRuntime", "echo")["status"].get("rollout") or {}
-            seen.append(ro.get("weight"))
-            if ro.get("phase") == "Promoted":
+            seen.append(ro.get("currentWeight"))
+            if ro.get("message") == "promoted":
                 break
             await asyncio.sleep(0.1)
         await mgr.settle(timeout=5)
         a = store.get("AgentRuntime", "echo")
         cand = store.try_get("Deployment", "echo-candidate")
+        events = [e["reason"] for e in store.list("Event")]
         await mgr.stop()
-        return a, cand, seen
+        kubelet.cancel()
+        return a, cand, seen, events
 
-    a, cand, seen = asyncio.run(go())
+    a, cand, seen, events = asyncio.run(go())
     assert "candidate" in seen and 20 in seen
-    assert a["status"]["rollout"]["phase"] == "Promoted" and a["status"]["rollout"]["weight"] == 100
+    ro = a["status"]["rollout"]
+    assert ro["active"] is False and ro["message"] == "promoted"
     assert cand is None  # candidate folded into stable after promotion
+    assert a["spec"]["promptPackRef"] == {"name": "echo-pack", "version": "1.0.0"}
+    assert "candidate" not in a["spec"]["rollout"]
+    for r in ("RolloutStep", "RolloutPromoting", "RolloutPromoted"):
+        assert r in events
 
 
 def test_rollout_traffic_routing_modes(monkeypatch):
@@ -331,7 +362,7 @@ def test_rollout_traffic_routing_modes(monkeypatch):
             store, mgr, _ = await _run_operator(docs + extra)
             for _ in range(60):
                 ro = store.get("AgentRuntime", "echo")["status"].get("rollout") or {}
-                if ro.get("weight") == 30 and ro.get("traffic"):
+                if ro.get("currentWeight") == 30 and ro.get("traffic"):
                     break
                 await asyncio.sleep(0.1)
             await mgr.settle(timeout=5)

@@ -64,6 +64,9 @@ class EngineConfig:
     # TP); "a2a" = data-parallel attention replicas + token all-to-all to the
     # experts' ranks, every rank stepping in lockstep (engine/ep.py)
     ep_mode: str = "tp"
+    # >0 (with WORLD_SIZE > 1, tp = 1): prompts of at least this many uncached
+    # tokens are prefilled context-parallel by the whole DP group (engine/cp.py)
+    cp_threshold: int = 0
 
     @classmethod
     def from_env(cls, **kw) -> "EngineConfig":
@@ -81,6 +84,7 @@ class EngineConfig:
             "OMNIA_ENGINE_USE_GRAPHS": ("use_graphs", lambda v: v.lower() != "false"),
             "OMNIA_ENGINE_MIXED_BUDGET": ("mixed_budget", int),
             "OMNIA_ENGINE_EP_MODE": ("ep_mode", str),
+            "OMNIA_ENGINE_CP_THRESHOLD": ("cp_threshold", int),
         }
         for k, (f, t) in m.items():
             if k in env:
@@ -121,7 +125,12 @@ class LLMEngine:
         runner_cls = ModelRunner
         # DP-attention + EP: every forward is a collective of the EP group
         self.ep_lockstep = cfg.ep_mode == "a2a" and st.world_size > 1
-        self._ep_active = 0
+        self._ep_active = 0  # any rank of the lockstep group still busy
+        self.cp_lockstep = (cfg.cp_threshold > 0 and st.world_size > 1 and st.tp_size == 1
+                            and not self.ep_lockstep)
+        self.lockstep = self.ep_lockstep or self.cp_lockstep
+        if self.cp_lockstep:
+            self._cp_desc = torch.zeros(st.dp_size + 1, dtype=torch.int64, device=dev)
         if self.ep_lockstep:
             from .ep import EPModelRunner
 
@@ -149,7 +158,8 @@ class LLMEngine:
                             max_model_len=cfg.max_model_len,
                             # mixed steps run on the TP-rank-0-only eager path: TP keeps
                             # separate prefill / decode steps
-                            mixed_budget=cfg.mixed_budget if self.model.tp == 1 else 0),
+                            mixed_budget=cfg.mixed_budget if self.model.tp == 1 else 0,
+                            cp_threshold=cfg.cp_threshold if self.cp_lockstep else 0),
             self.blocks)
         self.tokenizer = make_tokenizer(self.model_cfg, cfg.tokenizer)
         self.eos = set(self.tokenizer.eos_token_ids)
@@ -183,7 +193,8 @@ class LLMEngine:
         st = pstate.get_state()
         if cfg.tp > 1 and st.tp_size != cfg.tp:
             st = pstate.init_distributed(tp_size=cfg.tp, device=dev.type)
-        elif cfg.ep_mode == "a2a" and st.world_size == 1 and pstate.env_world()[0] > 1:
+        elif ((cfg.ep_mode == "a2a" or cfg.cp_threshold > 0) and st.world_size == 1
+              and pstate.env_world()[0] > 1):
             st = pstate.init_distributed(tp_size=1, device=dev.type)
         return st
 
@@ -253,6 +264,10 @@ class LLMEngine:
             from .ep import run_ep_step
 
             return run_ep_step(self)
+        if self.cp_lockstep:
+            from .cp import run_cp_step
+
+            return run_cp_step(self)
         if self.cfg.pipeline and self.runner.use_graphs:
             return self._step_pipelined()
         return self._step_sync()
@@ -493,7 +508,7 @@ class LLMEngine:
 
     def run_until_done(self, max_steps: int = 10**9) -> None:
         n = 0
-        if self.ep_lockstep:  # step until the whole EP group is idle
+        if self.lockstep:  # step until the whole EP / CP group is idle
             while n < max_steps:
                 self.step()
                 n += 1
@@ -514,8 +529,8 @@ class LLMEngine:
             for s in seqs:
                 if s.is_finished:
                     finished.add(s.seq_id)
-        if self.ep_lockstep:
-            self.run_until_done()  # keep serving the group's all-to-alls until all idle
+        if self.lockstep:
+            self.run_until_done()  # keep serving the group's collectives until all idle
         return seqs
 
 
@@ -635,7 +650,7 @@ class AsyncLLMEngine:
                     fn()
                 except Exception as e:  # surface to the submitter
                     log.exception("engine request failed: %s", e)
-            if eng.has_work() or eng.ep_lockstep:
+            if eng.has_work() or eng.lockstep:
                 self._step_t0 = time.monotonic()
                 try:
                     eng.step()
@@ -655,7 +670,7 @@ class AsyncLLMEngine:
                         self.healthy = False  # fault storm: stop advertising readiness
                 self._step_t0 = None
                 self._flush()
-                if eng.ep_lockstep and not eng._ep_active:
+                if eng.lockstep and not eng._ep_active:
                     self._wake.wait(0.001)  # group idle: keep the lockstep cadence cheap
                     self._wake.clear()
             else:

@@ -30,6 +30,9 @@ class SchedulerConfig:
     max_model_len: int = 8192
     prefill_chunk: int = 8192  # max new tokens of ONE sequence per prefill step
     mixed_budget: int = 0  # >0: co-schedule decode rows with <= this many prefill tokens
+    # >0: prompts with at least this many uncached tokens are held for a
+    # context-parallel prefill over the DP group (engine/cp.py)
+    cp_threshold: int = 0
 
 
 @dataclass
@@ -46,6 +49,7 @@ class Scheduler:
         self.waiting: deque[Sequence] = deque()
         self.running: list[Sequence] = []
         self.partial: list[Sequence] = []  # prompts mid-way through chunked prefill
+        self.cp_pending: Sequence | None = None  # admitted, waiting for its CP prefill
 
     # ------------------------------------------------------------ admission
     def add(self, seq: Sequence) -> None:
@@ -58,6 +62,12 @@ class Scheduler:
         self.waiting.append(seq)
 
     def abort(self, seq_id: int) -> Sequence | None:
+        if self.cp_pending is not None and self.cp_pending.seq_id == seq_id:
+            s, self.cp_pending = self.cp_pending, None
+            self._free(s, retain=False)
+            s.status = SeqStatus.FINISHED
+            s.finish_reason = FinishReason.ABORT
+            return s
         for q in (self.waiting, self.running, self.partial):
             for s in list(q):
                 if s.seq_id == seq_id:
@@ -69,11 +79,45 @@ class Scheduler:
         return None
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.running or self.partial)
+        return bool(self.waiting or self.running or self.partial or self.cp_pending)
 
     @property
     def num_active(self) -> int:
-        return len(self.running) + len(self.partial)
+        return len(self.running) + len(self.partial) + (self.cp_pending is not None)
+
+    # ------------------------------------------------------------ context parallel
+    def _cp_eligible(self, s: Sequence) -> bool:
+        thr = self.cfg.cp_threshold
+        return bool(thr) and s.num_cached == 0 and s.length >= thr and not getattr(
+            s, "cp_skip", False)
+
+    def cp_candidate(self) -> Sequence | None:
+        """The sequence this rank wants prefilled context-parallel (admitted with
+        pages for its whole prompt), or None.  Held until :meth:`cp_done`."""
+        if self.cp_pending is not None:
+            return self.cp_pending
+        if not self.cfg.cp_threshold or not self.waiting or self.num_active >= self.cfg.max_batch:
+            return None
+        s = self.waiting[0]
+        if s.num_cached == 0 and not s.blocks:
+            self._admit(s)
+        if not self._cp_eligible(s):
+            return None
+        try:
+            self._ensure_blocks(s, s.length + 1)
+        except OutOfBlocks:
+            s.cp_skip = True  # the ordinary chunked path preempts / fails it
+            return None
+        self.waiting.popleft()
+        s.status = SeqStatus.RUNNING
+        self.cp_pending = s
+        return s
+
+    def cp_done(self, s: Sequence, tok: int) -> list[tuple[Sequence, int]]:
+        self.cp_pending = None
+        s.num_cached = s.length
+        self.running.append(s)
+        return [(s, tok)]
 
     # ------------------------------------------------------------ KV helpers
     def _ensure_blocks(self, s: Sequence, upto_tokens: int) -> None:
@@ -146,6 +190,8 @@ class Scheduler:
             s = self.waiting[0]
             if s.num_cached == 0 and not s.blocks:
                 self._admit(s)
+            if self._cp_eligible(s):
+                break  # the next lockstep step prefills it context-parallel
             n = min(s.num_uncached, cfg.prefill_chunk, budget)
             try:
                 self._ensure_blocks(s, s.num_cached + n + (1 if n == s.num_uncached else 0))

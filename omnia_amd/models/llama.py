@@ -47,6 +47,10 @@ class ForwardBatch:
     num_decode: int = 0
     dec_block_tables: torch.Tensor | None = None  # int32 [Bd, max_blocks]
     dec_seq_lens: torch.Tensor | None = None  # int32 [Bd]
+    # context-parallel prefill (parallel/context_parallel.py CPPrefill): this
+    # rank's zig-zag shard of one long prompt; K/V go to the CP scratch pages and
+    # attention is the ring over the CP group
+    cp: object = None
 
 
 class Parts:
@@ -225,6 +229,14 @@ class LlamaModel:
         D = self.cfg.head_dim
         wqkv = self.w["layers"][li]["qkv"]
         qkv = self._proj("qkv", h, wqkv, fb.is_decode)
+        if fb.cp is not None:
+            cp = fb.cp
+            q = qkv[:, : self.hq * D]
+            ops.rope_kv(q, qkv[:, self.hq * D: (self.hq + self.hkv) * D],
+                        qkv[:, (self.hq + self.hkv) * D:], fb.positions, self.cos_sin,
+                        cp.scratch[0], cp.scratch[1], fb.slots, self.hq, self.hkv, cp.bs)
+            o = cp.attention(kv.k[li], kv.v[li], q.view(T, self.hq, D), self.scale)
+            return self._proj("o", o.view(T, self.hq * D), self.w["layers"][li]["o"], False)
         if isinstance(qkv, Parts):
             q = ops.splitk_rope_kv(qkv.t, fb.positions, self.cos_sin, kv.k[li], kv.v[li],
                                    fb.slots, self.hq, self.hkv, kv.block_size)

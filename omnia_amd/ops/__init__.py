@@ -404,8 +404,15 @@ def prefill_tiles(q_lens: list[int], tile: int | None = None) -> tuple[list[int]
 
 def prefill_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, scale,
                       tile_seq=None, tile_q0=None, out=None, heads_per_wave: int = 0,
-                      q_tile: int | None = None):
-    """q: [T, Hq, D] new tokens of several sequences (varlen, causal w/ cached prefix)."""
+                      q_tile: int | None = None, lse=None, kv_lens=None):
+    """q: [T, Hq, D] new tokens of several sequences (varlen, causal w/ cached prefix).
+
+    ``lse`` (fp32 [T, Hq], optional) receives each row's natural-log sum of
+    exp of the scaled scores -- the statistic ring attention merges blocks
+    with.  ``kv_lens`` (int32 [B], optional) caps the visible keys of sequence
+    ``s`` at ``kv_lens[s]`` on top of the causal bound, so a K/V block that lies
+    wholly before the queries is attended in full: ``seq_lens = kv_len + qlen``
+    puts the queries after every key."""
     if q.is_cuda:
         if tile_seq is None:
             qsl = q_start_loc.cpu().tolist()
@@ -415,9 +422,15 @@ def prefill_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, 
         out = torch.empty_like(q) if out is None else out
         kernels().prefill_attention(out, q, k_cache, v_cache, block_tables, q_start_loc,
                                     seq_lens, tile_seq, tile_q0, scale, heads_per_wave,
-                                    q_tile or PREFILL_Q_TILE)
+                                    q_tile or PREFILL_Q_TILE, lse, kv_lens)
         return out
-    r = ref.paged_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, scale)
+    if lse is not None or kv_lens is not None:
+        r, l = ref.paged_attention_lse(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens,
+                                       scale, kv_lens)
+        if lse is not None:
+            lse[: l.shape[0]].copy_(l)
+    else:
+        r = ref.paged_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, scale)
     if out is not None:
         out.copy_(r)
         return out

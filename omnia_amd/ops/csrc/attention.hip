@@ -249,7 +249,8 @@ __global__ __launch_bounds__(64 * NW) void prefill_attn_kernel(
     const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ q_start_loc, const int* __restrict__ seq_lens,
     const int* __restrict__ tile_seq, const int* __restrict__ tile_q0, int hkv, int64_t q_stride,
-    int64_t out_stride, float scale_log2) {
+    int64_t out_stride, float scale_log2, float* __restrict__ lse_out,
+    const int* __restrict__ kv_lens) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 64 * 256];
   char* Kl = lds;
   char* Vl = lds + 64 * 256;
@@ -281,7 +282,10 @@ __global__ __launch_bounds__(64 * NW) void prefill_attn_kernel(
   }
 
   const int last_row = min(q0 + 16 * NW - 1, qlen - 1);
-  const int kv_end = off + last_row + 1;  // keys [0, kv_end)
+  // kv_lens (ring-attention blocks): keys >= klim are not part of this K/V block
+  // even where the causal offset would admit them
+  const int klim = kv_lens ? kv_lens[s] : 0x7fffffff;
+  const int kv_end = min(off + last_row + 1, klim);  // keys [0, kv_end)
   const int ntiles = (kv_end + 63) / 64;
   const int min_qpos = off + q0;
 
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(64 * NW) void prefill_attn_kernel(
         for (int hh = 0; hh < HP; ++hh) sacc[hh][nb] = mfma16(a, qf[hh][kk], sacc[hh][nb]);
       }
     }
-    const bool need_mask = (k0 + 63 > min_qpos) || (k0 + 63 >= ctx);
+    const bool need_mask = (k0 + 63 > min_qpos) || (k0 + 63 >= ctx) || (k0 + 63 >= klim);
     short8 pb[HP][2];
 #pragma unroll
     for (int hh = 0; hh < HP; ++hh) {
@@ -356,7 +360,7 @@ __global__ __launch_bounds__(64 * NW) void prefill_attn_kernel(
           float v = sacc[hh][nb][r] * scale_log2;
           if (need_mask) {
             const int key = k0 + nb * 16 + g4 * 4 + r;
-            if (key > qpos) v = -INFINITY;
+            if (key > qpos || key >= klim) v = -INFINITY;
           }
           sacc[hh][nb][r] = v;
           mloc = fmaxf(mloc, v);
@@ -428,6 +432,10 @@ __global__ __launch_bounds__(64 * NW) void prefill_attn_kernel(
         pk[1] = pack_bf2(o[hh][mb][2] * inv, o[hh][mb][3] * inv);
         *reinterpret_cast<uint2v*>(orow + mb * 16 + g4 * 4) = pk;
       }
+      // natural-log sum of exp of the scaled scores (m_run is in log2 units):
+      // the merge statistic of ring attention / split-KV prefill
+      if (lse_out && g4 == 0)
+        lse_out[(int64_t)(qs + qr) * hq + h0 + hh] = (m_run[hh] + log2f(l_run[hh])) * 0.6931471805599453f;
     }
   }
 }
@@ -484,7 +492,8 @@ int omnia_prefill_attention(void* out, const void* q, const void* k_cache, const
                             const int* block_tables, int bt_stride, const int* q_start_loc,
                             const int* seq_lens, const int* tile_seq, const int* tile_q0,
                             int n_tiles, int hq, int hkv, int head_dim, int block_size,
-                            int64_t q_stride, int64_t out_stride, float scale, int hp_req, int q_tile, hipStream_t s) {
+                            int64_t q_stride, int64_t out_stride, float scale, int hp_req, int q_tile,
+                            float* lse_out, const int* kv_lens, hipStream_t s) {
   if (head_dim != 128) return -1;
   if (hq % hkv) return -2;
   if (n_tiles == 0) return 0;
@@ -503,7 +512,7 @@ int omnia_prefill_attention(void* out, const void* q, const void* k_cache, const
   prefill_attn_kernel<BB, HH, NN><<<grid, block, 0, s>>>(                                    \
       (bf16_t*)out, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache,        \
       block_tables, bt_stride, q_start_loc, seq_lens, tile_seq, tile_q0, hkv, q_stride,      \
-      out_stride, scale_log2)
+      out_stride, scale_log2, lse_out, kv_lens)
 #define OMNIA_PRE_HP(BB)                              \
   if (nw == 8) OMNIA_PRE(BB, 1, 8);                   \
   else if (hp == 4) OMNIA_PRE(BB, 4, 4);              \

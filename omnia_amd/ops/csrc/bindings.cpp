@@ -27,7 +27,7 @@ int omnia_prefill_attention(void* out, const void* q, const void* k_cache, const
                             const int* seq_lens, const int* tile_seq, const int* tile_q0,
                             int n_tiles, int hq, int hkv, int head_dim, int block_size,
                             int64_t q_stride, int64_t out_stride, float scale, int hp,
-                            int q_tile, hipStream_t s);
+                            int q_tile, float* lse_out, const int* kv_lens, hipStream_t s);
 int omnia_apply_token_mask(void* logits, int logits_is_bf16, int rows, int64_t row_stride,
                            int vocab, const uint32_t* mask, int words, hipStream_t s);
 int omnia_sample(int* out_tok, float* out_logprob, const void* logits, int logits_is_bf16,
@@ -195,7 +195,8 @@ void decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tens
 void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                        at::Tensor block_tables, at::Tensor q_start_loc, at::Tensor seq_lens,
                        at::Tensor tile_seq, at::Tensor tile_q0, double scale, int64_t hp,
-                       int64_t q_tile) {
+                       int64_t q_tile, c10::optional<at::Tensor> lse,
+                       c10::optional<at::Tensor> kv_lens) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_BF16(k_cache);
   CHECK_I32(block_tables); CHECK_I32(q_start_loc); CHECK_I32(seq_lens); CHECK_I32(tile_seq);
   CHECK_I32(tile_q0);
@@ -204,13 +205,26 @@ void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Ten
   TORCH_CHECK(out.dim() == 3 && out.stride(2) == 1 && out.stride(1) == D, "out [T, Hq, D]");
   TORCH_CHECK(tile_seq.numel() == tile_q0.numel(), "tiles");
   TORCH_CHECK(block_tables.stride(1) == 1, "block_tables rows contiguous");
+  float* lse_p = nullptr;
+  if (lse.has_value()) {
+    TORCH_CHECK(lse->scalar_type() == at::kFloat && lse->is_contiguous() && lse->dim() == 2 &&
+                    lse->size(0) >= q.size(0) && lse->size(1) == q.size(1),
+                "lse fp32 [T, Hq] contiguous");
+    lse_p = lse->data_ptr<float>();
+  }
+  const int* kvl_p = nullptr;
+  if (kv_lens.has_value()) {
+    CHECK_I32((*kv_lens));
+    TORCH_CHECK(kv_lens->numel() == seq_lens.numel(), "kv_lens [B]");
+    kvl_p = kv_lens->data_ptr<int>();
+  }
   CHECK_RC(omnia_prefill_attention(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(),
                                    v_cache.data_ptr(), block_tables.data_ptr<int>(),
                                    block_tables.stride(0), q_start_loc.data_ptr<int>(),
                                    seq_lens.data_ptr<int>(), tile_seq.data_ptr<int>(),
                                    tile_q0.data_ptr<int>(), tile_seq.numel(), q.size(1), hkv, D,
                                    bs, q.stride(0), out.stride(0), (float)scale, (int)hp,
-                                   (int)q_tile, cur_stream()),
+                                   (int)q_tile, lse_p, kvl_p, cur_stream()),
            "prefill_attention");
 }
 
@@ -645,7 +659,8 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("prefill_attention", &prefill_attention, py::arg("out"), py::arg("q"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("q_start_loc"),
         py::arg("seq_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("scale"),
-        py::arg("hp") = 0, py::arg("q_tile") = 64);
+        py::arg("hp") = 0, py::arg("q_tile") = 64, py::arg("lse") = py::none(),
+        py::arg("kv_lens") = py::none());
   m.def("sample", &sample);
   m.def("mean_pool_l2", &mean_pool_l2);
   m.def("cosine_scores", &cosine_scores);

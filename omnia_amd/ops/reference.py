@@ -103,6 +103,33 @@ def paged_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, sc
     return out
 
 
+def paged_attention_lse(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, scale,
+                        kv_lens=None):
+    """:func:`paged_attention` that also returns the fp32 natural-log LSE
+    [T, Hq] of every row, with keys of sequence s capped at ``kv_lens[s]``."""
+    out = torch.zeros_like(q)
+    T, hq = q.shape[0], q.shape[1]
+    lse = torch.full((T, hq), float("-inf"), dtype=torch.float32, device=q.device)
+    g = hq // k_cache.shape[1]
+    for s in range(seq_lens.numel()):
+        a, b = int(q_start_loc[s]), int(q_start_loc[s + 1])
+        ctx, qlen = int(seq_lens[s]), b - a
+        if qlen == 0:
+            continue
+        klen = min(ctx, int(kv_lens[s])) if kv_lens is not None else ctx
+        kk = gather_kv(k_cache, block_tables[s], klen).float().repeat_interleave(g, dim=1)
+        vv = gather_kv(v_cache, block_tables[s], klen).float().repeat_interleave(g, dim=1)
+        scores = torch.einsum("qhd,khd->hqk", q[a:b].float(), kk) * scale
+        qpos = torch.arange(ctx - qlen, ctx, device=q.device)[:, None]
+        kpos = torch.arange(klen, device=q.device)[None, :]
+        scores = scores.masked_fill((kpos > qpos)[None], float("-inf"))
+        l = torch.logsumexp(scores, dim=-1)  # [h, q]
+        p = torch.exp(scores - l[..., None]).nan_to_num(0.0)
+        out[a:b] = torch.einsum("hqk,khd->qhd", p, vv).to(q.dtype)
+        lse[a:b] = l.t()
+    return out, lse
+
+
 def silu_mul(x: torch.Tensor) -> torch.Tensor:
     inter = x.shape[-1] // 2
     g, u = x[..., :inter].float(), x[..., inter:].float()

@@ -18,9 +18,20 @@ one GPU's prefill budget can still be spread over W ranks:
 
 GQA is native: K/V stay at ``Hkv`` heads on the wire (G x fewer bytes than
 expanded heads) and are broadcast to the G query heads of each group inside
-the block product.  The block product runs on hipBLASLt (batched matmul in the
-activation dtype, fp32 softmax statistics); query rows are processed in tiles
-so the score block never exceeds ``q_tile x kv_len`` per head.
+the block product.
+
+Two block products:
+
+* :func:`ring_attention` -- generic (any head dim, causal or not) on batched
+  matmuls with fp32 statistics; the reference implementation of the ring.
+* :func:`ring_attention_paged` -- the serving path (:class:`CPPrefill`, used by
+  the engine for prompts over ``EngineConfig.cp_threshold``): K/V travel as
+  the engine's paged layout ``[2, pages, Hkv, BS, D]`` and every ring step is
+  ONE launch of the hand flash-prefill kernel (``ops/csrc/attention.hip``) over
+  the step's zig-zag chunk pairs, with the kernel's LSE output and per-pair key
+  bound (``kv_lens``) -- no score matrix is ever materialised.  The rank that
+  owns the request copies every K/V block it sees go by into its paged KV
+  cache, so after the prefill the owner decodes alone with no extra gather.
 """
 from __future__ import annotations
 
@@ -141,3 +152,160 @@ def reference_attention(q, k, v, scale=None, causal=True):
     if causal:
         s = s.masked_fill(torch.ones(T, T, dtype=torch.bool, device=q.device).triu(1), -math.inf)
     return torch.einsum("hqk,khd->qhd", s.softmax(-1), vv)
+
+
+# ============================================================ serving path
+def _pairs(rank: int, src: int) -> list[tuple[int, int, bool]]:
+    """(q chunk, k chunk, causal) products of one ring step: chunk 0 = the
+    rank's low zig-zag chunk (index r), 1 = its high chunk (2W-1-r).  Chunk
+    pairs whose keys all lie after the queries are skipped; every other pair
+    is either the causal diagonal or attended in full."""
+    if src == rank:
+        return [(0, 0, True), (1, 0, False), (1, 1, True)]
+    if src < rank:
+        return [(0, 0, False), (1, 0, False)]
+    return [(1, 0, False), (1, 1, False)]
+
+
+class _StepLaunch:
+    """Kernel metadata of one ring-step pattern (device tensors, built once)."""
+
+    def __init__(self, pairs, c: int, pages: int, device):
+        from .. import ops
+
+        n = len(pairs)
+        self.pairs = pairs
+        self.rows = torch.cat([torch.arange(qc * c, (qc + 1) * c) for qc, _, _ in pairs]).to(device)
+        qsl = [i * c for i in range(n + 1)]
+        self.q_start_loc = torch.tensor(qsl, dtype=torch.int32, device=device)
+        # causal diagonal: queries at relative 0..c-1 over keys 0..c-1; full: queries
+        # placed after all c keys (seq_len = 2c, offset c), keys capped at c
+        self.seq_lens = torch.tensor([c if causal else 2 * c for _, _, causal in pairs],
+                                     dtype=torch.int32, device=device)
+        self.kv_lens = torch.full((n,), c, dtype=torch.int32, device=device)
+        bt = [list(range(kc * pages, (kc + 1) * pages)) for _, kc, _ in pairs]
+        self.block_tables = torch.tensor(bt, dtype=torch.int32, device=device)
+        ts, tq = ops.prefill_tiles([c] * n)
+        self.tile_seq = torch.tensor(ts, dtype=torch.int32, device=device)
+        self.tile_q0 = torch.tensor(tq, dtype=torch.int32, device=device)
+
+
+def ring_attention_paged(q: torch.Tensor, kv: torch.Tensor, c: int, scale: float, group=None,
+                         launches: dict | None = None, on_block=None) -> torch.Tensor:
+    """Causal ring attention of this rank's zig-zag shard.
+
+    q: [2c, Hq, D] (rows 0..c-1 = low chunk, c..2c-1 = high chunk); kv: this
+    rank's K/V pages [2, 2c/BS, Hkv, BS, D] (low chunk pages first).
+    ``on_block(src, kv_src)`` sees every rank's K/V block once (own included).
+    Returns o [2c, Hq, D] in q's dtype."""
+    from .. import ops
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if world > 1 else 0
+    pages = kv.shape[1] // 2
+    Hq, D = q.shape[1], q.shape[2]
+    o = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
+    lse = torch.full(q.shape[:2], -math.inf, dtype=torch.float32, device=q.device)
+    launches = {} if launches is None else launches
+    nxt, prv = (rank + 1) % world, (rank - 1) % world
+    granks = (dist.get_process_group_ranks(group) if (group is not None and world > 1)
+              else list(range(world)))
+    cur = kv.contiguous()
+    for step in range(world):
+        src = (rank - step) % world
+        reqs, recv = [], None
+        if step + 1 < world:
+            recv = torch.empty_like(cur)
+            reqs = dist.batch_isend_irecv([
+                dist.P2POp(dist.isend, cur, granks[nxt], group),
+                dist.P2POp(dist.irecv, recv, granks[prv], group)])
+        if on_block is not None:
+            on_block(src, cur)
+        key = (src == rank, src < rank)
+        L = launches.get(key)
+        if L is None:
+            L = launches[key] = _StepLaunch(_pairs(rank, src), c, pages, q.device)
+        qb = q.index_select(0, L.rows)
+        lb = torch.empty(qb.shape[:2], dtype=torch.float32, device=q.device)
+        ob = ops.prefill_attention(qb, cur[0], cur[1], L.block_tables, L.q_start_loc,
+                                   L.seq_lens, scale, L.tile_seq, L.tile_q0, lse=lb,
+                                   kv_lens=L.kv_lens)
+        for i, (qc, _, _) in enumerate(L.pairs):
+            sl = slice(qc * c, (qc + 1) * c)
+            o[sl], lse[sl] = _merge(o[sl], lse[sl], ob[i * c:(i + 1) * c].float(),
+                                    lb[i * c:(i + 1) * c])
+        for r in reqs:
+            r.wait()
+        if recv is not None:
+            cur = recv
+    return o.to(q.dtype)
+
+
+class CPPrefill:
+    """One context-parallel prefill of an ``L``-token prompt over the ranks of
+    ``group`` (every rank holds the full model; the request's owner holds its
+    KV pages).  The prompt is padded to a multiple of 2W pages; padded rows sit
+    after every real token, so causal masking keeps them out of real rows.
+
+    The model's attention (``models/llama.py``) sees ``fb.cp`` and, instead of
+    writing K/V into the paged cache, writes them into this rank's scratch pages
+    and calls :meth:`attention`."""
+
+    def __init__(self, L: int, world: int, rank: int, group, hkv: int, head_dim: int,
+                 block_size: int, device, dtype, owner: bool = False,
+                 owner_blocks: list[int] | None = None, max_position: int | None = None):
+        self.L, self.world, self.rank, self.group = L, world, rank, group
+        unit = 2 * world * block_size
+        self.L_pad = -(-L // unit) * unit
+        self.c = self.L_pad // (2 * world)
+        self.bs = block_size
+        self.pages = self.c // block_size  # pages per chunk
+        idx = zigzag_indices(self.L_pad, world, rank)
+        self.index = idx.to(device)  # rows of the padded prompt this rank holds
+        pos = idx.clamp(max=(max_position or self.L_pad) - 1)
+        self.positions = pos.to(device=device, dtype=torch.int32)
+        self.slots = torch.arange(2 * self.c, dtype=torch.int64, device=device)
+        self.scratch = torch.empty(2, 2 * self.pages, hkv, block_size, head_dim, dtype=dtype,
+                                   device=device)
+        self.owner = owner
+        self.owner_blocks = owner_blocks
+        self._launches: dict = {}
+        self._dst = None
+        if owner:
+            nreal = -(-L // block_size)  # pages holding real tokens
+            if owner_blocks is None or len(owner_blocks) < nreal:
+                raise ValueError("owner needs KV blocks for the whole prompt")
+            self._dst = torch.tensor(list(owner_blocks[:nreal]), dtype=torch.long, device=device)
+            self._nreal = nreal
+
+    def locate(self, p: int) -> tuple[int, int]:
+        """(rank, row) holding absolute position ``p`` of the padded prompt."""
+        ch = p // self.c
+        if ch < self.world:
+            return ch, p % self.c
+        return 2 * self.world - 1 - ch, self.c + p % self.c
+
+    def _chunk_pages(self, src: int):
+        """[(chunk-local page range, first absolute page)] of rank src's chunks."""
+        W, P = self.world, self.pages
+        return [(0, src * P), (1, (2 * W - 1 - src) * P)]
+
+    def attention(self, kc: torch.Tensor, vc: torch.Tensor, q3: torch.Tensor, scale: float
+                  ) -> torch.Tensor:
+        """q3: [2c, Hq, D] after RoPE; this rank's K/V already in ``scratch``.
+        ``kc`` / ``vc``: the owner's paged cache of this layer."""
+        def keep(src, blk):
+            if not self.owner:
+                return
+            for half, first in self._chunk_pages(src):
+                lo = first
+                hi = min(first + self.pages, self._nreal)
+                if hi <= lo:
+                    continue
+                src_pages = blk[:, half * self.pages: half * self.pages + (hi - lo)]
+                dst = self._dst[lo:hi]
+                kc.index_copy_(0, dst, src_pages[0])
+                vc.index_copy_(0, dst, src_pages[1])
+
+        return ring_attention_paged(q3, self.scratch, self.c, scale, self.group,
+                                    self._launches, keep)

@@ -93,14 +93,33 @@ class LocalKMS:
         self.key_id = key_id
         self.path = path
         self._lock = threading.Lock()
+        self._mtime = 0.0
         if path and os.path.exists(path):
-            d = json.loads(open(path).read())
-            keys = {v: base64.b64decode(k) for v, k in d["keys"].items()}
-            current = d["current"]
+            keys, current = self._read()
         self.keys = dict(keys or {"1": os.urandom(32)})
         self.current = current or max(self.keys, key=int)
         self.created = {v: time.time() for v in self.keys}
         self._save()
+
+    def _read(self):
+        with open(self.path) as f:
+            d = json.loads(f.read())
+        self._mtime = os.stat(self.path).st_mtime
+        return {v: base64.b64decode(k) for v, k in d["keys"].items()}, d["current"]
+
+    def _maybe_reload(self):
+        """Another process (the key-rotation controller) rotated the shared key
+        file: pick up the new current version and keep every old one."""
+        if not self.path or not os.path.exists(self.path):
+            return
+        if os.stat(self.path).st_mtime == self._mtime:
+            return
+        with self._lock:
+            keys, current = self._read()
+            for v in keys:
+                self.created.setdefault(v, time.time())
+            self.keys.update(keys)
+            self.current = current
 
     def _save(self):
         if self.path:
@@ -111,8 +130,10 @@ class LocalKMS:
                                     self.keys.items()}}, f)
             os.chmod(tmp, 0o600)
             os.replace(tmp, self.path)
+            self._mtime = os.stat(self.path).st_mtime
 
     def encrypt(self, plaintext: bytes) -> EncryptOutput:
+        self._maybe_reload()
         dek = os.urandom(32)
         with self._lock:
             ver, kek = self.current, self.keys[self.current]
@@ -127,14 +148,19 @@ class LocalKMS:
             raise ValueError(f"envelope sealed under key {kid!r}, not {self.key_id!r}")
         kek = self.keys.get(ver)
         if kek is None:
+            self._maybe_reload()
+            kek = self.keys.get(ver)
+        if kek is None:
             raise ValueError(f"unknown key version {ver}")
         dek = open_(kek, edk, f"{kid}:{ver}".encode())
         return open_(dek, body)
 
     def key_metadata(self) -> KeyMetadata:
+        self._maybe_reload()
         return KeyMetadata(self.key_id, self.current, created_at=self.created[self.current])
 
     def rotate(self) -> tuple[str, str]:
+        self._maybe_reload()
         with self._lock:
             prev = self.current
             nv = str(max(int(v) for v in self.keys) + 1)

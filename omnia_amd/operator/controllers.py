@@ -709,7 +709,10 @@ def default_reconcilers(gpu_count: int | None = None,
 
     rs += [AgentPolicyReconciler(cfg.istio), MemoryPolicyReconciler(cfg.namespace),
            SessionRetentionPolicyReconciler(cfg.namespace)]
-    for k in ("ToolPolicy", "SessionPrivacyPolicy", "RolloutAnalysis", "ArenaDevSession"):
+    from ..ee.controllers import SessionPrivacyPolicyReconciler, ToolPolicyReconciler
+
+    rs += [ToolPolicyReconciler(), SessionPrivacyPolicyReconciler()]
+    for k in ("RolloutAnalysis", "ArenaDevSession"):
         rs.append(SimplePolicyReconciler(k))
     from .sourcesync import SourceReconciler
 

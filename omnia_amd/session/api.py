@@ -336,6 +336,12 @@ def main(argv=None):
                     default=int(os.environ.get("OTLP_GRPC_PORT", 4317)))
     ap.add_argument("--otlp-http-port", type=int,
                     default=int(os.environ.get("OTLP_HTTP_PORT", 4318)))
+    ap.add_argument("--encryption-provider", default=os.environ.get("ENCRYPTION_PROVIDER", ""),
+                    help="EE: encrypt message content/metadata at rest (local | vault | ...)")
+    ap.add_argument("--encryption-key-id", default=os.environ.get("ENCRYPTION_KEY_ID", "local"))
+    ap.add_argument("--encryption-key-file", default=os.environ.get("ENCRYPTION_KEY_FILE", ""),
+                    help="local provider: versioned KEK ring (rotated by the key-rotation "
+                         "controller)")
     a = ap.parse_args(argv)
     cold = ColdArchive(LocalBlobStore(a.cold_dir)) if a.cold_dir else None
     if a.cold_backend and a.cold_bucket:
@@ -371,6 +377,12 @@ def main(argv=None):
                    ttl_s=retention.get("hot_ttl_s", 3600),
                    max_messages=retention.get("hot_max_messages", 200))
     svc = TieredSessionService(hot, warm, cold, a.ttl, pub)
+    if a.encryption_provider:
+        from ..ee.encryption import Encryptor, build_provider
+
+        svc.encryptor = Encryptor(build_provider({"type": a.encryption_provider,
+                                                  "keyID": a.encryption_key_id,
+                                                  "keyFile": a.encryption_key_file or None}))
     audit_logger = None
     app_kw = {}
     if a.audit_db:

@@ -138,6 +138,13 @@ class WarmStore:
         self._upsert("messages", (m.id, sid, m.sequence_num, m.timestamp, m.role, m.content,
                                   json.dumps(m.to_json())))
 
+    def scan_messages(self, after_id: str = "", limit: int = 100) -> list[tuple[str, str, dict]]:
+        """(id, session_id, doc) of every message in id order after ``after_id``
+        (the key-rotation re-encryption cursor)."""
+        r = self._x("SELECT id, session_id, doc FROM messages WHERE id > ? ORDER BY id LIMIT ?",
+                    (after_id, limit))
+        return [(x[0], x[1], json.loads(x[2])) for x in r]
+
     def messages(self, sid: str, limit: int = 1000, offset: int = 0) -> list[Message]:
         r = self._x("SELECT doc FROM messages WHERE session_id=? ORDER BY seq, ts LIMIT ? "
                     "OFFSET ?", (sid, limit, offset))
@@ -363,6 +370,58 @@ class TieredSessionService:
         self.publisher = publisher  # async publish(namespace, event_dict)
         self.lock = threading.Lock()
         self.degraded_reads = 0
+        # ee/encryption.Encryptor when a SessionPrivacyPolicy enables encryption at
+        # rest: message content / metadata are sealed before the warm tier and
+        # opened on the way out (the hot cache holds plaintext in process memory)
+        self.encryptor = None
+
+    # ------------------------------------------------------------ encryption
+    def _seal(self, m: Message) -> Message:
+        if self.encryptor is None:
+            return m
+        import dataclasses
+
+        enc, _ = self.encryptor.encrypt_message({"content": m.content,
+                                                 "metadata": dict(m.metadata or {})})
+        return dataclasses.replace(m, content=enc.get("content", ""),
+                                   metadata=enc.get("metadata") or {})
+
+    def _unseal(self, m: Message) -> Message:
+        from ..ee.encryption import META_KEY
+
+        if self.encryptor is None or META_KEY not in (m.metadata or {}):
+            return m
+        import dataclasses
+
+        dec = self.encryptor.decrypt_message({"content": m.content,
+                                              "metadata": dict(m.metadata)})
+        return dataclasses.replace(m, content=dec.get("content", ""),
+                                   metadata=dec.get("metadata") or {})
+
+    def reencrypt_batch(self, current_version: str, after_id: str = "", limit: int = 100
+                        ) -> tuple[str, bool, int, int]:
+        """Re-seal up to ``limit`` warm messages whose ``_encryption.keyVersion``
+        is not ``current_version`` (``ee/pkg/encryption`` ``ReEncryptBatch``).
+        Returns (last scanned id, more?, re-encrypted, errors)."""
+        from ..ee.encryption import META_KEY
+
+        rows = self.warm.scan_messages(after_id, limit)
+        done = errors = 0
+        last = after_id
+        for mid, sid, doc in rows:
+            last = mid
+            m = Message.from_json(doc)
+            rec = (m.metadata or {}).get(META_KEY)
+            if rec is None:
+                continue
+            try:
+                if json.loads(rec).get("keyVersion") == current_version:
+                    continue
+                self.warm.add_message(sid, self._seal(self._unseal(m)))
+                done += 1
+            except Exception:  # noqa: BLE001 - counted, the batch goes on
+                errors += 1
+        return last, len(rows) == limit, done, errors
 
     # ------------------------------------------------------------ writes
     def create(self, s: Session) -> Session:
@@ -390,9 +449,9 @@ class TieredSessionService:
             s.total_input_tokens += m.input_tokens
             s.total_output_tokens += m.output_tokens
             s.estimated_cost_usd += m.cost_usd
-            if m.content:
+            if m.content and self.encryptor is None:
                 s.last_message_preview = m.content[:120]
-        self.warm.add_message(sid, m)
+        self.warm.add_message(sid, self._seal(m))
         self.warm.put_session(s)
         try:
             self.hot.put(s)
@@ -493,7 +552,8 @@ class TieredSessionService:
         try:
             s = self.warm.get_session(sid)
             if s is not None:
-                msgs = self.warm.messages(sid) if with_messages else []
+                msgs = [self._unseal(m) for m in self.warm.messages(sid)] if with_messages \
+                    else []
                 try:
                     self.hot.put(s, msgs)
                 except TierError:
@@ -506,7 +566,7 @@ class TieredSessionService:
             try:
                 v = self.cold.get(sid)
                 if v is not None:
-                    return v
+                    return v[0], [self._unseal(m) for m in v[1]]
             except TierError as e:
                 if warm_err is not None:
                     raise TierError("warm and cold tiers unavailable") from e

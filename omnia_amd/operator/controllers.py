@@ -712,8 +712,10 @@ def default_reconcilers(gpu_count: int | None = None,
     from ..ee.controllers import SessionPrivacyPolicyReconciler, ToolPolicyReconciler
 
     rs += [ToolPolicyReconciler(), SessionPrivacyPolicyReconciler()]
-    for k in ("RolloutAnalysis", "ArenaDevSession"):
-        rs.append(SimplePolicyReconciler(k))
+    rs.append(SimplePolicyReconciler("RolloutAnalysis"))
+    from ..ee.arena.devsession import ArenaDevSessionReconciler
+
+    rs.append(ArenaDevSessionReconciler())
     from .sourcesync import SourceReconciler
 
     for k in ("SkillSource", "ArenaSource", "ArenaTemplateSource", "PromptPackSource"):

@@ -156,7 +156,7 @@ class LocalLauncher:
         pod.facade = fac
 
     # ------------------------------------------------------------ service pods
-    SERVICE_COMPONENTS = ("session-api", "memory-api")
+    SERVICE_COMPONENTS = ("session-api", "memory-api", "arena-dev-console")
 
     async def _sync_services(self):
         """Workspace session-api / memory-api Deployments as service processes."""

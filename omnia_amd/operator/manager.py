@@ -97,6 +97,16 @@ class Manager:
                  namespace: str = "omnia-system"):
         self.store = store
         self.reconcilers = {r.kind: r for r in (reconcilers or default_reconcilers(gpu_count))}
+        if reconcilers is None and os.environ.get("OMNIA_LICENSE_SERVER"):
+            # EE: activate the license against the license server, heartbeat daily
+            from ..ee import license as lic
+            from ..ee.license_activation import ActivationClient, LicenseActivationReconciler
+
+            self.reconcilers["Secret"] = LicenseActivationReconciler(
+                license_validator_for(store, os.environ.get("OMNIA_LICENSE_PUBLIC_KEY")),
+                ActivationClient(os.environ["OMNIA_LICENSE_SERVER"]),
+                cluster_name=os.environ.get("OMNIA_CLUSTER_NAME", ""),
+                secret_name=lic.SECRET_NAME)
         self.queue: asyncio.Queue | None = None
         self.pending: set = set()
         self.delayed: dict = {}

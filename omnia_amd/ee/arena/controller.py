@@ -146,11 +146,21 @@ class ArenaJobController:
         return {"access_key": data.get("AWS_ACCESS_KEY_ID") or data.get("access-key", ""),
                 "secret_key": data.get("AWS_SECRET_ACCESS_KEY") or data.get("secret-key", "")}
 
-    def __init__(self, store, queue, provider_objects: dict | None = None):
+    def __init__(self, store, queue, provider_objects: dict | None = None,
+                 worker_mode: str = "inproc", redis_url: str = "",
+                 worker_image: str = "ghcr.io/altairalabs/omnia-arena-worker:latest",
+                 poll_s: float = 2.0):
+        """``worker_mode`` "inproc": worker tasks on this event loop (single
+        process); "pods": a batch/v1 Job of worker pods sharing the Redis-Streams
+        queue at ``redis_url`` (``arenajob_controller_pod.go``)."""
         self.store = store
         self.q = queue
         self.provider_objects = provider_objects or {}
         self.tasks: dict[str, asyncio.Task] = {}
+        self.worker_mode = worker_mode
+        self.redis_url = redis_url
+        self.worker_image = worker_image
+        self.poll_s = poll_s
 
     async def reconcile(self, ns: str, name: str):
         job = self.store.get("ArenaJob", name, ns)
@@ -174,8 +184,21 @@ class ArenaJobController:
             log.debug("status update failed: %s", e)
 
     async def _run(self, job):
+        try:
+            return await self._run_inner(job)
+        except Exception as e:  # noqa: BLE001 - surfaced in status, not lost in a task
+            log.exception("arena job %s failed", job["metadata"]["name"])
+            cur = self.store.try_get("ArenaJob", job["metadata"]["name"],
+                                     job["metadata"].get("namespace", "default"))
+            if cur is not None:
+                self._status(cur, "Failed", message=str(e)[:500], completionTime=time.time())
+            return None
+
+    async def _run_inner(self, job):
         md, spec = job["metadata"], job["spec"]
         cfg = load_arena_config(self.store, job)
+        if self.worker_mode == "pods":
+            return await self._run_pods(job, cfg)
         scenarios = {s["id"]: s for s in cfg.get("scenarios", [])}
         providers = {}
         for p in cfg.get("providers", []):
@@ -207,6 +230,12 @@ class ArenaJobController:
                                job_type=job_type)
                    for _ in range(replicas)]
         await asyncio.gather(*(w.run() for w in workers))
+        return await self._finish(job, spec, items, t0)
+
+    async def _finish(self, job, spec, items, t0):
+        md = job["metadata"]
+        job_type = spec.get("type", "evaluation")
+        lt = spec.get("loadTest") or {}
         wall = time.perf_counter() - t0
         results = await self.q.results_of(md["name"])
         turn_results = []
@@ -234,22 +263,175 @@ class ArenaJobController:
         return stats
 
 
+    # ------------------------------------------------------------ worker pods
+    def _worker_objects(self, job, cfg: dict, n_items: int) -> list[dict]:
+        """SA / Role / RoleBinding (``arena_worker_rbac.go``), the resolved
+        config ConfigMap and the worker Job (``arenajob_controller_pod.go``)."""
+        from ...operator.apistore import owner_ref
+        from .worker_main import secret_env_name
+
+        md, spec = job["metadata"], job["spec"]
+        ns, name = md.get("namespace", "default"), md["name"]
+        wn = f"arena-worker-{name}"[:63]
+        own = [owner_ref(job)]
+        labels = {"app.kubernetes.io/name": "arena-worker",
+                  "omnia.altairalabs.ai/component": "arena-worker",
+                  "omnia.altairalabs.ai/arena-job": name}
+        providers, secret_env = [], []
+        for p in cfg.get("providers", []):
+            p = dict(p)
+            if p.get("mode") == "direct":
+                ref = p.get("providerRef") or p["id"]
+                pobj = self.store.try_get("Provider", ref if isinstance(ref, str) else
+                                          ref.get("name"), ns)
+                if pobj is not None:
+                    p["spec"] = pobj.get("spec") or {}
+                    sref = ((p["spec"].get("credential") or {}).get("secretRef") or
+                            p["spec"].get("secretRef") or {})
+                    if sref.get("name"):
+                        secret_env.append({"name": secret_env_name(p["id"]), "valueFrom": {
+                            "secretKeyRef": {"name": sref["name"],
+                                             "key": sref.get("key") or "api-key",
+                                             "optional": True}}})
+                p.pop("object", None)
+            providers.append(p)
+        lt = spec.get("loadTest") or {}
+        ramp = lt.get("ramp") or {}
+        replicas = int((spec.get("workers") or {}).get("replicas") or 1)
+        conc = int(lt.get("concurrency") or lt.get("vusPerWorker") or 4)
+        env = [{"name": "ARENA_JOB_NAME", "value": name},
+               {"name": "ARENA_JOB_NAMESPACE", "value": ns},
+               {"name": "ARENA_JOB_TYPE", "value": spec.get("type", "evaluation")},
+               {"name": "ARENA_SOURCE_NAME", "value": spec["sourceRef"]["name"]},
+               {"name": "ARENA_FILE", "value": spec.get("arenaFile") or "config.arena.yaml"},
+               {"name": "REDIS_URL", "value": self.redis_url},
+               {"name": "ARENA_CONFIG_FILE", "value": "/etc/arena/config.json"},
+               {"name": "ARENA_VUS_PER_WORKER", "value": str(max(1, conc // replicas))},
+               {"name": "ARENA_CONCURRENCY", "value": str(conc)},
+               {"name": "ARENA_RAMP_UP", "value": str(float(ramp.get("upSeconds") or 0))},
+               {"name": "ARENA_RAMP_DOWN", "value": str(float(ramp.get("downSeconds") or 0))},
+               {"name": "ARENA_TOTAL_ITEMS", "value": str(n_items)},
+               {"name": "LOG_LEVEL", "value": "info"}] + secret_env
+        if lt.get("budgetLimit"):
+            env.append({"name": "ARENA_BUDGET",
+                        "value": str(float(lt["budgetLimit"]) / replicas)})
+        ttl = spec.get("ttlSecondsAfterFinished")
+        return [
+            {"apiVersion": "v1", "kind": "ServiceAccount",
+             "metadata": {"name": wn, "namespace": ns, "labels": labels,
+                          "ownerReferences": own}},
+            {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role",
+             "metadata": {"name": wn, "namespace": ns, "labels": labels, "ownerReferences": own},
+             "rules": [{"apiGroups": ["omnia.altairalabs.ai"],
+                        "resources": ["arenajobs", "arenasources", "providers"],
+                        "verbs": ["get", "list", "watch"]},
+                       {"apiGroups": ["omnia.altairalabs.ai"], "resources": ["arenajobs/status"],
+                        "verbs": ["get", "patch", "update"]},
+                       {"apiGroups": [""], "resources": ["configmaps", "secrets"],
+                        "verbs": ["get"]}]},
+            {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding",
+             "metadata": {"name": wn, "namespace": ns, "labels": labels, "ownerReferences": own},
+             "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "Role", "name": wn},
+             "subjects": [{"kind": "ServiceAccount", "name": wn, "namespace": ns}]},
+            {"apiVersion": "v1", "kind": "ConfigMap",
+             "metadata": {"name": f"{wn}-config", "namespace": ns, "labels": labels,
+                          "ownerReferences": own},
+             "data": {"config.json": json.dumps({"scenarios": cfg.get("scenarios", []),
+                                                 "providers": providers}, sort_keys=True)}},
+            {"apiVersion": "batch/v1", "kind": "Job",
+             "metadata": {"name": wn, "namespace": ns, "labels": labels,
+                          "ownerReferences": own},
+             "spec": {"parallelism": replicas, "completions": replicas,
+                      "backoffLimit": int(spec.get("backoffLimit") or 3),
+                      "ttlSecondsAfterFinished": int(ttl) if ttl is not None else 3600,
+                      "template": {"metadata": {"labels": labels}, "spec": {
+                          "serviceAccountName": wn, "restartPolicy": "Never",
+                          "containers": [{
+                              "name": "worker", "image": self.worker_image,
+                              "command": ["python", "-m", "omnia_amd.ee.arena.worker_main"],
+                              "env": env,
+                              "volumeMounts": [{"name": "config", "mountPath": "/etc/arena",
+                                                "readOnly": True}]}],
+                          "volumes": [{"name": "config",
+                                       "configMap": {"name": f"{wn}-config"}}]}}}},
+        ]
+
+    async def _run_pods(self, job, cfg):
+        md, spec = job["metadata"], job["spec"]
+        ns, name = md.get("namespace", "default"), md["name"]
+        scenarios = {s["id"]: s for s in cfg.get("scenarios", [])}
+        providers = {p["id"]: p for p in cfg.get("providers", [])}
+        trials = int(spec.get("trials") or 1)
+        if spec.get("type") == "datagen":
+            trials = int((spec.get("dataGen") or {}).get("count") or 100)
+        items = partition(name, scenarios, providers, trials)
+        await self.q.enqueue(items)
+        for obj in self._worker_objects(job, cfg, len(items)):
+            self.store.apply(obj)
+        self._status(job, "Running", progress={"total": len(items), "done": 0},
+                     startTime=time.time(), workerJob=f"arena-worker-{name}"[:63])
+        t0 = time.perf_counter()
+        wn = f"arena-worker-{name}"[:63]
+        while True:
+            await asyncio.sleep(self.poll_s)
+            kj = self.store.try_get("Job", wn, ns)
+            jst = (kj or {}).get("status") or {}
+            prog = await self.q.progress(name)
+            done = int(prog.get("done", 0))
+            cur = self.store.try_get("ArenaJob", name, ns)
+            if cur is None:  # deleted: the owned Job goes with it
+                return None
+            if (cur.get("spec") or {}).get("cancelled"):
+                self.store.delete("Job", wn, ns)
+                self._status(cur, "Cancelled", completionTime=time.time())
+                return None
+            st = cur.get("status") or {}
+            if (st.get("progress") or {}).get("done") != done or \
+                    st.get("activeWorkers") != jst.get("active", 0):
+                self._status(cur, "Running", progress={"total": len(items), "done": done},
+                             activeWorkers=jst.get("active", 0))
+            failed_job = any(c.get("type") == "Failed" and c.get("status") == "True"
+                             for c in jst.get("conditions") or [])
+            if failed_job:
+                self._status(cur, "Failed", message="worker Job failed",
+                             completionTime=time.time())
+                return None
+            complete = int(jst.get("succeeded", 0)) >= int(
+                (spec.get("workers") or {}).get("replicas") or 1)
+            if complete or done >= len(items):
+                return await self._finish(cur, spec, items, t0)
+
+
 class ArenaJobReconciler:
     """Manager adapter: the operator's reconcile loop is synchronous; jobs run as
     tasks on the manager's event loop (one worker "pod" group per job)."""
 
     kind = "ArenaJob"
 
-    def __init__(self, queue=None, provider_objects: dict | None = None):
-        from .queue import MemoryQueue
+    def __init__(self, queue=None, provider_objects: dict | None = None,
+                 worker_mode: str | None = None, redis_url: str | None = None):
+        import os
 
+        from .queue import MemoryQueue, StreamQueue
+
+        # OMNIA_ARENA_WORKER_MODE=pods + OMNIA_ARENA_REDIS_URL: worker Jobs on a
+        # shared Redis-Streams queue; default: in-process worker tasks
+        self.worker_mode = worker_mode or os.environ.get("OMNIA_ARENA_WORKER_MODE", "inproc")
+        self.redis_url = redis_url or os.environ.get("OMNIA_ARENA_REDIS_URL", "")
+        if queue is None and self.worker_mode == "pods" and self.redis_url:
+            from ...utils.resp import RedisClient
+
+            queue = StreamQueue(RedisClient(self.redis_url))
+        elif self.worker_mode == "pods" and not self.redis_url:
+            self.worker_mode = "inproc"  # worker pods need the shared queue
         self.queue = queue or MemoryQueue()
         self.provider_objects = provider_objects or {}
         self.ctl = None
 
     def reconcile(self, store, ns, name):
         if self.ctl is None:
-            self.ctl = ArenaJobController(store, self.queue, self.provider_objects)
+            self.ctl = ArenaJobController(store, self.queue, self.provider_objects,
+                                          worker_mode=self.worker_mode, redis_url=self.redis_url)
         try:
             store.get("ArenaJob", name, ns or "default")
         except KeyError:

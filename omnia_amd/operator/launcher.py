@@ -100,6 +100,7 @@ class LocalLauncher:
         self.pods: dict[tuple, Pod] = {}
         self.replicas: dict[tuple, list] = {}  # process mode: key -> [_ProcReplica]
         self.services: dict[tuple, tuple] = {}  # (ns, name) -> (ServiceProcess, hash)
+        self.jobs: dict[tuple, dict] = {}  # (ns, name) -> {"pods": [...], "failed": n, ...}
         self.engine_factory = engine_factory  # fn(engine_cfg) -> AsyncLLMEngine
         self.use_grpc = use_grpc
         self.mode = mode
@@ -154,6 +155,87 @@ class LocalLauncher:
         fac = build_facade(_env(cs["facade"]), client)
         pod.port = await fac.start("127.0.0.1", 0)
         pod.facade = fac
+
+    # ------------------------------------------------------------ batch Jobs
+    async def _sync_jobs(self):
+        """batch/v1 Jobs (arena workers) as run-to-completion processes:
+        ``parallelism`` pods at a time until ``completions`` succeeded; a failed
+        pod is retried until ``backoffLimit`` failures, then the Job is Failed.
+        Job ``status`` (active / succeeded / failed / conditions) is written back."""
+        from .pods import JobPodProcess
+
+        loop = asyncio.get_running_loop()
+        live = set()
+        for j in self.store.list("Job"):
+            ns, name = j["metadata"]["namespace"], j["metadata"]["name"]
+            key = (ns, name)
+            live.add(key)
+            spec = j["spec"]
+            st = self.jobs.setdefault(key, {"pods": [], "succeeded": 0, "failed": 0, "n": 0,
+                                            "done": False})
+            if st["done"]:
+                continue
+            want = int(spec.get("completions") or 1)
+            par = int(spec.get("parallelism") or 1)
+            backoff = int(spec.get("backoffLimit") if spec.get("backoffLimit") is not None else 6)
+            for p in list(st["pods"]):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                st["pods"].remove(p)
+                await loop.run_in_executor(None, p.stop)
+                if rc == 0:
+                    st["succeeded"] += 1
+                else:
+                    st["failed"] += 1
+            conds = []
+            if st["succeeded"] >= want:
+                conds = [{"type": "Complete", "status": "True"}]
+            elif st["failed"] > backoff:
+                conds = [{"type": "Failed", "status": "True", "reason": "BackoffLimitExceeded"}]
+            if conds:
+                for p in st["pods"]:
+                    await loop.run_in_executor(None, p.stop)
+                st["pods"], st["done"] = [], True
+            else:
+                tmpl = spec["template"]["spec"]
+                while len(st["pods"]) < min(par, want - st["succeeded"]):
+                    wd = tempfile.mkdtemp(prefix=f"omnia-job-{name}-")
+                    mounts = self._job_mounts(ns, tmpl, wd)
+                    st["n"] += 1
+                    pod = JobPodProcess(f"{name}-{st['n']}", tmpl["containers"][0], wd, mounts)
+                    try:
+                        await loop.run_in_executor(None, pod.start)
+                    except Exception:  # noqa: BLE001
+                        log.exception("job pod %s failed to start", pod.name)
+                        st["failed"] += 1
+                        break
+                    st["pods"].append(pod)
+            new = {"active": len(st["pods"]), "succeeded": st["succeeded"],
+                   "failed": st["failed"], **({"conditions": conds} if conds else {})}
+            if (j.get("status") or {}) != new:
+                j["status"] = new
+                j["metadata"].pop("resourceVersion", None)
+                self.store.update_status(j)
+        for key in [k for k in self.jobs if k not in live]:  # Job deleted: kill its pods
+            for p in self.jobs.pop(key)["pods"]:
+                await loop.run_in_executor(None, p.stop)
+
+    def _job_mounts(self, ns: str, tmpl: dict, workdir: str) -> dict[str, str]:
+        mounts = {}
+        vols = {v["name"]: v for v in tmpl.get("volumes", [])}
+        for vm in tmpl["containers"][0].get("volumeMounts", []):
+            v = vols.get(vm["name"]) or {}
+            local = os.path.join(workdir, vm["name"])
+            os.makedirs(local, exist_ok=True)
+            cm = v.get("configMap")
+            if cm:
+                obj = self.store.try_get("ConfigMap", cm["name"], ns)
+                for fname, content in ((obj or {}).get("data") or {}).items():
+                    with open(os.path.join(local, fname), "w") as f:
+                        f.write(content)
+            mounts[vm["mountPath"]] = local
+        return mounts
 
     # ------------------------------------------------------------ service pods
     SERVICE_COMPONENTS = ("session-api", "memory-api", "arena-dev-console")
@@ -285,6 +367,7 @@ class LocalLauncher:
         live = set()
         if self.mode == "process":
             await self._sync_services()
+            await self._sync_jobs()
         for d in deps:
             ns, name = d["metadata"]["namespace"], d["metadata"]["name"]
             replicas = d["spec"].get("replicas", 1)
@@ -393,3 +476,7 @@ class LocalLauncher:
         for sp, _ in self.services.values():
             sp.stop()
         self.services.clear()
+        for st in self.jobs.values():
+            for p in st["pods"]:
+                p.stop()
+        self.jobs.clear()

@@ -302,3 +302,57 @@ def resolve_service_urls(env: dict, lookup) -> dict:
         return f"{m.group(1)}{ep}" if ep else m.group(0)
 
     return {k: _SVC_URL.sub(sub, v) if isinstance(v, str) else v for k, v in env.items()}
+
+
+class JobPodProcess:
+    """One pod of a batch/v1 Job (arena workers) as a run-to-completion OS
+    process: the container's command + args + env, its ConfigMap volumes
+    materialised under a per-pod directory (``mountPath`` prefixes in env values
+    and args are rewritten to it)."""
+
+    def __init__(self, name: str, container: dict, workdir: str, mounts: dict[str, str],
+                 python: str = sys.executable):
+        self.name = name
+        self.container = container
+        self.workdir = workdir
+        self.mounts = mounts  # mountPath -> local dir
+        self.python = python
+        self.proc: subprocess.Popen | None = None
+        self._log = None
+
+    def _map(self, v: str) -> str:
+        for mp, local in self.mounts.items():
+            if v == mp or v.startswith(mp.rstrip("/") + "/"):
+                return local + v[len(mp.rstrip("/")):]
+        return v
+
+    def start(self) -> "JobPodProcess":
+        cmd = list(self.container.get("command") or []) + list(self.container.get("args") or [])
+        if cmd and cmd[0] in ("python", "python3"):
+            cmd[0] = self.python
+        cmd = [self._map(a) for a in cmd]
+        env = dict(os.environ)
+        for e in self.container.get("env", []):
+            if "value" in e:
+                env[e["name"]] = self._map(str(e["value"]))
+        env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+        env["HOSTNAME"] = self.name
+        os.makedirs(self.workdir, exist_ok=True)
+        self._log = open(os.path.join(self.workdir, "pod.log"), "wb")
+        self.proc = subprocess.Popen(cmd, env=env, stdout=self._log, stderr=subprocess.STDOUT,
+                                     cwd=ROOT, start_new_session=True)
+        return self
+
+    def poll(self) -> int | None:
+        return None if self.proc is None else self.proc.poll()
+
+    def stop(self):
+        if self.proc is not None and self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(10)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+        if self._log:
+            self._log.close()
+            self._log = None

@@ -306,7 +306,12 @@ class FacadeServer:
     async def start(self, host: str = "0.0.0.0", port: int | None = None) -> int:
         self.runner = web.AppRunner(self.app)
         await self.runner.setup()
-        site = web.TCPSite(self.runner, host, self.cfg.port if port is None else port)
+        # listen backlog sized for connection bursts: aiohttp's default of 128
+        # drops the SYNs of a burst of new sessions beyond it, and the kernel's
+        # 1 s SYN retransmit then delays their first turn (a 256-session wave
+        # otherwise loses ~1 s per wave); the kernel caps it at somaxconn
+        site = web.TCPSite(self.runner, host, self.cfg.port if port is None else port,
+                           backlog=max(1024, 2 * self.cfg.max_connections))
         await site.start()
         return site._server.sockets[0].getsockname()[1]
 

@@ -208,7 +208,7 @@ class MiniRedis:
         self.port = 0
 
     async def start(self, host="127.0.0.1", port=0):
-        self.server = await asyncio.start_server(self._handle, host, port)
+        self.server = await asyncio.start_server(self._handle, host, port, backlog=1024)
         self.port = self.server.sockets[0].getsockname()[1]
         return self
 

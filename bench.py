@@ -123,6 +123,7 @@ class WSDriver:
         self.tmp = tempfile.mkdtemp(prefix=f"omnia-bench-r{rank}-")
         self.rng = random.Random(1234 + rank)
         self.pod = None
+        self._ready = []  # pre-opened sessions for the next wave (one per virtual user)
         self.overhead = self._template_overhead()
         if a.prompt_len <= self.overhead:
             raise SystemExit(f"--prompt-len {a.prompt_len} must exceed the chat-template "
@@ -180,18 +181,34 @@ class WSDriver:
         # printable ASCII, one byte token each; fresh per turn (no cross-turn prefix reuse)
         return "".join(self.rng.choice("abcdefghijklmnopqrstuvwxyz ,.") for _ in range(n))
 
-    async def _turn(self, content: str):
+    async def _connect(self):
         from omnia_amd.ee.arena.fleet import FleetSession
 
-        async with FleetSession(self.pod.ws_url, http=self.http, timeout_s=600) as fs:
+        return await FleetSession(self.pod.ws_url, http=self.http, timeout_s=600).__aenter__()
+
+    async def _turn(self, content: str, fs=None, reconnect: bool = False):
+        """One turn on a fresh session.  A virtual user keeps its next session
+        open while it waits (``reconnect``): the WebSocket handshake of its next
+        turn overlaps the rest of this wave instead of stalling the next wave's
+        start (turn timing starts at the ``message`` frame either way)."""
+        fs = fs or await self._connect()
+        try:
             r = await fs.turn(content)
+        finally:
+            await fs.__aexit__(None, None, None)
+        if reconnect:
+            self._ready.append(await self._connect())
         u = r["usage"] or {}
         return (r["ttft_ms"] / 1e3, r["latency_ms"] / 1e3, int(u.get("output_tokens", 0)),
                 int(u.get("input_tokens", 0)), r["chunk_times_s"])
 
     async def _wave(self):
-        return await asyncio.gather(*(self._turn(self._content())
-                                      for _ in range(self.a.concurrency)))
+        ready, self._ready = self._ready, []
+        n = self.a.concurrency
+        return await asyncio.gather(*(self._turn(self._content(),
+                                                 ready[i] if i < len(ready) else None,
+                                                 reconnect=True)
+                                      for i in range(n)))
 
     def wave(self, step: int):
         if self.pod is None:
@@ -223,6 +240,13 @@ class WSDriver:
 
     def close(self):
         if self.pod is not None:
+            ready, self._ready = self._ready, []
+
+            async def _close_ready():
+                await asyncio.gather(*(fs.__aexit__(None, None, None) for fs in ready),
+                                     return_exceptions=True)
+
+            self.loop.run_until_complete(_close_ready())
             self.loop.run_until_complete(self.http.close())
             self.pod.stop()
             self.pod = None

@@ -288,7 +288,7 @@ class SourceReconciler:
             return None
         spec = o["spec"]
         st = dict(o.get("status") or {})
-        interval = parse_duration(spec.get("interval"), 300.0)
+        interval = parse_duration(spec.get("interval") or spec.get("syncInterval"), 300.0)
         if spec.get("suspend"):
             st["phase"] = "Suspended"
             set_condition(st, "Ready", False, "Suspended", "", o["metadata"]["generation"])
@@ -302,6 +302,8 @@ class SourceReconciler:
                     st["skillCount"] = sum(1 for _ in Path(art["path"]).rglob("SKILL.md"))
                 if self.kind == "PromptPackSource" and changed:
                     self._publish_pack(store, o, art)
+                if self.kind == "ArenaTemplateSource":
+                    self._scan_templates(o, art, st)
                 set_condition(st, "Ready", True, "Synced", f"revision {art['revision']}",
                               o["metadata"]["generation"])
             except (SyncError, subprocess.TimeoutExpired, OSError, ValueError, KeyError) as e:
@@ -312,6 +314,32 @@ class SourceReconciler:
         o["status"] = st
         store.update_status(o)
         return interval
+
+    def _scan_templates(self, src: dict, art: dict, st: dict):
+        """ArenaTemplateSource: discover the templates of the synced revision and
+        publish their index as ``<content root>/<ns>/.arena/template-index/<name>.json``
+        (``arenatemplatesource_controller.go`` ``writeTemplateIndex``)."""
+        import json as _json
+
+        from ..ee.arena.templates import discover
+
+        gen = src["metadata"]["generation"]
+        ts = discover(art["path"], (src.get("spec") or {}).get("templatesPath") or "templates")
+        ns = src["metadata"].get("namespace") or "default"
+        idx_dir = Path(self.syncer.root) / ns / ".arena" / "template-index"
+        idx_dir.mkdir(parents=True, exist_ok=True)
+        tmp = idx_dir / (src["metadata"]["name"] + ".json.tmp")
+        tmp.write_text(_json.dumps([t.to_json() for t in ts], indent=2))
+        os.replace(tmp, idx_dir / (src["metadata"]["name"] + ".json"))
+        st.update(templateCount=len(ts), headVersion=art["revision"],
+                  templateIndex=str(idx_dir / (src["metadata"]["name"] + ".json")),
+                  nextFetchTime=time.time() + parse_duration(
+                      (src.get("spec") or {}).get("interval") or
+                      (src.get("spec") or {}).get("syncInterval"), 300.0))
+        set_condition(st, "TemplatesScanned", True, "ScanComplete",
+                      f"Discovered {len(ts)} templates", gen)
+        set_condition(st, "ArtifactAvailable", True, "ArtifactStored",
+                      f"revision {art['revision']}", gen)
 
     @staticmethod
     def _publish_pack(store: APIStore, src: dict, art: dict):

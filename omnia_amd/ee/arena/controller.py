@@ -47,6 +47,20 @@ def load_arena_config(store, job: dict) -> dict:
         return yaml.safe_load(f) or {}
 
 
+def check_budget(limit, currency: str, total_cost: float) -> dict:
+    """``budget.go`` ``checkBudget``: result details when the job's total cost
+    exceeds ``loadTest.budgetLimit`` (the workers also stop claiming work once
+    their share is spent); {} otherwise or when no / an unparsable limit is set."""
+    try:
+        lim = float(limit) if limit not in (None, "") else None
+    except (TypeError, ValueError):
+        lim = None
+    if lim is None or total_cost <= lim:
+        return {}
+    return {"budgetBreached": "true", "totalCost": f"{total_cost:.2f}",
+            "budgetLimit": f"{lim:.2f}", "budgetCurrency": currency}
+
+
 def output_location(output: dict | None) -> dict | None:
     """``spec.output`` (``ee/api/v1alpha1/arenajob_types.go:197-257``) -> where a
     job's artefacts go: ``pvc`` = ``<OMNIA_PVC_ROOT>/<claimName>/<subPath>`` (the
@@ -254,11 +268,15 @@ class ArenaJobController:
                                     self._s3_creds(spec.get("output"),
                                                    md.get("namespace", "default")))
         phase = "Succeeded" if ok and stats.errors < max(1, stats.total) else "Failed"
+        budget = check_budget(lt.get("budgetLimit"), lt.get("budgetCurrency") or "USD",
+                              stats.total_cost)
         job = self.store.get("ArenaJob", md["name"], md.get("namespace", "default"))
         self._status(job, phase, progress={"total": len(items), "done": len(results)},
-                     results=stats.to_json(), thresholds=[str(v) for v in verdicts],
+                     results={**stats.to_json(), **budget},
+                     thresholds=[str(v) for v in verdicts],
                      completionTime=time.time(), message="thresholds " + (
-                         "passed" if ok else "failed"),
+                         "passed" if ok else "failed") + (
+                         "; budget exceeded" if budget else ""),
                      **({"dataset": dataset} if dataset else {}))
         return stats
 

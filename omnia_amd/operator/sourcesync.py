@@ -302,6 +302,9 @@ class SourceReconciler:
                     st["skillCount"] = sum(1 for _ in Path(art["path"]).rglob("SKILL.md"))
                 if self.kind == "PromptPackSource" and changed:
                     self._publish_pack(store, o, art)
+                if self.kind == "PromptPackSource":
+                    st["versionsDeleted"] = int(st.get("versionsDeleted", 0)) + \
+                        self._gc_pack_versions(store, o)
                 if self.kind == "ArenaTemplateSource":
                     self._scan_templates(o, art, st)
                 set_condition(st, "Ready", True, "Synced", f"revision {art['revision']}",
@@ -340,6 +343,43 @@ class SourceReconciler:
                       f"Discovered {len(ts)} templates", gen)
         set_condition(st, "ArtifactAvailable", True, "ArtifactStored",
                       f"revision {art['revision']}", gen)
+
+    MIN_RETENTION_S = float(os.environ.get("OMNIA_PACK_MIN_RETENTION_S", "0"))
+
+    def _gc_pack_versions(self, store: APIStore, src: dict) -> int:
+        """Keep the newest ``historyLimit`` published versions of the pack; older
+        ones go unless a PromptPack still points at them (``configMapRef``) or
+        they are younger than the minimum retention age
+        (``ee/internal/controller/promptpacksource_gc.go``)."""
+        ns = src["metadata"].get("namespace", "default")
+        pack = src["spec"]["packName"]
+        limit = max(0, int(src["spec"].get("historyLimit", 10)))
+        versions = [c for c in store.list("ConfigMap", ns)
+                    if (c["metadata"].get("labels") or {}).get(
+                        "omnia.altairalabs.ai/pack") == pack]
+        if len(versions) <= limit:
+            return 0
+        versions.sort(key=lambda c: (c["metadata"].get("creationTimestamp", ""),
+                                     int(c["metadata"].get("resourceVersion") or 0)),
+                      reverse=True)
+        used = {((pp.get("spec") or {}).get("source") or {}).get("configMapRef", {}).get("name")
+                for pp in store.list("PromptPack", ns)}
+        now = time.time()
+        deleted = 0
+        for c in versions[limit:]:
+            name = c["metadata"]["name"]
+            if name in used:
+                continue
+            created = c["metadata"].get("creationTimestamp")
+            if created and self.MIN_RETENTION_S > 0:
+                import calendar
+
+                t = calendar.timegm(time.strptime(created[:19], "%Y-%m-%dT%H:%M:%S"))
+                if now - t < self.MIN_RETENTION_S:
+                    continue
+            store.delete("ConfigMap", name, ns)
+            deleted += 1
+        return deleted
 
     @staticmethod
     def _publish_pack(store: APIStore, src: dict, art: dict):

@@ -112,3 +112,12 @@ def test_arena_job_runs_on_worker_pods():
     assert r["total"] == 6 and r["passed"] == 6, r
     assert st["workerJob"] == "arena-worker-eval1"
     assert kj["status"]["succeeded"] == 2 and kj["status"]["conditions"][0]["type"] == "Complete"
+
+
+def test_budget_check():
+    from omnia_amd.ee.arena.controller import check_budget
+
+    assert check_budget(None, "USD", 5.0) == {} and check_budget("x", "USD", 5.0) == {}
+    assert check_budget("10", "USD", 9.99) == {}
+    assert check_budget("1.5", "EUR", 2.0) == {"budgetBreached": "true", "totalCost": "2.00",
+                                                "budgetLimit": "1.50", "budgetCurrency": "EUR"}

@@ -127,3 +127,38 @@ def test_git_path_traversal_rejected(tmp_path, repo):
     rec.reconcile(store, "default", "t")
     st = store.get("SkillSource", "t", "default")["status"]
     assert st["phase"] == "Failed" and "escapes" in st["conditions"][0]["message"]
+
+
+def test_promptpack_source_publishes_and_gcs_versions(tmp_path):
+    """Every new revision of a PromptPackSource becomes a pack-version ConfigMap;
+    versions beyond historyLimit are deleted unless a PromptPack still uses
+    them (``promptpacksource_gc_test.go``)."""
+    from omnia_amd.operator.sourcesync import SourceReconciler
+
+    ws = tmp_path / "pack"
+    ws.mkdir()
+    store = APIStore()
+    store.objs[store.key("PromptPackSource", "default", "pps")] = {
+        "apiVersion": "omnia.altairalabs.ai/v1alpha1", "kind": "PromptPackSource",
+        "metadata": {"name": "pps", "namespace": "default", "generation": 1,
+                     "resourceVersion": "1", "uid": "u"},
+        "spec": {"type": "workspace", "workspace": {"path": str(ws)}, "packName": "support",
+                 "interval": "1m", "historyLimit": 2}}
+    rec = SourceReconciler("PromptPackSource", root=str(tmp_path / "content"))
+    names = []
+    for i in range(5):
+        (ws / "pack.json").write_text('{"id": "support", "version": "1.0.%d"}' % i)
+        rec.reconcile(store, "default", "pps")
+        cms = [c["metadata"]["name"] for c in store.list("ConfigMap", "default")]
+        names.append(sorted(cms))
+        if i == 1:
+            # a PromptPack pins the second version: it must survive GC
+            pinned = [n for n in cms if n not in names[0]][0]
+            store.objs[store.key("PromptPack", "default", "support")] = {
+                "apiVersion": "omnia.altairalabs.ai/v1alpha1", "kind": "PromptPack",
+                "metadata": {"name": "support", "namespace": "default"},
+                "spec": {"source": {"type": "configmap", "configMapRef": {"name": pinned}}}}
+    final = {c["metadata"]["name"] for c in store.list("ConfigMap", "default")}
+    assert pinned in final and len(final) == 3  # 2 newest + the pinned one
+    st = store.get("PromptPackSource", "pps", "default")["status"]
+    assert st["versionsDeleted"] == 2

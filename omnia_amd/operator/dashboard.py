@@ -16,9 +16,19 @@ one dependency-free page plus a small aiohttp backend:
   reference proxies through the dashboard's mgmt-plane twin; here the facade's
   own auth chain applies).
 
-Every ``/api/*`` route is read-only.  With ``--oidc-jwks-file`` the API
-requires an IdP-issued bearer JWT (RS256, issuer / audience checked) -- the
-dashboard holds no credentials of its own to lend to callers.
+Management writes (``--allow-writes``; off by default):
+
+* ``POST /api/resources/{plural}`` -- create an object from a JSON or YAML body
+  (the API server's admission -- schemas, CEL rules, webhooks -- applies);
+* ``DELETE /api/resources/{plural}/{ns}/{name}``;
+* ``POST /api/agents/{ns}/{name}/scale`` ``{"replicas": n}`` -- merge-patches
+  ``spec.runtime.replicas``;
+* ``POST /api/arena/jobs/{ns}/{name}/cancel`` -- sets ``spec.cancelled``.
+
+With ``--oidc-jwks-file`` every ``/api/*`` route requires an IdP-issued bearer
+JWT (RS256, issuer / audience checked) and the caller's bearer is forwarded to
+the API server, whose own authorisation decides writes -- the dashboard holds no
+credentials of its own to lend to callers.
 Run: ``python -m omnia_amd.operator.dashboard --port 3000 --api http://operator:8090``.
 """
 from __future__ import annotations
@@ -41,6 +51,8 @@ border:1px solid #ccc;padding:6px;white-space:pre-wrap}</style></head><body>
 <h2>Agents</h2><table id="agents"><tr><th>namespace</th><th>name</th><th>phase</th>
 <th>replicas</th><th>provider</th></tr></table>
 <h2>Resources</h2><select id="kind"></select><table id="res"></table>
+<h3>Apply</h3><textarea id="yaml" rows="8" cols="80" placeholder="YAML or JSON object"></textarea><br>
+<button onclick="applyObj()">create</button> <span id="applied"></span>
 <h2>Sessions</h2><table id="sess"><tr><th>id</th><th>agent</th><th>messages</th></tr></table>
 <pre id="msgs"></pre>
 <h2>Arena</h2><table id="arena"><tr><th>namespace</th><th>name</th><th>type</th><th>phase</th>
@@ -53,6 +65,9 @@ border:1px solid #ccc;padding:6px;white-space:pre-wrap}</style></head><body>
 <script>
 const KINDS=__KINDS__;let sock;
 async function j(u){const r=await fetch(u);return r.json()}
+async function applyObj(){const k=document.getElementById('kind').value;
+ const r=await fetch('/api/resources/'+k,{method:'POST',body:document.getElementById('yaml').value});
+ const o=await r.json();document.getElementById('applied').textContent=r.status+' '+(o.error||o.message||(o.metadata||{}).name||'')}
 async function agents(){const o=await j('/api/overview');const t=document.getElementById('agents');
  for(const a of o.agents){const r=t.insertRow();for(const v of [a.namespace,a.name,a.phase,a.replicas,a.provider])
  r.insertCell().textContent=v??''}}
@@ -103,8 +118,9 @@ def oidc_middleware(jwks: dict, issuer: str = "", audience: str = ""):
 
 
 def build_app(api: str, session_api: str = "", privacy_api: str = "",
-              oidc: dict | None = None) -> web.Application:
-    """``oidc``: ``{"jwks": {...}, "issuer": ..., "audience": ...}`` gates the API."""
+              oidc: dict | None = None, allow_writes: bool = False) -> web.Application:
+    """``oidc``: ``{"jwks": {...}, "issuer": ..., "audience": ...}`` gates the API;
+    ``allow_writes`` enables the management routes (module doc)."""
     mws = [oidc_middleware(oidc["jwks"], oidc.get("issuer", ""), oidc.get("audience", ""))] \
         if oidc else []
     app = web.Application(middlewares=mws)
@@ -114,6 +130,85 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
         async with aiohttp.ClientSession() as s:
             async with s.get(url, timeout=aiohttp.ClientTimeout(total=10)) as r:
                 return r.status, await r.json(content_type=None)
+
+    async def _send(request, method, url, body=None, ctype="application/json"):
+        hdrs = {"Content-Type": ctype}
+        auth = request.headers.get("Authorization")
+        if auth:
+            hdrs["Authorization"] = auth  # the API server authorises the caller
+        data = None if body is None else (body if isinstance(body, (bytes, str))
+                                          else json.dumps(body))
+        async with aiohttp.ClientSession() as s:
+            async with s.request(method, url, data=data, headers=hdrs,
+                                 timeout=aiohttp.ClientTimeout(total=10)) as r:
+                return r.status, await r.json(content_type=None)
+
+    def _writes_on():
+        if not allow_writes:
+            return web.json_response({"error": "dashboard is read-only "
+                                               "(start it with --allow-writes)"}, status=403)
+        return None
+
+    base = f"{api}/apis/{crds.GROUP}/{crds.VERSION}"
+
+    def _ns_url(plural, ns, name=""):
+        kind = next(k for k in crds.KINDS.values() if k.plural == plural)
+        root = f"{base}/namespaces/{ns}/{plural}" if kind.scope == "Namespaced" else \
+            f"{base}/{plural}"
+        return root + (f"/{urllib.parse.quote(name, safe='')}" if name else "")
+
+    async def create(request):
+        if (deny := _writes_on()) is not None:
+            return deny
+        plural = request.match_info["plural"]
+        if plural not in plurals:
+            return web.json_response({"error": "unknown resource"}, status=404)
+        raw = await request.text()
+        try:
+            import yaml
+
+            obj = yaml.safe_load(raw) if raw.strip() else None
+        except Exception as e:  # noqa: BLE001 - yaml.YAMLError and friends
+            return web.json_response({"error": f"unparsable body: {e}"}, status=400)
+        if not isinstance(obj, dict) or not (obj.get("metadata") or {}).get("name"):
+            return web.json_response({"error": "body must be one object with metadata.name"},
+                                     status=400)
+        ns = obj["metadata"].get("namespace") or "default"
+        st, body = await _send(request, "POST", _ns_url(plural, ns), obj)
+        return web.json_response(body, status=st)
+
+    async def delete(request):
+        if (deny := _writes_on()) is not None:
+            return deny
+        plural, ns, name = (request.match_info[k] for k in ("plural", "ns", "name"))
+        if plural not in plurals:
+            return web.json_response({"error": "unknown resource"}, status=404)
+        st, body = await _send(request, "DELETE", _ns_url(plural, ns, name))
+        return web.json_response(body, status=st)
+
+    async def scale(request):
+        if (deny := _writes_on()) is not None:
+            return deny
+        try:
+            n = int((await request.json())["replicas"])
+            if n < 0:
+                raise ValueError
+        except (KeyError, ValueError, TypeError, json.JSONDecodeError):
+            return web.json_response({"error": "body must be {\"replicas\": n >= 0}"},
+                                     status=400)
+        ns, name = request.match_info["ns"], request.match_info["name"]
+        st, body = await _send(request, "PATCH", _ns_url("agentruntimes", ns, name),
+                               {"spec": {"runtime": {"replicas": n}}},
+                               "application/merge-patch+json")
+        return web.json_response(body, status=st)
+
+    async def cancel_job(request):
+        if (deny := _writes_on()) is not None:
+            return deny
+        ns, name = request.match_info["ns"], request.match_info["name"]
+        st, body = await _send(request, "PATCH", _ns_url("arenajobs", ns, name),
+                               {"spec": {"cancelled": True}}, "application/merge-patch+json")
+        return web.json_response(body, status=st)
 
     async def page(_):
         return web.Response(text=PAGE.replace("__KINDS__", json.dumps(plurals)),
@@ -182,6 +277,10 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
     app.router.add_get("/api/arena/jobs", arena_jobs)
     app.router.add_get("/api/consent/{user}", consent)
     app.router.add_get("/healthz", healthz)
+    app.router.add_post("/api/resources/{plural}", create)
+    app.router.add_delete("/api/resources/{plural}/{ns}/{name}", delete)
+    app.router.add_post("/api/agents/{ns}/{name}/scale", scale)
+    app.router.add_post("/api/arena/jobs/{ns}/{name}/cancel", cancel_job)
     return app
 
 
@@ -195,6 +294,8 @@ def main(argv=None):
     ap.add_argument("--oidc-jwks-file", default="", help="IdP JWKS; gates /api/* when set")
     ap.add_argument("--oidc-issuer", default="")
     ap.add_argument("--oidc-audience", default="")
+    ap.add_argument("--allow-writes", action="store_true",
+                    help="enable create / delete / scale / cancel routes")
     a = ap.parse_args(argv)
     oidc = None
     if a.oidc_jwks_file:
@@ -202,7 +303,8 @@ def main(argv=None):
             oidc = {"jwks": json.load(f), "issuer": a.oidc_issuer, "audience": a.oidc_audience}
 
     async def run():
-        runner = web.AppRunner(build_app(a.api, a.session_api, a.privacy_api, oidc))
+        runner = web.AppRunner(build_app(a.api, a.session_api, a.privacy_api, oidc,
+                                         allow_writes=a.allow_writes))
         await runner.setup()
         await web.TCPSite(runner, a.host, a.port).start()
         await asyncio.Event().wait()

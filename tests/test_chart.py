@@ -182,3 +182,54 @@ def test_dashboard_views_and_oidc_gate():
             await sides.close()
 
     asyncio.run(run())
+
+
+def test_dashboard_management_writes():
+    """--allow-writes: create from YAML (admission applies), scale an agent,
+    cancel an arena job, delete; read-only by default."""
+    from aiohttp.test_utils import TestClient, TestServer
+
+    from omnia_amd.operator.apiserver import build_app as api_app
+    from omnia_amd.operator.apistore import APIStore
+    from omnia_amd.operator.dashboard import build_app
+
+    prov = ("apiVersion: %s\nkind: Provider\nmetadata: {name: p1, namespace: default}\n"
+            "spec: {type: mock}\n" % crds.API_VERSION)
+
+    async def run():
+        store = APIStore()
+        store.objs[store.key("AgentRuntime", "default", "a1")] = {
+            "apiVersion": crds.API_VERSION, "kind": "AgentRuntime",
+            "metadata": {"name": "a1", "namespace": "default", "generation": 1,
+                         "resourceVersion": "1", "uid": "u1"},
+            "spec": {"promptPackRef": {"name": "pack"}, "facades": [{"type": "websocket"}],
+                     "runtime": {"replicas": 1}}}
+        api = TestServer(api_app(store))
+        await api.start_server()
+        url = str(api.make_url("")).rstrip("/")
+        ro = TestClient(TestServer(build_app(url)))
+        rw = TestClient(TestServer(build_app(url, allow_writes=True)))
+        await ro.start_server()
+        await rw.start_server()
+        try:
+            assert (await ro.post("/api/resources/providers", data=prov)).status == 403
+            r = await rw.post("/api/resources/providers", data=prov)
+            assert r.status in (200, 201), await r.text()
+            assert store.try_get("Provider", "p1", "default") is not None
+            bad = prov.replace("type: mock", "type: nosuchtype")
+            r = await rw.post("/api/resources/providers", data=bad.replace("p1", "p2"))
+            assert r.status >= 400  # the API server's admission rejected it
+            assert (await rw.post("/api/resources/providers", data="- a\n- b")).status == 400
+            r = await rw.post("/api/agents/default/a1/scale", json={"replicas": 3})
+            assert r.status == 200, await r.text()
+            assert store.get("AgentRuntime", "a1", "default")["spec"]["runtime"]["replicas"] == 3
+            assert (await rw.post("/api/agents/default/a1/scale", json={"replicas": -1})
+                    ).status == 400
+            r = await rw.delete("/api/resources/providers/default/p1")
+            assert r.status == 200 and store.try_get("Provider", "p1", "default") is None
+        finally:
+            await ro.close()
+            await rw.close()
+            await api.close()
+
+    asyncio.run(run())

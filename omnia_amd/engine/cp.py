@@ -47,7 +47,8 @@ def run_cp_prefill(runner, seq, L: int, owner: int, group) -> int | None:
     ids = torch.zeros(cp.L_pad, dtype=torch.int64, device=dev)
     if is_owner:
         ids[:L] = torch.tensor(seq.all_tokens[:L], dtype=torch.int64)
-    dist.broadcast(ids, granks[owner], group=group)
+    if world > 1:
+        dist.broadcast(ids, granks[owner], group=group)
     fb = ForwardBatch(input_ids=ids.index_select(0, cp.index).to(torch.int32),
                       positions=cp.positions, slots=cp.slots, block_tables=None,
                       seq_lens=None, logits_indices=None, is_decode=False, cp=cp)
@@ -55,7 +56,8 @@ def run_cp_prefill(runner, seq, L: int, owner: int, group) -> int | None:
     holder, row = cp.locate(L - 1)
     last = h[row:row + 1].contiguous() if rank == holder else torch.empty(
         1, h.shape[1], dtype=h.dtype, device=dev)
-    dist.broadcast(last, granks[holder], group=group)
+    if world > 1:
+        dist.broadcast(last, granks[holder], group=group)
     runner.stats["cp_prefills"] = runner.stats.get("cp_prefills", 0) + 1
     if not is_owner:
         return None

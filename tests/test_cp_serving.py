@@ -199,3 +199,59 @@ def test_paged_ring_kernel_lse_on_gpu():
                                                lb[i * c:(i + 1) * c])
         err = (out - ref[shards[r]]).abs().max().item()
         assert err < 3e-2, (r, err)
+
+
+def _cp_oracle(device):
+    """A long prompt prefilled through the CP path (ring of one rank: scratch
+    pages, prefill kernel with LSE + key cap, owner page copy, last-hidden
+    pick), then decoded normally from the copied KV; every logit row is checked
+    against the fp32 dense forward of the same weights."""
+    import random
+    import socket as _s
+    import time as _time
+
+    import torch.distributed as dist
+
+    from omnia_amd.engine.cp import run_cp_prefill
+    from omnia_amd.engine.sampling_params import SamplingParams
+    from omnia_amd.models.config import resolve
+    import sys as _sys
+
+    _sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_model_correctness import _check, _engine
+
+    if not dist.is_initialized():
+        with _s.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1)
+    try:
+        mc = resolve("tiny-llama")
+        torch.manual_seed(0)
+        eng = _engine(device, mc, 256)
+        eng.scheduler.cfg.cp_threshold = 64
+        rng = random.Random(11)
+        prompt = [rng.randrange(10, mc.vocab_size - 10) for _ in range(709)]
+        s = eng.add_request(prompt, SamplingParams(temperature=0.0, max_tokens=6,
+                                                   ignore_eos=True))
+        assert eng.scheduler.cp_candidate() is s
+        tok = run_cp_prefill(eng.runner, s, s.length, 0, dist.group.WORLD)
+        for x, t in eng.scheduler.cp_done(s, tok):
+            eng._append(x, t, _time.perf_counter())
+        eng.run_until_done()
+        assert len(s.output) == 6 and eng.runner.stats["cp_prefills"] == 1
+        frac, worst = _check(mc, eng.model.w, [s], eng.runner.logit_tap, 0.03)
+        assert frac == 1.0, worst
+        return worst
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cp_prefill_matches_dense_oracle_cpu():
+    _cp_oracle("cpu")
+
+
+@pytest.mark.gpu
+def test_cp_prefill_matches_dense_oracle_gpu():
+    _cp_oracle("cuda")

@@ -47,6 +47,63 @@ def load_arena_config(store, job: dict) -> dict:
         return yaml.safe_load(f) or {}
 
 
+class JobInvalid(ValueError):
+    """The job cannot run as specified (license limits, missing provider groups)."""
+
+
+def select_scenarios(scenarios: dict, sel: dict | None) -> dict:
+    """``spec.scenarios.include`` / ``exclude`` glob patterns over scenario ids."""
+    import fnmatch
+
+    sel = sel or {}
+    inc, exc = sel.get("include") or ["*"], sel.get("exclude") or []
+    return {k: v for k, v in scenarios.items()
+            if any(fnmatch.fnmatchcase(k, p) for p in inc)
+            and not any(fnmatch.fnmatchcase(k, p) for p in exc)}
+
+
+def required_provider_groups(cfg: dict) -> list[str]:
+    """Provider groups the arena config needs (``arena_config_validation.go``):
+    every provider's ``group`` (default "default") plus self-play role providers."""
+    groups = {(p.get("group") or "default") for p in cfg.get("providers", [])}
+    sp = cfg.get("self_play") or {}
+    if sp.get("enabled"):
+        groups |= {r["provider"] for r in sp.get("roles") or [] if r.get("provider")}
+    return sorted(groups)
+
+
+def validate_job(spec: dict, cfg: dict, scenarios: dict, lic=None, source_type: str = ""):
+    """License gates and provider-group coverage; raises :class:`JobInvalid`."""
+    errs = []
+    if lic is not None:
+        jt = spec.get("type", "evaluation")
+        if not lic.can_use_job_type(jt):
+            errs.append(f"job type {jt!r} requires an enterprise license")
+        reps = int((spec.get("workers") or {}).get("replicas") or 1)
+        if not lic.can_use_worker_replicas(reps):
+            errs.append(f"{reps} worker replicas exceed the license limit "
+                        f"({lic.limits.maxWorkerReplicas})")
+        if not lic.can_use_scenario_count(len(scenarios)):
+            errs.append(f"{len(scenarios)} scenarios exceed the license limit "
+                        f"({lic.limits.maxScenarios})")
+        if source_type and not lic.can_use_source_type(source_type) and \
+                source_type != "workspace":
+            errs.append(f"source type {source_type!r} requires an enterprise license")
+        if spec.get("schedule") and not lic.can_use_scheduling():
+            errs.append("scheduled jobs require an enterprise license")
+    pg = spec.get("providers")
+    if pg:
+        need = required_provider_groups(cfg)
+        missing = [g for g in need if not pg.get(g)]
+        if missing:
+            errs.append(f"arena config needs provider groups {', '.join(need)}; "
+                        f"missing in spec.providers: {', '.join(missing)}")
+    if not scenarios:
+        errs.append("no scenarios selected")
+    if errs:
+        raise JobInvalid("; ".join(errs))
+
+
 def check_budget(limit, currency: str, total_cost: float) -> dict:
     """``budget.go`` ``checkBudget``: result details when the job's total cost
     exceeds ``loadTest.budgetLimit`` (the workers also stop claiming work once
@@ -161,7 +218,7 @@ class ArenaJobController:
                 "secret_key": data.get("AWS_SECRET_ACCESS_KEY") or data.get("secret-key", "")}
 
     def __init__(self, store, queue, provider_objects: dict | None = None,
-                 worker_mode: str = "inproc", redis_url: str = "",
+                 worker_mode: str = "inproc", redis_url: str = "", license=None,
                  worker_image: str = "ghcr.io/altairalabs/omnia-arena-worker:latest",
                  poll_s: float = 2.0):
         """``worker_mode`` "inproc": worker tasks on this event loop (single
@@ -173,6 +230,7 @@ class ArenaJobController:
         self.tasks: dict[str, asyncio.Task] = {}
         self.worker_mode = worker_mode
         self.redis_url = redis_url
+        self.license = license  # ee/license.License (or a Validator); None = no gates
         self.worker_image = worker_image
         self.poll_s = poll_s
 
@@ -200,6 +258,13 @@ class ArenaJobController:
     async def _run(self, job):
         try:
             return await self._run_inner(job)
+        except JobInvalid as e:
+            cur = self.store.try_get("ArenaJob", job["metadata"]["name"],
+                                     job["metadata"].get("namespace", "default"))
+            if cur is not None:
+                self._status(cur, "Failed", message=str(e)[:500], completionTime=time.time(),
+                             reason="ValidationFailed")
+            return None
         except Exception as e:  # noqa: BLE001 - surfaced in status, not lost in a task
             log.exception("arena job %s failed", job["metadata"]["name"])
             cur = self.store.try_get("ArenaJob", job["metadata"]["name"],
@@ -211,6 +276,15 @@ class ArenaJobController:
     async def _run_inner(self, job):
         md, spec = job["metadata"], job["spec"]
         cfg = load_arena_config(self.store, job)
+        cfg["scenarios"] = list(select_scenarios(
+            {s_["id"]: s_ for s_ in cfg.get("scenarios", [])}, spec.get("scenarios")).values())
+        lic = self.license
+        if lic is not None and hasattr(lic, "get_or_default"):
+            lic = lic.get_or_default()
+        src = self.store.try_get("ArenaSource", spec["sourceRef"]["name"],
+                                 md.get("namespace", "default")) or {}
+        validate_job(spec, cfg, cfg["scenarios"], lic,
+                     (src.get("spec") or {}).get("type", ""))
         if self.worker_mode == "pods":
             return await self._run_pods(job, cfg)
         scenarios = {s["id"]: s for s in cfg.get("scenarios", [])}
@@ -448,8 +522,11 @@ class ArenaJobReconciler:
 
     def reconcile(self, store, ns, name):
         if self.ctl is None:
+            from ...operator import manager as _mgr
+
             self.ctl = ArenaJobController(store, self.queue, self.provider_objects,
-                                          worker_mode=self.worker_mode, redis_url=self.redis_url)
+                                          worker_mode=self.worker_mode, redis_url=self.redis_url,
+                                          license=getattr(_mgr, "_LICENSE", None))
         try:
             store.get("ArenaJob", name, ns or "default")
         except KeyError:

@@ -7,6 +7,7 @@ the controller aggregates results and thresholds from the queue."""
 import asyncio
 import json
 
+import pytest
 import yaml
 
 from omnia_amd.ee.arena.controller import ArenaJobController
@@ -121,3 +122,50 @@ def test_budget_check():
     assert check_budget("10", "USD", 9.99) == {}
     assert check_budget("1.5", "EUR", 2.0) == {"budgetBreached": "true", "totalCost": "2.00",
                                                 "budgetLimit": "1.50", "budgetCurrency": "EUR"}
+
+
+def test_scenario_selection_and_job_validation():
+    from omnia_amd.ee import license as L
+    from omnia_amd.ee.arena.controller import (JobInvalid, required_provider_groups,
+                                               select_scenarios, validate_job)
+
+    sc = {"greet": {}, "greet-2": {}, "load": {}}
+    assert set(select_scenarios(sc, {"include": ["greet*"], "exclude": ["*-2"]})) == {"greet"}
+    assert set(select_scenarios(sc, None)) == set(sc)
+    cfg = {"providers": [{"id": "a"}, {"id": "b", "group": "judges"}],
+           "self_play": {"enabled": True, "roles": [{"id": "u", "provider": "persona"}]}}
+    assert required_provider_groups(cfg) == ["default", "judges", "persona"]
+    with pytest.raises(JobInvalid, match="missing in spec.providers: persona"):
+        validate_job({"providers": {"default": ["x"], "judges": ["y"]}}, cfg, sc)
+    validate_job({"providers": {"default": ["x"], "judges": ["y"], "persona": ["p"]}}, cfg, sc)
+    oc = L.open_core_license()
+    with pytest.raises(JobInvalid, match="loadtest"):
+        validate_job({"type": "loadtest"}, {}, sc, oc)
+    with pytest.raises(JobInvalid, match="source type 'oci'"):
+        validate_job({"type": "evaluation"}, {}, sc, oc, "oci")
+    with pytest.raises(JobInvalid, match="worker replicas exceed"):
+        validate_job({"workers": {"replicas": 4}}, {}, sc, oc)
+    validate_job({"type": "evaluation"}, {}, sc, oc, "git")  # open core allows git
+    with pytest.raises(JobInvalid, match="no scenarios"):
+        validate_job({}, {}, {})
+
+
+def test_invalid_job_fails_with_reason():
+    from omnia_amd.ee import license as L
+    from omnia_amd.ee.arena.queue import MemoryQueue
+
+    store = APIStore()
+    _setup(store)  # a loadtest-capable config run as type "evaluation" ...
+    job = store.get("ArenaJob", "eval1", "default")
+    job["spec"]["type"] = "loadtest"  # ... switched to loadtest under open core
+    store.objs[store.key("ArenaJob", "default", "eval1")] = job
+
+    async def go():
+        ctl = ArenaJobController(store, MemoryQueue(), license=L.open_core_license())
+        await ctl.reconcile("default", "eval1")
+        await ctl.tasks["eval1"]
+
+    asyncio.run(go())
+    st = store.get("ArenaJob", "eval1", "default")["status"]
+    assert st["phase"] == "Failed" and st["reason"] == "ValidationFailed"
+    assert "enterprise license" in st["message"]

@@ -237,8 +237,14 @@ class SessionPrivacyPolicyReconciler:
         if prog.get("status") == "InProgress":
             return self._reencrypt_batch(store, pol)
         ann = pol["metadata"].get("annotations") or {}
+        if ROTATE_KEY_ANNOTATION in ann and krs.get("handledRotateRequest") == \
+                f"{ann[ROTATE_KEY_ANNOTATION]}@{pol['metadata'].get('uid', '')}":
+            ann = {}  # this request was already served (its removal failed): no re-rotation
         if ROTATE_KEY_ANNOTATION in ann:
             ok = self._rotate(store, pol, "annotation")
+            if ok:
+                krs["handledRotateRequest"] = \
+                    f"{ann[ROTATE_KEY_ANNOTATION]}@{pol['metadata'].get('uid', '')}"
             # clear the trigger (metadata update; status is written by the caller)
             cur = store.try_get(self.kind, pol["metadata"]["name"], pol["metadata"].get(
                 "namespace"))

@@ -203,7 +203,8 @@ class LocalLauncher:
                     wd = tempfile.mkdtemp(prefix=f"omnia-job-{name}-")
                     mounts = self._job_mounts(ns, tmpl, wd)
                     st["n"] += 1
-                    pod = JobPodProcess(f"{name}-{st['n']}", tmpl["containers"][0], wd, mounts)
+                    pod = JobPodProcess(f"{name}-{st['n']}",
+                                        self._resolve_env(ns, tmpl["containers"][0]), wd, mounts)
                     try:
                         await loop.run_in_executor(None, pod.start)
                     except Exception:  # noqa: BLE001
@@ -220,6 +221,35 @@ class LocalLauncher:
         for key in [k for k in self.jobs if k not in live]:  # Job deleted: kill its pods
             for p in self.jobs.pop(key)["pods"]:
                 await loop.run_in_executor(None, p.stop)
+
+    def _resolve_env(self, ns: str, container: dict) -> dict:
+        """Container copy whose ``secretKeyRef`` / ``configMapKeyRef`` env entries
+        carry their values (what the kubelet injects); missing optional keys are
+        dropped, a missing required key fails the pod start."""
+        import base64
+        import copy
+
+        c = copy.deepcopy(container)
+        env = []
+        for e in c.get("env", []):
+            vf = e.get("valueFrom") or {}
+            ref = vf.get("secretKeyRef") or vf.get("configMapKeyRef")
+            if not ref:
+                env.append(e)
+                continue
+            kind = "Secret" if "secretKeyRef" in vf else "ConfigMap"
+            obj = self.store.try_get(kind, ref.get("name", ""), ns) or {}
+            val = (obj.get("stringData") or {}).get(ref.get("key"))
+            if val is None and ref.get("key") in (obj.get("data") or {}):
+                raw = obj["data"][ref["key"]]
+                val = base64.b64decode(raw).decode() if kind == "Secret" else raw
+            if val is None:
+                if ref.get("optional"):
+                    continue
+                raise KeyError(f"{kind} {ref.get('name')}/{ref.get('key')} not found")
+            env.append({"name": e["name"], "value": val})
+        c["env"] = env
+        return c
 
     def _job_mounts(self, ns: str, tmpl: dict, workdir: str) -> dict[str, str]:
         mounts = {}

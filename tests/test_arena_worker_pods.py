@@ -169,3 +169,22 @@ def test_invalid_job_fails_with_reason():
     st = store.get("ArenaJob", "eval1", "default")["status"]
     assert st["phase"] == "Failed" and st["reason"] == "ValidationFailed"
     assert "enterprise license" in st["message"]
+
+
+def test_launcher_resolves_secret_env_for_job_pods():
+    import base64
+
+    store = APIStore()
+    store.create({"apiVersion": "v1", "kind": "Secret",
+                  "metadata": {"name": "k", "namespace": "default"},
+                  "data": {"api-key": base64.b64encode(b"sk-123").decode()}})
+    launcher = LocalLauncher(store, mode="process")
+    c = {"env": [{"name": "A", "value": "1"},
+                 {"name": "KEY", "valueFrom": {"secretKeyRef": {"name": "k", "key": "api-key"}}},
+                 {"name": "OPT", "valueFrom": {"secretKeyRef": {"name": "nope", "key": "x",
+                                                                "optional": True}}}]}
+    out = launcher._resolve_env("default", c)
+    assert out["env"] == [{"name": "A", "value": "1"}, {"name": "KEY", "value": "sk-123"}]
+    with pytest.raises(KeyError):
+        launcher._resolve_env("default", {"env": [{"name": "X", "valueFrom": {
+            "secretKeyRef": {"name": "nope", "key": "x"}}}]})

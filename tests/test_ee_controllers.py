@@ -266,3 +266,23 @@ def test_policy_without_rotation_is_just_active():
     assert rec.reconcile(store, "default", "p") is None
     st = store.get("SessionPrivacyPolicy", "p", "default")["status"]
     assert st["phase"] == "Active" and get_condition({"status": st}, "Ready")["reason"] == "PolicyValidated"
+
+
+def test_rotate_request_is_served_once_even_if_annotation_sticks(tmp_path):
+    """If clearing the annotation fails, the same request must not rotate again."""
+    keyfile = str(tmp_path / "keys.json")
+    store = APIStore()
+    rec = SessionPrivacyPolicyReconciler(provider_factory=lambda cfg: LocalKMS(path=keyfile))
+    _put(store, _spp({"enabled": True}, annotations={ROTATE_KEY_ANNOTATION: "r1"}))
+    orig = store.update
+
+    def no_meta_updates(obj, subresource=None, **kw):
+        if subresource is None:
+            raise RuntimeError("conflict")
+        return orig(obj, subresource=subresource, **kw)
+
+    store.update = no_meta_updates
+    rec.reconcile(store, "default", "privacy")
+    rec.reconcile(store, "default", "privacy")
+    krs = store.get("SessionPrivacyPolicy", "privacy", "default")["status"]["keyRotation"]
+    assert krs["currentKeyVersion"] == "2"  # not 3

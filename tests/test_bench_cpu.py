@@ -47,3 +47,29 @@ def test_tp2_pod_serves_over_ws():
     assert rec["config"]["parallelism"] == "dp1-tp2" and rec["n_gpus"] == 2
     assert rec["turns"] == 2 and rec["per_rank_tokens_per_s"][1] == 0.0
     assert rec["value"] > 0
+
+
+def test_driver_torchrun_invocation_two_ranks():
+    """The driver's exact N>1 launch: torch.distributed.run starts one rank per
+    GPU with RANK/WORLD_SIZE set; bench.py must not spawn ranks again, and rank 0
+    prints one aggregated line."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--device", "cpu",
+                        "--model", "tiny-llama", "--prompt-len", "96", "--gen-len", "6",
+                        "--concurrency", "3"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["steps"] == 2
+    assert len(rec["per_rank_tokens_per_s"]) == 2 and rec["config"]["parallelism"] == "dp2"

@@ -170,3 +170,89 @@ def test_miniredis_streams_consumer_group():
 
     v, n, acked, again = asyncio.run(go())
     assert v == b"v" and n == 2 and acked == 2 and again is None
+
+
+# ------------------------------------------------------------------ service semantics
+def _svc2():
+    from omnia_amd.session.store import TieredSessionService, WarmStore
+
+    events = []
+
+    async def pub(ev):
+        events.append(ev)
+
+    return TieredSessionService(warm=WarmStore(), publisher=pub), events
+
+
+def test_append_accounting_sequence_and_events():
+    import asyncio
+
+    from omnia_amd.session.model import Message, Session
+
+    svc, events = _svc2()
+    s0 = svc.create(Session(id="s1", agent_name="a", namespace="ns"))
+    assert svc.create(Session(id="s1", agent_name="other")) is not None  # idempotent
+    assert svc.get("s1")[0].agent_name == "a"
+    for i in range(3):
+        asyncio.run(svc.append_message("s1", Message(
+            role="user" if i % 2 == 0 else "assistant", content=f"m{i}" * 100,
+            input_tokens=10, output_tokens=5, cost_usd=0.01)))
+    s, msgs = svc.get("s1")
+    assert [m.sequence_num for m in msgs] == [0, 1, 2] and s.message_count == 3
+    assert (s.total_input_tokens, s.total_output_tokens) == (30, 15)
+    assert abs(s.estimated_cost_usd - 0.03) < 1e-9 and len(s.last_message_preview) == 120
+    assert [e["type"] for e in events] == ["message.appended"] * 3
+    assert events[0]["namespace"] == "ns" and events[1]["role"] == "assistant"
+    # hot cache dropped: the warm tier answers with the same view
+    svc.hot.invalidate("s1")
+    s2, msgs2 = svc.get("s1")
+    assert s2.message_count == 3 and [m.content for m in msgs2] == [m.content for m in msgs]
+    with pytest.raises(KeyError):
+        asyncio.run(svc.append_message("nope", Message(content="x")))
+    assert s0.expires_at > 0  # default TTL applied on create
+
+
+def test_status_ttl_decorate_delete_and_tool_calls():
+    import time
+
+    from omnia_amd.session.model import Session, ToolCall
+
+    svc, _ = _svc2()
+    svc.create(Session(id="s2", agent_name="a", namespace="ns"))
+    svc.record("tool_calls", "s2", ToolCall(name="search", status="success"))
+    svc.record("tool_calls", "s2", ToolCall(name="fetch", status="error"))
+    s, _ = svc.get("s2")
+    assert s.tool_call_count == 2
+    assert [r["name"] for r in svc.warm.list_rows("tool_calls", "s2")] == ["search", "fetch"]
+    t = time.time()
+    s = svc.update_status("s2", "completed", ended_at=t)
+    assert s.status == "completed" and s.ended_at == t
+    s = svc.refresh_ttl("s2", 60)
+    assert 55 < s.expires_at - time.time() <= 61
+    s = svc.decorate("s2", tags=["vip"], state={"k": 1})
+    assert "vip" in s.tags and s.state.get("k") == 1
+    assert svc.delete("s2") and svc.get("s2") is None
+    with pytest.raises(KeyError):
+        svc.record("tool_calls", "s2", ToolCall(name="x"))
+
+
+def test_list_sessions_filters_and_search():
+    import asyncio
+
+    from omnia_amd.session.model import Message, Session
+
+    svc, _ = _svc2()
+    base = 1_700_000_000.0
+    for i in range(6):
+        svc.create(Session(id=f"q{i}", agent_name="a" if i % 2 else "b",
+                           namespace="ns1" if i < 4 else "ns2", created_at=base + i))
+    asyncio.run(svc.append_message("q3", Message(content="the refund policy")))
+    w = svc.warm
+    assert {s.id for s in w.list_sessions(namespace="ns1")} == {"q0", "q1", "q2", "q3"}
+    assert {s.id for s in w.list_sessions(namespace="ns1", agent="a")} == {"q1", "q3"}
+    assert [s.id for s in w.list_sessions(after=base + 3.5)] == ["q5", "q4"]  # newest first
+    assert [s.id for s in w.list_sessions(before=base + 1.5)] == ["q1", "q0"]
+    assert [s.id for s in w.list_sessions(q="refund")] == ["q3"]
+    page1 = [s.id for s in w.list_sessions(limit=2)]
+    page2 = [s.id for s in w.list_sessions(limit=2, offset=2)]
+    assert page1 == ["q5", "q4"] and page2 == ["q3", "q2"]

@@ -262,8 +262,11 @@ class Agent:
         if strategy == "custom":
             log.warning("custom truncation strategy not supported; falling back to sliding")
             strategy = "sliding"
+        pinned = []  # a summary of dropped turns stays, like the system prompt
         if strategy == "summarize" and len(rest) > 2:
             cut = len(rest) // 2
+            while cut < len(rest) and rest[cut].role == "tool":
+                cut += 1  # never separate a tool call from its results
             old, keep = rest[:cut], rest[cut:]
             convo = "\n".join(f"{m.role}: {m.content}" for m in old)
             try:
@@ -273,16 +276,18 @@ class Agent:
                     params=SamplingParams(temperature=0.0, max_tokens=128))
             except Exception:  # noqa: BLE001
                 summary = ""
-            rest = [Message("system", f"Summary of earlier conversation: {summary}")] + keep
-            msgs = system + rest
+            pinned = [Message("system", f"Summary of earlier conversation: {summary}")]
+            rest = keep
+            msgs = system + pinned + rest
             if sum(self._count(m) for m in msgs) <= budget:
                 return msgs
-        # sliding: drop oldest non-system messages (keep tool call/result pairs together)
-        while rest and sum(self._count(m) for m in system + rest) > budget:
-            drop = rest.pop(0)
-            while rest and rest[0].role == "tool" and drop.role == "assistant":
+        # sliding: drop oldest non-system messages; a tool result never survives
+        # without the assistant message that called it
+        while rest and sum(self._count(m) for m in system + pinned + rest) > budget:
+            rest.pop(0)
+            while rest and rest[0].role == "tool":
                 rest.pop(0)
-        return system + rest
+        return system + pinned + rest
 
     # ------------------------------------------------------------ the turn
     async def run_turn(self, session_id: str, content: str, io: TurnIO, parts: list | None = None,

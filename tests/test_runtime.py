@@ -279,3 +279,54 @@ def test_stream_interval_coalesces_chunks():
     assert len(per_delta) == 30 and "".join(per_delta) == words
     assert "".join(merged) == words and merged[0] == "w0"
     assert 2 <= len(merged) < 15
+
+
+# ------------------------------------------------------------------ context window
+class _WordTok:
+    def encode(self, s):
+        return s.split()
+
+
+def _agent_with(truncation, window, summary="the user asked about weather"):
+    from omnia_amd.runtime.agent import Agent, AgentConfig
+
+    class _Summ(MockProvider):
+        async def complete(self, msgs, params=None, **kw):
+            return summary, None, None
+
+    a = Agent(PromptPack(PACK), _Summ(scenarios=SCEN), MemoryContextStore(), None,
+              AgentConfig(context_window=window, truncation=truncation), tokenizer=_WordTok())
+    return a
+
+
+def _msgs():
+    from omnia_amd.runtime.chat import Message
+
+    return [Message("system", "sys prompt"), Message("user", "one two three"),
+            Message("assistant", "call tool"), Message("tool", "tool result here"),
+            Message("user", "four five"), Message("assistant", "six")]
+
+
+def test_sliding_window_keeps_system_and_tool_pairs():
+    a = _agent_with("sliding", 0)
+    assert len(_run_sync(a._truncate(_msgs(), 0))) == len(_msgs())  # 0 = unlimited
+    full = _msgs()
+    assert [m.content for m in _run_sync(a._truncate(full, 10_000))] == [m.content for m in full]
+    out = _run_sync(a._truncate(_msgs(), 19))
+    roles = [m.role for m in out]
+    assert roles[0] == "system" and out[0].content == "sys prompt"
+    # the assistant tool call and its tool result went together; never a lone tool row
+    assert "tool" not in roles and roles[1:] == ["user", "assistant"]
+    assert sum(a._count(m) for m in out) <= 19
+
+
+def test_summarize_strategy_replaces_old_turns_with_a_summary():
+    a = _agent_with("summarize", 30)
+    out = _run_sync(a._truncate(_msgs(), 30))
+    assert out[0].content == "sys prompt"
+    assert out[1].role == "system" and "the user asked about weather" in out[1].content
+    assert out[-1].content == "six" and sum(a._count(m) for m in out) <= 30
+    assert all(m.role != "tool" for m in out[:3])  # no orphaned tool result
+    # custom falls back to sliding
+    c = _agent_with("custom", 19)
+    assert [m.role for m in _run_sync(c._truncate(_msgs(), 19))][0] == "system"

@@ -378,15 +378,26 @@ def render(root: str, t: Template, values: dict) -> dict[str, str]:
     variables, errs = resolve_variables(t, values)
     if errs:
         raise TemplateError("; ".join(errs))
-    tdir = os.path.join(root, t.path)
+    # template.yaml is untrusted: every path it names (and every file a directory
+    # walk reaches, symlinks resolved) must stay inside the template directory,
+    # which itself must stay inside the source root
+    root_real = os.path.realpath(root)
+    tdir = os.path.realpath(os.path.join(root_real, t.path))
+    if not _inside(tdir, root_real):
+        raise TemplateError(f"template path escapes the source root: {t.path}")
     files: dict[str, str] = {}
     for spec in t.files:
         rel = spec["path"]
-        src = os.path.join(tdir, rel.rstrip("/"))
+        src = os.path.realpath(os.path.join(tdir, rel.rstrip("/")))
+        if not _inside(src, tdir):
+            raise TemplateError(f"template file escapes the template directory: {rel}")
         if os.path.isdir(src):
             for d, _, fs in os.walk(src):
                 for fn in fs:
-                    p = os.path.join(d, fn)
+                    p = os.path.realpath(os.path.join(d, fn))
+                    if not _inside(p, tdir):
+                        raise TemplateError(f"template file escapes the template directory: "
+                                            f"{os.path.join(d, fn)}")
                     r = os.path.relpath(p, tdir)
                     with open(p) as f:
                         body = f.read()
@@ -397,6 +408,10 @@ def render(root: str, t: Template, values: dict) -> dict[str, str]:
                 body = f.read()
             files[rel] = render_string(body, variables) if spec.get("render") else body
     return files
+
+
+def _inside(path: str, base: str) -> bool:
+    return path == base or path.startswith(base.rstrip(os.sep) + os.sep)
 
 
 def write_output(files: dict[str, str], out_dir: str) -> None:

@@ -27,8 +27,18 @@ Management writes (``--allow-writes``; off by default):
 
 With ``--oidc-jwks-file`` every ``/api/*`` route requires an IdP-issued bearer
 JWT (RS256, issuer / audience checked) and the caller's bearer is forwarded to
-the API server, whose own authorisation decides writes -- the dashboard holds no
-credentials of its own to lend to callers.
+the API server -- the dashboard holds no credentials of its own to lend to
+callers.  Write routes are guarded independently of the API server:
+
+* ``--allow-writes`` refuses to start without OIDC (``--insecure-dev-writes``
+  lifts that for a dashboard bound to loopback only);
+* the caller's token must carry a write group (``--oidc-write-group``, default
+  ``omnia-admin``) in its ``groups`` or ``roles`` claim -- an authenticated
+  read-only user cannot write;
+* a write must be ``application/json`` / ``application/yaml`` (a cross-site
+  form or ``text/plain`` POST cannot be sent without a CORS preflight, which the
+  dashboard never answers) and, when the browser sends ``Origin``, it must be
+  the dashboard's own origin (or ``--allowed-origin``).
 Run: ``python -m omnia_amd.operator.dashboard --port 3000 --api http://operator:8090``.
 """
 from __future__ import annotations
@@ -66,7 +76,7 @@ border:1px solid #ccc;padding:6px;white-space:pre-wrap}</style></head><body>
 const KINDS=__KINDS__;let sock;
 async function j(u){const r=await fetch(u);return r.json()}
 async function applyObj(){const k=document.getElementById('kind').value;
- const r=await fetch('/api/resources/'+k,{method:'POST',body:document.getElementById('yaml').value});
+ const r=await fetch('/api/resources/'+k,{method:'POST',headers:{'Content-Type':'application/yaml'},body:document.getElementById('yaml').value});
  const o=await r.json();document.getElementById('applied').textContent=r.status+' '+(o.error||o.message||(o.metadata||{}).name||'')}
 async function agents(){const o=await j('/api/overview');const t=document.getElementById('agents');
  for(const a of o.agents){const r=t.insertRow();for(const v of [a.namespace,a.name,a.phase,a.replicas,a.provider])
@@ -95,8 +105,23 @@ const sel=document.getElementById('kind');for(const k of KINDS){const o=document
 </script></body></html>"""
 
 
+WRITE_TYPES = ("application/json", "application/yaml", "application/x-yaml")
+
+
+def _claim_set(claims: dict, *names) -> set:
+    out = set()
+    for n in names:
+        v = claims.get(n)
+        if isinstance(v, str):
+            out.update(v.replace(",", " ").split())
+        elif isinstance(v, (list, tuple)):
+            out.update(str(x) for x in v)
+    return out
+
+
 def oidc_middleware(jwks: dict, issuer: str = "", audience: str = ""):
-    """401 on ``/api/*`` without a valid IdP bearer token."""
+    """401 on ``/api/*`` without a valid IdP bearer token; the verified claims
+    ride on the request (``request["claims"]``) for the write guard."""
     from ..facade.auth import AuthError, bearer, jwt_decode
 
     @web.middleware
@@ -112,15 +137,23 @@ def oidc_middleware(jwks: dict, issuer: str = "", audience: str = ""):
                 return web.json_response({"error": "invalid token"}, status=401)
             if "exp" not in claims:
                 return web.json_response({"error": "token without exp"}, status=401)
+            request["claims"] = claims
         return await handler(request)
 
     return mw
 
 
 def build_app(api: str, session_api: str = "", privacy_api: str = "",
-              oidc: dict | None = None, allow_writes: bool = False) -> web.Application:
-    """``oidc``: ``{"jwks": {...}, "issuer": ..., "audience": ...}`` gates the API;
-    ``allow_writes`` enables the management routes (module doc)."""
+              oidc: dict | None = None, allow_writes: bool = False,
+              insecure_dev_writes: bool = False,
+              allowed_origins: tuple = ()) -> web.Application:
+    """``oidc``: ``{"jwks": {...}, "issuer": ..., "audience": ...,
+    "write_groups": [...]}`` gates the API; ``allow_writes`` enables the
+    management routes, which need OIDC unless ``insecure_dev_writes`` (module doc)."""
+    if allow_writes and not oidc and not insecure_dev_writes:
+        raise ValueError("--allow-writes needs OIDC (--oidc-jwks-file); use "
+                         "--insecure-dev-writes only for a loopback-bound dev dashboard")
+    write_groups = set((oidc or {}).get("write_groups") or ["omnia-admin"])
     mws = [oidc_middleware(oidc["jwks"], oidc.get("issuer", ""), oidc.get("audience", ""))] \
         if oidc else []
     app = web.Application(middlewares=mws)
@@ -143,10 +176,26 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
                                  timeout=aiohttp.ClientTimeout(total=10)) as r:
                 return r.status, await r.json(content_type=None)
 
-    def _writes_on():
+    def _writes_on(request):
         if not allow_writes:
             return web.json_response({"error": "dashboard is read-only "
                                                "(start it with --allow-writes)"}, status=403)
+        ctype = (request.headers.get("Content-Type") or "").split(";")[0].strip().lower()
+        if request.method != "DELETE" and ctype not in WRITE_TYPES:
+            return web.json_response({"error": "writes must be application/json or "
+                                               "application/yaml"}, status=415)
+        origin = request.headers.get("Origin")
+        if origin:
+            own = {f"{request.scheme}://{request.host}", f"http://{request.host}",
+                   f"https://{request.host}"}
+            if origin not in own and origin not in allowed_origins:
+                return web.json_response({"error": "cross-origin write refused"}, status=403)
+        if oidc:
+            have = _claim_set(request.get("claims") or {}, "groups", "roles")
+            if not have & write_groups:
+                return web.json_response({"error": "caller lacks a write group "
+                                                   f"({', '.join(sorted(write_groups))})"},
+                                         status=403)
         return None
 
     base = f"{api}/apis/{crds.GROUP}/{crds.VERSION}"
@@ -158,7 +207,7 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
         return root + (f"/{urllib.parse.quote(name, safe='')}" if name else "")
 
     async def create(request):
-        if (deny := _writes_on()) is not None:
+        if (deny := _writes_on(request)) is not None:
             return deny
         plural = request.match_info["plural"]
         if plural not in plurals:
@@ -178,7 +227,7 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
         return web.json_response(body, status=st)
 
     async def delete(request):
-        if (deny := _writes_on()) is not None:
+        if (deny := _writes_on(request)) is not None:
             return deny
         plural, ns, name = (request.match_info[k] for k in ("plural", "ns", "name"))
         if plural not in plurals:
@@ -187,7 +236,7 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
         return web.json_response(body, status=st)
 
     async def scale(request):
-        if (deny := _writes_on()) is not None:
+        if (deny := _writes_on(request)) is not None:
             return deny
         try:
             n = int((await request.json())["replicas"])
@@ -203,7 +252,7 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
         return web.json_response(body, status=st)
 
     async def cancel_job(request):
-        if (deny := _writes_on()) is not None:
+        if (deny := _writes_on(request)) is not None:
             return deny
         ns, name = request.match_info["ns"], request.match_info["name"]
         st, body = await _send(request, "PATCH", _ns_url("arenajobs", ns, name),
@@ -295,16 +344,26 @@ def main(argv=None):
     ap.add_argument("--oidc-issuer", default="")
     ap.add_argument("--oidc-audience", default="")
     ap.add_argument("--allow-writes", action="store_true",
-                    help="enable create / delete / scale / cancel routes")
+                    help="enable create / delete / scale / cancel routes (needs OIDC)")
+    ap.add_argument("--oidc-write-group", action="append", default=[],
+                    help="group / role claim allowed to write (repeatable; default omnia-admin)")
+    ap.add_argument("--allowed-origin", action="append", default=[])
+    ap.add_argument("--insecure-dev-writes", action="store_true",
+                    help="allow writes without OIDC; only with a loopback --host")
     a = ap.parse_args(argv)
     oidc = None
     if a.oidc_jwks_file:
         with open(a.oidc_jwks_file) as f:
-            oidc = {"jwks": json.load(f), "issuer": a.oidc_issuer, "audience": a.oidc_audience}
+            oidc = {"jwks": json.load(f), "issuer": a.oidc_issuer, "audience": a.oidc_audience,
+                    "write_groups": a.oidc_write_group or ["omnia-admin"]}
+    if a.insecure_dev_writes and a.host not in ("127.0.0.1", "localhost", "::1"):
+        ap.error("--insecure-dev-writes needs --host 127.0.0.1")
 
     async def run():
         runner = web.AppRunner(build_app(a.api, a.session_api, a.privacy_api, oidc,
-                                         allow_writes=a.allow_writes))
+                                         allow_writes=a.allow_writes,
+                                         insecure_dev_writes=a.insecure_dev_writes,
+                                         allowed_origins=tuple(a.allowed_origin)))
         await runner.setup()
         await web.TCPSite(runner, a.host, a.port).start()
         await asyncio.Event().wait()

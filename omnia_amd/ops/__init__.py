@@ -206,7 +206,8 @@ WGEMM_BUCKETS = (16, 32, 64, 128, 192, 256)
 def wgemm_config(M: int, N: int, K: int, mode: int) -> tuple[int, int, int] | None:
     """(nw, nwaves, splits) of the weight-streaming kernel for a decode projection
     (nwaves == 0 selects the wide-batch 32x32x16 kernel, wgemm_wide.hip, with nw
-    32-column tiles per wave),
+    32-column tiles per wave; nwaves < 0 the full-batch tile kernel, tgemm.hip,
+    with nw weight rows per block and non-temporal weight loads when -2),
     or None to keep the library / gemm.hip path.  ``mode`` 0 = plain projection
     (its split-K slabs are reduced by the consumer kernel), 1 = gate_up + SwiGLU.
     Measured dispatch: ``ops/tuned/wgemm_mi355x.json`` (scripts/wgemm_sweep.py +
@@ -238,6 +239,8 @@ def wgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, nw: int 
     sum is ``x @ w.T`` (reduced by the consumer kernel)."""
     if nwaves == 0:  # table code for the wide-batch kernel: nw = 32-col tiles per wave
         return wgemm_wide(mode, x, w, splits, nw, out)
+    if nwaves < 0:  # table code for the full-batch tile kernel: nw = weight rows per block
+        return tgemm(mode, x, w, splits, nw, int(nwaves == -2), out)
     M, K = x.shape
     N = w.shape[0] // 2 if mode == 1 else w.shape[0]
     if out is None:
@@ -257,6 +260,31 @@ def wgemm_wide(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, wt:
         out = (torch.empty(splits, M, N, dtype=torch.float32, device=x.device) if mode == 2
                else x.new_empty(M, N))
     kernels().wgemm_wide(mode, out, x.contiguous(), w, splits, wt)
+    return out
+
+
+def tgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, bn: int = 128,
+          wnt: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Full-batch (M <= 256) tile decode GEMM (``csrc/tgemm.hip``): every block
+    owns all M rows x ``bn`` weight rows, both operands LDS-DMA staged through an
+    NS-deep ring with counted waits.  Same modes / outputs as :func:`wgemm`
+    (mode 1 = fused SwiGLU needs ``splits == 1``)."""
+    M, K = x.shape
+    N = w.shape[0] // 2 if mode == 1 else w.shape[0]
+    if out is None:
+        out = (torch.empty(splits, M, N, dtype=torch.float32, device=x.device) if mode == 2
+               else x.new_empty(M, N))
+    if not x.is_cuda:
+        r = x.float() @ w.float().t()
+        if mode == 1:
+            r = ref.silu_mul(r.to(x.dtype)).float()
+        if mode == 2:
+            out.zero_()
+            out[0].copy_(r)
+        else:
+            out.copy_(r.to(out.dtype))
+        return out
+    kernels().tgemm(mode, out, x.contiguous(), w, splits, bn, wnt)
     return out
 
 

@@ -79,6 +79,8 @@ int omnia_wgemm_wide(int mode, void* out, const void* X, const void* W, int M, i
 int omnia_dgemm(int mode, void* out, const void* X, const void* W, float* ws, int* cnt, int M,
                 int N, int K, int S, int wm, int wn, int ldo, int64_t ws_floats, int cnt_len,
                 hipStream_t s);
+int omnia_tgemm(int mode, void* out, const void* X, const void* W, int M, int N, int K, int S,
+                int bn, int wnt, int ldo, hipStream_t s);
 }
 
 namespace {
@@ -468,6 +470,37 @@ void wgemm_wide(int64_t mode, at::Tensor out, at::Tensor x, at::Tensor W, int64_
            "wgemm_wide");
 }
 
+// full-batch tile decode GEMM (tgemm.hip, M <= 256): same modes / out shapes as
+// wgemm; bn = weight rows per block (64/128/256), wnt = non-temporal weight loads
+void tgemm(int64_t mode, at::Tensor out, at::Tensor x, at::Tensor W, int64_t splits, int64_t bn,
+           int64_t wnt) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(W);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2, "2-D operands");
+  TORCH_CHECK(x.is_contiguous() && W.is_contiguous(), "contiguous x / W");
+  TORCH_CHECK(x.device() == W.device() && x.device() == out.device(), "same device");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(W.size(1) == K, "K mismatch");
+  TORCH_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");
+  TORCH_CHECK(mode != 1 || W.size(0) % 2 == 0, "gate_up rows even");
+  const int N = mode == 1 ? W.size(0) / 2 : W.size(0);
+  int ldo;
+  if (mode == 2) {
+    TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous(),
+                "mode 2: fp32 contiguous slabs");
+    TORCH_CHECK(out.dim() == 3 && out.size(0) == splits && out.size(1) == M && out.size(2) == N,
+                "mode 2: out [S, M, N]");
+    ldo = N;
+  } else {
+    CHECK_BF16(out);
+    TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N && out.stride(1) == 1,
+                "out [M, N]");
+    ldo = out.stride(0);
+  }
+  CHECK_RC(omnia_tgemm((int)mode, out.data_ptr(), x.data_ptr(), W.data_ptr(), M, N, K,
+                       (int)splits, (int)bn, (int)wnt, ldo, cur_stream()),
+           "tgemm");
+}
+
 // ------------------------------------------------- split-K consumers (splitk.hip)
 static void check_parts(const at::Tensor& p) {
   TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat && p.is_contiguous() && p.dim() == 3,
@@ -673,6 +706,7 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("dgemm", &dgemm);
   m.def("wgemm", &wgemm);
   m.def("wgemm_wide", &wgemm_wide);
+  m.def("tgemm", &tgemm);
   m.def("ar_twoshot", &ar_twoshot);
   m.def("ar_region_bytes", &omnia_ar_region_bytes);
   m.def("splitk_add_rmsnorm", &splitk_add_rmsnorm);

@@ -1,0 +1,286 @@
+// Full-batch tile GEMM for decode projections on gfx950:
+//   out = x[M, K] . W[N, K]^T   with 129 <= M <= 256 (one continuous-batching
+// decode step), bf16 operands, fp32 MFMA accumulate.  SURVEY §2.4 K3/K8/K9/K10.
+//
+// At M = 256 a Llama-3-8B projection sits on the MI355X ridge (256 FLOP per
+// weight byte vs ~400 FLOP/B of dense bf16 peak over achievable HBM), so the
+// kernel has to keep the matrix cores busy WHILE the weights stream at HBM
+// speed.  The per-CU limit is the load path, not HBM: every column tile
+// re-reads its x slab from L2.  The design therefore maximises FLOP per staged
+// byte and keeps the staging pipeline full:
+//   * one block owns ALL 256 batch rows x BN weight rows (BN = 64/128/256), so
+//     W crosses HBM -> LDS exactly once and x crosses L2 -> LDS once per BN
+//     weight rows (BM*BN/(BM+BN) = 85 FLOP/B at BN = 128, 128 at BN = 256);
+//   * both operands go global -> LDS by direct LDS-DMA (global_load_lds_dwordx4,
+//     16 B per lane, 1 KB = 8 rows x 128 B per wave instruction).  The LDS image
+//     is lane-linear; the bank-conflict XOR swizzle (chunk c of row r at
+//     c ^ (r & 7)) is applied to the per-lane SOURCE address and to the
+//     fragment reads (the same involution);
+//   * NS-deep LDS ring (NS = 4/3/2 stages of 64 k for BN = 64/128/256, as many
+//     as 160 KB allows) with a COUNTED `s_waitcnt vmcnt` and raw `s_barrier`,
+//     so NS-2 stages of loads stay in flight across every barrier -- hipcc's
+//     __syncthreads() would drain them (vmcnt(0)) on every k-step;
+//   * 8 waves (512 threads) on 16x16x32 bf16 MFMA, wave tile 64x64 (BN 128),
+//     128x64 (BN 256) or 64x32 (BN 64);
+//   * split-K over S slices (uneven splits allowed) fills the 256 CUs; slices
+//     write fp32 partial slabs [S][M][N] that the NEXT kernel reduces as part of
+//     its own work (splitk.hip: QKV -> RoPE + paged KV write, O / down ->
+//     residual add + RMSNorm, gate_up -> SwiGLU), so no combine launch exists;
+//   * MODE 1 fuses SwiGLU into the epilogue (S = 1): each wave's BN/2 columns
+//     are gate features and the matching up features of W = [Wg; Wu];
+//   * block order: XCD-remapped, split-major, so the blocks sharing an XCD's L2
+//     mostly share one x slice.
+// MODE 0: bf16 out[M, ldo]; MODE 1: bf16 SwiGLU out[M, ldo] (N = features);
+// MODE 2: fp32 partial slabs out[S][M][N].
+#include "common.h"
+
+using namespace omnia;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ float4v mfma16(short8 a, short8 b, float4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// element offset of 16-B chunk `ch` (0..7) of row `row` in a [rows][64] bf16 image
+__device__ __forceinline__ int swz(int row, int ch) { return row * 64 + ((ch ^ (row & 7)) << 3); }
+
+__device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+template <int BN>
+struct Geo {
+  static constexpr int BM = 256, BK = 64;
+  static constexpr int WGN = BN >= 256 ? 4 : 2;  // waves along N
+  static constexpr int WGM = 8 / WGN;
+  static constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  static constexpr int FM = WTM / 16, FN = WTN / 16;
+  static constexpr int STAGE = (BM + BN) * BK;                  // bf16 elements per stage
+  static constexpr int NS_FIT = (160 * 1024) / (STAGE * 2);
+  static constexpr int NS = NS_FIT > 4 ? 4 : NS_FIT;            // LDS ring depth
+  static constexpr int A_IN = BM / 64, B_IN = BN / 64;          // glds per wave per stage
+  static constexpr int L = A_IN + B_IN;
+};
+
+template <int BN, int MODE, int WNT>
+__global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
+                                                       const bf16_t* __restrict__ X,
+                                                       const bf16_t* __restrict__ W, int M, int N,
+                                                       int K, int S, int ldo) {
+  using G = Geo<BN>;
+  constexpr int NS = G::NS, L = G::L, A_IN = G::A_IN, B_IN = G::B_IN;
+  constexpr int FM = G::FM, FN = G::FN, WTM = G::WTM, WTN = G::WTN;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NS * G::STAGE];
+
+  // mode 1 tiles hold BN/2 output features (gate + up rows of W)
+  const int ntiles = MODE == 1 ? N / (BN / 2) : N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / ntiles, tile = bid - split * ntiles;
+  const int nk = K >> 6;
+  const int kb = split * nk / S, ke = (split + 1) * nk / S;
+  const int n_loc = ke - kb;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / G::WGN, wn = w - wm * G::WGN;
+
+  // ---- per-lane LDS-DMA sources: instruction i of this wave covers 8 rows; lane l
+  // fills row 8*i' + (l >> 3), LDS chunk (l & 7) <- global chunk (l & 7) ^ (l >> 3)
+  const int lr = lane >> 3, lc = (lane & 7) ^ lr;
+  const bf16_t* a_src[A_IN];
+#pragma unroll
+  for (int i = 0; i < A_IN; ++i) {
+    const int row = 8 * (w * A_IN + i) + lr;
+    const int r = row < M ? row : M - 1;  // rows past the batch: clamped copies, never stored
+    a_src[i] = X + (int64_t)r * K + (int64_t)kb * 64 + lc * 8;
+  }
+  const bf16_t* b_src[B_IN];
+#pragma unroll
+  for (int i = 0; i < B_IN; ++i) {
+    const int rr = 8 * (w * B_IN + i) + lr;  // row of the B tile
+    int64_t wrow;
+    if (MODE == 1) {
+      const int wv = rr / WTN, q = rr - wv * WTN;
+      const int64_t f0 = (int64_t)tile * (BN / 2) + wv * (WTN / 2);
+      wrow = q < WTN / 2 ? f0 + q : (int64_t)N + f0 + (q - WTN / 2);
+    } else {
+      wrow = (int64_t)tile * BN + rr;
+    }
+    b_src[i] = W + wrow * K + (int64_t)kb * 64 + lc * 8;
+  }
+  const int a_dst0 = (8 * w * A_IN) * 64;                // element offsets inside a stage
+  const int b_dst0 = 256 * 64 + (8 * w * B_IN) * 64;
+
+  auto issue = [&](int stage, int kl) {
+    bf16_t* base = lds + stage * G::STAGE;
+    const int koff = kl * 64;
+#pragma unroll
+    for (int i = 0; i < A_IN; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + koff),
+                                       (lds_ptr_t)(base + a_dst0 + i * 512), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < B_IN; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + koff),
+                                       (lds_ptr_t)(base + b_dst0 + i * 512), 16, 0,
+                                       WNT ? 2 : 0);
+  };
+
+  float4v acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // both 32-k halves of the stage are read up front, so the second half's LDS
+  // reads are in flight under the first half's MFMAs (counted lgkmcnt by hipcc)
+  auto compute = [&](int stage) {
+    const bf16_t* As = lds + stage * G::STAGE;
+    const bf16_t* Bs = As + 256 * 64;
+    short8 a[2][FM], b[2][FN];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[ks][j] = *reinterpret_cast<const short8*>(Bs + swz(wn * WTN + 16 * j + fr, ks * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        a[ks][i] = *reinterpret_cast<const short8*>(As + swz(wm * WTM + 16 * i + fr, ks * 4 + fq));
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(a[ks][i], b[ks][j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- pipeline: stages 0..NS-2 in flight before the loop; step t waits for its
+  // own stage (NS-2 younger stages stay outstanding), passes ONE raw barrier (every
+  // wave's DMA for stage t has landed, and every wave is done reading stage t-1's
+  // buffer), refills that buffer with stage t+NS-1, then computes stage t.  Past
+  // the slice end the refill re-reads the last stage into a buffer nobody reads,
+  // which keeps the vmcnt count constant (branch-free pipeline).
+  const int klast = n_loc - 1;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue(s, s < klast ? s : klast);
+  for (int t0 = 0; t0 < n_loc; t0 += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int t = t0 + u;
+      if (t < n_loc) {
+        wait_vm<(NS - 2) * L>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const int nxt = t + NS - 1;
+        issue((u + NS - 1) % NS, nxt < klast ? nxt : klast);
+        compute(u);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  wait_vm<0>();
+
+  // ---- epilogue: lane holds rows wm*WTM + 16i + 4fq + r, tile columns wn*WTN + 16j + fr
+  if (MODE == 2) {
+    float* o = reinterpret_cast<float*>(out) + (int64_t)split * M * N + (int64_t)tile * BN +
+               wn * WTN + fr;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WTM + 16 * i + 4 * fq + r;
+        if (row < M) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) o[(int64_t)row * N + 16 * j] = acc[i][j][r];
+        }
+      }
+  } else if (MODE == 0) {
+    bf16_t* o = reinterpret_cast<bf16_t*>(out) + (int64_t)tile * BN + wn * WTN + fr;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WTM + 16 * i + 4 * fq + r;
+        if (row < M) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) o[(int64_t)row * ldo + 16 * j] = f2bf(acc[i][j][r]);
+        }
+      }
+  } else {
+    bf16_t* o = reinterpret_cast<bf16_t*>(out) + (int64_t)tile * (BN / 2) + wn * (WTN / 2) + fr;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WTM + 16 * i + 4 * fq + r;
+        if (row < M) {
+#pragma unroll
+          for (int j = 0; j < FN / 2; ++j)
+            o[(int64_t)row * ldo + 16 * j] = f2bf(silu(acc[i][j][r]) * acc[i][j + FN / 2][r]);
+        }
+      }
+  }
+}
+
+template <int BN, int MODE>
+int launch_bn(void* out, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int ldo,
+              int wnt, hipStream_t s) {
+  const int ntiles = MODE == 1 ? N / (BN / 2) : N / BN;
+  const dim3 grid(ntiles * S), block(512);
+  if (wnt)
+    tgemm_kernel<BN, MODE, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+  else
+    tgemm_kernel<BN, MODE, 0><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+  return (int)hipGetLastError();
+}
+
+template <int MODE>
+int launch_mode(void* out, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int ldo,
+                int bn, int wnt, hipStream_t s) {
+  if (bn == 64) return launch_bn<64, MODE>(out, X, W, M, N, K, S, ldo, wnt, s);
+  if (bn == 128) return launch_bn<128, MODE>(out, X, W, M, N, K, S, ldo, wnt, s);
+  if (bn == 256) return launch_bn<256, MODE>(out, X, W, M, N, K, S, ldo, wnt, s);
+  return -20;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Returns 0 on success, < 0 for a shape the kernel does not cover (checked
+// BEFORE any launch).  mode 0: bf16 out[M, ldo]; mode 1: SwiGLU bf16 out[M, ldo]
+// from W = [Wg; Wu] ([2N, K]); mode 2: fp32 slabs out[S][M][N].
+int omnia_tgemm(int mode, void* out, const void* X, const void* W, int M, int N, int K, int S,
+                int bn, int wnt, int ldo, hipStream_t s) {
+  if (mode < 0 || mode > 2) return -1;
+  if (M < 1 || M > 256) return -2;
+  if (K % 64 || K <= 0) return -3;
+  if (S < 1 || S > 16 || S > K / 64) return -4;
+  if (bn != 64 && bn != 128 && bn != 256) return -5;
+  const int cols = mode == 1 ? bn / 2 : bn;
+  if (N % cols) return -6;
+  if (mode != 2 && S != 1) return -7;
+  if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) |
+       reinterpret_cast<uintptr_t>(out)) & 15)
+    return -8;
+  if (mode != 2 && ldo < N) return -9;
+  const bf16_t* x = (const bf16_t*)X;
+  const bf16_t* w = (const bf16_t*)W;
+  if (mode == 0) return launch_mode<0>(out, x, w, M, N, K, S, ldo, bn, wnt, s);
+  if (mode == 1) return launch_mode<1>(out, x, w, M, N, K, S, ldo, bn, wnt, s);
+  return launch_mode<2>(out, x, w, M, N, K, S, N, bn, wnt, s);
+}
+
+}  // extern "C"

@@ -31,12 +31,19 @@ static-shaped and hipGraph-capturable:
 
 Capacity ``C`` must be the same on every rank of a step (it is a collective's
 shape); the engine passes the step-global token count (``ForwardBatch.ep_tokens``)
-so ``C = T_global * k`` is lossless.  The price of static shapes is padding
+so ``C = T_global * k`` is lossless.  Large (prefill) steps run the layer in
+fixed chunks of at most ``chunk_tokens`` (``OMNIA_EP_CHUNK_TOKENS``, default
+2048) tokens, the chunk count derived from the step-global token count so every
+rank issues the same collectives: transients stay at ``ep * chunk * k`` rows
+(at ep = 8, k = 2, I = 14336: ~0.5 GiB of activations for 2048 tokens, instead
+of ~15 GiB for an unchunked 16K-token prefill).  The price of static shapes is padding
 bandwidth: each rank moves ``ep * C * d`` bytes per direction, of which only
 ``T*k*d`` are real -- measured and documented against EP-inside-TP in
 ``docs/PARALLELISM.md``.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.distributed as dist
@@ -75,7 +82,8 @@ class ExpertParallelMoE:
         if self.e_local * self.ep != self.n_experts:
             raise ValueError("experts must split evenly over the EP group")
         self.renorm = renorm
-        self.stats = {"calls": 0, "rows_sent": 0, "bytes_sent": 0}
+        self.chunk_tokens = max(1, int(os.environ.get("OMNIA_EP_CHUNK_TOKENS", "2048")))
+        self.stats = {"calls": 0, "rows_sent": 0, "bytes_sent": 0, "chunks": 0}
 
     def route(self, x: torch.Tensor):
         if x.is_cuda:
@@ -98,6 +106,20 @@ class ExpertParallelMoE:
     def __call__(self, x: torch.Tensor, ids=None, wts=None, tokens: int = 0) -> torch.Tensor:
         """``tokens``: the step-global max token count across the EP group (sets
         the capacity; defaults to this rank's own T, correct for a lone call)."""
+        T, d = x.shape
+        G = max(tokens, T)
+        if G > self.chunk_tokens:
+            if ids is None:
+                ids, wts = self.route(x)
+            c = self.chunk_tokens
+            outs = []
+            for i in range((G + c - 1) // c):  # same count on every rank (collectives)
+                lo, hi = min(i * c, T), min((i + 1) * c, T)
+                outs.append(self._layer(x[lo:hi], ids[lo:hi], wts[lo:hi], c))
+            return torch.cat(outs) if outs else x.new_empty(0, d)
+        return self._layer(x, ids, wts, tokens)
+
+    def _layer(self, x: torch.Tensor, ids, wts, tokens: int) -> torch.Tensor:
         from .. import ops
 
         T, d = x.shape
@@ -120,6 +142,7 @@ class ExpertParallelMoE:
         got = back.index_select(0, slot).float().view(T, k, d)
         out = (got * wts.to(torch.float32).view(T, k, 1)).sum(dim=1)  # fixed slot order
         self.stats["calls"] += 1
+        self.stats["chunks"] += 1
         self.stats["rows_sent"] += self.ep * cap
         self.stats["bytes_sent"] += self.ep * cap * d * x.element_size()
         return out.to(x.dtype)

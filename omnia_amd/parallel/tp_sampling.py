@@ -9,9 +9,12 @@ floats, 0.5 MB at K = 64, tp = 8):
 * greedy rows (temperature 0): the global argmax is the argmax of the ranks'
   local top-1s -- exact;
 * pure temperature rows (no top-k / top-p): Gumbel-max -- every rank adds
-  independent Gumbel noise to its logits / T and keeps the local winner; the
-  arg-max of the winners is an exact sample from softmax(logits / T) over the
-  whole vocabulary;
+  Gumbel noise to its logits / T and keeps the local winner; the arg-max of the
+  winners is an exact sample from softmax(logits / T) over the whole
+  vocabulary.  The noise of (row, GLOBAL vocab index v) is a counter-based hash
+  of (request seed, step, v): draws are independent across ranks (each hashes
+  its own vocab range) without any per-rank RNG state, and a seeded request is
+  reproducible whatever the TP degree;
 * top-k / top-p rows: the fused sampler runs over the union of the ranks'
   local top-K logits (K = 64): exact for top_k <= K; top-p is taken inside that
   candidate set (exact whenever the nucleus has <= K tokens per rank).
@@ -28,6 +31,36 @@ import torch.distributed as dist
 from .. import ops
 
 
+_M32 = 0xFFFFFFFF
+
+
+def _mul32(x: torch.Tensor, c: int) -> torch.Tensor:
+    """(x * c) mod 2**32 for int64 x in [0, 2**32) without int64 overflow."""
+    return (x * (c & 0xFFFF) + (((x * (c >> 16)) & 0xFFFF) << 16)) & _M32
+
+
+def _fmix32(h: torch.Tensor) -> torch.Tensor:
+    """murmur3 finaliser on int64 tensors holding 32-bit values."""
+    h = h ^ (h >> 16)
+    h = _mul32(h, 0x85EBCA6B)
+    h = h ^ (h >> 13)
+    h = _mul32(h, 0xC2B2AE35)
+    return h ^ (h >> 16)
+
+
+def gumbel_uniform(seeds: torch.Tensor, steps: torch.Tensor, vocab_start: int, n: int
+                   ) -> torch.Tensor:
+    """Uniform (0, 1) noise [B, n] for global vocab ids vocab_start .. +n: a pure
+    function of (seed, step, vocab id), identical on every device and TP layout."""
+    dev = seeds.device
+    s = seeds.to(torch.int64)
+    row = _fmix32((s & _M32) ^ _fmix32(((s >> 32) & _M32) ^ 0x68BC21EB))
+    row = _fmix32(row ^ _fmix32((steps.to(torch.int64) & _M32) ^ 0x02E5BE93))
+    v = torch.arange(vocab_start, vocab_start + n, dtype=torch.int64, device=dev)
+    h = _fmix32(row[:, None] ^ _fmix32((v + 0x9E3779B9) & _M32)[None, :])
+    return (h.to(torch.float64) + 0.5).mul_(1.0 / 4294967296.0).float()
+
+
 def tp_sample(local_logits: torch.Tensor, vocab_start: int, temperature: torch.Tensor,
               top_k: torch.Tensor, top_p: torch.Tensor, seeds: torch.Tensor | None = None,
               steps: torch.Tensor | None = None, out: torch.Tensor | None = None, group=None,
@@ -38,7 +71,12 @@ def tp_sample(local_logits: torch.Tensor, vocab_start: int, temperature: torch.T
     lf = local_logits.float()
     cv, ci = torch.topk(lf, K, dim=1)
     t = temperature.float().clamp(min=1e-6)[:, None]
-    u = torch.rand(B, Vl, device=lf.device, generator=generator).clamp_(1e-10, 1.0 - 1e-7)
+    if seeds is not None:
+        st = steps if steps is not None else torch.zeros(B, dtype=torch.int64, device=lf.device)
+        u = gumbel_uniform(seeds.to(lf.device), st.to(lf.device), vocab_start, Vl)
+    else:  # no per-request seeds: the caller's generator (must differ per rank)
+        u = torch.rand(B, Vl, device=lf.device, generator=generator)
+    u = u.clamp_(1e-10, 1.0 - 1e-7)
     gv, gi = (lf / t - torch.log(-torch.log(u))).max(dim=1)
     pack = torch.cat([cv, (ci + vocab_start).float(), gv[:, None],
                       (gi + vocab_start).float()[:, None]], dim=1).contiguous()

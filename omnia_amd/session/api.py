@@ -342,7 +342,14 @@ def main(argv=None):
     ap.add_argument("--encryption-key-file", default=os.environ.get("ENCRYPTION_KEY_FILE", ""),
                     help="local provider: versioned KEK ring (rotated by the key-rotation "
                          "controller)")
+    ap.add_argument("--tokens-file", default=os.environ.get("OMNIA_SESSION_API_TOKENS_FILE", ""),
+                    help="JSON {bearer token: service-account identity}; enables auth on the "
+                         "REST and both OTLP listeners")
     a = ap.parse_args(argv)
+    tokens = None
+    if a.tokens_file:
+        with open(a.tokens_file) as f:
+            tokens = {str(k): str(v) for k, v in json.load(f).items()}
     cold = ColdArchive(LocalBlobStore(a.cold_dir)) if a.cold_dir else None
     if a.cold_backend and a.cold_bucket:
         from .blobstores import build_cold_blobstore
@@ -384,7 +391,7 @@ def main(argv=None):
                                                   "keyID": a.encryption_key_id,
                                                   "keyFile": a.encryption_key_file or None}))
     audit_logger = None
-    app_kw = {}
+    app_kw = {"tokens": tokens}
     if a.audit_db:
         from ..ee.audit import AuditLogger, Forwarder
 
@@ -436,10 +443,10 @@ def main(argv=None):
             from .otlp import Transformer, build_otlp_app, serve_otlp_grpc
 
             tr = Transformer(svc)
-            runner = web.AppRunner(build_otlp_app(tr))
+            runner = web.AppRunner(build_otlp_app(tr, tokens=tokens))
             await runner.setup()
             await web.TCPSite(runner, "0.0.0.0", a.otlp_http_port).start()
-            grpc_srv, _ = await serve_otlp_grpc(tr, a.otlp_grpc_port)
+            grpc_srv, _ = await serve_otlp_grpc(tr, a.otlp_grpc_port, tokens=tokens)
             yield
             await grpc_srv.stop(1)
             await runner.cleanup()

@@ -360,10 +360,38 @@ def grpc_trace_handler(transformer: Transformer):
             response_serializer=ot.ExportTraceServiceResponse.SerializeToString)})
 
 
-async def serve_otlp_grpc(transformer: Transformer, port: int = 4317, host: str = "0.0.0.0"):
+def token_interceptor(tokens: dict):
+    """gRPC twin of the HTTP guard: ``authorization: Bearer <token>`` metadata
+    must name a token of the session-api's token map (reference
+    ``otlpGRPCServerOptions``), else UNAUTHENTICATED before the handler runs."""
     import grpc
 
-    server = grpc.aio.server(options=[("grpc.max_receive_message_length", MAX_BODY)])
+    async def deny(_req, context):
+        await context.abort(grpc.StatusCode.UNAUTHENTICATED, "unauthorized")
+
+    denied = grpc.unary_unary_rpc_method_handler(deny)
+
+    class _Guard(grpc.aio.ServerInterceptor):
+        async def intercept_service(self, continuation, details):
+            md = {k.lower(): v for k, v in (details.invocation_metadata or ())}
+            h = md.get("authorization", "")
+            tok = h[7:] if isinstance(h, str) and h.lower().startswith("bearer ") else ""
+            if tokens.get(tok) is None:
+                return denied
+            return await continuation(details)
+
+    return _Guard()
+
+
+async def serve_otlp_grpc(transformer: Transformer, port: int = 4317, host: str = "0.0.0.0",
+                          tokens: dict | None = None):
+    """``tokens``: the session-api bearer-token map; when set every export must
+    carry one (same review as the HTTP listener)."""
+    import grpc
+
+    server = grpc.aio.server(options=[("grpc.max_receive_message_length", MAX_BODY)],
+                             interceptors=[token_interceptor(tokens)] if tokens is not None
+                             else None)
     server.add_generic_rpc_handlers((grpc_trace_handler(transformer),))
     bound = server.add_insecure_port(f"{host}:{port}")
     await server.start()

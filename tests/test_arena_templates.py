@@ -105,6 +105,27 @@ def test_render_go_template_subset(tmp_path):
         T.render(str(root), t, {})
 
 
+def test_render_confines_reads_to_the_template(tmp_path):
+    """template.yaml is untrusted: absolute / '..' file paths, a template path
+    outside the source root, and symlinks out of the template are refused."""
+    import dataclasses
+
+    root = _tree(tmp_path / "src")
+    secret = tmp_path / "secret.txt"
+    secret.write_text("top secret")
+    t = T.discover(str(root))[0]
+    ok = {"projectName": "x"}
+    for bad in ("../../../secret.txt", str(secret)):
+        evil = dataclasses.replace(t, files=[{"path": bad, "render": False}])
+        with pytest.raises(T.TemplateError, match="escapes"):
+            T.render(str(root), evil, ok)
+    with pytest.raises(T.TemplateError, match="escapes"):
+        T.render(str(root), dataclasses.replace(t, path="../.."), ok)
+    (root / "templates" / "chatbot" / "prompts" / "leak.md").symlink_to(secret)
+    with pytest.raises(T.TemplateError, match="escapes"):
+        T.render(str(root), t, ok)
+
+
 def test_render_string_edge_cases():
     r = T.render_string
     assert r("{{ .a.b }}", {"a": {"b": 3}}) == "3"

@@ -208,18 +208,25 @@ def test_dashboard_management_writes():
         await api.start_server()
         url = str(api.make_url("")).rstrip("/")
         ro = TestClient(TestServer(build_app(url)))
-        rw = TestClient(TestServer(build_app(url, allow_writes=True)))
+        rw = TestClient(TestServer(build_app(url, allow_writes=True, insecure_dev_writes=True)))
         await ro.start_server()
         await rw.start_server()
+        Y = {"Content-Type": "application/yaml"}
         try:
-            assert (await ro.post("/api/resources/providers", data=prov)).status == 403
-            r = await rw.post("/api/resources/providers", data=prov)
+            assert (await ro.post("/api/resources/providers", data=prov, headers=Y)).status == 403
+            # CSRF guards: a text/plain (form-simple) body and a foreign Origin are refused
+            assert (await rw.post("/api/resources/providers", data=prov)).status == 415
+            r = await rw.post("/api/resources/providers", data=prov,
+                              headers={**Y, "Origin": "https://evil.example"})
+            assert r.status == 403 and store.try_get("Provider", "p1", "default") is None
+            r = await rw.post("/api/resources/providers", data=prov, headers=Y)
             assert r.status in (200, 201), await r.text()
             assert store.try_get("Provider", "p1", "default") is not None
             bad = prov.replace("type: mock", "type: nosuchtype")
-            r = await rw.post("/api/resources/providers", data=bad.replace("p1", "p2"))
+            r = await rw.post("/api/resources/providers", data=bad.replace("p1", "p2"), headers=Y)
             assert r.status >= 400  # the API server's admission rejected it
-            assert (await rw.post("/api/resources/providers", data="- a\n- b")).status == 400
+            assert (await rw.post("/api/resources/providers", data="- a\n- b",
+                                  headers=Y)).status == 400
             r = await rw.post("/api/agents/default/a1/scale", json={"replicas": 3})
             assert r.status == 200, await r.text()
             assert store.get("AgentRuntime", "a1", "default")["spec"]["runtime"]["replicas"] == 3
@@ -230,6 +237,51 @@ def test_dashboard_management_writes():
         finally:
             await ro.close()
             await rw.close()
+            await api.close()
+
+    asyncio.run(run())
+
+
+def test_dashboard_writes_need_oidc_and_a_write_group():
+    import time
+
+    import pytest
+    from aiohttp.test_utils import TestClient, TestServer
+
+    from omnia_amd.operator.apiserver import build_app as api_app
+    from omnia_amd.operator.apistore import APIStore
+    from omnia_amd.operator.dashboard import build_app
+
+    with pytest.raises(ValueError, match="OIDC"):
+        build_app("http://127.0.0.1:1", allow_writes=True)
+    pub, n, d = _rsa_jwk()
+    prov = ("apiVersion: %s\nkind: Provider\nmetadata: {name: p9, namespace: default}\n"
+            "spec: {type: mock}\n" % crds.API_VERSION)
+
+    async def run():
+        store = APIStore()
+        api = TestServer(api_app(store))
+        await api.start_server()
+        dash = TestClient(TestServer(build_app(
+            str(api.make_url("")).rstrip("/"), allow_writes=True,
+            oidc={"jwks": {"keys": [pub]}, "issuer": "https://idp", "audience": "dash",
+                  "write_groups": ["ops"]})))
+        await dash.start_server()
+        try:
+            base = {"iss": "https://idp", "aud": "dash", "sub": "u1", "exp": time.time() + 60}
+            reader = _rs256(base, n, d)
+            writer = _rs256({**base, "groups": ["dev", "ops"]}, n, d)
+            Y = {"Content-Type": "application/yaml"}
+            r = await dash.post("/api/resources/providers", data=prov,
+                                headers={**Y, "Authorization": f"Bearer {reader}"})
+            assert r.status == 403 and "write group" in (await r.json())["error"]
+            assert store.try_get("Provider", "p9", "default") is None
+            r = await dash.post("/api/resources/providers", data=prov,
+                                headers={**Y, "Authorization": f"Bearer {writer}"})
+            assert r.status in (200, 201), await r.text()
+            assert store.try_get("Provider", "p9", "default") is not None
+        finally:
+            await dash.close()
             await api.close()
 
     asyncio.run(run())

@@ -95,7 +95,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _ep_worker(rank, world, port, q):
+def _ep_worker(rank, world, port, q, chunk=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -113,6 +113,8 @@ def _ep_worker(rank, world, port, q):
         el = E // world
         moe = ExpertParallelMoE(router, w_gu[rank * el:(rank + 1) * el],
                                 w_down[rank * el:(rank + 1) * el], k)
+        if chunk:
+            moe.chunk_tokens = chunk  # prefill-size steps run in fixed token chunks
         ids, wts = moe.route(x)
         # capacity is a collective shape: every rank passes the step-global max T
         got = moe(x, ids, wts, tokens=max(len(t) for t in xs))
@@ -126,12 +128,13 @@ def _ep_worker(rank, world, port, q):
         q.put(("err", rank, traceback.format_exc(), None))
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_expert_parallel_all_to_all_gloo(world):
+@pytest.mark.parametrize("world,chunk", [(2, 0), (4, 0), (2, 5), (4, 6)])
+def test_expert_parallel_all_to_all_gloo(world, chunk):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ep_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ep_worker, args=(r, world, port, q, chunk))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
@@ -140,7 +143,12 @@ def test_expert_parallel_all_to_all_gloo(world):
     for status, rank, val, stats in res:
         assert status == "ok", val
         assert val < 1e-4, (rank, val)
-        assert stats["calls"] == 1 and stats["rows_sent"] == world * (13 + 7 * (world - 1)) * 2
+        G = 13 + 7 * (world - 1)  # the step-global max token count
+        if chunk:  # every rank runs the same number of fixed-capacity chunks
+            n = (G + chunk - 1) // chunk
+            assert stats["chunks"] == n and stats["rows_sent"] == n * world * chunk * 2
+        else:
+            assert stats["calls"] == 1 and stats["rows_sent"] == world * G * 2
 
 
 def test_replicated_engine_health_rehomes_sessions():

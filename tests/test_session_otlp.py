@@ -199,6 +199,40 @@ def test_otlp_grpc_export():
     _check_conv1(svc)
 
 
+def test_otlp_grpc_requires_a_session_api_token():
+    import grpc
+
+    svc = TieredSessionService()
+
+    async def run():
+        tr = Transformer(svc)
+        server, port = await serve_otlp_grpc(tr, 0, "127.0.0.1", tokens={"sekrit": "sa:x"})
+        codes = []
+        try:
+            async with grpc.aio.insecure_channel(f"127.0.0.1:{port}") as ch:
+                export = ch.unary_unary(ot.METHOD_EXPORT,
+                                        request_serializer=ot.ExportTraceServiceRequest
+                                        .SerializeToString,
+                                        response_deserializer=ot.ExportTraceServiceResponse
+                                        .FromString)
+                for md in (None, (("authorization", "Bearer wrong"),)):
+                    try:
+                        await export(_request([CHAT]), metadata=md)
+                        codes.append("OK")
+                    except grpc.aio.AioRpcError as e:
+                        codes.append(e.code().name)
+                await export(_request([CHAT, TOOL, WF, WFC]),
+                             metadata=(("authorization", "Bearer sekrit"),))
+            return codes, tr.stats
+        finally:
+            await server.stop(0)
+
+    codes, stats = asyncio.run(run())
+    assert codes == ["UNAUTHENTICATED", "UNAUTHENTICATED"]
+    assert stats["spans"] == 4  # only the authorised export was ingested
+    _check_conv1(svc)
+
+
 def test_event_and_legacy_strategies_and_resource_session_id():
     svc = TieredSessionService()
     ev_span = ("chat", T0 + 1, {"gen_ai.request.model": "m1"}, [

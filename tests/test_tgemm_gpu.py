@@ -1,0 +1,83 @@
+"""Full-batch tile decode GEMM (ops/csrc/tgemm.hip) vs the fp32 PyTorch oracle:
+bf16 output, fused SwiGLU and fp32 split-K slabs (even and uneven splits), for
+every block width, with and without non-temporal weight loads, across batch
+sizes that exercise the clamped tail rows.  The asymmetric random operands
+catch a transposed or row/column-swapped epilogue."""
+import pytest
+import torch
+
+from omnia_amd import ops
+from omnia_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(M, N, K, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
+    return x, w
+
+
+@pytest.mark.parametrize("M", [1, 77, 129, 200, 256])
+@pytest.mark.parametrize("bn", [64, 128, 256])
+def test_mode0_matches_fp32(M, bn):
+    x, w = _mk(M, 1024, 512, seed=M + bn)
+    out = ops.tgemm(0, x, w, 1, bn, bn == 128)
+    want = x.float() @ w.float().t()
+    torch.testing.assert_close(out.float(), want, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("M", [3, 190, 256])
+@pytest.mark.parametrize("bn", [64, 128, 256])
+def test_mode1_swiglu_matches_fp32(M, bn):
+    I = 512
+    x, w = _mk(M, 2 * I, 1024, seed=7 + M + bn)
+    out = ops.tgemm(1, x, w, 1, bn, 1)
+    want = ref.silu_mul((x.float() @ w.float().t()))
+    torch.testing.assert_close(out.float(), want.float(), rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("M,S,bn", [(256, 1, 128), (256, 3, 128), (256, 5, 64), (201, 7, 256),
+                                    (256, 16, 64), (130, 2, 256)])
+def test_mode2_splitk_slabs_sum_to_product(M, S, bn):
+    x, w = _mk(M, 1024, 2048, seed=M + S + bn)  # 32 k-steps: S = 3, 5, 7 split unevenly
+    part = ops.tgemm(2, x, w, S, bn, 0)
+    assert part.shape == (S, M, 1024) and part.dtype == torch.float32
+    want = x.float() @ w.float().t()
+    torch.testing.assert_close(part.sum(0), want, rtol=1e-3, atol=3e-3)
+
+
+def test_llama3_8b_shapes():
+    """The four Llama-3-8B decode projections at the serving batch."""
+    M = 256
+    for N, K, mode, S, bn in ((6144, 4096, 2, 5, 128), (4096, 4096, 2, 8, 128),
+                              (14336, 4096, 1, 1, 128), (4096, 14336, 2, 7, 128)):
+        x, w = _mk(M, 2 * N if mode == 1 else N, K, seed=N + K)
+        out = ops.tgemm(mode, x, w, S, bn, 1)
+        full = x.float() @ w.float().t()
+        want = ref.silu_mul(full) if mode == 1 else full
+        got = out.sum(0) if mode == 2 else out.float()
+        torch.testing.assert_close(got, want.float(), rtol=3e-2, atol=3e-2)
+
+
+def test_repeat_launches_are_deterministic():
+    x, w = _mk(256, 2048, 4096, seed=3)
+    a = ops.tgemm(2, x, w, 4, 128, 1).clone()
+    for _ in range(3):
+        b = ops.tgemm(2, x, w, 4, 128, 1)
+        assert torch.equal(a, b)
+
+
+def test_rejects_bad_shapes_before_launch():
+    x, w = _mk(16, 1000, 512)
+    with pytest.raises(RuntimeError, match="tgemm"):
+        ops.tgemm(0, x, w, 1, 128, 0)  # 1000 rows not a multiple of the block's 128
+    x, w = _mk(300, 1024, 512)
+    with pytest.raises(RuntimeError, match="tgemm"):
+        ops.tgemm(0, x, w, 1, 128, 0)  # M > 256
+    x, w = _mk(64, 1024, 512)
+    with pytest.raises(RuntimeError, match="tgemm"):
+        ops.tgemm(2, x, w, 9, 128, 0)  # more splits than 64-k steps
+    with pytest.raises(RuntimeError, match="tgemm"):
+        ops.tgemm(0, x, w, 1, 96, 0)  # unsupported block width

@@ -40,6 +40,14 @@ def _worker(rank, world, port, q):
         res["topk"] = tp_sample(local, rank * sl, ones, torch.full((B,), 3, dtype=torch.int32),
                                 ones, seeds=torch.arange(B), steps=torch.zeros(B, dtype=torch.int64),
                                 generator=gen, K=8)
+        # the model_runner call path: per-request seeds + steps, NO generator (every
+        # rank runs the same calls, so only the hashed noise keeps ranks independent)
+        seeds = torch.full((B,), 1234, dtype=torch.int64)
+        steps = torch.arange(B, dtype=torch.int64)
+        res["temp_seeded"] = tp_sample(local, rank * sl, ones, zeros, ones, seeds=seeds,
+                                       steps=steps, K=8)
+        res["temp_seeded_again"] = tp_sample(local, rank * sl, ones, zeros, ones, seeds=seeds,
+                                             steps=steps, K=8)
         q.put(("ok", rank, {k: v.tolist() for k, v in res.items()}, base.tolist()))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover
@@ -63,7 +71,7 @@ def test_tp_sample_matches_full_vocab(world):
         assert st == "ok", val
     outs = {r: v for _, r, v, _ in res}
     base = torch.tensor(res[0][3])
-    for k in ("greedy", "temp", "topk"):
+    for k in ("greedy", "temp", "topk", "temp_seeded"):
         assert all(outs[r][k] == outs[0][k] for r in outs), f"ranks disagree on {k}"
     assert set(outs[0]["greedy"]) == {int(base.argmax())}
     top3 = set(base.topk(3).indices.tolist())
@@ -72,3 +80,27 @@ def test_tp_sample_matches_full_vocab(world):
     p = torch.softmax(base, 0)
     freq = torch.bincount(torch.tensor(outs[0]["temp"]), minlength=base.numel()).float() / 4000
     assert (freq - p).abs().max() < 0.03
+    # seeded rows on the runner's path: same law, and reproducible
+    freq = torch.bincount(torch.tensor(outs[0]["temp_seeded"]),
+                          minlength=base.numel()).float() / 4000
+    assert (freq - p).abs().max() < 0.03
+    assert outs[0]["temp_seeded"] == outs[0]["temp_seeded_again"]
+
+
+def test_seeded_noise_is_layout_independent():
+    """The hashed noise of a vocab id does not depend on how the vocabulary is
+    split over ranks, so a seeded request samples the same token at any TP degree."""
+    from omnia_amd.parallel.tp_sampling import gumbel_uniform
+
+    seeds = torch.tensor([7, 2**40 + 3], dtype=torch.int64)
+    steps = torch.tensor([0, 5], dtype=torch.int64)
+    full = gumbel_uniform(seeds, steps, 0, 1000)
+    halves = torch.cat([gumbel_uniform(seeds, steps, 0, 500),
+                        gumbel_uniform(seeds, steps, 500, 500)], dim=1)
+    assert torch.equal(full, halves)
+    assert float(full.min()) > 0.0 and float(full.max()) < 1.0
+    # roughly uniform, and distinct rows / steps draw different noise
+    assert abs(float(full.mean()) - 0.5) < 0.03
+    assert not torch.equal(full[0], full[1])
+    other = gumbel_uniform(seeds, steps + 1, 0, 1000)
+    assert not torch.equal(full, other)

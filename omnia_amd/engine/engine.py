@@ -207,7 +207,10 @@ class LLMEngine:
             free, total = torch.cuda.mem_get_info(device)
             # leave room for activations / graphs
             reserve = 6 * 2**30 + cfg.max_prefill_tokens * mc.hidden_size * 40
-            budget = max(0, int(free * cfg.kv_fraction) - reserve)
+            from ..parallel import state as pstate
+
+            share = pstate.ranks_per_device()  # TP ranks rehearsed on one device
+            budget = max(0, int(free * cfg.kv_fraction / share) - reserve)
         else:
             budget = 256 * 2**20
         return int(max(16, budget // per_block))

@@ -9,6 +9,7 @@ async copy.  Only sampled token ids come back to the host.
 from __future__ import annotations
 
 import bisect
+import os
 import time
 
 import numpy as np
@@ -125,6 +126,9 @@ class ModelRunner:
         # correctness tap (tests): fp32 copies of every sampled logits row
         self.logit_tap: list | None = None
         self._tap = None
+        self._prefill_host = None  # last packed prefill upload (host), for TP workers
+        if os.environ.get("OMNIA_LOGIT_TAP") == "1":  # every TP rank (same collectives)
+            self.enable_logit_tap()
 
     def enable_logit_tap(self):
         """Record ``(seq_ids, fp32 logits rows)`` for every step, for whole-model
@@ -211,7 +215,7 @@ class ModelRunner:
             ev.synchronize()  # the pinned token buffer of step N-2 has been read
         if n:
             if tp:
-                tok = self._prefill_tp_sample(t, meta, logits)
+                tok = self._prefill_tp_sample(t, meta, logits, sample_seqs)
             else:
                 self._tap_rows(sample_seqs, logits[:n])
                 temp, top_k, top_p, seeds, steps = self._prefill_sampling(t, meta)
@@ -231,12 +235,18 @@ class ModelRunner:
                 t[o + 2 * n:o + 3 * n].view(torch.float64).float(),
                 t[o + 3 * n:o + 4 * n], t[o + 4 * n:o + 5 * n])
 
-    def _prefill_tp_sample(self, t, meta, local_logits):
-        """TP: the distributed sampler (every rank runs it: it is a collective)."""
+    def _prefill_tp_sample(self, t, meta, local_logits, seqs=None):
+        """TP: the distributed sampler (every rank runs it: it is a collective).
+        With the logit tap on, every rank first all-gathers the vocab slices
+        (rank 0 records the full rows)."""
         from ..parallel import state as pstate
         from ..parallel.tp_sampling import tp_sample
 
         n = meta[4]
+        if self._tap is not None:
+            full = pstate.tp_all_gather_lastdim(local_logits[:n].contiguous())
+            if seqs is not None:
+                self._tap_rows(seqs, full)
         temp, top_k, top_p, seeds, steps = self._prefill_sampling(t, meta)
         return tp_sample(local_logits[:n], self.model.vocab_start, temp, top_k, top_p,
                          seeds=seeds, steps=steps, group=pstate.get_state().tp_group)
@@ -288,6 +298,7 @@ class ModelRunner:
                                 for p, x in zip(ps, sample_seqs)], np.int64),
                       np.array([len(x.output) for x in sample_seqs], np.int64)]
         t = torch.from_numpy(np.concatenate(parts))
+        self._prefill_host = t
         if self.is_gpu:
             t = t.pin_memory().to(self.device, non_blocking=True)
         return t, meta, sample_seqs
@@ -509,6 +520,8 @@ class ModelRunner:
             from ..parallel.tp_sampling import tp_sample
 
             local = self.model.forward(fb, self.kv, gather=False)
+            if self._tap is not None:  # correctness tap: full rows (a collective)
+                self._tap[:nrows].copy_(pstate.tp_all_gather_lastdim(local))
             tp_sample(local, self.model.vocab_start, d["temp"][:nrows], d["top_k"][:nrows],
                       d["top_p"][:nrows], seeds=d["seeds"][:nrows], steps=d["steps"][:nrows],
                       out=self.out_tok[:nrows], group=pstate.get_state().tp_group)
@@ -574,7 +587,7 @@ class ModelRunner:
             self.stats["graph_replays"] += 1
         else:
             self._decode_inputs(seqs, nrows, ncols, st)
-            self._before_replay(nrows, ncols)
+            self._before_replay(nrows, ncols, st)
             self._replay(nrows, ncols)
             out_host[:n].copy_(self.out_tok[:n], non_blocking=True)
             ev = torch.cuda.Event()
@@ -584,8 +597,8 @@ class ModelRunner:
             s.slot = i
         return DecodeHandle(seqs, out_host, ev, n)
 
-    def _before_replay(self, nrows: int, ncols: int):
-        """Hook: TP runners broadcast the step inputs to their workers here."""
+    def _before_replay(self, nrows: int, ncols: int, st: "_Staging | None" = None):
+        """Hook: TP runners publish the step inputs (``st.host``) to their workers."""
 
     def _replay(self, nrows: int, ncols: int):
         g = self.graphs.get((nrows, ncols)) or self._capture(nrows, ncols)
@@ -608,13 +621,13 @@ class ModelRunner:
         ncols = self._ctx_bucket(max(s.length for s in seqs))
         st = self.stage[0]
         self._decode_inputs(seqs, n, ncols, st)
-        self._before_eager(n, ncols)
+        self._before_eager(n, ncols, st)
         logits = self._eager_forward(n, ncols)
         self._tap_rows(seqs, logits[:n])
         return self._sample_eager(logits, seqs)
 
-    def _before_eager(self, n: int, ncols: int):
-        """Hook: TP runners broadcast the eager-decode inputs here."""
+    def _before_eager(self, n: int, ncols: int, st: "_Staging | None" = None):
+        """Hook: TP runners publish the eager-decode inputs here."""
 
     def _eager_forward(self, n: int, ncols: int):
         fb = self._decode_fb(n, ncols)

@@ -1,33 +1,46 @@
-"""Tensor-parallel engine: one process per GPU, rank 0 drives.
+"""Tensor-parallel engine: one process per TP rank, rank 0 drives.
 
 Process model: every TP rank holds its Megatron shard of the
-weights and of the KV cache (``Hkv / tp`` heads per page, same page ids on every
+weights and of the KV cache (``Hkv / tp`` heads per page -- one replicated head
+per rank when ``Hkv < tp``, e.g. Llama-3-70B at TP=8 -- same page ids on every
 rank).  Only TP-rank 0 runs the scheduler, the block manager and the runtime;
-each step it broadcasts the step's packed inputs to the other ranks over the TP
-group (RCCL on GPU, gloo on CPU) and every rank then executes the same forward,
-meeting in the per-layer all-reduces (IPC one-/two-shot kernels with the
-residual add + RMSNorm fused in, ``parallel/custom_allreduce.py``).  Decode
-inputs are broadcast straight from rank 0's device staging buffer into the
-workers' (one small collective per step, stream-ordered before the graph
-replay), so the workers' captured graphs read identical inputs.  Sampling is
-distributed (``parallel/tp_sampling.py``): each rank reduces its vocab slice to
-candidates, only those are all-gathered, and every rank picks the same token,
-which keeps the device-side token feedback of pipelined decode consistent.
+every rank executes the same forward and meets the others in the per-layer
+all-reduces (IPC one-/two-shot kernels with the residual add + RMSNorm fused in,
+``parallel/custom_allreduce.py``).  Sampling is distributed
+(``parallel/tp_sampling.py``): each rank reduces its vocab slice to candidates,
+only those are all-gathered, and every rank picks the same token, which keeps
+the device-side token feedback of pipelined decode consistent.
 
-Commands (int64 header of 16 words, then an optional payload):
-``PREFILL (T,B,maxb,tiles,nsample,len)``, ``DECODE (nrows,ncols)``,
-``EAGER (n,ncols)``, ``SWAP_OUT (handle,n)``, ``SWAP_IN (handle,n)``,
-``SWAP_DROP (handle)``, ``STOP``.
+Step channel (no collective, no device sync on the control path): rank 0 writes
+each command -- a 16-word header and the step's packed host inputs (the decode
+staging buffer, the prefill upload, swap block lists) -- into a host
+shared-memory ring (:class:`ShmRing`, one writer, ``tp - 1`` readers, per-reader
+consumed counters for flow control).  A worker polls the ring, copies the
+payload into its own pinned staging buffer (double-buffered, reused only after
+the H2D copy that read it has completed), enqueues the same H2D copy + graph
+replay rank 0 enqueued, and goes straight back to the ring: like rank 0 it runs
+ahead of its GPU by a step, and nothing on the decode path waits on the device.
+The previous design broadcast header and payload over RCCL every step and read
+the header back with ``.tolist()`` (a device -> host sync per step per worker).
 
-RCCL and hipGraph capture: decode graphs are captured in lockstep on all ranks
-(the capture is itself driven by the broadcast command stream).  Set
-``EngineConfig.use_graphs=False`` to run TP decode eagerly.
+Commands: ``PREFILL (T,B,maxb,tiles,nsample,len,gather,sampling offset)``,
+``DECODE (nrows,ncols)``, ``EAGER (n,ncols)``, ``SWAP_OUT (handle,n)``,
+``SWAP_IN (handle,n)``, ``SWAP_DROP (handle)``, ``STOP``.
+
+Decode graphs are captured in lockstep on all ranks: a worker captures when it
+first sees a ``DECODE`` for a (rows, cols) bucket, exactly when rank 0 does, so
+the collectives of the warm-up runs pair up.
 """
 from __future__ import annotations
 
 import itertools
 import logging
+import mmap
+import os
+import time
+import uuid
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -40,55 +53,165 @@ STOP, PREFILL, DECODE, EAGER, SWAP_OUT, SWAP_IN, SWAP_DROP = range(7)
 HDR = 16
 
 
+class ShmRing:
+    """Single-writer / multi-reader command ring in host shared memory.
+
+    Layout: a 4 KiB control page (int64 ``[0]`` = slots published, ``[8 + r]`` =
+    slots consumed by reader ``r``, ``[1]`` slot count, ``[2]`` payload bytes per
+    slot, ``[3]`` reader count) followed by ``nslots`` slots of ``HDR`` int64 +
+    payload.  Ordering: the writer stores payload, header, then the published
+    counter; x86-64 keeps stores in order and loads in order, so a reader that
+    sees the counter sees the slot."""
+
+    CTRL = 4096
+
+    def __init__(self, path: str, create: bool, nslots: int = 8, payload: int = 1 << 20,
+                 readers: int = 1):
+        self.path = path
+        if create:
+            size = self.CTRL + nslots * (HDR * 8 + payload)
+            fd = os.open(path, os.O_CREAT | os.O_RDWR | os.O_TRUNC, 0o600)
+            os.ftruncate(fd, size)
+        else:
+            fd = os.open(path, os.O_RDWR)
+            size = os.fstat(fd).st_size
+        self.mm = mmap.mmap(fd, size)
+        os.close(fd)
+        self.ctrl = np.ndarray((self.CTRL // 8,), dtype=np.int64, buffer=self.mm)
+        if create:
+            self.ctrl[:] = 0
+            self.ctrl[1], self.ctrl[2], self.ctrl[3] = nslots, payload, readers
+        self.nslots, self.payload, self.readers = (int(self.ctrl[1]), int(self.ctrl[2]),
+                                                   int(self.ctrl[3]))
+        self.stride = HDR * 8 + self.payload
+        self.hdrs = [np.ndarray((HDR,), dtype=np.int64, buffer=self.mm,
+                                offset=self.CTRL + i * self.stride) for i in range(self.nslots)]
+        self.bodies = [np.ndarray((self.payload,), dtype=np.uint8, buffer=self.mm,
+                                  offset=self.CTRL + i * self.stride + HDR * 8)
+                       for i in range(self.nslots)]
+        self.stats = {"puts": 0, "full_waits": 0}
+
+    # ------------------------------------------------------------- writer
+    def put(self, hdr: list[int], payload: np.ndarray | None = None, timeout_s: float = 600.0):
+        seq = int(self.ctrl[0])
+        t0 = None
+        while seq - int(self.ctrl[8:8 + self.readers].min()) >= self.nslots:
+            if t0 is None:
+                t0 = time.monotonic()
+                self.stats["full_waits"] += 1
+            elif time.monotonic() - t0 > timeout_s:
+                raise TimeoutError("TP command ring full: a worker stopped consuming")
+            time.sleep(0)
+        i = seq % self.nslots
+        n = 0
+        if payload is not None:
+            b = payload.reshape(-1).view(np.uint8)
+            n = b.size
+            if n > self.payload:
+                raise ValueError(f"TP step payload {n} B exceeds the ring slot ({self.payload} B)")
+            self.bodies[i][:n] = b
+        h = self.hdrs[i]
+        h[:] = 0
+        h[:len(hdr)] = hdr
+        h[HDR - 1] = n
+        self.ctrl[0] = seq + 1  # publish last
+        self.stats["puts"] += 1
+
+    # ------------------------------------------------------------- reader
+    def get(self, reader: int, spin_s: float = 0.002) -> tuple[list[int], np.ndarray]:
+        mine = int(self.ctrl[8 + reader])
+        t0 = time.perf_counter()
+        while int(self.ctrl[0]) <= mine:
+            if time.perf_counter() - t0 > spin_s:
+                time.sleep(0.0002)
+        i = mine % self.nslots
+        hdr = self.hdrs[i].tolist()
+        return hdr, self.bodies[i][:hdr[HDR - 1]]
+
+    def done(self, reader: int):
+        """Release the slot returned by the last :meth:`get` (after copying it)."""
+        self.ctrl[8 + reader] += 1
+
+    def close(self, unlink: bool = False):
+        try:
+            self.hdrs = self.bodies = None
+            self.ctrl = None
+            self.mm.close()
+        except (BufferError, ValueError):  # views still alive: the OS reclaims at exit
+            pass
+        if unlink:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+
+def _ring_payload_bytes(runner) -> int:
+    """Upper bound of one step's payload: the decode staging buffer or a packed
+    prefill upload of ``max_prefill_tokens`` tokens (``ModelRunner._prefill_pack``)."""
+    T, B, mb = runner.max_prefill_tokens, runner.max_batch, runner.max_blocks
+    prefill = 8 * (3 * T + 2 * (B + 1) + 2 * (T // 64 + B + 1) + B + B * mb + 5 * B + 64)
+    return max(runner.dec.nbytes, prefill, 8 * mb + 64)
+
+
 class TPChannel:
-    def __init__(self, device):
+    """Rank 0 -> workers step channel over a :class:`ShmRing` (created by TP rank
+    0, its path handed to the group once over the process group)."""
+
+    def __init__(self, device, runner=None, nslots: int = 8):
         st = pstate.get_state()
         self.group = st.tp_group
         self.src = st.rank - st.tp_rank  # global rank of this group's TP-rank 0
+        self.reader = st.tp_rank - 1
         self.device = device
         self.is_gpu = device.type == "cuda"
-        self.hdr = torch.zeros(HDR, dtype=torch.int64, device=device)
-        self.hdr_host = torch.zeros(HDR, dtype=torch.int64, pin_memory=self.is_gpu)
+        create = st.tp_rank == 0
+        path = [None]
+        if create:
+            path[0] = f"/dev/shm/omnia-tp-{os.getpid()}-{uuid.uuid4().hex[:10]}"
+            self.ring = ShmRing(path[0], True, nslots, _ring_payload_bytes(runner),
+                                st.tp_size - 1)
+        dist.broadcast_object_list(path, src=self.src, group=self.group)
+        if not create:
+            self.ring = ShmRing(path[0], False)
+        pstate.barrier_group(self.group)  # every reader attached before any unlink
+        if create:
+            os.unlink(path[0])  # the mappings stay valid; nothing is left in /dev/shm
 
-    def send(self, cmd: int, *vals, payload: torch.Tensor | None = None):
-        self.hdr_host.zero_()
-        self.hdr_host[0] = cmd
-        for i, v in enumerate(vals):
-            self.hdr_host[1 + i] = int(v)
-        self.hdr.copy_(self.hdr_host, non_blocking=self.is_gpu)
-        dist.broadcast(self.hdr, self.src, group=self.group)
-        if payload is not None:
-            dist.broadcast(payload, self.src, group=self.group)
+    def send(self, cmd: int, *vals, payload=None):
+        if isinstance(payload, torch.Tensor):
+            payload = payload.numpy() if payload.device.type == "cpu" else \
+                payload.cpu().numpy()
+        self.ring.put([cmd] + [int(v) for v in vals], payload)
 
-    def recv(self) -> list[int]:
-        dist.broadcast(self.hdr, self.src, group=self.group)
-        return self.hdr.tolist()
+    def recv(self) -> tuple[list[int], np.ndarray]:
+        return self.ring.get(self.reader)
 
-    def recv_into(self, t: torch.Tensor):
-        dist.broadcast(t, self.src, group=self.group)
-        return t
+    def release(self):
+        self.ring.done(self.reader)
 
 
 class TPModelRunner(ModelRunner):
-    """Rank-0 runner: broadcasts every step to the TP workers."""
+    """Rank-0 runner: publishes every step to the TP workers."""
 
     fused_launch = False
 
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
-        self.chan = TPChannel(self.device)
+        self.chan = TPChannel(self.device, self)
 
     def _prefill_forward(self, t, meta, gather: bool = True):
         # header: T, B, maxb, tiles, n_sample, payload len, gather flag, sampling offset
+        host = self._prefill_host if self._prefill_host is not None else t.cpu()
         self.chan.send(PREFILL, *meta[:5], t.numel(), int(gather),
-                       meta[5] if len(meta) > 5 else 0, payload=t)
+                       meta[5] if len(meta) > 5 else 0, payload=host)
         return super()._prefill_forward(t, meta, gather)
 
-    def _before_replay(self, nrows, ncols):
-        self.chan.send(DECODE, nrows, ncols, payload=self.dec.dev)
+    def _before_replay(self, nrows, ncols, st=None):
+        self.chan.send(DECODE, nrows, ncols, payload=(st or self.dec).host)
 
-    def _before_eager(self, n, ncols):
-        self.chan.send(EAGER, n, ncols, payload=self.dec.dev)
+    def _before_eager(self, n, ncols, st=None):
+        self.chan.send(EAGER, n, ncols, payload=(st or self.dec).host)
 
     def shutdown(self):
         self.chan.send(STOP)
@@ -99,39 +222,60 @@ class TPWorker(ModelRunner):
 
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
-        self.chan = TPChannel(self.device)
+        self.chan = TPChannel(self.device, self)
         self.swapped: dict[int, torch.Tensor] = {}
         self.swap = None
+        self.wflip = 0
+        self.wevents = [None, None]
+
+    def _stage_in(self, body: np.ndarray):
+        """Payload -> this worker's pinned staging (the buffer of two steps ago,
+        once its H2D has completed) -> H2D into the device twin the graphs read."""
+        slot = self.wflip
+        self.wflip ^= 1
+        st = self.stage[slot]
+        if self.wevents[slot] is not None:
+            self.wevents[slot].synchronize()
+        st.host.numpy()[:body.size] = body
+        self.chan.release()
+        self.dec.dev.copy_(st.host, non_blocking=True)
+        if self.is_gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.wevents[slot] = ev
 
     def run(self):
         while True:
-            h = self.chan.recv()
+            h, body = self.chan.recv()
             cmd = h[0]
             if cmd == STOP:
+                self.chan.release()
                 return
             if cmd == PREFILL:
                 T, B, maxb, tiles, ns, n, gather, so = h[1:9]
-                t = torch.empty(n, dtype=torch.int64, device=self.device)
-                self.chan.recv_into(t)
+                host = torch.from_numpy(body.view(np.int64)[:n].copy())
+                self.chan.release()
+                t = host.pin_memory().to(self.device, non_blocking=True) if self.is_gpu \
+                    else host
                 meta = (T, B, maxb, tiles, ns, so)
                 lg = ModelRunner._prefill_forward(self, t, meta, bool(gather))
                 if not gather and ns:
                     self._prefill_tp_sample(t, meta, lg)  # collective: mirror rank 0
             elif cmd == DECODE:
-                self.chan.recv_into(self.dec.dev)
+                self._stage_in(body)
                 self._replay(h[1], h[2])
             elif cmd == EAGER:
-                self.chan.recv_into(self.dec.dev)
+                self._stage_in(body)
                 self._eager_forward(h[1], h[2])
-            elif cmd == SWAP_OUT:
-                blocks = torch.empty(h[2], dtype=torch.int64, device=self.device)
-                self.chan.recv_into(blocks)
-                self.swapped[h[1]] = self.swap.swap_out(blocks.tolist())
-            elif cmd == SWAP_IN:
-                blocks = torch.empty(h[2], dtype=torch.int64, device=self.device)
-                self.chan.recv_into(blocks)
-                self.swap.swap_in(self.swapped.pop(h[1]), blocks.tolist())
+            elif cmd in (SWAP_OUT, SWAP_IN):
+                blocks = body.view(np.int64)[:h[2]].tolist()
+                self.chan.release()
+                if cmd == SWAP_OUT:
+                    self.swapped[h[1]] = self.swap.swap_out(blocks)
+                else:
+                    self.swap.swap_in(self.swapped.pop(h[1]), blocks)
             elif cmd == SWAP_DROP:
+                self.chan.release()
                 self.swap.drop(self.swapped.pop(h[1], None))
             else:
                 raise RuntimeError(f"unknown TP command {cmd}")
@@ -155,8 +299,9 @@ class TPSwapProxy:
             self.drop(s.swapped)
         return self.inner.used + n_pages <= self.inner.capacity_pages
 
-    def _blocks(self, blocks):
-        return torch.tensor(blocks, dtype=torch.int64, device=self.chan.device)
+    @staticmethod
+    def _blocks(blocks):
+        return np.asarray(blocks, dtype=np.int64)
 
     def swap_out(self, blocks):
         h = next(self.ids)
@@ -180,13 +325,14 @@ class TPSwapProxy:
 
 
 def agree_num_blocks(nb: int, device) -> int:
-    """Every TP rank must allocate the same page ids: take the minimum."""
+    """Every TP rank must allocate the same page ids: take the minimum (a host
+    collective: the group may be gloo)."""
     st = pstate.get_state()
     if st.tp_size == 1:
         return nb
-    t = torch.tensor([nb], dtype=torch.int64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=st.tp_group)
-    return int(t.item())
+    vals = [None] * st.tp_size
+    dist.all_gather_object(vals, int(nb), group=st.tp_group)
+    return int(min(vals))
 
 
 def run_worker(cfg, model_cfg=None, weights=None):
@@ -215,7 +361,10 @@ def run_worker(cfg, model_cfg=None, weights=None):
 
         w.swap = SwapSpace(kv, cfg.swap_gib)
     log.info("TP worker rank %d ready (%d KV blocks)", pstate.get_state().rank, nb)
-    w.run()
+    try:
+        w.run()
+    finally:
+        w.chan.ring.close()
 
 
 def start(cfg, model_cfg=None, weights=None):

@@ -87,6 +87,11 @@ TINY_EMBED = ModelConfig(name="tiny-embed", vocab_size=512, hidden_size=256,
 TINY_LLAMA = ModelConfig(name="tiny-llama", vocab_size=512, hidden_size=256,
                          intermediate_size=512, num_layers=2, num_heads=4, num_kv_heads=2,
                          max_position=4096, bos_token_id=256, eos_token_ids=(257,))
+# TP=4/8 rehearsal shape: 8 q heads over 2 kv heads, so at TP 4 and 8 every rank
+# holds ONE replicated kv head -- the per-rank layout of Llama-3-70B at TP=8
+TINY_LLAMA_H8 = ModelConfig(name="tiny-llama-h8", vocab_size=512, hidden_size=1024,
+                            intermediate_size=1024, num_layers=2, num_heads=8, num_kv_heads=2,
+                            max_position=4096, bos_token_id=256, eos_token_ids=(257,))
 TINY_MIXTRAL = ModelConfig(name="tiny-mixtral", arch="mixtral", vocab_size=512,
                            hidden_size=256, intermediate_size=256, num_layers=2, num_heads=4,
                            num_kv_heads=2, max_position=4096, num_experts=4,
@@ -94,7 +99,7 @@ TINY_MIXTRAL = ModelConfig(name="tiny-mixtral", arch="mixtral", vocab_size=512,
 
 REGISTRY: dict[str, ModelConfig] = {
     c.name: c for c in [LLAMA3_8B, LLAMA31_8B, LLAMA3_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_MIXTRAL,
-                   EMBED_1B, TINY_EMBED]
+                   EMBED_1B, TINY_EMBED, TINY_LLAMA_H8]
 }
 ALIASES = {
     "meta-llama/Meta-Llama-3-8B": "llama-3-8b",

@@ -79,6 +79,8 @@ int omnia_wgemm_wide(int mode, void* out, const void* X, const void* W, int M, i
 int omnia_dgemm(int mode, void* out, const void* X, const void* W, float* ws, int* cnt, int M,
                 int N, int K, int S, int wm, int wn, int ldo, int64_t ws_floats, int cnt_len,
                 hipStream_t s);
+int omnia_ar_allgather(void* out, const void* in, void* const* regions, int* epochs, int* err,
+                       int64_t nbytes, int64_t slot_bytes, int rank, int world, hipStream_t s);
 int omnia_tgemm(int mode, void* out, const void* X, const void* W, int M, int N, int K, int S,
                 int bn, int wnt, int ldo, hipStream_t s);
 }
@@ -599,6 +601,25 @@ void ar_oneshot(at::Tensor out, at::Tensor in, at::Tensor regions, at::Tensor ep
                             cur_stream()), "ar_oneshot");
 }
 
+// all-gather of any contiguous tensor's bytes over the IPC regions: out holds
+// world x in.nbytes (rank order)
+void ar_allgather(at::Tensor out, at::Tensor in, at::Tensor regions, at::Tensor epochs,
+                  at::Tensor err, int64_t slot_bytes, int64_t rank) {
+  CHECK_GPU(in); CHECK_GPU(out); CHECK_I32(epochs); CHECK_I32(err);
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous(), "contiguous");
+  TORCH_CHECK(regions.device().is_cpu() && regions.scalar_type() == at::kLong, "regions cpu i64");
+  TORCH_CHECK(epochs.numel() >= omnia_ar_blocks(), "epochs per block");
+  const int world = regions.numel();
+  TORCH_CHECK(world <= omnia_ar_max_ranks(), "world too large");
+  const int64_t nb = in.numel() * in.element_size();
+  TORCH_CHECK(out.numel() * out.element_size() == nb * world, "out must hold world x in bytes");
+  std::vector<void*> regs(world);
+  for (int p = 0; p < world; ++p) regs[p] = reinterpret_cast<void*>(regions.data_ptr<int64_t>()[p]);
+  CHECK_RC(omnia_ar_allgather(out.data_ptr(), in.data_ptr(), regs.data(), epochs.data_ptr<int>(),
+                              err.data_ptr<int>(), nb, slot_bytes, (int)rank, world,
+                              cur_stream()), "ar_allgather");
+}
+
 // two-shot (reduce-scatter + all-gather) over the same IPC regions; with w the
 // fused residual add + RMSNorm variant (residual updated in place)
 void ar_twoshot(at::Tensor out, at::Tensor in, c10::optional<at::Tensor> residual,
@@ -719,6 +740,7 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("ipc_open", &ipc_open);
   m.def("ipc_close", &ipc_close);
   m.def("ar_oneshot", &ar_oneshot);
+  m.def("ar_allgather", &ar_allgather);
   m.def("ar_blocks", &omnia_ar_blocks);
   m.def("ar_max_ranks", &omnia_ar_max_ranks);
   m.def("apply_token_mask", &apply_token_mask);

@@ -142,6 +142,39 @@ __global__ __launch_bounds__(256) void ar_oneshot_kernel(bf16_t* __restrict__ ou
   if (tid == 0) epochs[b] = epoch;
 }
 
+// All-gather of an opaque byte buffer (nbytes per rank, multiple of 16) into
+// out[world][nbytes]: block b stages its slice of `in` into my data slot,
+// publishes, waits for every peer's slice b, then copies slice b of every peer's
+// slot into out[p].  Same flags / epochs / parity slots as the one-shot
+// all-reduce (every collective of a group bumps every block's epoch once).
+__global__ __launch_bounds__(256) void ar_allgather_kernel(char* __restrict__ out,
+                                                           const char* __restrict__ in,
+                                                           PeerPtrs peers, int* __restrict__ epochs,
+                                                           int* __restrict__ err, int64_t nbytes,
+                                                           int64_t slot_bytes, int rank, int world) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ int s_epoch;
+  if (tid == 0) s_epoch = epochs[b] + 1;
+  __syncthreads();
+  const int epoch = s_epoch;
+  const int64_t slot = (epoch & 1) * slot_bytes;
+  const int64_t nv = nbytes / 16;
+  const int64_t per = (nv + kBlocks - 1) / kBlocks;
+  const int64_t v0 = b * per, v1 = v0 + per < nv ? v0 + per : nv;
+  uint4v* mine = reinterpret_cast<uint4v*>(peers.data[rank] + slot);
+  const uint4v* src = reinterpret_cast<const uint4v*>(in);
+  for (int64_t v = v0 + tid; v < v1; v += 256) mine[v] = src[v];
+  publish(peers.flags, b, rank, world, epoch);
+  wait_peers(peers.flags, b, rank, world, epoch, err);
+  for (int p = 0; p < world; ++p) {
+    const uint4v* ps = reinterpret_cast<const uint4v*>(peers.data[p] + slot);
+    uint4v* dst = reinterpret_cast<uint4v*>(out + (int64_t)p * nbytes);
+    for (int64_t v = v0 + tid; v < v1; v += 256) dst[v] = __builtin_nontemporal_load(ps + v);
+  }
+  __syncthreads();
+  if (tid == 0) epochs[b] = epoch;
+}
+
 // Row chunk of (rank r, block b): [r*R + b*Rb, min(r*R + (b+1)*Rb, (r+1)*R, M)).
 // VEC = 16-B vectors per thread per row (d <= 256 * 8 * VEC).
 template <bool NORM, int VEC>
@@ -338,6 +371,24 @@ int omnia_ar_twoshot(void* out, const void* in, void* residual, const void* w,
   return (int)hipGetLastError();
 }
 int omnia_ar_max_ranks() { return kMaxRanks; }
+
+// out[world][nbytes] <- every rank's `in` (nbytes, multiple of 16, <= slot_bytes).
+int omnia_ar_allgather(void* out, const void* in, void* const* regions, int* epochs, int* err,
+                       int64_t nbytes, int64_t slot_bytes, int rank, int world, hipStream_t s) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return -1;
+  if (nbytes % 16 || nbytes > slot_bytes || slot_bytes % 16 || nbytes <= 0) return -2;
+  if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(in)) & 15) return -4;
+  PeerPtrs pp{};
+  for (int p = 0; p < world; ++p) {
+    if (!regions[p]) return -3;
+    pp.data[p] = reinterpret_cast<char*>(regions[p]);
+    pp.flags[p] = reinterpret_cast<int*>(reinterpret_cast<char*>(regions[p]) + 4 * slot_bytes);
+    pp.flags2[p] = pp.flags[p] + kBlocks * kMaxRanks;
+  }
+  ar_allgather_kernel<<<kBlocks, 256, 0, s>>>((char*)out, (const char*)in, pp, epochs, err, nbytes,
+                                              slot_bytes, rank, world);
+  return (int)hipGetLastError();
+}
 
 // regions[p]: base pointer of rank p's region (own one from omnia_ipc_alloc,
 // peers' from omnia_ipc_open).  Layout: [2 * slot_bytes data][2 * slot_bytes

@@ -87,6 +87,46 @@ class CustomAllReduce:
                               self.rank)
         return out
 
+    def all_reduce_any(self, x: torch.Tensor) -> torch.Tensor:
+        """In-place all-reduce of ANY size: messages above one slot run as a
+        sequence of slot-sized one-shot launches over the flat tensor (the
+        ``ipc`` TP transport, where ranks may share a device and RCCL cannot be
+        used at all)."""
+        if 2 * x.numel() <= self.max_bytes:
+            return self.all_reduce(x)
+        flat = x.view(-1)
+        step = (self.max_bytes // 2) // 8 * 8
+        for i in range(0, flat.numel(), step):
+            self.all_reduce(flat[i:i + step], algo="oneshot")
+        return x
+
+    def all_gather(self, x: torch.Tensor) -> torch.Tensor:
+        """``[W, *x.shape]`` stack of every rank's ``x`` (rank order), any dtype;
+        graph-capturable.  Leading-dim chunks when a rank's bytes exceed a slot."""
+        x = x.contiguous()
+        out = torch.empty((self.world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        nbytes = x.numel() * x.element_size()
+        if nbytes % 16:
+            raise ValueError("all_gather needs a multiple of 16 bytes per rank")
+        if nbytes <= self.max_bytes:
+            self.k.ar_allgather(out, x, self.regions, self.epochs, self.err, self.slot_bytes,
+                                self.rank)
+            return out
+        rows = x.shape[0]
+        row_bytes = nbytes // rows
+        step = max(1, self.max_bytes // row_bytes)
+        while step > 1 and (step * row_bytes) % 16:
+            step -= 1
+        if (step * row_bytes) % 16:
+            raise ValueError("all_gather rows do not chunk into 16-byte pieces")
+        for r0 in range(0, rows, step):
+            piece = x[r0:r0 + step]
+            tmp = torch.empty((self.world,) + tuple(piece.shape), dtype=x.dtype, device=x.device)
+            self.k.ar_allgather(tmp, piece, self.regions, self.epochs, self.err,
+                                self.slot_bytes, self.rank)
+            out[:, r0:r0 + piece.shape[0]] = tmp
+        return out
+
     def can_fuse_norm(self, x: torch.Tensor) -> bool:
         return (self.should_use(x) and x.dim() == 2 and x.shape[1] % 8 == 0
                 and 4 * x.numel() <= self.slot_bytes)

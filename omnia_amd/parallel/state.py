@@ -10,6 +10,15 @@ Scaling model (MI355X-first):
   * EP  -- Mixtral experts spread over the TP group, token dispatch/combine by
            all-to-all (:mod:`omnia_amd.parallel.expert`).
 The backend string ``"nccl"`` IS RCCL on ROCm; ``gloo`` drives the CPU tests.
+
+TP device transport (``ParallelState.transport``):
+  * ``"rccl"`` -- one GPU per rank: decode-size collectives on the IPC kernels,
+    prefill-size all-reduces and gathers on RCCL;
+  * ``"ipc"``  -- ranks SHARE devices (more TP ranks than visible GPUs, e.g. a
+    TP=8 engine rehearsed on one MI355X, or ``OMNIA_TP_TRANSPORT=ipc``): RCCL
+    cannot place two ranks on one device, so the process group is gloo (host
+    control only) and EVERY device collective runs on the IPC kernels
+    (slot-chunked all-reduce, IPC all-gather).
 """
 from __future__ import annotations
 
@@ -34,6 +43,7 @@ class ParallelState:
     dp_group: object = None
     backend: str = "none"
     custom_ar: object = None  # CustomAllReduce when available
+    transport: str = "none"  # TP device collectives: "rccl" | "ipc" | "gloo" (CPU)
 
     @property
     def is_distributed(self) -> bool:
@@ -69,13 +79,19 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, device: str |
     if ws % tp_size:
         raise ValueError(f"world_size {ws} not divisible by tp_size {tp_size}")
     use_gpu = device != "cpu" and torch.cuda.is_available()
-    if backend is None:
-        backend = "nccl" if use_gpu else "gloo"
+    ndev = torch.cuda.device_count() if use_gpu else 0
+    transport = "gloo"
     if use_gpu:
-        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        shared = ndev < int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
+        transport = os.environ.get("OMNIA_TP_TRANSPORT") or ("ipc" if shared else "rccl")
+    if backend is None:
+        backend = "nccl" if use_gpu and transport == "rccl" else "gloo"
+    if use_gpu:
+        torch.cuda.set_device(local % max(1, ndev))
     st = ParallelState(world_size=ws, rank=rank, local_rank=local, tp_size=tp_size,
                        tp_rank=rank % tp_size, dp_size=ws // tp_size, dp_rank=rank // tp_size,
-                       backend=backend if ws > 1 else "none")
+                       backend=backend if ws > 1 else "none",
+                       transport=transport if ws > 1 else "none")
     if ws > 1:
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -95,7 +111,8 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, device: str |
             g = dist.new_group(ranks) if len(ranks) > 1 else None
             if rank in ranks:
                 st.dp_group = g
-        if use_gpu and tp_size > 1 and os.environ.get("OMNIA_CUSTOM_AR", "1") == "1":
+        if use_gpu and tp_size > 1 and (transport == "ipc" or
+                                        os.environ.get("OMNIA_CUSTOM_AR", "1") == "1"):
             # one-/two-shot IPC all-reduce for decode-size TP collectives (RCCL for
             # prefill-size messages and as the correctness oracle in the tests)
             from .custom_allreduce import CustomAllReduce
@@ -111,8 +128,30 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
         return x
     if st.custom_ar is not None and x.is_cuda and st.custom_ar.should_use(x):
         return st.custom_ar.all_reduce(x)
+    if st.transport == "ipc" and x.is_cuda:
+        if x.dtype != torch.bfloat16 or not x.is_contiguous() or x.numel() % 8:
+            raise ValueError("ipc TP transport all-reduces contiguous bf16 tensors (n % 8 == 0)")
+        return st.custom_ar.all_reduce_any(x)
     dist.all_reduce(x, group=st.tp_group)
     return x
+
+
+def tp_all_gather(x: torch.Tensor) -> torch.Tensor:
+    """``[tp, *x.shape]``: every TP rank's ``x`` in rank order."""
+    st = _STATE
+    if st.tp_size == 1:
+        return x.unsqueeze(0)
+    if x.is_cuda and st.custom_ar is not None and (
+            st.transport == "ipc" or x.numel() * x.element_size() <= 256 << 10):
+        return st.custom_ar.all_gather(x)
+    x = x.contiguous()
+    if x.is_cuda:
+        out = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out.view(-1), x.view(-1), group=st.tp_group)
+        return out
+    parts = [torch.empty_like(x) for _ in range(st.tp_size)]
+    dist.all_gather(parts, x, group=st.tp_group)
+    return torch.stack(parts)
 
 
 def tp_all_reduce_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
@@ -135,9 +174,8 @@ def tp_all_gather_lastdim(x: torch.Tensor) -> torch.Tensor:
     st = _STATE
     if st.tp_size == 1:
         return x
-    parts = [torch.empty_like(x) for _ in range(st.tp_size)]
-    dist.all_gather(parts, x.contiguous(), group=st.tp_group)
-    return torch.cat(parts, dim=-1)
+    g = tp_all_gather(x)  # [tp, ..., n]
+    return torch.cat(list(g.unbind(0)), dim=-1)
 
 
 def shard_range(total: int, parts: int, idx: int) -> tuple[int, int]:
@@ -150,3 +188,16 @@ def shard_range(total: int, parts: int, idx: int) -> tuple[int, int]:
 def barrier():
     if dist.is_initialized():
         dist.barrier()
+
+
+def barrier_group(group):
+    if dist.is_initialized():
+        dist.barrier(group=group)
+
+
+def ranks_per_device() -> int:
+    """TP ranks sharing one device under the ``ipc`` transport (else 1)."""
+    st = _STATE
+    if st.transport != "ipc" or not torch.cuda.is_available():
+        return 1
+    return max(1, -(-st.tp_size // max(1, torch.cuda.device_count())))

@@ -78,9 +78,16 @@ def tp_sample(local_logits: torch.Tensor, vocab_start: int, temperature: torch.T
         u = torch.rand(B, Vl, device=lf.device, generator=generator)
     u = u.clamp_(1e-10, 1.0 - 1e-7)
     gv, gi = (lf / t - torch.log(-torch.log(u))).max(dim=1)
+    pad = (-(2 * K + 2)) % 4  # 16-byte rows for the IPC all-gather
     pack = torch.cat([cv, (ci + vocab_start).float(), gv[:, None],
-                      (gi + vocab_start).float()[:, None]], dim=1).contiguous()
-    if pack.is_cuda:
+                      (gi + vocab_start).float()[:, None]]
+                     + ([lf.new_zeros(B, pad)] if pad else []), dim=1).contiguous()
+    from . import state as pstate
+
+    st = pstate.get_state()
+    if st.tp_size == W and (group is None or group is st.tp_group) and st.tp_size > 1:
+        allp = pstate.tp_all_gather(pack)  # IPC kernel on the node (capturable)
+    elif pack.is_cuda:
         allp = torch.empty(W * B, pack.shape[1], dtype=pack.dtype, device=pack.device)
         dist.all_gather_into_tensor(allp, pack, group=group)
         allp = allp.view(W, B, -1)

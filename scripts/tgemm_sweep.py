@@ -139,7 +139,7 @@ def main():
                         continue
                     md = mode if S == 1 and mode == 1 else 2
                     for wnt in (0, 1):
-                        outb = (torch.empty(S, M, N, device="cuda") if md == 2 else
+                        outb = (torch.empty(S, M, rows, device="cuda") if md == 2 else
                                 torch.empty(M, N, device="cuda", dtype=torch.bfloat16))
 
                         def f(i, md=md, S=S, bn=bn, wnt=wnt, outb=outb):

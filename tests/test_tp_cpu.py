@@ -1,7 +1,9 @@
-"""Tensor parallelism on CPU (gloo, world_size 2): the rank-0-driven TP engine
-(command broadcast, Megatron shards, vocab-parallel embed/lm_head, all-reduce per
-layer) must reproduce the single-rank model exactly in fp32, including chunked
-prefill, pipelined/eager decode and session prefix reuse."""
+"""Tensor parallelism on CPU (gloo, world_size 2, 4 and 8): the rank-0-driven TP
+engine (shared-memory step ring, Megatron shards, vocab-parallel embed/lm_head,
+all-reduce per layer) must reproduce the single-rank model exactly in fp32,
+including chunked prefill, pipelined/eager decode and session prefix reuse.  At
+TP 4 and 8 tiny-llama-h8 leaves every rank one replicated kv head -- the
+per-rank layout of Llama-3-70B at TP=8 (BASELINE config 4)."""
 import os
 import socket
 
@@ -90,3 +92,65 @@ def test_tp2_engine_matches_single_rank(model):
     outs, hit = res
     assert hit > 0
     assert outs == ref[0]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_tp_world4_world8_engine_matches_single_rank(world):
+    model = "tiny-llama-h8"
+    ref = _generate(LLMEngine(_cfg(1, model), weights=_full_weights(model)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, model)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        status, res = q.get(timeout=600)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert status == "ok", res
+    outs, hit = res
+    assert hit > 0
+    assert outs == ref[0]
+
+
+def test_shm_ring_flow_control(tmp_path):
+    """The step ring: ordered delivery to every reader, payload bytes intact,
+    and a full ring blocks the writer until the slowest reader releases."""
+    import threading
+
+    import numpy as np
+
+    from omnia_amd.engine.tp import ShmRing
+
+    path = str(tmp_path / "ring")
+    w = ShmRing(path, True, nslots=2, payload=64, readers=2)
+    r = ShmRing(path, False)
+    got = {0: [], 1: []}
+
+    def reader(k):
+        for _ in range(5):
+            h, body = r.get(k)
+            got[k].append((h[0], bytes(body)))
+            r.done(k)
+
+    ts = [threading.Thread(target=reader, args=(k,)) for k in (0, 1)]
+    for t in ts:
+        t.start()
+    for i in range(5):
+        w.put([i, 7], np.arange(i + 1, dtype=np.uint8))
+    for t in ts:
+        t.join(10)
+    want = [(i, bytes(range(i + 1))) for i in range(5)]
+    assert got[0] == want and got[1] == want
+    with pytest.raises(ValueError, match="exceeds"):
+        w.put([9], np.zeros(65, dtype=np.uint8))
+    w.put([1])
+    w.put([2])  # ring of 2 now full (nobody consumes)
+    with pytest.raises(TimeoutError):
+        w.put([3], timeout_s=0.05)
+    r.close()
+    w.close(unlink=True)

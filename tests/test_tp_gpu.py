@@ -1,0 +1,138 @@
+"""The tensor-parallel engine on ONE MI355X: TP = 2, 4 and 8 ranks as separate
+processes sharing cuda:0 (BASELINE config 4's TP=8 path rehearsed on one
+device).  RCCL cannot place two ranks on one device, so the group runs the
+``ipc`` transport: gloo for host bootstrap only, the shared-memory step ring for
+the control path, and every device collective on the IPC kernels (fused
+all-reduce + RMSNorm, slot-chunked all-reduce, all-gather for the distributed
+sampler) inside the captured decode graphs.
+
+Model: Llama-3-70B's exact layer shapes (hidden 8192, 64 q / 8 kv heads, MLP
+28672, vocab 128256) with 2 layers; at TP=8 every rank holds one kv head.  Every
+logit row the engine sampled from (chunked prefill, graph decode, a second turn
+reusing the session's resident KV) is checked against the fp32 dense oracle
+``ops.reference.dense_forward`` of the FULL weights, with a negative control
+(a swapped kv-head slice in the oracle must fail the gate)."""
+import os
+import random
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _check(mc, w, seqs, rows_by_seq, rel_tol):
+    from omnia_amd.ops import reference as ref
+
+    ok = total = 0
+    worst = 0.0
+    for sid, prompt, output in seqs:
+        got = rows_by_seq[sid]
+        assert len(got) == len(output), (len(got), len(output))
+        full = prompt + output
+        want = ref.dense_forward(mc, w, full[:-1])[len(prompt) - 1:]
+        for g, r in zip(got, want):
+            err = float((g - r).abs().max() / r.abs().max())
+            worst = max(worst, err)
+            ok += err < rel_tol
+            total += 1
+    return ok / total, worst
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
+                      OMNIA_LOGIT_TAP="1")
+    try:
+        from omnia_amd.engine import tp
+        from omnia_amd.engine.engine import EngineConfig
+        from omnia_amd.engine.sampling_params import SamplingParams
+        from omnia_amd.models import build_model
+        from omnia_amd.models.config import resolve
+        from omnia_amd.models.loader import shard_weights
+        from omnia_amd.parallel import state as pstate
+
+        mc = resolve("llama-3-70b").replace(name="llama-3-70b-2l", num_layers=2)
+        torch.cuda.set_device(0)
+        full = build_model(mc, device="cuda", dtype=torch.bfloat16, seed=3).w  # tp=1: whole
+        st = pstate.init_distributed(tp_size=world, device="cuda")
+        assert st.transport == "ipc" and st.backend == "gloo", (st.transport, st.backend)
+        shard = shard_weights(full, mc, world, rank)
+        if rank != 0:
+            del full
+        cfg = EngineConfig(model=mc.name, device="cuda", tp=world, num_blocks=256, block_size=16,
+                           max_batch=8, max_model_len=1024, max_prefill_tokens=64,
+                           pipeline=False, seed=3)
+        eng = tp.start(cfg, model_cfg=mc, weights=shard)
+        if eng is None:
+            return  # worker: rank 0 shut the group down
+        rng = random.Random(11)
+        V = mc.vocab_size
+        greedy = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+        prompts = [[rng.randrange(10, V - 10) for _ in range(n)] for n in (90, 41)]
+        seqs = eng.generate(prompts, greedy, session_ids=["a", "b"])
+        p2 = prompts[0] + seqs[0].output + [rng.randrange(10, V - 10) for _ in range(12)]
+        s2 = eng.generate([p2], greedy, session_ids=["a"])[0]
+        hit = s2.prefix_hit
+        seqs = seqs + [s2]
+        rows = {}
+        for ids, r in eng.runner.logit_tap:
+            for i, sid in enumerate(ids):
+                rows.setdefault(sid, []).append(r[i])
+        stats = dict(eng.runner.stats)
+        ring = dict(eng.runner.chan.ring.stats)
+        eng.shutdown()
+        plain = [(s.seq_id, list(s.prompt), list(s.output)) for s in seqs]
+        f = lambda t: t.detach().to("cpu", torch.float32)  # noqa: E731 - one host copy
+        full = {"embed": f(full["embed"]), "lm_head": f(full["lm_head"]),
+                "final_norm": f(full["final_norm"]),
+                "layers": [{k: f(v) for k, v in x.items()} for x in full["layers"]]}
+        frac, worst = _check(mc, full, plain, rows, 0.05)
+        bad = {"embed": full["embed"], "lm_head": full["lm_head"],
+               "final_norm": full["final_norm"], "layers": [dict(x) for x in full["layers"]]}
+        D, hq = mc.head_dim, mc.num_heads
+        qkv = bad["layers"][0]["qkv"].clone()
+        k0 = hq * D
+        qkv[k0:k0 + D], qkv[k0 + D:k0 + 2 * D] = (qkv[k0 + D:k0 + 2 * D].clone(),
+                                                  qkv[k0:k0 + D].clone())
+        bad["layers"][0]["qkv"] = qkv
+        bfrac, bworst = _check(mc, bad, plain, rows, 0.05)
+        err = int(pstate.get_state().custom_ar.err.item())
+        q.put(("ok", {"frac": frac, "worst": worst, "neg_frac": bfrac, "neg_worst": bworst,
+                      "hit": hit, "graph_replays": stats["graph_replays"],
+                      "captures": stats["captures"], "ring_puts": ring["puts"], "ar_err": err}))
+    except Exception:  # pragma: no cover - surfaced through the queue
+        import traceback
+
+        q.put(("err", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tp_engine_on_one_gpu_matches_dense_oracle(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        status, res = q.get(timeout=420)
+    finally:
+        for p in procs:
+            p.join(timeout=90)
+            if p.is_alive():
+                p.kill()
+    assert status == "ok", res
+    print(f"TP={world}: {res}")
+    assert res["ar_err"] == 0
+    assert res["hit"] > 0 and res["graph_replays"] > 0 and res["captures"] > 0
+    assert res["frac"] == 1.0, res
+    assert res["neg_frac"] < 1.0 and res["neg_worst"] > 0.05, res

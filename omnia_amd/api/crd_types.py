@@ -255,12 +255,16 @@ PROVIDER_TYPES = ("claude", "openai", "gemini", "ollama", "mock", "vllm", "voyag
                   "cartesia", "elevenlabs", "imagen", "huggingface", "local")
 ENGINE = Obj({
     "model": Str(), "tp": Int(1, 1, 8), "ep": Int(1, 1, 8),
-    "dtype": Enum("bfloat16", "float16", default="bfloat16"),
+    "dtype": Enum("bfloat16", "float16", "float32", default="bfloat16"),
     "maxBatch": Int(256, 1), "kvFraction": {"type": "number", "default": 0.85,
                                             "minimum": 0.05, "maximum": 0.98},
     "maxModelLen": Int(8192, 16), "blockSize": Int(32, 8, 256),
     "swapGiB": {"type": "number", "default": 0, "minimum": 0}, "tokenizer": Str(),
-    "mixedBudget": Int(minimum=0), "contextParallel": Int(minimum=1, maximum=8)})
+    "mixedBudget": Int(minimum=0), "contextParallel": Int(minimum=1, maximum=8),
+    # single-node engine knobs (device "cpu" runs the reference ops: tests, dev boxes)
+    "device": Enum("cuda", "cpu"), "epMode": Enum("tp", "a2a"),
+    "numBlocks": Int(minimum=16), "useGraphs": {"type": "boolean"},
+    "cpThreshold": Int(minimum=0)})
 PROVIDER = Obj({
     "type": Enum(*PROVIDER_TYPES), "role": Enum("llm", "embedding", "tts", "stt", "image",
                                                 "inference", default="llm"),

@@ -38,6 +38,14 @@ RECORDING_DROPPED = Counter("omnia_facade_recording_dropped_total",
 RATE_LIMITED = Counter("omnia_facade_rate_limited_total", "Messages rejected by rate limit",
                        ["kind"], registry=REGISTRY)
 DRAINING = Gauge("omnia_facade_draining", "1 while the facade drains", registry=REGISTRY)
+POD_COLD_START = Histogram("omnia_pod_cold_start_seconds",
+                           "Agent pod start to ready (process spawn, engine weights + KV, facade)",
+                           ["agent", "namespace"],
+                           buckets=(1, 2, 5, 10, 20, 30, 60, 120, 300, 600, 900),
+                           registry=REGISTRY)
+ENGINE_COLD_START = Gauge("omnia_engine_cold_start_seconds",
+                          "Engine start-up time by phase (weights, kv_alloc, graph_warmup, total)",
+                          ["phase"], registry=REGISTRY)
 # realtime blip-resume + drain (internal/agent/metrics.go:298-340)
 REALTIME_PARKED = Counter("omnia_facade_realtime_sessions_parked_total",
                           "Realtime sessions parked after a client disconnect", registry=REGISTRY)

@@ -103,6 +103,12 @@ def runtime_config(ar: dict, pack: dict, providers: list[dict], registry: dict |
                     "max_model_len": eng.get("maxModelLen", 8192),
                     "block_size": eng.get("blockSize", 32), "dtype": eng.get("dtype",
                                                                              "bfloat16")}
+        extra = {"swapGiB": "swap_gib", "mixedBudget": "mixed_budget", "epMode": "ep_mode",
+                 "numBlocks": "num_blocks", "useGraphs": "use_graphs", "device": "device",
+                 "cpThreshold": "cp_threshold", "tokenizer": "tokenizer"}
+        for k, v in eng.items():  # the engine knobs beyond the core sizing fields
+            if k in extra and v is not None:
+                c.engine[extra[k]] = v
     mem = spec.get("memory") or {}
     c.memory_enabled = bool(mem.get("enabled"))
     c.eval_enabled = bool((spec.get("evals") or {}).get("enabled"))

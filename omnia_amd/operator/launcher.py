@@ -20,6 +20,15 @@ It writes back ``status.readyReplicas`` and the Service's ``status.endpoint``
 (``status.endpoints`` lists every ready replica).  Pod template changes
 (config-hash annotation) restart the pods; replicas=0 (scale-to-zero /
 capability gate) stops them.
+
+Autoscaling (process mode): KEDA ScaledObjects are evaluated here
+(:class:`~omnia_amd.operator.keda.KedaScaler`, metrics scraped from the
+replicas' facades), and an agent whose ScaledObject allows zero replicas is
+fronted by an :class:`~omnia_amd.operator.keda.Activator` -- the Service's
+stable endpoint -- which parks connections while the first replica cold-starts.
+Each replica's cold start (process spawn, engine weights + KV allocation, to
+readiness) is recorded on the Deployment status (``coldStartSeconds``) and as
+``omnia_pod_cold_start_seconds``.
 """
 from __future__ import annotations
 
@@ -106,6 +115,42 @@ class LocalLauncher:
         self.mode = mode
         self.devices = DeviceAllocator(gpu_count)
         self.task = None
+        from .keda import KedaScaler
+
+        self.scaler = KedaScaler(store, self._keda_samples)
+        self.activators: dict[tuple, object] = {}  # (ns, name) -> Activator
+        self.cold_start_s: dict[tuple, float] = {}
+
+    async def _keda_samples(self, ns: str, name: str) -> list:
+        """Metric samples of one scale target: every ready replica's facade
+        ``/metrics`` plus the activator's parked connections."""
+        import aiohttp
+
+        from .keda import parse_prom_text
+
+        out = []
+        reps = [r for r in self.replicas.get((ns, name), []) if r.ready and r.port]
+        if reps:
+            async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=5)) as s:
+                for r in reps:
+                    async with s.get(f"http://127.0.0.1:{r.port}/metrics") as resp:
+                        out.extend(parse_prom_text(await resp.text()))
+        act = self.activators.get((ns, name))
+        if act is not None:
+            out.extend(act.samples())
+        return out
+
+    async def _sync_activators(self):
+        from .keda import Activator
+
+        want = self.scaler.scale_to_zero_targets()
+        for key in [k for k in self.activators if k not in want]:
+            await self.activators.pop(key).stop()
+        for key in want:
+            if key not in self.activators:
+                act = Activator(key[1], key[0])
+                await act.start()
+                self.activators[key] = act
 
     def _materialise(self, dep: dict, pod: Pod):
         ns = dep["metadata"]["namespace"]
@@ -351,11 +396,20 @@ class LocalLauncher:
         pod = ProcessPod(f"{key[1]}-{index}", renv, fenv, device_index=devices,
                          log_dir=os.path.join(workdir, "logs"),
                          tp=int(renv.get("OMNIA_ENGINE_TP", "1") or 1))
+        import time
+
+        t0 = time.perf_counter()
         try:
             pod.start(timeout_s=float(os.environ.get("OMNIA_POD_START_TIMEOUT", "900")))
         except Exception:
             self.devices.release(who)
             raise
+        cold = time.perf_counter() - t0
+        self.cold_start_s[key] = cold
+        from ..observability import metrics as M
+
+        M.POD_COLD_START.labels(key[1], key[0]).observe(cold)
+        log.info("pod %s/%s replica %d ready in %.2fs (cold start)", key[0], key[1], index, cold)
         r = _ProcReplica(key, index, thash, pod, devices)
         r.port = pod.facade_port
         r.ready = True
@@ -398,6 +452,7 @@ class LocalLauncher:
         if self.mode == "process":
             await self._sync_services()
             await self._sync_jobs()
+            await self._sync_activators()
         for d in deps:
             ns, name = d["metadata"]["namespace"], d["metadata"]["name"]
             replicas = d["spec"].get("replicas", 1)
@@ -451,11 +506,15 @@ class LocalLauncher:
                 for r in self.replicas.pop(key):
                     await r.stop()
                     self.devices.release((key, r.index))
+        if self.mode == "process":
+            await self.scaler.tick()
 
     def _write_status(self, d: dict, ready: int, name: str, ns: str, key):
         st = d.get("status") or {}
         want = {"replicas": ready, "readyReplicas": ready, "availableReplicas": ready,
                 "observedGeneration": d["metadata"]["generation"]}
+        if key in self.cold_start_s:
+            want["coldStartSeconds"] = round(self.cold_start_s[key], 3)
         if any(st.get(k) != v for k, v in want.items()):
             d["status"] = {**st, **want}
             d["metadata"].pop("resourceVersion", None)
@@ -463,11 +522,15 @@ class LocalLauncher:
         track = d["metadata"].get("labels", {}).get(B.LABEL_TRACK, "stable")
         svc = self.store.try_get("Service", name, ns) if track == "stable" else None
         reps = [r for r in self.replicas.get(key, []) if r.ready]
-        if svc is not None and reps:
-            eps = [f"127.0.0.1:{r.port}" for r in reps]
+        eps = [f"127.0.0.1:{r.port}" for r in reps]
+        act = self.activators.get(key)
+        if act is not None:
+            act.set_backends(eps)  # the stable front parks traffic while eps == []
+        if svc is not None and (reps or act is not None):
+            front = act.endpoint if act is not None else eps[0]
             cur = svc.get("status") or {}
-            if cur.get("endpoint") != eps[0] or cur.get("endpoints") != eps:
-                svc["status"] = {**cur, "endpoint": eps[0], "endpoints": eps}
+            if cur.get("endpoint") != front or cur.get("endpoints") != eps:
+                svc["status"] = {**cur, "endpoint": front, "endpoints": eps}
                 svc["metadata"].pop("resourceVersion", None)
                 self.store.update_status(svc)
 
@@ -498,6 +561,9 @@ class LocalLauncher:
         for p in list(self.pods.values()):
             await p.stop()
         self.pods.clear()
+        for act in list(self.activators.values()):
+            await act.stop()
+        self.activators.clear()
         for key, reps in list(self.replicas.items()):
             for r in reps:
                 await r.stop()

@@ -5,13 +5,13 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=gpurun_out/r3
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 420 --timeout-method thread > $O/gpu_tests.log 2>&1
-rc=$?; echo "gpu tests rc=$rc"; grep -E "passed|failed|error" $O/gpu_tests.log | tail -3
-grep -E "^TP=" $O/gpu_tests.log | head
-[ $rc -eq 0 ] || { tail -60 $O/gpu_tests.log; exit $rc; }
 timeout -k 10 600 python -u bench.py --steps 5 --warmup 2 > $O/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 $O/bench.log | cut -c1-700
 [ $rc -eq 0 ] || { tail -30 $O/bench.log; exit $rc; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 420 --timeout-method thread > $O/gpu_tests.log 2>&1
+rc=$?; echo "gpu tests rc=$rc"; grep -E "passed|failed|error" $O/gpu_tests.log | tail -3
+grep -E "^TP=|FAILED" $O/gpu_tests.log | head
+[ $rc -eq 0 ] || { grep -B5 -A30 "Error" $O/gpu_tests.log | head -80; exit $rc; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/r3prof -o run -- python3 bench.py --steps 2 --warmup 1 > $O/prof_bench.log 2>&1
 rc=$?; echo "prof rc=$rc"; tail -1 $O/prof_bench.log | cut -c1-300
 [ $rc -eq 0 ] || exit $rc

@@ -1,0 +1,258 @@
+"""Single-node KEDA (BASELINE config 4's "KEDA scale-to-zero on the
+active-connection metric"): the PromQL subset, the ScaledObject replica math
+(``internal/controller/autoscaling.go:167-325`` semantics: threshold per pod,
+immediate scale-up, scale-down to minReplicaCount after cooldownPeriod), the
+activator that parks connections while a replica cold-starts, and the whole
+loop under ``omnia serve``'s process launcher: connect -> scale from zero -> the
+turn streams from a TP=2 engine -> idle -> scale to zero."""
+import asyncio
+import time
+
+import aiohttp
+import pytest
+from aiohttp import web
+
+from omnia_amd.api import crds
+from omnia_amd.operator.apistore import APIStore, get_condition
+from omnia_amd.operator.keda import Activator, KedaScaler, eval_query, parse_prom_text
+
+PROM = """# HELP omnia_agent_connections_active Active WebSocket connections
+# TYPE omnia_agent_connections_active gauge
+omnia_agent_connections_active{agent="a",namespace="default"} 150.0
+omnia_agent_connections_active{agent="a",namespace="other"} 7.0
+omnia_agent_connections_active{agent="b",namespace="default"} 3.0
+omnia_agent_requests_total{agent="a",namespace="default",status="ok"} 12.0
+"""
+
+
+def test_prom_text_and_query_subset():
+    s = parse_prom_text(PROM)
+    assert len(s) == 4 and s[0] == ("omnia_agent_connections_active",
+                                    {"agent": "a", "namespace": "default"}, 150.0)
+    q = 'sum(omnia_agent_connections_active{agent="a",namespace="default"})'
+    assert eval_query(q, s) == 150.0
+    assert eval_query('sum(omnia_agent_connections_active{namespace="default"})', s) == 153.0
+    assert eval_query('max(omnia_agent_connections_active{agent=~"a|b"})', s) == 150.0
+    assert eval_query('count(omnia_agent_connections_active{namespace!="default"})', s) == 1.0
+    assert eval_query('sum(omnia_agent_connections_active{agent="zz"})', s) is None
+    assert eval_query('sum(omnia_agent_connections_active{agent="zz"}) or vector(0)', s) == 0.0
+    assert eval_query('omnia_agent_requests_total{status="ok"}', s) == 12.0
+    with pytest.raises(ValueError):
+        eval_query("rate(x[5m])", s)
+
+
+def _store_with(min_r=0, max_r=4, poll=1, cool=3, threshold="200", replicas=1):
+    st = APIStore()
+    st.apply({"apiVersion": "apps/v1", "kind": "Deployment",
+              "metadata": {"name": "a", "namespace": "default"},
+              "spec": {"replicas": replicas, "template": {"metadata": {}, "spec": {}}}})
+    st.apply({"apiVersion": "keda.sh/v1alpha1", "kind": "ScaledObject",
+              "metadata": {"name": "a", "namespace": "default"},
+              "spec": {"scaleTargetRef": {"name": "a"}, "minReplicaCount": min_r,
+                       "maxReplicaCount": max_r, "pollingInterval": poll, "cooldownPeriod": cool,
+                       "triggers": [{"type": "prometheus", "metadata": {
+                           "query": 'sum(omnia_agent_connections_active{agent="a",'
+                                    'namespace="default"})', "threshold": threshold}}]}})
+    return st
+
+
+def test_scaler_replica_math_and_cooldown():
+    st = _store_with()
+    now = [1000.0]
+    conns = [0.0]
+
+    async def samples(ns, name):
+        return [("omnia_agent_connections_active", {"agent": "a", "namespace": "default"},
+                 conns[0])]
+
+    sc = KedaScaler(st, samples, clock=lambda: now[0])
+    reps = lambda: st.get("Deployment", "a", "default")["spec"]["replicas"]  # noqa: E731
+
+    async def run():
+        out = []
+        for t, c in [(0, 0), (1, 0), (2, 0), (3, 0), (4, 450), (4.5, 450), (5, 450), (6, 10),
+                     (7, 10), (8, 10), (9, 10), (10, 0), (11, 0), (12, 0), (13, 0)]:
+            now[0] = 1000.0 + t
+            conns[0] = c
+            await sc.tick()
+            out.append(reps())
+        return out
+
+    got = asyncio.run(run())
+    # idle from the start: cooldown (3 s) then min (0); 450 conns / 200 -> 3 pods at once
+    # (polling interval 1 s skips t=4.5); 10 conns hold 3 pods until the cooldown after
+    # the scale-up (t=7), then ceil(10/200)=1; idle from t=10 -> 0 once the last
+    # activity (t=9) is 3 s old
+    assert got == [1, 1, 1, 0, 3, 3, 3, 3, 1, 1, 1, 1, 1, 0, 0], got
+    so = st.get("ScaledObject", "a", "default")
+    assert get_condition(so, "Ready")["status"] == "True"
+    assert get_condition(so, "Active")["status"] == "False"
+    assert so["status"]["currentReplicas"] == 0 and "lastActiveTime" in so["status"]
+
+
+def test_scaler_respects_min_and_max():
+    st = _store_with(min_r=2, max_r=3, cool=0, replicas=2)
+
+    async def samples(ns, name):
+        return [("omnia_agent_connections_active", {"agent": "a", "namespace": "default"},
+                 5000.0)]
+
+    sc = KedaScaler(st, samples, clock=lambda: 0.0)
+    asyncio.run(sc.tick())
+    assert st.get("Deployment", "a", "default")["spec"]["replicas"] == 3
+
+    async def idle(ns, name):
+        return []
+
+    sc2 = KedaScaler(st, idle, clock=lambda: 100.0)
+    asyncio.run(sc2.tick())
+    assert st.get("Deployment", "a", "default")["spec"]["replicas"] == 2  # never below min
+
+
+def test_activator_parks_until_a_backend_is_ready_then_relays():
+    async def run():
+        up = web.Application()
+
+        async def ws(request):
+            w = web.WebSocketResponse()
+            await w.prepare(request)
+            async for m in w:
+                await w.send_str("echo:" + m.data)
+            return w
+
+        up.router.add_get("/ws", ws)
+        up.router.add_get("/hello", lambda r: web.json_response({"q": r.query.get("x")}))
+        runner = web.AppRunner(up)
+        await runner.setup()
+        site = web.TCPSite(runner, "127.0.0.1", 0)
+        await site.start()
+        be = f"127.0.0.1:{site._server.sockets[0].getsockname()[1]}"
+        act = Activator("a", "default", timeout_s=10)
+        ep = await act.start()
+        try:
+            async with aiohttp.ClientSession() as s:
+                task = asyncio.ensure_future(s.ws_connect(f"ws://{ep}/ws"))
+                for _ in range(100):
+                    if act.parked:
+                        break
+                    await asyncio.sleep(0.02)
+                parked = act.parked
+                assert act.samples()[0][2] == 1.0  # counted as an active connection
+                act.set_backends([be])
+                w = await asyncio.wait_for(task, 5)
+                await w.send_str("hi")
+                msg = await w.receive_str(timeout=5)
+                await w.close()
+                r = await s.get(f"http://{ep}/hello?x=1")
+                body = await r.json()
+                act.set_backends([])
+                act.timeout_s = 0.2
+                r2 = await s.get(f"http://{ep}/hello")
+                return parked, msg, body, r2.status
+        finally:
+            await act.stop()
+            await runner.cleanup()
+
+    parked, msg, body, late = asyncio.run(run())
+    assert parked == 1 and msg == "echo:hi" and body == {"q": "1"} and late == 503
+
+
+MANIFESTS = """
+apiVersion: omnia.altairalabs.ai/v1alpha1
+kind: Provider
+metadata: {name: tiny, namespace: default}
+spec:
+  type: local
+  model: tiny-llama
+  engine: {model: tiny-llama, tp: 2, maxBatch: 4, maxModelLen: 512, numBlocks: 64,
+           blockSize: 16, dtype: float32, useGraphs: false}
+---
+apiVersion: v1
+kind: ConfigMap
+metadata: {name: pack, namespace: default}
+data:
+  pack.json: |
+    {"id": "p", "name": "P", "version": "1.0.0",
+     "template_engine": {"version": "v1", "syntax": "{{variable}}"},
+     "prompts": {"default": {"id": "default", "name": "D", "version": "1.0.0",
+       "system_template": "You are terse.",
+       "parameters": {"temperature": 0, "max_tokens": 6, "ignore_eos": true}}}}
+---
+apiVersion: omnia.altairalabs.ai/v1alpha1
+kind: PromptPack
+metadata: {name: pack, namespace: default}
+spec: {packName: p, version: "1.0.0", source: {type: configmap, configMapRef: {name: pack}}}
+---
+apiVersion: omnia.altairalabs.ai/v1alpha1
+kind: AgentRuntime
+metadata: {name: z, namespace: default}
+spec:
+  promptPackRef: {name: pack}
+  facades: [{type: websocket}]
+  providers: [{name: llm, providerRef: {name: tiny}}]
+  runtime:
+    replicas: 0
+    autoscaling:
+      enabled: true
+      type: keda
+      minReplicas: 0
+      maxReplicas: 1
+      keda: {pollingInterval: 1, cooldownPeriod: 3}
+"""
+
+
+def test_serve_scales_from_zero_and_back_to_zero_tp2_cpu():
+    import yaml
+
+    from omnia_amd.ee.arena.fleet import FleetSession
+    from omnia_amd.operator.launcher import LocalLauncher
+    from omnia_amd.operator.manager import Manager, new_store
+
+    docs = [d for d in yaml.safe_load_all(MANIFESTS) if d]
+    for d in docs:
+        d.setdefault("apiVersion", crds.API_VERSION)
+
+    async def go():
+        store = new_store()
+        mgr = Manager(store)
+        await mgr.start()
+        launcher = LocalLauncher(store, mode="process")
+        launcher.start()
+        try:
+            for d in docs:
+                store.apply(d)
+            ep = None
+            for _ in range(300):
+                svc = store.try_get("Service", "z")
+                ep = ((svc or {}).get("status") or {}).get("endpoint")
+                if ep and store.try_get("ScaledObject", "z") is not None:
+                    break
+                await asyncio.sleep(0.1)
+            assert ep, "activator endpoint never published"
+            assert not launcher.replicas.get(("default", "z"))  # at zero: no pod
+            t0 = time.monotonic()
+            async with FleetSession(f"ws://{ep}/ws", timeout_s=300) as fs:
+                r = await fs.turn("hello there")
+            first_turn_s = time.monotonic() - t0
+            dep = store.get("Deployment", "z")
+            cold = dep["status"].get("coldStartSeconds")
+            up = dep["spec"]["replicas"]
+            # idle: cooldown 3 s, poll 1 s -> back to zero, pod stopped
+            for _ in range(300):
+                if store.get("Deployment", "z")["spec"]["replicas"] == 0 and \
+                        not launcher.replicas.get(("default", "z")):
+                    break
+                await asyncio.sleep(0.1)
+            down = store.get("Deployment", "z")["spec"]["replicas"]
+            so = store.get("ScaledObject", "z")
+            return r, up, down, cold, first_turn_s, so, launcher.replicas.get(("default", "z"))
+        finally:
+            await launcher.stop()
+            await mgr.stop()
+
+    r, up, down, cold, first_s, so, reps = asyncio.run(go())
+    assert (r["usage"] or {}).get("output_tokens") == 6 and not r.get("error"), r
+    assert up == 1 and down == 0 and not reps
+    assert cold and 0 < cold < first_s
+    assert get_condition(so, "Ready")["status"] == "True"
+    print(f"scale-from-zero: pod cold start {cold:.1f}s, first turn {first_s:.1f}s")

@@ -260,11 +260,13 @@ class A2AClient:
         return d["result"]
 
 
-def a2a_tool_handler(name: str, url: str, description: str = ""):
+def a2a_tool_handler(name: str, url: str, description: str = "",
+                     headers: dict | None = None):
     """An InProcessHandler exposing a remote agent as a tool (multi-agent chains)."""
     from ..tools.executor import InProcessHandler
 
-    client = A2AClient(url)
+    client = A2AClient(url if url.rstrip("/").endswith("/a2a") else url.rstrip("/") + "/a2a",
+                       headers=headers)
 
     async def call(args, ctx):
         task = await client.send(args.get("message") or args.get("input") or json.dumps(args),

@@ -8,6 +8,7 @@ AgentRuntimes that reference it, a Deployment change re-queues its owner).
 from __future__ import annotations
 
 import json
+import re
 import logging
 import time
 
@@ -320,6 +321,44 @@ def workspace_service_group(store: APIStore, ns: str, group: str) -> dict | None
     return None
 
 
+def resolve_a2a_clients(store, ar: dict) -> tuple[list, list]:
+    """``spec.facades[].a2a.clients[]`` -> (resolved ``OMNIA_A2A_CLIENTS`` entries,
+    per-client status ``{name, ready, resolvedURL | error}``)
+    (``internal/controller/a2a_client_resolver.go``)."""
+    from .builders import FACADE_PORT
+
+    md = ar["metadata"]
+    out, status = [], []
+    for fac in ar["spec"].get("facades") or []:
+        for c in ((fac.get("a2a") or {}).get("clients") or []):
+            st = {"name": c["name"]}
+            url = ""
+            ref = c.get("agentRuntimeRef")
+            if ref:
+                ns = ref.get("namespace") or md["namespace"]
+                tgt = store.try_get("AgentRuntime", ref["name"], ns)
+                if tgt is None:
+                    st.update(ready=False, error=f"AgentRuntime {ns}/{ref['name']} not found")
+                    status.append(st)
+                    continue
+                ep = ((tgt.get("status") or {}).get("a2a") or {}).get("endpoint")
+                url = ep or f"http://{ref['name']}.{ns}.svc.cluster.local:{FACADE_PORT}/a2a"
+            elif c.get("url"):
+                url = c["url"]
+            else:
+                st.update(ready=False, error="either agentRuntimeRef or url must be specified")
+                status.append(st)
+                continue
+            st.update(ready=True, resolvedURL=url)
+            status.append(st)
+            rc = {"name": c["name"], "url": url, "exposeAsTools": bool(c.get("exposeAsTools"))}
+            if (c.get("authentication") or {}).get("secretRef"):
+                rc["authTokenEnv"] = "OMNIA_A2A_CLIENT_TOKEN_" + re.sub(
+                    r"[^A-Z0-9]", "_", c["name"].upper())
+            out.append(rc)
+    return out, status
+
+
 class AgentRuntimeReconciler:
     kind = "AgentRuntime"
 
@@ -404,6 +443,13 @@ class AgentRuntimeReconciler:
                       (spec.get("framework") or {}).get("type", "omnia-mi355x"), gen)
         # ---- capability gate: a local engine needs GPUs on the node
         rc = B.runtime_config(ar, pack, providers, registry)
+        # ---- outbound A2A clients (a2a_client_resolver.go): agentRuntimeRef -> the
+        # target's service DNS (the node launcher rewrites it to the local endpoint)
+        rc.a2a_clients, a2a_status = resolve_a2a_clients(store, ar)
+        if a2a_status:
+            st["a2a"] = {**(st.get("a2a") or {}), "clients": a2a_status}
+        else:
+            (st.get("a2a") or {}).pop("clients", None)
         replicas = None
         cap_ok = True
         if rc.provider.get("type") == "local" and self.gpu_count is not None:

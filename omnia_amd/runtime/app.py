@@ -140,6 +140,19 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
                                      strategy=cfg.memory_strategy, deny_cel=cfg.memory_deny_cel,
                                      limit=cfg.memory_limit)
         executor.add_handler(memory_tools(memory.client, ws, cfg.agent_name))
+    for c in cfg.a2a_clients:  # remote agents as tools (client_resolver.go BuildA2AAgentOptions)
+        if not c.get("exposeAsTools") or not c.get("url"):
+            continue
+        from ..facade.a2a import a2a_tool_handler
+
+        headers = {}
+        tok = os.environ.get(c.get("authTokenEnv") or "", "")
+        if tok:
+            headers["Authorization"] = f"Bearer {tok}"
+        executor.add_handler(a2a_tool_handler(c["name"], c["url"], c.get("description", ""),
+                                              headers=headers))
+        log.info("A2A agent %s (%s) registered as tool ask_%s", c["name"], c["url"],
+                 c["name"])
     try:
         from .skills import attach_skills
 

@@ -52,6 +52,9 @@ class RuntimeConfig:
     grpc_port: int = 9000
     health_port: int = 9001
     engine: dict = field(default_factory=dict)
+    # resolved outbound A2A clients ``[{name, url, exposeAsTools, authTokenEnv}]``
+    # (OMNIA_A2A_CLIENTS, ``internal/controller/a2a_client_resolver.go``)
+    a2a_clients: list = field(default_factory=list)
 
     @classmethod
     def from_env(cls, env=None) -> "RuntimeConfig":
@@ -107,6 +110,8 @@ class RuntimeConfig:
         c.health_port = int(e.get("OMNIA_HEALTH_PORT", c.health_port))
         c.engine = {k[len("OMNIA_ENGINE_"):].lower(): v for k, v in e.items()
                     if k.startswith("OMNIA_ENGINE_")}
+        if e.get("OMNIA_A2A_CLIENTS"):
+            c.a2a_clients = json.loads(e["OMNIA_A2A_CLIENTS"])
         return c
 
     def to_env(self) -> dict:
@@ -148,6 +153,8 @@ class RuntimeConfig:
                 env["OMNIA_MEMORY_DENY_CEL"] = self.memory_deny_cel
         if self.eval_enabled:
             env["OMNIA_EVAL_ENABLED"] = "true"
+        if self.a2a_clients:
+            env["OMNIA_A2A_CLIENTS"] = json.dumps(self.a2a_clients)
         for k, v in self.engine.items():
             env["OMNIA_ENGINE_" + k.upper()] = str(v)
         return env

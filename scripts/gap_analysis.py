@@ -34,6 +34,25 @@ def main(path, out=None):
         g = [x[0] for x in gaps if lo <= x[0] < hi]
         lines.append(f"gaps {lo / 1e3:>8.0f}-{hi / 1e3:<10.0f}us: n={len(g):7d} "
                      f"total={sum(g) / 1e6:9.1f} ms")
+    # where the mid-size gaps (0.1-10 ms: host-side stalls inside a wave, not the
+    # wave-boundary waits) sit: by the kernel pair around them
+    from collections import Counter
+
+    pairs = Counter()
+    tot = Counter()
+    for g, t, a, b in gaps:
+        if 1e5 <= g < 1e7:
+            k = f"{a[:45]} -> {b[:45]}"
+            pairs[k] += 1
+            tot[k] += g
+    lines.append("0.1-10 ms gaps by kernel pair (count, total ms):")
+    for k, n in pairs.most_common(12):
+        lines.append(f"  {n:5d} {tot[k] / 1e6:9.1f} ms  {k}")
+    # timeline of the mid-size gaps: count per 100 ms bucket of the run
+    buckets = Counter(int((t - iv[0][0]) / 1e8) for g, t, a, b in gaps if 1e5 <= g < 1e7)
+    if buckets:
+        lines.append("0.1-10 ms gaps per 100 ms of the run (bucket: count): " + ", ".join(
+            f"{k / 10:.1f}s:{v}" for k, v in sorted(buckets.items())))
     lines.append("largest gaps (ms, at s from start, after -> before):")
     for g, t, a, b in sorted(gaps, reverse=True)[:25]:
         lines.append(f"  {g / 1e6:8.2f} ms at {(t - iv[0][0]) / 1e9:8.3f} s  {a} -> {b}")

@@ -29,3 +29,31 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+def release_gpu_memory():
+    """Free what earlier GPU tests left in this pytest process: the runtime's
+    process-wide cached engines (each holds a KV pool sized from free HBM) and
+    the caching allocator's blocks -- before a test that shares the card with
+    child processes."""
+    import gc
+
+    try:
+        import torch
+    except Exception:  # pragma: no cover
+        return
+    try:
+        from omnia_amd.runtime import app
+
+        for eng in list(app._ENGINES.values()):
+            try:
+                eng.shutdown()
+            except Exception:  # noqa: BLE001
+                pass
+        app._ENGINES.clear()
+    except Exception:  # noqa: BLE001
+        pass
+    gc.collect()
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()

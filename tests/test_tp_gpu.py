@@ -47,6 +47,47 @@ def _check(mc, w, seqs, rows_by_seq, rel_tol):
     return ok / total, worst
 
 
+def _sharded_weights(mc, rank, world, keep_full: bool):
+    """This rank's Megatron shard of a seeded random model, generated tensor by
+    tensor on the GPU (every rank draws the same sequence) and sliced at once,
+    so a rank never holds more than one full layer; rank 0 also keeps an fp32
+    host copy of the full model for the oracle."""
+    import math
+
+    from omnia_amd.models.loader import shard_layer, shard_weights
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    dt, d, D = torch.bfloat16, mc.hidden_size, mc.head_dim
+
+    def init(shape, std):
+        t = torch.empty(shape, dtype=torch.float32, device="cuda").normal_(0.0, std, generator=g)
+        return t.to(dt)
+
+    host = lambda t: t.detach().to("cpu", torch.float32)  # noqa: E731
+    embed = init((mc.vocab_size, d), 0.02)
+    lm = init((mc.vocab_size, d), 0.02)
+    norm = torch.ones(d, dtype=dt, device="cuda")
+    top = {"embed": embed, "lm_head": lm, "final_norm": norm, "layers": []}
+    shard = shard_weights(top, mc, world, rank)
+    full = {"embed": host(embed), "lm_head": host(lm), "final_norm": host(norm),
+            "layers": []} if keep_full else None
+    del embed, lm, top
+    std_o = 0.02 / math.sqrt(2 * mc.num_layers)
+    for _ in range(mc.num_layers):
+        layer = {"in_norm": torch.ones(d, dtype=dt, device="cuda"),
+                 "post_norm": torch.ones(d, dtype=dt, device="cuda"),
+                 "qkv": init(((mc.num_heads + 2 * mc.num_kv_heads) * D, d), 0.02),
+                 "o": init((d, mc.num_heads * D), std_o),
+                 "gate_up": init((2 * mc.intermediate_size, d), 0.02),
+                 "down": init((d, mc.intermediate_size), std_o)}
+        shard["layers"].append(shard_layer(layer, mc, world, rank))
+        if keep_full:
+            full["layers"].append({k: host(v) for k, v in layer.items()})
+        del layer
+        torch.cuda.empty_cache()
+    return shard, full
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
@@ -55,23 +96,14 @@ def _worker(rank, world, port, q):
         from omnia_amd.engine import tp
         from omnia_amd.engine.engine import EngineConfig
         from omnia_amd.engine.sampling_params import SamplingParams
-        from omnia_amd.models import build_model
         from omnia_amd.models.config import resolve
-        from omnia_amd.models.loader import shard_weights
         from omnia_amd.parallel import state as pstate
 
         mc = resolve("llama-3-70b").replace(name="llama-3-70b-2l", num_layers=2)
         torch.cuda.set_device(0)
-        full = build_model(mc, device="cuda", dtype=torch.bfloat16, seed=3).w  # tp=1: whole
+        shard, full = _sharded_weights(mc, rank, world, keep_full=rank == 0)
         st = pstate.init_distributed(tp_size=world, device="cuda")
         assert st.transport == "ipc" and st.backend == "gloo", (st.transport, st.backend)
-        shard = shard_weights(full, mc, world, rank)
-        f = lambda t: t.detach().to("cpu", torch.float32)  # noqa: E731 - the oracle's copy
-        full = ({"embed": f(full["embed"]), "lm_head": f(full["lm_head"]),
-                 "final_norm": f(full["final_norm"]),
-                 "layers": [{k: f(v) for k, v in x.items()} for x in full["layers"]]}
-                if rank == 0 else None)
-        torch.cuda.empty_cache()  # 8 ranks share the card: hand the full model back
         cfg = EngineConfig(model=mc.name, device="cuda", tp=world, num_blocks=256, block_size=16,
                            max_batch=8, max_model_len=1024, max_prefill_tokens=64,
                            pipeline=False, seed=3)
@@ -117,8 +149,9 @@ def _worker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_tp_engine_on_one_gpu_matches_dense_oracle(world):
-    if torch.cuda.is_initialized():
-        torch.cuda.empty_cache()  # this process's cached blocks from earlier tests
+    from conftest import release_gpu_memory
+
+    release_gpu_memory()  # engines / cached blocks earlier tests left in this process
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

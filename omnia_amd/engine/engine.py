@@ -140,8 +140,14 @@ class LLMEngine:
 
             nb = agree_num_blocks(nb, dev)
             runner_cls = TPModelRunner
+        t_kv = time.perf_counter()
         self.kv = KVCache.allocate(self.model_cfg, nb, cfg.block_size, dev,
                                    tp_size=self.model.tp, dtype=dtype)
+        self.kv_alloc_s = time.perf_counter() - t_kv
+        # pod cold-start breakdown (omnia_engine_cold_start_seconds{phase}); decode
+        # graphs are captured lazily per bucket and reported as graph_warmup
+        M.ENGINE_COLD_START.labels("weights").set(self.load_s)
+        M.ENGINE_COLD_START.labels("kv_alloc").set(self.kv_alloc_s)
         self.runner = runner_cls(self.model, self.kv, max_batch=cfg.max_batch,
                                  max_model_len=cfg.max_model_len, use_graphs=cfg.use_graphs,
                                  max_prefill_tokens=cfg.max_prefill_tokens)
@@ -161,6 +167,7 @@ class LLMEngine:
                             mixed_budget=cfg.mixed_budget if self.model.tp == 1 else 0,
                             cp_threshold=cfg.cp_threshold if self.cp_lockstep else 0),
             self.blocks)
+        self.scheduler.on_capped = self._finish_capped
         self.tokenizer = make_tokenizer(self.model_cfg, cfg.tokenizer)
         self.eos = set(self.tokenizer.eos_token_ids)
         self.seqs: dict[int, Sequence] = {}
@@ -175,8 +182,10 @@ class LLMEngine:
                        "append_s": 0.0, "pipeline_breaks": 0, "gpu_starved_launches": 0}
         self.step_trace = [] if os.environ.get("OMNIA_STEP_TRACE") else None
         self.gpu_trace: list = []
-        log.info("engine ready: %s on %s (tp=%d), %d KV blocks x %d tokens, load %.1fs",
-                 self.model_cfg.name, dev, st.tp_size, nb, cfg.block_size, self.load_s)
+        M.ENGINE_COLD_START.labels("total").set(time.perf_counter() - t0)
+        log.info("engine ready: %s on %s (tp=%d), %d KV blocks x %d tokens, load %.1fs, "
+                 "kv alloc %.2fs", self.model_cfg.name, dev, st.tp_size, nb, cfg.block_size,
+                 self.load_s, self.kv_alloc_s)
 
     @staticmethod
     def _pick_device(cfg: EngineConfig) -> torch.device:
@@ -210,6 +219,11 @@ class LLMEngine:
             from ..parallel import state as pstate
 
             share = pstate.ranks_per_device()  # TP ranks rehearsed on one device
+            # pods sharing each GPU (the launcher's OMNIA_GPU_SHARE, 288 GB devices):
+            # this pod's slice is total / pods, less what it already holds
+            pods = max(1, int(os.environ.get("OMNIA_GPU_SHARE", "1") or 1))
+            if pods > 1:
+                free = max(0, min(free, int(total / pods) - torch.cuda.memory_reserved(device)))
             budget = max(0, int(free * cfg.kv_fraction / share) - reserve)
         else:
             budget = 256 * 2**20
@@ -494,6 +508,15 @@ class LLMEngine:
                 s.num_cached = min(s.num_cached, s.length - 1)
             self.scheduler.finish(s, reason)
             self._finalize(s)
+
+    def _finish_capped(self, s: Sequence) -> None:
+        """The scheduler finished ``s`` because the KV pool cannot hold its next
+        token and nothing else can be preempted."""
+        log.warning("sequence %s hit the KV pool capacity (%d tokens): finished as length",
+                    s.request_id, s.length)
+        if s.n_real < len(s.output):
+            del s.output[s.n_real:]
+        self._finalize(s)
 
     def _finalize(self, s: Sequence) -> None:
         self.counters["finished"] += 1

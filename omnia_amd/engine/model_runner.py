@@ -555,6 +555,9 @@ class ModelRunner:
             self.graph_exec[(nrows, ncols)] = int(g.raw_cuda_graph_exec())
         self.stats["captures"] += 1
         self.stats["capture_s"] += time.perf_counter() - t0
+        from ..observability import metrics as M
+
+        M.ENGINE_COLD_START.labels("graph_warmup").set(self.stats["capture_s"])
         return g
 
     def can_pipeline(self, seqs: list[Sequence]) -> bool:

@@ -50,6 +50,7 @@ class Scheduler:
         self.running: list[Sequence] = []
         self.partial: list[Sequence] = []  # prompts mid-way through chunked prefill
         self.cp_pending: Sequence | None = None  # admitted, waiting for its CP prefill
+        self.on_capped = None  # engine hook: a running sequence finished at pool capacity
 
     # ------------------------------------------------------------ admission
     def add(self, seq: Sequence) -> None:
@@ -168,7 +169,9 @@ class Scheduler:
         if chunks:
             return StepPlan("prefill", chunks, [])
         if self.running:
-            return StepPlan("decode", [], self._decode_rows())
+            decode = self._decode_rows()  # may cap the last sequence at pool capacity
+            if decode:
+                return StepPlan("decode", [], decode)
         return StepPlan("idle", [], [])
 
     def _prefill_chunks(self, budget: int) -> list:
@@ -227,7 +230,13 @@ class Scheduler:
                     break
                 except OutOfBlocks:
                     if not self._preempt_one(protect=s):
-                        raise
+                        if self.on_capped is None:
+                            raise
+                        # nothing left to preempt: the KV pool is this sequence's
+                        # context limit -- finish it ("length") instead of faulting
+                        self.finish(s, FinishReason.LENGTH)
+                        self.on_capped(s)
+                        break
         return list(self.running)
 
     # ------------------------------------------------------------ results

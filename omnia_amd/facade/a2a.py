@@ -278,7 +278,8 @@ def a2a_tool_handler(name: str, url: str, description: str = "",
         return {"agent": name, "state": st.get("state"),
                 "response": " ".join(p.get("text", "") for p in parts)}
 
-    schema = {"type": "object", "properties": {"message": {"type": "string",
+    # bounded so the local engine's tool-call grammar always closes the string
+    schema = {"type": "object", "properties": {"message": {"type": "string", "maxLength": 512,
                                                            "description": "what to ask"}},
               "required": ["message"]}
     return InProcessHandler(f"a2a-{name}", {f"ask_{name}": (

@@ -43,7 +43,14 @@ def auth_from_env(env) -> AuthChain:
         vs.append(OIDCValidator(env.get("OMNIA_OIDC_ISSUER"), env.get("OMNIA_OIDC_AUDIENCE"),
                                 jwks=jwks, hs_key=hs.encode() if hs else None))
     if env.get("OMNIA_EDGE_TRUST", "").lower() == "true":
-        vs.append(EdgeTrustValidator())
+        et = json.loads(env.get("OMNIA_EDGE_TRUST_CONFIG", "{}") or "{}")
+        hm = et.get("headerMapping") or {}
+        peers = env.get("OMNIA_EDGE_TRUST_PEERS", "127.0.0.1,::1")
+        vs.append(EdgeTrustValidator(hm.get("subject", ""), hm.get("endUser", ""),
+                                     hm.get("email", ""),
+                                     claims_from_headers=et.get("claimsFromHeaders") or {},
+                                     trusted_peers=[p for p in peers.split(",") if p]
+                                     if peers != "*" else None))
     anon = env.get("OMNIA_AUTH_ALLOW_ANONYMOUS", "true" if not vs else "false").lower() == "true"
     return AuthChain(vs, allow_anonymous=anon)
 

@@ -194,23 +194,51 @@ class OIDCValidator:
 
 
 class EdgeTrustValidator:
-    """Trust identity headers set by an authenticating edge proxy (edge_trust.go)."""
+    """Trust claim headers injected by an authenticating edge, e.g. Istio
+    RequestAuthentication with outputClaimToHeaders (``edge_trust.go``):
+    subject / end user default to ``x-user-id``, email ``x-user-email``, role
+    ``x-user-roles`` (default role viewer); ``claims_from_headers`` maps extra
+    inbound headers to claim names.  The reference relies on the pod's network
+    policy to keep the headers honest; here the peer must also be in
+    ``trusted_peers`` (the sidecar / edge on loopback by default)."""
 
-    def __init__(self, user_header: str = "X-Forwarded-User", trusted_peers=("127.0.0.1",),
-                 claims_prefix: str = "X-Forwarded-Claim-"):
-        self.user_header = user_header
-        self.trusted = set(trusted_peers)
-        self.claims_prefix = claims_prefix
+    def __init__(self, subject_header: str = "x-user-id", end_user_header: str = "x-user-id",
+                 email_header: str = "x-user-email", role_header: str = "x-user-roles",
+                 claims_from_headers: dict | None = None, default_role: str = "viewer",
+                 trusted_peers=("127.0.0.1", "::1")):
+        self.subject_header = subject_header or "x-user-id"
+        self.end_user_header = end_user_header or "x-user-id"
+        self.email_header = email_header or "x-user-email"
+        self.role_header = role_header
+        self.extra = {k.lower(): v for k, v in (claims_from_headers or {}).items() if k and v}
+        self.default_role = default_role
+        self.trusted = set(trusted_peers) if trusted_peers else None
+
+    @staticmethod
+    def _get(headers, name):
+        v = headers.get(name)
+        if v is None:
+            low = name.lower()
+            v = next((hv for hk, hv in headers.items() if hk.lower() == low), None)
+        return v or ""
 
     def validate(self, headers, query, peer):
-        u = headers.get(self.user_header)
-        if not u:
+        subject = self._get(headers, self.subject_header)
+        if not subject:
             return None
-        if peer not in self.trusted:
+        if self.trusted is not None and peer not in self.trusted:
             raise AuthError("untrusted edge")
-        claims = {k[len(self.claims_prefix):].lower(): v for k, v in headers.items()
-                  if k.startswith(self.claims_prefix)}
-        return Identity("edge", subject=u, end_user=u, claims=claims)
+        claims = {"role": self._get(headers, self.role_header) or self.default_role}
+        email = self._get(headers, self.email_header)
+        if email:
+            claims["email"] = email
+        for h, name in self.extra.items():
+            v = self._get(headers, h)
+            if v:
+                claims[name] = v
+        return Identity("edge", subject=subject,
+                        end_user=self._get(headers, self.end_user_header) or subject,
+                        claims=claims, role=claims["role"])
 
 
 class MgmtPlaneValidator:

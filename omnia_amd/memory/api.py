@@ -15,6 +15,7 @@ import argparse
 import asyncio
 import json
 import logging
+import os
 import time
 
 from aiohttp import web
@@ -579,6 +580,13 @@ def main(argv=None):
     ap.add_argument("--reembed-interval", type=float, default=5.0)
     ap.add_argument("--policy-file", default="",
                     help="MemoryPolicy spec (JSON; the operator's memory-policy-<name> ConfigMap)")
+    ap.add_argument("--compaction-interval", default=os.environ.get("COMPACTION_INTERVAL", ""),
+                    help="temporal-summarisation worker period (e.g. 6h); empty disables")
+    ap.add_argument("--compaction-age", default=os.environ.get("COMPACTION_AGE", ""),
+                    help="age threshold of compaction candidates (e.g. 720h)")
+    ap.add_argument("--access-touch-interval", type=float,
+                    default=float(os.environ.get("ACCESS_TOUCH_INTERVAL", "1.0")),
+                    help="seconds per batched access-count flush; 0 = one update per read")
     a = ap.parse_args(argv)
     from .embedding import build_embedder
     from .store import MemoryStore
@@ -600,16 +608,42 @@ def main(argv=None):
     if a.policy_file:
         with open(a.policy_file) as f:
             policy = json.load(f)
-    svc = MemoryService(MemoryStore(a.db), emb, publisher=pub, enterprise=a.enterprise)
+    store = MemoryStore(a.db)
+    if a.access_touch_interval > 0:
+        store.enable_touch_batching(a.access_touch_interval)
+    svc = MemoryService(store, emb, publisher=pub, enterprise=a.enterprise)
     app = build_app(svc, a.enterprise, a.ingest_chunk_size, a.ingest_chunk_overlap)
+    compaction = None
+    if a.compaction_interval:
+        from ..utils.durations import parse_duration
+        from .workers import CompactionWorker
+
+        try:
+            every = parse_duration(a.compaction_interval)
+        except ValueError:
+            every = 0
+        if every > 0:
+            kw = {}
+            if a.compaction_age:
+                try:
+                    kw["older_than_s"] = parse_duration(a.compaction_age)
+                except ValueError:
+                    log.error("invalid compaction age %r, using the default", a.compaction_age)
+            compaction = CompactionWorker(svc, interval=every, **kw)
+        else:
+            log.error("invalid compaction interval %r: worker disabled", a.compaction_interval)
 
     async def start_workers(app):
         app["workers"] = [asyncio.create_task(ReembedWorker(svc, a.reembed_interval).run()),
                           asyncio.create_task(RetentionWorker(svc, policy=policy).run())]
+        if compaction is not None:
+            app["workers"].append(asyncio.create_task(compaction.run()))
 
     async def stop_workers(app):
         for t in app.get("workers", []):
             t.cancel()
+        if store.touch_batcher is not None:
+            store.touch_batcher.stop()
 
     app.on_startup.append(start_workers)
     app.on_cleanup.append(stop_workers)

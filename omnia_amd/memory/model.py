@@ -95,6 +95,8 @@ class Memory:
             d["turn_range"] = list(self.turn_range)
         if self.accessed_at:
             d["accessed_at"] = _iso(self.accessed_at)
+        if self.access_count:
+            d["access_count"] = self.access_count
         if self.expires_at:
             d["expires_at"] = _iso(self.expires_at)
         if self.title:

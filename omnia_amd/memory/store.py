@@ -96,6 +96,61 @@ def _f32(blob):
     return None if blob is None else np.frombuffer(blob, dtype=np.float32)
 
 
+class AccessTouchBatcher:
+    """Window-coalesced access bumps (``access_tracker.go``): ``add`` counts ids
+    into the pending window; a daemon thread flushes every ``interval_s`` (or at
+    once when ``cap`` distinct ids are pending) with ONE batched update carrying
+    per-id increments; ``stop`` drains.  Flush failures are counted, never
+    raised into the read path."""
+
+    def __init__(self, execute, interval_s: float = 1.0, cap: int = 5000):
+        self.execute = execute
+        self.interval_s = interval_s
+        self.cap = cap
+        self.pending: dict[str, int] = {}
+        self.mu = threading.Lock()
+        self.wake = threading.Event()
+        self.stopped = threading.Event()
+        self.stats = {"flushes": 0, "rows": 0, "errors": 0}
+        self.thread = threading.Thread(target=self._run, name="memory-access-touch",
+                                       daemon=True)
+        self.thread.start()
+
+    def add(self, ids):
+        with self.mu:
+            for i in ids:
+                if i:
+                    self.pending[i] = self.pending.get(i, 0) + 1
+            overflow = len(self.pending) >= self.cap
+        if overflow:
+            self.wake.set()
+
+    def flush(self) -> int:
+        with self.mu:
+            if not self.pending:
+                return 0
+            batch, self.pending = self.pending, {}
+        try:
+            self.execute(list(batch), list(batch.values()))
+            self.stats["flushes"] += 1
+            self.stats["rows"] += len(batch)
+        except Exception:  # noqa: BLE001 - best effort, like the reference's
+            self.stats["errors"] += 1
+        return len(batch)
+
+    def _run(self):
+        while not self.stopped.is_set():
+            self.wake.wait(self.interval_s)
+            self.wake.clear()
+            self.flush()
+        self.flush()
+
+    def stop(self):
+        self.stopped.set()
+        self.wake.set()
+        self.thread.join(timeout=5)
+
+
 class MemoryStore:
     def __init__(self, path: str = ":memory:"):
         self.db = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
@@ -103,6 +158,7 @@ class MemoryStore:
         self.db.execute("PRAGMA synchronous=NORMAL")
         self.db.executescript(SCHEMA)
         self.lock = threading.RLock()
+        self.touch_batcher: AccessTouchBatcher | None = None
 
     # ------------------------------------------------------------ helpers
     def _tx(self):
@@ -210,12 +266,30 @@ class MemoryStore:
         return {r[0]: r[1] for r in rows}
 
     def touch(self, obs_ids: list[str]):
+        """Reads bump ``accessed_at`` / ``access_count``: through the access-touch
+        batcher when one is attached (``enable_touch_batching``), else at once."""
         if not obs_ids:
             return
+        if self.touch_batcher is not None:
+            self.touch_batcher.add(obs_ids)
+            return
+        self.apply_touches(list(dict.fromkeys(obs_ids)), None)
+
+    def apply_touches(self, obs_ids: list[str], counts: list[int] | None):
+        """One statement for a window of reads: each row gets its own increment."""
         now = time.time()
+        counts = counts or [1] * len(obs_ids)
         with self.lock:
             self.db.executemany("UPDATE memory_observations SET accessed_at = ?, access_count = "
-                                "access_count + 1 WHERE id = ?", [(now, i) for i in obs_ids])
+                                "access_count + ? WHERE id = ? AND superseded_by IS NULL",
+                                [(now, c, i) for i, c in zip(obs_ids, counts)])
+
+    def enable_touch_batching(self, interval_s: float = 1.0, cap: int = 5000):
+        """Coalesce read-path access bumps (``internal/memory/access_tracker.go``):
+        hot retrieval paths stop paying one UPDATE per read."""
+        if self.touch_batcher is None:
+            self.touch_batcher = AccessTouchBatcher(self.apply_touches, interval_s, cap)
+        return self.touch_batcher
 
     # ------------------------------------------------------------ writes
     def save(self, mem: Memory, require_user: bool = True) -> dict:
@@ -711,6 +785,12 @@ class MemoryStore:
         return mems
 
     # ------------------------------------------------------------ compaction / ingest
+    def list_workspace_ids(self) -> list[str]:
+        """Workspaces holding live (not forgotten) memories (``ListWorkspaceIDs``):
+        the compaction worker's discoverer."""
+        return [r[0] for r in self._q("SELECT DISTINCT workspace_id FROM memory_entities "
+                                      "WHERE forgotten = 0 ORDER BY workspace_id")]
+
     def compaction_candidates(self, workspace: str, older_than_s: float, min_count: int = 10,
                               limit: int = 20) -> list[dict]:
         """Per (user, agent) scope: the old active observations to summarise."""

@@ -80,16 +80,33 @@ def default_summarizer_prompt(texts: list[str]) -> str:
             "facts. Drop duplicates and superseded details.\n" + joined)
 
 
+async def noop_summarizer(texts: list[str]) -> str:
+    """Deterministic default summary (``compaction_worker.go`` NoopSummarizer):
+    the originals are still superseded, so the retrieval surface shrinks even
+    without an LLM summarizer."""
+    if not texts:
+        raise ValueError("noop summarizer called with no entries")
+    return f"Summary of {len(texts)} observations. First: {texts[0][:80]}"
+
+
 class CompactionWorker:
-    def __init__(self, svc, summarize, workspaces: list[str], older_than_s: float = 30 * 86400,
+    """Temporal summarisation of old memories.  ``workspaces`` is a fixed list or
+    a callable discovering them (the store's workspaces with live memories, as
+    ``ListWorkspaceIDs``)."""
+
+    def __init__(self, svc, summarize=None, workspaces=None, older_than_s: float = 30 * 86400,
                  min_count: int = 10, interval: float = 3600.0):
-        self.svc, self.summarize = svc, summarize
-        self.workspaces = workspaces
+        self.svc, self.summarize = svc, summarize or noop_summarizer
+        self.workspaces = workspaces if workspaces is not None else \
+            svc.store.list_workspace_ids
         self.older_than_s, self.min_count, self.interval = older_than_s, min_count, interval
+        self.passes = 0
 
     async def run_once(self) -> int:
         done = 0
-        for ws in self.workspaces:
+        self.passes += 1
+        wss = self.workspaces() if callable(self.workspaces) else self.workspaces
+        for ws in wss:
             for cand in self.svc.store.compaction_candidates(ws, self.older_than_s,
                                                              self.min_count):
                 texts = [e["content"] for e in cand["entries"]]

@@ -104,6 +104,7 @@ def runtime_config(ar: dict, pack: dict, providers: list[dict], registry: dict |
                     "block_size": eng.get("blockSize", 32), "dtype": eng.get("dtype",
                                                                              "bfloat16")}
         extra = {"swapGiB": "swap_gib", "mixedBudget": "mixed_budget", "epMode": "ep_mode",
+                 "ep": "ep",
                  "numBlocks": "num_blocks", "useGraphs": "use_graphs", "device": "device",
                  "cpThreshold": "cp_threshold", "tokenizer": "tokenizer"}
         for k, v in eng.items():  # the engine knobs beyond the core sizing fields
@@ -111,6 +112,13 @@ def runtime_config(ar: dict, pack: dict, providers: list[dict], registry: dict |
                 c.engine[extra[k]] = v
     mem = spec.get("memory") or {}
     c.memory_enabled = bool(mem.get("enabled"))
+    ret = mem.get("retrieval") or {}
+    if ret.get("strategy"):
+        c.memory_strategy = ret["strategy"]
+    if ret.get("limit"):
+        c.memory_limit = int(ret["limit"])
+    if (ret.get("accessFilter") or {}).get("denyCEL"):
+        c.memory_deny_cel = ret["accessFilter"]["denyCEL"]
     c.eval_enabled = bool((spec.get("evals") or {}).get("enabled"))
     return c
 
@@ -146,8 +154,10 @@ def facade_env(ar: dict) -> dict:
         if oidc.get("audience"):
             env["OMNIA_OIDC_AUDIENCE"] = oidc["audience"]
         env["OMNIA_OIDC_JWKS_FILE"] = "/etc/omnia/oidc/jwks.json"
-    if (ea.get("edgeTrust") or {}).get("enabled"):
+    if ea.get("edgeTrust") is not None:  # presence enables it (external_auth_types.go:59)
         env["OMNIA_EDGE_TRUST"] = "true"
+        if ea["edgeTrust"]:
+            env["OMNIA_EDGE_TRUST_CONFIG"] = json.dumps(ea["edgeTrust"], sort_keys=True)
     # blip-resume route hints share the Redis of a Redis context store
     # (internal/controller/deployment_builder_env.go:147-162)
     ctx = spec.get("context") or {}
@@ -189,10 +199,12 @@ def deployment(ar: dict, rc: RuntimeConfig, pack_cm: str, track: str = "stable",
     for n, p in MGMT_PORTS.items():
         ports.append({"name": n, "containerPort": p})
     resources = dict(rt.get("resources") or {})
-    if rc.provider.get("type") == "local":
-        tp = int(rc.engine.get("tp", 1))
-        resources.setdefault("limits", {})["amd.com/gpu"] = str(tp)
-        resources.setdefault("requests", {})["amd.com/gpu"] = str(tp)
+    if rc.provider.get("type") == "local" and rc.engine.get("device", "cuda") != "cpu":
+        n = int(rc.engine.get("tp", 1))
+        if rc.engine.get("ep_mode") == "a2a":  # one GPU per EP rank
+            n = max(n, int(rc.engine.get("ep", 1) or 1))
+        resources.setdefault("limits", {})["amd.com/gpu"] = str(n)
+        resources.setdefault("requests", {})["amd.com/gpu"] = str(n)
     fw = spec.get("framework") or {}
     containers = [
         {"name": "facade", "image": FACADE_IMAGE, "ports": ports, "env": _env_list(fenv),

@@ -454,12 +454,14 @@ class AgentRuntimeReconciler:
         cap_ok = True
         if rc.provider.get("type") == "local" and self.gpu_count is not None:
             need = int(rc.engine.get("tp", 1))
-            if need > self.gpu_count:
+            if rc.engine.get("ep_mode") == "a2a":  # one rank per GPU of the EP group
+                need = max(need, int(rc.engine.get("ep", 1) or 1))
+            if need > self.gpu_count and rc.engine.get("device", "cuda") != "cpu":
                 cap_ok = False
                 replicas = 0
         set_condition(st, "CapabilitiesSatisfied", cap_ok,
                       "CapabilitiesSatisfied" if cap_ok else "CapabilitiesMissing",
-                      "" if cap_ok else "insufficient GPUs for engine.tp", gen)
+                      "" if cap_ok else "insufficient GPUs for the engine's TP/EP group", gen)
         # ---- workspace service group: session-api / memory-api endpoints
         facade_extra = {}
         sg = workspace_service_group(store, ns, spec.get("serviceGroup") or "default")
@@ -676,6 +678,9 @@ class WorkspaceReconciler:
                                                    "spec": {"containers": [{
                                                        "name": svc, "image": f"omnia-{svc}",
                                                        "command": cmd[:3], "args": args,
+                                                       "env": list((cfg.get("podOverrides")
+                                                                    or {}).get("extraEnv")
+                                                                   or []),
                                                        "ports": [{"name": "http",
                                                                   "containerPort": 8080}],
                                                        "volumeMounts": mounts,

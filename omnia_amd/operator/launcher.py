@@ -67,23 +67,36 @@ class Pod:
 
 
 class DeviceAllocator:
-    """GPUs of this node handed to pods (first-fit contiguous ranges, so a TP
-    group sits on neighbouring xGMI peers)."""
+    """GPUs of this node handed to pods (first-fit contiguous ranges, so a TP /
+    EP group sits on neighbouring xGMI peers).  ``share`` pods may hold one GPU
+    (``OMNIA_PODS_PER_GPU``: a 288 GB MI355X fits e.g. a Mixtral EP shard and an
+    8B planner); empty ranges are preferred, so sharing only starts once every
+    GPU is taken."""
 
-    def __init__(self, count: int):
+    def __init__(self, count: int, share: int = 1):
         self.count = count
-        self.owner: list = [None] * count
+        self.share = max(1, share)
+        self.owner: list[list] = [[] for _ in range(count)]
 
     def take(self, who, n: int) -> list[int] | None:
-        for start in range(0, self.count - n + 1):
-            if all(o is None for o in self.owner[start:start + n]):
-                for i in range(start, start + n):
-                    self.owner[i] = who
-                return list(range(start, start + n))
+        for cap in range(1, self.share + 1):  # least-loaded ranges first
+            for start in range(0, self.count - n + 1):
+                if all(len(o) < cap for o in self.owner[start:start + n]):
+                    for i in range(start, start + n):
+                        self.owner[i].append(who)
+                    return list(range(start, start + n))
         return None
 
     def release(self, who):
-        self.owner = [None if o == who else o for o in self.owner]
+        self.owner = [[w for w in o if w != who] for o in self.owner]
+
+    def load(self, devices) -> int:
+        """Pods on the busiest GPU of ``devices`` (sizes the engine's KV slice)."""
+        return max((len(self.owner[d]) for d in devices or []), default=1)
+
+
+class _WaitingForServices(Exception):
+    pass
 
 
 class _ProcReplica:
@@ -113,13 +126,15 @@ class LocalLauncher:
         self.engine_factory = engine_factory  # fn(engine_cfg) -> AsyncLLMEngine
         self.use_grpc = use_grpc
         self.mode = mode
-        self.devices = DeviceAllocator(gpu_count)
+        self.devices = DeviceAllocator(gpu_count,
+                                       int(os.environ.get("OMNIA_PODS_PER_GPU", "1") or 1))
         self.task = None
         from .keda import KedaScaler
 
         self.scaler = KedaScaler(store, self._keda_samples)
         self.activators: dict[tuple, object] = {}  # (ns, name) -> Activator
         self.cold_start_s: dict[tuple, float] = {}
+        self._dep_wait: dict[tuple, float] = {}  # key -> first deferral (dependencies)
 
     async def _keda_samples(self, ns: str, name: str) -> list:
         """Metric samples of one scale target: every ready replica's facade
@@ -376,26 +391,59 @@ class LocalLauncher:
         svc = self.store.try_get("Service", name, ns)
         return ((svc or {}).get("status") or {}).get("endpoint")
 
+    def _pending_services(self, key, dep: dict) -> list[str]:
+        """In-cluster Services the pod's env points at that exist but have no
+        endpoint yet (e.g. an A2A peer still cold-starting).  Cluster DNS would
+        resolve them later; a process pod's URLs are rewritten once at start, so
+        the start waits for them -- up to ``OMNIA_POD_DEPENDENCY_WAIT_S`` (600 s),
+        after which it starts anyway (mutual references cannot deadlock)."""
+        from .pods import service_refs
+
+        env = {}
+        for c in dep["spec"]["template"]["spec"]["containers"]:
+            env.update(_env(c))
+        pending = [f"{ns}/{svc}" for svc, ns in sorted(service_refs(env))
+                   if (s := self.store.try_get("Service", svc, ns)) is not None
+                   and not (s.get("status") or {}).get("endpoint")
+                   and (svc, ns) != (key[1], key[0])]
+        if not pending:
+            self._dep_wait.pop(key, None)
+            return []
+        import time
+
+        t0 = self._dep_wait.setdefault(key, time.monotonic())
+        if time.monotonic() - t0 > float(os.environ.get("OMNIA_POD_DEPENDENCY_WAIT_S", "600")):
+            return []
+        return pending
+
     def _start_replica(self, dep: dict, key, index: int, thash) -> _ProcReplica:
         from .pods import ProcessPod
 
+        pending = self._pending_services(key, dep)
+        if pending:
+            raise _WaitingForServices(", ".join(pending))
         workdir = tempfile.mkdtemp(prefix=f"omnia-{key[1]}-{index}-")
         renv, fenv = self._pod_envs(dep, workdir)
         rc_provider = (json.loads(renv.get("OMNIA_PROVIDER_JSON", "{}") or "{}").get("type")
                        or renv.get("OMNIA_PROVIDER_TYPE", "mock"))
         devices = None
         who = (key, index)
+        tp = int(renv.get("OMNIA_ENGINE_TP", "1") or 1)
+        world = tp  # engine ranks of one pod: TP group, or the EP (a2a) group
+        if renv.get("OMNIA_ENGINE_EP_MODE") == "a2a":
+            world = max(tp, int(renv.get("OMNIA_ENGINE_EP", "1") or 1))
         if rc_provider in ("local", "engine", "omnia", "rocm") and self.devices.count:
-            tp = int(renv.get("OMNIA_ENGINE_TP", "1") or 1)
-            devices = self.devices.take(who, tp)
+            devices = self.devices.take(who, world)
             if devices is None:
-                raise RuntimeError(f"no {tp} free GPU(s) for {key[0]}/{key[1]} replica {index}")
+                raise RuntimeError(f"no {world} free GPU(s) for {key[0]}/{key[1]} replica "
+                                   f"{index}")
+        if devices is not None and self.devices.share > 1:
+            renv["OMNIA_GPU_SHARE"] = str(self.devices.share)  # KV slice per pod
         for k in ("OMNIA_GRPC_PORT", "OMNIA_HEALTH_PORT"):
             renv.pop(k, None)
         fenv.pop("OMNIA_FACADE_PORT", None)
         pod = ProcessPod(f"{key[1]}-{index}", renv, fenv, device_index=devices,
-                         log_dir=os.path.join(workdir, "logs"),
-                         tp=int(renv.get("OMNIA_ENGINE_TP", "1") or 1))
+                         log_dir=os.path.join(workdir, "logs"), tp=world)
         import time
 
         t0 = time.perf_counter()
@@ -436,6 +484,10 @@ class LocalLauncher:
                 continue
             try:
                 r = await loop.run_in_executor(None, self._start_replica, d, key, i, thash)
+            except _WaitingForServices as e:
+                log.info("pod %s/%s replica %d waits for service endpoints: %s", key[0],
+                         key[1], i, e)
+                break
             except Exception:  # noqa: BLE001
                 log.exception("pod %s/%s replica %d failed to start", key[0], key[1], i)
                 continue

@@ -113,10 +113,12 @@ class ProcessPod:
                "OMNIA_HEALTH_PORT": self.health_port}
         launcher = None
         if self.tp > 1:
-            # one runtime process per GPU of the pod; TP rank 0 serves gRPC
+            # one runtime process per GPU of the pod; rank 0 serves gRPC
             # (``omnia_amd/runtime/__main__.py``); torchrun's agent itself never
-            # touches a GPU, it only starts the ranks
-            env["OMNIA_ENGINE_TP"] = self.tp
+            # touches a GPU, it only starts the ranks.  ``tp`` is the pod's engine
+            # world: the TP group, or the EP group under ep_mode a2a
+            if env.get("OMNIA_ENGINE_EP_MODE") != "a2a":
+                env["OMNIA_ENGINE_TP"] = self.tp
             launcher = ["-m", "torch.distributed.run", "--nnodes=1",
                         f"--nproc-per-node={self.tp}", "--master-addr=127.0.0.1",
                         f"--master-port={free_port()}"]
@@ -286,6 +288,16 @@ class ServiceProcess:
 
 
 _SVC_URL = None
+
+
+def service_refs(env: dict) -> set[tuple[str, str]]:
+    """(service, namespace) of every in-cluster URL in ``env``'s values."""
+    resolve_service_urls({}, lambda *_: None)  # compiles the pattern
+    out = set()
+    for v in env.values():
+        if isinstance(v, str):
+            out.update((m.group(2), m.group(3)) for m in _SVC_URL.finditer(v))
+    return out
 
 
 def resolve_service_urls(env: dict, lookup) -> dict:

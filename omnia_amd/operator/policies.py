@@ -45,6 +45,7 @@ import re
 import yaml
 
 from ..api import crds
+from ..utils.durations import parse_duration as _parse_duration
 from .apistore import APIStore, Conflict, NotFound, owner_ref, set_condition
 
 ISTIO_API = "security.istio.io/v1"
@@ -61,25 +62,13 @@ class PolicyInvalid(ValueError):
 
 
 # ------------------------------------------------------------------ parsing helpers
-_GO_DUR = re.compile(r"(\d+(?:\.\d+)?)(ns|us|µs|ms|s|m|h|d)")
-_UNIT = {"ns": 1e-9, "us": 1e-6, "µs": 1e-6, "ms": 1e-3, "s": 1.0, "m": 60.0, "h": 3600.0,
-         "d": 86400.0}
-
-
 def parse_duration(s: str) -> float:
     """Go ``time.ParseDuration`` plus ``d`` days (``parseExtendedDuration``):
     "720h", "30d", "1d12h", "90m".  Returns seconds."""
-    if not s:
-        raise PolicyInvalid("empty duration")
-    pos, total = 0, 0.0
-    for m in _GO_DUR.finditer(s):
-        if m.start() != pos:
-            break
-        total += float(m.group(1)) * _UNIT[m.group(2)]
-        pos = m.end()
-    if pos != len(s) or pos == 0:
-        raise PolicyInvalid(f"invalid duration {s!r}")
-    return total
+    try:
+        return _parse_duration(s)
+    except ValueError as e:
+        raise PolicyInvalid(str(e)) from None
 
 
 _CRON_FIELD = r"(\*|\d+(,\d+)*|\d+[-/]\d+|\*/\d+)"

@@ -487,9 +487,20 @@ class Agent:
 
         async def run(c):
             span = tracing.start_span("omnia.tool.call", {"tool.name": c.name})
+            sid = getattr(ctx, "session_id", "") or ""
+            # session-api tool_calls rows (runtime/event_store.go:498-568): a pending
+            # row when the call starts, a success / error row linked by call id
+            await self._emit(sid, "tool_call", {"call_id": c.id, "name": c.name,
+                                                "arguments": c.arguments or {},
+                                                "status": "pending"})
+            t0 = time.perf_counter()
             r, err = await self.executor.execute(c.name, c.arguments, ctx)
             tracing.end_span(span, {"tool.error": err})
             out[c.id] = {"result_json": r, "is_error": err}
+            await self._emit(sid, "tool_call", {
+                "call_id": c.id, "name": c.name, "status": "error" if err else "success",
+                "duration_ms": int((time.perf_counter() - t0) * 1000),
+                "result": r if not err else None, "error": r if err else ""})
 
         if server:
             await asyncio.gather(*(run(c) for c in server))

@@ -79,6 +79,8 @@ def _use_engine_process(cfg) -> bool:
     mode = os.environ.get("OMNIA_ENGINE_PROC", "auto").lower()
     if mode in ("0", "false", "no"):
         return False
+    if getattr(cfg, "ep_mode", "tp") == "a2a" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return False  # this process IS rank 0 of the EP group (torchrun env)
     if mode in ("1", "true", "yes"):
         return True
     return (cfg.device == "cuda" and cfg.tp == 1 and torch.cuda.device_count() > 0

@@ -136,6 +136,17 @@ class SessionEventSink:
                 "outputTokens": payload.get("output_tokens", 0),
                 "cachedTokens": payload.get("cached_tokens", 0),
                 "costUsd": payload.get("cost_usd", 0.0)})
+        elif kind == "tool_call":
+            body = {"callId": payload.get("call_id", ""), "name": payload.get("name", ""),
+                    "status": payload.get("status", "success"),
+                    "durationMs": payload.get("duration_ms", 0)}
+            if payload.get("arguments") is not None:
+                body["arguments"] = payload["arguments"]
+            if payload.get("result") is not None:
+                body["result"] = payload["result"]
+            if payload.get("error"):
+                body["errorMessage"] = payload["error"]
+            await self.client.write("POST", f"/api/v1/sessions/{session_id}/tool-calls", body)
         elif kind == "eval_result":
             await self.client.write("POST", "/api/v1/eval-results", {
                 "sessionId": session_id, "evalId": payload.get("id"),

@@ -105,6 +105,7 @@ class ToolCall(_JSON):
     result: object = None
     status: str = "success"  # success | error | pending
     duration_ms: int = 0
+    error_message: str = ""
     execution: str = "server"
     created_at: float = field(default_factory=time.time)
 

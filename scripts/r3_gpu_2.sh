@@ -10,6 +10,9 @@ timeout -k 10 600 python -u -m pytest tests/test_tp_gpu.py -v -s --timeout 420 -
 trc=$?; echo "tp gpu rc=$trc"; grep -E "^TP=|passed|failed" $O/tp_gpu.log | tail -5
 [ $trc -eq 0 ] || grep -A12 "Error" $O/tp_gpu.log | head -40
 [ $trc -eq 0 ] || [ $trc -eq 1 ] || exit $trc
+timeout -k 10 400 python -u -m pytest tests/test_config5.py -m gpu -v -s --timeout 360 --timeout-method thread > $O/cfg5_gpu.log 2>&1
+crc=$?; echo "cfg5 gpu rc=$crc"; tail -3 $O/cfg5_gpu.log
+[ $crc -eq 0 ] || [ $crc -eq 1 ] || exit $crc
 for cfg in "gate_up 256 128 1 0" "qkv 256 128 4 0" "down 256 128 8 0"; do
   tag=$(echo $cfg | tr ' ' '_')
   timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d /tmp/pmc_$tag -o a -- python3 scripts/tgemm_pmc.py $cfg > $O/pmc_a_$tag.log 2>&1

@@ -1,0 +1,153 @@
+"""BASELINE config 5 end to end under ``omnia serve``'s process launcher, from the
+shipped manifests (``examples/mixtral-a2a/manifests.yaml``): a Workspace with a
+managed memory-api (compaction + batched access tracking) and session-api, a
+Mixtral researcher whose engine is an expert-parallel group (``epMode: a2a``,
+one process per EP rank), and a planner that reads the user's memories and
+delegates through the A2A client the operator resolved and exposed as the tool
+``ask_researcher``.
+
+CPU variant: the two Provider engines are swapped for tiny random-init models
+(tiny-mixtral EP=2 over gloo, tiny-llama).  Random weights cannot decide to call
+a tool, so the planner pack's ``tool_choice: required`` is enforced by the
+engine's tool-call grammar; what is checked is the plumbing: the tool call
+reaches the researcher's EP engine over A2A and comes back completed, the
+planner's retrieval read the seeded memory (access count), and session-api holds
+the tool-call rows.  GPU variant: tiny shapes swapped for Mixtral-8x7B EP=1
+(one rank) is covered by tests/test_ep_gpu.py's engine path; this file's GPU
+test runs the same manifests with the researcher on cuda:0."""
+import asyncio
+import json
+import os
+import time
+
+import aiohttp
+import pytest
+import yaml
+
+from omnia_amd.api import crds
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+MANIFESTS = os.path.join(HERE, "..", "examples", "mixtral-a2a", "manifests.yaml")
+NS = "research"
+
+
+def _docs(engine_patch: dict, max_tokens: int):
+    with open(MANIFESTS) as f:
+        docs = [d for d in yaml.safe_load_all(f) if d]
+    for d in docs:
+        d.setdefault("apiVersion", crds.API_VERSION)
+        if d["kind"] == "Provider":
+            d["spec"]["engine"].update(engine_patch[d["metadata"]["name"]])
+            d["spec"]["model"] = d["spec"]["engine"]["model"]
+        if d["kind"] == "ConfigMap" and d["metadata"]["name"] == "planner-pack":
+            pack = json.loads(d["data"]["pack.json"])
+            pack["prompts"]["default"]["parameters"]["max_tokens"] = max_tokens
+            d["data"]["pack.json"] = json.dumps(pack)
+    return docs
+
+
+def _run(engine_patch: dict, max_tokens: int = 1024, gpu_count: int = 0):
+    from omnia_amd.ee.arena.fleet import FleetSession
+    from omnia_amd.operator.launcher import LocalLauncher
+    from omnia_amd.operator.manager import Manager, new_store
+
+    docs = _docs(engine_patch, max_tokens)
+
+    def ep(store, name):
+        svc = store.try_get("Service", name, NS)
+        return ((svc or {}).get("status") or {}).get("endpoint")
+
+    async def go():
+        store = new_store()
+        mgr = Manager(store)
+        await mgr.start()
+        launcher = LocalLauncher(store, mode="process", gpu_count=gpu_count)
+        launcher.start()
+        try:
+            for d in docs:
+                store.apply(d)
+            mem_ep = planner_ep = None
+            for _ in range(3000):
+                mem_ep = ep(store, "memory-api-research-default")
+                planner_ep = ep(store, "planner")
+                res_dep = store.try_get("Deployment", "researcher", NS)
+                if mem_ep and planner_ep and ((res_dep or {}).get("status") or {}).get(
+                        "readyReplicas"):
+                    break
+                await asyncio.sleep(0.1)
+            assert mem_ep and planner_ep, "workspace services / planner never came up"
+            ar = store.get("AgentRuntime", "planner", NS)
+            clients = ar["status"]["a2a"]["clients"]
+            async with aiohttp.ClientSession() as http:
+                r = await http.post(f"http://{mem_ep}/api/v1/memories", json={
+                    "scope": {"workspace_id": "research", "virtual_user_id": "alice"},
+                    "content": "The user's project is codenamed Bluebird and ships in May",
+                    "type": "fact", "confidence": 0.9})
+                assert r.status == 201, await r.text()
+                mid = (await r.json())["memory"]["id"]
+                async with FleetSession(f"ws://{planner_ep}/ws", headers={"x-user-id": "alice"},
+                                        timeout_s=600) as fs:
+                    turn = await fs.turn("What should I do next on my project?")
+                    sid = fs.session_id
+                await asyncio.sleep(1.5)  # one access-touch window
+                r = await http.get(f"http://{mem_ep}/api/v1/memories",
+                                   params={"workspace": "research", "virtual_user_id": "alice"})
+                mems = (await r.json())["memories"]
+                sess_ep = ep(store, "session-api-research-default")
+                calls = []
+                for _ in range(50):
+                    r = await http.get(f"http://{sess_ep}/api/v1/sessions/{sid}/tool-calls")
+                    calls = (await r.json()).get("tool-calls", []) if r.status == 200 else []
+                    if any(c.get("status") == "success" for c in calls):
+                        break
+                    await asyncio.sleep(0.1)
+            res_logs = launcher.replicas[(NS, "researcher")][0].pod
+            return turn, clients, mems, mid, calls, res_logs
+        finally:
+            await launcher.stop()
+            await mgr.stop()
+
+    return asyncio.run(go())
+
+
+def _check(turn, clients, mems, mid, calls):
+    assert clients and clients[0]["ready"] and clients[0]["resolvedURL"].endswith("/a2a")
+    assert (turn["usage"] or {}).get("output_tokens", 0) > 0, turn
+    seeded = next(m for m in mems if m["id"] == mid)
+    assert seeded.get("access_count", 0) >= 1, seeded  # the planner's retrieval read it
+    done = [c for c in calls if c.get("status") == "success"]
+    assert [c["name"] for c in done] == ["ask_researcher"], calls
+    res = done[0]["result"]
+    res = json.loads(res) if isinstance(res, str) else res
+    assert res["agent"] == "researcher" and res["state"] == "completed", res
+    assert res["response"], res  # the EP engine's answer came back over A2A
+    pend = [c for c in calls if c.get("status") == "pending"]
+    assert pend and pend[0]["callId"] == done[0]["callId"]
+    assert len(pend[0]["arguments"]["message"]) <= 512
+
+
+def test_config5_manifests_cpu_ep2():
+    t0 = time.monotonic()
+    turn, clients, mems, mid, calls, _ = _run({
+        "mixtral": {"model": "tiny-mixtral", "ep": 2, "device": "cpu", "dtype": "float32",
+                    "numBlocks": 64, "blockSize": 16, "maxModelLen": 2048, "maxBatch": 4,
+                    "useGraphs": False},
+        "planner-llm": {"model": "tiny-llama", "device": "cpu", "dtype": "float32",
+                        "numBlocks": 320, "blockSize": 16, "maxModelLen": 4096, "maxBatch": 4,
+                        "useGraphs": False}})
+    _check(turn, clients, mems, mid, calls)
+    print(f"config 5 turn: {turn['latency_ms']:.0f} ms, whole test {time.monotonic() - t0:.0f}s")
+
+
+@pytest.mark.gpu
+def test_config5_manifests_gpu():
+    """The same manifests on one MI355X: researcher Mixtral shape (2 layers, EP=1
+    on cuda:0 -- the EP=8 group is the driver's 8-GPU node), planner tiny-llama on
+    the CPU so the single box holds both pods."""
+    turn, clients, mems, mid, calls, _ = _run({
+        "mixtral": {"model": "tiny-mixtral", "ep": 1, "device": "cuda", "dtype": "bfloat16",
+                    "numBlocks": 256, "maxModelLen": 4096, "maxBatch": 8},
+        "planner-llm": {"model": "tiny-llama", "device": "cpu", "dtype": "float32",
+                        "numBlocks": 320, "blockSize": 16, "maxModelLen": 4096, "maxBatch": 4,
+                        "useGraphs": False}}, gpu_count=1)
+    _check(turn, clients, mems, mid, calls)

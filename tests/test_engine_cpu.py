@@ -71,6 +71,20 @@ def test_preemption_recovers():
     assert seqs[0].output == ref_out
 
 
+def test_single_sequence_capped_at_pool_capacity():
+    # one sequence alone outgrows the pool (max_model_len > pool): it finishes
+    # "length" at capacity instead of faulting the engine; the next request runs
+    from omnia_amd.engine.sequence import FinishReason
+
+    e = make_engine(num_blocks=8, block_size=16, max_model_len=1024)
+    p = SamplingParams(temperature=0, max_tokens=500, ignore_eos=True)
+    s = e.generate([list(range(5, 45))], p)[0]
+    assert s.finish_reason == FinishReason.LENGTH and 0 < len(s.output) < 500
+    assert s.length <= 8 * 16
+    s2 = e.generate([list(range(5, 25))], SamplingParams(temperature=0, max_tokens=4))[0]
+    assert len(s2.output) == 4
+
+
 def test_stop_conditions():
     e = make_engine()
     s = e.generate(["x"], SamplingParams(temperature=0, max_tokens=3))[0]

@@ -363,3 +363,36 @@ def test_connection_cap_origin_check_and_burst_connects():
     # aiohttp's default backlog (128) drops the SYNs of such a burst and the 1 s
     # retransmit delays half the sessions; the facade sizes it for bursts
     assert out["burst_n"] == 300 and out["backlog"] >= 1024, out
+
+
+def test_edge_trust_headers_defaults_mapping_and_peer():
+    """edge_trust.go: x-user-id / x-user-email / x-user-roles by default, header
+    mapping + claimsFromHeaders from the CRD, default role viewer; the operator's
+    env (builders.facade_env) carries the CRD block."""
+    from omnia_amd.facade.app import auth_from_env
+    from omnia_amd.facade.auth import EdgeTrustValidator
+    from omnia_amd.operator.builders import facade_env
+
+    v = EdgeTrustValidator()
+    assert v.validate({"Authorization": "x"}, {}, "127.0.0.1") is None  # not mine
+    ident = v.validate({"X-User-Id": "alice", "x-user-email": "a@x.io"}, {}, "127.0.0.1")
+    assert (ident.origin, ident.subject, ident.end_user) == ("edge", "alice", "alice")
+    assert ident.claims == {"role": "viewer", "email": "a@x.io"}
+    assert ident.to_metadata()["x-omnia-user-id"] == "alice"
+    with pytest.raises(AuthError):
+        v.validate({"x-user-id": "mallory"}, {}, "10.0.0.9")
+    ar = {"metadata": {"name": "a", "namespace": "n"},
+          "spec": {"facades": [{"type": "websocket"}], "externalAuth": {"edgeTrust": {
+              "headerMapping": {"subject": "x-sub", "endUser": "x-end"},
+              "claimsFromHeaders": {"x-user-groups": "groups"}}}}}
+    env = facade_env(ar)
+    assert env["OMNIA_EDGE_TRUST"] == "true"
+    chain = auth_from_env(env)
+    ident = chain.validators[-1].validate({"x-sub": "svc", "x-end": "bob",
+                                           "x-user-groups": "ops", "x-user-roles": "editor"},
+                                          {}, "127.0.0.1")
+    assert (ident.subject, ident.end_user) == ("svc", "bob")
+    assert ident.claims["groups"] == "ops" and ident.role == "editor"
+    assert facade_env({"metadata": {"name": "a", "namespace": "n"},
+                       "spec": {"facades": [{"type": "websocket"}],
+                                "externalAuth": {"edgeTrust": {}}}})["OMNIA_EDGE_TRUST"] == "true"

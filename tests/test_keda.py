@@ -6,6 +6,7 @@ activator that parks connections while a replica cold-starts, and the whole
 loop under ``omnia serve``'s process launcher: connect -> scale from zero -> the
 turn streams from a TP=2 engine -> idle -> scale to zero."""
 import asyncio
+import os
 import time
 
 import aiohttp
@@ -157,95 +158,78 @@ def test_activator_parks_until_a_backend_is_ready_then_relays():
     assert parked == 1 and msg == "echo:hi" and body == {"q": "1"} and late == 503
 
 
-MANIFESTS = """
-apiVersion: omnia.altairalabs.ai/v1alpha1
-kind: Provider
-metadata: {name: tiny, namespace: default}
-spec:
-  type: local
-  model: tiny-llama
-  engine: {model: tiny-llama, tp: 2, maxBatch: 4, maxModelLen: 512, numBlocks: 64,
-           blockSize: 16, dtype: float32, useGraphs: false}
----
-apiVersion: v1
-kind: ConfigMap
-metadata: {name: pack, namespace: default}
-data:
-  pack.json: |
-    {"id": "p", "name": "P", "version": "1.0.0",
-     "template_engine": {"version": "v1", "syntax": "{{variable}}"},
-     "prompts": {"default": {"id": "default", "name": "D", "version": "1.0.0",
-       "system_template": "You are terse.",
-       "parameters": {"temperature": 0, "max_tokens": 6, "ignore_eos": true}}}}
----
-apiVersion: omnia.altairalabs.ai/v1alpha1
-kind: PromptPack
-metadata: {name: pack, namespace: default}
-spec: {packName: p, version: "1.0.0", source: {type: configmap, configMapRef: {name: pack}}}
----
-apiVersion: omnia.altairalabs.ai/v1alpha1
-kind: AgentRuntime
-metadata: {name: z, namespace: default}
-spec:
-  promptPackRef: {name: pack}
-  facades: [{type: websocket}]
-  providers: [{name: llm, providerRef: {name: tiny}}]
-  runtime:
-    replicas: 0
-    autoscaling:
-      enabled: true
-      type: keda
-      minReplicas: 0
-      maxReplicas: 1
-      keda: {pollingInterval: 1, cooldownPeriod: 3}
-"""
+EXAMPLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "examples",
+                       "llama3-70b-tp8", "manifests.yaml")
+AGENT = "assistant-70b"
 
 
-def test_serve_scales_from_zero_and_back_to_zero_tp2_cpu():
+def _example_docs(engine: dict, max_tokens: int = 6, poll: int = 1, cool: int = 3):
+    """The shipped config-4 manifests with the engine swapped for a test-sized
+    one and the KEDA periods shortened."""
+    import json
+
     import yaml
 
+    with open(EXAMPLE) as f:
+        docs = [d for d in yaml.safe_load_all(f) if d]
+    for d in docs:
+        d.setdefault("apiVersion", crds.API_VERSION)
+        if d["kind"] == "Provider":
+            d["spec"]["engine"] = dict(engine)
+            d["spec"]["model"] = engine["model"]
+        elif d["kind"] == "ConfigMap":
+            pack = json.loads(d["data"]["pack.json"])
+            pack["prompts"]["default"]["parameters"] = {"temperature": 0,
+                                                        "max_tokens": max_tokens,
+                                                        "ignore_eos": True}
+            d["data"]["pack.json"] = json.dumps(pack)
+        elif d["kind"] == "AgentRuntime":
+            d["spec"]["runtime"]["autoscaling"]["keda"].update(pollingInterval=poll,
+                                                               cooldownPeriod=cool)
+    return docs
+
+
+def _scale_cycle(engine: dict, gpu_count: int = 0):
     from omnia_amd.ee.arena.fleet import FleetSession
     from omnia_amd.operator.launcher import LocalLauncher
     from omnia_amd.operator.manager import Manager, new_store
 
-    docs = [d for d in yaml.safe_load_all(MANIFESTS) if d]
-    for d in docs:
-        d.setdefault("apiVersion", crds.API_VERSION)
+    docs = _example_docs(engine)
 
     async def go():
         store = new_store()
         mgr = Manager(store)
         await mgr.start()
-        launcher = LocalLauncher(store, mode="process")
+        launcher = LocalLauncher(store, mode="process", gpu_count=gpu_count)
         launcher.start()
         try:
             for d in docs:
                 store.apply(d)
             ep = None
             for _ in range(300):
-                svc = store.try_get("Service", "z")
+                svc = store.try_get("Service", AGENT)
                 ep = ((svc or {}).get("status") or {}).get("endpoint")
-                if ep and store.try_get("ScaledObject", "z") is not None:
+                if ep and store.try_get("ScaledObject", AGENT) is not None:
                     break
                 await asyncio.sleep(0.1)
             assert ep, "activator endpoint never published"
-            assert not launcher.replicas.get(("default", "z"))  # at zero: no pod
+            assert not launcher.replicas.get(("default", AGENT))  # at zero: no pod
             t0 = time.monotonic()
-            async with FleetSession(f"ws://{ep}/ws", timeout_s=300) as fs:
+            async with FleetSession(f"ws://{ep}/ws", timeout_s=600) as fs:
                 r = await fs.turn("hello there")
             first_turn_s = time.monotonic() - t0
-            dep = store.get("Deployment", "z")
+            dep = store.get("Deployment", AGENT)
             cold = dep["status"].get("coldStartSeconds")
             up = dep["spec"]["replicas"]
             # idle: cooldown 3 s, poll 1 s -> back to zero, pod stopped
             for _ in range(300):
-                if store.get("Deployment", "z")["spec"]["replicas"] == 0 and \
-                        not launcher.replicas.get(("default", "z")):
+                if store.get("Deployment", AGENT)["spec"]["replicas"] == 0 and \
+                        not launcher.replicas.get(("default", AGENT)):
                     break
                 await asyncio.sleep(0.1)
-            down = store.get("Deployment", "z")["spec"]["replicas"]
-            so = store.get("ScaledObject", "z")
-            return r, up, down, cold, first_turn_s, so, launcher.replicas.get(("default", "z"))
+            down = store.get("Deployment", AGENT)["spec"]["replicas"]
+            so = store.get("ScaledObject", AGENT)
+            return r, up, down, cold, first_turn_s, so, launcher.replicas.get(("default", AGENT))
         finally:
             await launcher.stop()
             await mgr.stop()
@@ -256,3 +240,22 @@ def test_serve_scales_from_zero_and_back_to_zero_tp2_cpu():
     assert cold and 0 < cold < first_s
     assert get_condition(so, "Ready")["status"] == "True"
     print(f"scale-from-zero: pod cold start {cold:.1f}s, first turn {first_s:.1f}s")
+    return cold, first_s
+
+
+def test_serve_scales_from_zero_and_back_to_zero_tp2_cpu():
+    _scale_cycle({"model": "tiny-llama", "tp": 2, "maxBatch": 4, "maxModelLen": 512,
+                  "numBlocks": 64, "blockSize": 16, "dtype": "float32", "useGraphs": False,
+                  "device": "cpu"})
+
+
+@pytest.mark.gpu
+def test_serve_scales_from_zero_llama3_8b_gpu():
+    """GPU variant: Llama-3-8B TP=1 on the box's one MI355X (graphs on); the pod's
+    cold start covers weights, KV pool and decode-graph capture."""
+    from conftest import release_gpu_memory
+
+    release_gpu_memory()
+    cold, first = _scale_cycle({"model": "llama-3-8b", "tp": 1, "maxBatch": 64,
+                                "maxModelLen": 4096, "kvFraction": 0.5}, gpu_count=1)
+    assert cold < 300

@@ -241,6 +241,68 @@ def test_retention_reembed_and_compaction_workers():
     asyncio.run(go())
 
 
+def test_access_touch_batcher_coalesces_reads():
+    """access_tracker.go: reads inside one window become ONE batched update with
+    per-row increments; stop() drains what is pending."""
+    st = MemoryStore()
+    a = st.save(mem("User prefers dark roast coffee"))
+    b = st.save(mem("User lives in Chicago"))
+    calls = []
+    inner = st.apply_touches
+    st.apply_touches = lambda ids, counts: (calls.append(dict(zip(ids, counts))),
+                                            inner(ids, counts))
+    bt = st.enable_touch_batching(interval_s=60.0)
+    scope = {"workspace_id": WS, "virtual_user_id": "u1"}
+    for _ in range(3):
+        st.search(scope, "coffee")
+    st.get(b["id"], touch=True)
+    assert calls == [] and st.get(a["id"]).access_count == 0  # still in the window
+    bt.stop()
+    assert len(calls) == 1 and sorted(calls[0].values()) == [1, 3]
+    assert st.get(a["id"]).access_count == 3 and st.get(b["id"]).access_count == 1
+    assert bt.stats["flushes"] == 1 and bt.stats["rows"] == 2
+    # overflow (cap distinct ids) flushes without waiting for the window
+    st2 = MemoryStore()
+    ids = [st2.save(mem(f"fact {i}"))["id"] for i in range(4)]
+    bt2 = st2.enable_touch_batching(interval_s=60.0, cap=3)
+    for i in ids:
+        st2.get(i, touch=True)
+    for _ in range(100):
+        if bt2.stats["flushes"]:
+            break
+        time.sleep(0.01)
+    assert bt2.stats["flushes"] >= 1
+    bt2.stop()
+    assert all(st2.get(i).access_count == 1 for i in ids)
+    assert st2.get(ids[0]).to_json()["access_count"] == 1
+
+
+def test_compaction_worker_discovers_workspaces_and_noop_summary():
+    from omnia_amd.memory.workers import noop_summarizer
+
+    async def go():
+        svc = MemoryService(MemoryStore(), None)
+        st = svc.store
+        old = time.time() - 40 * R.DAY
+        for ws in ("wa", "wb"):
+            for i in range(3):
+                r = st.save(Memory(content=f"{ws} old fact {i}",
+                                   scope={"workspace_id": ws, "virtual_user_id": "u"}))
+                with st.lock:
+                    st.db.execute("UPDATE memory_observations SET observed_at = ? WHERE id = ?",
+                                  (old, r["observation_id"]))
+        assert st.list_workspace_ids() == ["wa", "wb"]
+        w = CompactionWorker(svc, min_count=3)  # default: noop summarizer, discoverer
+        assert await w.run_once() == 2
+        left = st.list({"workspace_id": "wb", "virtual_user_id": "u"})
+        assert [m.content for m in left] == ["Summary of 3 observations. First: wb old fact 0"] \
+            or left[0].content.startswith("Summary of 3 observations. First: wb old fact")
+        with pytest.raises(ValueError):
+            await noop_summarizer([])
+
+    asyncio.run(go())
+
+
 def test_vector_index_cpu_matches_bruteforce():
     g = torch.Generator().manual_seed(0)
     idx = VectorIndex(32, device="cpu", capacity=4)

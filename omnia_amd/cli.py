@@ -199,6 +199,11 @@ async def run_operator(kubeconfig: str | None, in_cluster: bool, leader_elect: b
 
 
 def main(argv=None):
+    args = list(sys.argv[1:] if argv is None else argv)
+    if args[:1] == ["doctor"]:  # its own parser (omnia_amd/doctor)
+        from .doctor import main as dmain
+
+        return dmain(args[1:])
     ap = argparse.ArgumentParser("omnia")
     ap.add_argument("--server", default=os.environ.get("OMNIA_SERVER", "http://127.0.0.1:8090"))
     sp = ap.add_subparsers(dest="cmd", required=True)
@@ -234,9 +239,8 @@ def main(argv=None):
     sp.add_parser("crds")
     p = sp.add_parser("conformance")
     p.add_argument("--target", default="127.0.0.1:9000")
-    p = sp.add_parser("doctor")
-    p.add_argument("--facade", default="ws://127.0.0.1:8080/ws")
-    p.add_argument("--session-api", default="")
+    sp.add_parser("doctor", help="diagnostics: omnia doctor --run-once --facade ... | "
+                                 "serve the doctor UI (see omnia doctor -h)")
     a = ap.parse_args(argv)
     if a.cmd == "serve":
         asyncio.run(serve(a.port, a.filename, not a.no_engine, enterprise=a.enterprise,
@@ -261,11 +265,6 @@ def main(argv=None):
         from .runtime import conformance
 
         conformance.main(["--target", a.target])
-    elif a.cmd == "doctor":
-        from .doctor import main as dmain
-
-        dmain(["--facade", a.facade] + (["--session-api", a.session_api]
-                                        if a.session_api else []))
 
 
 if __name__ == "__main__":

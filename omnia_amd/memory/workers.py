@@ -15,6 +15,7 @@ from __future__ import annotations
 import asyncio
 import logging
 
+from ..observability import metrics as M
 from .model import SCOPE_WORKSPACE, Memory
 
 log = logging.getLogger("omnia.memory.workers")
@@ -33,12 +34,16 @@ class ReembedWorker:
                 return total
 
     async def run(self):
-        while True:
-            try:
-                await self.run_once()
-            except Exception as e:  # noqa: BLE001
-                log.warning("reembed pass failed: %s", e)
-            await asyncio.sleep(self.interval)
+        M.MEMORY_WORKER_RUNNING.labels("reembed").set(1)  # doctor liveness gauge
+        try:
+            while True:
+                try:
+                    await self.run_once()
+                except Exception as e:  # noqa: BLE001
+                    log.warning("reembed pass failed: %s", e)
+                await asyncio.sleep(self.interval)
+        finally:
+            M.MEMORY_WORKER_RUNNING.labels("reembed").set(0)
 
 
 class RetentionWorker:
@@ -66,12 +71,16 @@ class RetentionWorker:
         return len(obs)
 
     async def run(self):
-        while True:
-            try:
-                self.run_once()
-            except Exception as e:  # noqa: BLE001
-                log.warning("retention pass failed: %s", e)
-            await asyncio.sleep(self.interval)
+        M.MEMORY_WORKER_RUNNING.labels("retention").set(1)  # doctor liveness gauge
+        try:
+            while True:
+                try:
+                    self.run_once()
+                except Exception as e:  # noqa: BLE001
+                    log.warning("retention pass failed: %s", e)
+                await asyncio.sleep(self.interval)
+        finally:
+            M.MEMORY_WORKER_RUNNING.labels("retention").set(0)
 
 
 def default_summarizer_prompt(texts: list[str]) -> str:
@@ -126,12 +135,16 @@ class CompactionWorker:
         return done
 
     async def run(self):
-        while True:
-            try:
-                await self.run_once()
-            except Exception as e:  # noqa: BLE001
-                log.warning("compaction pass failed: %s", e)
-            await asyncio.sleep(self.interval)
+        M.MEMORY_WORKER_RUNNING.labels("compaction").set(1)  # doctor liveness gauge
+        try:
+            while True:
+                try:
+                    await self.run_once()
+                except Exception as e:  # noqa: BLE001
+                    log.warning("compaction pass failed: %s", e)
+                await asyncio.sleep(self.interval)
+        finally:
+            M.MEMORY_WORKER_RUNNING.labels("compaction").set(0)
 
 
 __all__ = ["ReembedWorker", "RetentionWorker", "CompactionWorker", "SCOPE_WORKSPACE"]

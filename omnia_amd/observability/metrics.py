@@ -43,6 +43,12 @@ POD_COLD_START = Histogram("omnia_pod_cold_start_seconds",
                            ["agent", "namespace"],
                            buckets=(1, 2, 5, 10, 20, 30, 60, 120, 300, 600, 900),
                            registry=REGISTRY)
+SESSION_API_REQUESTS = Counter("omnia_session_api_requests_total",
+                               "session-api HTTP requests by route and status",
+                               ["method", "route", "status"], registry=REGISTRY)
+MEMORY_WORKER_RUNNING = Gauge("omnia_memory_worker_running",
+                              "1 while a memory-api background worker loop is alive",
+                              ["name"], registry=REGISTRY)
 ENGINE_COLD_START = Gauge("omnia_engine_cold_start_seconds",
                           "Engine start-up time by phase (weights, kv_alloc, graph_warmup, total)",
                           ["phase"], registry=REGISTRY)

@@ -71,8 +71,23 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
                                      userId=request.headers.get("x-omnia-user-id", ""), **kw))
 
     @web.middleware
+    async def count(request, handler):
+        route = request.match_info.route.resource
+        name = route.canonical if route is not None else "?"
+        status = 500
+        try:
+            resp = await handler(request)
+            status = resp.status
+            return resp
+        except web.HTTPException as e:
+            status = e.status
+            raise
+        finally:
+            M.SESSION_API_REQUESTS.labels(request.method, name, str(status)).inc()
+
+    @web.middleware
     async def guard(request, handler):
-        if request.path == "/healthz":
+        if request.path in ("/healthz", "/metrics"):
             return await handler(request)
         if not limiter.allow(request.remote or "?"):
             return web.json_response({"error": "rate_limited"}, status=429)
@@ -88,7 +103,7 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
                 return web.json_response({"error": "forbidden"}, status=403)
         return await handler(request)
 
-    app = web.Application(middlewares=[guard], client_max_size=32 * 2**20)
+    app = web.Application(middlewares=[count, guard], client_max_size=32 * 2**20)
     r = app.router
 
     def nf(sid):
@@ -270,7 +285,23 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         n = sum(1 for s in rows if svc.delete(s.id))
         return web.json_response({"sessions_deleted": n, "errors": []})
 
+    async def metrics(_):
+        return web.Response(body=M.exposition(), content_type="text/plain")
+
+    async def openapi(_):
+        routes = sorted({(rt.method, rt.resource.canonical) for rt in app.router.routes()
+                         if rt.resource is not None and rt.method != "HEAD"})
+        paths: dict = {}
+        for method, path in routes:
+            paths.setdefault(path, {})[method.lower()] = {"responses": {"200": {
+                "description": "ok"}}}
+        return web.json_response({"openapi": "3.0.3", "info": {"title": "Omnia Session API",
+                                                               "version": "v1"},
+                                  "paths": paths})
+
     r.add_get("/healthz", healthz)
+    r.add_get("/metrics", metrics)
+    r.add_get("/api/v1/openapi.json", openapi)
     if audit_logger is not None:
         from ..ee.audit import mount_routes
 

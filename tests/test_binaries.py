@@ -69,53 +69,3 @@ def test_runtime_and_facade_processes():
             except subprocess.TimeoutExpired:
                 p.kill()
     assert fa.returncode == 0 and rt.returncode == 0
-
-
-def test_doctor_against_live_services():
-    """Doctor probes a live facade + session-api + memory-api + metrics."""
-    from aiohttp import web
-
-    from omnia_amd.doctor import FAIL, PASS, SKIP, run_checks
-    from omnia_amd.memory.api import build_app as memory_app
-    from omnia_amd.memory.service import MemoryService
-    from omnia_amd.session.api import build_app as session_app
-    from omnia_amd.session.store import TieredSessionService
-
-    async def serve(app):
-        runner = web.AppRunner(app)
-        await runner.setup()
-        site = web.TCPSite(runner, "127.0.0.1", 0)
-        await site.start()
-        return runner, f"http://127.0.0.1:{site._server.sockets[0].getsockname()[1]}"
-
-    class A:
-        token = ""
-        redis = ""
-        privacy_api = ""
-
-    async def go():
-        from omnia_amd.facade.runtime_client import InProcessRuntimeClient
-        from omnia_amd.facade.server import FacadeConfig, FacadeServer
-        from omnia_amd.runtime.app import build_runtime
-        from omnia_amd.runtime.config import RuntimeConfig
-
-        svc = await build_runtime(RuntimeConfig(provider={"type": "mock"}))
-        fac = FacadeServer(FacadeConfig(), runtime_client=InProcessRuntimeClient(svc))
-        port = await fac.start("127.0.0.1", 0)
-        r1, s_url = await serve(session_app(TieredSessionService()))
-        r2, m_url = await serve(memory_app(MemoryService()))
-        a = A()
-        a.facade, a.session_api, a.memory_api = f"ws://127.0.0.1:{port}/ws", s_url, m_url
-        a.metrics = f"http://127.0.0.1:{port}/metrics"
-        try:
-            return {r.name: r for r in await run_checks(a)}
-        finally:
-            await fac.stop()
-            await r1.cleanup()
-            await r2.cleanup()
-
-    res = asyncio.run(go())
-    for n in ("crds", "agent", "sessions", "memory", "observability"):
-        assert res[n].status == PASS, res[n]
-    assert res["redis"].status == SKIP and res["gpu"].status in (SKIP, PASS)
-    assert all(r.status != FAIL for r in res.values())

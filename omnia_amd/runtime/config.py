@@ -112,6 +112,82 @@ class RuntimeConfig:
                     if k.startswith("OMNIA_ENGINE_")}
         if e.get("OMNIA_A2A_CLIENTS"):
             c.a2a_clients = json.loads(e["OMNIA_A2A_CLIENTS"])
+        if e.get("OMNIA_CONFIG_DIR"):
+            c = c.with_config_dir(e["OMNIA_CONFIG_DIR"], e)
+        return c
+
+    def with_config_dir(self, path: str, env) -> "RuntimeConfig":
+        """Cluster-less configuration (``OMNIA_CONFIG_DIR``, the reference's
+        fake-client devroot, ``examples/custom-runtime/README.md``): the
+        AgentRuntime / Provider / PromptPack / Secret objects are read from every
+        ``*.yaml`` / ``*.yml`` in ``path`` and resolved exactly as the operator
+        would (CRD values win over env, as ``config_crd.go``); the mounted-file
+        paths and ports keep coming from the environment."""
+        import base64
+        import glob
+
+        import yaml
+
+        docs = []
+        for f in sorted(glob.glob(os.path.join(path, "*.yaml")) +
+                        glob.glob(os.path.join(path, "*.yml"))):
+            with open(f) as fh:
+                docs += [d for d in yaml.safe_load_all(fh) if isinstance(d, dict)]
+
+        def find(kind, name=None, ns=None):
+            return [d for d in docs if d.get("kind") == kind
+                    and (name is None or d["metadata"].get("name") == name)
+                    and (ns is None or d["metadata"].get("namespace", "default") == ns)]
+
+        ars = find("AgentRuntime", self.agent_name, self.namespace) or \
+            (find("AgentRuntime") if len(find("AgentRuntime")) == 1 else [])
+        if not ars:
+            raise ValueError(f"OMNIA_CONFIG_DIR {path}: no AgentRuntime "
+                             f"{self.namespace}/{self.agent_name}")
+        ar = ars[0]
+        ar["metadata"].setdefault("namespace", self.namespace)
+        ns = ar["metadata"]["namespace"]
+        providers = []
+        for ref in ar["spec"].get("providers") or []:
+            pr = (ref.get("providerRef") or {}).get("name")
+            got = find("Provider", pr, ref.get("providerRef", {}).get("namespace", ns))
+            if got:
+                p = {"metadata": got[0]["metadata"], "spec": dict(got[0]["spec"])}
+                if ref.get("name") and ref["name"] != "llm":
+                    p["spec"].setdefault("role", ref["name"])
+                cred = (p["spec"].get("credential") or {}).get("secretRef") or \
+                    p["spec"].get("secretRef")
+                if cred:  # the provider key, read like the in-cluster path would
+                    sec = find("Secret", cred.get("name"), ns)
+                    if sec:
+                        data = {k: base64.b64decode(v).decode()
+                                for k, v in (sec[0].get("data") or {}).items()}
+                        data.update(sec[0].get("stringData") or {})
+                        key = cred.get("key") or next(iter(data), None)
+                        if key in data:
+                            p["spec"]["apiKey"] = data[key]
+                providers.append(p)
+        pref = (ar["spec"].get("promptPackRef") or {}).get("name", "")
+        packs = find("PromptPack", pref, ns)
+        pack = packs[0] if packs else {"spec": {"packName": pref,
+                                                "version": (ar["spec"].get("promptPackRef")
+                                                            or {}).get("version", "")}}
+        from ..operator.builders import runtime_config
+
+        c = runtime_config(ar, pack, providers, None)
+        for f in ("promptpack_path", "tools_config_path", "grpc_port", "health_port",
+                  "session_api_url", "memory_api_url", "workspace", "workspace_uid",
+                  "tool_secrets_dir", "a2a_clients", "policy_broker_url", "tracing_enabled",
+                  "tracing_endpoint", "stream_interval_ms"):
+            setattr(c, f, getattr(self, f))
+        if env.get("OMNIA_PROMPTPACK_PATH") is None:
+            c.promptpack_path = self.promptpack_path
+        if self.engine and not c.engine:
+            c.engine = dict(self.engine)
+        wss = [w for w in find("Workspace")
+               if ((w.get("spec") or {}).get("namespace") or {}).get("name") == ns]
+        if wss and not c.workspace:
+            c.workspace = wss[0]["metadata"]["name"]
         return c
 
     def to_env(self) -> dict:

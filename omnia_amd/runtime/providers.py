@@ -479,9 +479,9 @@ def build_provider(spec: dict, engine=None, secrets: dict | None = None) -> Prov
                       float(pr.get("outputCostPer1K", 0) or 0),
                       float(pr.get("cachedCostPer1K", 0) or 0))
     defaults = spec.get("defaults") or {}
-    key = None
+    key = spec.get("apiKey")  # resolved from a devroot Secret (OMNIA_CONFIG_DIR)
     cred = spec.get("credential") or {}
-    if secrets:
+    if secrets and key is None:
         key = secrets.get(cred.get("secretRef", {}).get("key", "api-key")) or \
             next(iter(secrets.values()), None)
     if t in ("local", "omnia", "rocm", "engine"):

@@ -432,7 +432,8 @@ class LocalLauncher:
         world = tp  # engine ranks of one pod: TP group, or the EP (a2a) group
         if renv.get("OMNIA_ENGINE_EP_MODE") == "a2a":
             world = max(tp, int(renv.get("OMNIA_ENGINE_EP", "1") or 1))
-        if rc_provider in ("local", "engine", "omnia", "rocm") and self.devices.count:
+        if rc_provider in ("local", "engine", "omnia", "rocm") and self.devices.count and \
+                renv.get("OMNIA_ENGINE_DEVICE", "cuda") != "cpu":
             devices = self.devices.take(who, world)
             if devices is None:
                 raise RuntimeError(f"no {world} free GPU(s) for {key[0]}/{key[1]} replica "

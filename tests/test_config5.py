@@ -67,7 +67,9 @@ def _run(engine_patch: dict, max_tokens: int = 1024, gpu_count: int = 0):
             for d in docs:
                 store.apply(d)
             mem_ep = planner_ep = None
-            for _ in range(3000):
+            for i in range(3000):
+                if i % 100 == 0:  # progress (GPU boxes kill silent runs)
+                    print(f"[cfg5] waiting for pods: {i // 10}s", flush=True)
                 mem_ep = ep(store, "memory-api-research-default")
                 planner_ep = ep(store, "planner")
                 res_dep = store.try_get("Deployment", "researcher", NS)
@@ -85,6 +87,7 @@ def _run(engine_patch: dict, max_tokens: int = 1024, gpu_count: int = 0):
                     "type": "fact", "confidence": 0.9})
                 assert r.status == 201, await r.text()
                 mid = (await r.json())["memory"]["id"]
+                print("[cfg5] pods up, running the turn", flush=True)
                 async with FleetSession(f"ws://{planner_ep}/ws", headers={"x-user-id": "alice"},
                                         timeout_s=600) as fs:
                     turn = await fs.turn("What should I do next on my project?")

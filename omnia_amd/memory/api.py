@@ -181,7 +181,8 @@ def build_app(svc: MemoryService, enterprise: bool = False, chunk_size: int = 20
                                    limit=limit)
             mems = svc.store.retrieve_multi_tier(req)
         else:
-            mems = svc.store.list(scope, _types(q.get("type")), limit, _int(q, "offset", 0))
+            mems = await svc.list_cached(scope, _types(q.get("type")), limit,
+                                         _int(q, "offset", 0))
         return web.json_response(_list_json(mems))
 
     async def search(request):
@@ -190,7 +191,7 @@ def build_app(svc: MemoryService, enterprise: bool = False, chunk_size: int = 20
         if not q.get("q"):
             return _err(400, "query parameter q is required")
         limit = min(max(_int(q, "limit", DEFAULT_LIST_LIMIT), 1), MAX_LIST_LIMIT)
-        mems = svc.store.search(scope, q["q"], limit)
+        mems = await svc.search_cached(scope, q["q"], limit)
         mc = float(q.get("min_confidence") or 0)
         mems = [m for m in mems if m.confidence >= mc]
         return web.json_response(_list_json(mems, preview=True,
@@ -464,9 +465,7 @@ def build_app(svc: MemoryService, enterprise: bool = False, chunk_size: int = 20
         t = int(d.get("target_dim") or 0)
         if not 1 <= t <= 2000:
             return _err(400, "target_dim must be in 1..2000")
-        with svc.store.lock:
-            svc.store.db.execute("INSERT OR REPLACE INTO memory_meta VALUES (?, ?)",
-                                 ("memory_embedding_dim_change_consent", str(t)))
+        svc.store.record_dim_consent(t)
         return web.json_response({"target_dim": t, "status": "recorded"})
 
     async def stats(request):
@@ -584,6 +583,16 @@ def main(argv=None):
                     help="temporal-summarisation worker period (e.g. 6h); empty disables")
     ap.add_argument("--compaction-age", default=os.environ.get("COMPACTION_AGE", ""),
                     help="age threshold of compaction candidates (e.g. 720h)")
+    ap.add_argument("--postgres-dsn", default=os.environ.get("MEMORY_POSTGRES_DSN", ""),
+                    help="Postgres + pgvector store (needs a DB-API driver); default SQLite --db")
+    ap.add_argument("--redis-cache", default=os.environ.get("MEMORY_CACHE_REDIS_URL", ""),
+                    help="redis://host:port for the list / search read cache")
+    ap.add_argument("--cache-ttl", type=int, default=300)
+    ap.add_argument("--tombstone-interval", default=os.environ.get("TOMBSTONE_INTERVAL", ""),
+                    help="tombstone GC period (e.g. 1h); empty disables")
+    ap.add_argument("--tombstone-min-age", default=os.environ.get("TOMBSTONE_MIN_AGE", "720h"))
+    ap.add_argument("--tombstone-min-inactive", type=int, default=20)
+    ap.add_argument("--tombstone-keep-recent", type=int, default=5)
     ap.add_argument("--access-touch-interval", type=float,
                     default=float(os.environ.get("ACCESS_TOUCH_INTERVAL", "1.0")),
                     help="seconds per batched access-count flush; 0 = one update per read")
@@ -608,11 +617,33 @@ def main(argv=None):
     if a.policy_file:
         with open(a.policy_file) as f:
             policy = json.load(f)
-    store = MemoryStore(a.db)
+    if a.postgres_dsn:
+        from .sqldialect import MemoryPostgres, connect_postgres
+
+        conn = connect_postgres(a.postgres_dsn)
+        if conn is None:
+            raise SystemExit("--postgres-dsn given but no Postgres DB-API driver is installed")
+        store = MemoryStore(dialect=MemoryPostgres(paramstyle="format"), conn=conn)
+    else:
+        store = MemoryStore(a.db)
     if a.access_touch_interval > 0:
         store.enable_touch_batching(a.access_touch_interval)
     svc = MemoryService(store, emb, publisher=pub, enterprise=a.enterprise)
+    if a.redis_cache:
+        from ..utils.resp import RedisClient
+        from .cache import CachedStore
+
+        svc.cache = CachedStore(store, RedisClient(a.redis_cache), a.cache_ttl)
     app = build_app(svc, a.enterprise, a.ingest_chunk_size, a.ingest_chunk_overlap)
+    tombstone = None
+    if a.tombstone_interval:
+        from ..utils.durations import parse_duration
+        from .workers import TombstoneWorker
+
+        tombstone = TombstoneWorker(svc, parse_duration(a.tombstone_interval),
+                                    min_age_s=parse_duration(a.tombstone_min_age),
+                                    min_inactive=a.tombstone_min_inactive,
+                                    keep_recent=a.tombstone_keep_recent)
     compaction = None
     if a.compaction_interval:
         from ..utils.durations import parse_duration
@@ -638,6 +669,8 @@ def main(argv=None):
                           asyncio.create_task(RetentionWorker(svc, policy=policy).run())]
         if compaction is not None:
             app["workers"].append(asyncio.create_task(compaction.run()))
+        if tombstone is not None:
+            app["workers"].append(asyncio.create_task(tombstone.run()))
 
     async def stop_workers(app):
         for t in app.get("workers", []):

@@ -47,7 +47,11 @@ class MemoryService:
         self.device = device
         self.indexes: dict[str, VectorIndex] = {}
         self.embed_model = getattr(embedder, "model", "") if embedder else ""
+        self.vec_seq = 0  # last memory_vector_log row this replica's indexes applied
+        self.cache = None  # optional CachedStore (Redis) for list / search reads
         if embedder is not None:
+            if getattr(embedder, "dim", 0):
+                self.store.ensure_embedding_dim(embedder.dim)
             self._warm_indexes()
 
     # ------------------------------------------------------------ indexes
@@ -60,6 +64,7 @@ class MemoryService:
         return idx
 
     def _warm_indexes(self):
+        self.vec_seq = self.store.max_vector_seq()
         by_ws: dict[str, list] = {}
         for oid, ws, vec in self.store.embeddings(model=self.embed_model or None):
             if vec is not None and len(vec) == getattr(self.embedder, "dim", -1):
@@ -68,6 +73,55 @@ class MemoryService:
             idx = self._index(ws)
             if idx is not None:
                 idx.upsert(items)
+
+    def sync_vectors(self) -> int:
+        """Apply the store's vector changes since the last sync to this replica's
+        device indexes (another replica's writes, deletes, supersessions): the
+        database is the source of truth, the GPU index a per-replica cache."""
+        if self.embedder is None:
+            return 0
+        applied = 0
+        while True:
+            rows = self.store.vector_changes(self.vec_seq)
+            if not rows:
+                return applied
+            last: dict[str, tuple] = {}  # obs_id -> (workspace, op) of its latest change
+            for seq, oid, ws, op in rows:
+                last[oid] = (ws, op)
+                self.vec_seq = seq
+            ups = [o for o, (_, op) in last.items() if op == "upsert"]
+            vecs = self.store.embedding_of(ups)
+            dim = getattr(self.embedder, "dim", -1)
+            by_ws: dict[str, list] = {}
+            for oid, (ws, op) in last.items():
+                if op == "upsert" and oid in vecs and len(vecs[oid]) == dim:
+                    by_ws.setdefault(ws, []).append((oid, vecs[oid].tolist()))
+                else:
+                    idx = self.indexes.get(ws)
+                    if idx is not None:
+                        idx.remove([oid])
+            for ws, items in by_ws.items():
+                idx = self._index(ws)
+                if idx is not None:
+                    idx.upsert(items)
+            applied += len(last)
+
+    async def _invalidate(self, scope_or_ws) -> None:
+        """Writes bump the workspace's read-cache version (cache.py)."""
+        if self.cache is not None:
+            scope = scope_or_ws if isinstance(scope_or_ws, dict) else \
+                {SCOPE_WORKSPACE: scope_or_ws}
+            await self.cache.bump(scope)
+
+    async def list_cached(self, scope: dict, types=None, limit: int = 50, offset: int = 0):
+        if self.cache is None:
+            return self.store.list(scope, types, limit, offset)
+        return await self.cache.list(scope, types, limit, offset)
+
+    async def search_cached(self, scope: dict, query: str, limit: int = 10):
+        if self.cache is None:
+            return self.store.search(scope, query, limit)
+        return await self.cache.search(scope, query, limit)
 
     def _drop_vectors(self, obs_ids):
         for idx in self.indexes.values():
@@ -138,6 +192,10 @@ class MemoryService:
                     mem.id = ent
                     res = self.store.save(mem, require_user=require_user)
                     with self.store._tx() as db:
+                        prev = [r[0] for r in db.execute(
+                            "SELECT id FROM memory_observations WHERE entity_id = ? AND id != ? "
+                            "AND superseded_by IS NULL", (ent, res["observation_id"])).fetchall()]
+                        self.store._log_vectors(db, "delete", prev)
                         db.execute("UPDATE memory_observations SET superseded_by = ? WHERE "
                                    "entity_id = ? AND id != ? AND superseded_by IS NULL",
                                    (res["observation_id"], ent, res["observation_id"]))
@@ -146,6 +204,7 @@ class MemoryService:
                     self._after_write(ws, res, vec, [near[0][0]])
                     await self._publish(ws, {"type": "memory.saved", "id": res["id"],
                                              "action": res["action"]})
+                    await self._invalidate(mem.scope)
                     return res
             for oid, sim in near:
                 if sim >= SURFACE_DUPLICATE_SIMILARITY and len(dups) < DUPLICATE_CANDIDATE_LIMIT:
@@ -157,6 +216,7 @@ class MemoryService:
         if dups:
             res["potential_duplicates"] = dups
         await self._publish(ws, {"type": "memory.saved", "id": res["id"], "action": res["action"]})
+        await self._invalidate(mem.scope)
         return res
 
     def _same_scope(self, near, scope):
@@ -194,6 +254,7 @@ class MemoryService:
                 self._after_write(m.scope[SCOPE_WORKSPACE], {"observation_id": m.observation_id},
                                   vv[0], [])
         await self._publish(m.scope[SCOPE_WORKSPACE], {"type": "memory.updated", "id": m.id})
+        await self._invalidate(m.scope)
         return m
 
     async def forget(self, entity_id: str, workspace: str | None = None) -> bool:
@@ -201,6 +262,7 @@ class MemoryService:
         if ok:
             self._drop_vectors(self.store.observation_ids_of([entity_id]))
             await self._publish(workspace or "", {"type": "memory.forgotten", "id": entity_id})
+            await self._invalidate(workspace or "")
         return ok
 
     async def delete_all(self, scope: dict) -> int:
@@ -208,11 +270,13 @@ class MemoryService:
         self._drop_vectors(obs)
         await self._publish(scope.get(SCOPE_WORKSPACE, ""), {"type": "memory.deleted_all",
                                                             "count": n})
+        await self._invalidate(scope)
         return n
 
     async def batch_delete(self, scope: dict, limit: int) -> int:
         n, obs = self.store.batch_delete(scope, limit)
         self._drop_vectors(obs)
+        await self._invalidate(scope)
         return n
 
     async def supersede(self, source_ids: list[str], mem: Memory) -> dict:
@@ -220,6 +284,7 @@ class MemoryService:
         self._drop_vectors(self.store.observation_ids_of(source_ids))
         vv = await self._embed([mem.content]) if self.embedder is not None else None
         self._after_write(mem.scope[SCOPE_WORKSPACE], res, vv[0] if vv else None, [])
+        await self._invalidate(mem.scope)
         return res
 
     async def ann(self, workspace: str, query: str, k: int):
@@ -228,6 +293,7 @@ class MemoryService:
         vv = await self._embed([query])
         if not vv:
             return []
+        self.sync_vectors()  # other replicas' writes since the last query
         idx = self._index(workspace)
         if idx is None:
             return []

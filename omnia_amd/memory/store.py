@@ -1,9 +1,12 @@
 """Memory store: entities / observations / relations (``internal/memory/store*.go``).
 
-SQLite replaces Postgres: an FTS5 table with the porter stemmer stands in for
-the ``search_vector`` tsvector column (bm25 for ``ts_rank_cd``), embeddings are
-kept as float32 blobs for durability and mirrored into a device-resident
-:class:`VectorIndex` per workspace for search.  Semantics kept from the reference:
+Two SQL dialects (``sqldialect.py``): SQLite by default (an FTS5 table with the
+porter stemmer for the ``search_vector`` tsvector column, bm25 for
+``ts_rank_cd``, embeddings as float32 blobs) and Postgres + pgvector.  The store
+(and every replica of the memory-api sharing it) is the vector source of truth:
+embeddings live in the database and every change to them is appended to
+``memory_vector_log``, which each replica tails to keep its device-resident
+:class:`VectorIndex` in step.  Semantics kept from the reference:
 
 * one entity carries a chain of observations; exactly the latest non-superseded,
   still-valid observation is "active" (``superseded_by IS NULL AND (valid_until IS
@@ -27,40 +30,13 @@ import numpy as np
 
 from . import retrieval as R
 from .fts import to_fts5
+from .sqldialect import (CONSENT_TABLE, EmbeddingDimConsentRequired, MemoryPostgres,
+                         MemorySQLite, parse_vector_literal, vector_literal)
 from .model import (META_ABOUT_KEY, META_ABOUT_KIND, META_CONSENT_CATEGORY, META_PURPOSE,
                     META_SOURCE_TYPE, META_TITLE, SCOPE_AGENT, SCOPE_USER, SCOPE_WORKSPACE,
                     SOURCE_TYPE_WEIGHT, Memory, Tier, derive_tier, new_id, normalize_scope)
 
-SCHEMA = """
-CREATE TABLE IF NOT EXISTS memory_entities (
-  id TEXT PRIMARY KEY, workspace_id TEXT NOT NULL, kind TEXT NOT NULL DEFAULT 'fact',
-  metadata TEXT NOT NULL DEFAULT '{}', created_at REAL NOT NULL, updated_at REAL NOT NULL,
-  expires_at REAL, title TEXT, virtual_user_id TEXT, agent_id TEXT,
-  source_type TEXT, trust_model TEXT, purpose TEXT, consent_category TEXT,
-  about_kind TEXT, about_key TEXT, forgotten INTEGER NOT NULL DEFAULT 0);
-CREATE INDEX IF NOT EXISTS ix_ent_ws ON memory_entities(workspace_id, virtual_user_id, agent_id);
-CREATE UNIQUE INDEX IF NOT EXISTS ux_ent_about ON memory_entities(
-  workspace_id, coalesce(virtual_user_id, ''), coalesce(agent_id, ''), about_kind, about_key)
-  WHERE about_kind IS NOT NULL AND forgotten = 0;
-CREATE TABLE IF NOT EXISTS memory_observations (
-  id TEXT PRIMARY KEY, entity_id TEXT NOT NULL, content TEXT NOT NULL,
-  confidence REAL NOT NULL DEFAULT 0.7, session_id TEXT, turn_range TEXT,
-  observed_at REAL NOT NULL, accessed_at REAL, access_count INTEGER NOT NULL DEFAULT 0,
-  summary TEXT, body_size_bytes INTEGER, superseded_by TEXT, valid_until REAL,
-  embedding BLOB, embedding_model TEXT);
-CREATE INDEX IF NOT EXISTS ix_obs_ent ON memory_observations(entity_id, observed_at);
-CREATE VIRTUAL TABLE IF NOT EXISTS memory_fts USING fts5(
-  content, title, obs_id UNINDEXED, tokenize = 'porter unicode61');
-CREATE TABLE IF NOT EXISTS memory_relations (
-  id TEXT PRIMARY KEY, workspace_id TEXT NOT NULL, source_entity_id TEXT NOT NULL,
-  target_entity_id TEXT NOT NULL, relation_type TEXT NOT NULL, weight REAL NOT NULL DEFAULT 1.0,
-  created_at REAL NOT NULL);
-CREATE INDEX IF NOT EXISTS ix_rel_src ON memory_relations(source_entity_id);
-CREATE TABLE IF NOT EXISTS memory_meta (key TEXT PRIMARY KEY, value TEXT);
-CREATE TABLE IF NOT EXISTS consent_revocations (
-  workspace_id TEXT, virtual_user_id TEXT, category TEXT, revoked_at REAL,
-  PRIMARY KEY (workspace_id, virtual_user_id, category));
-"""
+SCHEMA = MemorySQLite().schema()  # the SQLite DDL (sqldialect.py)
 
 _ACTIVE = "o.superseded_by IS NULL AND (o.valid_until IS NULL OR o.valid_until > ?)"
 _ENT_COLS = ("e.id, e.kind, e.metadata, e.created_at, e.expires_at, e.title, e.virtual_user_id, "
@@ -151,12 +127,58 @@ class AccessTouchBatcher:
         self.thread.join(timeout=5)
 
 
+class _DB:
+    """The store's connection: every statement passes through the dialect
+    (placeholders) before it reaches SQLite or a DB-API Postgres connection."""
+
+    def __init__(self, raw, dialect):
+        self.raw, self.d = raw, dialect
+        self.sqlite = isinstance(raw, sqlite3.Connection)
+
+    def execute(self, sql: str, args=()):
+        sql = self.d.q(sql)
+        if self.sqlite:
+            return self.raw.execute(sql, tuple(args))
+        cur = self.raw.cursor()
+        cur.execute(sql, tuple(args))
+        return cur
+
+    def executemany(self, sql: str, rows):
+        sql = self.d.q(sql)
+        if self.sqlite:
+            return self.raw.executemany(sql, rows)
+        cur = self.raw.cursor()
+        cur.executemany(sql, rows)
+        return cur
+
+
+def default_dialect():
+    """SQLite unless ``OMNIA_MEMORY_SQL_DIALECT=postgres-emulated`` (the Postgres
+    DML on SQLite, as the dialect tests run it)."""
+    import os
+
+    if os.environ.get("OMNIA_MEMORY_SQL_DIALECT") == "postgres-emulated":
+        return MemoryPostgres(emulate=True)
+    return MemorySQLite()
+
+
 class MemoryStore:
-    def __init__(self, path: str = ":memory:"):
-        self.db = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
-        self.db.execute("PRAGMA journal_mode=WAL")
-        self.db.execute("PRAGMA synchronous=NORMAL")
-        self.db.executescript(SCHEMA)
+    """``path``: SQLite file (":memory:" default).  ``dialect``: MemorySQLite
+    (default) or MemoryPostgres; ``conn``: an open Postgres DB-API connection
+    (``sqldialect.connect_postgres``), otherwise SQLite at ``path``."""
+
+    def __init__(self, path: str = ":memory:", dialect=None, conn=None):
+        self.d = dialect or default_dialect()
+        if conn is None:
+            raw = sqlite3.connect(path, check_same_thread=False, isolation_level=None,
+                                  timeout=30)
+            raw.execute("PRAGMA journal_mode=WAL")
+            raw.execute("PRAGMA synchronous=NORMAL")
+        else:
+            raw = conn
+        self.db = _DB(raw, self.d)
+        for stmt in self.d.schema():
+            self.db.raw.execute(stmt) if self.db.sqlite else self.db.execute(stmt)
         self.lock = threading.RLock()
         self.touch_batcher: AccessTouchBatcher | None = None
 
@@ -167,7 +189,7 @@ class MemoryStore:
         class _T:
             def __enter__(self_):
                 store.lock.acquire()
-                store.db.execute("BEGIN IMMEDIATE")
+                store.db.execute(store.d.begin())
                 return store.db
 
             def __exit__(self_, et, ev, tb):
@@ -255,12 +277,12 @@ class MemoryStore:
 
     def _fts_ids(self, query: str, limit: int) -> dict[str, float]:
         """obs_id -> bm25 (lower = better) for a websearch-style query."""
-        expr = to_fts5(query)
+        expr = to_fts5(query) if self.d.uses_fts_table else query.strip()
         if not expr:
             return {}
+        sql, args = self.d.fts_search(expr, limit)
         try:
-            rows = self._q("SELECT obs_id, bm25(memory_fts) FROM memory_fts WHERE memory_fts "
-                           "MATCH ? ORDER BY bm25(memory_fts) LIMIT ?", (expr, limit))
+            rows = self._q(sql, args)
         except sqlite3.OperationalError:
             return {}
         return {r[0]: r[1] for r in rows}
@@ -333,6 +355,7 @@ class MemoryStore:
                     raise NotFound(mem.id)
             oid = self._insert_observation(db, mem, now)
             if res["action"] == "auto_superseded":
+                self._log_vectors(db, "delete", res["supersedes"])
                 db.execute("UPDATE memory_observations SET superseded_by = ? WHERE id IN (%s)"
                            % ",".join("?" * len(res["supersedes"])), [oid] + res["supersedes"]) \
                     if res["supersedes"] else None
@@ -365,9 +388,43 @@ class MemoryStore:
              json.dumps(mem.turn_range) if mem.turn_range else None, now, mem.summary or None,
              len(mem.content.encode())))
         title = mem.title or (mem.metadata or {}).get(META_TITLE) or ""
-        db.execute("INSERT INTO memory_fts (content, title, obs_id) VALUES (?,?,?)",
-                   (mem.content, title, oid))
+        if self.d.uses_fts_table:  # Postgres: the generated search_vector column
+            db.execute("INSERT INTO memory_fts (content, title, obs_id) VALUES (?,?,?)",
+                       (mem.content, title, oid))
         return oid
+
+    # ------------------------------------------------------------ vector log
+    def _log_vectors(self, db, op: str, obs_ids: list[str], only_embedded: bool = True):
+        """Append ``op`` ("upsert" / "delete") for these observations to the change
+        log every replica's vector index tails (``vector_changes``)."""
+        if not obs_ids:
+            return
+        ph = ",".join("?" * len(obs_ids))
+        cond = " AND o.embedding IS NOT NULL" if only_embedded else ""
+        db.execute(f"INSERT INTO memory_vector_log (obs_id, workspace_id, op, at) SELECT o.id, "
+                   f"e.workspace_id, ?, ? FROM memory_observations o JOIN memory_entities e ON "
+                   f"e.id = o.entity_id WHERE o.id IN ({ph}){cond}",
+                   [op, time.time()] + list(obs_ids))
+
+    def vector_changes(self, after_seq: int, limit: int = 10000) -> list[tuple]:
+        """(seq, obs_id, workspace, op) after ``after_seq``, oldest first."""
+        return self._q("SELECT seq, obs_id, workspace_id, op FROM memory_vector_log WHERE "
+                       "seq > ? ORDER BY seq LIMIT ?", (after_seq, limit))
+
+    def max_vector_seq(self) -> int:
+        return int(self._q("SELECT coalesce(max(seq), 0) FROM memory_vector_log")[0][0])
+
+    def embedding_of(self, obs_ids: list[str]) -> dict[str, np.ndarray]:
+        if not obs_ids:
+            return {}
+        ph = ",".join("?" * len(obs_ids))
+        return {r[0]: self._vec(r[1]) for r in self._q(
+            f"SELECT o.id, {self.d.vec_select()} FROM memory_observations o WHERE o.id IN "
+            f"({ph}) AND o.embedding IS NOT NULL", obs_ids)}
+
+    @staticmethod
+    def _vec(v):
+        return parse_vector_literal(v) if isinstance(v, str) else _f32(v)
 
     def _supersede_active(self, db, entity_id: str, new_oid) -> list[str]:
         now = time.time()
@@ -375,6 +432,7 @@ class MemoryStore:
             "SELECT id FROM memory_observations o WHERE entity_id = ? AND " + _ACTIVE,
             (entity_id, now)).fetchall()]
         if ids and new_oid:
+            self._log_vectors(db, "delete", ids)
             db.execute("UPDATE memory_observations SET superseded_by = ? WHERE id IN (%s)"
                        % ",".join("?" * len(ids)), [new_oid] + ids)
         return ids
@@ -393,6 +451,10 @@ class MemoryStore:
             db.execute("UPDATE memory_entities SET metadata = ?, updated_at = ? WHERE id = ?",
                        (json.dumps(mem.metadata), time.time(), entity_id))
             oid = self._insert_observation(db, mem, time.time())
+            old = [r[0] for r in db.execute(
+                "SELECT id FROM memory_observations WHERE entity_id = ? AND id != ? AND "
+                "superseded_by IS NULL", (entity_id, oid)).fetchall()]
+            self._log_vectors(db, "delete", old)
             db.execute("UPDATE memory_observations SET superseded_by = ? WHERE entity_id = ? "
                        "AND id != ? AND superseded_by IS NULL", (oid, entity_id, oid))
         mem.observation_id = oid
@@ -403,6 +465,11 @@ class MemoryStore:
         res = self.save(mem, require_user=False)
         with self._tx() as db:
             ph = ",".join("?" * len(source_ids))
+            old = [r[0] for r in db.execute(
+                f"SELECT id FROM memory_observations WHERE entity_id IN ({ph}) AND "
+                f"superseded_by IS NULL AND entity_id != ?",
+                list(source_ids) + [res["id"]]).fetchall()]
+            self._log_vectors(db, "delete", old)
             db.execute(f"UPDATE memory_observations SET superseded_by = ? WHERE entity_id IN "
                        f"({ph}) AND superseded_by IS NULL AND entity_id != ?",
                        [res["observation_id"]] + list(source_ids) + [res["id"]])
@@ -410,10 +477,15 @@ class MemoryStore:
         return res
 
     def set_embedding(self, obs_id: str, vec, model: str):
-        blob = None if vec is None else np.asarray(vec, dtype=np.float32).tobytes()
-        with self.lock:
-            self.db.execute("UPDATE memory_observations SET embedding = ?, embedding_model = ? "
-                            "WHERE id = ?", (blob, model, obs_id))
+        arr = None if vec is None else np.asarray(vec, dtype=np.float32)
+        param = None if arr is None else self.d.vec_param(arr.tobytes(), vector_literal(arr))
+        with self._tx() as db:
+            if arr is None:
+                self._log_vectors(db, "delete", [obs_id])
+            db.execute("UPDATE memory_observations SET embedding = ?, embedding_model = ? "
+                       "WHERE id = ?", (param, model, obs_id))
+            if arr is not None:
+                self._log_vectors(db, "upsert", [obs_id])
 
     def link(self, workspace: str, source: str, target: str, rtype: str,
              weight: float = 1.0) -> str:
@@ -434,8 +506,13 @@ class MemoryStore:
         if workspace:
             sql += " AND workspace_id = ?"
             args.append(workspace)
-        with self.lock:
-            return self.db.execute(sql, args).rowcount > 0
+        with self._tx() as db:
+            n = db.execute(sql, args).rowcount
+            if n:
+                obs = [r[0] for r in db.execute("SELECT id FROM memory_observations WHERE "
+                                                "entity_id = ?", (entity_id,)).fetchall()]
+                self._log_vectors(db, "delete", obs)
+            return n > 0
 
     def _hard_delete(self, db, entity_ids: list[str]) -> list[str]:
         if not entity_ids:
@@ -444,8 +521,10 @@ class MemoryStore:
         obs = [r[0] for r in db.execute(
             f"SELECT id FROM memory_observations WHERE entity_id IN ({ph})", entity_ids)]
         if obs:
-            oph = ",".join("?" * len(obs))
-            db.execute(f"DELETE FROM memory_fts WHERE obs_id IN ({oph})", obs)
+            self._log_vectors(db, "delete", obs)
+            if self.d.uses_fts_table:
+                oph = ",".join("?" * len(obs))
+                db.execute(f"DELETE FROM memory_fts WHERE obs_id IN ({oph})", obs)
         db.execute(f"DELETE FROM memory_observations WHERE entity_id IN ({ph})", entity_ids)
         db.execute(f"DELETE FROM memory_relations WHERE source_entity_id IN ({ph}) OR "
                    f"target_entity_id IN ({ph})", entity_ids + entity_ids)
@@ -489,7 +568,8 @@ class MemoryStore:
     def revoke_consent(self, workspace: str, user: str, category: str) -> list[str]:
         """Consent revocation: delete that user's memories of the category."""
         with self._tx() as db:
-            db.execute("INSERT OR REPLACE INTO consent_revocations VALUES (?,?,?,?)",
+            db.execute(self.d.upsert("consent_revocations", ["workspace_id", "virtual_user_id",
+                                                            "category", "revoked_at"]),
                        (workspace, user, category, time.time()))
             ids = [r[0] for r in db.execute(
                 "SELECT id FROM memory_entities WHERE workspace_id = ? AND virtual_user_id = ? "
@@ -613,7 +693,7 @@ class MemoryStore:
 
     def aggregate(self, workspace: str, group_by: str = "category") -> list[dict]:
         col = {"category": "coalesce(e.consent_category, '')", "agent": "coalesce(e.agent_id, '')",
-               "day": "date(e.created_at, 'unixepoch')",
+               "day": self.d.day_expr("e.created_at"),
                "tier": "CASE WHEN e.virtual_user_id IS NOT NULL THEN 'user' WHEN e.agent_id IS "
                        "NOT NULL THEN 'agent' ELSE 'institutional' END",
                "type": "e.kind"}.get(group_by)
@@ -650,7 +730,8 @@ class MemoryStore:
     def embeddings(self, workspace: str | None = None, model: str | None = None):
         """(obs_id, workspace, vector) of active embedded observations -- index warm-up."""
         now = time.time()
-        sql = ("SELECT o.id, e.workspace_id, o.embedding FROM memory_observations o JOIN "
+        sql = (f"SELECT o.id, e.workspace_id, {self.d.vec_select()} FROM memory_observations o "
+               "JOIN "
                "memory_entities e ON e.id = o.entity_id WHERE e.forgotten = 0 AND " + _ACTIVE +
                " AND o.embedding IS NOT NULL")
         args = [now]
@@ -660,7 +741,7 @@ class MemoryStore:
         if model:
             sql += " AND o.embedding_model = ?"
             args.append(model)
-        return [(r[0], r[1], _f32(r[2])) for r in self._q(sql, args)]
+        return [(r[0], r[1], self._vec(r[2])) for r in self._q(sql, args)]
 
     def observation_ids_of(self, entity_ids: list[str]) -> list[str]:
         if not entity_ids:
@@ -815,3 +896,79 @@ class MemoryStore:
                         "count": n, "entries": [{"id": r[0], "content": r[1]} for r in rows]})
         return out
 
+
+    # ------------------------------------------------------------ tombstones / dims
+    def tombstone_gc(self, workspace: str, min_age_s: float = 30 * 86400,
+                     min_inactive: int = 20, keep_recent: int = 5) -> int:
+        """``RunTombstoneGC`` (``internal/memory/tombstone.go:76``): in entities whose
+        chain holds more than ``min_inactive`` inactive (superseded or expired)
+        observations older than ``min_age_s``, delete all but the ``keep_recent``
+        newest inactive ones.  Active observations are never touched."""
+        if not workspace:
+            raise ValueError("workspace_id is required")
+        if keep_recent >= min_inactive:
+            raise ValueError(f"keep_recent ({keep_recent}) must be less than min_inactive "
+                             f"({min_inactive})")
+        now = time.time()
+        inactive = "(o.superseded_by IS NOT NULL OR (o.valid_until IS NOT NULL AND " \
+                   "o.valid_until <= ?))"
+        with self._tx() as db:
+            ids = [r[0] for r in db.execute(
+                f"WITH chains AS (SELECT o.entity_id FROM memory_observations o JOIN "
+                f"memory_entities e ON e.id = o.entity_id WHERE e.workspace_id = ? AND "
+                f"{inactive} AND o.observed_at < ? GROUP BY o.entity_id HAVING count(*) > ?), "
+                f"ranked AS (SELECT o.id, row_number() OVER (PARTITION BY o.entity_id ORDER BY "
+                f"o.observed_at DESC) AS rn FROM memory_observations o JOIN chains c ON "
+                f"c.entity_id = o.entity_id JOIN memory_entities e ON e.id = o.entity_id AND "
+                f"e.workspace_id = ? WHERE {inactive}) SELECT id FROM ranked WHERE rn > ?",
+                (workspace, now, now - min_age_s, min_inactive, workspace, now,
+                 keep_recent)).fetchall()]
+            if ids:
+                ph = ",".join("?" * len(ids))
+                self._log_vectors(db, "delete", ids)
+                if self.d.uses_fts_table:
+                    db.execute(f"DELETE FROM memory_fts WHERE obs_id IN ({ph})", ids)
+                db.execute(f"DELETE FROM memory_observations WHERE id IN ({ph})", ids)
+        return len(ids)
+
+    def record_dim_consent(self, target_dim: int):
+        with self.lock:
+            self.db.execute(self.d.upsert(CONSENT_TABLE, ["id", "target_dim", "recorded_at"]),
+                            (1, int(target_dim), time.time()))
+
+    def ensure_embedding_dim(self, dim: int) -> dict:
+        """Reconcile the stored embedding dimension with the embedder's
+        (``EnsureEmbeddingSchema``).  Changing it while embeddings exist discards
+        them, so it needs one-shot consent for exactly ``dim``; the consent is
+        consumed and the re-embed worker backfills.  Postgres also reshapes the
+        ``vector(D)`` column (``MemoryPostgres.embedding_schema``)."""
+        cur = self._q("SELECT value FROM memory_meta WHERE key = 'embedding_dim'")
+        cur_dim = int(cur[0][0]) if cur else None
+        has = bool(self._q("SELECT 1 FROM memory_observations WHERE embedding IS NOT NULL "
+                           "LIMIT 1"))
+        consent = self._q(f"SELECT target_dim FROM {CONSENT_TABLE} WHERE id = 1")
+        consent_dim = int(consent[0][0]) if consent else None
+        if isinstance(self.d, MemoryPostgres) and not self.d.emulated:
+            stmts = self.d.embedding_schema(dim, cur_dim, has, consent_dim)
+        else:
+            stmts = MemoryPostgres.embedding_schema(dim, cur_dim, has, consent_dim)
+            stmts = [f"DELETE FROM {CONSENT_TABLE}"]  # SQLite blobs carry any dimension
+            if cur_dim not in (None, dim) and has:
+                stmts.insert(0, "UPDATE memory_observations SET embedding = NULL, "
+                                "embedding_model = NULL")
+        dropped = cur_dim not in (None, dim) and has
+        with self._tx() as db:
+            if dropped:
+                ids = [r[0] for r in db.execute("SELECT id FROM memory_observations WHERE "
+                                                "embedding IS NOT NULL").fetchall()]
+                for i in range(0, len(ids), 500):
+                    self._log_vectors(db, "delete", ids[i:i + 500])
+            for st in stmts:
+                db.execute(st)
+            db.execute(self.d.upsert("memory_meta", ["key", "value"]), ("embedding_dim",
+                                                                          str(dim)))
+        return {"from": cur_dim, "to": dim, "dropped_embeddings": dropped}
+
+
+__all__ = ["MemoryStore", "MultiTierRequest", "NotFound", "AccessTouchBatcher",
+           "EmbeddingDimConsentRequired", "MemorySQLite", "MemoryPostgres"]

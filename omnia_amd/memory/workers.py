@@ -147,4 +147,45 @@ class CompactionWorker:
             M.MEMORY_WORKER_RUNNING.labels("compaction").set(0)
 
 
-__all__ = ["ReembedWorker", "RetentionWorker", "CompactionWorker", "SCOPE_WORKSPACE"]
+class TombstoneWorker:
+    """Prunes superseded / expired observation chains (``tombstone_worker.go``):
+    every ``interval`` seconds, per workspace (a fixed list or the store's
+    discoverer), ``store.tombstone_gc(min_age, min_inactive, keep_recent)``."""
+
+    def __init__(self, svc, interval: float = 3600.0, workspaces=None,
+                 min_age_s: float = 30 * 86400, min_inactive: int = 20, keep_recent: int = 5):
+        if keep_recent >= min_inactive:
+            raise ValueError("keep_recent must be less than min_inactive")
+        self.svc, self.interval = svc, interval
+        self.workspaces = workspaces if workspaces is not None else \
+            svc.store.list_workspace_ids
+        self.min_age_s, self.min_inactive, self.keep_recent = min_age_s, min_inactive, keep_recent
+        self.deleted = 0
+
+    def run_once(self) -> int:
+        n = 0
+        wss = self.workspaces() if callable(self.workspaces) else self.workspaces
+        for ws in wss:
+            try:
+                n += self.svc.store.tombstone_gc(ws, self.min_age_s, self.min_inactive,
+                                                 self.keep_recent)
+            except Exception as e:  # noqa: BLE001 - one workspace never stops the pass
+                log.warning("tombstone gc failed for %s: %s", ws, e)
+        self.deleted += n
+        return n
+
+    async def run(self):
+        M.MEMORY_WORKER_RUNNING.labels("tombstone_gc").set(1)
+        try:
+            while True:
+                await asyncio.sleep(self.interval)
+                try:
+                    self.run_once()
+                except Exception as e:  # noqa: BLE001
+                    log.warning("tombstone pass failed: %s", e)
+        finally:
+            M.MEMORY_WORKER_RUNNING.labels("tombstone_gc").set(0)
+
+
+__all__ = ["ReembedWorker", "RetentionWorker", "CompactionWorker", "TombstoneWorker",
+           "SCOPE_WORKSPACE"]

@@ -46,6 +46,9 @@ POD_COLD_START = Histogram("omnia_pod_cold_start_seconds",
 SESSION_API_REQUESTS = Counter("omnia_session_api_requests_total",
                                "session-api HTTP requests by route and status",
                                ["method", "route", "status"], registry=REGISTRY)
+MEMORY_CACHE_LOOKUPS = Counter("omnia_memory_cache_lookups_total",
+                               "memory-api Redis read-cache lookups", ["op", "result"],
+                               registry=REGISTRY)
 MEMORY_WORKER_RUNNING = Gauge("omnia_memory_worker_running",
                               "1 while a memory-api background worker loop is alive",
                               ["name"], registry=REGISTRY)

@@ -28,7 +28,7 @@ import time
 import uuid
 
 from aiohttp import web
-from ..observability.logging import configure as configure_logging
+from ...observability.logging import configure as configure_logging
 
 log = logging.getLogger("omnia.privacy")
 
@@ -143,43 +143,29 @@ class PrivacyStore:
 
 
 class FanoutEraser:
-    """Executes a deletion request against the data-plane services."""
+    """Executes a deletion request: every service group's session-api and
+    memory-api through :class:`erasure.FanOutSubjectEraser`.  ``session_api`` /
+    ``memory_api``: the default group; ``groups``: more :class:`GroupTarget` s."""
 
     def __init__(self, store: PrivacyStore, session_api: str = "", memory_api: str = "",
-                 workspaces: list[str] | None = None):
+                 workspaces: list[str] | None = None, groups: list | None = None):
+        from .erasure import FanOutSubjectEraser, GroupTarget
+
         self.store = store
-        self.session_api = session_api.rstrip("/")
-        self.memory_api = memory_api.rstrip("/")
-        self.workspaces = workspaces or []
+        tg = list(groups or [])
+        if session_api or memory_api:
+            tg.insert(0, GroupTarget("default", session_api.rstrip("/"), memory_api.rstrip("/")))
+        self.fanout = FanOutSubjectEraser(tg, workspaces or [])
 
     async def run(self, rid: str):
-        import aiohttp
-
         r = self.store.get_request(rid)
         r.update(status="in_progress", startedAt=time.time())
         self.store.put_request(r)
-        user, errors, deleted = r["virtualUserId"], [], 0
-        async with aiohttp.ClientSession() as s:
-            if self.session_api and r.get("scope", "all") in ("all", "sessions"):
-                try:
-                    async with s.post(f"{self.session_api}/api/v1/privacy/sessions/"
-                                      f"delete-by-user", json={"virtual_user_id": user}) as d:
-                        body = await d.json()
-                        if d.status >= 300:
-                            errors.append(f"session-api: HTTP {d.status}")
-                        deleted += int(body.get("sessions_deleted", 0))
-                        errors += body.get("errors") or []
-                except Exception as e:  # noqa: BLE001
-                    errors.append(f"session-api: {e}")
-            if self.memory_api and r.get("scope", "all") in ("all", "memories"):
-                for ws in ([r["workspace"]] if r.get("workspace") else self.workspaces):
-                    try:
-                        async with s.delete(f"{self.memory_api}/api/v1/memories", params={
-                                "workspace": ws, "virtual_user_id": user}) as d:
-                            if d.status >= 300:
-                                errors.append(f"memory {ws}: HTTP {d.status}")
-                    except Exception as e:  # noqa: BLE001
-                        errors.append(f"memory-api: {e}")
+        user = r["virtualUserId"]
+        try:
+            deleted, errors = await self.fanout.erase_subject(r)
+        except Exception as e:  # noqa: BLE001
+            deleted, errors = 0, [str(e)]
         r.update(status="completed" if not errors else "failed", completedAt=time.time(),
                  sessionsDeleted=deleted, errors=errors)
         self.store.put_request(r)
@@ -189,8 +175,16 @@ class FanoutEraser:
 
 
 def build_app(store: PrivacyStore, eraser: FanoutEraser | None = None,
-              memory_api: str = "") -> web.Application:
+              memory_api: str = "", notifier=None) -> web.Application:
+    """``notifier``: consent-revocation notifier (``outbox.MemoryAPINotifier``);
+    when given, revocations go through the transactional outbox.  ``memory_api``
+    alone builds a single-target notifier."""
+    from .outbox import MemoryAPINotifier, Outbox, deliver
+
     eraser = eraser or FanoutEraser(store)
+    if notifier is None and memory_api:
+        notifier = MemoryAPINotifier([memory_api])
+    outbox = Outbox(store)
     tasks: set = set()
 
     def bad(msg, code=400):
@@ -199,22 +193,18 @@ def build_app(store: PrivacyStore, eraser: FanoutEraser | None = None,
     async def set_consent(request):
         d = await request.json()
         user = request.match_info["userID"]
+        revs = d.get("revocations") or []
         try:
-            store.set_consent(user, d.get("grants") or [], d.get("revocations") or [])
+            store.set_consent(user, d.get("grants") or [], [])
+            bad_revs = [c for c in revs if c not in CATEGORIES]
+            if bad_revs:
+                raise ValueError(f"unknown consent categories: {bad_revs}")
         except ValueError as e:
             return bad(str(e))
-        if memory_api and d.get("revocations"):
-            import aiohttp
-
-            async with aiohttp.ClientSession() as s:
-                for c in d["revocations"]:
-                    try:
-                        await s.post(f"{memory_api.rstrip('/')}/api/v1/memories/consent-events",
-                                     json={"workspace_id": d.get("workspace", ""),
-                                           "virtual_user_id": user, "category": c,
-                                           "action": "revoked"})
-                    except Exception as e:  # noqa: BLE001
-                        log.warning("consent fan-out failed: %s", e)
+        for c in revs:  # revocation + outbox row in one transaction, then notify
+            oid = outbox.revoke_with_outbox(user, c)
+            if oid is not None and notifier is not None:
+                await deliver(outbox, notifier, oid, user, c)
         store.ingest([{"source": "privacy-api", "type": "consent.updated", "userId": user,
                        "grants": d.get("grants") or [], "revocations": d.get("revocations")
                        or []}])
@@ -278,6 +268,7 @@ def build_app(store: PrivacyStore, eraser: FanoutEraser | None = None,
         return web.json_response({"status": "ok"})
 
     app = web.Application()
+    app["outbox"] = outbox
     r = app.router
     r.add_put("/api/v1/privacy/preferences/{userID}/consent", set_consent)
     r.add_get("/api/v1/privacy/preferences/{userID}/consent", get_consent)
@@ -302,12 +293,37 @@ def main(argv=None):
     ap.add_argument("--session-api", default="")
     ap.add_argument("--memory-api", default="")
     ap.add_argument("--workspaces", default="")
+    ap.add_argument("--group", action="append", default=[],
+                    help="extra service group NAME=SESSION_URL,MEMORY_URL (repeatable)")
+    ap.add_argument("--outbox-replay-interval", type=float, default=30.0)
+    ap.add_argument("--operator-url", default="",
+                    help="watch SessionPrivacyPolicies through this API server")
     a = ap.parse_args(argv)
+    from .erasure import GroupTarget
+    from .outbox import MemoryAPINotifier, Outbox, OutboxReplayWorker
+
     store = PrivacyStore(a.db)
+    groups = []
+    for g in a.group:
+        name, _, urls = g.partition("=")
+        su, _, mu = urls.partition(",")
+        groups.append(GroupTarget(name, su, mu))
     er = FanoutEraser(store, a.session_api, a.memory_api,
-                      [w for w in a.workspaces.split(",") if w])
+                      [w for w in a.workspaces.split(",") if w], groups)
+    notifier = MemoryAPINotifier([a.memory_api] + [g.memory_url for g in groups])
+    app = build_app(store, er, notifier=notifier)
+    replay = OutboxReplayWorker(Outbox(store), notifier, a.outbox_replay_interval)
+
+    async def start(app):
+        app["replay"] = asyncio.create_task(replay.run())
+
+    async def stop(app):
+        app["replay"].cancel()
+
+    app.on_startup.append(start)
+    app.on_cleanup.append(stop)
     configure_logging()
-    web.run_app(build_app(store, er, a.memory_api), port=a.port)
+    web.run_app(app, port=a.port)
 
 
 if __name__ == "__main__":

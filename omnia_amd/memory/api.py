@@ -447,14 +447,21 @@ def build_app(svc: MemoryService, enterprise: bool = False, chunk_size: int = 20
 
     async def consent_event(request):
         d = await _body(request)
-        ws, user, cat = d.get("workspace_id"), d.get("virtual_user_id") or d.get("user_id"), \
-            d.get("category")
-        if not (ws and user and cat):
-            return _err(400, "workspace_id, virtual_user_id and category are required")
+        # the privacy-api notifier's body is {"userId", "category"} with ?workspace=
+        ws = d.get("workspace_id") or request.query.get("workspace") or ""
+        user = d.get("virtual_user_id") or d.get("user_id") or d.get("userId")
+        cat = d.get("category")
+        if not (user and cat):
+            return _err(400, "virtual_user_id and category are required")
         if (d.get("action") or "revoked") == "revoked":
-            obs = svc.store.revoke_consent(ws, user, cat)
+            obs = []
+            for w in ([ws] if ws else svc.store.list_workspace_ids()):
+                obs += svc.store.revoke_consent(w, user, cat)
+                await svc._invalidate(w)
             svc._drop_vectors(obs)
             return web.json_response({"deleted_observations": len(obs)})
+        if not ws:
+            return _err(400, "workspace_id is required to re-grant consent")
         with svc.store.lock:
             svc.store.db.execute("DELETE FROM consent_revocations WHERE workspace_id = ? AND "
                                  "virtual_user_id = ? AND category = ?", (ws, user, cat))
@@ -583,6 +590,10 @@ def main(argv=None):
                     help="temporal-summarisation worker period (e.g. 6h); empty disables")
     ap.add_argument("--compaction-age", default=os.environ.get("COMPACTION_AGE", ""),
                     help="age threshold of compaction candidates (e.g. 720h)")
+    ap.add_argument("--privacy-operator-url", default=os.environ.get("OMNIA_OPERATOR_URL", ""),
+                    help="EE: redact writes under the SessionPrivacyPolicy watched here")
+    ap.add_argument("--privacy-namespace", default=os.environ.get("OMNIA_NAMESPACE", ""))
+    ap.add_argument("--privacy-workspace", default=os.environ.get("OMNIA_WORKSPACE", ""))
     ap.add_argument("--postgres-dsn", default=os.environ.get("MEMORY_POSTGRES_DSN", ""),
                     help="Postgres + pgvector store (needs a DB-API driver); default SQLite --db")
     ap.add_argument("--redis-cache", default=os.environ.get("MEMORY_CACHE_REDIS_URL", ""),
@@ -635,6 +646,17 @@ def main(argv=None):
 
         svc.cache = CachedStore(store, RedisClient(a.redis_cache), a.cache_ttl)
     app = build_app(svc, a.enterprise, a.ingest_chunk_size, a.ingest_chunk_overlap)
+    watcher = None
+    if a.privacy_operator_url:
+        from ..ee.privacy.policy import HTTPSource, PolicyWatcher, memory_privacy_middleware
+
+        watcher = PolicyWatcher(HTTPSource(a.privacy_operator_url), a.privacy_workspace,
+                                a.privacy_namespace)
+        app.middlewares.append(memory_privacy_middleware(watcher, a.privacy_namespace))
+    if a.enterprise and emb is not None:
+        from ..ee.privacy.classify import EmbeddingClassifier
+
+        svc.embedding_classifier = EmbeddingClassifier(emb)
     tombstone = None
     if a.tombstone_interval:
         from ..utils.durations import parse_duration
@@ -667,6 +689,14 @@ def main(argv=None):
     async def start_workers(app):
         app["workers"] = [asyncio.create_task(ReembedWorker(svc, a.reembed_interval).run()),
                           asyncio.create_task(RetentionWorker(svc, policy=policy).run())]
+        if watcher is not None:
+            app["workers"].append(asyncio.create_task(watcher.run()))
+        ec = getattr(svc, "embedding_classifier", None)
+        if ec is not None:
+            try:
+                await ec.prewarm()  # exemplar centroids on the in-node embedder
+            except Exception as e:  # noqa: BLE001 - rules-only classification then
+                log.warning("embedding classifier prewarm failed: %s", e)
         if compaction is not None:
             app["workers"].append(asyncio.create_task(compaction.run()))
         if tombstone is not None:

@@ -167,11 +167,35 @@ class MemoryService:
             M.MEMORY_CLASSIFY_CATEGORY.labels(category=best, source="regex").inc()
         return best
 
+    async def classify_async(self, mem: Memory) -> str | None:
+        """Rules, then (EE, when ``self.embedding_classifier`` is prewarmed) the
+        embedding classifier for content the rules do not place
+        (``ee/pkg/privacy/classify/embedding.go``)."""
+        best = self.classify(mem)
+        emb = getattr(self, "embedding_classifier", None)
+        claimed = (mem.metadata or {}).get(META_CONSENT_CATEGORY)
+        if not (self.enterprise and self.classify_pii) or emb is None or \
+                emb.centroids is None or (best and best != claimed):
+            return best
+        try:
+            cat, _ = await emb.classify(mem.content)
+        except Exception as e:  # noqa: BLE001
+            M.MEMORY_EMBED_ERRORS.inc()
+            log.debug("embedding classification failed: %s", e)
+            return best
+        if cat and _SEVERITY.get(cat, 0) > _SEVERITY.get(best or "", 0):
+            if best != cat:
+                M.MEMORY_CLASSIFY_OVERRIDES.labels(**{"from": best or "", "to": cat,
+                                                      "source": "embedding"}).inc()
+            M.MEMORY_CLASSIFY_CATEGORY.labels(category=cat, source="embedding").inc()
+            return cat
+        return best
+
     # ------------------------------------------------------------ API
     async def save(self, mem: Memory, require_user: bool = True) -> dict:
         mem.scope = normalize_scope(mem.scope)
         ws = mem.scope.get(SCOPE_WORKSPACE, "")
-        cat = self.classify(mem)
+        cat = await self.classify_async(mem)
         if cat:
             mem.metadata = {**(mem.metadata or {}), META_CONSENT_CATEGORY: cat}
             if self.store.is_revoked(ws, mem.scope.get(SCOPE_USER, ""), cat):

@@ -46,6 +46,12 @@ POD_COLD_START = Histogram("omnia_pod_cold_start_seconds",
 SESSION_API_REQUESTS = Counter("omnia_session_api_requests_total",
                                "session-api HTTP requests by route and status",
                                ["method", "route", "status"], registry=REGISTRY)
+SESSION_API_WRITES_DROPPED = Counter("omnia_session_api_writes_dropped_total",
+                                     "session-api writes dropped by the privacy middleware",
+                                     ["reason"], registry=REGISTRY)
+PRIVACY_OUTBOX_STUCK = Gauge("omnia_privacy_outbox_stuck",
+                             "consent-revocation outbox rows undelivered past the stuck age",
+                             registry=REGISTRY)
 MEMORY_CACHE_LOOKUPS = Counter("omnia_memory_cache_lookups_total",
                                "memory-api Redis read-cache lookups", ["op", "result"],
                                registry=REGISTRY)

@@ -53,9 +53,34 @@ class MemoryPublisher:
         self.events.append(ev)
 
 
+def session_resolver(svc: TieredSessionService, cache_size: int = 10000):
+    """session id -> (namespace, agent) for the privacy middleware (bounded cache,
+    ``session_cache.go``)."""
+    cache: dict[str, tuple[str, str]] = {}
+
+    def resolve(sid: str):
+        hit = cache.get(sid)
+        if hit is not None:
+            return hit
+        try:
+            v = svc.get(sid, with_messages=False)
+        except Exception:  # noqa: BLE001 - unknown / unreadable: no policy applies
+            return None
+        if v is None:
+            return None
+        s = v[0]
+        if len(cache) >= cache_size:
+            cache.pop(next(iter(cache)))
+        cache[sid] = (s.namespace, s.agent_name)
+        return cache[sid]
+
+    return resolve
+
+
 def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400.0,
               tokens: dict | None = None, allowed_namespaces: set | None = None,
-              redactor=None, optout=None, audit_logger=None) -> web.Application:
+              redactor=None, optout=None, audit_logger=None, media_deleter=None,
+              privacy_middleware=None) -> web.Application:
     """``audit_logger`` (EE, :class:`omnia_amd.ee.audit.AuditLogger`): record
     session created/accessed/searched/deleted events and serve them at
     ``/api/v1/audit/sessions`` (reference session-api audit wiring)."""
@@ -103,7 +128,8 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
                 return web.json_response({"error": "forbidden"}, status=403)
         return await handler(request)
 
-    app = web.Application(middlewares=[count, guard], client_max_size=32 * 2**20)
+    mws = [count, guard] + ([privacy_middleware] if privacy_middleware is not None else [])
+    app = web.Application(middlewares=mws, client_max_size=32 * 2**20)
     r = app.router
 
     def nf(sid):
@@ -277,13 +303,31 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         return web.json_response({"deleted": n})
 
     async def delete_by_user(request):
+        """Session-tier DSAR (``session_erase_handler.go``): the user's sessions,
+        optionally one workspace / a created-at range, and their media."""
+        from ..ee.privacy.erasure import EraseScope, SessionTierEraser
+
         body = await request.json()
         uid = body.get("virtual_user_id", "")
         if not uid:
             return web.json_response({"error": "virtual_user_id required"}, status=400)
-        rows = svc.warm.list_sessions(user=uid, limit=100000)
-        n = sum(1 for s in rows if svc.delete(s.id))
-        return web.json_response({"sessions_deleted": n, "errors": []})
+
+        def ts(v):
+            if v in (None, ""):
+                return None
+            if isinstance(v, (int, float)):
+                return float(v)
+            import datetime as dt
+
+            return dt.datetime.fromisoformat(str(v).replace("Z", "+00:00")).timestamp()
+
+        try:
+            scope = EraseScope(uid, body.get("workspace") or "", ts(body.get("date_from")),
+                               ts(body.get("date_to")))
+        except ValueError as e:
+            return web.json_response({"error": f"bad date: {e}"}, status=400)
+        res = await SessionTierEraser(svc, media_deleter).erase(scope)
+        return web.json_response(res)
 
     async def metrics(_):
         return web.Response(body=M.exposition(), content_type="text/plain")
@@ -373,6 +417,15 @@ def main(argv=None):
     ap.add_argument("--encryption-key-file", default=os.environ.get("ENCRYPTION_KEY_FILE", ""),
                     help="local provider: versioned KEK ring (rotated by the key-rotation "
                          "controller)")
+    ap.add_argument("--media-root", default=os.environ.get("OMNIA_MEDIA_ROOT", ""),
+                    help="local media store root: DSAR erasure deletes each session's media")
+    ap.add_argument("--privacy-operator-url", default=os.environ.get("OMNIA_OPERATOR_URL", ""),
+                    help="EE: watch SessionPrivacyPolicies through this API server and "
+                         "enforce them on writes")
+    ap.add_argument("--privacy-namespace", default=os.environ.get("OMNIA_NAMESPACE", ""))
+    ap.add_argument("--privacy-workspace", default=os.environ.get("OMNIA_WORKSPACE", ""))
+    ap.add_argument("--privacy-api-url", default=os.environ.get("OMNIA_PRIVACY_API_URL", ""),
+                    help="EE: opt-out lookups for the privacy middleware")
     ap.add_argument("--tokens-file", default=os.environ.get("OMNIA_SESSION_API_TOKENS_FILE", ""),
                     help="JSON {bearer token: service-account identity}; enables auth on the "
                          "REST and both OTLP listeners")
@@ -428,7 +481,30 @@ def main(argv=None):
 
         audit_logger = AuditLogger(a.audit_db, retention_days=a.audit_retention_days)
         app_kw["audit_logger"] = audit_logger
+    if a.media_root:
+        from ..ee.privacy.erasure import LocalMediaDeleter
+
+        app_kw["media_deleter"] = LocalMediaDeleter(a.media_root)
+    watcher = None
+    if a.privacy_operator_url:
+        from ..ee.privacy.policy import (HTTPSource, PolicyWatcher, PrivacyPrefsClient,
+                                         session_privacy_middleware)
+
+        watcher = PolicyWatcher(HTTPSource(a.privacy_operator_url), a.privacy_workspace,
+                                a.privacy_namespace)
+        app_kw["privacy_middleware"] = session_privacy_middleware(
+            watcher, session_resolver(svc),
+            PrivacyPrefsClient(a.privacy_api_url) if a.privacy_api_url else None)
     app = build_app(svc, **app_kw)
+    if watcher is not None:
+        async def watch(_app):
+            import asyncio
+
+            task = asyncio.create_task(watcher.run())
+            yield
+            task.cancel()
+
+        app.cleanup_ctx.append(watch)
     if audit_logger is not None and a.audit_hub:
         fw = Forwarder(audit_logger, a.audit_hub)
 

@@ -135,6 +135,7 @@ class LocalLauncher:
         self.activators: dict[tuple, object] = {}  # (ns, name) -> Activator
         self.cold_start_s: dict[tuple, float] = {}
         self._dep_wait: dict[tuple, float] = {}  # key -> first deferral (dependencies)
+        self._cron_seen: dict[tuple, float] = {}  # CronJob first seen (schedule origin)
 
     async def _keda_samples(self, ns: str, name: str) -> list:
         """Metric samples of one scale target: every ready replica's facade
@@ -215,6 +216,78 @@ class LocalLauncher:
         fac = build_facade(_env(cs["facade"]), client)
         pod.port = await fac.start("127.0.0.1", 0)
         pod.facade = fac
+
+    # ------------------------------------------------------------ CronJobs
+    def _sync_cronjobs(self, now: float | None = None) -> list[str]:
+        """batch/v1 CronJobs (the chart's session compaction, scheduled
+        maintenance): at each schedule time a Job is created from
+        ``jobTemplate`` (owned by the CronJob, named ``<cron>-<minute>``), which
+        ``_sync_jobs`` then runs.  ``concurrencyPolicy: Forbid`` skips a run while
+        the previous Job is active, ``Replace`` deletes it first; ``suspend``
+        stops scheduling; missed runs are not back-filled (one run per sync at
+        most, as with ``startingDeadlineSeconds`` unset after a long outage);
+        the ``successfulJobsHistoryLimit`` newest finished Jobs are kept.
+        ``status.lastScheduleTime`` / ``active`` are written back."""
+        import time
+
+        from ..utils.cron import next_fire
+        from .apistore import owner_ref
+
+        now = time.time() if now is None else now
+        made = []
+        for cj in self.store.list("CronJob"):
+            spec, md = cj.get("spec") or {}, cj["metadata"]
+            ns, name = md["namespace"], md["name"]
+            st = dict(cj.get("status") or {})
+            owned = [j for j in self.store.list("Job", ns)
+                     if any(o.get("uid") == md.get("uid") for o in
+                            j["metadata"].get("ownerReferences") or [])]
+            active = [j for j in owned if not any(
+                c.get("type") in ("Complete", "Failed") and c.get("status") == "True"
+                for c in (j.get("status") or {}).get("conditions") or [])]
+            last = float(st.get("lastScheduleTime") or md.get("creationTimestampUnix") or 0) \
+                or self._cron_seen.setdefault((ns, name), now)
+            try:
+                due = next_fire(spec.get("schedule", ""), last)
+            except ValueError:
+                continue
+            if not spec.get("suspend") and due <= now:
+                policy = spec.get("concurrencyPolicy", "Allow")
+                if active and policy == "Forbid":
+                    st["lastScheduleTime"] = now  # this run is skipped, not queued
+                else:
+                    if active and policy == "Replace":
+                        for j in active:
+                            self.store.delete("Job", j["metadata"]["name"], ns)
+                    jname = f"{name}-{int(due // 60)}"
+                    tmpl = spec.get("jobTemplate") or {}
+                    if self.store.try_get("Job", jname, ns) is None:
+                        self.store.apply({
+                            "apiVersion": "batch/v1", "kind": "Job",
+                            "metadata": {"name": jname, "namespace": ns,
+                                         "labels": dict((tmpl.get("metadata") or {}).get(
+                                             "labels") or {}),
+                                         "ownerReferences": [owner_ref(cj)]},
+                            "spec": dict(tmpl.get("spec") or {})})
+                        made.append(jname)
+                    st["lastScheduleTime"] = now
+            owned = [j for j in self.store.list("Job", ns)
+                     if any(o.get("uid") == md.get("uid") for o in
+                            j["metadata"].get("ownerReferences") or [])]
+            active = [j for j in owned if not any(
+                c.get("type") in ("Complete", "Failed") and c.get("status") == "True"
+                for c in (j.get("status") or {}).get("conditions") or [])]
+            keep = int(spec.get("successfulJobsHistoryLimit", 3))
+            done = sorted((j for j in owned if j not in active),
+                          key=lambda j: j["metadata"]["name"])
+            for j in done[:max(0, len(done) - keep)]:
+                self.store.delete("Job", j["metadata"]["name"], ns)
+            st["active"] = [{"name": j["metadata"]["name"]} for j in active]
+            if st != (cj.get("status") or {}):
+                cj["status"] = st
+                cj["metadata"].pop("resourceVersion", None)
+                self.store.update_status(cj)
+        return made
 
     # ------------------------------------------------------------ batch Jobs
     async def _sync_jobs(self):
@@ -504,6 +577,7 @@ class LocalLauncher:
         live = set()
         if self.mode == "process":
             await self._sync_services()
+            self._sync_cronjobs()
             await self._sync_jobs()
             await self._sync_activators()
         for d in deps:

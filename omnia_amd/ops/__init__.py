@@ -265,8 +265,8 @@ def wgemm_wide(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, wt:
 
 def tgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, bn: int = 128,
           wnt: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Full-batch (M <= 256) tile decode GEMM (``csrc/tgemm.hip``): every block
-    owns all M rows x ``bn`` weight rows, both operands LDS-DMA staged through an
+    """Tile GEMM (``csrc/tgemm.hip``): decode batches (M <= 256, one block owns all
+    rows x ``bn`` weight rows) and prefill chunks (256-row tiles), both operands LDS-DMA staged through an
     NS-deep ring with counted waits.  Same modes / outputs as :func:`wgemm`
     (mode 1 = fused SwiGLU needs ``splits == 1``)."""
     M, K = x.shape

@@ -1,6 +1,8 @@
 // Full-batch tile GEMM for decode projections on gfx950:
-//   out = x[M, K] . W[N, K]^T   with 129 <= M <= 256 (one continuous-batching
-// decode step), bf16 operands, fp32 MFMA accumulate.  SURVEY §2.4 K3/K8/K9/K10.
+//   out = x[M, K] . W[N, K]^T   for 129 <= M <= 256 (one continuous-batching
+// decode step) and, tiled 256 rows at a time, any larger M (prefill chunks:
+// MODE 1 then fuses SwiGLU into the prefill gate_up GEMM); bf16 operands, fp32
+// MFMA accumulate.  SURVEY §2.4 K3/K8/K9/K10.
 //
 // At M = 256 a Llama-3-8B projection sits on the MI355X ridge (256 FLOP per
 // weight byte vs ~400 FLOP/B of dense bf16 peak over achievable HBM), so the
@@ -83,8 +85,21 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
 
   // mode 1 tiles hold BN/2 output features (gate + up rows of W)
   const int ntiles = MODE == 1 ? N / (BN / 2) : N / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
+  // M > 256 (prefill): 256-row tiles, grouped GM at a time per (split, tile) so
+  // consecutive blocks -- one XCD after the remap -- share the W tile in L2
+  const int per_m = ntiles * S, mtiles = (M + 255) >> 8;
+  int mt = 0, bid = bid0;
+  if (mtiles > 1) {
+    constexpr int GM = 4;
+    const int g = bid0 / (GM * per_m), gm0 = g * GM;
+    const int gsz = mtiles - gm0 < GM ? mtiles - gm0 : GM;
+    const int idx = bid0 - gm0 * per_m;
+    mt = gm0 + idx % gsz;
+    bid = idx / gsz;
+  }
   const int split = bid / ntiles, tile = bid - split * ntiles;
+  const int m0 = mt << 8, Mt = M - m0 < 256 ? M - m0 : 256;  // rows of this tile
   const int nk = K >> 6;
   const int kb = split * nk / S, ke = (split + 1) * nk / S;
   const int n_loc = ke - kb;
@@ -100,8 +115,8 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
 #pragma unroll
   for (int i = 0; i < A_IN; ++i) {
     const int row = 8 * (w * A_IN + i) + lr;
-    const int r = row < M ? row : M - 1;  // rows past the batch: clamped copies, never stored
-    a_src[i] = X + (int64_t)r * K + (int64_t)kb * 64 + lc * 8;
+    const int r = row < Mt ? row : Mt - 1;  // rows past the batch: clamped copies, never stored
+    a_src[i] = X + (int64_t)(m0 + r) * K + (int64_t)kb * 64 + lc * 8;
   }
   const bf16_t* b_src[B_IN];
 #pragma unroll
@@ -194,38 +209,40 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
 
   // ---- epilogue: lane holds rows wm*WTM + 16i + 4fq + r, tile columns wn*WTN + 16j + fr
   if (MODE == 2) {
-    float* o = reinterpret_cast<float*>(out) + (int64_t)split * M * N + (int64_t)tile * BN +
-               wn * WTN + fr;
+    float* o = reinterpret_cast<float*>(out) + (int64_t)split * M * N + (int64_t)m0 * N +
+               (int64_t)tile * BN + wn * WTN + fr;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wm * WTM + 16 * i + 4 * fq + r;
-        if (row < M) {
+        if (row < Mt) {
 #pragma unroll
           for (int j = 0; j < FN; ++j) o[(int64_t)row * N + 16 * j] = acc[i][j][r];
         }
       }
   } else if (MODE == 0) {
-    bf16_t* o = reinterpret_cast<bf16_t*>(out) + (int64_t)tile * BN + wn * WTN + fr;
+    bf16_t* o = reinterpret_cast<bf16_t*>(out) + (int64_t)m0 * ldo + (int64_t)tile * BN +
+                wn * WTN + fr;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wm * WTM + 16 * i + 4 * fq + r;
-        if (row < M) {
+        if (row < Mt) {
 #pragma unroll
           for (int j = 0; j < FN; ++j) o[(int64_t)row * ldo + 16 * j] = f2bf(acc[i][j][r]);
         }
       }
   } else {
-    bf16_t* o = reinterpret_cast<bf16_t*>(out) + (int64_t)tile * (BN / 2) + wn * (WTN / 2) + fr;
+    bf16_t* o = reinterpret_cast<bf16_t*>(out) + (int64_t)m0 * ldo + (int64_t)tile * (BN / 2) +
+                wn * (WTN / 2) + fr;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wm * WTM + 16 * i + 4 * fq + r;
-        if (row < M) {
+        if (row < Mt) {
 #pragma unroll
           for (int j = 0; j < FN / 2; ++j)
             o[(int64_t)row * ldo + 16 * j] = f2bf(silu(acc[i][j][r]) * acc[i][j + FN / 2][r]);
@@ -238,7 +255,7 @@ template <int BN, int MODE>
 int launch_bn(void* out, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int ldo,
               int wnt, hipStream_t s) {
   const int ntiles = MODE == 1 ? N / (BN / 2) : N / BN;
-  const dim3 grid(ntiles * S), block(512);
+  const dim3 grid(ntiles * S * ((M + 255) / 256)), block(512);
   if (wnt)
     tgemm_kernel<BN, MODE, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
   else
@@ -265,7 +282,7 @@ extern "C" {
 int omnia_tgemm(int mode, void* out, const void* X, const void* W, int M, int N, int K, int S,
                 int bn, int wnt, int ldo, hipStream_t s) {
   if (mode < 0 || mode > 2) return -1;
-  if (M < 1 || M > 256) return -2;
+  if (M < 1 || (int64_t)((M + 255) / 256) * S * (N / 64) > (1 << 30)) return -2;
   if (K % 64 || K <= 0) return -3;
   if (S < 1 || S > 16 || S > K / 64) return -4;
   if (bn != 64 && bn != 128 && bn != 256) return -5;

@@ -8,6 +8,10 @@ mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_config5.py tests/test_keda.py -m gpu -v -s --timeout 360 --timeout-method thread 2>&1 | tee $O/cfg45_gpu.log
 crc=$?; echo "cfg4/5 gpu rc=$crc"
 [ $crc -eq 0 ] || [ $crc -eq 1 ] || exit $crc
+timeout -k 10 300 python -u -m pytest tests/test_tgemm_gpu.py -q --timeout 120 --timeout-method thread > $O/tgemm_test.log 2>&1
+echo "tgemm test rc=$?"; tail -2 $O/tgemm_test.log
+timeout -k 10 400 python -u scripts/prefill_sweep.py --out $O/prefill_sweep.json 2>&1 | tee $O/prefill_sweep.log
+echo "prefill sweep rc=$?"
 for cfg in "gate_up 256 128 1 0" "qkv 256 128 4 0" "down 256 128 8 0"; do
   tag=$(echo $cfg | tr ' ' '_')
   timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d /tmp/pmc_$tag -o a -- python3 scripts/tgemm_pmc.py $cfg > $O/pmc_a_$tag.log 2>&1

@@ -81,3 +81,21 @@ def test_rejects_bad_shapes_before_launch():
         ops.tgemm(2, x, w, 9, 128, 0)  # more splits than 64-k steps
     with pytest.raises(RuntimeError, match="tgemm"):
         ops.tgemm(0, x, w, 1, 96, 0)  # unsupported block width
+
+
+@pytest.mark.parametrize("M,mode,bn,S", [(257, 0, 128, 1), (600, 0, 256, 1), (1024, 1, 256, 1),
+                                         (777, 1, 128, 1), (1000, 2, 128, 3), (4096, 1, 256, 1)])
+def test_prefill_row_tiles_match_fp32(M, mode, bn, S):
+    """M > 256: 256-row tiles in grouped order (the prefill path), ragged last tile."""
+    N = 512
+    x, w = _mk(M, 2 * N if mode == 1 else N, 1024, seed=M + mode)
+    out = ops.tgemm(mode, x, w, S, bn, 0)
+    full = x.float() @ w.float().t()
+    if mode == 1:
+        torch.testing.assert_close(out.float(), ref.silu_mul(full).float(), rtol=3e-2,
+                                   atol=3e-2)
+    elif mode == 2:
+        assert out.shape == (S, M, N)
+        torch.testing.assert_close(out.sum(0), full, rtol=1e-3, atol=3e-3)
+    else:
+        torch.testing.assert_close(out.float(), full, rtol=2e-2, atol=2e-2)

@@ -124,6 +124,7 @@ class WSDriver:
         self.rng = random.Random(1234 + rank)
         self.pod = None
         self._ready = []  # pre-opened sessions for the next wave (one per virtual user)
+        self._next_contents = None  # the next wave's messages, written during this one
         self.overhead = self._template_overhead()
         if a.prompt_len <= self.overhead:
             raise SystemExit(f"--prompt-len {a.prompt_len} must exceed the chat-template "
@@ -179,7 +180,10 @@ class WSDriver:
     def _content(self) -> str:
         n = self.a.prompt_len - self.overhead
         # printable ASCII, one byte token each; fresh per turn (no cross-turn prefix reuse)
-        return "".join(self.rng.choice("abcdefghijklmnopqrstuvwxyz ,.") for _ in range(n))
+        return "".join(self.rng.choices("abcdefghijklmnopqrstuvwxyz ,.", k=n))
+
+    def _contents(self, n: int) -> list[str]:
+        return [self._content() for _ in range(n)]
 
     async def _connect(self):
         from omnia_amd.ee.arena.fleet import FleetSession
@@ -203,12 +207,19 @@ class WSDriver:
                 int(u.get("input_tokens", 0)), r["chunk_times_s"])
 
     async def _wave(self):
+        """One closed-loop wave.  The virtual users' NEXT messages are written on
+        a helper thread while this wave runs (as real users type while the agent
+        answers), so no client-side text generation sits between two waves."""
         ready, self._ready = self._ready, []
         n = self.a.concurrency
-        return await asyncio.gather(*(self._turn(self._content(),
-                                                 ready[i] if i < len(ready) else None,
-                                                 reconnect=True)
-                                      for i in range(n)))
+        contents = self._next_contents or self._contents(n)
+        nxt = asyncio.get_running_loop().run_in_executor(None, self._contents, n)
+        res = await asyncio.gather(*(self._turn(contents[i],
+                                                ready[i] if i < len(ready) else None,
+                                                reconnect=True)
+                                     for i in range(n)))
+        self._next_contents = await nxt
+        return res
 
     def wave(self, step: int):
         if self.pod is None:

@@ -196,12 +196,15 @@ class WSDriver:
         turn overlaps the rest of this wave instead of stalling the next wave's
         start (turn timing starts at the ``message`` frame either way)."""
         fs = fs or await self._connect()
+        # the user's NEXT session opens while this turn streams, so no WebSocket
+        # handshake (facade session setup) sits at the wave boundary
+        nxt = asyncio.ensure_future(self._connect()) if reconnect else None
         try:
             r = await fs.turn(content)
         finally:
             await fs.__aexit__(None, None, None)
-        if reconnect:
-            self._ready.append(await self._connect())
+        if nxt is not None:
+            self._ready.append(await nxt)
         u = r["usage"] or {}
         return (r["ttft_ms"] / 1e3, r["latency_ms"] / 1e3, int(u.get("output_tokens", 0)),
                 int(u.get("input_tokens", 0)), r["chunk_times_s"])

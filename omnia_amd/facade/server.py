@@ -81,13 +81,13 @@ class _WSWriter(Writer):
         async with self.lock:
             if not self.ws.closed:
                 await self.ws.send_str(json.dumps(msg, separators=(",", ":")))
-                M.MESSAGES_SENT.labels(*self.labels).inc()
+                M.child(M.MESSAGES_SENT, *self.labels).inc()
 
     async def write_bytes(self, data: bytes) -> None:
         async with self.lock:
             if not self.ws.closed:
                 await self.ws.send_bytes(data)
-                M.MESSAGES_SENT.labels(*self.labels).inc()
+                M.child(M.MESSAGES_SENT, *self.labels).inc()
 
 
 class FacadeServer:
@@ -199,8 +199,8 @@ class FacadeServer:
                                    max_msg_size=self.cfg.max_message_bytes)
         await ws.prepare(request)
         self.connections += 1
-        M.CONNECTIONS_ACTIVE.labels(*self.labels).inc()
-        M.CONNECTIONS_TOTAL.labels(*self.labels).inc()
+        M.child(M.CONNECTIONS_ACTIVE, *self.labels).inc()
+        M.child(M.CONNECTIONS_TOTAL, *self.labels).inc()
         binary = request.query.get("binary", "false").lower() == "true" and self.cfg.binary_frames
         owner = self._owner(ident)
         parked = await self.parked.take(resume, owner) if resume else None
@@ -217,7 +217,7 @@ class FacadeServer:
             await conn.read_loop()
         finally:
             self.connections -= 1
-            M.CONNECTIONS_ACTIVE.labels(*self.labels).dec()
+            M.child(M.CONNECTIONS_ACTIVE, *self.labels).dec()
             for t in list(conn.tasks):
                 t.cancel()
             if self.connections == 0:
@@ -385,7 +385,7 @@ class _Connection:
         labels = self.srv.labels
         async for m in self.ws:
             if m.type == WSMsgType.TEXT:
-                M.MESSAGES_RECEIVED.labels(*labels).inc()
+                M.child(M.MESSAGES_RECEIVED, *labels).inc()
                 if not self.text_bucket.allow():
                     M.RATE_LIMITED.labels("text").inc()
                     await self.writer.write(P.error(self.session_id, P.E_RATE_LIMITED,
@@ -523,7 +523,7 @@ class _Connection:
         t0 = time.perf_counter()
         logctx.bind(session_id=self.session_id, agent=srv.cfg.agent,
                     namespace=srv.cfg.namespace)
-        M.REQUESTS_INFLIGHT.labels(*labels).inc()
+        M.child(M.REQUESTS_INFLIGHT, *labels).inc()
         status = "ok"
         sid = msg.get("session_id") or self.session_id
         span = tracing.start_span("omnia.facade.message", {"session.id": sid},
@@ -558,9 +558,9 @@ class _Connection:
                                     usage=res.get("usage"))
         finally:
             self.inflight -= 1
-            M.REQUESTS_INFLIGHT.labels(*labels).dec()
-            M.REQUESTS_TOTAL.labels(*labels, status).inc()
-            M.REQUEST_DURATION.labels(*labels).observe(time.perf_counter() - t0)
+            M.child(M.REQUESTS_INFLIGHT, *labels).dec()
+            M.child(M.REQUESTS_TOTAL, *labels, status).inc()
+            M.child(M.REQUEST_DURATION, *labels).observe(time.perf_counter() - t0)
             tracing.end_span(span, error=status != "ok")
 
 

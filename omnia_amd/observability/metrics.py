@@ -184,3 +184,16 @@ MEMORY_OPS = Counter("omnia_memory_operations_total", "Memory API operations", [
 
 def exposition() -> bytes:
     return generate_latest(REGISTRY)
+
+
+_CHILDREN: dict = {}
+
+
+def child(metric, *labels):
+    """``metric.labels(*labels)`` memoised: the per-turn hot paths (runtime turn
+    completion, facade frames) skip prometheus_client's locked label lookup."""
+    key = (id(metric), labels)
+    c = _CHILDREN.get(key)
+    if c is None:
+        c = _CHILDREN[key] = metric.labels(*labels)
+    return c

@@ -389,9 +389,9 @@ class Agent:
                     status = "error"
                     raise
                 finally:
-                    M.PROVIDER_REQUESTS.labels(self.provider.type, self.provider.model,
-                                               status).inc()
-                    M.PROVIDER_DURATION.labels(self.provider.type, self.provider.model).observe(
+                    M.child(M.PROVIDER_REQUESTS, self.provider.type, self.provider.model,
+                            status).inc()
+                    M.child(M.PROVIDER_DURATION, self.provider.type, self.provider.model).observe(
                         time.perf_counter() - t_llm)
                     tracing.end_span(span_llm, {"gen_ai.usage.input_tokens": res.usage.input_tokens,
                                                 "gen_ai.usage.output_tokens":
@@ -432,11 +432,11 @@ class Agent:
             for v in res.violations:
                 M.VALIDATIONS.labels(v.split(":")[0], "fail").inc()
             res.cost = self.provider.pricing.cost(res.usage)
-            M.PROVIDER_INPUT_TOKENS.labels(self.provider.type, self.provider.model).inc(
+            M.child(M.PROVIDER_INPUT_TOKENS, self.provider.type, self.provider.model).inc(
                 res.usage.input_tokens)
-            M.PROVIDER_OUTPUT_TOKENS.labels(self.provider.type, self.provider.model).inc(
+            M.child(M.PROVIDER_OUTPUT_TOKENS, self.provider.type, self.provider.model).inc(
                 res.usage.output_tokens)
-            M.PROVIDER_COST.labels(self.provider.type, self.provider.model).inc(res.cost)
+            M.child(M.PROVIDER_COST, self.provider.type, self.provider.model).inc(res.cost)
             if persist:
                 state["messages"] = [m.to_dict() for m in msgs
                                      if not (m.role == "system" and m.content.startswith(

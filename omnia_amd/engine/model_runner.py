@@ -29,6 +29,7 @@ class _Staging:
     def __init__(self, spec: dict, device, pin: bool, dev=None):
         self.event = None
         self.nev = None
+        self._dsrc = None
         self.off = {}
         o = 0
         for name, (dtype, n) in spec.items():
@@ -49,6 +50,13 @@ class _Staging:
         nrows = spec["ids"][1]
         self.row_seq: list = [None] * nrows  # sequence whose data each row holds
         self.row_nb = [0] * nrows  # block-table entries already written for it
+
+    def device_src(self) -> int:
+        """Device-visible address of the pinned host buffer (0: not mapped)."""
+        if self._dsrc is None:
+            self._dsrc = ops.kernels().host_device_ptr(self.host) if self.host.is_pinned() \
+                else 0
+        return self._dsrc
 
     def native_event(self):
         if self.nev is None:
@@ -82,6 +90,9 @@ class ModelRunner:
     # single-call native step launch; TP rank 0 broadcasts the uploaded staging
     # buffer between the H2D copy and the replay, so it keeps the split path
     fused_launch = True
+    # decode-step inputs uploaded by a compute-queue kernel reading the mapped
+    # pinned staging buffer (ops/csrc/staging.hip) rather than an SDMA copy
+    stage_kernel = os.environ.get("OMNIA_STAGE_KERNEL", "1") != "0"
     def __init__(self, model, kv: KVCache, max_batch: int = 256, max_model_len: int = 8192,
                  use_graphs: bool = True, max_prefill_tokens: int = 16384):
         self.model = model
@@ -584,9 +595,20 @@ class ModelRunner:
             # held throughout instead of being dropped/re-taken around each enqueue
             self._decode_inputs(seqs, nrows, ncols, st, upload=False)
             ev = st.native_event()
-            ops.kernels().graph_launch_step(
-                gx, self.dec.dev.data_ptr(), st.host.data_ptr(), st.nbytes,
-                out_host.data_ptr(), self.out_tok.data_ptr(), 4 * n, ev.h)
+            src = st.device_src() if self.stage_kernel and ncols % 4 == 0 and \
+                self.max_blocks % 4 == 0 else 0
+            if src:
+                # upload = compute-queue kernel over the mapped pinned buffer, only
+                # the block-table window this bucket reads (no SDMA hand-off)
+                bt_off = st.off["bt"][0]
+                ops.kernels().graph_launch_staged(
+                    gx, self.dec.dev.data_ptr(), src, bt_off, bt_off, 4 * self.max_blocks,
+                    nrows, 4 * ncols, out_host.data_ptr(), self.out_tok.data_ptr(), 4 * n,
+                    ev.h)
+            else:
+                ops.kernels().graph_launch_step(
+                    gx, self.dec.dev.data_ptr(), st.host.data_ptr(), st.nbytes,
+                    out_host.data_ptr(), self.out_tok.data_ptr(), 4 * n, ev.h)
             self.stats["graph_replays"] += 1
         else:
             self._decode_inputs(seqs, nrows, ncols, st)

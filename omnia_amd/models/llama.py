@@ -311,14 +311,23 @@ class LlamaModel:
             m = self.mlp(layer, h, fb.is_decode)
         return self.add_norm(m, residual, self.w["final_norm"])
 
-    def logits(self, h: torch.Tensor, gather: bool = True) -> torch.Tensor:
+    def logits(self, h: torch.Tensor, gather: bool = True,
+               is_decode: bool = False) -> torch.Tensor:
         """LM head.  Under TP the result is this rank's vocab slice unless
         ``gather`` (the distributed sampler, parallel/tp_sampling.py, needs
-        only the slice)."""
-        lg = ops.linear(h, self.w["lm_head"])
+        only the slice).  Decode batches use the weight-streaming tile kernel
+        when the measured table lists an unsplit (bf16-out) config for it."""
+        W = self.w["lm_head"]
+        cfg = self._wcfg(h.shape[0], W.shape[0], h.shape[1], 0, is_decode)
+        if cfg is not None and cfg[2] == 1:
+            lg = ops.wgemm(0, h, W, 1, cfg[0], cfg[1])
+        else:
+            lg = ops.linear(h, W)
         return pstate.tp_all_gather_lastdim(lg) if (self.tp > 1 and gather) else lg
 
     def forward(self, fb: ForwardBatch, kv: KVCache, gather: bool = True) -> torch.Tensor:
         h = self.hidden_states(fb, kv)
-        sel = h.index_select(0, fb.logits_indices)
-        return self.logits(sel, gather)
+        # decode rows are their own logits rows (logits_indices is the identity)
+        sel = h if fb.is_decode and fb.logits_indices.shape[0] == h.shape[0] else \
+            h.index_select(0, fb.logits_indices)
+        return self.logits(sel, gather, fb.is_decode)

@@ -83,6 +83,9 @@ int omnia_ar_allgather(void* out, const void* in, void* const* regions, int* epo
                        int64_t nbytes, int64_t slot_bytes, int rank, int world, hipStream_t s);
 int omnia_tgemm(int mode, void* out, const void* X, const void* W, int M, int N, int K, int S,
                 int bn, int wnt, int ldo, hipStream_t s);
+int omnia_stage_copy(void* dst, const void* src, int64_t head_bytes, int64_t bt_off,
+                     int64_t row_stride, int rows, int64_t row_bytes, hipStream_t s);
+int64_t omnia_host_device_ptr(void* host);
 }
 
 namespace {
@@ -671,6 +674,43 @@ void graph_launch_step(int64_t graph_exec, int64_t h2d_dst, int64_t h2d_src, int
                 "hipEventRecord");
 }
 
+// Same step, but the staging upload is a compute-queue kernel reading the
+// mapped pinned buffer (`src_dev` = omnia_host_device_ptr of it) instead of an
+// SDMA copy the compute queue would have to wait on; only the scalar head and
+// the [rows x row_bytes] block-table window the graph bucket reads are moved.
+void graph_launch_staged(int64_t graph_exec, int64_t dst, int64_t src_dev, int64_t head_bytes,
+                         int64_t bt_off, int64_t row_stride, int64_t rows, int64_t row_bytes,
+                         int64_t d2h_dst, int64_t d2h_src, int64_t d2h_bytes, int64_t event) {
+  hipStream_t s = cur_stream();
+  TORCH_CHECK(dst && src_dev && rows >= 0 && rows <= (1 << 20), "bad staging operands");
+  CHECK_RC(omnia_stage_copy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src_dev),
+                            head_bytes, bt_off, row_stride, (int)rows, row_bytes, s),
+           "stage_copy");
+  TORCH_CHECK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(graph_exec), s) == hipSuccess,
+              "hipGraphLaunch");
+  if (d2h_bytes > 0)
+    TORCH_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(d2h_dst),
+                               reinterpret_cast<const void*>(d2h_src), d2h_bytes,
+                               hipMemcpyDeviceToHost, s) == hipSuccess, "D2H token copy");
+  if (event)
+    TORCH_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(event), s) == hipSuccess,
+                "hipEventRecord");
+}
+
+// standalone staged upload (tests / non-graph paths)
+void stage_copy(int64_t dst, int64_t src_dev, int64_t head_bytes, int64_t bt_off,
+                int64_t row_stride, int64_t rows, int64_t row_bytes) {
+  TORCH_CHECK(dst && src_dev && rows >= 0 && rows <= (1 << 20), "bad staging operands");
+  CHECK_RC(omnia_stage_copy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src_dev),
+                            head_bytes, bt_off, row_stride, (int)rows, row_bytes, cur_stream()),
+           "stage_copy");
+}
+
+int64_t host_device_ptr(at::Tensor host) {
+  TORCH_CHECK(host.is_pinned(), "host_device_ptr needs a pinned tensor");
+  return omnia_host_device_ptr(host.data_ptr());
+}
+
 int64_t event_create() {
   hipEvent_t e;
   TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess,
@@ -745,6 +785,9 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("ar_max_ranks", &omnia_ar_max_ranks);
   m.def("apply_token_mask", &apply_token_mask);
   m.def("graph_launch_step", &graph_launch_step);
+  m.def("graph_launch_staged", &graph_launch_staged);
+  m.def("stage_copy", &stage_copy);
+  m.def("host_device_ptr", &host_device_ptr);
   m.def("event_create", &event_create);
   m.def("event_destroy", &event_destroy);
   m.def("event_query", &event_query);

@@ -25,7 +25,7 @@ from omnia_amd.ops import reference as ref  # noqa: E402
 
 SHAPES = {  # name: (N, K, mode)   (Llama-3-8B; 70B TP=8 shard)
     "qkv": (6144, 4096, 0), "o": (4096, 4096, 0), "gate_up": (14336, 4096, 1),
-    "down": (4096, 14336, 0),
+    "down": (4096, 14336, 0), "lm_head": (128256, 4096, 0),
     "70b_qkv_tp8": (1280, 8192, 0), "70b_o_tp8": (8192, 1024, 0),
     "70b_gu_tp8": (3584, 8192, 1), "70b_down_tp8": (8192, 3584, 0),
 }
@@ -63,12 +63,16 @@ class Consumer:
             self.bs = bs
         elif name.startswith("gate") or name.endswith("gu_tp8"):
             self.kind = "swiglu"
+        elif name == "lm_head":  # the sampler reads the bf16 logits as they are
+            self.kind = "none"
         else:
             self.kind = "norm"
             self.res = torch.randn(M, N, device=dev).to(torch.bfloat16)
             self.w = torch.ones(N, dtype=torch.bfloat16, device=dev)
 
     def unfused(self, y):
+        if self.kind == "none":
+            return y
         if self.kind == "rope":
             D = 128
             q = y[:, : self.hq * D]
@@ -135,9 +139,12 @@ def main():
                     continue
                 ntiles = N // cols
                 for S in (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16):
-                    if S > K // 64 or ntiles * S > 640 or (ntiles * S < 96 and S < 16):
+                    if cons.kind == "none":  # bf16 output straight to its reader
+                        if S > 1:
+                            continue
+                    elif S > K // 64 or ntiles * S > 640 or (ntiles * S < 96 and S < 16):
                         continue
-                    md = mode if S == 1 and mode == 1 else 2
+                    md = mode if S == 1 and mode == 1 or cons.kind == "none" else 2
                     for wnt in (0, 1):
                         outb = (torch.empty(S, M, rows, device="cuda") if md == 2 else
                                 torch.empty(M, N, device="cuda", dtype=torch.bfloat16))

@@ -73,9 +73,10 @@ def test_rejects_bad_shapes_before_launch():
     x, w = _mk(16, 1000, 512)
     with pytest.raises(RuntimeError, match="tgemm"):
         ops.tgemm(0, x, w, 1, 128, 0)  # 1000 rows not a multiple of the block's 128
-    x, w = _mk(300, 1024, 512)
-    with pytest.raises(RuntimeError, match="tgemm"):
-        ops.tgemm(0, x, w, 1, 128, 0)  # M > 256
+    x, _ = _mk(300, 1024, 512)
+    _, w = _mk(300, 1024, 256)
+    with pytest.raises(RuntimeError, match="K mismatch"):
+        ops.tgemm(0, x, w, 1, 128, 0)  # K mismatch (M > 256 is valid: 256-row tiles)
     x, w = _mk(64, 1024, 512)
     with pytest.raises(RuntimeError, match="tgemm"):
         ops.tgemm(2, x, w, 9, 128, 0)  # more splits than 64-k steps

@@ -392,6 +392,47 @@ def main():
         dist.destroy_process_group()
 
 
+def _client_profiler():
+    """OMNIA_PYPROFILE=<dir>: profile this client over the timed waves (the pod's
+    processes profile themselves, utils/pyprof.py)."""
+    if not os.environ.get("OMNIA_PYPROFILE"):
+        return None
+    import cProfile
+
+    p = cProfile.Profile()
+    p.enable()
+    return p
+
+
+def _dump_profiles(prof, drv):
+    import signal
+
+    prof.disable()
+    d = os.environ["OMNIA_PYPROFILE"]
+    os.makedirs(d, exist_ok=True)
+    prof.dump_stats(os.path.join(d, f"client-{os.getpid()}.prof"))
+    pod = getattr(drv, "pod", None)
+    if pod is None:
+        return
+    import psutil
+
+    pids = [p.pid for p in (pod.runtime, pod.facade) if p is not None]
+    for pid in list(pids):
+        try:
+            pids += [c.pid for c in psutil.Process(pid).children(recursive=True)]
+        except psutil.Error:
+            pass
+    for pid in pids:  # only the processes that installed the SIGUSR1 dump handler
+        try:
+            cmd = " ".join(psutil.Process(pid).cmdline())
+            if any(m in cmd for m in ("omnia_amd.runtime", "omnia_amd.facade",
+                                      "omnia_amd.engine.core_proc")):
+                os.kill(pid, signal.SIGUSR1)
+        except (OSError, psutil.Error):
+            pass
+    time.sleep(3.0)  # let them write
+
+
 def run(a, drv, ws, rank, use_gpu, host_only):
     import torch
     import torch.distributed as dist
@@ -414,10 +455,13 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             raise SystemExit("--arrival poisson needs --rate > 0 (turns/s per replica)")
         results = drv.open_loop(a.steps * a.concurrency, a.rate) if a.path == "ws" else []
     else:
+        prof = _client_profiler()
         for k in range(a.steps):
             results.extend(drv.wave(k))
     sync()
     elapsed = time.perf_counter() - t0
+    if a.arrival != "poisson" and prof is not None:
+        _dump_profiles(prof, drv)
 
     out_tokens = sum(r[2] for r in results)
     ttfts = [r[0] for r in results if r[0] is not None]

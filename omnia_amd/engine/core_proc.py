@@ -185,6 +185,9 @@ class _Core:
             eng._finalize(s)
 
     def run(self):
+        from ..utils.pyprof import maybe_start
+
+        maybe_start("engine-core")
         eng = self.eng
         mc = eng.model_cfg
         _send(self.sock, ["ready", {"model": mc.name, "vocab": mc.vocab_size,

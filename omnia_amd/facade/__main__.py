@@ -13,6 +13,9 @@ from ..observability.logging import configure as configure_logging
 
 
 async def main():
+    from ..utils.pyprof import maybe_start
+
+    maybe_start("facade")
     configure_logging()
     env = dict(os.environ)
     client = await dial_runtime(env.get("OMNIA_RUNTIME_ADDRESS", "127.0.0.1:9000"))

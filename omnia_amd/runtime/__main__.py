@@ -39,7 +39,9 @@ def main():
         tpmod.start(EngineConfig.from_env())
         return
     from .app import run
+    from ..utils.pyprof import maybe_start
 
+    maybe_start("runtime")
     asyncio.run(run())
 
 

@@ -336,45 +336,79 @@ class LLMEngine:
 
     def _steady(self) -> bool:
         sch = self.scheduler
-        return (not sch.waiting and not sch.partial and
-                self.blocks.num_free >= len(sch.running) + 1)
+        if not self.handoff and (sch.waiting or sch.partial):
+            return False
+        # every running sequence can take its next token's page without a
+        # preemption (never preempt a sequence whose tokens are in flight)
+        return self.blocks.num_free >= len(sch.running) + 1
+
+    @property
+    def handoff(self) -> bool:
+        """Steps of every kind feed in-flight tokens from the device token slots,
+        so no step kind waits for the previous one's tokens on the host."""
+        return getattr(self.runner, "device_handoff", False)
+
+    def _launched(self, h, prefill, decode=()) -> int:
+        """Book-keeping after a step was enqueued: counters advance now, the
+        sampled tokens arrive at collect (their PLACEHOLDER is filled then)."""
+        for sq in decode:
+            sq.num_cached = sq.length  # the fed token's KV is written by this step
+            sq.output.append(PLACEHOLDER)
+        self.scheduler.on_prefill_done(prefill, {})
+        if self.handoff:
+            for sq in h.seqs[len(decode):]:  # completed prompts: token in its slot
+                sq.output.append(PLACEHOLDER)
+        n = self._flush_inflight()
+        self.inflight = h
+        ntok = sum(k for _, k in prefill)
+        self.counters["prefill_tokens"] += ntok
+        M.PREFILL_TOKENS.inc(ntok)
+        if decode:
+            self.counters["decode_tokens"] += len(decode)
+            M.DECODE_TOKENS.inc(len(decode))
+        self.step_count += 1
+        return n
 
     def _step_pipelined(self) -> int:
         sch = self.scheduler
         h0 = self.inflight
         if h0 is not None:
-            if h0.kind == "decode" and not self._steady():
+            if h0.kind in ("decode", "mixed") and not self._steady():
                 self.timing["pipeline_breaks"] += 1
                 return self._flush_inflight()
-            if h0.kind == "prefill" and not (sch.waiting or sch.partial):
+            if h0.kind == "prefill" and not self.handoff and not (sch.waiting or sch.partial):
                 # the next step decodes: it feeds the prefill's sampled tokens
                 return self._flush_inflight()
         ts = time.perf_counter()
         plan = sch.schedule()
         if plan.kind == "prefill" and self.runner.can_pipeline_prefill(plan.prefill):
-            # prefill N+1 is assembled and enqueued while prefill N runs on the GPU;
-            # counters advance now, the completed prompts' tokens arrive at collect
+            # prefill N+1 is assembled and enqueued while step N runs on the GPU
             t0 = time.perf_counter()
             self.timing["schedule_s"] += t0 - ts
             h = self.runner.launch_prefill(plan.prefill)
             self.timing["launch_s"] += time.perf_counter() - t0
-            sch.on_prefill_done(plan.prefill, {})
-            n = self._flush_inflight()
-            self.inflight = h
-            ntok = sum(k for _, k in plan.prefill)
-            self.counters["prefill_tokens"] += ntok
             self.counters["steps_prefill"] += 1
-            M.PREFILL_TOKENS.inc(ntok)
-            self.step_count += 1
-            return n
+            return self._launched(h, plan.prefill)
+        if plan.kind == "mixed" and self.runner.can_pipeline_mixed(plan.decode, plan.prefill):
+            # decode rows ride along a prefill chunk; their input tokens (and those
+            # of prompts completed by the step before) come from the token slots
+            t0 = time.perf_counter()
+            self.timing["schedule_s"] += t0 - ts
+            h = self.runner.launch_mixed(plan.decode, plan.prefill)
+            self.timing["launch_s"] += time.perf_counter() - t0
+            self.counters["steps_mixed"] = self.counters.get("steps_mixed", 0) + 1
+            M.BATCH_SIZE.observe(len(plan.decode))
+            return self._launched(h, plan.prefill, plan.decode)
         if plan.kind == "mixed":
-            # decode rows need their real last tokens: drain the in-flight step
+            # synchronous mixed step (penalties / grammars): drain the in-flight step
+            self.counters["steps_mixed_sync"] = self.counters.get("steps_mixed_sync", 0) + 1
             n0 = self._flush_inflight()
             plan.decode = [sq for sq in plan.decode if not sq.is_finished]
             if not plan.decode:
                 plan.kind = "prefill"
             return n0 + self._run_plan(plan)
-        if h0 is not None and h0.kind == "prefill" and plan.kind != "prefill":
+        if h0 is not None and h0.kind == "prefill" and plan.kind != "prefill" and \
+                not self.handoff:
             n0 = self._flush_inflight()
             if plan.kind == "decode":
                 plan.decode = [sq for sq in plan.decode if not sq.is_finished]
@@ -520,6 +554,9 @@ class LLMEngine:
 
     def _finalize(self, s: Sequence) -> None:
         self.counters["finished"] += 1
+        rel = getattr(self.runner, "release_slot", None)
+        if rel is not None:
+            rel(s)
         if s.finish_time is None:
             s.finish_time = time.perf_counter()
         if s.on_token is not None:

@@ -86,8 +86,6 @@ class EPModelRunner(ModelRunner):
         n = len(seqs)
         self._decode_inputs(seqs, nrows, ncols, self.stage[0])
         self._replay(nrows, ncols)
-        for i, s in enumerate(seqs):
-            s.slot = i
         if n == 0:
             self.ep_stats["idle_fill"] += 1
             torch.cuda.current_stream().synchronize()

@@ -114,7 +114,7 @@ class ModelRunner:
             "slots": (torch.int64, B), "seq_lens": (torch.int32, B),
             "temp": (torch.float32, B), "top_k": (torch.int32, B),
             "top_p": (torch.float32, B), "seeds": (torch.int64, B), "steps": (torch.int64, B),
-            "bt": (torch.int32, B * MB),
+            "dst": (torch.int64, B), "bt": (torch.int32, B * MB),
         }
         # double-buffered pinned host staging (step N+1 is prepared while N runs);
         # both halves upload into ONE device twin that the captured graphs read.
@@ -123,6 +123,16 @@ class ModelRunner:
         self.flip = 0
         self.logits_idx = torch.arange(B, dtype=torch.int64, device=self.device)
         self.out_tok = torch.zeros(B, dtype=torch.int32, device=self.device)
+        # device token slots: every sampled token (decode, prefill, mixed step) is
+        # also scattered to its sequence's persistent slot, and every step gathers
+        # its not-yet-collected input tokens from there -- so a step never waits
+        # for the previous one's tokens to reach the host, whatever the step kinds.
+        # Slot 0 takes the padded rows' writes.
+        self.n_slots = 2 * B + 8
+        self.tok_slots = torch.zeros(self.n_slots, dtype=torch.int32, device=self.device)
+        self.slot_owner: list = [None] * self.n_slots
+        self.free_slots = list(range(self.n_slots - 1, 0, -1))
+        self._launch_no = 0
         self.out_hosts = [torch.zeros(B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         # prefill steps are pipelined too: two pinned token buffers + their events
         self.pf_hosts = [torch.zeros(B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
@@ -203,6 +213,12 @@ class ModelRunner:
         toks = self._sample_eager(logits[: len(sample_seqs)], sample_seqs)
         return {s.seq_id: t for s, t in zip(sample_seqs, toks)}
 
+    @property
+    def device_handoff(self) -> bool:
+        """Steps feed not-yet-collected tokens from the device token slots (single
+        rank; TP workers keep the host hand-off for prefill-sampled tokens)."""
+        return self.is_gpu and self.model.tp == 1
+
     def can_pipeline_prefill(self, chunks) -> bool:
         return self.is_gpu and not any(s.params.needs_penalties or s.guide is not None
                                        for s, _ in chunks)
@@ -231,6 +247,9 @@ class ModelRunner:
                 self._tap_rows(sample_seqs, logits[:n])
                 temp, top_k, top_p, seeds, steps = self._prefill_sampling(t, meta)
                 tok = ops.sample(logits[:n], temp, top_k, top_p, seeds=seeds, steps=steps)
+            if self.device_handoff:  # the next step may feed these tokens on the GPU
+                o = meta[5] + 5 * n
+                self.tok_slots.index_copy_(0, t[o:o + n], tok.to(torch.int32))
             out_host[:n].copy_(tok, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
@@ -308,6 +327,8 @@ class ModelRunner:
                       np.array([p.seed if p.seed is not None else x.seq_id * 7919 + 17
                                 for p, x in zip(ps, sample_seqs)], np.int64),
                       np.array([len(x.output) for x in sample_seqs], np.int64)]
+            self._launch_no += 1
+            parts.append(np.array([self.assign_slot(x) for x in sample_seqs], np.int64))
         t = torch.from_numpy(np.concatenate(parts))
         self._prefill_host = t
         if self.is_gpu:
@@ -337,11 +358,14 @@ class ModelRunner:
         return self.model.forward(fb, self.kv, gather)
 
     # ------------------------------------------------------------------ mixed
-    def run_mixed(self, dseqs: list[Sequence], chunks: list[tuple[Sequence, int]]
-                  ) -> tuple[list[int], dict[int, int]]:
-        """One forward over the running sequences' next tokens (decode rows,
-        first) and prefill chunks.  Returns (tokens of ``dseqs``, {seq_id: token}
-        of the prompts this step completed)."""
+    def _mixed_forward(self, dseqs: list[Sequence], chunks: list[tuple[Sequence, int]],
+                       launch: bool = False):
+        """Pack + upload + forward of one mixed step: the running sequences' next
+        tokens (decode rows, first) and prefill chunks.  ``launch``: decode rows
+        whose input token is still on the device gather it from their token slot,
+        and the sampling parameters + destination slots of every sampled row ride
+        in the same upload.  Returns (logits, sampled seqs, packed device tensor,
+        offset of the sampling tail)."""
         bs = self.bs
         Bd, B = len(dseqs), len(chunks)
         lens = np.fromiter((n for _, n in chunks), np.int64, B)
@@ -352,12 +376,20 @@ class ModelRunner:
         ids = np.empty(T, np.int64)
         pos = np.empty(T, np.int64)
         slots = np.empty(T, np.int64)
+        src = np.full(Bd, -1, np.int64)
         mbd = self._ctx_bucket(max(s.length for s in dseqs))
         dbt = np.zeros((Bd, mbd), np.int64)
         dlen = np.empty(Bd, np.int64)
         for i, s in enumerate(dseqs):
             p = s.length - 1
-            ids[i] = s.output[-1] if s.output else s.prompt[-1]
+            last = s.output[-1] if s.output else s.prompt[-1]
+            if last == PLACEHOLDER:
+                if not launch:
+                    raise RuntimeError("synchronous mixed step with a token in flight")
+                src[i] = s.slot
+                ids[i] = 0
+            else:
+                ids[i] = last
             pos[i] = p
             slots[i] = s.blocks[p // bs] * bs + p % bs
             dbt[i, :len(s.blocks)] = s.blocks
@@ -368,8 +400,8 @@ class ModelRunner:
         sample_rows, sample_seqs = list(range(Bd)), list(dseqs)
         for i, (s, n) in enumerate(chunks):
             start, q0 = s.num_cached, Bd + int(qsl[i])
-            src = s.prompt if start + n <= len(s.prompt) else s.all_tokens
-            ids[q0:q0 + n] = src[start:start + n]
+            src_t = s.prompt if start + n <= len(s.prompt) else s.all_tokens
+            ids[q0:q0 + n] = src_t[start:start + n]
             pos[q0:q0 + n] = np.arange(start, start + n)
             bt[i, :len(s.blocks)] = s.blocks
             seq_lens[i] = start + n
@@ -382,6 +414,19 @@ class ModelRunner:
         parts = [ids, pos, slots, qsl, seq_lens, np.asarray(tseq, np.int64),
                  np.asarray(tq0, np.int64), np.asarray(sample_rows, np.int64), bt.reshape(-1),
                  dbt.reshape(-1), dlen]
+        tail = None
+        if launch:
+            parts.append(src)
+            tail = sum(len(x) for x in parts)
+            ps = [x.params for x in sample_seqs]
+            self._launch_no += 1
+            parts += [np.array([p.temperature for p in ps], np.float64).view(np.int64),
+                      np.array([p.top_k for p in ps], np.int64),
+                      np.array([p.top_p for p in ps], np.float64).view(np.int64),
+                      np.array([p.seed if p.seed is not None else x.seq_id * 7919 + 17
+                                for p, x in zip(ps, sample_seqs)], np.int64),
+                      np.array([len(x.output) for x in sample_seqs], np.int64),
+                      np.array([self.assign_slot(x) for x in sample_seqs], np.int64)]
         t = torch.from_numpy(np.concatenate(parts))
         if self.is_gpu:
             t = t.pin_memory().to(self.device, non_blocking=True)
@@ -405,11 +450,58 @@ class ModelRunner:
         fb.dec_block_tables = take(Bd * mbd, torch.int32).view(Bd, mbd)
         fb.dec_seq_lens = take(Bd, torch.int32)
         fb.num_decode = Bd
+        if launch and Bd:
+            dsrc = t[o:o + Bd]
+            ids_d = fb.input_ids[:Bd]
+            ids_d.copy_(torch.where(dsrc >= 0, self.tok_slots.index_select(0, dsrc.clamp(min=0)),
+                                    ids_d))
         logits = self.model.forward(fb, self.kv)
         self.stats["mixed_steps"] = self.stats.get("mixed_steps", 0) + 1
+        return logits, sample_seqs, t, tail
+
+    def run_mixed(self, dseqs: list[Sequence], chunks: list[tuple[Sequence, int]]
+                  ) -> tuple[list[int], dict[int, int]]:
+        """One synchronous mixed step (eager sampling: penalties, grammars).
+        Returns (tokens of ``dseqs``, {seq_id: token} of the prompts this step
+        completed)."""
+        Bd = len(dseqs)
+        logits, sample_seqs, _, _ = self._mixed_forward(dseqs, chunks)
         self._tap_rows(sample_seqs, logits)
         toks = self._sample_eager(logits, sample_seqs)
         return toks[:Bd], {s.seq_id: tk for s, tk in zip(sample_seqs[Bd:], toks[Bd:])}
+
+    def can_pipeline_mixed(self, dseqs, chunks) -> bool:
+        return (self.device_handoff and self.can_pipeline(dseqs)
+                and self.can_pipeline_prefill(chunks))
+
+    def launch_mixed(self, dseqs: list[Sequence], chunks: list[tuple[Sequence, int]]
+                     ) -> "DecodeHandle":
+        """Enqueue one mixed step with on-device sampling, the tokens scattered to
+        the sampled sequences' slots and copied to a pinned buffer; returns
+        without waiting (the handle's seqs = decode rows then completed prompts)."""
+        logits, sample_seqs, t, o = self._mixed_forward(dseqs, chunks, launch=True)
+        n = len(sample_seqs)
+        o += len(dseqs)
+        temp = t[o:o + n].view(torch.float64).float()
+        top_k = t[o + n:o + 2 * n].int()
+        top_p = t[o + 2 * n:o + 3 * n].view(torch.float64).float()
+        tok = ops.sample(logits[:n], temp, top_k, top_p, seeds=t[o + 3 * n:o + 4 * n],
+                         steps=t[o + 4 * n:o + 5 * n])
+        self.tok_slots.index_copy_(0, t[o + 5 * n:o + 6 * n], tok)
+        slot = self.pf_flip
+        self.pf_flip ^= 1
+        out_host = self.pf_hosts[slot]
+        ev = self.pf_events[slot]
+        if ev is not None:
+            ev.synchronize()  # the pinned token buffer of step N-2 has been read
+        if n > out_host.numel():
+            self.pf_hosts[slot] = out_host = torch.zeros(
+                max(n, 2 * out_host.numel()), dtype=torch.int32, pin_memory=True)
+        out_host[:n].copy_(tok, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pf_events[slot] = ev
+        return DecodeHandle(sample_seqs, out_host, ev, n, "mixed")
 
     def _sample_eager(self, logits, seqs: list[Sequence]) -> list[int]:
         n = len(seqs)
@@ -439,6 +531,42 @@ class ModelRunner:
         tok = ops.sample(logits, temp, top_k, top_p, seeds=seeds, steps=steps, **kw)
         return tok.cpu().tolist()
 
+    # ------------------------------------------------------------------ slots
+    def assign_slot(self, s: Sequence) -> int:
+        """The persistent device token slot of ``s`` (allocated on first use)."""
+        sl = s.slot
+        if sl > 0 and self.slot_owner[sl] is s:
+            s.slot_launch = self._launch_no
+            return sl
+        if not self.free_slots:
+            self._reclaim_slots()
+        sl = self.free_slots.pop()
+        self.slot_owner[sl] = s
+        s.slot = sl
+        s.slot_launch = self._launch_no
+        return sl
+
+    def _reclaim_slots(self):
+        """Slot table full (preempted sequences keep theirs): take back slots whose
+        owner has no token in flight and is not part of the launch being built."""
+        for sl in range(1, self.n_slots):
+            o = self.slot_owner[sl]
+            if o is None or o.is_finished or (o.n_real == len(o.output) and
+                                              getattr(o, "slot_launch", -1) != self._launch_no):
+                if o is not None:
+                    o.slot = -1
+                self.slot_owner[sl] = None
+                self.free_slots.append(sl)
+        if not self.free_slots:
+            raise RuntimeError("device token slots exhausted")
+
+    def release_slot(self, s: Sequence) -> None:
+        sl = s.slot
+        if sl > 0 and self.slot_owner[sl] is s:
+            self.slot_owner[sl] = None
+            self.free_slots.append(sl)
+        s.slot = -1
+
     # ------------------------------------------------------------------ decode
     def _decode_inputs(self, seqs: list[Sequence], nrows: int, ncols: int, st: "_Staging",
                        upload: bool = True):
@@ -450,15 +578,17 @@ class ModelRunner:
         npv = st.np
         ids, pos, slots, lens, src = npv["ids"], npv["pos"], npv["slots"], npv["seq_lens"], \
             npv["src"]
-        steps = npv["steps"]
+        steps, dst = npv["steps"], npv["dst"]
         bt = npv["bt"].reshape(self.max_batch, self.max_blocks)
         row_seq, row_nb = st.row_seq, st.row_nb
         bs = self.bs
+        self._launch_no += 1
         for i, s in enumerate(seqs):
             p = s.length - 1
             last = s.output[-1] if s.output else s.prompt[-1]
+            dst[i] = self.assign_slot(s)
             if last == PLACEHOLDER:
-                # token still on the device: gather it from the previous step's sampler output
+                # token still on the device: gather it from the sequence's token slot
                 src[i] = s.slot
                 ids[i] = 0
             else:
@@ -484,6 +614,7 @@ class ModelRunner:
                 row_nb[i] = nb
                 self._fill_row_sampling(npv, i, s)
             steps[i] = len(s.output)
+        dst[n:nrows] = 0
         for i in range(n, nrows):  # padded rows -> null page, no KV write
             if row_seq[i] is not _PAD:
                 ids[i] = 0
@@ -521,8 +652,8 @@ class ModelRunner:
     def _decode_body(self, nrows: int, ncols: int):
         d = self.dec.d
         src = d["src"][:nrows]
-        # tokens sampled by the previous step stay on the GPU (async scheduling)
-        ids = torch.where(src >= 0, self.out_tok.index_select(0, src.clamp(min=0)),
+        # tokens sampled by earlier steps stay on the GPU (async scheduling)
+        ids = torch.where(src >= 0, self.tok_slots.index_select(0, src.clamp(min=0)),
                           d["ids"][:nrows])
         fb = self._decode_fb(nrows, ncols, ids)
         if self.model.tp > 1:
@@ -536,6 +667,7 @@ class ModelRunner:
             tp_sample(local, self.model.vocab_start, d["temp"][:nrows], d["top_k"][:nrows],
                       d["top_p"][:nrows], seeds=d["seeds"][:nrows], steps=d["steps"][:nrows],
                       out=self.out_tok[:nrows], group=pstate.get_state().tp_group)
+            self.tok_slots.index_copy_(0, d["dst"][:nrows], self.out_tok[:nrows])
             return
         logits = self.model.forward(fb, self.kv)
         if self._tap is not None:
@@ -543,6 +675,7 @@ class ModelRunner:
         ops.sample(logits, d["temp"][:nrows], d["top_k"][:nrows], d["top_p"][:nrows],
                    seeds=d["seeds"][:nrows], steps=d["steps"][:nrows],
                    out=self.out_tok[:nrows])
+        self.tok_slots.index_copy_(0, d["dst"][:nrows], self.out_tok[:nrows])
 
     def _capture(self, nrows: int, ncols: int):
         t0 = time.perf_counter()
@@ -550,6 +683,7 @@ class ModelRunner:
             self.graph_pool = torch.cuda.graph_pool_handle()
         # warm-up/capture must not clobber live sampler outputs of an in-flight step
         saved = self.out_tok.clone()
+        saved_slots = self.tok_slots.clone()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -561,6 +695,7 @@ class ModelRunner:
             self._decode_body(nrows, ncols)
         torch.cuda.synchronize()
         self.out_tok.copy_(saved)
+        self.tok_slots.copy_(saved_slots)
         self.graphs[(nrows, ncols)] = g
         if self.fused_launch:
             self.graph_exec[(nrows, ncols)] = int(g.raw_cuda_graph_exec())
@@ -618,8 +753,6 @@ class ModelRunner:
             ev = torch.cuda.Event()
             ev.record()
         st.event = ev
-        for i, s in enumerate(seqs):
-            s.slot = i
         return DecodeHandle(seqs, out_host, ev, n)
 
     def _before_replay(self, nrows: int, ncols: int, st: "_Staging | None" = None):

@@ -46,7 +46,8 @@ class Sequence:
     preemptions: int = 0
     prefix_hit: int = 0
     text_tail: str = ""  # recent decoded text for stop-string matching
-    slot: int = -1  # row in the last launched decode step
+    slot: int = -1  # device token slot (ModelRunner.tok_slots), -1 = none
+    slot_launch: int = -1  # launch that last used the slot
     n_real: int = 0  # output tokens whose value is known on the host
     guide: object = None  # K13 grammar matcher (engine/guided.py) for constrained output
 

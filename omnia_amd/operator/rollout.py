@@ -53,6 +53,7 @@ import json
 import logging
 import math
 import re
+import calendar
 import time
 import urllib.parse
 import urllib.request
@@ -320,14 +321,18 @@ def _event(store, ar: dict, reason: str, message: str, warning: bool = False):
 
 
 def _ts(t: float) -> str:
-    return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(t))
+    """RFC 3339 with microseconds (metav1.MicroTime form): a pause measured from a
+    second-truncated start could end up to a second early."""
+    return time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(t)) + f".{int(t % 1 * 1e6):06d}Z"
 
 
 def _parse_ts(s: str | None) -> float | None:
     if not s:
         return None
     try:
-        return float(time.mktime(time.strptime(s, "%Y-%m-%dT%H:%M:%SZ"))) - time.timezone
+        base, _, frac = s.rstrip("Z").partition(".")
+        return float(calendar.timegm(time.strptime(base, "%Y-%m-%dT%H:%M:%S"))) + \
+            (float("0." + frac) if frac else 0.0)
     except (TypeError, ValueError):
         return None
 

@@ -117,3 +117,54 @@ def test_guided_json_mixed_with_pipelined_batch():
         js.validate(json.loads(e.tokenizer.decode(s.output)), schema)
     assert all(len(s.output) == 20 for s in free)
     assert free[0].output == free[1].output == free[2].output
+
+
+def _staggered(e, prompts, params, first=4, every=3):
+    """Admit ``first`` requests, then one more every ``every`` engine steps, so
+    prompts arrive while others decode (mixed steps with tokens in flight)."""
+    seqs = [e.add_request(p, params[i], session_id=f"m{i}") for i, p in
+            enumerate(prompts[:first])]
+    k, steps = first, 0
+    while e.has_work() or k < len(prompts):
+        if k < len(prompts) and steps % every == every - 1:
+            seqs.append(e.add_request(prompts[k], params[k], session_id=f"m{k}"))
+            k += 1
+        e.step()
+        steps += 1
+    return [s.output for s in seqs]
+
+
+@pytest.mark.parametrize("temp", [0.0, 0.8])
+def test_pipelined_mixed_steps_with_arrivals_match_single_request(temp):
+    """Prompts arriving during decode are co-scheduled with the running rows in
+    pipelined mixed steps: decode rows (and prompts completed one step earlier)
+    feed their in-flight tokens from the device token slots, nothing drains.
+    Every sequence's tokens equal generating it alone on the eager engine."""
+    prompts = [list(range(7 + 3 * i, 7 + 3 * i + 20 + 17 * i)) for i in range(10)]
+    max_toks = [9, 23, 4, 31, 12, 17, 2, 26, 8, 15]
+    params = [SamplingParams(temperature=temp, top_k=30, seed=11 + i, max_tokens=m,
+                             ignore_eos=True) for i, m in enumerate(max_toks)]
+    e = eng(mixed_budget=64, max_prefill_tokens=64)
+    got = _staggered(e, prompts, params)
+    assert e.counters.get("steps_mixed", 0) > 3
+    assert e.counters.get("steps_mixed_sync", 0) == 0
+    assert e.runner.stats.get("mixed_steps", 0) == e.counters["steps_mixed"]
+    ref = [eng(use_graphs=False).generate([p], q)[0].output for p, q in zip(prompts, params)]
+    assert got == ref
+    assert [len(x) for x in got] == max_toks
+
+
+def test_prefill_tokens_feed_next_decode_without_drain():
+    """A decode step right after a pipelined prefill gathers the prefill-sampled
+    tokens on the device (no flush between the two launches)."""
+    e = eng(max_prefill_tokens=4096)
+    p = SamplingParams(temperature=0, max_tokens=6, ignore_eos=True)
+    seqs = [e.add_request(list(range(3 + i, 90 + i)), p, session_id=f"d{i}") for i in range(5)]
+    e.step()  # launches the prefill
+    assert e.inflight is not None and e.inflight.kind == "prefill"
+    assert all(s.output and s.output[-1] == -1 for s in seqs)  # token in its device slot
+    e.step()  # launches decode straight away; collects the prefill
+    assert e.inflight is not None and e.inflight.kind == "decode"
+    e.run_until_done()
+    ref = [eng(use_graphs=False).generate([s.prompt], p)[0].output for s in seqs]
+    assert [s.output for s in seqs] == ref

@@ -481,7 +481,6 @@ class ModelRunner:
         without waiting (the handle's seqs = decode rows then completed prompts)."""
         logits, sample_seqs, t, o = self._mixed_forward(dseqs, chunks, launch=True)
         n = len(sample_seqs)
-        o += len(dseqs)
         temp = t[o:o + n].view(torch.float64).float()
         top_k = t[o + n:o + 2 * n].int()
         top_p = t[o + 2 * n:o + 3 * n].view(torch.float64).float()

@@ -239,8 +239,9 @@ def wgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, nw: int 
     sum is ``x @ w.T`` (reduced by the consumer kernel)."""
     if nwaves == 0:  # table code for the wide-batch kernel: nw = 32-col tiles per wave
         return wgemm_wide(mode, x, w, splits, nw, out)
-    if nwaves < 0:  # table code for the full-batch tile kernel: nw = weight rows per block
-        return tgemm(mode, x, w, splits, nw, int(nwaves == -2), out)
+    if nwaves < 0:  # table code for the full-batch tile kernel: nw = weight rows per block,
+        # -1 - nwaves = tgemm flags (bit 0 non-temporal W, bit 1 32-k stages)
+        return tgemm(mode, x, w, splits, nw, -1 - nwaves, out)
     M, K = x.shape
     N = w.shape[0] // 2 if mode == 1 else w.shape[0]
     if out is None:
@@ -268,7 +269,8 @@ def tgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, bn: int 
     """Tile GEMM (``csrc/tgemm.hip``): decode batches (M <= 256, one block owns all
     rows x ``bn`` weight rows) and prefill chunks (256-row tiles), both operands LDS-DMA staged through an
     NS-deep ring with counted waits.  Same modes / outputs as :func:`wgemm`
-    (mode 1 = fused SwiGLU needs ``splits == 1``)."""
+    (mode 1 = fused SwiGLU needs ``splits == 1``).  ``wnt`` bit 0: non-temporal
+    weight loads; bit 1: 32-k ring stages (twice the stages in flight, BN >= 128)."""
     M, K = x.shape
     N = w.shape[0] // 2 if mode == 1 else w.shape[0]
     if out is None:

@@ -48,8 +48,6 @@ __device__ __forceinline__ float4v mfma16(short8 a, short8 b, float4v c) {
                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
-// element offset of 16-B chunk `ch` (0..7) of row `row` in a [rows][64] bf16 image
-__device__ __forceinline__ int swz(int row, int ch) { return row * 64 + ((ch ^ (row & 7)) << 3); }
 
 __device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
@@ -59,27 +57,44 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
-template <int BN>
+// BK = 64: stages of 64 k (8 x 16-B chunks per row, chunk c of row r at
+// c ^ (r & 7)); BK = 32: half-size stages (4 chunks per row at c ^ ((r >> 2) & 3),
+// conflict-free for the 16 rows x 16 B a ds_read_b128 quarter-wave reads), so the
+// ring holds twice as many stages and ~2x the bytes stay in flight per CU -- the
+// per-CU L2 -> LDS intake is latency x bytes in flight.
+template <int BK>
+__device__ __forceinline__ int swz(int row, int ch) {
+  return BK == 64 ? row * 64 + ((ch ^ (row & 7)) << 3)
+                  : row * 32 + ((ch ^ ((row >> 2) & 3)) << 3);
+}
+
+template <int BN, int BK_>
 struct Geo {
-  static constexpr int BM = 256, BK = 64;
+  static constexpr int BM = 256, BK = BK_;
   static constexpr int WGN = BN >= 256 ? 4 : 2;  // waves along N
   static constexpr int WGM = 8 / WGN;
   static constexpr int WTM = BM / WGM, WTN = BN / WGN;
   static constexpr int FM = WTM / 16, FN = WTN / 16;
   static constexpr int STAGE = (BM + BN) * BK;                  // bf16 elements per stage
   static constexpr int NS_FIT = (160 * 1024) / (STAGE * 2);
-  static constexpr int NS = NS_FIT > 4 ? 4 : NS_FIT;            // LDS ring depth
-  static constexpr int A_IN = BM / 64, B_IN = BN / 64;          // glds per wave per stage
+  static constexpr int NS_MAX = BK == 64 ? 4 : 8;
+  static constexpr int NS = NS_FIT > NS_MAX ? NS_MAX : NS_FIT;  // LDS ring depth
+  static constexpr int CH = BK / 8;                             // 16-B chunks per row
+  static constexpr int RPI = 64 / CH;                           // rows per wave instruction
+  static constexpr int A_IN = BM / (8 * RPI), B_IN = BN / (8 * RPI);  // glds per wave per stage
   static constexpr int L = A_IN + B_IN;
+  static_assert(A_IN * 8 * RPI == BM && B_IN * 8 * RPI == BN, "stage rows per wave");
+  static_assert(NS >= 2, "ring too shallow");
 };
 
-template <int BN, int MODE, int WNT>
+template <int BN, int MODE, int WNT, int BK>
 __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
                                                        const bf16_t* __restrict__ X,
                                                        const bf16_t* __restrict__ W, int M, int N,
                                                        int K, int S, int ldo) {
-  using G = Geo<BN>;
+  using G = Geo<BN, BK>;
   constexpr int NS = G::NS, L = G::L, A_IN = G::A_IN, B_IN = G::B_IN;
+  constexpr int CH = G::CH, RPI = G::RPI;
   constexpr int FM = G::FM, FN = G::FN, WTM = G::WTM, WTN = G::WTN;
   __shared__ __attribute__((aligned(16))) bf16_t lds[NS * G::STAGE];
 
@@ -100,7 +115,7 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
   }
   const int split = bid / ntiles, tile = bid - split * ntiles;
   const int m0 = mt << 8, Mt = M - m0 < 256 ? M - m0 : 256;  // rows of this tile
-  const int nk = K >> 6;
+  const int nk = K / BK;
   const int kb = split * nk / S, ke = (split + 1) * nk / S;
   const int n_loc = ke - kb;
 
@@ -108,20 +123,22 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w / G::WGN, wn = w - wm * G::WGN;
 
-  // ---- per-lane LDS-DMA sources: instruction i of this wave covers 8 rows; lane l
-  // fills row 8*i' + (l >> 3), LDS chunk (l & 7) <- global chunk (l & 7) ^ (l >> 3)
-  const int lr = lane >> 3, lc = (lane & 7) ^ lr;
+  // ---- per-lane LDS-DMA sources: instruction i of this wave covers RPI rows; lane
+  // l fills row RPI*i' + l / CH, LDS chunk l % CH <- the global chunk that the
+  // swizzle places there (the XOR is an involution: swz<BK>(row, c) position)
+  const int lr = lane / CH, lp = lane % CH;
+  auto gchunk = [&](int row) { return BK == 64 ? lp ^ (row & 7) : lp ^ ((row >> 2) & 3); };
   const bf16_t* a_src[A_IN];
 #pragma unroll
   for (int i = 0; i < A_IN; ++i) {
-    const int row = 8 * (w * A_IN + i) + lr;
+    const int row = RPI * (w * A_IN + i) + lr;
     const int r = row < Mt ? row : Mt - 1;  // rows past the batch: clamped copies, never stored
-    a_src[i] = X + (int64_t)(m0 + r) * K + (int64_t)kb * 64 + lc * 8;
+    a_src[i] = X + (int64_t)(m0 + r) * K + (int64_t)kb * BK + gchunk(row) * 8;
   }
   const bf16_t* b_src[B_IN];
 #pragma unroll
   for (int i = 0; i < B_IN; ++i) {
-    const int rr = 8 * (w * B_IN + i) + lr;  // row of the B tile
+    const int rr = RPI * (w * B_IN + i) + lr;  // row of the B tile
     int64_t wrow;
     if (MODE == 1) {
       const int wv = rr / WTN, q = rr - wv * WTN;
@@ -130,14 +147,14 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
     } else {
       wrow = (int64_t)tile * BN + rr;
     }
-    b_src[i] = W + wrow * K + (int64_t)kb * 64 + lc * 8;
+    b_src[i] = W + wrow * K + (int64_t)kb * BK + gchunk(rr) * 8;
   }
-  const int a_dst0 = (8 * w * A_IN) * 64;                // element offsets inside a stage
-  const int b_dst0 = 256 * 64 + (8 * w * B_IN) * 64;
+  const int a_dst0 = (RPI * w * A_IN) * BK;              // element offsets inside a stage
+  const int b_dst0 = 256 * BK + (RPI * w * B_IN) * BK;
 
   auto issue = [&](int stage, int kl) {
     bf16_t* base = lds + stage * G::STAGE;
-    const int koff = kl * 64;
+    const int koff = kl * BK;
 #pragma unroll
     for (int i = 0; i < A_IN; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + koff),
@@ -158,22 +175,25 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
   const int fr = lane & 15, fq = lane >> 4;
   // both 32-k halves of the stage are read up front, so the second half's LDS
   // reads are in flight under the first half's MFMAs (counted lgkmcnt by hipcc)
+  constexpr int KS = BK / 32;  // 32-k MFMA steps per stage
   auto compute = [&](int stage) {
     const bf16_t* As = lds + stage * G::STAGE;
-    const bf16_t* Bs = As + 256 * 64;
-    short8 a[2][FM], b[2][FN];
+    const bf16_t* Bs = As + 256 * BK;
+    short8 a[KS][FM], b[KS][FN];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        b[ks][j] = *reinterpret_cast<const short8*>(Bs + swz(wn * WTN + 16 * j + fr, ks * 4 + fq));
+        b[ks][j] = *reinterpret_cast<const short8*>(Bs + swz<BK>(wn * WTN + 16 * j + fr,
+                                                                 ks * 4 + fq));
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        a[ks][i] = *reinterpret_cast<const short8*>(As + swz(wm * WTM + 16 * i + fr, ks * 4 + fq));
+        a[ks][i] = *reinterpret_cast<const short8*>(As + swz<BK>(wm * WTM + 16 * i + fr,
+                                                                 ks * 4 + fq));
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -251,15 +271,28 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
   }
 }
 
+// wnt bit 0: non-temporal W loads; bit 1: 32-k stages (BN >= 128)
 template <int BN, int MODE>
 int launch_bn(void* out, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int ldo,
               int wnt, hipStream_t s) {
   const int ntiles = MODE == 1 ? N / (BN / 2) : N / BN;
   const dim3 grid(ntiles * S * ((M + 255) / 256)), block(512);
-  if (wnt)
-    tgemm_kernel<BN, MODE, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+  const bool nt = wnt & 1, bk32 = wnt & 2;
+  if constexpr (BN >= 128) {
+    if (bk32) {
+      if (nt)
+        tgemm_kernel<BN, MODE, 1, 32><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+      else
+        tgemm_kernel<BN, MODE, 0, 32><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+      return (int)hipGetLastError();
+    }
+  } else {
+    if (bk32) return -21;
+  }
+  if (nt)
+    tgemm_kernel<BN, MODE, 1, 64><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
   else
-    tgemm_kernel<BN, MODE, 0><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+    tgemm_kernel<BN, MODE, 0, 64><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
   return (int)hipGetLastError();
 }
 

@@ -145,7 +145,7 @@ def main():
                     elif S > K // 64 or ntiles * S > 640 or (ntiles * S < 96 and S < 16):
                         continue
                     md = mode if S == 1 and mode == 1 or cons.kind == "none" else 2
-                    for wnt in (0, 1):
+                    for wnt in ((0, 1, 2, 3) if bn >= 128 else (0, 1)):
                         outb = (torch.empty(S, M, rows, device="cuda") if md == 2 else
                                 torch.empty(M, N, device="cuda", dtype=torch.bfloat16))
 
@@ -187,7 +187,7 @@ def main():
                                   "N": N, "K": K, "mode": mode, "M": M}
             if best[5] < 0.02 and (t_cur or t_lib) / best[0] >= a.min_gain:
                 bucket = next(b for b in ops.WGEMM_BUCKETS if M <= b)
-                table_upd[f"{mode}:{bucket}:{N}:{K}"] = [best[1], -2 if best[3] else -1, best[2]]
+                table_upd[f"{mode}:{bucket}:{N}:{K}"] = [best[1], -1 - best[3], best[2]]
         del ws
         torch.cuda.empty_cache()
     with open(a.out, "w") as f:

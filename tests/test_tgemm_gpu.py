@@ -29,11 +29,11 @@ def test_mode0_matches_fp32(M, bn):
 
 
 @pytest.mark.parametrize("M", [3, 190, 256])
-@pytest.mark.parametrize("bn", [64, 128, 256])
-def test_mode1_swiglu_matches_fp32(M, bn):
+@pytest.mark.parametrize("bn,wnt", [(64, 1), (128, 1), (256, 1), (128, 2), (256, 3)])
+def test_mode1_swiglu_matches_fp32(M, bn, wnt):
     I = 512
     x, w = _mk(M, 2 * I, 1024, seed=7 + M + bn)
-    out = ops.tgemm(1, x, w, 1, bn, 1)
+    out = ops.tgemm(1, x, w, 1, bn, wnt)
     want = ref.silu_mul((x.float() @ w.float().t()))
     torch.testing.assert_close(out.float(), want.float(), rtol=3e-2, atol=3e-2)
 
@@ -48,13 +48,16 @@ def test_mode2_splitk_slabs_sum_to_product(M, S, bn):
     torch.testing.assert_close(part.sum(0), want, rtol=1e-3, atol=3e-3)
 
 
-def test_llama3_8b_shapes():
-    """The four Llama-3-8B decode projections at the serving batch."""
+@pytest.mark.parametrize("wnt", [1, 2, 3])
+def test_llama3_8b_shapes(wnt):
+    """The four Llama-3-8B decode projections at the serving batch (64-k and
+    32-k ring stages)."""
     M = 256
     for N, K, mode, S, bn in ((6144, 4096, 2, 5, 128), (4096, 4096, 2, 8, 128),
-                              (14336, 4096, 1, 1, 128), (4096, 14336, 2, 7, 128)):
+                              (14336, 4096, 1, 1, 128), (4096, 14336, 2, 7, 128),
+                              (4096, 4096, 2, 4, 256)):
         x, w = _mk(M, 2 * N if mode == 1 else N, K, seed=N + K)
-        out = ops.tgemm(mode, x, w, S, bn, 1)
+        out = ops.tgemm(mode, x, w, S, bn, wnt)
         full = x.float() @ w.float().t()
         want = ref.silu_mul(full) if mode == 1 else full
         got = out.sum(0) if mode == 2 else out.float()
@@ -82,15 +85,18 @@ def test_rejects_bad_shapes_before_launch():
         ops.tgemm(2, x, w, 9, 128, 0)  # more splits than 64-k steps
     with pytest.raises(RuntimeError, match="tgemm"):
         ops.tgemm(0, x, w, 1, 96, 0)  # unsupported block width
+    with pytest.raises(RuntimeError, match="tgemm"):
+        ops.tgemm(0, x, w, 1, 64, 2)  # 32-k stages need BN >= 128
 
 
-@pytest.mark.parametrize("M,mode,bn,S", [(257, 0, 128, 1), (600, 0, 256, 1), (1024, 1, 256, 1),
-                                         (777, 1, 128, 1), (1000, 2, 128, 3), (4096, 1, 256, 1)])
-def test_prefill_row_tiles_match_fp32(M, mode, bn, S):
+@pytest.mark.parametrize("M,mode,bn,S,wnt", [(257, 0, 128, 1, 0), (600, 0, 256, 1, 0),
+                                              (1024, 1, 256, 1, 0), (777, 1, 128, 1, 2),
+                                              (1000, 2, 128, 3, 2), (4096, 1, 256, 1, 0)])
+def test_prefill_row_tiles_match_fp32(M, mode, bn, S, wnt):
     """M > 256: 256-row tiles in grouped order (the prefill path), ragged last tile."""
     N = 512
     x, w = _mk(M, 2 * N if mode == 1 else N, 1024, seed=M + mode)
-    out = ops.tgemm(mode, x, w, S, bn, 0)
+    out = ops.tgemm(mode, x, w, S, bn, wnt)
     full = x.float() @ w.float().t()
     if mode == 1:
         torch.testing.assert_close(out.float(), ref.silu_mul(full).float(), rtol=3e-2,

@@ -159,7 +159,9 @@ class Scheduler:
         cfg = self.cfg
         if cfg.mixed_budget > 0 and self.running and (self.partial or self.waiting):
             decode = self._decode_rows()
-            chunks = self._prefill_chunks(cfg.mixed_budget)
+            # the decode rows count against the budget: a full mixed step is exactly
+            # mixed_budget tokens, the GEMM shape the prefill GEMMs were tuned for
+            chunks = self._prefill_chunks(max(0, cfg.mixed_budget - len(decode)))
             if chunks and decode:
                 return StepPlan("mixed", chunks, decode)
             if chunks:

@@ -25,6 +25,7 @@ Draining still admits such resume upgrades and waits for live + parked calls.
 from __future__ import annotations
 
 import asyncio
+import os
 import json
 import logging
 import time
@@ -304,7 +305,11 @@ class FacadeServer:
 
     # ---------------------------------------------------------------- lifecycle
     async def start(self, host: str = "0.0.0.0", port: int | None = None) -> int:
-        self.runner = web.AppRunner(self.app)
+        # per-connection access logging is opt-in (OMNIA_ACCESS_LOG=1): a formatted
+        # log record per closed session sits on the event loop exactly when a burst
+        # of turns completes
+        access = {} if os.environ.get("OMNIA_ACCESS_LOG") == "1" else {"access_log": None}
+        self.runner = web.AppRunner(self.app, **access)
         await self.runner.setup()
         # listen backlog sized for connection bursts: aiohttp's default of 128
         # drops the SYNs of a burst of new sessions beyond it, and the kernel's

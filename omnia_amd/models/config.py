@@ -96,10 +96,15 @@ TINY_MIXTRAL = ModelConfig(name="tiny-mixtral", arch="mixtral", vocab_size=512,
                            hidden_size=256, intermediate_size=256, num_layers=2, num_heads=4,
                            num_kv_heads=2, max_position=4096, num_experts=4,
                            experts_per_token=2, bos_token_id=256, eos_token_ids=(257,))
+# 8 experts: one per rank of an 8-way expert-parallel group (EP world-8 tests)
+TINY_MIXTRAL_E8 = ModelConfig(name="tiny-mixtral-e8", arch="mixtral", vocab_size=512,
+                              hidden_size=256, intermediate_size=128, num_layers=2,
+                              num_heads=4, num_kv_heads=2, max_position=4096, num_experts=8,
+                              experts_per_token=2, bos_token_id=256, eos_token_ids=(257,))
 
 REGISTRY: dict[str, ModelConfig] = {
     c.name: c for c in [LLAMA3_8B, LLAMA31_8B, LLAMA3_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_MIXTRAL,
-                   EMBED_1B, TINY_EMBED, TINY_LLAMA_H8]
+                   TINY_MIXTRAL_E8, EMBED_1B, TINY_EMBED, TINY_LLAMA_H8]
 }
 ALIASES = {
     "meta-llama/Meta-Llama-3-8B": "llama-3-8b",

@@ -2,8 +2,8 @@
 rank is its own engine with its own prompts, the Mixtral MoE layers exchange
 tokens through the fixed-capacity all-to-all, and the ranks step in lockstep
 (prefill on one rank while another decodes or idles).  Outputs must equal a
-single-rank engine with all experts local on the same prompts (gloo, world 2
-and 4; the same weights by construction: experts are drawn per global id)."""
+single-rank engine with all experts local on the same prompts (gloo, world 2,
+4 and 8; the same weights by construction: experts are drawn per global id)."""
 import os
 import socket
 
@@ -28,12 +28,16 @@ def _port():
     return p
 
 
-def _cfg(**kw):
+def _cfg(model="tiny-mixtral", **kw):
     from omnia_amd.engine.engine import EngineConfig
 
-    return EngineConfig(model="tiny-mixtral", device="cpu", dtype="float32", num_blocks=64,
+    return EngineConfig(model=model, device="cpu", dtype="float32", num_blocks=64,
                         block_size=4, max_batch=8, max_model_len=128, use_graphs=False,
                         seed=5, **kw)
+
+
+def _model(world):
+    return "tiny-mixtral-e8" if world > 4 else "tiny-mixtral"
 
 
 def _worker(rank, world, port, q):
@@ -43,9 +47,9 @@ def _worker(rank, world, port, q):
         from omnia_amd.engine.engine import LLMEngine
         from omnia_amd.engine.sampling_params import SamplingParams
 
-        eng = LLMEngine(_cfg(ep_mode="a2a"))
+        eng = LLMEngine(_cfg(_model(world), ep_mode="a2a"))
         assert eng.ep_lockstep and eng.model.e_local == eng.model_cfg.num_experts // world
-        prompts, mt = PROMPTS[rank], MAX_TOKENS[rank]
+        prompts, mt = PROMPTS[rank % 4], MAX_TOKENS[rank % 4]
         outs = []
         if prompts:
             seqs = eng.generate(prompts, SamplingParams(temperature=0.0, max_tokens=mt,
@@ -63,7 +67,7 @@ def _worker(rank, world, port, q):
         q.put(("err", rank, traceback.format_exc(), None))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_attention_ep_engine_matches_single_rank(world):
     from omnia_amd.engine.engine import LLMEngine
     from omnia_amd.engine.sampling_params import SamplingParams
@@ -79,17 +83,17 @@ def test_dp_attention_ep_engine_matches_single_rank(world):
         p.join(60)
     for status, rank, val, _ in res:
         assert status == "ok", val
-    oracle = LLMEngine(_cfg(ep_mode="tp"))  # one rank, every expert local
+    oracle = LLMEngine(_cfg(_model(world), ep_mode="tp"))  # one rank, every expert local
     for _, rank, outs, stats in res:
-        prompts = PROMPTS[rank]
+        prompts = PROMPTS[rank % 4]
         if not prompts:
             assert outs == [] and stats["idle_fill"] > 0  # served the others' MoE layers
             continue
         want = oracle.generate(prompts, SamplingParams(temperature=0.0,
-                                                       max_tokens=MAX_TOKENS[rank],
+                                                       max_tokens=MAX_TOKENS[rank % 4],
                                                        ignore_eos=True))
         assert outs == [s.output for s in want], (rank, outs)
-        assert stats["steps"] >= MAX_TOKENS[rank]
+        assert stats["steps"] >= MAX_TOKENS[rank % 4]
 
 
 def test_capacity_is_step_global_and_lossless():

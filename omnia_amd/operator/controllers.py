@@ -694,6 +694,10 @@ class WorkspaceReconciler:
                              "spec": {"selector": {"app": dn},
                                       "ports": [{"name": "http", "port": 8080}]}})
                 urls[svc] = f"http://{dn}.{nsname}:8080"
+                if svc == "session-api":
+                    self._compaction_cronjob(store, nsname, name, g, dn, own,
+                                             store.try_get("SessionRetentionPolicy", pref, None)
+                                             if pref else None)
                 dep = store.try_get("Deployment", dn, nsname) or {}
                 if not (dep.get("status") or {}).get("readyReplicas"):
                     ready = False
@@ -713,6 +717,41 @@ class WorkspaceReconciler:
         ws["status"] = st
         store.update_status(ws)
         return None if all_ready else 5.0  # re-check service readiness
+
+    @staticmethod
+    def _compaction_cronjob(store: APIStore, nsname: str, ws: str, group: str, dn: str, own,
+                            policy: dict | None):
+        """The service group's session compaction CronJob (the chart's
+        ``compaction-cronjob.yaml``, per workspace here): scheduled by the
+        SessionRetentionPolicy's ``coldArchive.compactionSchedule`` when its cold
+        archive is enabled; each run asks the group's session-api to compact its
+        own tiers (``python -m omnia_amd.session.compaction --session-api``)."""
+        name = f"compaction-{ws}-{group}"
+        cold = ((policy or {}).get("spec") or {}).get("coldArchive") or {}
+        if not cold.get("enabled"):
+            try:
+                store.delete("CronJob", name, nsname)
+            except NotFound:
+                pass
+            return
+        labels = {"app.kubernetes.io/component": "compaction",
+                  "omnia.altairalabs.ai/workspace": ws,
+                  "omnia.altairalabs.ai/service-group": group}
+        store.apply({"apiVersion": "batch/v1", "kind": "CronJob",
+                     "metadata": {"name": name, "namespace": nsname, "labels": labels,
+                                  "ownerReferences": own},
+                     "spec": {"schedule": cold.get("compactionSchedule", "0 2 * * *"),
+                              "concurrencyPolicy": "Forbid",
+                              "successfulJobsHistoryLimit": 3, "failedJobsHistoryLimit": 1,
+                              "jobTemplate": {"metadata": {"labels": labels}, "spec": {
+                                  "backoffLimit": 2, "template": {"spec": {
+                                      "restartPolicy": "Never",
+                                      "containers": [{
+                                          "name": "compaction", "image": "omnia-compaction",
+                                          "command": ["python", "-m",
+                                                      "omnia_amd.session.compaction"],
+                                          "args": ["--session-api",
+                                                   f"http://{dn}.{nsname}:8080"]}]}}}}}})
 
 
 # ===================================================================== policies

@@ -381,7 +381,19 @@ class LocalLauncher:
                     continue
                 raise KeyError(f"{kind} {ref.get('name')}/{ref.get('key')} not found")
             env.append({"name": e["name"], "value": val})
+        # cluster DNS on one node: in-cluster Service URLs in env values and args
+        # point at the Services' local endpoints (a compaction Job dials its
+        # workspace's session-api by Service URL)
+        from .pods import resolve_service_urls
+
+        vals = resolve_service_urls({i: e["value"] for i, e in enumerate(env) if "value" in e},
+                                    self._service_endpoint)
+        for i, v in vals.items():
+            env[i] = dict(env[i], value=v)
         c["env"] = env
+        if c.get("args"):
+            c["args"] = list(resolve_service_urls(dict(enumerate(c["args"])),
+                                                  self._service_endpoint).values())
         return c
 
     def _job_mounts(self, ns: str, tmpl: dict, workdir: str) -> dict[str, str]:
@@ -424,7 +436,9 @@ class LocalLauncher:
                 c = d["spec"]["template"]["spec"]["containers"][0]
                 if not c.get("command"):
                     continue
-                sp = ServiceProcess(key[1], c, tempfile.mkdtemp(prefix=f"omnia-{key[1]}-"))
+                wd = tempfile.mkdtemp(prefix=f"omnia-{key[1]}-")
+                sp = ServiceProcess(key[1], c, wd, mounts=self._job_mounts(
+                    key[0], d["spec"]["template"]["spec"], wd))
                 try:
                     await loop.run_in_executor(None, sp.start)
                 except Exception:  # noqa: BLE001

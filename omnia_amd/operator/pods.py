@@ -212,14 +212,16 @@ class ProcessPod:
 class ServiceProcess:
     """A single-container service pod (workspace session-api / memory-api,
     ``internal/controller/workspace_services.go``) as one OS process: the
-    container's ``command`` + ``args`` with its port rebound to a free local port
-    and ``/data`` mapped into a per-pod directory."""
+    container's ``command`` + ``args`` with its port rebound to a free local port,
+    ``/data`` mapped into a per-pod directory and ConfigMap volume ``mounts``
+    (mountPath -> materialised local dir) rewritten in args and env values."""
 
     def __init__(self, name: str, container: dict, workdir: str,
-                 python: str = sys.executable):
+                 python: str = sys.executable, mounts: dict[str, str] | None = None):
         self.name = name
         self.container = container
         self.workdir = workdir
+        self.mounts = mounts or {}
         self.python = python
         self.port = None
         self.proc: subprocess.Popen | None = None
@@ -238,16 +240,24 @@ class ServiceProcess:
                 out += ["--port", str(self.port)]
                 i += 2
                 continue
-            out.append(a.replace("/data/", data + "/") if a.startswith("/data/") else a)
+            out.append(a.replace("/data/", data + "/") if a.startswith("/data/")
+                       else self._map(a))
             i += 1
         if "--port" not in out:
             out += ["--port", str(self.port)]
         return out
 
+    def _map(self, v: str) -> str:
+        for mp, local in self.mounts.items():
+            if v == mp or v.startswith(mp.rstrip("/") + "/"):
+                return local + v[len(mp.rstrip("/")):]
+        return v
+
     def start(self, timeout_s: float = 60.0) -> "ServiceProcess":
         self.port = free_port()
         env = dict(os.environ)
-        env.update({e["name"]: str(e.get("value", "")) for e in self.container.get("env", [])})
+        env.update({e["name"]: self._map(str(e.get("value", "")))
+                    for e in self.container.get("env", [])})
         env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
         os.makedirs(self.workdir, exist_ok=True)
         self._log = open(os.path.join(self.workdir, "service.log"), "wb")

@@ -80,7 +80,7 @@ def session_resolver(svc: TieredSessionService, cache_size: int = 10000):
 def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400.0,
               tokens: dict | None = None, allowed_namespaces: set | None = None,
               redactor=None, optout=None, audit_logger=None, media_deleter=None,
-              privacy_middleware=None) -> web.Application:
+              privacy_middleware=None, retention: dict | None = None) -> web.Application:
     """``audit_logger`` (EE, :class:`omnia_amd.ee.audit.AuditLogger`): record
     session created/accessed/searched/deleted events and serve them at
     ``/api/v1/audit/sessions`` (reference session-api audit wiring)."""
@@ -332,6 +332,35 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
     async def metrics(_):
         return web.Response(body=M.exposition(), content_type="text/plain")
 
+    async def compact(request):
+        """One compaction run (warm -> cold archival, warm purge, cold expiry) on
+        this replica's tiers -- what the workspace's compaction CronJob calls
+        (``python -m omnia_amd.session.compaction --session-api URL``).  Body:
+        optional ``warmRetentionSeconds`` / ``coldRetentionSeconds`` / ``dryRun``
+        overriding the mounted SessionRetentionPolicy."""
+        from .compaction import CompactionConfig, CompactionEngine
+
+        try:
+            body = await request.json() if request.can_read_body else {}
+        except ValueError:
+            return web.json_response({"error": "body must be JSON"}, status=400)
+        ret = retention or {}
+        try:
+            cfg = CompactionConfig(
+                float(body.get("warmRetentionSeconds", ret.get("warm_retention_s", 7 * 86400))),
+                float(body.get("coldRetentionSeconds",
+                               ret.get("cold_retention_s", 365 * 86400))),
+                dry_run=bool(body.get("dryRun", False)))
+        except (TypeError, ValueError):
+            return web.json_response({"error": "retention must be a number"}, status=400)
+        if cfg.warm_retention_s < 0 or cfg.cold_retention_s < 0:
+            return web.json_response({"error": "retention must be >= 0"}, status=400)
+        res = await asyncio.to_thread(CompactionEngine(svc.warm, svc.cold, svc.hot, cfg).run)
+        return web.json_response({"archived": res.archived, "purged": res.purged,
+                                  "coldExpired": res.cold_expired, "skipped": res.skipped,
+                                  "errors": res.errors, "coldArchive": svc.cold is not None},
+                                 status=500 if res.errors else 200)
+
     async def openapi(_):
         routes = sorted({(rt.method, rt.resource.canonical) for rt in app.router.routes()
                          if rt.resource is not None and rt.method != "HEAD"})
@@ -376,6 +405,7 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
     r.add_patch("/api/v1/sessions/{id}/stats", status)
     r.add_patch("/api/v1/sessions/{id}/decorate", decorate)
     r.add_post("/api/v1/privacy/sessions/delete-by-user", delete_by_user)
+    r.add_post("/api/v1/admin/compaction", compact)
     return app
 
 
@@ -388,7 +418,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser("session-api")
     ap.add_argument("--port", type=int, default=8300)
     ap.add_argument("--db", default=":memory:")
-    ap.add_argument("--cold-dir", default="")
+    ap.add_argument("--cold-dir", default=os.environ.get("OMNIA_SESSION_COLD_DIR", ""),
+                    help="local-directory cold archive (single-node deployments)")
     # cmd/session-api/main.go:120-155: object-store cold archive (env fallbacks)
     ap.add_argument("--cold-backend", default=os.environ.get("COLD_BACKEND", ""),
                     help="s3 | gcs | azure")
@@ -495,7 +526,7 @@ def main(argv=None):
         app_kw["privacy_middleware"] = session_privacy_middleware(
             watcher, session_resolver(svc),
             PrivacyPrefsClient(a.privacy_api_url) if a.privacy_api_url else None)
-    app = build_app(svc, **app_kw)
+    app = build_app(svc, retention=retention, **app_kw)
     if watcher is not None:
         async def watch(_app):
             import asyncio

@@ -103,18 +103,53 @@ class CompactionEngine:
         return res
 
 
+def run_remote(url: str, warm_s: float | None, cold_s: float | None, dry_run: bool,
+               token: str = "", timeout_s: float = 600.0) -> dict:
+    """Drive one compaction run on a session-api replica
+    (``POST /api/v1/admin/compaction``): the CronJob form for deployments whose
+    warm store lives inside the session-api pod."""
+    import json
+    import urllib.request
+
+    body = {"dryRun": dry_run}
+    if warm_s is not None:
+        body["warmRetentionSeconds"] = warm_s
+    if cold_s is not None:
+        body["coldRetentionSeconds"] = cold_s
+    req = urllib.request.Request(url.rstrip("/") + "/api/v1/admin/compaction",
+                                 data=json.dumps(body).encode(), method="POST",
+                                 headers={"Content-Type": "application/json"})
+    if token:
+        req.add_header("Authorization", f"Bearer {token}")
+    with urllib.request.urlopen(req, timeout=timeout_s) as r:
+        return json.loads(r.read() or b"{}")
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser("compaction")
-    ap.add_argument("--db", required=True)
+    ap.add_argument("--db", default="", help="warm store (SQLite path / postgres DSN)")
+    ap.add_argument("--session-api", default="",
+                    help="run the compaction inside this session-api replica instead")
+    ap.add_argument("--token", default="")
     ap.add_argument("--cold-dir", default="")
-    ap.add_argument("--warm-retention", type=float, default=7 * 86400)
-    ap.add_argument("--cold-retention", type=float, default=365 * 86400)
+    ap.add_argument("--warm-retention", type=float, default=None,
+                    help="seconds (default: the policy's, else 7 days)")
+    ap.add_argument("--cold-retention", type=float, default=None,
+                    help="seconds (default: the policy's, else 365 days)")
     ap.add_argument("--dry-run", action="store_true")
     ap.add_argument("--retention-config", default="",
                     help="retention.yaml of a SessionRetentionPolicy (operator ConfigMap "
                          "retention-policy-<name>); overrides the two retention flags")
     a = ap.parse_args(argv)
-    warm_s, cold_s = a.warm_retention, a.cold_retention
+    if a.session_api:
+        res = run_remote(a.session_api, a.warm_retention, a.cold_retention, a.dry_run,
+                         a.token)
+        print(res)
+        return 1 if res.get("errors") else 0
+    if not a.db:
+        ap.error("--db or --session-api is required")
+    warm_s = a.warm_retention if a.warm_retention is not None else 7 * 86400
+    cold_s = a.cold_retention if a.cold_retention is not None else 365 * 86400
     if a.retention_config:
         import yaml
 
@@ -130,4 +165,6 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+
+    sys.exit(main(sys.argv[1:]))

@@ -256,3 +256,47 @@ def test_list_sessions_filters_and_search():
     page1 = [s.id for s in w.list_sessions(limit=2)]
     page2 = [s.id for s in w.list_sessions(limit=2, offset=2)]
     assert page1 == ["q5", "q4"] and page2 == ["q3", "q2"]
+
+
+def test_admin_compaction_endpoint_and_remote_cli():
+    """``POST /api/v1/admin/compaction`` runs one compaction on the replica's own
+    tiers (the workspace compaction CronJob's target): policy retention by
+    default, overridable per call; the CLI's ``--session-api`` mode drives it."""
+    from omnia_amd.session import compaction as C
+
+    async def go():
+        svc = _svc()
+        old = time.time() - 30 * 86400
+        svc.warm.put_session(Session(id="old", namespace="ns", created_at=old, updated_at=old))
+        svc.warm.add_message("old", Message(role="user", content="hi", sequence_num=0))
+        svc.create(Session(id="new", namespace="ns"))
+        app = build_app(svc, retention={"warm_retention_s": 7 * 86400})
+        runner = web.AppRunner(app)
+        await runner.setup()
+        site = web.TCPSite(runner, "127.0.0.1", 0)
+        await site.start()
+        port = site._server.sockets[0].getsockname()[1]
+        url = f"http://127.0.0.1:{port}"
+        out = {}
+        async with aiohttp.ClientSession() as s:
+            r = await s.post(f"{url}/api/v1/admin/compaction", json={"dryRun": True})
+            out["dry"] = await r.json()
+            r = await s.post(f"{url}/api/v1/admin/compaction")
+            out["policy"] = await r.json()
+            out["bad"] = (await s.post(f"{url}/api/v1/admin/compaction",
+                                       json={"warmRetentionSeconds": -1})).status
+        # the CronJob's CLI form, zero retention: the fresh session goes too
+        out["cli"] = await asyncio.to_thread(
+            C.main, ["--session-api", url, "--warm-retention", "0"])
+        await runner.cleanup()
+        return svc, out
+
+    svc, out = asyncio.run(go())
+    assert out["dry"]["archived"] == 1
+    assert out["policy"]["archived"] == 1 and out["policy"]["coldArchive"] is True
+    assert out["bad"] == 400
+    assert out["cli"] == 0
+    assert svc.warm.get_session("old") is None and svc.warm.get_session("new") is None
+    sess, msgs = svc.get("old")  # read back from the cold archive
+    assert sess.id == "old" and [m.content for m in msgs] == ["hi"]
+    assert svc.get("new")[0].id == "new"

@@ -87,7 +87,13 @@ struct Geo {
   static_assert(NS >= 2, "ring too shallow");
 };
 
-template <int BN, int MODE, int WNT, int BK>
+// PIPE = 1 (BK = 64, BN <= 128): the LDS -> register fragment reads of stage t+1
+// are issued right after stage t+1's barrier and run under stage t's MFMAs
+// (fragments double-buffered in registers), instead of all 8 waves bursting their
+// reads after each barrier and then waiting on them; the ring also keeps one more
+// stage in flight, since a stage's buffer is free as soon as its fragments are
+// in registers.
+template <int BN, int MODE, int WNT, int BK, int PIPE>
 __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
                                                        const bf16_t* __restrict__ X,
                                                        const bf16_t* __restrict__ W, int M, int N,
@@ -201,27 +207,82 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // ---- pipeline: stages 0..NS-2 in flight before the loop; step t waits for its
-  // own stage (NS-2 younger stages stay outstanding), passes ONE raw barrier (every
-  // wave's DMA for stage t has landed, and every wave is done reading stage t-1's
-  // buffer), refills that buffer with stage t+NS-1, then computes stage t.  Past
-  // the slice end the refill re-reads the last stage into a buffer nobody reads,
-  // which keeps the vmcnt count constant (branch-free pipeline).
   const int klast = n_loc - 1;
+  if constexpr (PIPE) {
+    static_assert(BK == 64 && BN <= 128, "register-pipelined variant: BK 64, BN <= 128");
+    auto ldfrag = [&](int stage, short8 (&a)[KS][FM], short8 (&b)[KS][FN]) {
+      const bf16_t* As = lds + stage * G::STAGE;
+      const bf16_t* Bs = As + 256 * BK;
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s) issue(s, s < klast ? s : klast);
-  for (int t0 = 0; t0 < n_loc; t0 += NS) {
+      for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      const int t = t0 + u;
-      if (t < n_loc) {
-        wait_vm<(NS - 2) * L>();
+        for (int j = 0; j < FN; ++j)
+          b[ks][j] = *reinterpret_cast<const short8*>(Bs + swz<BK>(wn * WTN + 16 * j + fr,
+                                                                   ks * 4 + fq));
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          a[ks][i] = *reinterpret_cast<const short8*>(As + swz<BK>(wm * WTM + 16 * i + fr,
+                                                                   ks * 4 + fq));
+      }
+    };
+    auto mma = [&](const short8 (&a)[KS][FM], const short8 (&b)[KS][FN]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(a[ks][i], b[ks][j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    // step t: stage t's fragments are in `ca/cb`; wait for stage t+1, refill stage
+    // t's buffer with stage t+NS, read stage t+1 into `na/nb`, MFMAs on stage t
+    auto step = [&](int t, short8 (&ca)[KS][FM], short8 (&cb)[KS][FN], short8 (&na)[KS][FM],
+                    short8 (&nb)[KS][FN]) {
+      if (t + 1 < n_loc) {
+        wait_vm<(NS - 2) * L>();                            // stage t+1 landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stage t is in registers
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        const int nxt = t + NS - 1;
-        issue((u + NS - 1) % NS, nxt < klast ? nxt : klast);
-        compute(u);
-        __builtin_amdgcn_sched_barrier(0);
+        const int nxt = t + NS;
+        issue(t % NS, nxt < klast ? nxt : klast);
+        ldfrag((t + 1) % NS, na, nb);
+      }
+      mma(ca, cb);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+#pragma unroll
+    for (int st = 0; st < NS; ++st) issue(st, st < klast ? st : klast);
+    wait_vm<(NS - 1) * L>();
+    __builtin_amdgcn_s_barrier();
+    short8 a0[KS][FM], b0[KS][FN], a1[KS][FM], b1[KS][FN];
+    ldfrag(0, a0, b0);
+    for (int t = 0; t < n_loc; t += 2) {
+      step(t, a0, b0, a1, b1);
+      if (t + 1 < n_loc) step(t + 1, a1, b1, a0, b0);
+    }
+  } else {
+    // ---- pipeline: stages 0..NS-2 in flight before the loop; step t waits for its
+    // own stage (NS-2 younger stages stay outstanding), passes ONE raw barrier (every
+    // wave's DMA for stage t has landed, and every wave is done reading stage t-1's
+    // buffer), refills that buffer with stage t+NS-1, then computes stage t.  Past
+    // the slice end the refill re-reads the last stage into a buffer nobody reads,
+    // which keeps the vmcnt count constant (branch-free pipeline).
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) issue(s, s < klast ? s : klast);
+    for (int t0 = 0; t0 < n_loc; t0 += NS) {
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        const int t = t0 + u;
+        if (t < n_loc) {
+          wait_vm<(NS - 2) * L>();
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+          const int nxt = t + NS - 1;
+          issue((u + NS - 1) % NS, nxt < klast ? nxt : klast);
+          compute(u);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
   }
@@ -271,28 +332,41 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
   }
 }
 
-// wnt bit 0: non-temporal W loads; bit 1: 32-k stages (BN >= 128)
+// wnt bit 0: non-temporal W loads; bit 1: 32-k stages (BN >= 128); bit 2:
+// register-pipelined fragment reads (BN <= 128, 64-k stages)
 template <int BN, int MODE>
 int launch_bn(void* out, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int ldo,
               int wnt, hipStream_t s) {
   const int ntiles = MODE == 1 ? N / (BN / 2) : N / BN;
   const dim3 grid(ntiles * S * ((M + 255) / 256)), block(512);
-  const bool nt = wnt & 1, bk32 = wnt & 2;
+  const bool nt = wnt & 1, bk32 = wnt & 2, pipe = wnt & 4;
+  if (bk32 && pipe) return -22;
   if constexpr (BN >= 128) {
     if (bk32) {
       if (nt)
-        tgemm_kernel<BN, MODE, 1, 32><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+        tgemm_kernel<BN, MODE, 1, 32, 0><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
       else
-        tgemm_kernel<BN, MODE, 0, 32><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+        tgemm_kernel<BN, MODE, 0, 32, 0><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
       return (int)hipGetLastError();
     }
   } else {
     if (bk32) return -21;
   }
+  if constexpr (BN <= 128) {
+    if (pipe) {
+      if (nt)
+        tgemm_kernel<BN, MODE, 1, 64, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+      else
+        tgemm_kernel<BN, MODE, 0, 64, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+      return (int)hipGetLastError();
+    }
+  } else {
+    if (pipe) return -23;
+  }
   if (nt)
-    tgemm_kernel<BN, MODE, 1, 64><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+    tgemm_kernel<BN, MODE, 1, 64, 0><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
   else
-    tgemm_kernel<BN, MODE, 0, 64><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+    tgemm_kernel<BN, MODE, 0, 64, 0><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
   return (int)hipGetLastError();
 }
 

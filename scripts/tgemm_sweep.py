@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--out", default="gpurun_out/tgemm_sweep.json")
     ap.add_argument("--table", default="", help="merge winners into this wgemm table json")
     ap.add_argument("--min-gain", type=float, default=1.03)
+    ap.add_argument("--bk32", action="store_true", help="also try the 32-k-stage variants")
     a = ap.parse_args()
     from omnia_amd.ops.gemm_tuning import enable_tuned_gemms
 
@@ -145,7 +146,11 @@ def main():
                     elif S > K // 64 or ntiles * S > 640 or (ntiles * S < 96 and S < 16):
                         continue
                     md = mode if S == 1 and mode == 1 or cons.kind == "none" else 2
-                    for wnt in ((0, 1, 2, 3) if bn >= 128 else (0, 1)):
+                    # bit 0 nt W loads, bit 1 32-k stages (lost everywhere, --bk32),
+                    # bit 2 register-pipelined fragment reads (BN <= 128)
+                    flags = [0, 1] + ([4, 5] if bn <= 128 else []) + \
+                        ([2, 3] if a.bk32 and bn >= 128 else [])
+                    for wnt in flags:
                         outb = (torch.empty(S, M, rows, device="cuda") if md == 2 else
                                 torch.empty(M, N, device="cuda", dtype=torch.bfloat16))
 

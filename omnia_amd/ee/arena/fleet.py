@@ -50,6 +50,9 @@ class FleetSession:
     async def turn(self, content: str, metadata: dict | None = None,
                    tool_result=lambda name, args: {"ok": True}) -> dict:
         t0 = time.perf_counter()
+        from ...utils.arrivals import mark
+
+        mark("client_send")
         await self.ws.send_json({"type": "message", "content": content,
                                  "metadata": metadata or {}})
         ttft, text, usage = None, [], {}

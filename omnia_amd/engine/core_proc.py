@@ -124,6 +124,9 @@ class _Core:
         eng = self.eng
         if op == "add":
             from .sampling_params import SamplingParams
+            from ..utils.arrivals import mark
+
+            mark("engine_add")
 
             _, rid, ids, params, sid = m
             try:
@@ -413,6 +416,9 @@ class EngineCoreClient:
         rid = request_id or f"r{next(self._rid)}"
         q = _Chan()
         self._chans[rid] = (loop, q)
+        from ..utils.arrivals import mark
+
+        mark("runtime_submit")
         _send(self.sock, ["add", rid, list(prompt), dataclasses.asdict(params), session_id],
               self._wlock)
         done = False

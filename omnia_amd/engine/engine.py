@@ -755,6 +755,9 @@ class AsyncLLMEngine:
 
     async def generate(self, prompt, params: SamplingParams | None = None,
                        session_id: str | None = None, request_id: str | None = None):
+        from ..utils.arrivals import mark
+
+        mark("runtime_submit")
         loop = asyncio.get_running_loop()
         q = _Chan()
         holder = {}

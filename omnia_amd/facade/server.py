@@ -34,6 +34,7 @@ from dataclasses import dataclass, field
 
 from aiohttp import WSMsgType, web
 
+from ..utils.arrivals import mark
 from ..api.proto import runtime_v1 as pb
 from ..observability import metrics as M
 from ..observability import tracing
@@ -450,6 +451,8 @@ class _Connection:
 
     async def on_message(self, msg: dict):
         t = msg["type"]
+        if t == P.MESSAGE:
+            mark("facade_msg")
         if t == P.HANGUP:
             return "hangup"
         if t == P.TOOL_RESULT:

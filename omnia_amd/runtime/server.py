@@ -23,6 +23,7 @@ import logging
 import time
 import uuid
 
+from ..utils.arrivals import mark
 from ..api.proto import runtime_v1 as pb
 from ..observability import metrics as M
 from ..observability import tracing
@@ -255,6 +256,7 @@ class RuntimeService:
             self.active_streams -= 1
 
     async def _turn(self, stream: Stream, msg, md: dict, pending: list):
+        mark("runtime_turn")
         sid = msg.session_id or md.get("x-omnia-session-id") or uuid.uuid4().hex
         content = msg.content
         parts = []

@@ -17,3 +17,6 @@ for mb in 2048 0; do
   rc=$?; echo "open-loop mixed_budget=$mb rc=$rc"; tail -1 $O/ol_mb$mb.log | summ
   [ $rc -eq 0 ] || exit $rc
 done
+timeout -k 10 400 python -u -m pytest tests/test_config5.py -m gpu -v -s --timeout 360 --timeout-method thread > $O/cfg5_gpu.log 2>&1
+rc=$?; echo "cfg5 gpu rc=$rc"; tail -3 $O/cfg5_gpu.log
+exit $rc

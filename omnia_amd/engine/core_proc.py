@@ -191,6 +191,9 @@ class _Core:
         from ..utils.pyprof import maybe_start
 
         maybe_start("engine-core")
+        from ..utils.proc_tune import tune_serving_process
+
+        tune_serving_process()
         eng = self.eng
         mc = eng.model_cfg
         _send(self.sock, ["ready", {"model": mc.name, "vocab": mc.vocab_size,

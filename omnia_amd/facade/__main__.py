@@ -21,6 +21,9 @@ async def main():
     client = await dial_runtime(env.get("OMNIA_RUNTIME_ADDRESS", "127.0.0.1:9000"))
     fac = build_facade(env, client)
     await fac.start("0.0.0.0", int(env.get("OMNIA_FACADE_PORT", 8080)))
+    from ..utils.proc_tune import tune_serving_process
+
+    tune_serving_process()
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
     for sig in (signal.SIGTERM, signal.SIGINT):

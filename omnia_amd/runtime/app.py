@@ -217,6 +217,9 @@ async def run(cfg: RuntimeConfig | None = None):
     svc = await build_runtime(cfg)
     server, gport = await serve_grpc(svc, cfg.grpc_port)
     runner, hport = await serve_health(svc, cfg.health_port)
+    from ..utils.proc_tune import tune_serving_process
+
+    tune_serving_process()
     log.info("runtime %s/%s serving gRPC :%d health :%d (provider %s)", cfg.namespace,
              cfg.agent_name, gport, hport, svc.agent.provider.type)
     stop = asyncio.Event()

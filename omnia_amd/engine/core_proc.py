@@ -32,6 +32,7 @@ core is started as a child process (never an exec of a GPU-initialised one).
 from __future__ import annotations
 
 import asyncio
+import collections
 import dataclasses
 import itertools
 import logging
@@ -99,6 +100,7 @@ class _Core:
         self.stop = False
         self.faults: list = []
         self.fatal = False
+        self._wlock = threading.Lock()
 
     # -- engine callbacks (engine thread == this thread)
     def _on_token(self, s, tok, text):
@@ -147,7 +149,7 @@ class _Core:
                 val = self._call(name, arg)
             except Exception as e:  # noqa: BLE001
                 val = {"error": str(e)}
-            _send(self.sock, ["reply", qid, val])
+            _send(self.sock, ["reply", qid, val], self._wlock)
         elif op == "stop":
             self.stop = True
 
@@ -199,21 +201,39 @@ class _Core:
         _send(self.sock, ["ready", {"model": mc.name, "vocab": mc.vocab_size,
                                     "kv_blocks": eng.blocks.num_blocks,
                                     "device": str(eng.device), "pid": os.getpid()}])
-        self.sock.setblocking(False)
-        fd = self.sock.fileno()
+        # A reader thread drains the socket while this thread sits in GPU waits:
+        # read only between steps, a burst of new requests (256 prompts at a
+        # wave start) filled the socket buffer during a 100+ ms prefill step and
+        # the runtime's send blocked its event loop until the step ended.
+        inbox: collections.deque = collections.deque()
+        wake = threading.Event()
+        gone = threading.Event()
+
+        def reader():
+            try:
+                while True:
+                    data = self.sock.recv(1 << 20)
+                    if not data:
+                        break
+                    msgs = self.frames.feed(data)
+                    if msgs:
+                        inbox.extend(msgs)
+                        wake.set()
+            except OSError:
+                pass
+            gone.set()
+            wake.set()
+
+        threading.Thread(target=reader, name="omnia-core-inbox", daemon=True).start()
         while not self.stop:
             busy = eng.has_work()
-            r, _, _ = select.select([fd], [], [], 0 if busy else 0.05)
-            if r:
-                try:
-                    data = self.sock.recv(1 << 20)
-                except BlockingIOError:
-                    data = None
-                if data == b"":
-                    break  # client went away
-                if data:
-                    for m in self.frames.feed(data):
-                        self._handle(m)
+            if not busy and not inbox:
+                wake.wait(0.05)
+            wake.clear()
+            while inbox:
+                self._handle(inbox.popleft())
+            if gone.is_set() and not inbox:
+                break  # client went away
             if eng.has_work():
                 try:
                     eng.step()
@@ -230,9 +250,7 @@ class _Core:
                 toks = [[rid, "".join(e[0]), e[1], e[2]] for rid, e in self.tok_out.items()]
                 fins, self.fin_out = self.fin_out, []
                 self.tok_out = {}
-                self.sock.setblocking(True)
-                _send(self.sock, ["out", toks, fins])
-                self.sock.setblocking(False)
+                _send(self.sock, ["out", toks, fins], self._wlock)
         eng.shutdown()
 
 

@@ -690,8 +690,19 @@ class ModelRunner:
                 self._decode_body(nrows, ncols)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.graph_pool):
-            self._decode_body(nrows, ncols)
+        # no cyclic-GC pass inside the capture: a collection there can run the
+        # deleter of a device tensor from an earlier step (a free on a capturing
+        # stream), which aborts the process
+        import gc
+
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                self._decode_body(nrows, ncols)
+        finally:
+            if gc_was:
+                gc.enable()
         torch.cuda.synchronize()
         self.out_tok.copy_(saved)
         self.tok_slots.copy_(saved_slots)

@@ -224,12 +224,29 @@ class _Core:
             gone.set()
             wake.set()
 
-        threading.Thread(target=reader, name="omnia-core-inbox", daemon=True).start()
+        threaded = os.environ.get("OMNIA_CORE_INBOX_THREAD", "1") != "0"
+        if threaded:
+            threading.Thread(target=reader, name="omnia-core-inbox", daemon=True).start()
+        else:
+            self.sock.setblocking(False)
+        fd = self.sock.fileno()
         while not self.stop:
             busy = eng.has_work()
-            if not busy and not inbox:
-                wake.wait(0.05)
-            wake.clear()
+            if threaded:
+                if not busy and not inbox:
+                    wake.wait(0.05)
+                wake.clear()
+            else:  # read only between steps (A/B switch)
+                r, _, _ = select.select([fd], [], [], 0 if busy else 0.05)
+                if r:
+                    try:
+                        data = self.sock.recv(1 << 20)
+                    except BlockingIOError:
+                        data = None
+                    if data == b"":
+                        gone.set()
+                    elif data:
+                        inbox.extend(self.frames.feed(data))
             while inbox:
                 self._handle(inbox.popleft())
             if gone.is_set() and not inbox:
@@ -250,7 +267,11 @@ class _Core:
                 toks = [[rid, "".join(e[0]), e[1], e[2]] for rid, e in self.tok_out.items()]
                 fins, self.fin_out = self.fin_out, []
                 self.tok_out = {}
+                if not threaded:
+                    self.sock.setblocking(True)
                 _send(self.sock, ["out", toks, fins], self._wlock)
+                if not threaded:
+                    self.sock.setblocking(False)
         eng.shutdown()
 
 

@@ -11,6 +11,8 @@ import time
 
 import aiohttp
 
+from ...utils.arrivals import mark
+
 
 class FleetSession:
     """One virtual user's WebSocket conversation.  ``http``: a shared
@@ -50,8 +52,6 @@ class FleetSession:
     async def turn(self, content: str, metadata: dict | None = None,
                    tool_result=lambda name, args: {"ok": True}) -> dict:
         t0 = time.perf_counter()
-        from ...utils.arrivals import mark
-
         mark("client_send")
         await self.ws.send_json({"type": "message", "content": content,
                                  "metadata": metadata or {}})
@@ -78,6 +78,7 @@ class FleetSession:
                                                                tc.get("arguments"))}})
             elif t == "done":
                 lat = time.perf_counter() - t0
+                mark("client_done")
                 if ttft is None:
                     ttft = lat
                 final = f.get("content") or "".join(text)

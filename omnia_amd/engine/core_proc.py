@@ -267,6 +267,11 @@ class _Core:
                 toks = [[rid, "".join(e[0]), e[1], e[2]] for rid, e in self.tok_out.items()]
                 fins, self.fin_out = self.fin_out, []
                 self.tok_out = {}
+                if fins:
+                    from ..utils.arrivals import mark
+
+                    for _ in fins:
+                        mark("engine_finish")
                 if not threaded:
                     self.sock.setblocking(True)
                 _send(self.sock, ["out", toks, fins], self._wlock)

@@ -13,6 +13,7 @@ import asyncio
 import json
 import time
 
+from ..utils.arrivals import mark
 from ..api.proto import runtime_v1 as pb
 from . import protocol as P
 
@@ -123,6 +124,7 @@ class RuntimeHandler:
                              "cost_usd": round(d.usage.cost_usd, 8)}
                     parts = [{"type": p.type, "text": p.text} for p in d.parts] or None
                     out.update(content=d.final_content, usage=usage)
+                    mark("facade_done")
                     await writer.write(P.done(session_id, d.final_content, parts, usage))
                     return out
                 elif kind == "error":

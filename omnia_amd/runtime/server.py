@@ -298,6 +298,7 @@ class RuntimeService:
                                                               message=GENERIC_ERROR)))
             return
         tracing.end_span(span)
+        mark("runtime_done")
         await stream.send(pb.ServerMessage(done=pb.Done(
             final_content=res.content,
             usage=pb.Usage(input_tokens=res.usage.input_tokens,

@@ -89,3 +89,41 @@ def test_abort_on_consumer_exit_and_errors(client):
         if st["counters"]["decode_tokens"] < 400 and client.call("has_session", "none") is False:
             break
     assert st["counters"]["decode_tokens"] < 400
+
+
+@pytest.mark.timeout(240)
+def test_request_burst_never_blocks_the_client_during_a_stalled_step():
+    """A wave's burst of new prompts arrives while the core sits in a long step
+    (here a 3 s simulated hang).  The core's inbox thread keeps draining the
+    socket, so the client's sends (made on the serving event loop) return at
+    once instead of blocking until the step ends."""
+    import time
+
+    c = EngineCoreClient(EngineConfig(**CFG), env={
+        "OMNIA_FAILPOINT": "engine.hang:once", "OMNIA_FAILPOINT_HANG_S": "3"})
+    try:
+        async def go():
+            # first request trips the hang inside the core's next step
+            first = asyncio.ensure_future(_drain(c, list(range(5, 60)), 2))
+            await asyncio.sleep(0.5)
+            big = list(range(256, 512)) * 2  # in-vocab 3-byte msgpack ids: ~1-1.3 KB/frame
+            t0 = time.perf_counter()
+            tasks = [asyncio.ensure_future(_drain(c, big[: 300 + i % 150], 1))
+                     for i in range(400)]
+            await asyncio.sleep(0)  # every generate() has sent its add
+            sent = time.perf_counter() - t0
+            await asyncio.gather(first, *tasks)
+            return sent
+
+        sent = asyncio.run(go())
+        assert sent < 1.0, f"client sends blocked for {sent:.2f}s behind the stalled step"
+    finally:
+        c.shutdown()
+
+
+async def _drain(c, prompt, n):
+    out = []
+    async for ev in c.generate(prompt, SamplingParams(temperature=0, max_tokens=n,
+                                                      ignore_eos=True)):
+        out.append(ev)
+    return out

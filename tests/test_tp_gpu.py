@@ -60,8 +60,8 @@ def _sharded_weights(mc, rank, world, keep_full: bool):
     dt, d, D = torch.bfloat16, mc.hidden_size, mc.head_dim
 
     def init(shape, std):
-        t = torch.empty(shape, dtype=torch.float32, device="cuda").normal_(0.0, std, generator=g)
-        return t.to(dt)
+        # drawn straight in bf16: no fp32 temporary (8 ranks share the card)
+        return torch.empty(shape, dtype=dt, device="cuda").normal_(0.0, std, generator=g)
 
     host = lambda t: t.detach().to("cpu", torch.float32)  # noqa: E731
     embed = init((mc.vocab_size, d), 0.02)
@@ -152,6 +152,9 @@ def test_tp_engine_on_one_gpu_matches_dense_oracle(world):
     from conftest import release_gpu_memory
 
     release_gpu_memory()  # engines / cached blocks earlier tests left in this process
+    free, total = torch.cuda.mem_get_info()
+    print(f"TP={world}: {free / 2**30:.1f} of {total / 2**30:.1f} GiB free before spawning; "
+          f"this process reserves {torch.cuda.memory_reserved() / 2**30:.1f} GiB", flush=True)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -165,7 +168,12 @@ def test_tp_engine_on_one_gpu_matches_dense_oracle(world):
             p.join(timeout=90)
             if p.is_alive():
                 p.kill()
-    assert status == "ok", res
+    if status != "ok":
+        import subprocess
+
+        smi = subprocess.run(["rocm-smi", "--showpids"], capture_output=True, text=True,
+                             timeout=30).stdout
+        raise AssertionError(f"{res}\nGPU processes:\n{smi}")
     print(f"TP={world}: {res}")
     assert res["ar_err"] == 0
     assert res["hit"] > 0 and res["graph_replays"] > 0 and res["captures"] > 0

@@ -171,7 +171,21 @@ async def serve(port: int, manifests: list[str], engine: bool, host: str = "127.
     await runner.setup()
     await web.TCPSite(runner, host, port).start()
     print(f"omnia single-node operator on http://{host}:{port} (gpus={gpus})", flush=True)
-    await asyncio.Event().wait()
+    # SIGTERM / SIGINT: stop every pod before exiting -- pods run in their own
+    # sessions, so an abrupt exit would orphan them (engines holding GPU memory)
+    import signal
+
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(sig, stop.set)
+    await stop.wait()
+    print("omnia serve: stopping pods", flush=True)
+    try:
+        await launcher.stop()
+    finally:
+        await mgr.stop()
+        await runner.cleanup()
 
 
 async def run_operator(kubeconfig: str | None, in_cluster: bool, leader_elect: bool,

@@ -33,6 +33,7 @@ readiness) is recorded on the Deployment status (``coldStartSeconds``) and as
 from __future__ import annotations
 
 import asyncio
+import threading
 import json
 import logging
 import os
@@ -119,6 +120,9 @@ class LocalLauncher:
     def __init__(self, store: APIStore, engine_factory=None, use_grpc: bool = False,
                  mode: str = "inproc", gpu_count: int = 0):
         self.store = store
+        self._starting: set = set()
+        self._stopping = False
+        self._start_lock = threading.Lock()
         self.pods: dict[tuple, Pod] = {}
         self.replicas: dict[tuple, list] = {}  # process mode: key -> [_ProcReplica]
         self.services: dict[tuple, tuple] = {}  # (ns, name) -> (ServiceProcess, hash)
@@ -535,11 +539,25 @@ class LocalLauncher:
         import time
 
         t0 = time.perf_counter()
+        # pods being started are tracked so stop() can kill one mid-start (an
+        # executor thread keeps starting it after the sync task is cancelled)
+        with self._start_lock:
+            if self._stopping:
+                self.devices.release(who)
+                raise RuntimeError("launcher stopping")
+            self._starting.add(pod)
         try:
             pod.start(timeout_s=float(os.environ.get("OMNIA_POD_START_TIMEOUT", "900")))
         except Exception:
             self.devices.release(who)
             raise
+        finally:
+            with self._start_lock:
+                self._starting.discard(pod)
+        if self._stopping:
+            pod.stop()
+            self.devices.release(who)
+            raise RuntimeError("launcher stopping")
         cold = time.perf_counter() - t0
         self.cold_start_s[key] = cold
         from ..observability import metrics as M
@@ -696,19 +714,31 @@ class LocalLauncher:
         self.task = asyncio.ensure_future(self.run())
 
     async def stop(self):
+        with self._start_lock:
+            self._stopping = True
+            starting = list(self._starting)
         if self.task is not None:
             self.task.cancel()
             await asyncio.gather(self.task, return_exceptions=True)
+        loop = asyncio.get_running_loop()
+        await asyncio.gather(*(loop.run_in_executor(None, p.stop) for p in starting),
+                             return_exceptions=True)
+        for _ in range(300):  # start threads notice the stop and clean up their pods
+            with self._start_lock:
+                if not self._starting:
+                    break
+            await asyncio.sleep(0.1)
         for p in list(self.pods.values()):
             await p.stop()
         self.pods.clear()
         for act in list(self.activators.values()):
             await act.stop()
         self.activators.clear()
-        for key, reps in list(self.replicas.items()):
-            for r in reps:
-                await r.stop()
-                self.devices.release((key, r.index))
+        # replicas stop concurrently: each pod drains its facade for up to 15 s
+        reps = [(key, r) for key, rs in list(self.replicas.items()) for r in rs]
+        await asyncio.gather(*(r.stop() for _, r in reps), return_exceptions=True)
+        for key, r in reps:
+            self.devices.release((key, r.index))
         self.replicas.clear()
         for sp, _ in self.services.values():
             sp.stop()

@@ -69,8 +69,12 @@ def test_omnia_serve_llama3_8b_streams_a_websocket_turn(tmp_path):
                 t2 = await fs.turn("And the weather in Lisbon?")
             return st, t1, t2
 
+    import psutil
+
+    pods = []
     try:
         st, t1, t2 = asyncio.run(go())
+        pods = psutil.Process(proc.pid).children(recursive=True)  # pod process trees
     finally:
         os.killpg(proc.pid, signal.SIGTERM)
         try:
@@ -79,6 +83,10 @@ def test_omnia_serve_llama3_8b_streams_a_websocket_turn(tmp_path):
             os.killpg(proc.pid, signal.SIGKILL)
             proc.wait(10)
         log.close()
+    # SIGTERM stopped every pod (they run in their own sessions: an abrupt exit of
+    # the operator would orphan engine-cores holding most of the GPU's memory)
+    gone, alive = psutil.wait_procs(pods, timeout=20)
+    assert not alive, [p.cmdline()[:4] for p in alive]
     for t in (t1, t2):
         assert t["usage"].get("output_tokens", 0) > 0 and t["usage"].get("input_tokens", 0) > 0
         assert len(t["chunk_times_s"]) >= 1

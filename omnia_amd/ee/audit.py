@@ -28,6 +28,7 @@ EVENT_TYPES = (
     "session_created", "session_accessed", "session_searched", "session_exported",
     "session_deleted", "pii_redacted", "memory_write_blocked", "decryption_requested",
     "memory_created", "memory_accessed", "memory_deleted", "memory_exported",
+    "memory_consolidated",
 )
 
 

@@ -607,6 +607,15 @@ def main(argv=None):
     ap.add_argument("--access-touch-interval", type=float,
                     default=float(os.environ.get("ACCESS_TOUCH_INTERVAL", "1.0")),
                     help="seconds per batched access-count flush; 0 = one update per read")
+    ap.add_argument("--consolidation-interval",
+                    default=os.environ.get("CONSOLIDATION_INTERVAL", ""),
+                    help="EE consolidation worker tick (e.g. 1m); per-axis cron schedules "
+                         "from the policy decide what runs; empty disables")
+    ap.add_argument("--consolidation-function-url",
+                    default=os.environ.get("CONSOLIDATION_FUNCTION_URL", ""),
+                    help="base URL of the consolidation function facades (default: the "
+                         "functionRef's in-cluster Service)")
+    ap.add_argument("--policy-name", default=os.environ.get("OMNIA_MEMORY_POLICY", "default"))
     a = ap.parse_args(argv)
     from .embedding import build_embedder
     from .store import MemoryStore
@@ -686,6 +695,16 @@ def main(argv=None):
         else:
             log.error("invalid compaction interval %r: worker disabled", a.compaction_interval)
 
+    consolidation = None
+    if a.consolidation_interval and a.enterprise and policy:
+        from ..ee.consolidation import ConsolidationWorker, FunctionClient
+        from ..utils.durations import parse_duration
+
+        consolidation = ConsolidationWorker(
+            store, [(a.policy_name, policy)], workspaces=lambda _p: store.list_workspace_ids(),
+            client=FunctionClient(base_url=a.consolidation_function_url),
+            interval_s=parse_duration(a.consolidation_interval))
+
     async def start_workers(app):
         app["workers"] = [asyncio.create_task(ReembedWorker(svc, a.reembed_interval).run()),
                           asyncio.create_task(RetentionWorker(svc, policy=policy).run())]
@@ -701,6 +720,8 @@ def main(argv=None):
             app["workers"].append(asyncio.create_task(compaction.run()))
         if tombstone is not None:
             app["workers"].append(asyncio.create_task(tombstone.run()))
+        if consolidation is not None:
+            app["workers"].append(asyncio.create_task(consolidation.run()))
 
     async def stop_workers(app):
         for t in app.get("workers", []):

@@ -525,50 +525,32 @@ def build_app(svc: MemoryService, enterprise: bool = False, chunk_size: int = 20
 
 
 def _project(svc: MemoryService, ws: str, user: str | None) -> dict:
-    """Memory Galaxy: 2-D PCA of the workspace's vectors (dense basis) or of
-    hashed term vectors (lexical basis); PII-category points are masked
-    server-side before serialisation (SERVICE.md "Memory Galaxy")."""
-    import torch
+    """Memory Galaxy (``ee/pkg/memory/projection``): the stored layout the
+    projection worker rendered for this scope when there is one, else a live
+    render (dense basis when >= 70 % of the rows carry embeddings, otherwise
+    TF-IDF/LSA; PCA below 30 points, t-SNE on the device above).  PII-category
+    points are masked server-side before serialisation (SERVICE.md "Memory
+    Galaxy")."""
+    from ..ee import projection as P
 
-    from .embedding import HashEmbedder
-
-    mems = svc.store.list({SCOPE_WORKSPACE: ws, **({SCOPE_USER: user} if user else {})},
-                          limit=5000, strict=bool(user))
-    if not mems:
+    inputs = P.gather_inputs(svc.store, ws, user)
+    if not inputs:
         return {"points": [], "basis": "none"}
-    idx = svc.indexes.get(ws)
-    vecs, basis = [], "dense"
-    for m in mems:
-        v = idx.get(m.observation_id) if idx is not None else None
-        if v is None:
-            basis = "lexical"
-            break
-        vecs.append(v)
-    if basis == "lexical":
-        he = HashEmbedder(256)
-        vecs = [torch.tensor(he._vec(m.content)) for m in mems]
-    X = torch.stack(vecs).float()
-    X = X - X.mean(0, keepdim=True)
-    if X.shape[0] >= 2:
-        _, _, V = torch.pca_lowrank(X, q=min(2, X.shape[1]), center=False)
-        P = X @ V[:, :2]
-    else:
-        P = torch.zeros(1, 2)
-    if P.shape[1] < 2:
-        P = torch.cat([P, torch.zeros(P.shape[0], 2 - P.shape[1])], 1)
+    stored = P.ProjectionStore(svc.store).load(P.scope_key(ws, user))
+    res = P.from_stored(stored, inputs) if stored else P.project(inputs)
+    if stored and not res["points"]:
+        res = P.project(inputs, stored.get("coords"))
+    cats = {i.entity_id: i.category for i in inputs}
     pts = []
-    for m, (x, y) in zip(mems, P.tolist()):
-        p = {"x": x, "y": y, "tier": m.tier, "confidence": m.confidence,
-             "created_at": m.to_json()["created_at"]}
-        if m.metadata.get(META_CONSENT_CATEGORY) in PII_CATEGORIES:
-            p["masked"] = True
+    for p in res["points"]:
+        if cats.get(p["id"]) in PII_CATEGORIES:
+            pts.append({"x": p["x"], "y": p["y"], "tier": p["tier"],
+                        "confidence": p["confidence"], "masked": True})
         else:
-            p.update(id=m.id, title=m.title, preview=m.content[:120], type=m.type,
-                     category=m.metadata.get(META_CONSENT_CATEGORY, ""),
-                     user=m.scope.get(SCOPE_USER, ""))
-        pts.append(p)
-    M.MEMORY_OPS.labels(op="projection", status=basis).inc()
-    return {"points": pts, "basis": basis}
+            pts.append(p)
+    M.MEMORY_OPS.labels(op="projection", status=res["basis"]).inc()
+    res["points"] = pts
+    return res
 
 
 def main(argv=None):
@@ -615,6 +597,9 @@ def main(argv=None):
                     default=os.environ.get("CONSOLIDATION_FUNCTION_URL", ""),
                     help="base URL of the consolidation function facades (default: the "
                          "functionRef's in-cluster Service)")
+    ap.add_argument("--projection-interval",
+                    default=os.environ.get("PROJECTION_INTERVAL", "5m"),
+                    help="Memory Galaxy render check period (policy spec.projection)")
     ap.add_argument("--policy-name", default=os.environ.get("OMNIA_MEMORY_POLICY", "default"))
     a = ap.parse_args(argv)
     from .embedding import build_embedder
@@ -705,6 +690,15 @@ def main(argv=None):
             client=FunctionClient(base_url=a.consolidation_function_url),
             interval_s=parse_duration(a.consolidation_interval))
 
+    projection = None
+    if a.enterprise and policy and (policy.get("projection") or {}).get("enabled"):
+        from ..ee.projection import ProjectionWorker
+        from ..utils.durations import parse_duration
+
+        projection = ProjectionWorker(store, [(a.policy_name, policy)],
+                                      workspaces=lambda _p: store.list_workspace_ids(),
+                                      interval_s=parse_duration(a.projection_interval))
+
     async def start_workers(app):
         app["workers"] = [asyncio.create_task(ReembedWorker(svc, a.reembed_interval).run()),
                           asyncio.create_task(RetentionWorker(svc, policy=policy).run())]
@@ -722,6 +716,8 @@ def main(argv=None):
             app["workers"].append(asyncio.create_task(tombstone.run()))
         if consolidation is not None:
             app["workers"].append(asyncio.create_task(consolidation.run()))
+        if projection is not None:
+            app["workers"].append(asyncio.create_task(projection.run()))
 
     async def stop_workers(app):
         for t in app.get("workers", []):

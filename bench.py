@@ -450,6 +450,7 @@ def run(a, drv, ws, rank, use_gpu, host_only):
     sync()
     t0 = time.perf_counter()
     results = []
+    wave_ms = []  # this rank's per-wave wall time (closed loop)
     if a.arrival == "poisson":
         if a.rate <= 0:
             raise SystemExit("--arrival poisson needs --rate > 0 (turns/s per replica)")
@@ -457,7 +458,9 @@ def run(a, drv, ws, rank, use_gpu, host_only):
     else:
         prof = _client_profiler()
         for k in range(a.steps):
+            tw = time.perf_counter()
             results.extend(drv.wave(k))
+            wave_ms.append(round(1000 * (time.perf_counter() - tw), 1))
     sync()
     elapsed = time.perf_counter() - t0
     if a.arrival != "poisson" and prof is not None:
@@ -518,6 +521,7 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             "p95_tpot_ms": ms(pct(tpot, 0.95)),
             "p95_frame_gap_ms": ms(pct(gaps, 0.95)),
             "turns": len(lats),
+            "wave_ms": wave_ms,
             "config": {
                 "model": a.model,
                 "global_batch": a.concurrency * (ws // a.tp),

@@ -339,8 +339,11 @@ class LLMEngine:
         if not self.handoff and (sch.waiting or sch.partial):
             return False
         # every running sequence can take its next token's page without a
-        # preemption (never preempt a sequence whose tokens are in flight)
-        return self.blocks.num_free >= len(sch.running) + 1
+        # preemption (never preempt a sequence whose tokens are in flight); pages
+        # of idle retained sessions count -- allocation reclaims them (LRU) on the
+        # host without touching in-flight work, so a pool full of parked
+        # multi-turn sessions does not drop the engine out of pipelined steps
+        return self.blocks.num_available >= len(sch.running) + 1
 
     @property
     def handoff(self) -> bool:

@@ -57,6 +57,7 @@ class BlockManager:
         self.num_blocks = num_blocks
         self.free: list[int] = list(range(num_blocks - 1, 0, -1))  # block 0 reserved
         self.sessions: "OrderedDict[str, SessionKV]" = OrderedDict()
+        self.idle_blocks = 0  # pages held by parked (evictable) sessions
         self.swap = swap
         self.stats = {"prefix_hit_tokens": 0, "prefix_miss_tokens": 0, "evictions": 0,
                       "swap_out": 0, "swap_in": 0}
@@ -65,6 +66,11 @@ class BlockManager:
     @property
     def num_free(self) -> int:
         return len(self.free)
+
+    @property
+    def num_available(self) -> int:
+        """Free pages plus pages an allocation may reclaim from idle sessions."""
+        return len(self.free) + self.idle_blocks
 
     def utilization(self) -> float:
         return 1.0 - len(self.free) / (self.num_blocks - 1)
@@ -76,6 +82,7 @@ class BlockManager:
         for sid, s in self.sessions.items():  # LRU order
             if not s.in_use:
                 self.sessions.pop(sid)
+                self.idle_blocks -= len(s.blocks)
                 if self.swap is not None and s.tokens and self.swap.can_hold(len(s.blocks)):
                     s.swapped = self.swap.swap_out(s.blocks)
                     self.swap.park(sid, s)
@@ -93,8 +100,7 @@ class BlockManager:
         return out
 
     def can_allocate(self, n: int) -> bool:
-        avail = len(self.free) + sum(len(s.blocks) for s in self.sessions.values() if not s.in_use)
-        return avail >= n
+        return self.num_available >= n
 
     def release(self, blocks: list[int]) -> None:
         self.free.extend(blocks)
@@ -109,7 +115,9 @@ class BlockManager:
             self.stats["prefix_miss_tokens"] += len(prompt)
             return [], 0
         s = self.sessions.pop(session_id, None)
-        if s is None and self.swap is not None:
+        if s is not None:
+            self.idle_blocks -= len(s.blocks)
+        elif self.swap is not None:
             s = self.swap.unpark(session_id)
             if s is not None:
                 try:
@@ -140,14 +148,17 @@ class BlockManager:
             return
         old = self.sessions.pop(session_id, None)
         if old is not None:
+            self.idle_blocks -= len(old.blocks)
             self.release(old.blocks)
         need = self.blocks_needed(len(tokens))
         self.release(blocks[need:])
         self.sessions[session_id] = SessionKV(session_id, blocks[:need], list(tokens))
+        self.idle_blocks += len(blocks[:need])
 
     def drop_session(self, session_id: str) -> bool:
         s = self.sessions.pop(session_id, None)
         if s is not None:
+            self.idle_blocks -= len(s.blocks)
             self.release(s.blocks)
         if self.swap is not None:
             p = self.swap.unpark(session_id)

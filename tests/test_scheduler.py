@@ -28,3 +28,43 @@ def test_decode_preempts_only_the_youngest():
     assert sched.running == [a] and a.preemptions == 0 and len(a.blocks) == 5
     assert b.preemptions == 1 and b.blocks == [] and b.status == SeqStatus.WAITING
     assert list(sched.waiting) == [b]
+
+
+def test_idle_session_pages_counted_and_reclaimable():
+    """``idle_blocks`` always equals the pages parked under idle sessions, and
+    ``num_available`` (free + idle) is what an allocation can reach -- the engine
+    keeps pipelining when the pool is full of parked multi-turn sessions."""
+    import random
+
+    from omnia_amd.engine.kv_manager import BlockManager
+
+    rng = random.Random(0)
+    bm = BlockManager(64, 4)
+    owned = []
+    for step in range(400):
+        op = rng.random()
+        sid = f"s{rng.randrange(12)}"
+        if op < 0.4 and bm.num_available >= 3:
+            owned.append((sid, bm.allocate(rng.randrange(1, 4))))
+        elif op < 0.7 and owned:
+            s, blocks = owned.pop(rng.randrange(len(owned)))
+            bm.retain(s, blocks, list(range(rng.randrange(0, 4 * len(blocks) + 1))))
+        elif op < 0.85:
+            blocks, _ = bm.acquire_prefix(sid, list(range(9)))
+            owned.append((sid, blocks))
+        else:
+            bm.drop_session(sid)
+        assert bm.idle_blocks == sum(len(s.blocks) for s in bm.sessions.values())
+        assert bm.num_available == bm.num_free + bm.idle_blocks
+        held = sum(len(b) for _, b in owned)
+        assert bm.num_free + bm.idle_blocks + held == 63
+    # a pool full of parked sessions still admits work
+    for _, b in owned:
+        bm.release(b)
+    i = 0
+    while bm.num_free:
+        bm.retain(f"p{i}", bm.allocate(1), [1, 2, 3])
+        i += 1
+    assert bm.num_free == 0 and bm.can_allocate(10)
+    got = bm.allocate(10)
+    assert len(got) == 10 and bm.stats["evictions"] >= 10

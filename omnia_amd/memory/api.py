@@ -289,8 +289,10 @@ def build_app(svc: MemoryService, enterprise: bool = False, chunk_size: int = 20
             seed_entity_ids=d.get("seed_entity_ids") or [],
             relation_types=d.get("relation_types") or [],
             max_graph_hops=int(d.get("max_graph_hops") or 1),
-            half_life=R.HalfLife(**{k: float(v) for k, v in hl.items()
-                                    if k in ("user", "agent", "institutional")}))
+            half_life=R.HalfLife(**{**svc.policy_half_life.__dict__,
+                                    **{k: float(v) for k, v in hl.items()
+                                       if k in ("user", "agent", "institutional")}}),
+            ranker=svc.policy_ranker)
         mems = await svc.retrieve_multi_tier(req)
         return web.json_response(_list_json(mems, preview=True,
                                             related=svc.store.related([m.id for m in mems])))
@@ -634,6 +636,10 @@ def main(argv=None):
     if a.access_touch_interval > 0:
         store.enable_touch_batching(a.access_touch_interval)
     svc = MemoryService(store, emb, publisher=pub, enterprise=a.enterprise)
+    if a.enterprise and policy:
+        # EE recall bias + per-tier decay from the workspace's MemoryPolicy
+        svc.policy_ranker = R.tier_ranker_from_policy(policy)
+        svc.policy_half_life = R.half_life_from_policy(policy)
     if a.redis_cache:
         from ..utils.resp import RedisClient
         from .cache import CachedStore

@@ -50,6 +50,45 @@ class TierRanker:
         return score * float(self.weights.get(tier, 1.0)) + float(self.boosts.get(tier, 0.0))
 
 
+def tier_ranker_from_policy(spec: dict | None) -> TierRanker:
+    """EE tier precedence (``ee/pkg/memory/tier_ranking.go``): MemoryPolicy
+    ``tierPrecedence.multiplicative.{institutional,agent,user}`` weights (decimal
+    strings, default 1.0); user-for-agent rows take the user weight.  A weight
+    that does not parse makes the whole ranker the identity (fail open to the
+    unbiased score, as the reference does)."""
+    mult = ((spec or {}).get("tierPrecedence") or {}).get("multiplicative")
+    if not mult:
+        return TierRanker()
+    w = {Tier.INSTITUTIONAL: 1.0, Tier.AGENT: 1.0, Tier.USER: 1.0}
+    for tier in (Tier.INSTITUTIONAL, Tier.AGENT, Tier.USER):
+        raw = mult.get(tier)
+        if raw in (None, ""):
+            continue
+        try:
+            w[tier] = float(raw)
+        except (TypeError, ValueError):
+            return TierRanker()
+    w[Tier.USER_FOR_AGENT] = w[Tier.USER]
+    return TierRanker(weights=w)
+
+
+def half_life_from_policy(spec: dict | None) -> HalfLife:
+    """``recall.halfLife.{user,agent,institutional}`` durations ("90d", "720h");
+    missing, malformed or non-positive values keep the 30-day default."""
+    from ..utils.durations import parse_duration
+
+    hl = HalfLife()
+    cfg = (((spec or {}).get("recall") or {}).get("halfLife")) or {}
+    for tier in ("user", "agent", "institutional"):
+        try:
+            v = parse_duration(cfg.get(tier) or "")
+        except ValueError:
+            continue
+        if v > 0:
+            setattr(hl, tier, v)
+    return hl
+
+
 def recency_decay(age_s: float, half_life_s: float) -> float:
     if half_life_s <= 0:
         return 1.0

@@ -46,6 +46,8 @@ class MemoryService:
         self.classify_pii = classify_pii
         self.device = device
         self.indexes: dict[str, VectorIndex] = {}
+        self.policy_ranker = None  # EE: retrieval.tier_ranker_from_policy
+        self.policy_half_life = R.HalfLife()
         self.embed_model = getattr(embedder, "model", "") if embedder else ""
         self.vec_seq = 0  # last memory_vector_log row this replica's indexes applied
         self.cache = None  # optional CachedStore (Redis) for list / search reads

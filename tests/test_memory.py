@@ -462,3 +462,29 @@ def test_redaction_strategies_and_trust():
     assert find_pii("call 555-123-4567") == {"phone_number"}
     assert classify("she lives in Paris") == "memory:location"
     assert classify("nothing here") == ""
+
+
+def test_policy_tier_precedence_and_half_life():
+    """EE tier ranking (``ee/pkg/memory/tier_ranking.go``) from a MemoryPolicy."""
+    r = R.tier_ranker_from_policy({"tierPrecedence": {"multiplicative": {
+        "institutional": "2.0", "user": "0.5"}}})
+    assert r.adjust(1.0, "institutional") == 2.0 and r.adjust(1.0, "agent") == 1.0
+    assert r.adjust(1.0, "user") == 0.5 and r.adjust(1.0, "user_for_agent") == 0.5
+    bad = R.tier_ranker_from_policy({"tierPrecedence": {"multiplicative": {"user": "x"}}})
+    assert bad.adjust(3.0, "user") == 3.0  # unparsable -> identity
+    assert R.tier_ranker_from_policy(None).adjust(3.0, "agent") == 3.0
+    hl = R.half_life_from_policy({"recall": {"halfLife": {"user": "7d", "agent": "bogus",
+                                                          "institutional": "720h"}}})
+    assert hl.user == 7 * R.DAY and hl.agent == 30 * R.DAY and hl.institutional == 30 * R.DAY
+    # the ranker reorders a real retrieval: institutional outranks an equal user row
+    st = MemoryStore()
+    st.save(mem("the office opens at nine", user="u1"))
+    st.save(mem("the office opens at nine", user=None), require_user=False)
+    req = MultiTierRequest(workspace_id=WS, user_id="u1", query="office",
+                           ranker=R.tier_ranker_from_policy({"tierPrecedence": {
+                               "multiplicative": {"institutional": "3"}}}))
+    got = st.retrieve_multi_tier(req)
+    assert [m.tier for m in got][:2] == ["institutional", "user"]
+    req.ranker = R.tier_ranker_from_policy({"tierPrecedence": {"multiplicative": {
+        "user": "3"}}})
+    assert [m.tier for m in st.retrieve_multi_tier(req)][:2] == ["user", "institutional"]

@@ -291,7 +291,8 @@ class MemoryChecker:
                 Check("MemoryUserOwnership", "Memory", self.ownership),
                 Check("MemoryUserIsolation", "Memory", self.isolation),
                 Check("MemoryDelete", "Memory", self.delete),
-                Check("ConsolidationWorkerRunning", "Memory", self.worker)]
+                Check("ConsolidationWorkerRunning", "Memory", self.worker),
+                Check("ConsolidationPassesHealthy", "Memory", self.passes)]
 
     @property
     def base(self) -> str:
@@ -396,6 +397,29 @@ class MemoryChecker:
                 return passed(f"{name} worker running") if vals[name] == 1 else \
                     failed(f"{name} worker not running (gauge={vals[name]:g})")
         return skipped("consolidation worker not enabled (gauge series absent)")
+
+    async def passes(self) -> TestResult:
+        """Consolidation pass outcomes (``omnia_memory_consolidation_passes_total``
+        by status): failing passes with no successful one mean the function or
+        the applier is broken for every workspace."""
+        if (r := self._need()) is not None:
+            return r
+        st, body = await _get(self.base + "/metrics")
+        if st != 200:
+            return failed(f"metrics HTTP {st}")
+        by: dict = {}
+        for m in re.finditer(r'^omnia_memory_consolidation_passes_total\{([^}]*)\} ([0-9.e+]+)$',
+                             body, re.M):
+            sm = re.search(r'status="([a-z_]+)"', m.group(1))
+            if sm:
+                by[sm.group(1)] = by.get(sm.group(1), 0.0) + float(m.group(2))
+        if not by:
+            return skipped("no consolidation passes yet")
+        good = by.get("ok", 0) + by.get("empty", 0)
+        bad = {k: v for k, v in by.items() if k not in ("ok", "empty") and v}
+        if bad and not good:
+            return failed("every pass failed: " + ", ".join(f"{k}={v:g}" for k, v in bad.items()))
+        return passed(f"{good:g} good passes" + (f", failures {bad}" if bad else ""))
 
 
 # ------------------------------------------------------------------ privacy

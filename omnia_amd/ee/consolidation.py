@@ -819,6 +819,49 @@ class FunctionClient:
         return unmarshal_actions(body)
 
 
+# ------------------------------------------------------------------ listers
+def workspace_opts_into(ws_obj: dict, policy_name: str) -> bool:
+    """A Workspace takes part in a policy's passes when one of its service
+    groups' memory block references the policy (``workspace_lister.go``)."""
+    for sg in ((ws_obj or {}).get("spec") or {}).get("services") or []:
+        ref = ((sg or {}).get("memory") or {}).get("policyRef") or {}
+        if ref.get("name") == policy_name:
+            return True
+    return False
+
+
+class KubePolicyLister:
+    """Cluster-scoped MemoryPolicies with a consolidation block, as
+    (name, spec) pairs, from any client with ``list(kind, ns)``
+    (``operator/kube.py`` KubeClient, or the in-repo API store)."""
+
+    def __init__(self, client):
+        self.client = client
+
+    def __call__(self) -> list:
+        return [(o["metadata"]["name"], o.get("spec") or {})
+                for o in self.client.list("MemoryPolicy", None)]
+
+
+class KubeWorkspaceLister:
+    """Only this memory-api's own Workspace, and only if it opts into the
+    policy; memory rows are keyed by the Workspace UID (its name when the object
+    carries no UID, as in single-node mode)."""
+
+    def __init__(self, client, own_workspace: str):
+        self.client, self.own = client, own_workspace
+
+    def __call__(self, policy_name: str) -> list:
+        if not self.own:
+            return []
+        getter = getattr(self.client, "try_get", None)
+        w = getter("Workspace", self.own, None) if getter else \
+            self.client.get("Workspace", self.own, None)
+        if not w or not workspace_opts_into(w, policy_name):
+            return []
+        return [w["metadata"].get("uid") or w["metadata"]["name"]]
+
+
 # ------------------------------------------------------------------ worker
 def resolved_schedule(spec: dict, axis: str) -> str:
     c = (spec or {}).get("consolidation") or {}

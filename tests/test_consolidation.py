@@ -373,3 +373,32 @@ def test_consolidation_example_manifests_admitted():
     assert C.resolved_schedule(pol, C.AXIS_CROSS_SCOPE) == "0 */6 * * *"
     assert C.resolved_schedule(pol, C.AXIS_ENTITY_DUPES) == "0 2 * * *"
     assert C.resolved_timeouts(pol) == (30.0, 600.0)
+
+
+def test_cluster_listers():
+    class FakeClient:
+        objs = {("MemoryPolicy", "pol"): {"metadata": {"name": "pol"}, "spec": POLICY},
+                ("MemoryPolicy", "plain"): {"metadata": {"name": "plain"}, "spec": {}},
+                ("Workspace", "team-a"): {"metadata": {"name": "team-a", "uid": "uid-a"},
+                                          "spec": {"services": [
+                                              {"name": "default", "memory": {
+                                                  "policyRef": {"name": "pol"}}}]}}}
+
+        def list(self, kind, ns=None):
+            return [o for (k, _), o in self.objs.items() if k == kind]
+
+        def try_get(self, kind, name, ns=None):
+            return self.objs.get((kind, name))
+
+    c = FakeClient()
+    pols = C.KubePolicyLister(c)()
+    assert [n for n, _ in pols] == ["pol", "plain"]
+    assert C.KubeWorkspaceLister(c, "team-a")("pol") == ["uid-a"]
+    assert C.KubeWorkspaceLister(c, "team-a")("plain") == []
+    assert C.KubeWorkspaceLister(c, "missing")("pol") == []
+    assert C.KubeWorkspaceLister(c, "")("pol") == []
+    # the worker skips policies without a consolidation block
+    w = C.ConsolidationWorker(MemoryStore(), C.KubePolicyLister(c),
+                              workspaces=C.KubeWorkspaceLister(c, "team-a"), device="cpu")
+    assert asyncio.run(w.run_once()) == [{"workspace": "uid-a", "axis": C.AXIS_CROSS_SCOPE,
+                                          "status": "anchored"}]

@@ -1,14 +1,15 @@
 """``python -m omnia_amd.facade`` -- the facade container entrypoint.
 
 Dials the runtime sidecar over gRPC (retrying until ready), serves WebSocket /
-REST functions (+ A2A / MCP when enabled) and drains gracefully on SIGTERM
+REST functions (+ A2A / MCP when enabled), and the management-plane twin
+(18080 / 19999 / 19998) behind its mgmt-only chain when the operator allocated it and drains gracefully on SIGTERM
 (in-flight turns finish, new connections refused, ``omnia_facade_draining`` = 1)."""
 import asyncio
 import logging
 import os
 import signal
 
-from .app import build_facade, dial_runtime
+from .app import build_facade, dial_runtime, start_facade, stop_facade
 from ..observability.logging import configure as configure_logging
 
 
@@ -20,7 +21,7 @@ async def main():
     env = dict(os.environ)
     client = await dial_runtime(env.get("OMNIA_RUNTIME_ADDRESS", "127.0.0.1:9000"))
     fac = build_facade(env, client)
-    await fac.start("0.0.0.0", int(env.get("OMNIA_FACADE_PORT", 8080)))
+    await start_facade(fac, env)
     from ..utils.proc_tune import tune_serving_process
 
     tune_serving_process()
@@ -29,8 +30,7 @@ async def main():
     for sig in (signal.SIGTERM, signal.SIGINT):
         loop.add_signal_handler(sig, stop.set)
     await stop.wait()
-    await fac.drain()
-    await fac.stop()
+    await stop_facade(fac)
 
 
 if __name__ == "__main__":

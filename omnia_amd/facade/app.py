@@ -10,8 +10,15 @@
   OMNIA_HANDLER_MODE (runtime|echo|demo), OMNIA_INPUT_SCHEMA / OMNIA_OUTPUT_SCHEMA
   auth: OMNIA_AUTH_SHARED_TOKEN, OMNIA_AUTH_CLIENT_KEYS (json {id: sha256}),
         OMNIA_OIDC_ISSUER / OMNIA_OIDC_AUDIENCE / OMNIA_OIDC_HS256_SECRET /
-        OMNIA_OIDC_JWKS_FILE, OMNIA_EDGE_TRUST=true, OMNIA_MGMT_PLANE_KEY,
+        OMNIA_OIDC_JWKS_FILE, OMNIA_EDGE_TRUST=true,
         OMNIA_AUTH_ALLOW_ANONYMOUS (default true when no validator is configured)
+  management-plane twin (cmd/agent/websocket.go:148-153, mgmt_plane.go:46-71):
+        OMNIA_INTERNAL_FACADE_PORT (18080) / OMNIA_INTERNAL_A2A_PORT (19999) /
+        OMNIA_INTERNAL_MCP_PORT (19998): the same routes served a second time
+        behind a chain holding ONLY the mgmt-plane validator (RS256 JWTs from
+        OMNIA_MGMT_PLANE_JWKS_URL, agent / workspace claims checked against
+        OMNIA_AGENT_NAME / OMNIA_WORKSPACE_NAME); never anonymous.  The public
+        chain never accepts mgmt-plane tokens.
   recording: OMNIA_SESSION_API_URL (+ OMNIA_RECORDING_WORKERS / _QUEUE)
   media: OMNIA_MEDIA_STORAGE=local|s3|gcs|azure (+ OMNIA_MEDIA_ROOT / _BUCKET / ...)
   limits: OMNIA_MAX_CONNECTIONS, OMNIA_MSG_RATE, OMNIA_MSG_BURST, OMNIA_DRAIN_TIMEOUT
@@ -21,15 +28,14 @@ from __future__ import annotations
 import json
 import os
 
-from .auth import (AuthChain, ClientKeyValidator, EdgeTrustValidator, MgmtPlaneValidator,
-                   OIDCValidator, SharedTokenValidator)
+from .auth import (AuthChain, ClientKeyValidator, EdgeTrustValidator, JWKSResolver,
+                   MgmtPlaneValidator, OIDCValidator, SharedTokenValidator)
 from .server import FacadeConfig, FacadeServer
 
 
 def auth_from_env(env) -> AuthChain:
+    """The public listener's chain: data-plane validators only."""
     vs = []
-    if env.get("OMNIA_MGMT_PLANE_KEY"):
-        vs.append(MgmtPlaneValidator(env["OMNIA_MGMT_PLANE_KEY"].encode()))
     if env.get("OMNIA_AUTH_SHARED_TOKEN"):
         vs.append(SharedTokenValidator(env["OMNIA_AUTH_SHARED_TOKEN"]))
     if env.get("OMNIA_AUTH_CLIENT_KEYS"):
@@ -53,6 +59,42 @@ def auth_from_env(env) -> AuthChain:
                                      if peers != "*" else None))
     anon = env.get("OMNIA_AUTH_ALLOW_ANONYMOUS", "true" if not vs else "false").lower() == "true"
     return AuthChain(vs, allow_anonymous=anon)
+
+
+def mgmt_auth_from_env(env, resolver: JWKSResolver | None = None) -> AuthChain:
+    """The twin listeners' chain: the mgmt-plane validator alone, strict."""
+    url = env.get("OMNIA_MGMT_PLANE_JWKS_URL", "")
+    vs = []
+    if url or resolver is not None:
+        vs.append(MgmtPlaneValidator(resolver or JWKSResolver(url),
+                                     expected_agent=env.get("OMNIA_AGENT_NAME", ""),
+                                     expected_workspace=env.get("OMNIA_WORKSPACE_NAME", "")))
+    return AuthChain(vs, allow_anonymous=False, strict=True)
+
+
+def internal_ports(env) -> list[int]:
+    """Twin listener ports the operator allocated (0 / unset = none)."""
+    out = []
+    for k in ("OMNIA_INTERNAL_FACADE_PORT", "OMNIA_INTERNAL_A2A_PORT", "OMNIA_INTERNAL_MCP_PORT"):
+        try:
+            p = int(env.get(k, "") or 0)
+        except ValueError:
+            p = 0
+        if p > 0 and p not in out:
+            out.append(p)
+    return out
+
+
+def public_ports(env, port: int) -> list[int]:
+    out = [port]
+    for k in ("OMNIA_A2A_PORT", "OMNIA_MCP_PORT"):
+        try:
+            p = int(env.get(k, "") or 0)
+        except ValueError:
+            p = 0
+        if p > 0 and p not in out:
+            out.append(p)
+    return out
 
 
 def config_from_env(env) -> FacadeConfig:
@@ -79,7 +121,8 @@ def config_from_env(env) -> FacadeConfig:
     return c
 
 
-def build_facade(env, runtime_client, recorder=None) -> FacadeServer:
+def build_facade(env, runtime_client, recorder=None, mgmt_resolver=None) -> FacadeServer:
+    """The public facade; ``.internal`` is its management-plane twin (or None)."""
     handler = None
     mode = env.get("OMNIA_HANDLER_MODE", "runtime")
     if mode in ("echo", "demo"):
@@ -101,22 +144,28 @@ def build_facade(env, runtime_client, recorder=None) -> FacadeServer:
     cfg.media_enabled = cfg.media_enabled or media is not None
     from .realtime import route_store_from_env
 
-    fac = FacadeServer(cfg, handler=handler, runtime_client=runtime_client,
-                       auth=auth_from_env(env), recorder=recorder, media_store=media,
-                       routes=route_store_from_env(env))  # OMNIA_ROUTE_REDIS_URL
-    if media is not None:
-        from ..media import mount_media
-
-        mount_media(fac.app, media)
+    routes = route_store_from_env(env)  # OMNIA_ROUTE_REDIS_URL
     types = set(filter(None, env.get("OMNIA_FACADE_TYPES", "").split(",")))
-    if "a2a" in types:
-        from .a2a import mount_a2a
 
-        mount_a2a(fac, runtime_client)
-    if "mcp" in types or env.get("OMNIA_MCP_ENABLED", "").lower() == "true":
-        from .mcp import mount_mcp
+    def make(auth: AuthChain) -> FacadeServer:
+        f = FacadeServer(cfg, handler=handler, runtime_client=runtime_client, auth=auth,
+                         recorder=recorder, media_store=media, routes=routes)
+        if media is not None:
+            from ..media import mount_media
 
-        mount_mcp(fac, runtime_client)
+            mount_media(f.app, media)
+        if "a2a" in types:
+            from .a2a import mount_a2a
+
+            mount_a2a(f, runtime_client)
+        if "mcp" in types or env.get("OMNIA_MCP_ENABLED", "").lower() == "true":
+            from .mcp import mount_mcp
+
+            mount_mcp(f, runtime_client)
+        return f
+
+    fac = make(auth_from_env(env))
+    fac.internal = make(mgmt_auth_from_env(env, mgmt_resolver)) if internal_ports(env) else None
     return fac
 
 
@@ -140,3 +189,21 @@ async def dial_runtime(address: str, attempts: int = 30, delay_s: float = 1.0):
 
 def env() -> dict:
     return dict(os.environ)
+
+
+async def start_facade(fac: FacadeServer, env, host: str = "0.0.0.0") -> dict:
+    """Bind the public listener(s) and the twin's; returns {name: bound port}."""
+    port = int(env.get("OMNIA_FACADE_PORT", 8080))
+    bound = {"facade": await fac.start(host, port, extra_ports=public_ports(env, port)[1:])}
+    if getattr(fac, "internal", None) is not None:
+        ports = internal_ports(env)
+        bound["facade-mgmt"] = await fac.internal.start(host, ports[0], extra_ports=ports[1:])
+    return bound
+
+
+async def stop_facade(fac: FacadeServer) -> None:
+    await fac.drain()
+    if getattr(fac, "internal", None) is not None:
+        await fac.internal.drain()
+        await fac.internal.stop()
+    await fac.stop()

@@ -241,30 +241,149 @@ class EdgeTrustValidator:
                         claims=claims, role=claims["role"])
 
 
-class MgmtPlaneValidator:
-    """Dashboard-minted HS256 JWTs on the management twin ports (mgmt_plane.go)."""
+MGMT_ISSUER = "omnia-dashboard"  # pkg/facade/auth/mgmt_plane.go DefaultMgmtPlaneIssuer
+MGMT_AUDIENCE = "omnia-facade"
+ORIGIN_MGMT = "management-plane"  # pkg/policy/identity.go OriginManagementPlane
 
-    def __init__(self, key: bytes, audience: str = "omnia-facade"):
-        self.key = key
-        self.audience = audience
+
+class JWKSResolver:
+    """Signing keys of the management plane by ``kid`` (``auth.JWKSResolver``).
+
+    Keys come from ``url`` (the dashboard's ``/api/auth/jwks``), fetched lazily
+    and re-fetched on an unknown ``kid`` at most every ``min_refresh_s`` (key
+    rotation without hammering the dashboard), or from a static ``jwks`` dict.
+    A fetch failure resolves to no key, i.e. an invalid credential."""
+
+    def __init__(self, url: str | None = None, jwks: dict | None = None,
+                 min_refresh_s: float = 2.0, timeout_s: float = 3.0, fetch=None):
+        if not url and jwks is None:
+            raise ValueError("mgmt-plane: JWKS URL required")
+        self.url = url
+        self.min_refresh_s = min_refresh_s
+        self.timeout_s = timeout_s
+        self._fetch = fetch or self._http_fetch
+        self._keys: dict = {}
+        self._last = float("-inf")
+        if jwks is not None:
+            self._load(jwks)
+
+    def _load(self, jwks: dict) -> None:
+        self._keys = {k.get("kid", ""): k for k in (jwks or {}).get("keys", [])
+                      if k.get("kty") == "RSA"}
+
+    def _http_fetch(self) -> dict:
+        import urllib.request
+
+        with urllib.request.urlopen(self.url, timeout=self.timeout_s) as r:
+            return json.loads(r.read())
+
+    def resolve(self, kid: str) -> dict | None:
+        k = self._keys.get(kid)
+        if k is not None or not self.url:
+            return k
+        now = time.monotonic()
+        if now - self._last < self.min_refresh_s:
+            return None
+        self._last = now
+        try:
+            self._load(self._fetch())
+        except Exception:  # noqa: BLE001 - dashboard down / DNS: invalid credential
+            return None
+        return self._keys.get(kid)
+
+
+class MgmtPlaneValidator:
+    """Dashboard-minted RS256 JWTs on the management-plane twin listeners only
+    (``pkg/facade/auth/mgmt_plane.go``): issuer ``omnia-dashboard``, audience
+    ``omnia-facade``, ``exp`` required, ``kid`` resolved through the JWKS,
+    claim ``origin == "management-plane"``, and when the facade knows its agent
+    / workspace a token naming another one is refused."""
+
+    def __init__(self, resolver: JWKSResolver, issuer: str = MGMT_ISSUER,
+                 audience: str = MGMT_AUDIENCE, expected_agent: str = "",
+                 expected_workspace: str = ""):
+        self.resolver = resolver
+        self.blocking = bool(resolver.url)
+        self.issuer, self.audience = issuer, audience
+        self.expected_agent, self.expected_workspace = expected_agent, expected_workspace
 
     def validate(self, headers, query, peer):
-        tok = bearer(headers) or query.get("mgmt_token")
-        if not tok or tok.count(".") != 2:
+        tok = bearer(headers)
+        if tok is None:
             return None
+        if not tok or tok.count(".") != 2:
+            raise AuthError("invalid credential: malformed bearer")
         try:
-            claims = jwt_decode(tok, self.key, None, None, self.audience)
-        except AuthError:
-            return None  # let other validators try (it may be an OIDC token)
-        return Identity("mgmt-plane", subject=str(claims.get("sub", "")),
-                        workspace=str(claims.get("workspace", "")), claims=claims,
-                        role=str(claims.get("role", "")))
+            hdr = json.loads(_b64url_dec(tok.split(".")[0]))
+        except Exception as e:  # noqa: BLE001
+            raise AuthError("invalid credential: malformed header") from e
+        if hdr.get("alg") != "RS256":
+            raise AuthError(f"unexpected signing method {hdr.get('alg')!r}")
+        kid = hdr.get("kid") or ""
+        if not kid:
+            raise AuthError("mgmt-plane JWT missing kid header")
+        key = self.resolver.resolve(kid)
+        if key is None:
+            raise AuthError("invalid credential: unknown signing key")
+        claims = jwt_decode(tok, None, {"keys": [key]}, self.issuer, self.audience)
+        if "exp" not in claims:
+            raise AuthError("invalid credential: exp required")
+        if claims.get("origin") != ORIGIN_MGMT:
+            raise AuthError(f"origin {claims.get('origin')!r} is not management-plane")
+        agent, ws = str(claims.get("agent") or ""), str(claims.get("workspace") or "")
+        if self.expected_agent and agent and agent != self.expected_agent:
+            raise AuthError(f"token agent {agent!r} does not match {self.expected_agent!r}")
+        if self.expected_workspace and ws and ws != self.expected_workspace:
+            raise AuthError(f"token workspace {ws!r} does not match {self.expected_workspace!r}")
+        sub = str(claims.get("sub", ""))
+        return Identity(ORIGIN_MGMT, subject=sub, end_user=sub, workspace=ws, agent=agent,
+                        claims=claims, role=str(claims.get("role", "")))
+
+
+def jwk_from_private(key, kid: str) -> dict:
+    """Public JWK of an :class:`omnia_amd.utils.rsa.PrivateKey` (JWKS endpoint)."""
+    n = key.n.to_bytes((key.n.bit_length() + 7) // 8, "big")
+    e = key.e.to_bytes((key.e.bit_length() + 7) // 8, "big")
+    return {"kty": "RSA", "kid": kid, "alg": "RS256", "use": "sig",
+            "n": _b64url_enc(n), "e": _b64url_enc(e)}
+
+
+def mint_mgmt_token(key, kid: str, subject: str, agent: str = "", workspace: str = "",
+                    ttl_s: int = 300, issuer: str = MGMT_ISSUER,
+                    audience: str = MGMT_AUDIENCE, **extra) -> str:
+    """RS256 management-plane JWT as the dashboard mints it for its WS proxy and
+    the doctor (origin ``management-plane``)."""
+    from ..utils.rsa import sign_pkcs1_sha256
+
+    now = int(time.time())
+    claims = {"iss": issuer, "aud": audience, "sub": subject, "iat": now, "exp": now + ttl_s,
+              "origin": ORIGIN_MGMT, **extra}
+    if agent:
+        claims["agent"] = agent
+    if workspace:
+        claims["workspace"] = workspace
+    hdr = {"alg": "RS256", "typ": "JWT", "kid": kid}
+    h = _b64url_enc(json.dumps(hdr, separators=(",", ":")).encode())
+    p = _b64url_enc(json.dumps(claims, separators=(",", ":")).encode())
+    sig = sign_pkcs1_sha256(key, f"{h}.{p}".encode())
+    return f"{h}.{p}.{_b64url_enc(sig)}"
 
 
 class AuthChain:
-    def __init__(self, validators: list | None = None, allow_anonymous: bool = True):
+    """``strict`` chains (the management-plane twin) never admit an anonymous
+    caller, even when empty (no JWKS configured): the twin exists only for
+    dashboard-minted tokens."""
+
+    def __init__(self, validators: list | None = None, allow_anonymous: bool = True,
+                 strict: bool = False):
         self.validators = validators or []
-        self.allow_anonymous = allow_anonymous
+        self.allow_anonymous = allow_anonymous and not strict
+        self.strict = strict
+
+    @property
+    def blocking(self) -> bool:
+        """True when a validator may do network I/O (a JWKS fetch)."""
+        return any(getattr(v, "blocking", False) for v in self.validators)
 
     def authenticate(self, headers, query=None, peer: str = "") -> Identity:
         query = query or {}
@@ -272,6 +391,6 @@ class AuthChain:
             ident = v.validate(headers, query, peer)
             if ident is not None:
                 return ident
-        if self.allow_anonymous or not self.validators:
+        if self.allow_anonymous or (not self.validators and not self.strict):
             return Identity("anonymous")
         raise AuthError("unauthenticated")

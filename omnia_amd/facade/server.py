@@ -113,7 +113,8 @@ class FacadeServer:
         self.routes = routes or NoopRouteStore()
         self.parked = RealtimeRegistry(self.routes, cfg.pod_addr, cfg.grace_window_s,
                                        self._park_expired)
-        self.app = web.Application(client_max_size=cfg.max_message_bytes)
+        self.app = web.Application(client_max_size=cfg.max_message_bytes,
+                                   middlewares=[self._auth_mw])
         r = self.app.router
         r.add_get("/ws", self.ws_handler)
         r.add_get("/", self.ws_handler)
@@ -169,9 +170,30 @@ class FacadeServer:
         return web.Response(body=M.exposition(), content_type="text/plain")
 
     # ---------------------------------------------------------------- auth
-    def _authenticate(self, request):
+    async def _authenticate(self, request):
         peer = request.remote or ""
-        return self.auth.authenticate(request.headers, dict(request.query), peer)
+        args = (request.headers, dict(request.query), peer)
+        if self.auth.blocking:  # a JWKS fetch may run: keep it off the event loop
+            return await asyncio.get_running_loop().run_in_executor(
+                None, self.auth.authenticate, *args)
+        return self.auth.authenticate(*args)
+
+    # routes that authenticate themselves, and the public probes / agent card
+    _SELF_AUTH = ("/ws", "/", "/healthz", "/readyz", "/metrics",
+                  "/.well-known/agent.json", "/.well-known/agent-card.json")
+
+    @web.middleware
+    async def _auth_mw(self, request, handler):
+        """The same chain in front of every other route (A2A JSON-RPC, MCP,
+        media), so the management-plane twin serves them only to mgmt tokens."""
+        path = request.path
+        if path in self._SELF_AUTH or path.startswith("/functions/"):
+            return await handler(request)
+        try:
+            request["omnia_identity"] = await self._authenticate(request)
+        except AuthError as e:
+            return web.json_response({"error": "unauthorized", "message": str(e)}, status=401)
+        return await handler(request)
 
     def _metadata(self, ident, session_id: str, request) -> dict:
         md = {"x-omnia-agent-name": self.cfg.agent, "x-omnia-namespace": self.cfg.namespace,
@@ -194,7 +216,7 @@ class FacadeServer:
         if self.cfg.allowed_origins and origin and origin not in self.cfg.allowed_origins:
             return web.Response(status=403, text="origin not allowed")
         try:
-            ident = self._authenticate(request)
+            ident = await self._authenticate(request)
         except AuthError as e:
             return web.Response(status=401, text=str(e))
         ws = web.WebSocketResponse(heartbeat=self.cfg.ping_interval_s,
@@ -250,7 +272,7 @@ class FacadeServer:
         if not name:
             return web.json_response({"error": "missing_function_name"}, status=400)
         try:
-            ident = self._authenticate(request)
+            ident = await self._authenticate(request)
         except AuthError as e:
             return web.json_response({"error": "unauthorized", "message": str(e)}, status=401)
         try:
@@ -305,7 +327,8 @@ class FacadeServer:
                                           "X-Omnia-Duration-Ms": str(resp.duration_ms)})
 
     # ---------------------------------------------------------------- lifecycle
-    async def start(self, host: str = "0.0.0.0", port: int | None = None) -> int:
+    async def start(self, host: str = "0.0.0.0", port: int | None = None,
+                    extra_ports=()) -> int:
         # per-connection access logging is opt-in (OMNIA_ACCESS_LOG=1): a formatted
         # log record per closed session sits on the event loop exactly when a burst
         # of turns completes
@@ -319,6 +342,8 @@ class FacadeServer:
         site = web.TCPSite(self.runner, host, self.cfg.port if port is None else port,
                            backlog=max(1024, 2 * self.cfg.max_connections))
         await site.start()
+        for p in extra_ports:  # A2A / MCP ports serve the same app (dual-protocol pods)
+            await web.TCPSite(self.runner, host, p, backlog=1024).start()
         return site._server.sockets[0].getsockname()[1]
 
     async def drain(self) -> int:

@@ -15,6 +15,7 @@ shards (O, down) follow Megatron.  The reference has no model code at all
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -109,6 +110,7 @@ class LlamaModel:
         self.cos_sin = ref.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
                                         cfg.rope_scaling, device=self.device)
         self.w = weights if weights is not None else self._random_weights(seed)
+        self.fold_norms()
         self._ws = {}
         ops.dgemm_prepare(self.device)  # split-K workspace, before any graph capture
 
@@ -168,6 +170,27 @@ class LlamaModel:
             else:
                 add(v)
         return n
+
+    # RMSNorm(h) @ W^T == rsqrt(mean(h^2) + eps) * (h @ (W diag(w))^T): the norm
+    # weight folds into the consumer's weight rows once at load, after which
+    # every norm of the model is weightless.  The prefill path (pgemm.hip) then
+    # applies the row scale in the QKV / gate_up epilogue from the row sums of
+    # squares its producer (O / down residual epilogue) emits, and the decode /
+    # TP / CP paths run their existing norm kernels with a ones weight.
+    fold_post_norm = True  # Mixtral's post-attention norm also feeds the router
+
+    def fold_norms(self) -> None:
+        for layer in self.w["layers"]:
+            pairs = [("in_norm", "qkv")]
+            if self.fold_post_norm:
+                pairs.append(("post_norm", "gate_up"))
+            for nk, wk in pairs:
+                nw = layer[nk]
+                if bool(torch.all(nw == 1)):
+                    continue
+                W = layer[wk]
+                layer[wk] = (W.float() * nw.float()[None, :]).to(W.dtype)
+                layer[nk] = torch.ones_like(nw)
 
     # ------------------------------------------------------------ forward
     # Projections return either a bf16 tensor (library / gemm.hip path, not yet
@@ -298,8 +321,55 @@ class LlamaModel:
         h = ops.embedding(ids, self.w["embed"], self.vocab_start)
         return pstate.tp_all_reduce(h) if self.tp > 1 else h
 
+    # ------------------------------------------------ fused prefill (pgemm.hip)
+    use_pgemm = os.environ.get("OMNIA_PGEMM", "1") != "0"
+    PGEMM_MIN_ROWS = int(os.environ.get("OMNIA_PGEMM_MIN_ROWS", "257"))
+
+    def _use_fused(self, fb: ForwardBatch) -> bool:
+        """Pure prefill chunks on one GPU run the fused-epilogue prefill layer:
+        QKV+RoPE+KV-write, O+residual, gate_up+SwiGLU, down+residual, with the
+        RMSNorms riding the epilogues (no standalone norm / SwiGLU / RoPE launch)."""
+        if not (self.use_pgemm and self.device.type == "cuda" and not fb.is_decode
+                and not fb.num_decode and fb.cp is None and self.tp == 1):
+            return False
+        if fb.input_ids.shape[0] < self.PGEMM_MIN_ROWS:
+            return False
+        cfg, d = self.cfg, self.cfg.hidden_size
+        return (cfg.head_dim == 128 and d % 256 == 0 and d % 128 == 0
+                and (self.hq * 128) % 256 == 0 and (self.hkv * 128) % 256 == 0
+                and self.inter % 128 == 0
+                and self.fold_post_norm and not self.cfg.is_moe)
+
+    def _fused_residual(self, fb: ForwardBatch, kv: KVCache) -> torch.Tensor:
+        """Residual stream after the last layer (un-normalised) of a prefill chunk."""
+        cfg = self.cfg
+        T, d, D = fb.input_ids.shape[0], cfg.hidden_size, cfg.head_dim
+        inv_d, eps = 1.0 / d, cfg.rms_eps
+        h = self.embed(fb.input_ids)
+        ss = ops.row_sumsq(h).view(T, 1)
+        nsl = d // 256
+        ss_mid = torch.empty(T, nsl, dtype=torch.float32, device=h.device)
+        ss_out = torch.empty(T, nsl, dtype=torch.float32, device=h.device)
+        q = torch.empty(T, self.hq * D, dtype=h.dtype, device=h.device)
+        act = torch.empty(T, self.inter, dtype=h.dtype, device=h.device)
+        for li, layer in enumerate(self.w["layers"]):
+            ops.pgemm(3, h, layer["qkv"], out=q, ss_in=ss, inv_d=inv_d, eps=eps,
+                      positions=fb.positions, cos_sin=self.cos_sin, k_cache=kv.k[li],
+                      v_cache=kv.v[li], slots=fb.slots, hq=self.hq, hkv=self.hkv,
+                      block_size=kv.block_size)
+            o = ops.prefill_attention(q.view(T, self.hq, D), kv.k[li], kv.v[li], fb.block_tables,
+                                      fb.q_start_loc, fb.seq_lens, self.scale, fb.tile_seq,
+                                      fb.tile_q0)
+            ops.pgemm(2, o.view(T, self.hq * D), layer["o"], out=h, ss_out=ss_mid)
+            ops.pgemm(1, h, layer["gate_up"], out=act, ss_in=ss_mid, inv_d=inv_d, eps=eps)
+            ops.pgemm(2, act, layer["down"], out=h, ss_out=ss_out)
+            ss = ss_out  # the next QKV reads it before the next down overwrites it
+        return h
+
     def hidden_states(self, fb: ForwardBatch, kv: KVCache) -> torch.Tensor:
         cfg = self.cfg
+        if self._use_fused(fb):
+            return ops.rmsnorm(self._fused_residual(fb, kv), self.w["final_norm"], cfg.rms_eps)
         residual = self.embed(fb.input_ids)
         h = ops.rmsnorm(residual, self.w["layers"][0]["in_norm"], cfg.rms_eps)
         m = None
@@ -326,6 +396,10 @@ class LlamaModel:
         return pstate.tp_all_gather_lastdim(lg) if (self.tp > 1 and gather) else lg
 
     def forward(self, fb: ForwardBatch, kv: KVCache, gather: bool = True) -> torch.Tensor:
+        if self._use_fused(fb):
+            h = self._fused_residual(fb, kv).index_select(0, fb.logits_indices)
+            return self.logits(ops.rmsnorm(h, self.w["final_norm"], self.cfg.rms_eps), gather,
+                               False)
         h = self.hidden_states(fb, kv)
         # decode rows are their own logits rows (logits_indices is the identity)
         sel = h if fb.is_decode and fb.logits_indices.shape[0] == h.shape[0] else \

@@ -30,6 +30,8 @@ from .llama import LlamaModel, _init
 
 
 class MixtralModel(LlamaModel):
+    fold_post_norm = False  # the post-attention norm feeds the router and every expert
+
     def __init__(self, cfg, *a, ep_mode: str = "tp", **kw):
         if not cfg.is_moe:
             raise ValueError("MixtralModel needs num_experts > 0")

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import hashlib
 import json
+import os
 
 import yaml
 
@@ -127,7 +128,29 @@ def _env_list(env: dict) -> list[dict]:
     return [{"name": k, "value": str(v)} for k, v in sorted(env.items())]
 
 
-def facade_env(ar: dict) -> dict:
+def _mgmt_enabled(f: dict | None) -> bool:
+    """facades[].managementPlane, default true (agentruntime_types.go:186-192)."""
+    return f is not None and f.get("managementPlane") is not False
+
+
+def management_endpoints(ar: dict) -> dict | None:
+    """Twin listener ports per surface (``deployment_builder_management.go:84-103``):
+    the primary facade's WS twin, the A2A twin of a dual-protocol pod, the MCP twin;
+    published as ``status.managementEndpoints`` and allocated on the facade."""
+    facs = ar["spec"].get("facades", [])
+    by = {f["type"]: f for f in facs}
+    primary = facs[0] if facs else None
+    me = {}
+    if _mgmt_enabled(primary):
+        me["ws"] = MGMT_PORTS["facade-mgmt"]
+    if primary is not None and primary.get("type") != "a2a" and _mgmt_enabled(by.get("a2a")):
+        me["a2a"] = MGMT_PORTS["a2a-mgmt"]
+    if _mgmt_enabled(by.get("mcp")):
+        me["mcp"] = MGMT_PORTS["mcp-mgmt"]
+    return me or None
+
+
+def facade_env(ar: dict, mgmt_jwks_url: str | None = None) -> dict:
     spec, md = ar["spec"], ar["metadata"]
     fac = {f["type"]: f for f in spec.get("facades", [])}
     env = {"OMNIA_AGENT_NAME": md["name"], "OMNIA_NAMESPACE": md["namespace"],
@@ -163,6 +186,21 @@ def facade_env(ar: dict) -> dict:
     ctx = spec.get("context") or {}
     if ctx.get("type") == "redis" and (ctx.get("storeRef") or {}).get("url"):
         env["OMNIA_ROUTE_REDIS_URL"] = ctx["storeRef"]["url"]
+    # management-plane twin listeners + the dashboard JWKS their chain trusts
+    # (deployment_builder_env.go:124-134; empty URL = no dashboard installed)
+    me = management_endpoints(ar) or {}
+    for surface, key in (("ws", "OMNIA_INTERNAL_FACADE_PORT"), ("a2a", "OMNIA_INTERNAL_A2A_PORT"),
+                         ("mcp", "OMNIA_INTERNAL_MCP_PORT")):
+        if surface in me:
+            env[key] = str(me[surface])
+    url = os.environ.get("OMNIA_MGMT_PLANE_JWKS_URL", "") if mgmt_jwks_url is None \
+        else mgmt_jwks_url
+    if url:
+        env["OMNIA_MGMT_PLANE_JWKS_URL"] = url
+    ws = (spec.get("workspaceRef") or {}).get("name") or md.get("labels", {}).get(
+        "omnia.altairalabs.ai/workspace", "")
+    if ws:
+        env["OMNIA_WORKSPACE_NAME"] = ws
     return env
 
 
@@ -196,8 +234,10 @@ def deployment(ar: dict, rc: RuntimeConfig, pack_cm: str, track: str = "stable",
         ports.append({"name": "a2a", "containerPort": A2A_PORT})
     if "mcp" in types:
         ports.append({"name": "mcp", "containerPort": MCP_PORT})
-    for n, p in MGMT_PORTS.items():
-        ports.append({"name": n, "containerPort": p})
+    me = management_endpoints(ar) or {}
+    for surface, n in (("ws", "facade-mgmt"), ("a2a", "a2a-mgmt"), ("mcp", "mcp-mgmt")):
+        if surface in me:
+            ports.append({"name": n, "containerPort": MGMT_PORTS[n]})
     resources = dict(rt.get("resources") or {})
     if rc.provider.get("type") == "local" and rc.engine.get("device", "cuda") != "cpu":
         n = int(rc.engine.get("tp", 1))
@@ -269,6 +309,11 @@ def service(ar: dict) -> dict:
         ports.append({"name": "a2a", "port": A2A_PORT, "targetPort": A2A_PORT})
     if "mcp" in types:
         ports.append({"name": "mcp", "port": MCP_PORT, "targetPort": MCP_PORT})
+    me = management_endpoints(ar) or {}
+    for surface, n in (("ws", "facade-mgmt"), ("a2a", "a2a-mgmt"), ("mcp", "mcp-mgmt")):
+        if surface in me:  # appendManagementServicePorts (deployment_builder_management.go)
+            ports.append({"name": n, "port": MGMT_PORTS[n], "targetPort": MGMT_PORTS[n],
+                          "appProtocol": "http"})
     ports.append({"name": "metrics", "port": RUNTIME_HEALTH_PORT,
                   "targetPort": RUNTIME_HEALTH_PORT})
     sel = {LABEL_NAME: "omnia-agent", LABEL_INSTANCE: md["name"]}

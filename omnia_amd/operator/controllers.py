@@ -543,6 +543,11 @@ class AgentRuntimeReconciler:
         st["facade"] = {"endpoints": [{"type": f["type"], "url": (
             f"ws://{ep}/ws" if f["type"] == "websocket" else f"http://{ep}")}
             for f in spec.get("facades", [])]}
+        me = B.management_endpoints(ar)
+        if me:
+            st["managementEndpoints"] = me
+        else:
+            st.pop("managementEndpoints", None)
         dep_ok = st["replicas"]["ready"] > 0
         set_condition(st, "DeploymentReady", dep_ok, "Available" if dep_ok else "Progressing",
                       "", gen)

@@ -58,10 +58,13 @@ class Pod:
         self.runtime_svc = None
         self.grpc = None
         self.port = None
+        self.mgmt_port = None
         self.dir = tempfile.mkdtemp(prefix="omnia-pod-")
 
     async def stop(self):
         if self.facade is not None:
+            if getattr(self.facade, "internal", None) is not None:
+                await self.facade.internal.stop()
             await self.facade.stop()
         if self.grpc is not None:
             await self.grpc.stop(0)
@@ -219,6 +222,8 @@ class LocalLauncher:
 
         fac = build_facade(_env(cs["facade"]), client)
         pod.port = await fac.start("127.0.0.1", 0)
+        if fac.internal is not None:  # management-plane twin (dashboard / doctor)
+            pod.mgmt_port = await fac.internal.start("127.0.0.1", 0)
         pod.facade = fac
 
     # ------------------------------------------------------------ CronJobs

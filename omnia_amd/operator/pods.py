@@ -128,6 +128,13 @@ class ProcessPod:
         self.facade_port = int(self.facade_env.get("OMNIA_FACADE_PORT") or free_port())
         env = {**self.facade_env, "OMNIA_FACADE_PORT": self.facade_port,
                "OMNIA_RUNTIME_ADDRESS": f"127.0.0.1:{self.grpc_port}"}
+        # the twin / dual-protocol ports are per-pod on a shared node: remap each
+        # allocated one to a free port (pods.mgmt_ports keeps the mapping)
+        self.mgmt_ports = {}
+        for k in ("OMNIA_INTERNAL_FACADE_PORT", "OMNIA_INTERNAL_A2A_PORT",
+                  "OMNIA_INTERNAL_MCP_PORT", "OMNIA_A2A_PORT", "OMNIA_MCP_PORT"):
+            if str(env.get(k, "") or "0") not in ("", "0"):
+                env[k] = self.mgmt_ports[k] = free_port()
         self.facade = self._spawn("omnia_amd.facade", env, "facade")
 
     def log_tail(self, tag: str, n: int = 4000) -> str:

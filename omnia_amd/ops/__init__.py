@@ -290,6 +290,61 @@ def tgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, bn: int 
     return out
 
 
+def pgemm(epi: int, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
+          ss_in: torch.Tensor | None = None, inv_d: float = 0.0, eps: float = 0.0,
+          ss_out: torch.Tensor | None = None, positions=None, cos_sin=None, k_cache=None,
+          v_cache=None, slots=None, hq: int = 0, hkv: int = 0, block_size: int = 0):
+    """Prefill GEMM ``x @ w.T`` with a fused epilogue (``csrc/pgemm.hip``).
+
+    ``ss_in`` ([M, n] fp32 partial row sums of squares of ``x``) scales row r by
+    ``rsqrt(sum(ss_in[r]) * inv_d + eps)`` -- RMSNorm with the norm weight folded
+    into ``w``.  epi 0: out = scaled GEMM; 1: out = silu(g) * u with
+    ``w = [Wg; Wu]``; 2: ``out`` is the residual, updated in place (out += GEMM)
+    with ``ss_out[r, t]`` = sum of squares of its new 256-column slice t;
+    3: QKV -> RoPE'd q in ``out`` [M, hq*128], RoPE'd k and v written to the
+    paged caches at ``slots``."""
+    M, K = x.shape
+    N = w.shape[0] // 2 if epi == 1 else w.shape[0]
+    if out is None:
+        out = x.new_empty(M, hq * 128 if epi == 3 else N)
+    if x.is_cuda:
+        kernels().pgemm(epi, out, x.contiguous(), w, ss_in, inv_d, eps, ss_out, positions,
+                        cos_sin, k_cache, v_cache, slots, hq, hkv, block_size)
+        return out
+    h = x.float() @ w.float().t()
+    if ss_in is not None and epi != 2:
+        h = h * torch.rsqrt(ss_in.float().sum(1) * inv_d + eps)[:, None]
+    if epi == 0:
+        out.copy_(h.to(out.dtype))
+    elif epi == 1:
+        out.copy_((F.silu(h[:, :N]) * h[:, N:]).to(out.dtype))
+    elif epi == 2:
+        new = (out.float() + h.to(out.dtype).float()).to(out.dtype)
+        out.copy_(new)
+        ss_out.copy_(new.float().pow(2).view(M, -1, 256).sum(-1))
+    else:
+        D = 128
+        qkv = h.to(out.dtype)
+        qq = ref.apply_rope(qkv[:, : hq * D].reshape(M, hq, D), positions, cos_sin)
+        kk = ref.apply_rope(qkv[:, hq * D:(hq + hkv) * D].reshape(M, hkv, D), positions, cos_sin)
+        vv = qkv[:, (hq + hkv) * D:].reshape(M, hkv, D)
+        keep = slots >= 0
+        ref.write_kv(k_cache, v_cache, kk[keep], vv[keep], slots[keep])
+        out.copy_(qq.reshape(M, hq * D))
+    return out
+
+
+def row_sumsq(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32 [M] sums of squares of the rows of a bf16 [M, d] matrix."""
+    if out is None:
+        out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+    if x.is_cuda:
+        kernels().row_sumsq(out, x)
+        return out
+    out.copy_(x.float().pow(2).sum(1))
+    return out
+
+
 def splitk_add_rmsnorm(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
                        out: torch.Tensor | None = None) -> torch.Tensor:
     """``residual += bf16(sum_s parts[s])`` in place; returns ``RMSNorm(residual) * w``."""

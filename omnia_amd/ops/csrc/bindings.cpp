@@ -8,6 +8,11 @@
 #include <hip/hip_runtime.h>
 
 extern "C" {
+int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, int K, int ldo,
+                const float* ss_in, int ss_in_n, float inv_d, float eps, float* ss_out,
+                const int* positions, const float* cos_sin, void* k_cache, void* v_cache,
+                const int64_t* slots, int hq, int hkv, int block_size, hipStream_t s);
+int omnia_row_sumsq(float* ss, const void* x, int rows, int d, int64_t stride, hipStream_t s);
 int omnia_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows, int d,
                   int64_t x_stride, int64_t out_stride, float eps, hipStream_t s);
 int omnia_rope_kv(void* q, void* k, const void* v, const int* positions, const float* cos_sin,
@@ -506,6 +511,86 @@ void tgemm(int64_t mode, at::Tensor out, at::Tensor x, at::Tensor W, int64_t spl
            "tgemm");
 }
 
+// prefill GEMM with fused epilogues (pgemm.hip, 256x256 tiles): epi 0 plain
+// (optionally row-scaled), 1 gate_up + SwiGLU, 2 residual add + row sum of
+// squares, 3 QKV + RoPE + paged KV write.  ss_in = partial row sums of squares
+// [M, n] of x (row scale rsqrt(sum / d + eps)), ss_out = [M, N / 256].
+void pgemm(int64_t epi, at::Tensor out, at::Tensor x, at::Tensor W,
+           c10::optional<at::Tensor> ss_in, double inv_d, double eps,
+           c10::optional<at::Tensor> ss_out, c10::optional<at::Tensor> positions,
+           c10::optional<at::Tensor> cos_sin, c10::optional<at::Tensor> k_cache,
+           c10::optional<at::Tensor> v_cache, c10::optional<at::Tensor> slots, int64_t hq,
+           int64_t hkv, int64_t block_size) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(W); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && out.dim() == 2, "2-D operands");
+  TORCH_CHECK(x.is_contiguous() && W.is_contiguous(), "contiguous x / W");
+  TORCH_CHECK(out.stride(1) == 1, "out rows contiguous");
+  TORCH_CHECK(x.device() == W.device() && x.device() == out.device(), "same device");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "epi");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(W.size(1) == K, "K mismatch");
+  TORCH_CHECK(epi != 1 || W.size(0) % 2 == 0, "gate_up rows even");
+  const int N = epi == 1 ? W.size(0) / 2 : W.size(0);
+  TORCH_CHECK(out.size(0) == M, "out rows");
+  TORCH_CHECK(out.size(1) == (epi == 3 ? hq * 128 : N), "out [M, N] (q [M, hq*128] for epi 3)");
+  const float* ssi = nullptr;
+  int ssn = 0;
+  if (ss_in.has_value() && ss_in->defined()) {
+    TORCH_CHECK(ss_in->scalar_type() == at::kFloat && ss_in->is_contiguous() && ss_in->dim() == 2 &&
+                ss_in->size(0) == M && ss_in->device() == x.device(), "ss_in fp32 [M, n]");
+    ssi = ss_in->data_ptr<float>();
+    ssn = ss_in->size(1);
+  }
+  float* sso = nullptr;
+  if (epi == 2) {
+    TORCH_CHECK(ss_out.has_value() && ss_out->defined(), "epi 2 needs ss_out");
+    TORCH_CHECK(ss_out->scalar_type() == at::kFloat && ss_out->is_contiguous() &&
+                ss_out->dim() == 2 && ss_out->size(0) == M && ss_out->size(1) == N / 256 &&
+                ss_out->device() == x.device(), "ss_out fp32 [M, N/256]");
+    sso = ss_out->data_ptr<float>();
+  }
+  const int* pos = nullptr;
+  const float* cs = nullptr;
+  void *kc = nullptr, *vc = nullptr;
+  const int64_t* sl = nullptr;
+  if (epi == 3) {
+    TORCH_CHECK(positions.has_value() && cos_sin.has_value() && k_cache.has_value() &&
+                v_cache.has_value() && slots.has_value(), "epi 3 needs rope / cache operands");
+    TORCH_CHECK(positions->scalar_type() == at::kInt && positions->numel() == M &&
+                positions->is_contiguous(), "positions int32 [M]");
+    TORCH_CHECK(cos_sin->scalar_type() == at::kFloat && cos_sin->is_contiguous() &&
+                cos_sin->dim() == 2 && cos_sin->size(1) == 128, "cos_sin f32 [P, 128]");
+    TORCH_CHECK(slots->scalar_type() == at::kLong && slots->numel() == M && slots->is_contiguous(),
+                "slots int64 [M]");
+    CHECK_BF16(*k_cache); CHECK_BF16(*v_cache);
+    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == hkv && k_cache->size(2) == block_size &&
+                k_cache->size(3) == 128 && k_cache->is_contiguous() && v_cache->is_contiguous() &&
+                v_cache->sizes() == k_cache->sizes(), "cache layout [NB, Hkv, BS, 128]");
+    for (const at::Tensor* t : {&*positions, &*cos_sin, &*k_cache, &*v_cache, &*slots})
+      TORCH_CHECK(t->device() == x.device(), "same device");
+    pos = positions->data_ptr<int>();
+    cs = cos_sin->data_ptr<float>();
+    kc = k_cache->data_ptr();
+    vc = v_cache->data_ptr();
+    sl = slots->data_ptr<int64_t>();
+  }
+  if (M == 0) return;
+  CHECK_RC(omnia_pgemm((int)epi, out.data_ptr(), x.data_ptr(), W.data_ptr(), M, N, K,
+                       out.stride(0), ssi, ssn, (float)inv_d, (float)eps, sso, pos, cs, kc, vc, sl,
+                       (int)hq, (int)hkv, (int)block_size, cur_stream()),
+           "pgemm");
+}
+
+void row_sumsq(at::Tensor ss, at::Tensor x) {
+  CHECK_GPU(x); CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x [M, d] rows contiguous");
+  TORCH_CHECK(ss.scalar_type() == at::kFloat && ss.is_contiguous() && ss.numel() == x.size(0) &&
+              ss.device() == x.device(), "ss fp32 [M]");
+  CHECK_RC(omnia_row_sumsq(ss.data_ptr<float>(), x.data_ptr(), x.size(0), x.size(1), x.stride(0),
+                           cur_stream()),
+           "row_sumsq");
+}
+
 // ------------------------------------------------- split-K consumers (splitk.hip)
 static void check_parts(const at::Tensor& p) {
   TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat && p.is_contiguous() && p.dim() == 3,
@@ -768,6 +853,8 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("wgemm", &wgemm);
   m.def("wgemm_wide", &wgemm_wide);
   m.def("tgemm", &tgemm);
+  m.def("pgemm", &pgemm);
+  m.def("row_sumsq", &row_sumsq);
   m.def("ar_twoshot", &ar_twoshot);
   m.def("ar_region_bytes", &omnia_ar_region_bytes);
   m.def("splitk_add_rmsnorm", &splitk_add_rmsnorm);

@@ -1,0 +1,473 @@
+// Prefill GEMM with fused epilogues on gfx950:  out = X[M, K] . W[N, K]^T  for
+// prefill chunks (M = hundreds to 16K rows), bf16 operands, fp32 MFMA accumulate.
+// SURVEY §2.4 K3 (QKV), K4/K5 (RoPE + paged KV write), K8 (O), K9 (SwiGLU),
+// K10 (down), K2 (residual add + RMSNorm).
+//
+// Main loop: the 256x256x64 "8-phase ping-pong" schedule (cdna_hip_programming.md
+// §5, "The 256² 8-phase template"; T1-T5):
+//   * 512 threads = 8 waves, 2 (rows) x 4 (cols); 16x16x32 bf16 MFMA; each wave
+//     owns a 64x32 piece of every 128x128 quadrant of the block tile (128x64 total,
+//     128 fp32 accumulators per lane);
+//   * a K-tile (64 k) is four 16 KB half-tiles: A0/A1 (rows 0-127 / 128-255) and
+//     B0/B1 (weight rows 0-127 / 128-255), each filled by direct LDS-DMA
+//     (global_load_lds_dwordx4, 2 per thread) with the bank XOR (chunk c of row r at
+//     c ^ (r & 7)) applied to the per-lane SOURCE address and to the reads;
+//   * two K-tile buffers (128 KB); one phase per quadrant Q(A0,B0) Q(A0,B1)
+//     Q(A1,B1) Q(A1,B0), so every half-tile is dead two phases after its last
+//     ds_read and is restaged right then: one half-tile is in flight per phase,
+//     retired by a counted `s_waitcnt vmcnt(4)` at phases 3 and 7 (never 0 in the
+//     loop), raw s_barrier (hipcc's __syncthreads() would drain the DMA);
+//   * the two wave rows run one barrier apart (ping-pong): while one wave of a
+//     SIMD issues its ds_reads and DMA, the other's 16 MFMAs run
+//     (s_setprio 1 around each MFMA cluster);
+//   * XCD-aware block order (bijective remap) with 8 m-tiles per group so the
+//     blocks resident on one XCD share W column tiles and X row tiles in its L2.
+// Epilogues (the accumulators are staged as bf16 through LDS, then every thread
+// owns whole 16-B row chunks, so the fused ops read and write coalesced rows):
+//   EPI 0  out = rs[r] * acc                                  (plain / row-scaled)
+//   EPI 1  out = silu(rs*g) * (rs*u),  W = [Wg; Wu]            (gate_up + SwiGLU)
+//   EPI 2  residual += acc  (in place), ss_out[r][tile] = sum of squares of the
+//          new bf16 residual row slice                          (O / down)
+//   EPI 3  rs-scaled QKV -> RoPE(q) to q_out, RoPE(k) and v to the paged KV cache
+// where rs[r] = rsqrt(sum_t ss_in[r][t] / d + eps): with the RMSNorm weight folded
+// into W (W' = W * diag(w), models/llama.py fold_norms), RMSNorm(h) @ W^T ==
+// rs * (h @ W'^T), so the normalisation rides the consumer's epilogue and the
+// residual's sum of squares rides the producer's -- no RMSNorm, SwiGLU or RoPE
+// launch exists in a prefill layer.
+#include <type_traits>
+
+#include "common.h"
+
+using namespace omnia;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int BK = 64;
+constexpr int HALF = 128 * BK;       // bf16 elements per half-tile (16 KB)
+constexpr int MAIN = 8 * HALF;       // 2 buffers x 4 half-tiles (128 KB)
+constexpr int SROW = 264;            // epilogue staging row stride (bf16): 528 B rows
+constexpr int STAGE = 256 * SROW;    // 132 KB staging tile
+constexpr int RS_OFF = STAGE > MAIN ? STAGE : MAIN;
+constexpr int LDS_ELEMS = RS_OFF + 2 * 256;  // + 256 fp32 row scales
+
+struct PArgs {
+  void* out;            // EPI 0/1: bf16 [M, ldo]; EPI 2: residual bf16 [M, ldo]; EPI 3: q [M, ldo]
+  const bf16_t* X;      // [M, K]
+  const bf16_t* W;      // [N, K] ([2N, K] for EPI 1)
+  int M, N, K, ldo;
+  const float* ss_in;   // [M, ss_in_n] partial sums of squares (nullptr: no row scale)
+  int ss_in_n;
+  float inv_d, eps;
+  float* ss_out;        // EPI 2: [M, N / 256]
+  const int* positions;  // EPI 3
+  const float* cos_sin;  // [max_pos, 128] = cos[64] | sin[64]
+  bf16_t* k_cache;
+  bf16_t* v_cache;       // [NB, hkv, BS, 128]
+  const int64_t* slots;  // [M] (< 0: no KV write)
+  int hq, hkv, block_size;
+};
+
+__device__ __forceinline__ float4v mfma16(short8 a, short8 b, float4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// element offset of 16-B chunk `ch` of row `row` inside a half-tile
+__device__ __forceinline__ int swz(int row, int ch) { return row * BK + ((ch ^ (row & 7)) << 3); }
+
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
+  constexpr int TN = EPI == 1 ? 128 : 256;  // output columns per block tile
+  const int ntn = p.N / TN, mtn = (p.M + 255) >> 8;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 8;
+  const int per_group = GM * ntn;
+  const int grp = bid / per_group, gm0 = grp * GM;
+  const int gsz = mtn - gm0 < GM ? mtn - gm0 : GM;
+  const int idx = bid - grp * per_group;
+  const int mt = gm0 + idx % gsz, nt = idx / gsz;
+  const int m0 = mt << 8, Mt = p.M - m0 < 256 ? p.M - m0 : 256;
+  const int K = p.K, nk = K / BK;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // ---- LDS-DMA sources: instruction i of wave w fills half-tile rows 16w + 8i + lane/8,
+  // LDS chunk lane%8 <- global chunk (lane%8) ^ (row & 7)
+  const bf16_t* src[4][2];  // [A0, A1, B0, B1][i]
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * w + 8 * i + (lane >> 3);
+    const int gch = (lane & 7) ^ (row & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int ar = m0 + h * 128 + row;
+      ar = ar < p.M ? ar : p.M - 1;  // rows past the chunk: clamped copies, never stored
+      src[h][i] = p.X + (int64_t)ar * K + gch * 8;
+      const int64_t br = EPI == 1 ? (int64_t)(h ? p.N : 0) + (int64_t)nt * 128 + row
+                                  : (int64_t)nt * 256 + h * 128 + row;
+      src[2 + h][i] = p.W + br * K + gch * 8;
+    }
+  }
+  auto issue = [&](int buf, auto HC, int kt) {
+    constexpr int hidx = decltype(HC)::value;
+    kt = kt < nk ? kt : nk - 1;  // past the end: reload the last tile into a dead slot
+    bf16_t* dst = lds + (buf * 4 + hidx) * HALF + 16 * w * BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[hidx][i] + (int64_t)kt * BK),
+                                       (lds_ptr_t)(dst + i * 512), 16, 0, 0);
+  };
+
+  float4v acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[a][b][m][n] = {0.f, 0.f, 0.f, 0.f};
+
+  short8 af[4][2], bfr[2][2];
+  auto rdA = [&](int buf, int h) {
+    const bf16_t* base = lds + (buf * 4 + h) * HALF;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        af[m][ks] = *reinterpret_cast<const short8*>(base + swz(wr * 64 + m * 16 + fr, ks * 4 + fq));
+  };
+  auto rdB = [&](int buf, int h) {
+    const bf16_t* base = lds + (buf * 4 + 2 + h) * HALF;
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        bfr[n][ks] = *reinterpret_cast<const short8*>(base + swz(wc * 32 + n * 16 + fr, ks * 4 + fq));
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+
+  // phase P (0..7) of iteration `it` (K-tiles 2it in buffer 0, 2it+1 in buffer 1):
+  //   quadrant q = P & 3 of buffer P >> 2: q0 (A0,B0) q1 (A0,B1) q2 (A1,B1) q3 (A1,B0)
+  //   DMA: P0 A1(2it+1)->1  P1 B0(2it+1)->1  P2..P5 A0,B1,A1,B0(2it+2)->0
+  //        P6,P7 A0,B1(2it+3)->1;   vmcnt(4) at P3 and P7
+  auto phase = [&](auto PC, int it) {
+    constexpr int P = decltype(PC)::value;
+    constexpr int buf = P >> 2, q = P & 3;
+    if constexpr (q == 0) {
+      rdB(buf, 0);
+      rdA(buf, 0);
+    } else if constexpr (q == 1) {
+      rdB(buf, 1);
+    } else if constexpr (q == 2) {
+      rdA(buf, 1);
+    } else {
+      rdB(buf, 0);
+    }
+    const int t0 = 2 * it;
+    if constexpr (P == 0) issue(1, I1{}, t0 + 1);
+    if constexpr (P == 1) issue(1, I2{}, t0 + 1);
+    if constexpr (P == 2) issue(0, I0{}, t0 + 2);
+    if constexpr (P == 3) issue(0, I3{}, t0 + 2);
+    if constexpr (P == 4) issue(0, I1{}, t0 + 2);
+    if constexpr (P == 5) issue(0, I2{}, t0 + 2);
+    if constexpr (P == 6) issue(1, I0{}, t0 + 3);
+    if constexpr (P == 7) issue(1, I3{}, t0 + 3);
+    if constexpr (P == 3 || P == 7) wait_vm<4>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int qa = (q == 0 || q == 1) ? 0 : 1;
+    constexpr int qb = (q == 0 || q == 3) ? 0 : 1;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[qa][qb][m][n] = mfma16(af[m][ks], bfr[n][ks], acc[qa][qb][m][n]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: K-tile 0 -> buffer 0, A0/B1 of K-tile 1 -> buffer 1
+  issue(0, I0{}, 0);
+  issue(0, I2{}, 0);
+  issue(0, I3{}, 0);
+  issue(0, I1{}, 0);
+  issue(1, I0{}, 1);
+  issue(1, I3{}, 1);
+  wait_vm<4>();
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the second wave row by one barrier
+  const int nit = nk >> 1;
+  for (int it = 0; it < nit; ++it) {
+    phase(std::integral_constant<int, 0>{}, it);
+    phase(std::integral_constant<int, 1>{}, it);
+    phase(std::integral_constant<int, 2>{}, it);
+    phase(std::integral_constant<int, 3>{}, it);
+    phase(std::integral_constant<int, 4>{}, it);
+    phase(std::integral_constant<int, 5>{}, it);
+    phase(std::integral_constant<int, 6>{}, it);
+    phase(std::integral_constant<int, 7>{}, it);
+  }
+  wait_vm<0>();  // the past-the-end reloads must land before LDS is reused
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_s_barrier();
+
+  // ---------------------------------------------------------------- epilogue
+  // lane rows: a*128 + wr*64 + m*16 + fq*4 + j ; cols: b*128 + wc*32 + n*16 + fr
+  float* rs_lds = reinterpret_cast<float*>(lds + RS_OFF);
+  const bool scaled = EPI != 2 && p.ss_in != nullptr;
+  if (scaled) {
+    if (tid < 256) {
+      int r = m0 + tid;
+      r = r < p.M ? r : p.M - 1;
+      const float* s = p.ss_in + (int64_t)r * p.ss_in_n;
+      float t = 0.f;
+      for (int i = 0; i < p.ss_in_n; ++i) t += s[i];
+      rs_lds[tid] = __builtin_amdgcn_rsqf(t * p.inv_d + p.eps);
+    }
+    __syncthreads();
+  }
+  bf16_t* stg = lds;
+  // write a 16x16 fragment's 4 rows x 1 col per lane as 2 rows x 2 cols (lane pairs
+  // swap halves), i.e. two 4-byte LDS stores per fragment
+  auto put = [&](int row0, int col, float v0, float v1, float v2, float v3) {
+    const bool odd = fr & 1;
+    const float s0 = odd ? v0 : v2, s1 = odd ? v1 : v3;
+    const float r0 = __shfl_xor(s0, 1, 64), r1 = __shfl_xor(s1, 1, 64);
+    uint32_t* d0;
+    uint32_t* d1;
+    uint32_t x0, x1;
+    if (!odd) {
+      d0 = reinterpret_cast<uint32_t*>(stg + (row0 + 0) * SROW + col);
+      d1 = reinterpret_cast<uint32_t*>(stg + (row0 + 1) * SROW + col);
+      x0 = pack_bf2(v0, r0);
+      x1 = pack_bf2(v1, r1);
+    } else {
+      d0 = reinterpret_cast<uint32_t*>(stg + (row0 + 2) * SROW + col - 1);
+      d1 = reinterpret_cast<uint32_t*>(stg + (row0 + 3) * SROW + col - 1);
+      x0 = pack_bf2(r0, v2);
+      x1 = pack_bf2(r1, v3);
+    }
+    *d0 = x0;
+    *d1 = x1;
+  };
+
+  if constexpr (EPI == 1) {
+    // gate (b = 0) and up (b = 1) of feature nt*128 + wc*32 + n*16 + fr in one lane
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int row0 = a * 128 + wr * 64 + m * 16 + fq * 4;
+        float4v rs = {1.f, 1.f, 1.f, 1.f};
+        if (scaled) rs = *reinterpret_cast<const float4v*>(rs_lds + row0);
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          float v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            v[j] = silu(acc[a][0][m][n][j] * rs[j]) * (acc[a][1][m][n][j] * rs[j]);
+          put(row0, wc * 32 + n * 16 + fr, v[0], v[1], v[2], v[3]);
+        }
+      }
+  } else {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int row0 = a * 128 + wr * 64 + m * 16 + fq * 4;
+        float4v rs = {1.f, 1.f, 1.f, 1.f};
+        if (scaled) rs = *reinterpret_cast<const float4v*>(rs_lds + row0);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const float4v v = acc[a][b][m][n];
+            put(row0, b * 128 + wc * 32 + n * 16 + fr, v[0] * rs[0], v[1] * rs[1], v[2] * rs[2],
+                v[3] * rs[3]);
+          }
+      }
+  }
+  __syncthreads();
+
+  if constexpr (EPI == 0 || EPI == 1) {
+    // coalesced copy-out: TN/8 chunks per row
+    constexpr int CPR = TN / 8;
+    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+#pragma unroll 4
+    for (int u = tid; u < 256 * CPR; u += 512) {
+      const int r = u / CPR, c = u - r * CPR;
+      if (r < Mt)
+        *reinterpret_cast<short8*>(out + (int64_t)(m0 + r) * p.ldo + (int64_t)nt * TN + c * 8) =
+            *reinterpret_cast<const short8*>(stg + r * SROW + c * 8);
+    }
+  } else if constexpr (EPI == 2) {
+    // residual += tile; 32 lanes per row (one 16-B chunk each) -> row sum of squares
+    bf16_t* res = reinterpret_cast<bf16_t*>(p.out);
+    const int c = lane & 31;
+    const int rsub = (tid >> 5);  // 16 rows per pass
+#pragma unroll 2
+    for (int r0 = 0; r0 < 256; r0 += 16) {
+      const int r = r0 + rsub;
+      float ss = 0.f;
+      if (r < Mt) {
+        bf16_t* rp = res + (int64_t)(m0 + r) * p.ldo + (int64_t)nt * 256 + c * 8;
+        const short8 g = *reinterpret_cast<const short8*>(stg + r * SROW + c * 8);
+        const short8 o = *reinterpret_cast<const short8*>(rp);
+        short8 y;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint16_t h = f2bf(bf2f((uint16_t)o[j]) + bf2f((uint16_t)g[j]));
+          const float hf = bf2f(h);
+          ss += hf * hf;
+          y[j] = (short)h;
+        }
+        *reinterpret_cast<short8*>(rp) = y;
+      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      if (c == 0 && r < Mt) p.ss_out[(int64_t)(m0 + r) * ntn + nt] = ss;
+    }
+  } else {
+    // QKV: tile columns = heads 2nt, 2nt+1 of [q | k | v]; thread job = (row, head,
+    // chunk pair c / c+8 = dims 8c..8c+7 and 64+8c..64+8c+7)
+    bf16_t* qo = reinterpret_cast<bf16_t*>(p.out);
+#pragma unroll 2
+    for (int u = tid; u < 256 * 16; u += 512) {
+      const int r = u >> 4, hh = (u >> 3) & 1, c = u & 7;
+      if (r >= Mt) continue;
+      const int t = m0 + r;
+      const int head = nt * 2 + hh;  // global head index in [q heads | k heads | v heads]
+      const short8 x1 = *reinterpret_cast<const short8*>(stg + r * SROW + hh * 128 + c * 8);
+      const short8 x2 = *reinterpret_cast<const short8*>(stg + r * SROW + hh * 128 + 64 + c * 8);
+      short8 o1 = x1, o2 = x2;
+      if (head < p.hq + p.hkv) {
+        const float* cs = p.cos_sin + (int64_t)p.positions[t] * 128;
+        const float4v c0 = *reinterpret_cast<const float4v*>(cs + c * 8);
+        const float4v c1 = *reinterpret_cast<const float4v*>(cs + c * 8 + 4);
+        const float4v s0 = *reinterpret_cast<const float4v*>(cs + 64 + c * 8);
+        const float4v s1 = *reinterpret_cast<const float4v*>(cs + 64 + c * 8 + 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float cj = j < 4 ? c0[j] : c1[j - 4], sj = j < 4 ? s0[j] : s1[j - 4];
+          const float a = bf2f((uint16_t)x1[j]), b = bf2f((uint16_t)x2[j]);
+          o1[j] = (short)f2bf(a * cj - b * sj);
+          o2[j] = (short)f2bf(b * cj + a * sj);
+        }
+      }
+      if (head < p.hq) {
+        bf16_t* d = qo + (int64_t)t * p.ldo + head * 128 + c * 8;
+        *reinterpret_cast<short8*>(d) = o1;
+        *reinterpret_cast<short8*>(d + 64) = o2;
+      } else {
+        const int64_t slot = p.slots[t];
+        if (slot >= 0) {
+          const bool isk = head < p.hq + p.hkv;
+          const int kh = isk ? head - p.hq : head - p.hq - p.hkv;
+          const int64_t blk = slot / p.block_size, off = slot - blk * p.block_size;
+          bf16_t* d = (isk ? p.k_cache : p.v_cache) +
+                      ((blk * p.hkv + kh) * p.block_size + off) * 128 + c * 8;
+          *reinterpret_cast<short8*>(d) = o1;
+          *reinterpret_cast<short8*>(d + 64) = o2;
+        }
+      }
+    }
+  }
+}
+
+// one workgroup (256 threads) per row: ss[r] = sum(x[r]^2) (layer-0 input of the
+// folded-norm prefill path: the embedding rows have no producer epilogue)
+__global__ __launch_bounds__(256) void row_sumsq_kernel(float* __restrict__ ss,
+                                                        const bf16_t* __restrict__ x, int d,
+                                                        int64_t stride) {
+  __shared__ float red[4];
+  const bf16_t* row = x + (int64_t)blockIdx.x * stride;
+  float t = 0.f;
+  for (int c = threadIdx.x * 8; c < d; c += 256 * 8) {
+    const short8 v = *reinterpret_cast<const short8*>(row + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = bf2f((uint16_t)v[j]);
+      t += f * f;
+    }
+  }
+  t = block_sum(t, red);
+  if (threadIdx.x == 0) ss[blockIdx.x] = t;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Returns 0 on success, < 0 for a shape / argument the kernel does not cover
+// (checked BEFORE any launch).
+int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, int K, int ldo,
+                const float* ss_in, int ss_in_n, float inv_d, float eps, float* ss_out,
+                const int* positions, const float* cos_sin, void* k_cache, void* v_cache,
+                const int64_t* slots, int hq, int hkv, int block_size, hipStream_t s) {
+  if (epi < 0 || epi > 3) return -1;
+  if (M < 1) return -2;
+  if (K <= 0 || K % (2 * BK)) return -3;  // whole iterations of two K-tiles
+  const int tn = epi == 1 ? 128 : 256;
+  if (N <= 0 || N % tn) return -4;
+  if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) |
+       reinterpret_cast<uintptr_t>(out)) & 15)
+    return -5;
+  if (ldo % 8 || ldo < (epi == 3 ? hq * 128 : N)) return -6;
+  if (ss_in != nullptr && ss_in_n < 1) return -7;
+  if (epi == 2 && ss_out == nullptr) return -8;
+  if (epi == 3) {
+    if (!positions || !cos_sin || !k_cache || !v_cache || !slots || block_size < 1) return -9;
+    if (hq < 1 || hkv < 1 || (hq * 128) % 256 || (hkv * 128) % 256) return -10;
+    if (N != (hq + 2 * hkv) * 128) return -11;
+    if ((reinterpret_cast<uintptr_t>(k_cache) | reinterpret_cast<uintptr_t>(v_cache)) & 15)
+      return -12;
+  }
+  const int64_t blocks = (int64_t)((M + 255) / 256) * (N / tn);
+  if (blocks > (1 << 30)) return -13;
+  PArgs a{out, (const bf16_t*)X, (const bf16_t*)W, M, N, K, ldo, ss_in, ss_in_n, inv_d, eps,
+          ss_out, positions, cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, slots, hq, hkv,
+          block_size};
+  const dim3 grid((unsigned)blocks), block(512);
+  switch (epi) {
+    case 0: pgemm_kernel<0><<<grid, block, 0, s>>>(a); break;
+    case 1: pgemm_kernel<1><<<grid, block, 0, s>>>(a); break;
+    case 2: pgemm_kernel<2><<<grid, block, 0, s>>>(a); break;
+    default: pgemm_kernel<3><<<grid, block, 0, s>>>(a); break;
+  }
+  return (int)hipGetLastError();
+}
+
+int omnia_row_sumsq(float* ss, const void* x, int rows, int d, int64_t stride, hipStream_t s) {
+  if (d % 8 || rows < 0) return -1;
+  if (rows == 0) return 0;
+  row_sumsq_kernel<<<rows, 256, 0, s>>>(ss, (const bf16_t*)x, d, stride);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -65,7 +65,8 @@ def _check(mc, w, seqs, tap, rel_tol, min_pass=1.0):
     return ok / total, worst
 
 
-def _gate(device, mc, chunk, rel_tol, min_pass=1.0, router_scale=None, **kw):
+def _gate(device, mc, chunk, rel_tol, min_pass=1.0, router_scale=None, prompt_lens=None,
+          **kw):
     rng = random.Random(7)
     torch.manual_seed(0)
     eng = _engine(device, mc, chunk, **kw)
@@ -73,7 +74,7 @@ def _gate(device, mc, chunk, rel_tol, min_pass=1.0, router_scale=None, **kw):
     if router_scale is not None:  # sharpen routing so bf16 vs fp32 top-k cannot tie
         for layer in w["layers"]:
             layer["router"].mul_(router_scale)
-    seqs = _run(eng, mc, rng)
+    seqs = _run(eng, mc, rng, **({"prompt_lens": prompt_lens} if prompt_lens else {}))
     assert eng.counters["steps_prefill"] > len(seqs)  # prompts really were chunked
     frac, worst = _check(mc, w, seqs, eng.runner.logit_tap, rel_tol)
     assert frac >= min_pass, f"{mc.name}: {frac:.3f} of rows within {rel_tol}, worst {worst:.4f}"
@@ -106,6 +107,50 @@ def test_gpu_llama3_8b_shaped_two_layers_matches_dense_oracle():
     mc = resolve("llama-3-8b").replace(name="llama-3-8b-2l", num_layers=2)
     frac, worst = _gate("cuda", mc, chunk=64, rel_tol=0.04)
     print(f"llama-3-8b-2l worst rel err {worst:.4f}")
+
+
+@pytest.mark.gpu
+def test_gpu_llama3_8b_shaped_fused_prefill_matches_dense_oracle():
+    """Prefill chunks of 512 rows run the fused-epilogue prefill layer (pgemm.hip:
+    QKV+RoPE+KV write, O/down + residual + row sumsq, gate_up + SwiGLU with the
+    folded RMSNorm row scale); decode and the second turn's 20-token prefill run
+    the split-K / tile paths.  Ragged chunk tails (600 = 512 + 88 rows) included."""
+    mc = resolve("llama-3-8b").replace(name="llama-3-8b-2l", num_layers=2)
+    frac, worst = _gate("cuda", mc, chunk=512, rel_tol=0.04, prompt_lens=(600, 300, 280))
+    print(f"llama-3-8b-2l fused prefill worst rel err {worst:.4f}")
+
+
+def test_norm_folding_is_exact_reparametrisation():
+    """fold_norms moves non-unit RMSNorm weights into the QKV / gate_up rows: the
+    dense oracle of the folded weights equals the oracle of the original ones."""
+    from omnia_amd.models.llama import LlamaModel
+
+    mc = resolve("tiny-llama")
+    torch.manual_seed(0)
+    base = LlamaModel(mc, device="cpu", seed=5)
+    orig = {"embed": base.w["embed"], "lm_head": base.w["lm_head"],
+            "final_norm": base.w["final_norm"], "layers": []}
+    for layer in base.w["layers"]:
+        l2 = {k: v.clone() for k, v in layer.items()}
+        l2["in_norm"] = (1 + 0.5 * torch.rand_like(l2["in_norm"].float())).to(l2["in_norm"].dtype)
+        l2["post_norm"] = (1 + 0.5 * torch.rand_like(l2["post_norm"].float())).to(l2["post_norm"].dtype)
+        orig["layers"].append(l2)
+    keep = {"layers": [{k: v.clone() for k, v in l.items()} for l in orig["layers"]],
+            **{k: v for k, v in orig.items() if k != "layers"}}
+    folded = LlamaModel(mc, device="cpu", seed=5, weights=orig)
+    for l in folded.w["layers"]:
+        assert bool(torch.all(l["in_norm"] == 1)) and bool(torch.all(l["post_norm"] == 1))
+    ids = list(range(100, 140))
+    want = ref.dense_forward(mc, keep, ids)
+    got = ref.dense_forward(mc, folded.w, ids)
+    err = float((got - want).abs().max() / want.abs().max())
+    assert err < 0.02, err
+    # negative control: dropping the norm weights entirely is visibly different
+    plain = {"layers": [dict(l, in_norm=torch.ones_like(l["in_norm"]),
+                             post_norm=torch.ones_like(l["post_norm"])) for l in keep["layers"]],
+             **{k: v for k, v in keep.items() if k != "layers"}}
+    bad = ref.dense_forward(mc, plain, ids)
+    assert float((bad - want).abs().max() / want.abs().max()) > 0.05
 
 
 @pytest.mark.gpu

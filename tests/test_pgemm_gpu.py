@@ -1,0 +1,142 @@
+"""Prefill GEMM with fused epilogues (ops/csrc/pgemm.hip) against fp32 PyTorch
+references of the same ops: plain / row-scaled GEMM, gate_up + SwiGLU, residual
+add + row sum of squares, QKV + RoPE + paged KV write.  Ragged M (not a multiple
+of the 256-row tile) and K > one iteration are covered; every check has a
+negative control (a deliberately wrong reference must FAIL the same tolerance)."""
+import pytest
+import torch
+
+from omnia_amd import ops
+from omnia_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rand(*shape, std=1.0, gen=None):
+    return (torch.randn(*shape, device=DEV, generator=gen) * std).to(torch.bfloat16)
+
+
+def _close(got, want, tol):
+    err = (got.float() - want.float()).abs().max().item()
+    scale = want.float().abs().max().item()
+    return err <= tol * scale, err / max(scale, 1e-30)
+
+
+@pytest.fixture(scope="module")
+def gen():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = torch.Generator(device=DEV)
+    g.manual_seed(1234)
+    return g
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 512, 128), (300, 768, 512), (1000, 1024, 1280)])
+def test_plain_and_row_scaled(gen, M, N, K):
+    x = _rand(M, K, gen=gen)
+    w = _rand(N, K, std=0.05, gen=gen)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.pgemm(0, x, w, out=out)
+    want = x.float() @ w.float().t()
+    ok, e = _close(out, want, 1e-2)
+    assert ok, e
+    # asymmetric negative control: the transposed-operand product must not match
+    bad = x.float() @ w.float().flip(0).t()
+    assert not _close(out, bad, 1e-2)[0]
+    # row scale from 3 partial sums of squares
+    ss = torch.rand(M, 3, device=DEV, generator=gen) * K
+    ops.pgemm(0, x, w, out=out, ss_in=ss, inv_d=1.0 / K, eps=1e-5)
+    rs = torch.rsqrt(ss.sum(1) / K + 1e-5)
+    ok, e = _close(out, want * rs[:, None], 1e-2)
+    assert ok, e
+    assert not _close(out, want, 1e-2)[0]
+
+
+@pytest.mark.parametrize("M,F,K", [(256, 256, 256), (517, 384, 640)])
+def test_swiglu(gen, M, F, K):
+    x = _rand(M, K, gen=gen)
+    w = _rand(2 * F, K, std=0.05, gen=gen)
+    ss = torch.rand(M, 2, device=DEV, generator=gen) * K
+    out = torch.empty(M, F, dtype=torch.bfloat16, device=DEV)
+    ops.pgemm(1, x, w, out=out, ss_in=ss, inv_d=1.0 / K, eps=1e-6)
+    rs = torch.rsqrt(ss.sum(1) / K + 1e-6)[:, None]
+    h = (x.float() @ w.float().t()) * rs
+    g, u = h[:, :F], h[:, F:]
+    want = torch.nn.functional.silu(g) * u
+    ok, e = _close(out, want, 1.5e-2)
+    assert ok, e
+    swapped = torch.nn.functional.silu(u) * g
+    assert not _close(out, swapped, 1.5e-2)[0]
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 512, 256), (389, 1024, 384)])
+def test_residual_sumsq(gen, M, N, K):
+    x = _rand(M, K, gen=gen)
+    w = _rand(N, K, std=0.05, gen=gen)
+    res = _rand(M, N, gen=gen)
+    res0 = res.clone()
+    ss = torch.full((M, N // 256), -1.0, device=DEV)
+    ops.pgemm(2, x, w, out=res, ss_out=ss)
+    g = (x.float() @ w.float().t()).to(torch.bfloat16)
+    want = (res0.float() + g.float()).to(torch.bfloat16)
+    ok, e = _close(res, want, 1e-2)
+    assert ok, e
+    want_ss = want.float().pow(2).view(M, N // 256, 256).sum(-1)
+    ok, e = _close(ss, want_ss, 1e-3)
+    assert ok, e
+    assert not _close(res, res0, 1e-2)[0]
+
+
+def test_qkv_rope_kv_write(gen):
+    hq, hkv, D, bs = 8, 2, 128, 16
+    M, K = 300, 512
+    N = (hq + 2 * hkv) * D
+    x = _rand(M, K, gen=gen)
+    w = _rand(N, K, std=0.05, gen=gen)
+    ss = torch.rand(M, 1, device=DEV, generator=gen) * K
+    positions = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int32, generator=gen)
+    cos_sin = ref.rope_cos_sin(8192, D, 5e5, {"rope_type": "llama3", "factor": 8.0}, device=DEV)
+    nb = 64
+    kc = torch.zeros(nb, hkv, bs, D, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    perm = torch.randperm(nb * bs, device=DEV, generator=gen)[:M]
+    slots = perm.to(torch.int64)
+    slots[5] = -1  # padding row: no KV write
+    q = torch.empty(M, hq * D, dtype=torch.bfloat16, device=DEV)
+    ops.pgemm(3, x, w, out=q, ss_in=ss, inv_d=1.0 / K, eps=1e-5, positions=positions,
+              cos_sin=cos_sin, k_cache=kc, v_cache=vc, slots=slots, hq=hq, hkv=hkv,
+              block_size=bs)
+    rs = torch.rsqrt(ss.sum(1) / K + 1e-5)[:, None]
+    qkv = ((x.float() @ w.float().t()) * rs).to(torch.bfloat16)
+    qq = ref.apply_rope(qkv[:, : hq * D].view(M, hq, D), positions, cos_sin)
+    kk = ref.apply_rope(qkv[:, hq * D:(hq + hkv) * D].view(M, hkv, D), positions, cos_sin)
+    vv = qkv[:, (hq + hkv) * D:].view(M, hkv, D)
+    ok, e = _close(q.view(M, hq, D), qq, 2e-2)
+    assert ok, e
+    unrotated = qkv[:, : hq * D]
+    assert not _close(q, unrotated, 2e-2)[0]
+    kc_want = torch.zeros_like(kc)
+    vc_want = torch.zeros_like(vc)
+    keep = slots >= 0
+    ref.write_kv(kc_want, vc_want, kk[keep], vv[keep], slots[keep])
+    ok, e = _close(kc, kc_want, 2e-2)
+    assert ok, e
+    ok, e = _close(vc, vc_want, 2e-2)
+    assert ok, e
+
+
+def test_row_sumsq(gen):
+    x = _rand(333, 4096, gen=gen)
+    ss = torch.empty(333, device=DEV)
+    ops.row_sumsq(x, out=ss)
+    ok, e = _close(ss, x.float().pow(2).sum(1), 1e-4)
+    assert ok, e
+
+
+def test_rejects_bad_shapes(gen):
+    x = _rand(256, 192, gen=gen)  # K not a multiple of 128
+    w = _rand(256, 192, gen=gen)
+    with pytest.raises(RuntimeError):
+        ops.pgemm(0, x, w, out=torch.empty(256, 256, dtype=torch.bfloat16, device=DEV))

@@ -43,6 +43,16 @@ def build_runner(a) -> Runner:
                                                                           a.operator_url))
     r.register(redis_check(a.redis_url), gpu_check())
     headers = dict(h.split(":", 1) for h in a.header) if a.header else {}
+    if a.mgmt_signing_key:
+        # the reference doctor dials the agent's management-plane twin (18080)
+        # with a dashboard-minted JWT: mint one from the dashboard's signing key
+        from ..facade.auth import mint_mgmt_token
+        from ..utils.rsa import load_private_key
+
+        with open(a.mgmt_signing_key) as f:
+            key = load_private_key(f.read())
+        headers["Authorization"] = "Bearer " + mint_mgmt_token(
+            key, a.mgmt_kid, "omnia-doctor", agent=a.agent, workspace=a.workspace or "")
     r.register(*AgentChecker(a.facade, st, a.token, {k.strip(): v.strip()
                                                      for k, v in headers.items()}).checks())
     r.register(*SessionChecker(st, a.namespace).checks())
@@ -70,6 +80,11 @@ def parser() -> argparse.ArgumentParser:
     ap.add_argument("--table", action="store_true", help="with --run-once: a table, not JSON")
     ap.add_argument("--facade", default=env("OMNIA_DOCTOR_FACADE", ""), help="agent WebSocket URL (ws://host:port/ws)")
     ap.add_argument("--token", default="")
+    ap.add_argument("--mgmt-signing-key", default=env("OMNIA_DOCTOR_MGMT_KEY", ""),
+                    help="dashboard PEM key: mint a management-plane JWT and dial the "
+                         "agent's twin listener (--facade ws://agent:18080/ws)")
+    ap.add_argument("--mgmt-kid", default="omnia-dashboard-1")
+    ap.add_argument("--agent", default="", help="agent name claimed in the mgmt-plane token")
     ap.add_argument("--header", action="append", default=[],
                     help="extra WebSocket header 'Name: value' (e.g. x-user-id behind an edge)")
     ap.add_argument("--namespace", default="default", help="agent namespace")

@@ -11,10 +11,14 @@ one dependency-free page plus a small aiohttp backend:
 * ``GET /api/overview`` -- AgentRuntime phase / replicas / engine summary;
 * ``GET /api/arena/jobs`` -- ArenaJobs with type, phase and result summary;
 * ``GET /api/consent/{user}`` -- the privacy API's consent record (read-only);
-* ``/`` -- the page: resource tables, session list, and a chat console that
-  opens ``ws://<facade>/ws?agent=...`` directly from the browser (the
-  reference proxies through the dashboard's mgmt-plane twin; here the facade's
-  own auth chain applies).
+* ``/`` -- the page: resource tables, session list, and a chat console;
+* ``GET /api/auth/jwks`` -- the management-plane signing key set (public, the
+  agents' facades fetch it: ``OMNIA_MGMT_PLANE_JWKS_URL``);
+* ``GET /api/agents/{ns}/{name}/ws`` -- the console's WebSocket, proxied to the
+  agent's management-plane twin (``status.managementEndpoints.ws``, port 18080)
+  with a freshly minted RS256 JWT (origin ``management-plane``, the agent /
+  workspace claims, the caller's subject): the browser never holds a token the
+  agent's public listener would accept (``dashboard/SERVICE.md``, WS proxy).
 
 Management writes (``--allow-writes``; off by default):
 
@@ -69,7 +73,7 @@ border:1px solid #ccc;padding:6px;white-space:pre-wrap}</style></head><body>
 <th>result</th></tr></table>
 <h2>Consent</h2><input id="cuser" placeholder="user id"><button onclick="consent()">lookup</button>
 <pre id="cons"></pre>
-<h2>Console</h2><input id="ws" size="40" value="ws://127.0.0.1:8080/ws">
+<h2>Console</h2><input id="ws" size="40" value="/api/agents/default/agent/ws">
 <button onclick="conn()">connect</button><br><input id="msg" size="60">
 <button onclick="send()">send</button><div id="log"></div>
 <script>
@@ -97,7 +101,8 @@ async function consent(){const u=document.getElementById('cuser').value;
  document.getElementById('cons').textContent=JSON.stringify(
  await j('/api/consent/'+encodeURIComponent(u)),null,1)}
 function log(x){const l=document.getElementById('log');l.textContent+=x+'\\n';l.scrollTop=1e9}
-function conn(){sock=new WebSocket(document.getElementById('ws').value);
+function conn(){const v=document.getElementById('ws').value;
+ sock=new WebSocket(v.startsWith('/')?(location.protocol==='https:'?'wss://':'ws://')+location.host+v:v);
  sock.onmessage=e=>{const m=JSON.parse(e.data);log(m.type+': '+(m.content||m.error?.message||''))}}
 function send(){sock.send(JSON.stringify({type:'message',content:document.getElementById('msg').value}))}
 const sel=document.getElementById('kind');for(const k of KINDS){const o=document.createElement('option');
@@ -126,7 +131,7 @@ def oidc_middleware(jwks: dict, issuer: str = "", audience: str = ""):
 
     @web.middleware
     async def mw(request, handler):
-        if request.path.startswith("/api/"):
+        if request.path.startswith("/api/") and request.path != "/api/auth/jwks":
             tok = bearer(request.headers)
             if not tok:
                 return web.json_response({"error": "missing bearer token"}, status=401)
@@ -146,7 +151,8 @@ def oidc_middleware(jwks: dict, issuer: str = "", audience: str = ""):
 def build_app(api: str, session_api: str = "", privacy_api: str = "",
               oidc: dict | None = None, allow_writes: bool = False,
               insecure_dev_writes: bool = False,
-              allowed_origins: tuple = ()) -> web.Application:
+              allowed_origins: tuple = (), mgmt_key=None, mgmt_kid: str = "omnia-dashboard-1",
+              twin_resolver=None, token_ttl_s: int = 300) -> web.Application:
     """``oidc``: ``{"jwks": {...}, "issuer": ..., "audience": ...,
     "write_groups": [...]}`` gates the API; ``allow_writes`` enables the
     management routes, which need OIDC unless ``insecure_dev_writes`` (module doc)."""
@@ -318,6 +324,72 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
     async def healthz(_):
         return web.json_response({"status": "ok"})
 
+    # ------------------------------------------------ management plane
+    from ..facade.auth import jwk_from_private, mint_mgmt_token
+
+    async def jwks(_):
+        keys = [jwk_from_private(mgmt_key, mgmt_kid)] if mgmt_key is not None else []
+        return web.json_response({"keys": keys})
+
+    async def _twin(ns: str, name: str):
+        """ws:// URL of an agent's mgmt twin + its workspace, from its status."""
+        if twin_resolver is not None:
+            return await twin_resolver(ns, name)
+        st, body = await _get(_ns_url("agentruntimes", ns, name))
+        if st != 200:
+            return None, ""
+        status = body.get("status") or {}
+        port = (status.get("managementEndpoints") or {}).get("ws")
+        ep = status.get("serviceEndpoint") or f"{name}.{ns}.svc.cluster.local"
+        if not port:
+            return None, ""
+        ws = ((body.get("spec") or {}).get("workspaceRef") or {}).get("name", "")
+        return f"ws://{ep.rsplit(':', 1)[0]}:{port}/ws", ws
+
+    async def agent_ws(request):
+        """Browser <-> dashboard <-> agent twin, frame for frame."""
+        if mgmt_key is None:
+            return web.json_response({"error": "management plane not configured"}, status=503)
+        ns, name = request.match_info["ns"], request.match_info["name"]
+        url, workspace = await _twin(ns, name)
+        if not url:
+            return web.json_response({"error": "agent has no management endpoint"}, status=404)
+        claims = request.get("claims") or {}
+        tok = mint_mgmt_token(mgmt_key, mgmt_kid, str(claims.get("sub") or "dashboard"),
+                              agent=name, workspace=workspace, ttl_s=token_ttl_s)
+        q = {k: v for k, v in request.query.items() if k in ("session", "binary", "resume")}
+        if q:
+            url += "?" + urllib.parse.urlencode(q)
+        down = web.WebSocketResponse(heartbeat=30.0)
+        await down.prepare(request)
+        async with aiohttp.ClientSession() as s:
+            try:
+                up = await s.ws_connect(url, headers={"Authorization": f"Bearer {tok}"},
+                                        heartbeat=30.0)
+            except aiohttp.WSServerHandshakeError as e:
+                await down.send_json({"type": "error", "error": {
+                    "code": "upstream_rejected", "message": f"agent twin: {e.status}"}})
+                await down.close()
+                return down
+
+            async def pump(src, dst):
+                async for m in src:
+                    if m.type == aiohttp.WSMsgType.TEXT:
+                        await dst.send_str(m.data)
+                    elif m.type == aiohttp.WSMsgType.BINARY:
+                        await dst.send_bytes(m.data)
+                    else:
+                        break
+                await dst.close()
+
+            async with up:
+                t1 = asyncio.ensure_future(pump(up, down))
+                t2 = asyncio.ensure_future(pump(down, up))
+                await asyncio.wait({t1, t2}, return_when=asyncio.FIRST_COMPLETED)
+                for t in (t1, t2):
+                    t.cancel()
+        return down
+
     app.router.add_get("/", page)
     app.router.add_get("/api/resources/{plural}", resources)
     app.router.add_get("/api/sessions", sessions)
@@ -326,6 +398,8 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
     app.router.add_get("/api/arena/jobs", arena_jobs)
     app.router.add_get("/api/consent/{user}", consent)
     app.router.add_get("/healthz", healthz)
+    app.router.add_get("/api/auth/jwks", jwks)
+    app.router.add_get("/api/agents/{ns}/{name}/ws", agent_ws)
     app.router.add_post("/api/resources/{plural}", create)
     app.router.add_delete("/api/resources/{plural}/{ns}/{name}", delete)
     app.router.add_post("/api/agents/{ns}/{name}/scale", scale)
@@ -350,7 +424,18 @@ def main(argv=None):
     ap.add_argument("--allowed-origin", action="append", default=[])
     ap.add_argument("--insecure-dev-writes", action="store_true",
                     help="allow writes without OIDC; only with a loopback --host")
+    ap.add_argument("--mgmt-signing-key", default="",
+                    help="PEM RSA key that signs management-plane JWTs (default: an "
+                         "ephemeral key generated at start; facades re-fetch the JWKS)")
+    ap.add_argument("--mgmt-kid", default="omnia-dashboard-1")
     a = ap.parse_args(argv)
+    from ..utils.rsa import generate_private_key, load_private_key
+
+    if a.mgmt_signing_key:
+        with open(a.mgmt_signing_key) as f:
+            mgmt_key = load_private_key(f.read())
+    else:
+        mgmt_key = generate_private_key(2048)
     oidc = None
     if a.oidc_jwks_file:
         with open(a.oidc_jwks_file) as f:
@@ -363,7 +448,8 @@ def main(argv=None):
         runner = web.AppRunner(build_app(a.api, a.session_api, a.privacy_api, oidc,
                                          allow_writes=a.allow_writes,
                                          insecure_dev_writes=a.insecure_dev_writes,
-                                         allowed_origins=tuple(a.allowed_origin)))
+                                         allowed_origins=tuple(a.allowed_origin),
+                                         mgmt_key=mgmt_key, mgmt_kid=a.mgmt_kid))
         await runner.setup()
         await web.TCPSite(runner, a.host, a.port).start()
         await asyncio.Event().wait()

@@ -219,18 +219,39 @@ class MemoryPostgres(MemorySQLite):
                 f"to_char(to_timestamp({col}), 'YYYY-MM-DD')")
 
     # ---- embedding dimension reconcile (embedding_schema.go:125)
+    # the column's dimension from the catalog (the column may not exist yet:
+    # _PG_SCHEMA never creates it) -- ``currentEmbeddingDim``, embedding_schema.go
+    CURRENT_DIM_SQL = ("SELECT format_type(a.atttypid, a.atttypmod) FROM pg_attribute a "
+                       "WHERE a.attrelid = 'memory_observations'::regclass AND "
+                       "a.attname = 'embedding' AND NOT a.attisdropped")
+    INDEX_NAME = "idx_memory_observations_embedding"
+    INVALID_INDEX_SQL = ("SELECT NOT i.indisvalid FROM pg_index i JOIN pg_class c ON "
+                         "c.oid = i.indexrelid WHERE c.relname = "
+                         "'idx_memory_observations_embedding'")
+    SCHEMA_LOCK, INDEX_LOCK = 1309, 1310
+
+    @staticmethod
+    def parse_dim(format_type: str | None) -> int | None:
+        import re
+
+        m = re.fullmatch(r"vector\((\d+)\)", (format_type or "").strip())
+        return int(m.group(1)) if m else None
+
     @staticmethod
     def embedding_schema(dim: int, current_dim: int | None, has_data: bool,
                          consent_dim: int | None) -> list[str]:
-        """Statements that bring ``memory_observations.embedding`` to ``vector(dim)``.
-        ``current_dim`` None = no column yet.  Raises when the reshape would drop
-        stored embeddings without consent for exactly ``dim``."""
+        """TRANSACTIONAL statements that bring ``memory_observations.embedding`` to
+        ``vector(dim)`` (``reconcileEmbeddingTx``): advisory xact lock, drop / add
+        the column, settle the consent.  ``current_dim`` None = no column yet.
+        Raises when the reshape would drop stored embeddings without consent for
+        exactly ``dim``.  The HNSW index is built AFTER the commit, outside any
+        transaction (:meth:`embedding_index_schema`)."""
         if dim <= 0:
             raise ValueError(f"invalid embedding dimension {dim}")
         if dim > MAX_INDEXABLE_DIM:
             raise ValueError(f"embedding dimension {dim} exceeds the maximum indexable "
                              f"dimension {MAX_INDEXABLE_DIM} (pgvector HNSW cap)")
-        out = ["SELECT pg_advisory_xact_lock(1309)"]
+        out = [f"SELECT pg_advisory_xact_lock({MemoryPostgres.SCHEMA_LOCK})"]
         if current_dim == dim:
             return out + [f"DELETE FROM {CONSENT_TABLE}"]  # stale consent cleared
         destructive = current_dim is not None and has_data
@@ -238,14 +259,28 @@ class MemoryPostgres(MemorySQLite):
             raise EmbeddingDimConsentRequired(
                 f"changing the embedding dimension to {dim} would discard existing embeddings "
                 f"and requires one-shot consent (recorded target={consent_dim}); record it via "
-                f"POST /api/v1/admin/embedding-dimension-change {{\"target_dim\": {dim}}}")
+                f"POST /admin/embedding-dimension-change {{\"target_dim\": {dim}}} or "
+                f"INSERT INTO {CONSENT_TABLE} (id, target_dim, recorded_at) VALUES (1, {dim}, "
+                f"now())")
         if current_dim is not None:
             out.append("ALTER TABLE memory_observations DROP COLUMN embedding")
         out.append(f"ALTER TABLE memory_observations ADD COLUMN embedding vector({dim})")
-        out.append("CREATE INDEX CONCURRENTLY IF NOT EXISTS idx_memory_observations_embedding "
+        out.append(f"DELETE FROM {CONSENT_TABLE}")  # consumed (or stale)
+        return out
+
+    @staticmethod
+    def embedding_index_schema(invalid_leftover: bool) -> list[str]:
+        """AUTOCOMMIT statements (``ensureEmbeddingIndexes``): Postgres refuses
+        ``CREATE INDEX CONCURRENTLY`` inside a transaction block, so the build
+        runs on an autocommit connection under a SESSION advisory lock, after
+        dropping an invalid index a failed concurrent build left behind."""
+        out = [f"SELECT pg_advisory_lock({MemoryPostgres.INDEX_LOCK})"]
+        if invalid_leftover:
+            out.append(f"DROP INDEX CONCURRENTLY IF EXISTS {MemoryPostgres.INDEX_NAME}")
+        out.append(f"CREATE INDEX CONCURRENTLY IF NOT EXISTS {MemoryPostgres.INDEX_NAME} "
                    "ON memory_observations USING hnsw (embedding vector_cosine_ops) WITH "
                    "(m = 16, ef_construction = 64)")
-        out.append(f"DELETE FROM {CONSENT_TABLE}")  # consumed (or stale)
+        out.append(f"SELECT pg_advisory_unlock({MemoryPostgres.INDEX_LOCK})")
         return out
 
 

@@ -940,22 +940,23 @@ class MemoryStore:
         """Reconcile the stored embedding dimension with the embedder's
         (``EnsureEmbeddingSchema``).  Changing it while embeddings exist discards
         them, so it needs one-shot consent for exactly ``dim``; the consent is
-        consumed and the re-embed worker backfills.  Postgres also reshapes the
-        ``vector(D)`` column (``MemoryPostgres.embedding_schema``)."""
+        consumed and the re-embed worker backfills.  On a real Postgres the
+        ``vector(D)`` column is reshaped in one transaction and the HNSW index
+        is built after the commit on an autocommit connection
+        (``internal/memory/postgres/embedding_schema.go``)."""
+        consent = self._q(f"SELECT target_dim FROM {CONSENT_TABLE} WHERE id = 1")
+        consent_dim = int(consent[0][0]) if consent else None
+        if isinstance(self.d, MemoryPostgres) and not self.d.emulated:
+            return self._ensure_embedding_dim_pg(dim, consent_dim)
         cur = self._q("SELECT value FROM memory_meta WHERE key = 'embedding_dim'")
         cur_dim = int(cur[0][0]) if cur else None
         has = bool(self._q("SELECT 1 FROM memory_observations WHERE embedding IS NOT NULL "
                            "LIMIT 1"))
-        consent = self._q(f"SELECT target_dim FROM {CONSENT_TABLE} WHERE id = 1")
-        consent_dim = int(consent[0][0]) if consent else None
-        if isinstance(self.d, MemoryPostgres) and not self.d.emulated:
-            stmts = self.d.embedding_schema(dim, cur_dim, has, consent_dim)
-        else:
-            stmts = MemoryPostgres.embedding_schema(dim, cur_dim, has, consent_dim)
-            stmts = [f"DELETE FROM {CONSENT_TABLE}"]  # SQLite blobs carry any dimension
-            if cur_dim not in (None, dim) and has:
-                stmts.insert(0, "UPDATE memory_observations SET embedding = NULL, "
-                                "embedding_model = NULL")
+        MemoryPostgres.embedding_schema(dim, cur_dim, has, consent_dim)  # consent rules
+        stmts = [f"DELETE FROM {CONSENT_TABLE}"]  # SQLite blobs carry any dimension
+        if cur_dim not in (None, dim) and has:
+            stmts.insert(0, "UPDATE memory_observations SET embedding = NULL, "
+                            "embedding_model = NULL")
         dropped = cur_dim not in (None, dim) and has
         with self._tx() as db:
             if dropped:
@@ -968,6 +969,49 @@ class MemoryStore:
             db.execute(self.d.upsert("memory_meta", ["key", "value"]), ("embedding_dim",
                                                                           str(dim)))
         return {"from": cur_dim, "to": dim, "dropped_embeddings": dropped}
+
+    def _ensure_embedding_dim_pg(self, dim: int, consent_dim: int | None) -> dict:
+        P = MemoryPostgres
+        with self._tx() as db:
+            db.execute(f"SELECT pg_advisory_xact_lock({P.SCHEMA_LOCK})")
+            row = db.execute(P.CURRENT_DIM_SQL).fetchall()
+            cur_dim = P.parse_dim(row[0][0]) if row else None
+            has = cur_dim is not None and bool(db.execute(
+                "SELECT 1 FROM memory_observations WHERE embedding IS NOT NULL LIMIT 1"
+            ).fetchall())
+            stmts = P.embedding_schema(dim, cur_dim, has, consent_dim)
+            dropped = cur_dim not in (None, dim) and has
+            if dropped:
+                ids = [r[0] for r in db.execute("SELECT id FROM memory_observations WHERE "
+                                                "embedding IS NOT NULL").fetchall()]
+                for i in range(0, len(ids), 500):
+                    self._log_vectors(db, "delete", ids[i:i + 500])
+            for st in stmts[1:]:  # the xact lock is already held
+                db.execute(st)
+            db.execute(self.d.upsert("memory_meta", ["key", "value"]), ("embedding_dim",
+                                                                          str(dim)))
+        self._build_embedding_index()
+        return {"from": cur_dim, "to": dim, "dropped_embeddings": dropped}
+
+    def _build_embedding_index(self):
+        """CONCURRENTLY builds cannot run in a transaction block: flip the DB-API
+        connection to autocommit for them (psycopg / psycopg2 ``.autocommit``)."""
+        P = MemoryPostgres
+        with self.lock:
+            raw = self.db.raw
+            prev = getattr(raw, "autocommit", False)
+            raw.autocommit = True
+            try:
+                row = self.db.execute(P.INVALID_INDEX_SQL).fetchall()
+                invalid = bool(row and row[0][0])
+                stmts = P.embedding_index_schema(invalid)
+                try:
+                    for st in stmts[:-1]:
+                        self.db.execute(st)
+                finally:
+                    self.db.execute(stmts[-1])  # session advisory unlock
+            finally:
+                raw.autocommit = prev
 
 
 __all__ = ["MemoryStore", "MultiTierRequest", "NotFound", "AccessTouchBatcher",

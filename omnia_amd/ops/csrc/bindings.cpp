@@ -13,6 +13,8 @@ int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, 
                 const int* positions, const float* cos_sin, void* k_cache, void* v_cache,
                 const int64_t* slots, int hq, int hkv, int block_size, hipStream_t s);
 int omnia_row_sumsq(float* ss, const void* x, int rows, int d, int64_t stride, hipStream_t s);
+int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, int M, int N,
+                        int K, hipStream_t s);
 int omnia_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows, int d,
                   int64_t x_stride, int64_t out_stride, float eps, hipStream_t s);
 int omnia_rope_kv(void* q, void* k, const void* v, const int* positions, const float* cos_sin,
@@ -581,6 +583,16 @@ void pgemm(int64_t epi, at::Tensor out, at::Tensor x, at::Tensor W,
            "pgemm");
 }
 
+void pgemm_variant(int64_t variant, at::Tensor out, at::Tensor x, at::Tensor W) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(W); CHECK_BF16(out);
+  TORCH_CHECK(x.is_contiguous() && W.is_contiguous() && out.is_contiguous(), "contiguous");
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && W.size(1) == x.size(1) && out.size(0) == x.size(0) &&
+              out.size(1) == W.size(0), "shapes");
+  CHECK_RC(omnia_pgemm_variant((int)variant, out.data_ptr(), x.data_ptr(), W.data_ptr(),
+                               x.size(0), W.size(0), x.size(1), cur_stream()),
+           "pgemm_variant");
+}
+
 void row_sumsq(at::Tensor ss, at::Tensor x) {
   CHECK_GPU(x); CHECK_BF16(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x [M, d] rows contiguous");
@@ -855,6 +867,7 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("tgemm", &tgemm);
   m.def("pgemm", &pgemm);
   m.def("row_sumsq", &row_sumsq);
+  m.def("pgemm_variant", &pgemm_variant);
   m.def("ar_twoshot", &ar_twoshot);
   m.def("ar_region_bytes", &omnia_ar_region_bytes);
   m.def("splitk_add_rmsnorm", &splitk_add_rmsnorm);

@@ -85,13 +85,17 @@ __device__ __forceinline__ void wait_vm() {
 // element offset of 16-B chunk `ch` of row `row` inside a half-tile
 __device__ __forceinline__ int swz(int row, int ch) { return row * BK + ((ch ^ (row & 7)) << 3); }
 
-template <int EPI>
+// VAR (tuning variants, EPI 0 only): bit 0 = no wave-row stagger, bit 1 = no
+// s_setprio around the MFMA clusters, bits 2-3 = m-tiles per L2 group (8/4/16/32)
+template <int EPI, int VAR = 0>
 __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
   constexpr int TN = EPI == 1 ? 128 : 256;  // output columns per block tile
   const int ntn = p.N / TN, mtn = (p.M + 255) >> 8;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GM = 8;
+  constexpr int GM = ((VAR >> 2) & 3) == 0 ? 8 : ((VAR >> 2) & 3) == 1 ? 4
+                                           : ((VAR >> 2) & 3) == 2 ? 16 : 32;
+  constexpr bool STAGGER = !(VAR & 1), PRIO = !(VAR & 2);
   const int per_group = GM * ntn;
   const int grp = bid / per_group, gm0 = grp * GM;
   const int gsz = mtn - gm0 < GM ? mtn - gm0 : GM;
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
     __builtin_amdgcn_sched_barrier(0);
     constexpr int qa = (q == 0 || q == 1) ? 0 : 1;
     constexpr int qb = (q == 0 || q == 3) ? 0 : 1;
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
 #pragma unroll
         for (int n = 0; n < 2; ++n)
           acc[qa][qb][m][n] = mfma16(af[m][ks], bfr[n][ks], acc[qa][qb][m][n]);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -221,7 +225,7 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   issue(1, I3{}, 1);
   wait_vm<4>();
   __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the second wave row by one barrier
+  if (STAGGER && wr == 1) __builtin_amdgcn_s_barrier();  // second wave row one barrier behind
   const int nit = nk >> 1;
   for (int it = 0; it < nit; ++it) {
     phase(std::integral_constant<int, 0>{}, it);
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
     phase(std::integral_constant<int, 7>{}, it);
   }
   wait_vm<0>();  // the past-the-end reloads must land before LDS is reused
-  if (wr == 0) __builtin_amdgcn_s_barrier();
+  if (STAGGER && wr == 0) __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_s_barrier();
 
   // ---------------------------------------------------------------- epilogue
@@ -426,6 +430,9 @@ extern "C" {
 
 // Returns 0 on success, < 0 for a shape / argument the kernel does not cover
 // (checked BEFORE any launch).
+int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, int M, int N,
+                        int K, hipStream_t s);
+
 int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, int K, int ldo,
                 const float* ss_in, int ss_in_n, float inv_d, float eps, float* ss_out,
                 const int* positions, const float* cos_sin, void* k_cache, void* v_cache,
@@ -459,6 +466,26 @@ int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, 
     case 1: pgemm_kernel<1><<<grid, block, 0, s>>>(a); break;
     case 2: pgemm_kernel<2><<<grid, block, 0, s>>>(a); break;
     default: pgemm_kernel<3><<<grid, block, 0, s>>>(a); break;
+  }
+  return (int)hipGetLastError();
+}
+
+// bare GEMM (EPI 0, no row scale) of a tuning variant: sweeps only
+int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, int M, int N,
+                        int K, hipStream_t s) {
+  if (M < 1 || K <= 0 || K % (2 * BK) || N <= 0 || N % 256) return -1;
+  PArgs a{out, (const bf16_t*)X, (const bf16_t*)W, M, N, K, N, nullptr, 0, 0.f, 0.f, nullptr,
+          nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
+  const dim3 grid((unsigned)(((M + 255) / 256) * (N / 256))), block(512);
+  switch (variant) {
+    case 0: pgemm_kernel<0, 0><<<grid, block, 0, s>>>(a); break;
+    case 1: pgemm_kernel<0, 1><<<grid, block, 0, s>>>(a); break;
+    case 2: pgemm_kernel<0, 2><<<grid, block, 0, s>>>(a); break;
+    case 3: pgemm_kernel<0, 3><<<grid, block, 0, s>>>(a); break;
+    case 4: pgemm_kernel<0, 4><<<grid, block, 0, s>>>(a); break;
+    case 8: pgemm_kernel<0, 8><<<grid, block, 0, s>>>(a); break;
+    case 12: pgemm_kernel<0, 12><<<grid, block, 0, s>>>(a); break;
+    default: return -2;
   }
   return (int)hipGetLastError();
 }

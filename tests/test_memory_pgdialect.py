@@ -64,7 +64,14 @@ def test_embedding_schema_reconcile_rules():
     es = MemoryPostgres.embedding_schema
     fresh = es(384, None, False, None)
     assert "ALTER TABLE memory_observations ADD COLUMN embedding vector(384)" in fresh
-    assert any("USING hnsw (embedding vector_cosine_ops)" in s for s in fresh)
+    # the CONCURRENTLY index build is never part of the transactional list
+    assert not any("CONCURRENTLY" in s or "hnsw" in s for s in fresh)
+    idx = MemoryPostgres.embedding_index_schema(False)
+    assert any("CREATE INDEX CONCURRENTLY" in s and "USING hnsw (embedding vector_cosine_ops)"
+               in s for s in idx)
+    assert idx[0].startswith("SELECT pg_advisory_lock(") and idx[-1].startswith(
+        "SELECT pg_advisory_unlock(")
+    assert any("DROP INDEX CONCURRENTLY" in s for s in MemoryPostgres.embedding_index_schema(True))
     assert not any("DROP COLUMN" in s for s in fresh)
     same = es(384, 384, True, None)
     assert not any("ALTER TABLE" in s for s in same)
@@ -78,6 +85,90 @@ def test_embedding_schema_reconcile_rules():
     assert ok[-1].startswith("DELETE FROM memory_embedding_dim_change_consent")
     with pytest.raises(ValueError):
         es(4096, None, False, None)  # beyond the HNSW cap
+
+
+class _FakePG:
+    """DB-API stand-in for a real Postgres: records every statement with the
+    connection's autocommit state and whether an explicit transaction is open;
+    answers the catalog probes (column ``vector(384)`` with data, an invalid
+    leftover index)."""
+
+    def __init__(self, dim="vector(384)", has=True, consent=None, invalid=True):
+        self.autocommit = False
+        self.in_tx = False
+        self.log = []
+        self.dim, self.has, self.consent, self.invalid = dim, has, consent, invalid
+
+    def cursor(self):
+        return self
+
+    def execute(self, sql, args=()):
+        up = sql.strip().upper()
+        if up.startswith("BEGIN"):
+            self.in_tx = True
+        self.log.append((sql, self.autocommit, self.in_tx))
+        if up in ("COMMIT", "ROLLBACK"):
+            self.in_tx = False
+        if "format_type" in sql:
+            self.rows = [(self.dim,)] if self.dim else []
+        elif "embedding IS NOT NULL" in sql and "SELECT 1" in sql:
+            self.rows = [(1,)] if self.has else []
+        elif "SELECT id FROM memory_observations" in sql:
+            self.rows = [("o1",), ("o2",)] if self.has else []
+        elif "target_dim FROM" in sql:
+            self.rows = [(self.consent,)] if self.consent else []
+        elif "indisvalid" in sql:
+            self.rows = [(True,)] if self.invalid else []
+        else:
+            self.rows = []
+
+    def executemany(self, sql, rows):
+        self.log.append((sql, self.autocommit, self.in_tx))
+
+    def fetchall(self):
+        return self.rows
+
+
+def test_postgres_reshape_commits_before_concurrent_index_build():
+    conn = _FakePG(consent=768)
+    st = MemoryStore(dialect=MemoryPostgres(paramstyle="format"), conn=conn)
+    conn.log.clear()
+    out = st.ensure_embedding_dim(768)
+    assert out == {"from": 384, "to": 768, "dropped_embeddings": True}
+    sql = [s for s, _, _ in conn.log]
+    # the dimension probe reads the catalog, never the (maybe absent) column
+    probe = next(i for i, s in enumerate(sql) if "format_type" in s)
+    assert not any("SELECT embedding" in s for s in sql[:probe])
+    alter = [(s, ac, tx) for s, ac, tx in conn.log if s.startswith("ALTER TABLE")]
+    assert [a[0].split()[3] for a in alter] == ["DROP", "ADD"]
+    assert all(tx and not ac for _, ac, tx in alter)  # column change inside the tx
+    commit = max(i for i, s in enumerate(sql) if s == "COMMIT")
+    create = next(i for i, s in enumerate(sql) if "CREATE INDEX CONCURRENTLY" in s)
+    drop = next(i for i, s in enumerate(sql) if "DROP INDEX CONCURRENTLY" in s)
+    assert commit < drop < create  # after the commit, invalid leftover dropped first
+    for i in (drop, create):
+        _, ac, tx = conn.log[i]
+        assert ac and not tx  # autocommit connection, no transaction block
+    assert sql[-1].startswith("SELECT pg_advisory_unlock(")
+    assert conn.autocommit is False  # restored
+    # same dimension: no reshape, but the index is (idempotently) ensured
+    conn2 = _FakePG(dim="vector(768)", invalid=False)
+    st2 = MemoryStore(dialect=MemoryPostgres(paramstyle="format"), conn=conn2)
+    conn2.log.clear()
+    st2.ensure_embedding_dim(768)
+    assert not any(s.startswith("ALTER TABLE") for s, _, _ in conn2.log)
+    assert not any("DROP INDEX" in s for s, _, _ in conn2.log)
+    # fresh database: no column yet -> add it, no consent needed
+    conn3 = _FakePG(dim=None, has=False, invalid=False)
+    st3 = MemoryStore(dialect=MemoryPostgres(paramstyle="format"), conn=conn3)
+    assert st3.ensure_embedding_dim(384)["from"] is None
+    # data present + no consent -> refused, nothing altered
+    conn4 = _FakePG(consent=None)
+    st4 = MemoryStore(dialect=MemoryPostgres(paramstyle="format"), conn=conn4)
+    conn4.log.clear()
+    with pytest.raises(EmbeddingDimConsentRequired, match="/admin/embedding-dimension-change"):
+        st4.ensure_embedding_dim(768)
+    assert not any(s.startswith("ALTER") or "CREATE INDEX" in s for s, _, _ in conn4.log)
 
 
 def test_dimension_change_needs_consent_and_drops_embeddings(tmp_path):

@@ -357,6 +357,29 @@ class LocalDriver:
 
 
 # ============================================================== main
+def check_streamed(results, gen_len: int, has_frames: bool, strict: bool = True) -> int:
+    """The headline counts ``done.usage.output_tokens``; cross-check it against
+    what the client actually received.  Every turn must report exactly
+    ``gen_len`` tokens (ignore_eos), and on the WS path the streamed chunk frames
+    it timed must account for them: at most one frame per token (plus a role
+    frame), and at most 2 % + 2 tokens merged into a neighbour's frame (UTF-8
+    fragments held back by the detokenizer, empty special tokens).  Returns the
+    total frame count; exits on a mismatch so a drifting count never reaches the
+    JSON line.  ``strict`` False (a tiny test vocabulary, mostly raw bytes whose
+    UTF-8 fragments the detokenizer holds back) counts the frames only."""
+    total = 0
+    for r in results:
+        n = r[2]
+        if n != gen_len:
+            raise SystemExit(f"turn reported {n} output tokens, expected {gen_len} (ignore_eos)")
+        if has_frames:
+            f = len(r[4])
+            total += f
+            if strict and (f > n + 1 or f < n - max(2, n // 50)):
+                raise SystemExit(f"turn streamed {f} frames for {n} reported output tokens")
+    return total
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -466,6 +489,12 @@ def run(a, drv, ws, rank, use_gpu, host_only):
     if a.arrival != "poisson" and prof is not None:
         _dump_profiles(prof, drv)
 
+    from omnia_amd.models.config import resolve as _resolve
+
+    # frames track tokens only with a full vocabulary: a tiny test vocab is
+    # mostly raw bytes, whose UTF-8 fragments the detokenizer holds back
+    frames = check_streamed(results, a.gen_len, a.path == "ws",
+                            strict=_resolve(a.model).vocab_size >= 32000)
     out_tokens = sum(r[2] for r in results)
     ttfts = [r[0] for r in results if r[0] is not None]
     lats = [r[1] for r in results if r[1] is not None]
@@ -520,6 +549,7 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             "p50_tpot_ms": ms(pct(tpot, 0.5)),
             "p95_tpot_ms": ms(pct(tpot, 0.95)),
             "p95_frame_gap_ms": ms(pct(gaps, 0.95)),
+            "streamed_frames_rank0": frames if a.path == "ws" else None,
             "turns": len(lats),
             "wave_ms": wave_ms,
             "config": {

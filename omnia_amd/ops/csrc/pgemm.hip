@@ -18,8 +18,8 @@
 //     retired by a counted `s_waitcnt vmcnt(4)` at phases 3 and 7 (never 0 in the
 //     loop), raw s_barrier (hipcc's __syncthreads() would drain the DMA);
 //   * the two wave rows run one barrier apart (ping-pong): while one wave of a
-//     SIMD issues its ds_reads and DMA, the other's 16 MFMAs run
-//     (s_setprio 1 around each MFMA cluster);
+//     SIMD issues its ds_reads and DMA, the other's 16 MFMAs run (no s_setprio:
+//     measured slower here);
 //   * XCD-aware block order (bijective remap) with 8 m-tiles per group so the
 //     blocks resident on one XCD share W column tiles and X row tiles in its L2.
 // Epilogues (the accumulators are staged as bf16 through LDS, then every thread
@@ -85,7 +85,7 @@ __device__ __forceinline__ void wait_vm() {
 // element offset of 16-B chunk `ch` of row `row` inside a half-tile
 __device__ __forceinline__ int swz(int row, int ch) { return row * BK + ((ch ^ (row & 7)) << 3); }
 
-// VAR (tuning variants, EPI 0 only): bit 0 = no wave-row stagger, bit 1 = no
+// VAR (tuning variants, EPI 0 only): bit 0 = no wave-row stagger, bit 1 = WITH
 // s_setprio around the MFMA clusters, bits 2-3 = m-tiles per L2 group (8/4/16/32)
 template <int EPI, int VAR = 0>
 __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
@@ -95,7 +95,10 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   constexpr int GM = ((VAR >> 2) & 3) == 0 ? 8 : ((VAR >> 2) & 3) == 1 ? 4
                                            : ((VAR >> 2) & 3) == 2 ? 16 : 32;
-  constexpr bool STAGGER = !(VAR & 1), PRIO = !(VAR & 2);
+  // s_setprio around the clusters measured 1.5-3.5 % SLOWER on every prefill shape
+  // (profiles/r4/pgemm_variants.log), so the default build (VAR 0) leaves it out;
+  // the wave-row stagger is worth ~15 % and stays
+  constexpr bool STAGGER = !(VAR & 1), PRIO = (VAR & 2) != 0;
   const int per_group = GM * ntn;
   const int grp = bid / per_group, gm0 = grp * GM;
   const int gsz = mtn - gm0 < GM ? mtn - gm0 : GM;

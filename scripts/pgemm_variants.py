@@ -1,6 +1,6 @@
 """A/B the pgemm.hip main-loop variants (bare GEMM, EPI 0) against tuned
 hipBLASLt, interleaved rounds in one process (cdna_hip_programming.md §5.4 rule
-24).  Variant bits: 1 no wave-row stagger, 2 no s_setprio, 4/8/12 = 4/16/32
+24).  Variant bits: 1 no wave-row stagger, 2 WITH s_setprio (v0 is the default build), 4/8/12 = 4/16/32
 m-tiles per L2 group (default 8)."""
 import argparse
 import statistics

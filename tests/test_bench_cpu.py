@@ -73,3 +73,31 @@ def test_driver_torchrun_invocation_two_ranks():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["steps"] == 2
     assert len(rec["per_rank_tokens_per_s"]) == 2 and rec["config"]["parallelism"] == "dp2"
+
+
+def test_streamed_frames_cross_check_usage():
+    """The headline's token count (done.usage.output_tokens) must agree with the
+    frames the client timed; a drifting server count aborts the bench."""
+    sys.path.insert(0, ROOT)
+    import pytest
+
+    from bench import check_streamed
+
+    ok = [(0.1, 1.0, 8, 96, [0.1 * i for i in range(8)])]
+    assert check_streamed(ok, 8, True) == 8
+    merged = [(0.1, 1.0, 128, 96, [0.0] * 126)]  # two tokens held back into neighbours
+    assert check_streamed(merged, 128, True) == 126
+    with pytest.raises(SystemExit, match="output tokens"):
+        check_streamed([(0.1, 1.0, 7, 96, [0.0] * 7)], 8, True)  # short turn
+    with pytest.raises(SystemExit, match="frames"):
+        check_streamed([(0.1, 1.0, 128, 96, [0.0] * 64)], 128, True)  # inflated usage
+    with pytest.raises(SystemExit, match="frames"):
+        check_streamed([(0.1, 1.0, 8, 96, [0.0] * 12)], 8, True)
+    assert check_streamed([(0.1, 1.0, 8, 96, [])], 8, False) == 0
+    assert check_streamed([(0.1, 1.0, 8, 96, [0.0])], 8, True, strict=False) == 1
+
+
+def test_ws_path_reports_streamed_frames():
+    rec = _bench("--concurrency", "2", "--steps", "1", "--stream-interval-ms", "0")
+    # tiny-llama's vocab is mostly raw bytes: frames are counted, not matched
+    assert 1 <= rec["streamed_frames_rank0"] <= rec["turns"] * 7

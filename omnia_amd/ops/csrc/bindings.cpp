@@ -13,6 +13,11 @@ int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, 
                 const int* positions, const float* cos_sin, void* k_cache, void* v_cache,
                 const int64_t* slots, int hq, int hkv, int block_size, hipStream_t s);
 int omnia_row_sumsq(float* ss, const void* x, int rows, int d, int64_t stride, hipStream_t s);
+int omnia_ar_alltoall(void* out, const void* in, void* const* regions, int* epochs, int* err,
+                      int64_t chunk, int64_t slot_bytes, int rank, int world, hipStream_t s);
+int omnia_ar_sendrecv(void* out, const void* in, void* const* regions, int* epochs, int* err,
+                      int64_t nbytes, int64_t slot_bytes, int rank, int world, int src_rank,
+                      hipStream_t s);
 int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, int M, int N,
                         int K, hipStream_t s);
 int omnia_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows, int d,
@@ -720,6 +725,47 @@ void ar_allgather(at::Tensor out, at::Tensor in, at::Tensor regions, at::Tensor 
                               cur_stream()), "ar_allgather");
 }
 
+// IPC all-to-all: in / out [world][chunk] (any dtype, chunk bytes % 16 == 0)
+void ar_alltoall(at::Tensor out, at::Tensor in, at::Tensor regions, at::Tensor epochs,
+                 at::Tensor err, int64_t slot_bytes, int64_t rank) {
+  CHECK_GPU(in); CHECK_GPU(out); CHECK_I32(epochs); CHECK_I32(err);
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous(), "contiguous");
+  TORCH_CHECK(in.device() == out.device() && epochs.device() == in.device() &&
+              err.device() == in.device(), "same device");
+  TORCH_CHECK(regions.device().is_cpu() && regions.scalar_type() == at::kLong, "regions cpu i64");
+  TORCH_CHECK(epochs.numel() >= omnia_ar_blocks(), "epochs per block");
+  const int world = regions.numel();
+  TORCH_CHECK(world <= omnia_ar_max_ranks(), "world too large");
+  const int64_t nb = in.numel() * in.element_size();
+  TORCH_CHECK(out.numel() * out.element_size() == nb && nb % world == 0,
+              "in / out: [world][chunk] bytes");
+  std::vector<void*> regs(world);
+  for (int p = 0; p < world; ++p) regs[p] = reinterpret_cast<void*>(regions.data_ptr<int64_t>()[p]);
+  CHECK_RC(omnia_ar_alltoall(out.data_ptr(), in.data_ptr(), regs.data(), epochs.data_ptr<int>(),
+                             err.data_ptr<int>(), nb / world, slot_bytes, (int)rank, world,
+                             cur_stream()), "ar_alltoall");
+}
+
+// IPC point-to-point: out <- rank src's `in` (same bytes on every rank)
+void ar_sendrecv(at::Tensor out, at::Tensor in, at::Tensor regions, at::Tensor epochs,
+                 at::Tensor err, int64_t slot_bytes, int64_t rank, int64_t src) {
+  CHECK_GPU(in); CHECK_GPU(out); CHECK_I32(epochs); CHECK_I32(err);
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous(), "contiguous");
+  TORCH_CHECK(in.device() == out.device() && epochs.device() == in.device() &&
+              err.device() == in.device(), "same device");
+  TORCH_CHECK(regions.device().is_cpu() && regions.scalar_type() == at::kLong, "regions cpu i64");
+  TORCH_CHECK(epochs.numel() >= omnia_ar_blocks(), "epochs per block");
+  const int world = regions.numel();
+  TORCH_CHECK(world <= omnia_ar_max_ranks(), "world too large");
+  const int64_t nb = in.numel() * in.element_size();
+  TORCH_CHECK(out.numel() * out.element_size() == nb, "out bytes == in bytes");
+  std::vector<void*> regs(world);
+  for (int p = 0; p < world; ++p) regs[p] = reinterpret_cast<void*>(regions.data_ptr<int64_t>()[p]);
+  CHECK_RC(omnia_ar_sendrecv(out.data_ptr(), in.data_ptr(), regs.data(), epochs.data_ptr<int>(),
+                             err.data_ptr<int>(), nb, slot_bytes, (int)rank, world, (int)src,
+                             cur_stream()), "ar_sendrecv");
+}
+
 // two-shot (reduce-scatter + all-gather) over the same IPC regions; with w the
 // fused residual add + RMSNorm variant (residual updated in place)
 void ar_twoshot(at::Tensor out, at::Tensor in, c10::optional<at::Tensor> residual,
@@ -881,6 +927,8 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("ipc_close", &ipc_close);
   m.def("ar_oneshot", &ar_oneshot);
   m.def("ar_allgather", &ar_allgather);
+  m.def("ar_alltoall", &ar_alltoall);
+  m.def("ar_sendrecv", &ar_sendrecv);
   m.def("ar_blocks", &omnia_ar_blocks);
   m.def("ar_max_ranks", &omnia_ar_max_ranks);
   m.def("apply_token_mask", &apply_token_mask);

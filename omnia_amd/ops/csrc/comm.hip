@@ -175,6 +175,75 @@ __global__ __launch_bounds__(256) void ar_allgather_kernel(char* __restrict__ ou
   if (tid == 0) epochs[b] = epoch;
 }
 
+// All-to-all of an opaque byte buffer: in = [world][chunk] (chunk bytes for each
+// destination rank, multiple of 16), out = [world][chunk] (chunk p = what rank p
+// sent to me).  Block b stages slice b of every destination chunk into my data
+// slot, publishes, waits for every peer's slice b, then pulls slice b of MY
+// chunk out of every peer's slot (peer p's slot holds its whole send buffer, so
+// my chunk sits at offset rank * chunk) -- one hop over the xGMI mesh per pair,
+// all links busy at once.  Same flags / epochs / parity slots as the other
+// collectives of the group (the EP all-to-all of DP-attention + EP, K15).
+__global__ __launch_bounds__(256) void ar_alltoall_kernel(char* __restrict__ out,
+                                                          const char* __restrict__ in,
+                                                          PeerPtrs peers, int* __restrict__ epochs,
+                                                          int* __restrict__ err, int64_t chunk,
+                                                          int64_t slot_bytes, int rank, int world) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ int s_epoch;
+  if (tid == 0) s_epoch = epochs[b] + 1;
+  __syncthreads();
+  const int epoch = s_epoch;
+  const int64_t slot = (epoch & 1) * slot_bytes;
+  const int64_t nv = chunk / 16;
+  const int64_t per = (nv + kBlocks - 1) / kBlocks;
+  const int64_t v0 = b * per, v1 = v0 + per < nv ? v0 + per : nv;
+  uint4v* mine = reinterpret_cast<uint4v*>(peers.data[rank] + slot);
+  const uint4v* src = reinterpret_cast<const uint4v*>(in);
+  for (int q = 0; q < world; ++q)
+    for (int64_t v = v0 + tid; v < v1; v += 256) mine[q * nv + v] = src[q * nv + v];
+  publish(peers.flags, b, rank, world, epoch);
+  wait_peers(peers.flags, b, rank, world, epoch, err);
+  for (int p = 0; p < world; ++p) {
+    const uint4v* ps = reinterpret_cast<const uint4v*>(peers.data[p] + slot) + rank * nv;
+    uint4v* dst = reinterpret_cast<uint4v*>(out) + p * nv;
+    for (int64_t v = v0 + tid; v < v1; v += 256) dst[v] = __builtin_nontemporal_load(ps + v);
+  }
+  __syncthreads();
+  if (tid == 0) epochs[b] = epoch;
+}
+
+// Point-to-point exchange (one ring hop of context-parallel attention): every
+// rank publishes `in` (nbytes) and receives rank `src`'s into `out`.  It waits on
+// every peer's flag (not only src's): that is what makes the parity-slot reuse
+// safe -- a slot is rewritten two calls later only after every reader of it has
+// signalled the next call.
+__global__ __launch_bounds__(256) void ar_sendrecv_kernel(char* __restrict__ out,
+                                                          const char* __restrict__ in,
+                                                          PeerPtrs peers, int* __restrict__ epochs,
+                                                          int* __restrict__ err, int64_t nbytes,
+                                                          int64_t slot_bytes, int rank, int world,
+                                                          int src_rank) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ int s_epoch;
+  if (tid == 0) s_epoch = epochs[b] + 1;
+  __syncthreads();
+  const int epoch = s_epoch;
+  const int64_t slot = (epoch & 1) * slot_bytes;
+  const int64_t nv = nbytes / 16;
+  const int64_t per = (nv + kBlocks - 1) / kBlocks;
+  const int64_t v0 = b * per, v1 = v0 + per < nv ? v0 + per : nv;
+  uint4v* mine = reinterpret_cast<uint4v*>(peers.data[rank] + slot);
+  const uint4v* src = reinterpret_cast<const uint4v*>(in);
+  for (int64_t v = v0 + tid; v < v1; v += 256) mine[v] = src[v];
+  publish(peers.flags, b, rank, world, epoch);
+  wait_peers(peers.flags, b, rank, world, epoch, err);
+  const uint4v* ps = reinterpret_cast<const uint4v*>(peers.data[src_rank] + slot);
+  uint4v* dst = reinterpret_cast<uint4v*>(out);
+  for (int64_t v = v0 + tid; v < v1; v += 256) dst[v] = __builtin_nontemporal_load(ps + v);
+  __syncthreads();
+  if (tid == 0) epochs[b] = epoch;
+}
+
 // Row chunk of (rank r, block b): [r*R + b*Rb, min(r*R + (b+1)*Rb, (r+1)*R, M)).
 // VEC = 16-B vectors per thread per row (d <= 256 * 8 * VEC).
 template <bool NORM, int VEC>
@@ -387,6 +456,45 @@ int omnia_ar_allgather(void* out, const void* in, void* const* regions, int* epo
   }
   ar_allgather_kernel<<<kBlocks, 256, 0, s>>>((char*)out, (const char*)in, pp, epochs, err, nbytes,
                                               slot_bytes, rank, world);
+  return (int)hipGetLastError();
+}
+
+static int fill_peers(PeerPtrs& pp, void* const* regions, int world, int64_t slot_bytes) {
+  for (int p = 0; p < world; ++p) {
+    if (!regions[p]) return -3;
+    pp.data[p] = reinterpret_cast<char*>(regions[p]);
+    pp.flags[p] = reinterpret_cast<int*>(reinterpret_cast<char*>(regions[p]) + 4 * slot_bytes);
+    pp.flags2[p] = pp.flags[p] + kBlocks * kMaxRanks;
+  }
+  return 0;
+}
+
+// out[world][chunk] <- chunk `rank` of every rank's in[world][chunk]
+// (world * chunk <= slot_bytes, chunk a multiple of 16).
+int omnia_ar_alltoall(void* out, const void* in, void* const* regions, int* epochs, int* err,
+                      int64_t chunk, int64_t slot_bytes, int rank, int world, hipStream_t s) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return -1;
+  if (chunk % 16 || chunk <= 0 || chunk * world > slot_bytes || slot_bytes % 16) return -2;
+  if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(in)) & 15) return -4;
+  PeerPtrs pp{};
+  if (int rc = fill_peers(pp, regions, world, slot_bytes)) return rc;
+  ar_alltoall_kernel<<<kBlocks, 256, 0, s>>>((char*)out, (const char*)in, pp, epochs, err, chunk,
+                                             slot_bytes, rank, world);
+  return (int)hipGetLastError();
+}
+
+// out[nbytes] <- rank src_rank's in[nbytes] (every rank calls with its own src).
+int omnia_ar_sendrecv(void* out, const void* in, void* const* regions, int* epochs, int* err,
+                      int64_t nbytes, int64_t slot_bytes, int rank, int world, int src_rank,
+                      hipStream_t s) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return -1;
+  if (src_rank < 0 || src_rank >= world) return -5;
+  if (nbytes % 16 || nbytes <= 0 || nbytes > slot_bytes || slot_bytes % 16) return -2;
+  if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(in)) & 15) return -4;
+  PeerPtrs pp{};
+  if (int rc = fill_peers(pp, regions, world, slot_bytes)) return rc;
+  ar_sendrecv_kernel<<<kBlocks, 256, 0, s>>>((char*)out, (const char*)in, pp, epochs, err, nbytes,
+                                             slot_bytes, rank, world, src_rank);
   return (int)hipGetLastError();
 }
 

@@ -12,8 +12,10 @@ decodes the sequence alone like any other.  TTFT of a long prompt drops by up
 to W x while the other ranks lose one step each.
 
 Because a CP prefill is a collective, every rank of the group steps in
-lockstep: one small all-reduce per step says who (if anyone) has a CP prompt
-at the head of its queue; with none, each rank runs its own ordinary step.
+lockstep: a host shared-memory all-gather per step (no device collective)
+says who (if anyone) has a CP prompt at the head of its queue; with none, each
+rank runs its own ordinary step.  When the ranks share a device (the ``ipc``
+transport) the ring hops run on the IPC point-to-point kernel instead of RCCL.
 
 The reference bounds context before the remote provider call and has no
 sequence parallelism at all (``api/v1alpha1/agentruntime_types.go:417-459``,
@@ -29,6 +31,7 @@ import torch.distributed as dist
 from ..models.llama import ForwardBatch
 from ..parallel import state as pstate
 from ..parallel.context_parallel import CPPrefill
+from ..parallel.hostsync import ShmAgreement
 
 
 def run_cp_prefill(runner, seq, L: int, owner: int, group) -> int | None:
@@ -72,15 +75,11 @@ def run_cp_step(engine) -> int:
     group, W, r = st.dp_group, st.dp_size, st.dp_rank
     sched = engine.scheduler
     cand = sched.cp_candidate()
-    desc = engine._cp_desc
-    desc.zero_()
-    vals = torch.zeros(W + 1, dtype=torch.int64)
-    vals[r] = cand.length if cand is not None else 0
-    vals[W] = 1 if sched.has_work() else 0
-    desc.copy_(vals)
-    dist.all_reduce(desc, op=dist.ReduceOp.MAX, group=group)
-    got = desc.tolist()
-    lens, busy = got[:W], got[W]
+    ag = getattr(engine, "_cp_agree", None)
+    if ag is None:  # host shared-memory agreement (parallel/hostsync.py), built once
+        ag = engine._cp_agree = ShmAgreement.for_group(group, 2)
+    got = ag.gather([cand.length if cand is not None else 0, 1 if sched.has_work() else 0])
+    lens, busy = [int(x) for x in got[:, 0]], int(got[:, 1].max())
     owners = [i for i, n in enumerate(lens) if n > 0]
     engine._ep_active = 1 if (owners or busy) else 0
     if not owners:

@@ -129,8 +129,6 @@ class LLMEngine:
         self.cp_lockstep = (cfg.cp_threshold > 0 and st.world_size > 1 and st.tp_size == 1
                             and not self.ep_lockstep)
         self.lockstep = self.ep_lockstep or self.cp_lockstep
-        if self.cp_lockstep:
-            self._cp_desc = torch.zeros(st.dp_size + 1, dtype=torch.int64, device=dev)
         if self.ep_lockstep:
             from .ep import EPModelRunner
 

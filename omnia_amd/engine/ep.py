@@ -5,8 +5,10 @@ but each Mixtral MoE layer is a collective: tokens go to their experts' rank and
 back (:mod:`omnia_amd.parallel.expert`).  So every rank must execute the same
 sequence of forwards with the same all-to-all shapes, whatever its own load:
 
-1. each step every rank publishes ``[active, tokens, eager, rows, cols]`` and the
-   group all-reduces it (MAX) -- one small collective per step;
+1. each step every rank publishes ``[active, tokens, eager, rows, cols]`` in a
+   host shared-memory page and takes the element-wise MAX over the group
+   (:class:`omnia_amd.parallel.hostsync.ShmAgreement`: no device collective,
+   no device -> host copy);
 2. nobody active -> everybody idles;
 3. anyone needs an eager forward (a prefill / mixed step, or a decode that
    cannot replay a graph -- penalties, grammars) -> EVERY rank runs eagerly with
@@ -24,9 +26,9 @@ from __future__ import annotations
 import bisect
 
 import torch
-import torch.distributed as dist
 
 from ..parallel import state as pstate
+from ..parallel.hostsync import ShmAgreement
 from .model_runner import ModelRunner
 
 
@@ -40,16 +42,16 @@ class EPModelRunner(ModelRunner):
         st = pstate.get_state()
         self.group = st.dp_group
         self.ep = st.dp_size
-        self.desc = torch.zeros(5, dtype=torch.int64, device=self.device)
         self.ep_stats = {"steps": 0, "eager_steps": 0, "graph_steps": 0, "idle_fill": 0}
+        # per-step agreement over host shared memory: no collective launch, no
+        # device -> host copy on the control path (parallel/hostsync.py)
+        self.agreement = ShmAgreement.for_group(self.group, 5) if self.ep > 1 else None
 
     # ------------------------------------------------------------ agreement
     def agree(self, active: int, tokens: int, eager: int, rows: int, cols: int) -> list[int]:
-        if self.ep == 1:
+        if self.agreement is None:
             return [active, tokens, eager, rows, cols]
-        self.desc.copy_(torch.tensor([active, tokens, eager, rows, cols], dtype=torch.int64))
-        dist.all_reduce(self.desc, op=dist.ReduceOp.MAX, group=self.group)
-        return self.desc.tolist()
+        return self.agreement.max([active, tokens, eager, rows, cols])
 
     def bucket(self, n: int) -> int:
         return self.buckets[bisect.bisect_left(self.buckets, max(1, n))]

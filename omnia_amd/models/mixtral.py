@@ -80,7 +80,8 @@ class MixtralModel(LlamaModel):
             if moe is None:
                 moe = self._ep_layers[key] = ExpertParallelMoE(
                     layer["router"], layer["experts_gate_up"], layer["experts_down"],
-                    self.cfg.experts_per_token, group=self.ep_group)
+                    self.cfg.experts_per_token, group=self.ep_group,
+                    comm=pstate.get_state().dp_comm)
             return moe(h, tokens=self.ep_tokens)
         return ops.moe(h, layer["router"], layer["experts_gate_up"], layer["experts_down"],
                        self.cfg.experts_per_token, self.cfg.num_experts, self.e_lo,

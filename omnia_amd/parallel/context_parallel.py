@@ -10,9 +10,11 @@ one GPU's prefill budget can still be spread over W ranks:
   chunks r and 2W-1-r ("zig-zag"). Under a causal mask every rank then does the
   same amount of work.
 * **Ring.** Each rank keeps its queries and passes its K/V around the ring with
-  ``isend`` / ``irecv`` over RCCL (point-to-point xGMI on a node). The transfer
-  of the next K/V block is posted before the current block is computed, so it
-  overlaps the math.
+  ``isend`` / ``irecv`` over RCCL (point-to-point xGMI on a node), or -- ranks
+  sharing a device, the ``ipc`` transport -- the IPC point-to-point kernel on a
+  side stream (``ops/csrc/comm.hip`` ar_sendrecv). The transfer of the next
+  K/V block is posted before the current block is computed, so it overlaps
+  the math.
 * **Merge.** Per-block partial attention is merged with the running
   (max, log-sum-exp) statistics, which is exact.
 
@@ -191,12 +193,17 @@ class _StepLaunch:
 
 
 def ring_attention_paged(q: torch.Tensor, kv: torch.Tensor, c: int, scale: float, group=None,
-                         launches: dict | None = None, on_block=None) -> torch.Tensor:
+                         launches: dict | None = None, on_block=None, comm=None,
+                         comm_stream=None) -> torch.Tensor:
     """Causal ring attention of this rank's zig-zag shard.
 
     q: [2c, Hq, D] (rows 0..c-1 = low chunk, c..2c-1 = high chunk); kv: this
     rank's K/V pages [2, 2c/BS, Hkv, BS, D] (low chunk pages first).
     ``on_block(src, kv_src)`` sees every rank's K/V block once (own included).
+    ``comm`` (a :class:`~omnia_amd.parallel.custom_allreduce.CustomAllReduce` over
+    ``group``): the ring hop runs on the IPC point-to-point kernel on
+    ``comm_stream`` -- ranks sharing a device, where RCCL cannot run -- still
+    overlapping the next block's transfer with this block's attention.
     Returns o [2c, Hq, D] in q's dtype."""
     from .. import ops
 
@@ -216,9 +223,16 @@ def ring_attention_paged(q: torch.Tensor, kv: torch.Tensor, c: int, scale: float
         reqs, recv = [], None
         if step + 1 < world:
             recv = torch.empty_like(cur)
-            reqs = dist.batch_isend_irecv([
-                dist.P2POp(dist.isend, cur, granks[nxt], group),
-                dist.P2POp(dist.irecv, recv, granks[prv], group)])
+            if comm is not None:
+                main = torch.cuda.current_stream()
+                side = comm_stream or main
+                side.wait_stream(main)  # cur / recv are ready on the side stream
+                with torch.cuda.stream(side):
+                    comm.send_recv(cur, prv, out=recv)
+            else:
+                reqs = dist.batch_isend_irecv([
+                    dist.P2POp(dist.isend, cur, granks[nxt], group),
+                    dist.P2POp(dist.irecv, recv, granks[prv], group)])
         if on_block is not None:
             on_block(src, cur)
         key = (src == rank, src < rank)
@@ -237,6 +251,8 @@ def ring_attention_paged(q: torch.Tensor, kv: torch.Tensor, c: int, scale: float
         for r in reqs:
             r.wait()
         if recv is not None:
+            if comm is not None and comm_stream is not None:
+                torch.cuda.current_stream().wait_stream(comm_stream)
             cur = recv
     return o.to(q.dtype)
 
@@ -307,5 +323,15 @@ class CPPrefill:
                 kc.index_copy_(0, dst, src_pages[0])
                 vc.index_copy_(0, dst, src_pages[1])
 
+        comm = None
+        if q3.is_cuda and self.world > 1:
+            from . import state as pstate
+
+            st = pstate.get_state()
+            if st.transport == "ipc" and st.dp_comm is not None and self.group is st.dp_group:
+                comm = st.dp_comm
+                if getattr(self, "_comm_stream", None) is None:
+                    self._comm_stream = torch.cuda.Stream(device=q3.device)
         return ring_attention_paged(q3, self.scratch, self.c, scale, self.group,
-                                    self._launches, keep)
+                                    self._launches, keep, comm=comm,
+                                    comm_stream=getattr(self, "_comm_stream", None))

@@ -127,6 +127,60 @@ class CustomAllReduce:
             out[:, r0:r0 + piece.shape[0]] = tmp
         return out
 
+    def all_to_all(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """``out[p] = x_of_rank_p[me]`` for ``x`` = ``[W, rows, ...]`` (any dtype,
+        the per-peer chunk a multiple of 16 bytes): the IPC all-to-all of the
+        EP token dispatch / combine (``comm.hip`` ar_alltoall, one hop per pair
+        over the xGMI mesh).  Chunks larger than a slot allows run as row pieces
+        (same count on every rank, so the collectives pair up)."""
+        x = x.contiguous()
+        out = torch.empty_like(x) if out is None else out
+        W = self.world
+        if x.shape[0] != W:
+            raise ValueError(f"all_to_all input must be [world={W}, ...]")
+        chunk = x[0].numel() * x.element_size()
+        if chunk % 16:
+            raise ValueError("all_to_all needs a multiple of 16 bytes per peer")
+        if W * chunk <= self.max_bytes:
+            self.k.ar_alltoall(out, x, self.regions, self.epochs, self.err, self.slot_bytes,
+                               self.rank)
+            return out
+        rows = x.shape[1]
+        row_bytes = chunk // rows
+        step = max(1, self.max_bytes // (W * row_bytes))
+        while step > 1 and (step * row_bytes) % 16:
+            step -= 1
+        if (step * row_bytes) % 16:
+            raise ValueError("all_to_all rows do not chunk into 16-byte pieces")
+        for r0 in range(0, rows, step):
+            piece = x[:, r0:r0 + step].contiguous()
+            tmp = torch.empty_like(piece)
+            self.k.ar_alltoall(tmp, piece, self.regions, self.epochs, self.err,
+                               self.slot_bytes, self.rank)
+            out[:, r0:r0 + piece.shape[1]] = tmp
+        return out
+
+    def send_recv(self, x: torch.Tensor, src: int, out: torch.Tensor | None = None
+                  ) -> torch.Tensor:
+        """Every rank publishes ``x`` and receives rank ``src``'s (same shape):
+        one ring hop of context-parallel attention over IPC (``ar_sendrecv``);
+        slot-sized pieces of the flat bytes for larger blocks."""
+        x = x.contiguous()
+        out = torch.empty_like(x) if out is None else out
+        nbytes = x.numel() * x.element_size()
+        if nbytes % 16:
+            raise ValueError("send_recv needs a multiple of 16 bytes")
+        if nbytes <= self.max_bytes:
+            self.k.ar_sendrecv(out, x, self.regions, self.epochs, self.err, self.slot_bytes,
+                               self.rank, src)
+            return out
+        fi, fo = x.view(-1).view(torch.uint8), out.view(-1).view(torch.uint8)
+        step = self.max_bytes // 16 * 16
+        for i in range(0, nbytes, step):
+            self.k.ar_sendrecv(fo[i:i + step], fi[i:i + step], self.regions, self.epochs,
+                               self.err, self.slot_bytes, self.rank, src)
+        return out
+
     def can_fuse_norm(self, x: torch.Tensor) -> bool:
         return (self.should_use(x) and x.dim() == 2 and x.shape[1] % 8 == 0
                 and 4 * x.numel() <= self.slot_bytes)

@@ -21,7 +21,10 @@ static-shaped and hipGraph-capturable:
   device-side one-hot cumsum, no ``.tolist()``, no host round trip;
 * an expert-id slab ``[ep, C]`` (padding = -1) rides in a second all-to-all;
 * ``dist.all_to_all_single`` with equal splits (RCCL over xGMI: each rank talks
-  to each peer over its own link, one hop per pair);
+  to each peer over its own link, one hop per pair), or -- when the ranks share
+  devices (the ``ipc`` transport, e.g. EP=8 rehearsed on one MI355X) -- the IPC
+  all-to-all kernel (``ops/csrc/comm.hip`` ar_alltoall: every rank pulls its
+  chunk straight out of each peer's exported buffer);
 * the receive side runs :func:`omnia_amd.ops.moe_rows` -- the grouped MFMA
   expert kernels with top-1 routing over the received rows; padding rows are
   skipped by ``moe_align`` (no per-expert Python loop);
@@ -72,9 +75,12 @@ class ExpertParallelMoE:
     replicated."""
 
     def __init__(self, router: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor, k: int,
-                 group=None, renorm: bool = True):
+                 group=None, renorm: bool = True, comm=None):
         self.router, self.w_gu, self.w_down, self.k = router, w_gu, w_down, k
         self.group = group
+        # IPC all-to-all (parallel.state ``dp_comm``) when the ranks share devices
+        # (``ipc`` transport: RCCL cannot place two ranks on one GPU); RCCL otherwise
+        self.comm = comm
         self.ep = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.e_local = w_gu.shape[0]
@@ -99,6 +105,8 @@ class ExpertParallelMoE:
     def _a2a(self, t: torch.Tensor) -> torch.Tensor:
         if self.ep == 1:
             return t
+        if self.comm is not None and t.is_cuda:
+            return self.comm.all_to_all(t.view(self.ep, -1, *t.shape[1:])).view(t.shape)
         out = torch.empty_like(t)
         dist.all_to_all_single(out, t, group=self.group)
         return out
@@ -129,7 +137,9 @@ class ExpertParallelMoE:
         # a slot index outside the send buffer would be an out-of-bounds device
         # write; routing always yields [0, E), the clamp keeps it so for any input
         ids = ids.clamp(0, self.n_experts - 1)
-        cap = max(1, max(tokens, T) * k)
+        # multiple of 8 rows: the int32 expert-id slab's per-peer chunk stays a
+        # multiple of 16 bytes (the IPC all-to-all's vector width)
+        cap = -(-max(1, max(tokens, T) * k) // 8) * 8
         slot = dispatch_slots(ids, self.e_local, self.ep, cap)         # [T*k]
         send = x.new_zeros(self.ep * cap, d)
         send.index_copy_(0, slot, x.repeat_interleave(k, dim=0))

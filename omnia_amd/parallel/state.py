@@ -43,6 +43,7 @@ class ParallelState:
     dp_group: object = None
     backend: str = "none"
     custom_ar: object = None  # CustomAllReduce when available
+    dp_comm: object = None  # IPC collectives over the DP group (EP all-to-all, CP ring)
     transport: str = "none"  # TP device collectives: "rccl" | "ipc" | "gloo" (CPU)
 
     @property
@@ -118,6 +119,13 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, device: str |
             from .custom_allreduce import CustomAllReduce
 
             st.custom_ar = CustomAllReduce(st.tp_group)
+        if use_gpu and transport == "ipc" and st.dp_size > 1:
+            # DP-attention + EP all-to-all and the context-parallel ring run over the
+            # DP group; ranks sharing a device cannot use RCCL, so they get the IPC
+            # all-to-all / point-to-point kernels (one region per rank)
+            from .custom_allreduce import CustomAllReduce
+
+            st.dp_comm = CustomAllReduce(st.dp_group, max_bytes=16 << 20)
     set_state(st)
     return st
 

@@ -12,9 +12,10 @@ a tool, so the planner pack's ``tool_choice: required`` is enforced by the
 engine's tool-call grammar; what is checked is the plumbing: the tool call
 reaches the researcher's EP engine over A2A and comes back completed, the
 planner's retrieval read the seeded memory (access count), and session-api holds
-the tool-call rows.  GPU variant: tiny shapes swapped for Mixtral-8x7B EP=1
-(one rank) is covered by tests/test_ep_gpu.py's engine path; this file's GPU
-test runs the same manifests with the researcher on cuda:0."""
+the tool-call rows.  This file's GPU test runs the same manifests with the
+researcher on cuda:0 (EP=1); the multi-rank expert-parallel engine itself (EP 2,
+4 and 8 ranks sharing one MI355X over the IPC all-to-all, against the dense
+oracle) is tests/test_ep_cp_gpu.py."""
 import asyncio
 import json
 import os

@@ -88,7 +88,7 @@ def _sharded_weights(mc, rank, world, keep_full: bool):
     return shard, full
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, pipeline=False, batch=8):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
                       OMNIA_LOGIT_TAP="1")
@@ -105,8 +105,9 @@ def _worker(rank, world, port, q):
         st = pstate.init_distributed(tp_size=world, device="cuda")
         assert st.transport == "ipc" and st.backend == "gloo", (st.transport, st.backend)
         cfg = EngineConfig(model=mc.name, device="cuda", tp=world, num_blocks=256, block_size=16,
-                           max_batch=8, max_model_len=1024, max_prefill_tokens=64,
-                           pipeline=False, seed=3)
+                           max_batch=batch, max_model_len=1024,
+                           max_prefill_tokens=64 if batch <= 8 else 1024,
+                           pipeline=pipeline, seed=3)
         eng = tp.start(cfg, model_cfg=mc, weights=shard)
         if eng is None:
             return  # worker: rank 0 shut the group down
@@ -114,7 +115,14 @@ def _worker(rank, world, port, q):
         V = mc.vocab_size
         greedy = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
         prompts = [[rng.randrange(10, V - 10) for _ in range(n)] for n in (90, 41)]
-        seqs = eng.generate(prompts, greedy, session_ids=["a", "b"])
+        # batch > 8: filler sessions share every decode step, so the decode rows are
+        # >= 64 x 8192 and the layer boundaries run the fused two-shot all-reduce
+        # + RMSNorm kernel (only the two checked sessions go to the oracle)
+        fill = [[rng.randrange(10, V - 10) for _ in range(12)] for _ in range(batch - 2)] \
+            if batch > 8 else []
+        seqs = eng.generate(prompts + fill, greedy,
+                            session_ids=["a", "b"] + [f"f{i}" for i in range(len(fill))])
+        seqs = seqs[:2]
         p2 = prompts[0] + seqs[0].output + [rng.randrange(10, V - 10) for _ in range(12)]
         s2 = eng.generate([p2], greedy, session_ids=["a"])[0]
         hit = s2.prefix_hit
@@ -124,6 +132,8 @@ def _worker(rank, world, port, q):
             for i, sid in enumerate(ids):
                 rows.setdefault(sid, []).append(r[i])
         stats = dict(eng.runner.stats)
+        stats["pipeline_breaks"] = eng.timing.get("pipeline_breaks", 0)
+        stats["pipelined"] = bool(eng.cfg.pipeline and eng.runner.use_graphs)
         ring = dict(eng.runner.chan.ring.stats)
         eng.shutdown()
         plain = [(s.seq_id, list(s.prompt), list(s.output)) for s in seqs]
@@ -140,15 +150,20 @@ def _worker(rank, world, port, q):
         err = int(pstate.get_state().custom_ar.err.item())
         q.put(("ok", {"frac": frac, "worst": worst, "neg_frac": bfrac, "neg_worst": bworst,
                       "hit": hit, "graph_replays": stats["graph_replays"],
-                      "captures": stats["captures"], "ring_puts": ring["puts"], "ar_err": err}))
+                      "captures": stats["captures"], "ring_puts": ring["puts"], "ar_err": err,
+                      "pipelined": stats["pipelined"], "max_batch": batch}))
     except Exception:  # pragma: no cover - surfaced through the queue
         import traceback
 
         q.put(("err", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_tp_engine_on_one_gpu_matches_dense_oracle(world):
+@pytest.mark.parametrize("world,pipeline,batch", [(2, False, 8), (4, False, 8), (8, False, 8),
+                                                  (2, True, 64), (4, True, 64), (8, True, 64)])
+def test_tp_engine_on_one_gpu_matches_dense_oracle(world, pipeline, batch):
+    """(pipeline=True, batch 64) is the config-4 engine as shipped: one-deep
+    pipelined graph decode over the shared-memory step ring, fused two-shot
+    all-reduce + RMSNorm at the layer boundaries."""
     from conftest import release_gpu_memory
 
     release_gpu_memory()  # engines / cached blocks earlier tests left in this process
@@ -158,7 +173,8 @@ def test_tp_engine_on_one_gpu_matches_dense_oracle(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipeline, batch))
+             for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -178,4 +194,5 @@ def test_tp_engine_on_one_gpu_matches_dense_oracle(world):
     assert res["ar_err"] == 0
     assert res["hit"] > 0 and res["graph_replays"] > 0 and res["captures"] > 0
     assert res["frac"] == 1.0, res
+    assert res["pipelined"] == pipeline
     assert res["neg_frac"] < 1.0 and res["neg_worst"] > 0.05, res

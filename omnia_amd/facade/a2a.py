@@ -7,7 +7,10 @@ Reference: ``internal/facade/a2a/server.go:56-104`` (PromptKit server/a2a),
 (``spec.facades[].a2a.clients[].exposeAsTools``).
 
 Methods: ``message/send`` (+ legacy ``tasks/send``), ``message/stream``
-(SSE; legacy ``tasks/sendSubscribe``), ``tasks/get``, ``tasks/cancel``.
+(SSE; legacy ``tasks/sendSubscribe``), ``tasks/get``, ``tasks/cancel``,
+``tasks/resubscribe`` (SSE).  Task lifecycle and cross-replica cancel:
+``redis_task_store.go:361-395`` (validated transitions, state changes published
+on a pub/sub channel per task).
 """
 from __future__ import annotations
 
@@ -22,21 +25,108 @@ from ..api.proto import runtime_v1 as pb
 from ..observability import metrics as M
 
 TERMINAL = {"completed", "failed", "canceled", "rejected"}
+# isValidTransition (internal/facade/a2a/redis_task_store.go:379-395)
+TRANSITIONS = {
+    "submitted": {"working"},
+    "working": {"completed", "failed", "canceled", "input-required", "auth-required",
+                "rejected"},
+    "input-required": {"working", "canceled"},
+    "auth-required": {"working", "canceled"},
+}
 
 
-class MemoryTaskStore:
-    def __init__(self):
+class InvalidTransition(Exception):
+    pass
+
+
+class TaskNotFound(Exception):
+    pass
+
+
+def _check(frm: str, to: str):
+    if to not in TRANSITIONS.get(frm, ()):
+        raise InvalidTransition(f"invalid task state transition {frm} -> {to}")
+
+
+class _TaskStoreBase:
+    """Lifecycle over a key/value + pub/sub backend: tasks are created
+    ``submitted``; every state change is validated against :data:`TRANSITIONS`
+    and published on the task's event channel, which is what makes a cancel on
+    one facade replica reach the replica running the task, and what
+    ``tasks/resubscribe`` streams."""
+
+    async def create(self, tid: str, ctx: str, message: dict) -> dict:
+        task = {"id": tid, "contextId": ctx, "kind": "task",
+                "status": {"state": "submitted", "timestamp": time.time()},
+                "history": [message], "artifacts": []}
+        await self.put(task)
+        return task
+
+    async def set_state(self, task: dict, state: str, message: dict | None = None) -> dict:
+        cur = await self.get(task["id"]) or task
+        _check(cur["status"]["state"], state)
+        task["status"] = {"state": state, "timestamp": time.time(),
+                          **({"message": message} if message else {})}
+        await self.put(task)
+        await self.publish(task["id"], state)
+        return task
+
+    async def cancel(self, tid: str) -> dict:
+        t = await self.get(tid)
+        if t is None:
+            raise TaskNotFound(tid)
+        _check(t["status"]["state"], "canceled")
+        t["status"] = {"state": "canceled", "timestamp": time.time()}
+        await self.put(t)
+        await self.publish(tid, "canceled")
+        return t
+
+
+class MemoryTaskStore(_TaskStoreBase):
+    def __init__(self, max_tasks: int = 10000):
         self.tasks: dict[str, dict] = {}
+        self.max_tasks = max_tasks
+        self.subs: dict[str, set] = {}
 
     async def put(self, task: dict):
         self.tasks[task["id"]] = json.loads(json.dumps(task))
+        if len(self.tasks) > self.max_tasks:  # evict the oldest terminal tasks
+            for k in [k for k, t in self.tasks.items()
+                      if t["status"]["state"] in TERMINAL][: len(self.tasks) - self.max_tasks]:
+                self.tasks.pop(k, None)
 
     async def get(self, tid: str):
         t = self.tasks.get(tid)
         return json.loads(json.dumps(t)) if t else None
 
+    async def publish(self, tid: str, state: str):
+        for q in list(self.subs.get(tid, ())):
+            q.put_nowait(state)
 
-class RedisTaskStore:
+    async def subscribe(self, tid: str):
+        q: asyncio.Queue = asyncio.Queue()
+        self.subs.setdefault(tid, set()).add(q)
+        store = self
+
+        class _Sub:
+            async def get(self, timeout=None):
+                try:
+                    return await asyncio.wait_for(q.get(), timeout)
+                except asyncio.TimeoutError:
+                    return None
+
+            def close(self):
+                store.subs.get(tid, set()).discard(q)
+                if not store.subs.get(tid):
+                    store.subs.pop(tid, None)
+
+        return _Sub()
+
+
+class RedisTaskStore(_TaskStoreBase):
+    """Tasks as JSON under ``omnia:a2a:task:<id>`` (TTL) and state events on the
+    pub/sub channel ``omnia:a2a:events:<id>`` (``redis_task_store.go``)."""
+
     def __init__(self, client, ttl_s: int = 86400):
         self.r = client
         self.ttl_s = ttl_s
@@ -47,6 +137,25 @@ class RedisTaskStore:
     async def get(self, tid):
         v = await self.r.get(f"omnia:a2a:task:{tid}")
         return json.loads(v) if v else None
+
+    async def publish(self, tid: str, state: str):
+        try:
+            await self.r.publish(f"omnia:a2a:events:{tid}", state)
+        except Exception:  # noqa: BLE001 - best effort, like the reference
+            pass
+
+    async def subscribe(self, tid: str):
+        sub = await self.r.subscribe(f"omnia:a2a:events:{tid}")
+
+        class _Sub:
+            async def get(self, timeout=None):
+                m = await sub.get(timeout)
+                return m[1] if m else None
+
+            def close(self):
+                sub.close()
+
+        return _Sub()
 
 
 def agent_card(name: str, description: str, url: str, skills: list | None = None,
@@ -71,9 +180,46 @@ def _text_of(message: dict) -> str:
     return "\n".join(out)
 
 
+def _tool_results(message: dict, pending: list[dict]) -> dict[str, str]:
+    """Client-tool results carried by a resume message: ``data`` parts
+    ``{"toolCallId": id, "result": ...}`` (or ``{"call_id", "result"}``); a
+    single pending call also accepts the message's text / data as its result."""
+    out = {}
+    for p in message.get("parts", []):
+        d = p.get("data") if p.get("kind") == "data" else None
+        if isinstance(d, dict) and (d.get("toolCallId") or d.get("call_id")):
+            cid = d.get("toolCallId") or d.get("call_id")
+            out[cid] = json.dumps(d.get("result"))
+    if not out and len(pending) == 1:
+        txt = _text_of(message)
+        try:
+            json.loads(txt)
+        except ValueError:
+            txt = json.dumps(txt)
+        out[pending[0]["id"]] = txt
+    return out
+
+
+class _Parked:
+    """A runtime stream waiting for a client-tool result (task input-required)."""
+
+    def __init__(self, stream, text: list, task: dict, timer):
+        self.stream, self.text, self.task, self.timer = stream, text, task, timer
+
+
 class A2AServer:
+    """JSON-RPC task lifecycle (PromptKit ``server/a2a`` semantics):
+    ``submitted -> working -> completed | failed | canceled | input-required``.
+    A client-tool call leaves the task ``input-required`` with its runtime
+    stream parked (``park_timeout_s``); a ``message/send`` on the same task with
+    the tool result resumes it (``input-required -> working``) on that stream.
+    ``tasks/cancel`` goes through the task store: the state change is published,
+    and whichever replica runs the task aborts its stream mid-turn.
+    ``tasks/resubscribe`` streams a task's remaining state events (SSE)."""
+
     def __init__(self, runtime_client, name: str, description: str = "", base_url: str = "",
-                 task_store=None, metadata: dict | None = None, skills: list | None = None):
+                 task_store=None, metadata: dict | None = None, skills: list | None = None,
+                 park_timeout_s: float = 300.0):
         self.client = runtime_client
         self.skills = skills
         self.name = name
@@ -81,36 +227,122 @@ class A2AServer:
         self.base_url = base_url
         self.tasks = task_store or MemoryTaskStore()
         self.md = metadata or {}
-        self.cancelled: set = set()
+        self.park_timeout_s = park_timeout_s
+        self.parked: dict[str, _Parked] = {}
 
     async def card(self, request):
         url = self.base_url or f"http://{request.host}/a2a"
         return web.json_response(agent_card(self.name, self.description, url, self.skills))
 
+    async def _watch_cancel(self, tid: str, flag: asyncio.Event, stream):
+        sub = await self.tasks.subscribe(tid)
+        try:
+            while True:
+                st = await sub.get()
+                if st is None:
+                    return
+                if st == "canceled":
+                    flag.set()
+                    await stream.close()  # unblocks a recv() waiting mid-turn
+                    return
+        finally:
+            sub.close()
+
     async def _run(self, message: dict, emit=None) -> dict:
-        tid = message.get("taskId") or str(uuid.uuid4())
+        tid = message.get("taskId") or ""
+        existing = await self.tasks.get(tid) if tid else None
+        if existing is not None:
+            return await self._resume(existing, message, emit)
+        tid = tid or str(uuid.uuid4())
         ctx = message.get("contextId") or str(uuid.uuid4())
-        task = {"id": tid, "contextId": ctx, "kind": "task",
-                "status": {"state": "working", "timestamp": time.time()},
-                "history": [message], "artifacts": []}
-        await self.tasks.put(task)
+        task = await self.tasks.create(tid, ctx, message)
+        await self.tasks.set_state(task, "working")
         if emit:
             await emit({"kind": "status-update", "taskId": tid, "contextId": ctx,
                         "status": task["status"], "final": False})
         stream = await self.client.open({**self.md, "x-omnia-session-id": ctx,
                                          "x-omnia-origin": "a2a"})
-        text = []
+        md = {str(k): str(v) for k, v in (message.get("metadata") or {}).items()}
+        await stream.send(pb.ClientMessage(session_id=ctx, content=_text_of(message),
+                                           metadata=md))
+        return await self._pump(task, stream, [], emit)
+
+    async def _resume(self, task: dict, message: dict, emit=None) -> dict:
+        tid, ctx = task["id"], task["contextId"]
+        if task["status"]["state"] != "input-required":
+            raise InvalidTransition(f"task {tid} is {task['status']['state']}, not "
+                                    "input-required")
+        task["history"].append(message)
+        pending = (task.get("metadata") or {}).get("pendingToolCalls") or []
+        parked = self.parked.pop(tid, None)
+        await self.tasks.set_state(task, "working")
+        if emit:
+            await emit({"kind": "status-update", "taskId": tid, "contextId": ctx,
+                        "status": task["status"], "final": False})
+        results = _tool_results(message, pending)
+        if parked is not None:
+            parked.timer.cancel()
+            stream, text = parked.stream, parked.text
+            for c in pending:
+                r = results.get(c["id"])
+                await stream.send(pb.ClientMessage(session_id=ctx, client_tool_result=(
+                    pb.ClientToolResult(call_id=c["id"], result_json=r) if r is not None else
+                    pb.ClientToolResult(call_id=c["id"], is_rejected=True,
+                                        rejection_reason="no result supplied"))))
+        else:
+            # the stream was parked on another replica (or timed out): continue the
+            # conversation on a fresh turn carrying the tool results as the message
+            stream, text = await self.client.open({**self.md, "x-omnia-session-id": ctx,
+                                                   "x-omnia-origin": "a2a"}), []
+            await stream.send(pb.ClientMessage(session_id=ctx, content=json.dumps(
+                {"tool_results": results}) if results else _text_of(message)))
+        task.setdefault("metadata", {}).pop("pendingToolCalls", None)
+        return await self._pump(task, stream, text, emit)
+
+    async def _park_watch(self, tid: str):
+        """A parked stream lives until the resume, a cancel published by ANY
+        replica, or ``park_timeout_s`` (then the task is canceled)."""
+        sub = await self.tasks.subscribe(tid)
         try:
-            await stream.send(pb.ClientMessage(session_id=ctx, content=_text_of(message)))
+            t0 = time.monotonic()
             while True:
-                f = await stream.recv()
+                left = self.park_timeout_s - (time.monotonic() - t0)
+                st = await sub.get(timeout=max(0.0, left)) if left > 0 else None
+                if st in (None, "canceled"):
+                    break
+        finally:
+            sub.close()
+        p = self.parked.pop(tid, None)
+        if p is None:
+            return
+        await p.stream.close()
+        try:
+            await self.tasks.cancel(tid)
+        except (InvalidTransition, TaskNotFound):
+            pass  # already canceled (or gone)
+
+    async def _pump(self, task: dict, stream, text: list, emit=None) -> dict:
+        tid, ctx = task["id"], task["contextId"]
+        cancelled = asyncio.Event()
+        watcher = asyncio.ensure_future(self._watch_cancel(tid, cancelled, stream))
+        park = False
+        final_state = None
+        try:
+            while True:
+                try:
+                    f = await stream.recv()
+                except (asyncio.CancelledError, Exception):
+                    # a cancel closes the stream under a pending recv (gRPC raises)
+                    if not cancelled.is_set():
+                        raise
+                    f = None
+                if cancelled.is_set():
+                    final_state = "canceled"
+                    break
                 if f is None:
-                    task["status"] = {"state": "failed", "timestamp": time.time()}
+                    await self.tasks.set_state(task, "failed")
                     break
                 k = f.WhichOneof("message")
-                if tid in self.cancelled:
-                    task["status"] = {"state": "canceled", "timestamp": time.time()}
-                    break
                 if k == "chunk":
                     text.append(f.chunk.content)
                     if emit:
@@ -126,26 +358,69 @@ class A2AServer:
                              "parts": [{"kind": "text", "text": final}], "contextId": ctx,
                              "taskId": tid}
                     task["history"].append(reply)
-                    task["status"] = {"state": "completed", "message": reply,
-                                      "timestamp": time.time()}
-                    task["metadata"] = {"usage": {"input_tokens": f.done.usage.input_tokens,
-                                                  "output_tokens": f.done.usage.output_tokens}}
+                    task.setdefault("metadata", {})["usage"] = {
+                        "input_tokens": f.done.usage.input_tokens,
+                        "output_tokens": f.done.usage.output_tokens}
+                    await self.tasks.set_state(task, "completed", reply)
                     break
                 elif k == "error":
-                    task["status"] = {"state": "failed", "timestamp": time.time(),
-                                      "message": {"role": "agent", "parts": [
-                                          {"kind": "text", "text": f.error.message}]}}
+                    await self.tasks.set_state(task, "failed", {"role": "agent", "parts": [
+                        {"kind": "text", "text": f.error.message}]})
                     break
                 elif k == "tool_call":
-                    task["status"] = {"state": "input-required", "timestamp": time.time()}
+                    tc = f.tool_call
+                    calls = [{"id": tc.id, "name": tc.name, "arguments": tc.arguments_json}]
+                    task.setdefault("metadata", {})["pendingToolCalls"] = calls
+                    msg = {"role": "agent", "kind": "message", "messageId": str(uuid.uuid4()),
+                           "contextId": ctx, "taskId": tid,
+                           "parts": [{"kind": "data", "data": {"toolCalls": calls}}]}
+                    await self.tasks.set_state(task, "input-required", msg)
+                    park = True
                     break
+        except (ConnectionError, OSError):
+            final_state = "canceled" if cancelled.is_set() else None
+            if final_state is None:
+                await self.tasks.set_state(task, "failed")
         finally:
-            await stream.close()
-        await self.tasks.put(task)
+            watcher.cancel()
+            if park and not cancelled.is_set():
+                self.parked[tid] = _Parked(stream, text, task, asyncio.ensure_future(
+                    self._park_watch(tid)))
+            else:
+                await stream.close()
+        if final_state == "canceled":
+            task = await self.tasks.get(tid) or task
         if emit:
             await emit({"kind": "status-update", "taskId": tid, "contextId": ctx,
-                        "status": task["status"], "final": True})
+                        "status": task["status"],
+                        "final": task["status"]["state"] in TERMINAL or park})
         return task
+
+    async def resubscribe(self, tid: str, emit) -> dict | None:
+        """``tasks/resubscribe``: the task's current status, then every state
+        change published for it until a terminal / input-required state."""
+        sub = await self.tasks.subscribe(tid)
+        try:
+            t = await self.tasks.get(tid)
+            if t is None:
+                return None
+            done = lambda s: s in TERMINAL or s == "input-required"  # noqa: E731
+            await emit({"kind": "status-update", "taskId": tid, "contextId": t["contextId"],
+                        "status": t["status"], "final": done(t["status"]["state"])})
+            while not done(t["status"]["state"]):
+                st = await sub.get(timeout=self.park_timeout_s)
+                if st is None:
+                    break
+                t = await self.tasks.get(tid) or t
+                if t["status"]["state"] == "completed" and t.get("artifacts"):
+                    await emit({"kind": "artifact-update", "taskId": tid,
+                                "contextId": t["contextId"], "artifact": t["artifacts"][0],
+                                "append": False})
+                await emit({"kind": "status-update", "taskId": tid, "contextId": t["contextId"],
+                            "status": t["status"], "final": done(t["status"]["state"])})
+            return t
+        finally:
+            sub.close()
 
     async def rpc(self, request):
         try:
@@ -164,15 +439,7 @@ class A2AServer:
             return web.json_response({"jsonrpc": "2.0", "id": rid,
                                       "error": {"code": code, "message": msg}})
 
-        if method in ("message/send", "tasks/send"):
-            msg = params.get("message")
-            if not msg:
-                return err(-32602, "params.message required")
-            return ok(await self._run(msg))
-        if method in ("message/stream", "tasks/sendSubscribe"):
-            msg = params.get("message")
-            if not msg:
-                return err(-32602, "params.message required")
+        async def sse(run):
             resp = web.StreamResponse(headers={"Content-Type": "text/event-stream",
                                                "Cache-Control": "no-cache"})
             await resp.prepare(request)
@@ -181,22 +448,48 @@ class A2AServer:
                 data = {"jsonrpc": "2.0", "id": rid, "result": ev}
                 await resp.write(f"data: {json.dumps(data)}\n\n".encode())
 
-            await self._run(msg, emit)
+            await run(emit)
             await resp.write_eof()
             M.A2A_REQUESTS.labels(method, "ok").inc()
             return resp
+
+        if method in ("message/send", "tasks/send"):
+            msg = params.get("message")
+            if not msg:
+                return err(-32602, "params.message required")
+            try:
+                return ok(await self._run(msg))
+            except InvalidTransition as e:
+                return err(-32002, str(e))
+        if method in ("message/stream", "tasks/sendSubscribe"):
+            msg = params.get("message")
+            if not msg:
+                return err(-32602, "params.message required")
+            t = await self.tasks.get(msg.get("taskId") or "") if msg.get("taskId") else None
+            if t is not None and t["status"]["state"] != "input-required":
+                return err(-32002, f"task {t['id']} is {t['status']['state']}, not "
+                                   "input-required")
+            return await sse(lambda emit: self._run(msg, emit))
+        if method == "tasks/resubscribe":
+            tid = params.get("id", "")
+            if await self.tasks.get(tid) is None:
+                return err(-32001, "task not found")
+            return await sse(lambda emit: self.resubscribe(tid, emit))
         if method == "tasks/get":
             t = await self.tasks.get(params.get("id", ""))
             return ok(t) if t else err(-32001, "task not found")
         if method == "tasks/cancel":
-            t = await self.tasks.get(params.get("id", ""))
-            if t is None:
+            tid = params.get("id", "")
+            try:
+                t = await self.tasks.cancel(tid)
+            except TaskNotFound:
                 return err(-32001, "task not found")
-            if t["status"]["state"] in TERMINAL:
+            except InvalidTransition:
                 return err(-32002, "task is not cancelable")
-            self.cancelled.add(t["id"])
-            t["status"] = {"state": "canceled", "timestamp": time.time()}
-            await self.tasks.put(t)
+            p = self.parked.pop(tid, None)
+            if p is not None:  # parked here: release its runtime stream now
+                p.timer.cancel()
+                await p.stream.close()
             return ok(t)
         return err(-32601, f"method {method} not found")
 

@@ -8,6 +8,7 @@
   OMNIA_MODE (agent|function), OMNIA_FACADE_TYPES (websocket,rest,a2a,mcp)
   OMNIA_GRACE_WINDOW_SECONDS / OMNIA_ROUTE_REDIS_URL / POD_IP (realtime blip-resume)
   OMNIA_HANDLER_MODE (runtime|echo|demo), OMNIA_INPUT_SCHEMA / OMNIA_OUTPUT_SCHEMA
+  OMNIA_A2A_TASK_STORE_URL (redis://...: A2A tasks + state pub/sub across replicas)
   auth: OMNIA_AUTH_SHARED_TOKEN, OMNIA_AUTH_CLIENT_KEYS (json {id: sha256}),
         OMNIA_OIDC_ISSUER / OMNIA_OIDC_AUDIENCE / OMNIA_OIDC_HS256_SECRET /
         OMNIA_OIDC_JWKS_FILE, OMNIA_EDGE_TRUST=true,
@@ -147,6 +148,8 @@ def build_facade(env, runtime_client, recorder=None, mgmt_resolver=None) -> Faca
     routes = route_store_from_env(env)  # OMNIA_ROUTE_REDIS_URL
     types = set(filter(None, env.get("OMNIA_FACADE_TYPES", "").split(",")))
 
+    a2a_store: dict = {}  # one task store for the public listener and its twin
+
     def make(auth: AuthChain) -> FacadeServer:
         f = FacadeServer(cfg, handler=handler, runtime_client=runtime_client, auth=auth,
                          recorder=recorder, media_store=media, routes=routes)
@@ -155,9 +158,15 @@ def build_facade(env, runtime_client, recorder=None, mgmt_resolver=None) -> Faca
 
             mount_media(f.app, media)
         if "a2a" in types:
-            from .a2a import mount_a2a
+            from .a2a import RedisTaskStore, mount_a2a
 
-            mount_a2a(f, runtime_client)
+            store = None
+            if env.get("OMNIA_A2A_TASK_STORE_URL"):  # redis://... shared by the replicas
+                from ..utils.resp import RedisClient
+
+                store = a2a_store.setdefault("s", RedisTaskStore(
+                    RedisClient(env["OMNIA_A2A_TASK_STORE_URL"])))
+            mount_a2a(f, runtime_client, task_store=store)
         if "mcp" in types or env.get("OMNIA_MCP_ENABLED", "").lower() == "true":
             from .mcp import mount_mcp
 

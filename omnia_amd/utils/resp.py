@@ -193,6 +193,69 @@ class RedisClient:
     async def xack(self, stream, group, *ids):
         return await self.execute("XACK", stream, group, *ids)
 
+    async def publish(self, channel, message) -> int:
+        return await self.execute("PUBLISH", channel, message)
+
+    async def subscribe(self, *channels) -> "Subscription":
+        """A dedicated connection in subscribe mode.  Returns once the server
+        confirmed every channel, so a PUBLISH issued after this cannot be lost."""
+        sub = Subscription(self)
+        await sub.open(*channels)
+        return sub
+
+
+class Subscription:
+    """``async for channel, payload in sub`` over a SUBSCRIBE connection."""
+
+    def __init__(self, client: RedisClient):
+        self.c = client
+        self._rw = None
+
+    async def open(self, *channels):
+        c = self.c
+        r, w = await asyncio.wait_for(asyncio.open_connection(c.host, c.port), c.timeout)
+        self._rw = (r, w)
+        if c.password:
+            w.write(encode("AUTH", c.password))
+            await w.drain()
+            await read_reply(r)
+        w.write(encode("SUBSCRIBE", *channels))
+        await w.drain()
+        for _ in channels:
+            await asyncio.wait_for(read_reply(r), c.timeout)  # ["subscribe", ch, n]
+
+    async def get(self, timeout: float | None = None):
+        """Next (channel, payload) message, or None on timeout / close."""
+        r, _ = self._rw
+        while True:
+            try:
+                m = await asyncio.wait_for(read_reply(r), timeout)
+            except asyncio.TimeoutError:
+                return None
+            except (ConnectionError, asyncio.IncompleteReadError):
+                return None
+            if isinstance(m, list) and len(m) == 3 and m[0] in (b"message", "message"):
+                ch, pl = m[1], m[2]
+                return (ch.decode() if isinstance(ch, bytes) else ch,
+                        pl.decode() if isinstance(pl, bytes) else pl)
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self):
+        m = await self.get()
+        if m is None:
+            raise StopAsyncIteration
+        return m
+
+    def close(self):
+        if self._rw is not None:
+            try:
+                self._rw[1].close()
+            except Exception:
+                pass
+            self._rw = None
+
 
 # ------------------------------------------------------------------ server
 class MiniRedis:
@@ -206,6 +269,7 @@ class MiniRedis:
         self._seq = itertools.count(1)
         self.server = None
         self.port = 0
+        self.subs: dict[bytes, set] = {}  # channel -> subscribed connection writers
 
     async def start(self, host="127.0.0.1", port=0):
         self.server = await asyncio.start_server(self._handle, host, port, backlog=1024)
@@ -229,14 +293,24 @@ class MiniRedis:
         return k in self.data
 
     async def _handle(self, r, w):
+        mine: set = set()
         try:
             while True:
                 req = await read_reply(r)
                 if not isinstance(req, list) or not req:
                     break
+                a = [x if isinstance(x, bytes) else str(x).encode() for x in req]
+                if a[0].upper() in (b"SUBSCRIBE", b"UNSUBSCRIBE"):
+                    sub = a[0].upper() == b"SUBSCRIBE"
+                    for ch in a[1:]:
+                        (self.subs.setdefault(ch, set()).add if sub else
+                         self.subs.setdefault(ch, set()).discard)(w)
+                        (mine.add if sub else mine.discard)(ch)
+                        w.write(_enc_reply([a[0].lower(), ch, len(mine)]))
+                    await w.drain()
+                    continue
                 try:
-                    out = self.dispatch([x if isinstance(x, bytes) else str(x).encode()
-                                         for x in req])
+                    out = self.dispatch(a)
                 except Exception as e:  # noqa: BLE001
                     out = _Err(f"ERR {e}")
                 w.write(_enc_reply(out))
@@ -244,7 +318,20 @@ class MiniRedis:
         except (ConnectionError, asyncio.IncompleteReadError):
             pass
         finally:
+            for ch in mine:
+                self.subs.get(ch, set()).discard(w)
             w.close()
+
+    def c_publish(self, a):
+        ch, msg = a[0], a[1]
+        n = 0
+        for w in list(self.subs.get(ch, ())):
+            try:
+                w.write(_enc_reply([b"message", ch, msg]))
+                n += 1
+            except Exception:  # noqa: BLE001 - a subscriber went away
+                self.subs[ch].discard(w)
+        return n
 
     def dispatch(self, a: list[bytes]):
         cmd = a[0].upper().decode()

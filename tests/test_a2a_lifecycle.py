@@ -1,0 +1,190 @@
+"""A2A task lifecycle (``internal/facade/a2a/redis_task_store.go:361-395``):
+validated transitions, a client-tool call parking the task ``input-required``
+and a resume on the same task carrying the tool result, cancel propagated
+through the task store's pub/sub to the replica running the task (mid-turn),
+``tasks/resubscribe`` over SSE, bounded state (no cancel set)."""
+import asyncio
+import json
+
+import aiohttp
+import pytest
+from aiohttp import web
+
+from omnia_amd.facade.a2a import (A2AServer, InvalidTransition, MemoryTaskStore, RedisTaskStore,
+                                  TRANSITIONS)
+from omnia_amd.facade.runtime_client import InProcessRuntimeClient
+from omnia_amd.utils.resp import MiniRedis, RedisClient
+
+from test_runtime import make_service
+
+
+def _msg(text, **kw):
+    return {"role": "user", "kind": "message", "messageId": "m", "parts": [
+        {"kind": "text", "text": text}], **kw}
+
+
+async def _serve(*servers):
+    out = []
+    for srv in servers:
+        app = web.Application()
+        app.router.add_post("/a2a", srv.rpc)
+        runner = web.AppRunner(app)
+        await runner.setup()
+        site = web.TCPSite(runner, "127.0.0.1", 0)
+        await site.start()
+        out.append((runner, f"http://127.0.0.1:{site._server.sockets[0].getsockname()[1]}/a2a"))
+    return out
+
+
+async def _rpc(s, url, method, params):
+    async with s.post(url, json={"jsonrpc": "2.0", "id": 1, "method": method,
+                                 "params": params}) as r:
+        return await r.json()
+
+
+def test_transition_table_matches_reference():
+    assert TRANSITIONS["submitted"] == {"working"}
+    assert TRANSITIONS["input-required"] == {"working", "canceled"}
+    assert "completed" not in TRANSITIONS  # terminal: nothing leaves it
+
+    async def go():
+        st = MemoryTaskStore()
+        t = await st.create("t1", "c1", _msg("x"))
+        with pytest.raises(InvalidTransition):
+            await st.set_state(t, "completed")  # submitted -> completed skips working
+        await st.set_state(t, "working")
+        await st.set_state(t, "completed")
+        with pytest.raises(InvalidTransition):
+            await st.cancel("t1")  # terminal
+
+    asyncio.run(go())
+
+
+def test_client_tool_input_required_then_resume():
+    async def go():
+        svc, _, _ = make_service()
+        srv = A2AServer(InProcessRuntimeClient(svc), "agent")
+        [(runner, url)] = await _serve(srv)
+        try:
+            async with aiohttp.ClientSession() as s:
+                r = await _rpc(s, url, "message/send", {"message": _msg(
+                    "where am i", metadata={"mock_scenario": "client"})})
+                t = r["result"]
+                assert t["status"]["state"] == "input-required", t
+                calls = t["metadata"]["pendingToolCalls"]
+                assert calls[0]["name"] == "get_location"
+                assert t["id"] in srv.parked
+                # a resume with the tool result on the same task continues the turn
+                r = await _rpc(s, url, "message/send", {"message": {
+                    "role": "user", "kind": "message", "messageId": "m2", "taskId": t["id"],
+                    "contextId": t["contextId"], "parts": [{"kind": "data", "data": {
+                        "toolCallId": calls[0]["id"], "result": {"place": "home"}}}]}})
+                t2 = r["result"]
+                assert t2["status"]["state"] == "completed", t2
+                assert "home" in t2["artifacts"][0]["parts"][0]["text"]
+                assert t2["id"] == t["id"] and not srv.parked
+                # a completed task cannot be resumed
+                r = await _rpc(s, url, "message/send", {"message": _msg("again",
+                                                                         taskId=t["id"])})
+                assert r["error"]["code"] == -32002
+        finally:
+            await runner.cleanup()
+
+    asyncio.run(go())
+
+
+def test_cancel_reaches_the_running_replica_mid_turn():
+    """Two facade replicas share a Redis task store; B cancels a task A is
+    streaming; A's runtime stream is closed mid-turn (not between frames)."""
+    async def go():
+        redis = await MiniRedis().start()
+        svc, prov, _ = make_service()
+        prov.delay_s = 0.5  # every streamed delta takes 0.5 s
+        a = A2AServer(InProcessRuntimeClient(svc), "agent",
+                      task_store=RedisTaskStore(RedisClient(redis.url)))
+        b = A2AServer(InProcessRuntimeClient(svc), "agent",
+                      task_store=RedisTaskStore(RedisClient(redis.url)))
+        (ra, ua), (rb, ub) = await _serve(a, b)
+        try:
+            async with aiohttp.ClientSession() as s:
+                run = asyncio.ensure_future(_rpc(s, ua, "message/send", {"message": _msg(
+                    "tell me a long story", taskId="task-x")}))
+                for _ in range(100):  # wait until A marked it working
+                    await asyncio.sleep(0.05)
+                    g = await _rpc(s, ub, "tasks/get", {"id": "task-x"})
+                    if "result" in g and g["result"]["status"]["state"] == "working":
+                        break
+                c = await _rpc(s, ub, "tasks/cancel", {"id": "task-x"})
+                assert c["result"]["status"]["state"] == "canceled"
+                t0 = asyncio.get_running_loop().time()
+                done = await asyncio.wait_for(run, 5)
+                assert done["result"]["status"]["state"] == "canceled"
+                assert asyncio.get_running_loop().time() - t0 < 2.0
+                again = await _rpc(s, ub, "tasks/cancel", {"id": "task-x"})
+                assert again["error"]["code"] == -32002  # terminal: not cancelable
+        finally:
+            await ra.cleanup()
+            await rb.cleanup()
+            await redis.stop()
+
+    asyncio.run(go())
+
+
+def test_resubscribe_streams_remaining_states():
+    async def go():
+        svc, prov, _ = make_service()
+        prov.delay_s = 0.2
+        srv = A2AServer(InProcessRuntimeClient(svc), "agent")
+        [(runner, url)] = await _serve(srv)
+        try:
+            async with aiohttp.ClientSession() as s:
+                run = asyncio.ensure_future(_rpc(s, url, "message/send", {"message": _msg(
+                    "hi", taskId="task-r")}))
+                await asyncio.sleep(0.1)
+                events = []
+                async with s.post(url, json={"jsonrpc": "2.0", "id": 2,
+                                             "method": "tasks/resubscribe",
+                                             "params": {"id": "task-r"}}) as r:
+                    async for line in r.content:
+                        if line.startswith(b"data: "):
+                            events.append(json.loads(line[6:])["result"])
+                await run
+                states = [e["status"]["state"] for e in events if e["kind"] == "status-update"]
+                assert states[0] == "working" and states[-1] == "completed", states
+                assert events[-1]["final"] is True
+                r = await _rpc(s, url, "tasks/resubscribe", {"id": "nope"})
+                assert r["error"]["code"] == -32001
+        finally:
+            await runner.cleanup()
+
+    asyncio.run(go())
+
+
+def test_parked_task_canceled_from_another_replica_releases_stream():
+    async def go():
+        redis = await MiniRedis().start()
+        svc, _, _ = make_service()
+        a = A2AServer(InProcessRuntimeClient(svc), "agent",
+                      task_store=RedisTaskStore(RedisClient(redis.url)))
+        b = A2AServer(InProcessRuntimeClient(svc), "agent",
+                      task_store=RedisTaskStore(RedisClient(redis.url)))
+        (ra, ua), (rb, ub) = await _serve(a, b)
+        try:
+            async with aiohttp.ClientSession() as s:
+                r = await _rpc(s, ua, "message/send", {"message": _msg(
+                    "where", metadata={"mock_scenario": "client"})})
+                tid = r["result"]["id"]
+                assert tid in a.parked
+                c = await _rpc(s, ub, "tasks/cancel", {"id": tid})
+                assert c["result"]["status"]["state"] == "canceled"
+                for _ in range(40):
+                    if tid not in a.parked:
+                        break
+                    await asyncio.sleep(0.05)
+                assert tid not in a.parked  # A saw the published cancel
+        finally:
+            await ra.cleanup()
+            await rb.cleanup()
+            await redis.stop()
+
+    asyncio.run(go())

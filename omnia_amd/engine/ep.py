@@ -92,6 +92,8 @@ class EPModelRunner(ModelRunner):
             self.ep_stats["idle_fill"] += 1
             torch.cuda.current_stream().synchronize()
             return []
+        if self._tap is not None:  # correctness tap (the graph copied the rows)
+            self._tap_rows(seqs, self._tap[:n])
         return self.out_tok[:n].tolist()
 
 

@@ -269,11 +269,26 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         st = body.get("status", STATUS_ACTIVE)
         if st not in TERMINAL | {STATUS_ACTIVE}:
             return web.json_response({"error": "invalid_status"}, status=400)
+        prev = svc._get_session_only(sid)
+        prev = prev.status if prev is not None else ""  # captured before the in-place update
         try:
             s = svc.update_status(sid, st, body.get("endedAt"))
         except KeyError:
             return nf(sid)
+        await svc.publish_completed_if(prev, s)
         return web.json_response(s.to_json())
+
+    async def evaluate(request):
+        """POST /api/v1/sessions/{id}/evaluate (handler.go:265): 202 + a
+        ``session.evaluate`` event for the eval worker."""
+        sid = request.match_info["id"]
+        try:
+            await svc.publish_evaluate(sid)
+        except KeyError:
+            return nf(sid)
+        except (RuntimeError, ValueError) as e:
+            return web.json_response({"error": str(e)}, status=409)
+        return web.json_response({"sessionId": sid, "status": "queued"}, status=202)
 
     async def decorate(request):
         sid = request.match_info["id"]
@@ -394,6 +409,7 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         r.add_post(f"/api/v1/sessions/{{id}}/{path}", p)
         r.add_get(f"/api/v1/sessions/{{id}}/{path}", g)
     r.add_post("/api/v1/eval-results", eval_results_post)
+    r.add_post("/api/v1/sessions/{id}/evaluate", evaluate)
     r.add_get("/api/v1/eval-results/aggregate", eval_aggregate)
     r.add_get("/api/v1/sessions/{id}/eval-results",
               lambda req: _rows(svc, "eval_results", req))

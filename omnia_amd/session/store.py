@@ -461,7 +461,10 @@ class TieredSessionService:
         if self.publisher is not None:
             await self.publisher({"type": "message.appended", "sessionId": sid,
                                   "namespace": s.namespace, "agentName": s.agent_name,
-                                  "messageId": m.id, "role": m.role})
+                                  "messageId": m.id, "role": m.role,
+                                  "promptPackName": s.prompt_pack_name,
+                                  "promptPackVersion": s.prompt_pack_version,
+                                  "timestamp": time.time()})
         return m
 
     def record(self, table: str, sid: str, obj) -> None:
@@ -477,6 +480,31 @@ class TieredSessionService:
                 self.hot.put(s)
             except TierError:
                 pass
+
+    def _event(self, typ: str, s: Session) -> dict:
+        return {"type": typ, "sessionId": s.id, "namespace": s.namespace,
+                "agentName": s.agent_name, "promptPackName": s.prompt_pack_name,
+                "promptPackVersion": s.prompt_pack_version, "timestamp": time.time()}
+
+    async def publish_completed_if(self, prev: str, s: Session) -> None:
+        """``session.completed`` on the transition into completed
+        (``publishSessionCompleted``, service.go:413-446): the eval worker's
+        on_session_complete trigger."""
+        if self.publisher is not None and s.status == "completed" and prev != "completed":
+            await self.publisher(self._event("session.completed", s))
+
+    async def publish_evaluate(self, sid: str) -> Session:
+        """``session.evaluate``: on-demand evaluation by the eval worker
+        (``PublishEvaluateEvent``, service.go:655-679)."""
+        s = self._get_session_only(sid)
+        if s is None:
+            raise KeyError(sid)
+        if self.publisher is None:
+            raise RuntimeError("event publisher not configured")
+        if not s.agent_name:
+            raise ValueError("session has no agent")
+        await self.publisher(self._event("session.evaluate", s))
+        return s
 
     def update_status(self, sid: str, status: str, ended_at: float | None = None) -> Session:
         s = self._get_session_only(sid)

@@ -546,6 +546,25 @@ class MiniRedis:
                 out.append([p[2][0], list(p[2][1])])
         return out
 
+    def c_xautoclaim(self, a):
+        # XAUTOCLAIM k g consumer min-idle start [COUNT n]
+        grp = self.groups.get(a[0], {}).get(a[1])
+        if grp is None:
+            return _Err("NOGROUP No such key or consumer group")
+        c, min_idle = a[2], int(a[3]) / 1000
+        count = 100
+        if len(a) > 6 and a[5].upper() == b"COUNT":
+            count = int(a[6])
+        now = time.time()
+        out = []
+        for i, p in list(grp["pending"].items()):
+            if len(out) >= count:
+                break
+            if now - p[1] >= min_idle:
+                grp["pending"][i] = (c, now, p[2])
+                out.append([p[2][0], list(p[2][1])])
+        return [b"0-0", out, []]
+
     def c_flushall(self, a):
         self.data.clear()
         self.exp.clear()

@@ -63,18 +63,30 @@ def _check(mc, w, seqs, rows_by_seq, tol):
 
 
 def _full_mixtral(mc, seed):
-    """The whole model (every expert) on the CPU from the same per-(layer,
-    expert) generators the EP ranks draw their shards from."""
+    """The whole model (every expert) from the same per-(layer, expert)
+    generators the EP ranks draw their shards from -- drawn on the DEVICE in
+    the ranks' dtype (CPU and HIP generators produce different streams), then
+    moved to the CPU in fp32 for the oracle."""
     from omnia_amd.models.mixtral import MixtralModel
     from omnia_amd.parallel import state as pstate
 
     saved = pstate.get_state()
     pstate.set_state(pstate.ParallelState())
     try:
-        m = MixtralModel(mc, device="cpu", dtype=torch.float32, seed=seed, ep_mode="tp")
+        m = MixtralModel(mc, device="cuda", dtype=torch.bfloat16, seed=seed, ep_mode="tp")
     finally:
         pstate.set_state(saved)
-    return m.w
+
+    def cpu(x):
+        if isinstance(x, torch.Tensor):
+            return x.float().cpu()
+        if isinstance(x, dict):
+            return {k: cpu(v) for k, v in x.items()}
+        if isinstance(x, list):
+            return [cpu(v) for v in x]
+        return x
+
+    return cpu(m.w)
 
 
 def _env(rank, world, port):

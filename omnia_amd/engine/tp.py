@@ -58,15 +58,24 @@ class ShmRing:
 
     Layout: a 4 KiB control page (int64 ``[0]`` = slots published, ``[8 + r]`` =
     slots consumed by reader ``r``, ``[1]`` slot count, ``[2]`` payload bytes per
-    slot, ``[3]`` reader count) followed by ``nslots`` slots of ``HDR`` int64 +
-    payload.  Ordering: the writer stores payload, header, then the published
-    counter; x86-64 keeps stores in order and loads in order, so a reader that
-    sees the counter sees the slot."""
+    slot, ``[3]`` reader count, ``[4]`` writer pid, ``[72 + r]`` reader pids)
+    followed by ``nslots`` slots of ``HDR`` int64 + payload.  Ordering: the
+    writer stores payload, header, then the published counter; x86-64 keeps
+    stores in order and loads in order, so a reader that sees the counter sees
+    the slot (asserted at construction: ``hostsync.check_tso``).  Liveness: a
+    blocked reader or writer probes the other side's pid once a second and
+    raises if it died, instead of spinning forever."""
 
     CTRL = 4096
+    WRITER_PID, READER_PIDS = 4, 72
 
     def __init__(self, path: str, create: bool, nslots: int = 8, payload: int = 1 << 20,
-                 readers: int = 1):
+                 readers: int = 1, reader: int = -1):
+        from ..parallel.hostsync import check_tso
+
+        check_tso()
+        if readers > 64:
+            raise ValueError("ShmRing supports at most 64 readers")
         self.path = path
         if create:
             size = self.CTRL + nslots * (HDR * 8 + payload)
@@ -83,6 +92,10 @@ class ShmRing:
             self.ctrl[1], self.ctrl[2], self.ctrl[3] = nslots, payload, readers
         self.nslots, self.payload, self.readers = (int(self.ctrl[1]), int(self.ctrl[2]),
                                                    int(self.ctrl[3]))
+        if create:
+            self.ctrl[self.WRITER_PID] = os.getpid()
+        if reader >= 0:
+            self.ctrl[self.READER_PIDS + reader] = os.getpid()
         self.stride = HDR * 8 + self.payload
         self.hdrs = [np.ndarray((HDR,), dtype=np.int64, buffer=self.mm,
                                 offset=self.CTRL + i * self.stride) for i in range(self.nslots)]
@@ -94,13 +107,19 @@ class ShmRing:
     # ------------------------------------------------------------- writer
     def put(self, hdr: list[int], payload: np.ndarray | None = None, timeout_s: float = 600.0):
         seq = int(self.ctrl[0])
-        t0 = None
+        t0 = probe = None
         while seq - int(self.ctrl[8:8 + self.readers].min()) >= self.nslots:
+            now = time.monotonic()
             if t0 is None:
-                t0 = time.monotonic()
+                t0, probe = now, now + 1.0
                 self.stats["full_waits"] += 1
-            elif time.monotonic() - t0 > timeout_s:
+            elif now - t0 > timeout_s:
                 raise TimeoutError("TP command ring full: a worker stopped consuming")
+            elif now > probe:
+                probe = now + 1.0
+                for r in range(self.readers):
+                    if seq - int(self.ctrl[8 + r]) >= self.nslots:
+                        self._check_alive(self.READER_PIDS + r, f"TP worker (reader {r})")
             time.sleep(0)
         i = seq % self.nslots
         n = 0
@@ -118,12 +137,30 @@ class ShmRing:
         self.stats["puts"] += 1
 
     # ------------------------------------------------------------- reader
-    def get(self, reader: int, spin_s: float = 0.002) -> tuple[list[int], np.ndarray]:
+    def _check_alive(self, idx: int, who: str):
+        from ..parallel.hostsync import _alive
+
+        pid = int(self.ctrl[idx])
+        if not _alive(pid):
+            raise RuntimeError(f"{who} (pid {pid}) died: TP command ring abandoned")
+
+    def get(self, reader: int, spin_s: float = 0.002,
+            timeout_s: float | None = None) -> tuple[list[int], np.ndarray]:
+        """Next command for ``reader``.  Spins ``spin_s``, then polls with short
+        sleeps; an idle server legitimately waits without bound (``timeout_s``
+        None), but a dead writer is detected within a second."""
         mine = int(self.ctrl[8 + reader])
         t0 = time.perf_counter()
+        probe = t0 + 1.0
         while int(self.ctrl[0]) <= mine:
-            if time.perf_counter() - t0 > spin_s:
+            now = time.perf_counter()
+            if now - t0 > spin_s:
                 time.sleep(0.0002)
+                if now > probe:
+                    probe = now + 1.0
+                    self._check_alive(self.WRITER_PID, "TP rank 0 (ring writer)")
+                    if timeout_s is not None and now - t0 > timeout_s:
+                        raise TimeoutError("TP command ring: no command within the deadline")
         i = mine % self.nslots
         hdr = self.hdrs[i].tolist()
         return hdr, self.bodies[i][:hdr[HDR - 1]]
@@ -173,7 +210,7 @@ class TPChannel:
                                 st.tp_size - 1)
         dist.broadcast_object_list(path, src=self.src, group=self.group)
         if not create:
-            self.ring = ShmRing(path[0], False)
+            self.ring = ShmRing(path[0], False, reader=self.reader)
         pstate.barrier_group(self.group)  # every reader attached before any unlink
         if create:
             os.unlink(path[0])  # the mappings stay valid; nothing is left in /dev/shm

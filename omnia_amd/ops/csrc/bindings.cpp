@@ -47,6 +47,10 @@ int omnia_sample(int* out_tok, float* out_logprob, const void* logits, int logit
                  const int* top_k, const float* top_p, const uint64_t* seeds,
                  const int64_t* steps, int* counts, const float* freq_pen, const float* pres_pen,
                  const float* rep_pen, hipStream_t s);
+int omnia_tp_gumbel(float* pack, int64_t ld, int col, const void* logits, int rows,
+                    int64_t row_stride, int vocab, int vocab_start, const float* temperature,
+                    const int* top_k, const float* top_p, const int64_t* seeds,
+                    const int64_t* steps, hipStream_t s);
 int omnia_mean_pool_l2(float* out, const void* hidden, int64_t stride, const int* cu, int B,
                        int D, hipStream_t s);
 int omnia_cosine_scores(float* scores, const float* q, int nq, const void* m, int64_t N, int D,
@@ -271,6 +275,34 @@ void sample(at::Tensor out_tok, c10::optional<at::Tensor> out_logprob, at::Tenso
 }
 
 // K13: grammar mask -> -inf logits (mask int32 [rows, ceil(V/32)], bit v = allowed)
+// TP sampling: per-row Gumbel-max winner of this rank's vocab slice, written
+// into columns col, col+1 of the fp32 candidate pack [B, ld]
+void tp_gumbel(at::Tensor pack, int64_t col, at::Tensor logits, int64_t vocab_start,
+               at::Tensor temperature, c10::optional<at::Tensor> top_k,
+               c10::optional<at::Tensor> top_p, at::Tensor seeds,
+               c10::optional<at::Tensor> steps) {
+  CHECK_GPU(pack); CHECK_GPU(logits); CHECK_BF16(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V] inner-contiguous");
+  const int rows = logits.size(0), vocab = logits.size(1);
+  TORCH_CHECK(pack.scalar_type() == at::kFloat && pack.dim() == 2 && pack.stride(1) == 1 &&
+              pack.size(0) == rows && col >= 0 && col + 2 <= pack.size(1), "pack fp32 [B, ld]");
+  TORCH_CHECK(temperature.scalar_type() == at::kFloat && temperature.numel() >= rows &&
+              temperature.is_cuda(), "temperature fp32 [B]");
+  TORCH_CHECK(seeds.scalar_type() == at::kLong && seeds.numel() >= rows && seeds.is_cuda(),
+              "seeds int64 [B]");
+  if (top_k.has_value() && top_k->defined())
+    TORCH_CHECK(top_k->scalar_type() == at::kInt && top_k->numel() >= rows, "top_k int32 [B]");
+  if (top_p.has_value() && top_p->defined())
+    TORCH_CHECK(top_p->scalar_type() == at::kFloat && top_p->numel() >= rows, "top_p fp32 [B]");
+  if (steps.has_value() && steps->defined())
+    TORCH_CHECK(steps->scalar_type() == at::kLong && steps->numel() >= rows, "steps int64 [B]");
+  CHECK_RC(omnia_tp_gumbel(pack.data_ptr<float>(), pack.stride(0), (int)col, logits.data_ptr(),
+                           rows, logits.stride(0), vocab, (int)vocab_start,
+                           temperature.data_ptr<float>(), opt_ptr<int>(top_k),
+                           opt_ptr<float>(top_p), seeds.data_ptr<int64_t>(),
+                           opt_ptr<int64_t>(steps), cur_stream()), "tp_gumbel");
+}
+
 void apply_token_mask(at::Tensor logits, at::Tensor mask) {
   CHECK_GPU(logits); CHECK_GPU(mask); CHECK_I32(mask);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V]");
@@ -932,6 +964,7 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("ar_blocks", &omnia_ar_blocks);
   m.def("ar_max_ranks", &omnia_ar_max_ranks);
   m.def("apply_token_mask", &apply_token_mask);
+  m.def("tp_gumbel", &tp_gumbel);
   m.def("graph_launch_step", &graph_launch_step);
   m.def("graph_launch_staged", &graph_launch_staged);
   m.def("stage_copy", &stage_copy);

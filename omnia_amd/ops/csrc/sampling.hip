@@ -299,3 +299,112 @@ extern "C" int omnia_apply_token_mask(void* logits, int logits_is_bf16, int rows
                                                         words);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- TP Gumbel winner
+// Tensor-parallel sampling (parallel/tp_sampling.py): every TP rank reduces its
+// vocabulary slice of each pure-temperature row to ONE Gumbel-max winner,
+// argmax_v (logit_v / T - log(-log u_v)), with u a counter-based hash of
+// (request seed, step, GLOBAL vocab id) -- murmur3 fmix32, bit-identical to
+// tp_sampling.gumbel_uniform.  One pass over the bf16 logits, no noise tensor:
+// a 256-thread workgroup per row, 8 contiguous bf16 (one 16-byte load) per lane
+// per iteration.  Rows that are greedy or top-k / top-p filtered never read
+// their logits (their winner is unused) and get (-inf, vocab_start).
+// The (value, global id as float) pair is written straight into the candidate
+// pack the ranks all-gather (columns col, col + 1 of a [B, ld] fp32 tensor).
+namespace {
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
+
+__global__ void __launch_bounds__(256)
+tp_gumbel_kernel(float* __restrict__ pack, int64_t ld, int col,
+                 const uint16_t* __restrict__ logits, int64_t row_stride, int vocab,
+                 int vocab_start, const float* __restrict__ temperature,
+                 const int* __restrict__ top_k, const float* __restrict__ top_p,
+                 const int64_t* __restrict__ seeds, const int64_t* __restrict__ steps) {
+  const int row = blockIdx.x;
+  const float t = temperature[row];
+  float* dst = pack + (int64_t)row * ld + col;
+  const bool pure = t > 0.f && (top_k == nullptr || top_k[row] <= 0) &&
+                    (top_p == nullptr || top_p[row] >= 1.f);
+  if (!pure) {
+    if (threadIdx.x == 0) {
+      dst[0] = -INFINITY;
+      dst[1] = (float)vocab_start;
+    }
+    return;
+  }
+  const float tt = fmaxf(t, 1e-6f);
+  const uint64_t sd = (uint64_t)seeds[row];
+  const uint64_t st = steps ? (uint64_t)steps[row] : 0ull;
+  uint32_t h = fmix32((uint32_t)sd ^ fmix32((uint32_t)(sd >> 32) ^ 0x68BC21EBu));
+  h = fmix32(h ^ fmix32((uint32_t)st ^ 0x02E5BE93u));
+  const uint16_t* lr = logits + (int64_t)row * row_stride;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  auto visit = [&](float x, int v) {
+    const uint32_t r = fmix32(h ^ fmix32((uint32_t)(vocab_start + v) + 0x9E3779B9u));
+    float u = (float)(((double)r + 0.5) * (1.0 / 4294967296.0));
+    u = fminf(fmaxf(u, 1e-10f), 1.f - 1e-7f);
+    const float g = x / tt - logf(-logf(u));
+    if (g > best || (g == best && v < bi)) {
+      best = g;
+      bi = v;
+    }
+  };
+  const bool vec = (row_stride % 8 == 0) && ((reinterpret_cast<uintptr_t>(logits) & 15) == 0);
+  const int nv = vec ? vocab / 8 : 0;
+  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+    const uint4 q = reinterpret_cast<const uint4*>(lr)[c];
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      visit(__uint_as_float(w[j] << 16), c * 8 + 2 * j);
+      visit(__uint_as_float(w[j] & 0xffff0000u), c * 8 + 2 * j + 1);
+    }
+  }
+  for (int v = nv * 8 + threadIdx.x; v < vocab; v += blockDim.x) visit(bf2f(lr[v]), v);
+  // wave argmax (ties -> lowest id), then across the 4 waves through LDS
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  __shared__ float sb[4];
+  __shared__ int si[4];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sb[wave] = best;
+    si[wave] = bi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 4; ++k)
+      if (sb[k] > best || (sb[k] == best && si[k] < bi)) {
+        best = sb[k];
+        bi = si[k];
+      }
+    dst[0] = best;
+    dst[1] = (float)(vocab_start + (bi == 0x7fffffff ? 0 : bi));
+  }
+}
+}  // namespace
+
+extern "C" int omnia_tp_gumbel(float* pack, int64_t ld, int col, const void* logits, int rows,
+                               int64_t row_stride, int vocab, int vocab_start,
+                               const float* temperature, const int* top_k, const float* top_p,
+                               const int64_t* seeds, const int64_t* steps, hipStream_t s) {
+  if (rows == 0) return 0;
+  tp_gumbel_kernel<<<rows, 256, 0, s>>>(pack, ld, col, (const uint16_t*)logits, row_stride,
+                                        vocab, vocab_start, temperature, top_k, top_p, seeds,
+                                        steps);
+  return (int)hipGetLastError();
+}

@@ -19,15 +19,53 @@ TP device transport (``ParallelState.transport``):
     cannot place two ranks on one device, so the process group is gloo (host
     control only) and EVERY device collective runs on the IPC kernels
     (slot-chunked all-reduce, IPC all-gather).
+
+Transport selection: ``OMNIA_TP_TRANSPORT`` wins; else ``ipc`` when the
+launcher's ``LOCAL_WORLD_SIZE`` exceeds the visible device count, else ``rccl``
+(also when ``LOCAL_WORLD_SIZE`` is absent: a plain multi-node launch is one
+rank per GPU).  The choice is then CHECKED by device identity: every rank
+publishes ``(host, device uuid)`` over a gloo side group, and ``rccl`` with two
+ranks on one device raises with the fix instead of failing inside RCCL's
+communicator init.  The chosen transport is logged once per rank.
 """
 from __future__ import annotations
 
 import datetime
+import logging
 import os
+import socket
 from dataclasses import dataclass
 
 import torch
 import torch.distributed as dist
+
+
+log = logging.getLogger("omnia.parallel")
+
+
+def _device_identity() -> str:
+    props = torch.cuda.get_device_properties(torch.cuda.current_device())
+    uid = getattr(props, "uuid", None)
+    if uid is not None:
+        return str(uid)
+    bus = getattr(props, "pci_bus_id", None)
+    return f"pci:{getattr(props, 'pci_domain_id', 0)}:{bus}" if bus is not None else \
+        f"idx:{os.environ.get('HIP_VISIBLE_DEVICES', '')}:{torch.cuda.current_device()}"
+
+
+def check_transport(transport: str, idents: list) -> None:
+    """Raise if ``transport`` cannot run on the ranks' devices: ``rccl`` needs
+    one rank per device.  ``idents`` = every rank's ``(host, device id)``."""
+    if transport != "rccl":
+        return
+    seen: dict = {}
+    for r, key in enumerate(idents):
+        if tuple(key) in seen:
+            raise RuntimeError(
+                f"ranks {seen[tuple(key)]} and {r} share device {key[1]} on {key[0]}: RCCL "
+                "places one rank per device -- set OMNIA_TP_TRANSPORT=ipc (or launch with "
+                "LOCAL_WORLD_SIZE set) to run shared-device ranks on the IPC collectives")
+        seen[tuple(key)] = r
 
 
 @dataclass
@@ -83,7 +121,8 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, device: str |
     ndev = torch.cuda.device_count() if use_gpu else 0
     transport = "gloo"
     if use_gpu:
-        shared = ndev < int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
+        lws = os.environ.get("LOCAL_WORLD_SIZE")
+        shared = lws is not None and ndev < int(lws)
         transport = os.environ.get("OMNIA_TP_TRANSPORT") or ("ipc" if shared else "rccl")
     if backend is None:
         backend = "nccl" if use_gpu and transport == "rccl" else "gloo"
@@ -102,6 +141,17 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, device: str |
                 kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
             dist.init_process_group(backend=backend, rank=rank, world_size=ws,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        if use_gpu:
+            # device identity check over a host-only side group (no RCCL comm yet)
+            side = dist.new_group(backend="gloo") if backend != "gloo" else None
+            idents = [None] * ws
+            dist.all_gather_object(idents, (socket.gethostname(), _device_identity()),
+                                   group=side)
+            check_transport(transport, idents)
+            if side is not None:
+                dist.destroy_process_group(side)
+            log.info("rank %d: transport %s (backend %s, %d rank(s) per device)", rank,
+                     transport, backend, sum(1 for x in idents if x == idents[rank]))
         for k in range(ws // tp_size):
             ranks = list(range(k * tp_size, (k + 1) * tp_size))
             g = dist.new_group(ranks) if tp_size > 1 else None

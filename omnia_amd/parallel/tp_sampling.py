@@ -14,7 +14,10 @@ floats, 0.5 MB at K = 64, tp = 8):
   vocabulary.  The noise of (row, GLOBAL vocab index v) is a counter-based hash
   of (request seed, step, v): draws are independent across ranks (each hashes
   its own vocab range) without any per-rank RNG state, and a seeded request is
-  reproducible whatever the TP degree;
+  reproducible whatever the TP degree.  On the GPU the hash, the log-log and
+  the arg-max are one kernel pass over the bf16 slice (``sampling.hip``
+  ``tp_gumbel``) that skips greedy / filtered rows; ``gumbel_uniform`` is its
+  bit-exact host reference;
 * top-k / top-p rows: the fused sampler runs over the union of the ranks'
   local top-K logits (K = 64): exact for top_k <= K; top-p is taken inside that
   candidate set (exact whenever the nucleus has <= K tokens per rank).
@@ -68,20 +71,33 @@ def tp_sample(local_logits: torch.Tensor, vocab_start: int, temperature: torch.T
     B, Vl = local_logits.shape
     W = dist.get_world_size(group)
     K = min(K, Vl)
-    lf = local_logits.float()
-    cv, ci = torch.topk(lf, K, dim=1)
-    t = temperature.float().clamp(min=1e-6)[:, None]
-    if seeds is not None:
-        st = steps if steps is not None else torch.zeros(B, dtype=torch.int64, device=lf.device)
-        u = gumbel_uniform(seeds.to(lf.device), st.to(lf.device), vocab_start, Vl)
-    else:  # no per-request seeds: the caller's generator (must differ per rank)
-        u = torch.rand(B, Vl, device=lf.device, generator=generator)
-    u = u.clamp_(1e-10, 1.0 - 1e-7)
-    gv, gi = (lf / t - torch.log(-torch.log(u))).max(dim=1)
     pad = (-(2 * K + 2)) % 4  # 16-byte rows for the IPC all-gather
-    pack = torch.cat([cv, (ci + vocab_start).float(), gv[:, None],
-                      (gi + vocab_start).float()[:, None]]
-                     + ([lf.new_zeros(B, pad)] if pad else []), dim=1).contiguous()
+    pack = torch.zeros(B, 2 * K + 2 + pad, dtype=torch.float32, device=local_logits.device)
+    cv, ci = torch.topk(local_logits, K, dim=1)
+    pack[:, :K] = cv
+    pack[:, K:2 * K] = ci + vocab_start
+    if (local_logits.is_cuda and local_logits.dtype == torch.bfloat16 and seeds is not None
+            and local_logits.stride(1) == 1):
+        # one fused pass: hash noise + Gumbel argmax straight into the pack; rows
+        # that are greedy / top-k / top-p never read their logits
+        ops.kernels().tp_gumbel(pack, 2 * K, local_logits, vocab_start, temperature.float(),
+                                top_k.int() if top_k is not None else None,
+                                top_p.float() if top_p is not None else None,
+                                seeds.to(torch.int64),
+                                steps.to(torch.int64) if steps is not None else None)
+    else:
+        lf = local_logits.float()
+        t = temperature.float().clamp(min=1e-6)[:, None]
+        if seeds is not None:
+            st = steps if steps is not None else torch.zeros(B, dtype=torch.int64,
+                                                             device=lf.device)
+            u = gumbel_uniform(seeds.to(lf.device), st.to(lf.device), vocab_start, Vl)
+        else:  # no per-request seeds: the caller's generator (must differ per rank)
+            u = torch.rand(B, Vl, device=lf.device, generator=generator)
+        u = u.clamp_(1e-10, 1.0 - 1e-7)
+        gv, gi = (lf / t - torch.log(-torch.log(u))).max(dim=1)
+        pack[:, 2 * K] = gv
+        pack[:, 2 * K + 1] = gi + vocab_start
     from . import state as pstate
 
     st = pstate.get_state()

@@ -154,3 +154,32 @@ def test_shm_ring_flow_control(tmp_path):
         w.put([3], timeout_s=0.05)
     r.close()
     w.close(unlink=True)
+
+
+def test_shm_ring_detects_dead_peers(tmp_path):
+    """A reader blocked on a ring whose writer died raises within about a second
+    (instead of spinning forever); so does a writer blocked on a dead reader."""
+    import subprocess
+    import sys
+
+    import numpy as np
+
+    from omnia_amd.engine.tp import ShmRing
+
+    path = str(tmp_path / "ring")
+    w = ShmRing(path, True, nslots=1, payload=8, readers=1)
+    dead = subprocess.Popen([sys.executable, "-c", "pass"])
+    dead.wait()
+    w.ctrl[ShmRing.WRITER_PID] = dead.pid  # the writer "died"
+    r = ShmRing(path, False, reader=0)
+    with pytest.raises(RuntimeError, match="died"):
+        r.get(0)
+    with pytest.raises(TimeoutError):  # deadline, writer alive
+        w.ctrl[ShmRing.WRITER_PID] = 0
+        r.get(0, timeout_s=1.5)
+    w.put([1], np.zeros(1, dtype=np.uint8))
+    w.ctrl[ShmRing.READER_PIDS] = dead.pid  # the reader "died" holding the only slot
+    with pytest.raises(RuntimeError, match="reader 0"):
+        w.put([2])
+    r.close()
+    w.close(unlink=True)

@@ -23,6 +23,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import reference as ref
+from ..parallel import overlap
 from ..parallel import state as pstate
 from .config import ModelConfig
 
@@ -61,6 +62,17 @@ class Parts:
 
     def __init__(self, t: torch.Tensor):
         self.t = t
+
+
+class RowPar:
+    """A deferred TP row-parallel projection ``x @ w.T`` (prefill): ``add_norm``
+    runs it chunked along M with each chunk's all-reduce + residual + RMSNorm
+    overlapped on a side stream (``parallel/overlap.py``)."""
+
+    __slots__ = ("x", "w")
+
+    def __init__(self, x: torch.Tensor, w: torch.Tensor):
+        self.x, self.w = x, w
 
 
 @dataclass
@@ -214,6 +226,8 @@ class LlamaModel:
     def _proj(self, tag, x: torch.Tensor, w: torch.Tensor, is_decode: bool):
         """Plain projection: Parts on the weight-streaming path, else bf16."""
         M, K = x.shape
+        if tag in ("o", "down") and not is_decode and overlap.applies(M, x.device):
+            return RowPar(x, w)
         cfg = self._wcfg(M, w.shape[0], K, 0, is_decode)
         if cfg is None:
             return ops.linear(x, w)
@@ -223,6 +237,8 @@ class LlamaModel:
     def add_norm(self, x, residual: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         """residual += x (TP-reduced); returns RMSNorm(residual) * w."""
         eps = self.cfg.rms_eps
+        if isinstance(x, RowPar):
+            return overlap.rowparallel_add_norm(x.x, x.w, residual, w, eps)
         if isinstance(x, Parts):
             if self.tp == 1:
                 return ops.splitk_add_rmsnorm(x.t, residual, w, eps)

@@ -91,7 +91,10 @@ def _sharded_weights(mc, rank, world, keep_full: bool):
 def _worker(rank, world, port, q, pipeline=False, batch=8):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
-                      OMNIA_LOGIT_TAP="1")
+                      OMNIA_LOGIT_TAP="1",
+                      # batch-64 prefill steps (~900 tokens) run the row-parallel
+                      # GEMM / all-reduce overlap (parallel/overlap.py) in-engine
+                      OMNIA_TP_OVERLAP_ROWS="256", OMNIA_TP_OVERLAP_MIN_ROWS="512")
     try:
         from omnia_amd.engine import tp
         from omnia_amd.engine.engine import EngineConfig

@@ -71,6 +71,9 @@ def parse(argv=None):
                     help="runtime path: engine as a thread of the serving process")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     ap.add_argument("--pod-timeout", type=float, default=900.0)
+    ap.add_argument("--engine", choices=["gpu", "synthetic"], default="gpu",
+                    help="synthetic: ws-path host capacity rehearsal -- the engine-core is a "
+                         "token source paced like the measured GPU engine (engine/synthetic.py)")
     return ap.parse_args(argv)
 
 
@@ -148,7 +151,9 @@ class WSDriver:
             "OMNIA_ENGINE_MAX_MODEL_LEN": max(2048, a.prompt_len + a.gen_len + 64),
             "OMNIA_ENGINE_MAX_PREFILL_TOKENS": a.max_prefill_tokens,
             "OMNIA_ENGINE_USE_GRAPHS": "false" if a.no_graphs else "true",
-            "OMNIA_ENGINE_SEED": rank, "OMNIA_ENGINE_PROC": "1" if use_gpu and a.tp == 1 else "0",
+            "OMNIA_ENGINE_SEED": rank,
+            "OMNIA_ENGINE_PROC": "1" if (use_gpu and a.tp == 1) or a.engine == "synthetic" else "0",
+            "OMNIA_ENGINE_SYNTHETIC": "1" if a.engine == "synthetic" else "0",
             "OMNIA_ENGINE_TP": a.tp, "OMNIA_ENGINE_MIXED_BUDGET": a.mixed_budget,
         }
         fenv = {"OMNIA_AGENT_NAME": f"bench-{rank}", "OMNIA_MAX_CONNECTIONS": 4 * C + 64,
@@ -397,7 +402,9 @@ def main():
     if a.tp > 1 and a.path != "ws":
         raise SystemExit("--tp > 1 is served by the ws path (one TP pod per replica)")
     # device_count() does not initialise the GPU: engine children start before any HIP call
-    use_gpu = a.device == "cuda" and torch.cuda.device_count() > 0
+    use_gpu = a.device == "cuda" and a.engine == "gpu" and torch.cuda.device_count() > 0
+    if a.engine == "synthetic" and a.path != "ws":
+        raise SystemExit("--engine synthetic rehearses the ws host path")
     host_only = a.path == "ws" or (a.path == "runtime" and not a.inproc)
     if ws > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -493,8 +500,10 @@ def run(a, drv, ws, rank, use_gpu, host_only):
 
     # frames track tokens only with a full vocabulary: a tiny test vocab is
     # mostly raw bytes, whose UTF-8 fragments the detokenizer holds back
+    # (the host-path rehearsal REPORTS merged frames -- a lagging serving loop
+    # drains several steps' tokens at once -- instead of failing on them)
     frames = check_streamed(results, a.gen_len, a.path == "ws",
-                            strict=_resolve(a.model).vocab_size >= 32000)
+                            strict=_resolve(a.model).vocab_size >= 32000 and a.engine == "gpu")
     out_tokens = sum(r[2] for r in results)
     ttfts = [r[0] for r in results if r[0] is not None]
     lats = [r[1] for r in results if r[1] is not None]
@@ -539,7 +548,10 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (random text prompts of exactly prompt_len tokens after the "
-                    "chat template, random-init weights of the named architecture, ignore_eos)",
+                    "chat template, random-init weights of the named architecture, ignore_eos)"
+                    if a.engine == "gpu" else
+                    "HOST-PATH REHEARSAL: synthetic engine-core paced like the measured GPU "
+                    "engine (engine/synthetic.py), no GPU compute",
             "world_size": ws,
             "per_rank_tokens_per_s": per_rank,
             "p50_turn_latency_ms": ms(statistics.median(lats)) if lats else None,
@@ -550,6 +562,8 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             "p95_tpot_ms": ms(pct(tpot, 0.95)),
             "p95_frame_gap_ms": ms(pct(gaps, 0.95)),
             "streamed_frames_rank0": frames if a.path == "ws" else None,
+            "frames_per_token_rank0": round(frames / max(1, sum(r[2] for r in results)), 4)
+            if a.path == "ws" else None,
             "turns": len(lats),
             "wave_ms": wave_ms,
             "config": {
@@ -566,6 +580,7 @@ def run(a, drv, ws, rank, use_gpu, host_only):
                 "mixed_budget": a.mixed_budget,
                 "tp": a.tp,
                 "hip_graphs": not a.no_graphs,
+                "engine": a.engine,
             },
         }
         if st is not None:

@@ -92,7 +92,12 @@ class _Core:
             import torch
 
             torch.cuda.set_device(int(dev))
-        self.eng = LLMEngine(EngineConfig(**cfg_dict))
+        if os.environ.get("OMNIA_ENGINE_SYNTHETIC", "0") == "1":
+            from .synthetic import SyntheticEngine  # host-path capacity rehearsal
+
+            self.eng = SyntheticEngine(EngineConfig(**cfg_dict))
+        else:
+            self.eng = LLMEngine(EngineConfig(**cfg_dict))
         self.reqs: dict = {}  # rid -> Sequence
         self.tok_out: dict = {}  # rid -> [parts, last_tok, n]
         self.fin_out: list = []

@@ -28,6 +28,12 @@ class Writer:
     async def write(self, msg: dict) -> None:  # pragma: no cover - interface
         raise NotImplementedError
 
+    async def write_chunk(self, session_id: str, session_json: str, content: str,
+                          role: str = "") -> None:
+        """A streamed ``chunk`` frame; writers that can send text override this
+        with the pre-serialized fast path (``protocol.chunk_text``)."""
+        await self.write(P.chunk(session_id, content, role))
+
 
 class PendingTools:
     """Client-tool waits of the active turn, fed by the connection read loop."""
@@ -97,16 +103,39 @@ class RuntimeHandler:
         stream = await self.client.open(metadata)
         out = {"content": "", "usage": None, "error": None, "ttft": None}
         t0 = time.perf_counter()
+        sj = json.dumps(session_id) if session_id else ""
+        # stream inactivity: one re-arming timer per turn instead of a wait_for
+        # (a task + a timer) around every streamed frame
+        loop = asyncio.get_running_loop()
+        task = asyncio.current_task()
+        wd = {"last": loop.time(), "fired": False, "h": None, "recv": False}
+
+        def watchdog():
+            if not wd["recv"]:  # only a wait on the runtime counts as inactivity
+                wd["last"] = loop.time()
+            idle = loop.time() - wd["last"]
+            if idle >= self.inactivity_s:
+                wd["fired"] = True
+                task.cancel()
+            else:
+                wd["h"] = loop.call_later(self.inactivity_s - idle, watchdog)
+
+        wd["h"] = loop.call_later(self.inactivity_s, watchdog)
         try:
             await stream.send(cm)
             while True:
+                wd["recv"] = True
+                wd["last"] = loop.time()  # idle = time in THIS wait on the runtime
                 try:
-                    resp = await asyncio.wait_for(stream.recv(), self.inactivity_s)
-                except asyncio.TimeoutError:
+                    resp = await stream.recv()
+                except asyncio.CancelledError:
+                    if not wd["fired"]:
+                        raise
                     out["error"] = "stream inactivity timeout"
                     await writer.write(P.error(session_id, P.E_INTERNAL,
                                                "agent did not respond in time"))
                     return out
+                wd["recv"] = False
                 if resp is None:
                     out["error"] = "runtime stream closed"
                     await writer.write(P.error(session_id, P.E_AGENT_UNAVAILABLE,
@@ -116,7 +145,8 @@ class RuntimeHandler:
                 if kind == "chunk":
                     if out["ttft"] is None:
                         out["ttft"] = time.perf_counter() - t0
-                    await writer.write(P.chunk(session_id, resp.chunk.content, resp.chunk.role))
+                    c = resp.chunk
+                    await writer.write_chunk(session_id, sj, c.content, c.role)
                 elif kind == "done":
                     d = resp.done
                     usage = {"input_tokens": d.usage.input_tokens,
@@ -149,6 +179,8 @@ class RuntimeHandler:
                     await writer.write(P.server_msg(P.INTERRUPT, session_id))
                 # runtime_hello: consumed
         finally:
+            if wd["h"] is not None:
+                wd["h"].cancel()
             await stream.close()
 
     async def _client_tool(self, session_id, tc, writer, pending: PendingTools, stream):

@@ -15,6 +15,8 @@ payload.  Flags: compressed 0x01, chunked 0x02, last 0x04.  Payloads above
 from __future__ import annotations
 
 import datetime as _dt
+import json as _json
+import time as _time
 import json
 import struct
 
@@ -54,8 +56,34 @@ E_RATE_LIMITED = "RATE_LIMITED"
 E_UNSATISFIABLE_FORMAT = "UNSATISFIABLE_FORMAT"
 
 
+_TS = [-1, ""]  # (whole second, "YYYY-MM-DDTHH:MM:SS") of the last stamp
+
+
 def now_rfc3339() -> str:
-    return _dt.datetime.now(_dt.timezone.utc).isoformat().replace("+00:00", "Z")
+    """UTC RFC 3339 with microseconds (``datetime.isoformat`` + ``Z``); the
+    date/time prefix is formatted once per second -- it is stamped on every
+    streamed frame."""
+    t = _time.time()
+    sec = int(t)
+    if sec != _TS[0]:
+        _TS[0] = sec
+        _TS[1] = _dt.datetime.fromtimestamp(sec, _dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%S")
+    us = int((t - sec) * 1e6)
+    return f"{_TS[1]}.{us:06d}Z" if us else _TS[1] + "Z"
+
+
+_enc = _json.encoder.encode_basestring_ascii  # what json.dumps uses for str
+
+
+def chunk_text(session_json: str, content: str, role: str = "") -> str:
+    """The serialized ``chunk`` frame -- byte-identical to
+    ``json.dumps(chunk(...), separators=(",", ":"))`` -- without building the
+    dict (the hot path: one frame per streamed token).  ``session_json`` is the
+    JSON-encoded session id (``""`` when there is none)."""
+    head = '{"type":"chunk"' + (',"session_id":' + session_json if session_json else "")
+    body = (',"content":' + _enc(content) if content else "") + \
+        (',"role":' + _enc(role) if role else "")
+    return head + body + ',"timestamp":"' + now_rfc3339() + '"}'
 
 
 def server_msg(mtype: str, session_id: str = "", **fields) -> dict:

@@ -78,12 +78,21 @@ class _WSWriter(Writer):
         self.ws = ws
         self.labels = labels
         self.lock = asyncio.Lock()
+        self.sent = M.child(M.MESSAGES_SENT, *labels)
 
     async def write(self, msg: dict) -> None:
         async with self.lock:
             if not self.ws.closed:
                 await self.ws.send_str(json.dumps(msg, separators=(",", ":")))
-                M.child(M.MESSAGES_SENT, *self.labels).inc()
+                self.sent.inc()
+
+    async def write_chunk(self, session_id: str, session_json: str, content: str,
+                          role: str = "") -> None:
+        # hot path (one frame per streamed token): pre-serialized, no dict
+        async with self.lock:
+            if not self.ws.closed:
+                await self.ws.send_str(P.chunk_text(session_json, content, role))
+                self.sent.inc()
 
     async def write_bytes(self, data: bytes) -> None:
         async with self.lock:

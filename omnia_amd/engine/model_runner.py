@@ -154,8 +154,10 @@ class ModelRunner:
     def enable_logit_tap(self):
         """Record ``(seq_ids, fp32 logits rows)`` for every step, for whole-model
         correctness checks against ``ops.reference.dense_forward``.  The decode
-        graphs capture one extra copy into a tap buffer, so they are re-captured.
-        Needs the synchronous (non-pipelined) engine loop."""
+        graphs capture one extra copy into a tap buffer, so they are re-captured;
+        each pipelined launch snapshots it behind its graph.  Under pipelined
+        decode a sequence may run one speculative step past its finish (its token
+        is dropped): its trailing extra row is recorded too."""
         self.logit_tap = []
         self._tap = torch.zeros(self.max_batch, self.vocab, dtype=torch.float32,
                                 device=self.device)
@@ -763,7 +765,12 @@ class ModelRunner:
             ev = torch.cuda.Event()
             ev.record()
         st.event = ev
-        return DecodeHandle(seqs, out_host, ev, n)
+        h = DecodeHandle(seqs, out_host, ev, n)
+        if self._tap is not None:
+            # snapshot on the same stream right behind this step's graph: the next
+            # (pipelined) step overwrites the tap buffer before this one is collected
+            h.tap = self._tap[:n].clone()
+        return h
 
     def _before_replay(self, nrows: int, ncols: int, st: "_Staging | None" = None):
         """Hook: TP runners publish the step inputs (``st.host``) to their workers."""
@@ -778,7 +785,7 @@ class ModelRunner:
         if gil_ns:
             self.stats["gil_wait_s"] += gil_ns * 1e-9
         if self._tap is not None and h.kind == "decode":
-            self._tap_rows(h.seqs, self._tap[: h.n])
+            self._tap_rows(h.seqs, h.tap if h.tap is not None else self._tap[: h.n])
         return h.out_host[: h.n].tolist()
 
     def run_decode(self, seqs: list[Sequence]) -> list[int]:
@@ -808,9 +815,10 @@ _PAD = object()  # row_seq marker of a padded (null) row
 
 
 class DecodeHandle:
-    __slots__ = ("seqs", "out_host", "event", "n", "kind")
+    __slots__ = ("seqs", "out_host", "event", "n", "kind", "tap")
 
     def __init__(self, seqs, out_host, event, n, kind="decode"):
+        self.tap = None
         self.kind = kind
         self.seqs = seqs
         self.out_host = out_host

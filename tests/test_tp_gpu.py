@@ -36,7 +36,10 @@ def _check(mc, w, seqs, rows_by_seq, rel_tol):
     worst = 0.0
     for sid, prompt, output in seqs:
         got = rows_by_seq[sid]
-        assert len(got) == len(output), (len(got), len(output))
+        # pipelined decode may run one speculative step past the finish (dropped
+        # token, recorded row): trailing, at most one
+        assert len(output) <= len(got) <= len(output) + 1, (sid, len(got), len(output))
+        got = got[:len(output)]
         full = prompt + output
         want = ref.dense_forward(mc, w, full[:-1])[len(prompt) - 1:]
         for g, r in zip(got, want):

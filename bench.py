@@ -366,12 +366,13 @@ def check_streamed(results, gen_len: int, has_frames: bool, strict: bool = True)
     """The headline counts ``done.usage.output_tokens``; cross-check it against
     what the client actually received.  Every turn must report exactly
     ``gen_len`` tokens (ignore_eos), and on the WS path the streamed chunk frames
-    it timed must account for them: at most one frame per token (plus a role
-    frame), and at most 2 % + 2 tokens merged into a neighbour's frame (UTF-8
-    fragments held back by the detokenizer, empty special tokens).  Returns the
-    total frame count; exits on a mismatch so a drifting count never reaches the
-    JSON line.  ``strict`` False (a tiny test vocabulary, mostly raw bytes whose
-    UTF-8 fragments the detokenizer holds back) counts the frames only."""
+    it timed must account for them: never more than one frame per token (plus a
+    role frame), and at least half as many frames as tokens (a token may share
+    a frame when the detokenizer holds an incomplete UTF-8 sequence -- random-
+    init weights emit raw byte tokens -- or when a lagging serving loop drains
+    several steps at once).  Returns the total frame count; exits on a violation
+    so a drifting count never reaches the JSON line (the exact frames/token ratio
+    is reported in it).  ``strict`` False (a tiny test vocabulary) counts only."""
     total = 0
     for r in results:
         n = r[2]
@@ -380,7 +381,7 @@ def check_streamed(results, gen_len: int, has_frames: bool, strict: bool = True)
         if has_frames:
             f = len(r[4])
             total += f
-            if strict and (f > n + 1 or f < n - max(2, n // 50)):
+            if strict and (f > n + 1 or f < n // 2):
                 raise SystemExit(f"turn streamed {f} frames for {n} reported output tokens")
     return total
 

@@ -18,8 +18,11 @@ sequence of forwards with the same all-to-all shapes, whatever its own load:
    bucket (idle ranks with all rows padded), so graph captures -- which run the
    collectives too -- happen on all ranks together.
 
-The runner is used with synchronous engine steps (no one-deep pipelining: a
-step's collective shape depends on every rank's schedule).
+Graph decode steps are pipelined one deep (``run_ep_step``): the agreement
+describes the NEXT step from the scheduler's view (in-flight tokens counted as
+placeholders), so a rank enqueues step N+1 before collecting step N; a sequence
+that finished at step N may ride one speculative step (its token is dropped).
+Eager steps drain the in-flight step first.
 """
 from __future__ import annotations
 
@@ -42,7 +45,8 @@ class EPModelRunner(ModelRunner):
         st = pstate.get_state()
         self.group = st.dp_group
         self.ep = st.dp_size
-        self.ep_stats = {"steps": 0, "eager_steps": 0, "graph_steps": 0, "idle_fill": 0}
+        self.ep_stats = {"steps": 0, "eager_steps": 0, "graph_steps": 0, "idle_fill": 0,
+                         "pipelined_steps": 0}
         # per-step agreement over host shared memory: no collective launch, no
         # device -> host copy on the control path (parallel/hostsync.py)
         self.agreement = ShmAgreement.for_group(self.group, 5) if self.ep > 1 else None
@@ -98,8 +102,17 @@ class EPModelRunner(ModelRunner):
 
 
 def run_ep_step(engine) -> int:
-    """One lockstep engine step (see module docstring).  Returns tokens produced."""
+    """One lockstep engine step (see module docstring).  Returns tokens produced.
+
+    Steady-state decode is pipelined one deep like the single-rank engine: when
+    the group agrees on a graph step, a rank with sequences enqueues its replay
+    of the agreed bucket (input tokens of the previous, still in-flight step
+    gathered on the device from the token slots), THEN collects the previous
+    step's tokens -- the host never waits for the GPU between two decode steps.
+    Eager steps (someone prefills, penalties, grammars) first drain the
+    in-flight step and run synchronously."""
     from . import engine as E
+    from .model_runner import PLACEHOLDER
 
     runner: EPModelRunner = engine.runner
     model = runner.model
@@ -107,8 +120,29 @@ def run_ep_step(engine) -> int:
     active, tokens, eager, rows, cols = runner.agree(*runner.describe(plan))
     engine._ep_active = active
     if not active:
-        return 0
+        return engine._flush_inflight()
     runner.ep_stats["steps"] += 1
+    pipelined = engine.cfg.pipeline and runner.use_graphs and runner.device_handoff
+    if not eager and pipelined and plan.kind == "decode" and plan.decode:
+        runner.ep_stats["graph_steps"] += 1
+        runner.ep_stats["pipelined_steps"] = runner.ep_stats.get("pipelined_steps", 0) + 1
+        h = runner.launch_decode(plan.decode, rows, cols)
+        for sq in plan.decode:
+            sq.num_cached = sq.length  # the fed token's KV is written by this step
+            sq.output.append(PLACEHOLDER)
+        n = engine._flush_inflight()
+        engine.inflight = h
+        engine.counters["decode_tokens"] += len(plan.decode)
+        engine.counters["steps_decode"] += 1
+        engine.step_count += 1
+        return n
+    n0 = engine._flush_inflight()  # eager / idle-rank steps run on settled state
+    if plan.decode:
+        plan.decode = [sq for sq in plan.decode if not sq.is_finished]
+        if plan.kind == "decode" and not plan.decode:
+            plan.kind = "idle"
+        elif plan.kind == "mixed" and not plan.decode:
+            plan.kind = "prefill"
     done = []
     if eager:
         runner.ep_stats["eager_steps"] += 1
@@ -149,4 +183,4 @@ def run_ep_step(engine) -> int:
         engine._append(s, tok, now)
     engine.step_count += 1
     E.M.KV_UTIL.set(engine.blocks.utilization())
-    return len(done)
+    return n0 + len(done)

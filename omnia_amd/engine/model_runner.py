@@ -723,14 +723,17 @@ class ModelRunner:
         return self.use_graphs and not any(s.params.needs_penalties or s.guide is not None
                                            for s in seqs)
 
-    def launch_decode(self, seqs: list[Sequence]) -> "DecodeHandle":
-        """Enqueue one decode step (graph replay) without waiting for it."""
+    def launch_decode(self, seqs: list[Sequence], nrows: int | None = None,
+                      ncols: int | None = None) -> "DecodeHandle":
+        """Enqueue one decode step (graph replay) without waiting for it.
+        ``nrows`` / ``ncols`` force a larger graph bucket (lockstep EP ranks
+        replay the bucket the group agreed on)."""
         n = len(seqs)
         if n > self.max_batch:
             raise ValueError("decode batch exceeds max_batch")
         max_len = max(s.length for s in seqs)
-        ncols = self._ctx_bucket(max_len)
-        nrows = self.buckets[bisect.bisect_left(self.buckets, n)]
+        ncols = max(ncols or 0, self._ctx_bucket(max_len))
+        nrows = max(nrows or 0, self.buckets[bisect.bisect_left(self.buckets, n)])
         st = self.stage[self.flip]
         out_host = self.out_hosts[self.flip]
         self.flip ^= 1

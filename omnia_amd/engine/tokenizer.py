@@ -122,34 +122,36 @@ def _token_bytes_cached(tok, tid: int) -> bytes:
 
 
 class Detokenizer:
-    """Incremental UTF-8-safe streaming detokeniser for one sequence."""
+    """Incremental UTF-8-safe streaming detokeniser for one sequence.
+
+    Incomplete multi-byte sequences are held until they complete; bytes that
+    can never become valid UTF-8 are emitted as U+FFFD at once (Python's
+    incremental decoder, ``errors="replace"``), so a run of invalid byte tokens
+    -- e.g. a random-init model repeating a lone lead byte -- still streams one
+    character per token instead of stalling the stream until the end."""
 
     def __init__(self, tok):
+        import codecs
+
         self.tok = tok
-        self.pending = bytearray()
+        self.dec = codecs.getincrementaldecoder("utf-8")(errors="replace")
+        self.held = False  # the decoder holds an incomplete sequence
 
     def push(self, tid: int) -> str:
         b = _token_bytes_cached(self.tok, tid)
-        if not self.pending:
+        if not self.held:
             # fast path: a token that is complete UTF-8 on its own (the common case)
             try:
                 return b.decode("utf-8")
             except UnicodeDecodeError:
                 pass
-        self.pending.extend(b)
-        # emit the longest valid UTF-8 prefix
-        for cut in range(len(self.pending), max(-1, len(self.pending) - 4), -1):
-            try:
-                s = bytes(self.pending[:cut]).decode("utf-8")
-            except UnicodeDecodeError:
-                continue
-            del self.pending[:cut]
-            return s
-        return ""
+        s = self.dec.decode(b)
+        self.held = bool(self.dec.getstate()[0])
+        return s
 
     def flush(self) -> str:
-        s = bytes(self.pending).decode("utf-8", errors="replace")
-        self.pending.clear()
+        s = self.dec.decode(b"", final=True)
+        self.held = False
         return s
 
 

@@ -90,7 +90,7 @@ def test_streamed_frames_cross_check_usage():
     with pytest.raises(SystemExit, match="output tokens"):
         check_streamed([(0.1, 1.0, 7, 96, [0.0] * 7)], 8, True)  # short turn
     with pytest.raises(SystemExit, match="frames"):
-        check_streamed([(0.1, 1.0, 128, 96, [0.0] * 64)], 128, True)  # inflated usage
+        check_streamed([(0.1, 1.0, 128, 96, [0.0] * 60)], 128, True)  # inflated usage
     with pytest.raises(SystemExit, match="frames"):
         check_streamed([(0.1, 1.0, 8, 96, [0.0] * 12)], 8, True)
     assert check_streamed([(0.1, 1.0, 8, 96, [])], 8, False) == 0

@@ -52,7 +52,10 @@ def _check(mc, w, seqs, rows_by_seq, tol):
     worst = 0.0
     for sid, prompt, output in seqs:
         got = rows_by_seq[sid]
-        assert len(got) == len(output), (len(got), len(output))
+        # pipelined decode may run one speculative step past the finish (dropped
+        # token, recorded row): trailing, at most one
+        assert len(output) <= len(got) <= len(output) + 1, (sid, len(got), len(output))
+        got = got[:len(output)]
         want = ref.dense_forward(mc, w, (prompt + output)[:-1])[len(prompt) - 1:]
         for g, r in zip(got, want):
             err = float((g.float().cpu() - r).abs().max() / r.abs().max())
@@ -242,6 +245,8 @@ def test_ep_a2a_on_one_gpu_matches_dense_oracle(world):
     assert len(steps) == 1, steps
     assert all(r["agree"]["calls"] >= r["stats"]["steps"] for r in res.values())
     assert all(r["stats"]["graph_steps"] > 0 for r in res.values())
+    # steady-state decode ran one step ahead of the host (launch N+1, then collect N)
+    assert any(r["stats"]["pipelined_steps"] > 0 for r in busy), res
     if world >= 4:
         assert res[world - 1]["stats"]["idle_fill"] > 0
 

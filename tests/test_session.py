@@ -131,7 +131,11 @@ def test_session_api_rest_and_event_stream():
     assert len(out["search"]["sessions"]) == 1
     assert out["status"] == "completed" and out["404"] == 404
     assert out["bulk"]["deleted"] == 1
-    assert len(stream) == 2  # message.appended events for the eval worker
+    import json as _json
+
+    types = [_json.loads(dict(zip(f[::2], f[1::2]))[b"event"])["type"] for _, f in stream]
+    # message.appended per message + session.completed on the status transition
+    assert types == ["message.appended", "message.appended", "session.completed"], types
 
 
 def test_ring_buffer_parks_and_flushes():

@@ -8,6 +8,7 @@ results, evaluate ``loadTest.thresholds`` and write ``status``
 from __future__ import annotations
 
 import asyncio
+import os
 import json
 import logging
 import time
@@ -17,6 +18,7 @@ import yaml
 from ...operator.apistore import set_condition
 from .profile import LoadProfile
 from .queue import WorkItem
+from .aggregate import aggregate, to_job_result
 from .stats import JobStats, evaluate
 from .worker import ArenaWorker
 
@@ -220,7 +222,7 @@ class ArenaJobController:
     def __init__(self, store, queue, provider_objects: dict | None = None,
                  worker_mode: str = "inproc", redis_url: str = "", license=None,
                  worker_image: str = "ghcr.io/altairalabs/omnia-arena-worker:latest",
-                 poll_s: float = 2.0):
+                 poll_s: float = 2.0, session_api_url: str = ""):
         """``worker_mode`` "inproc": worker tasks on this event loop (single
         process); "pods": a batch/v1 Job of worker pods sharing the Redis-Streams
         queue at ``redis_url`` (``arenajob_controller_pod.go``)."""
@@ -230,6 +232,7 @@ class ArenaJobController:
         self.tasks: dict[str, asyncio.Task] = {}
         self.worker_mode = worker_mode
         self.redis_url = redis_url
+        self.session_api_url = session_api_url
         self.license = license  # ee/license.License (or a Validator); None = no gates
         self.worker_image = worker_image
         self.poll_s = poll_s
@@ -310,14 +313,26 @@ class ArenaJobController:
                      startTime=time.time())
         t0 = time.perf_counter()
         budget = float(lt["budgetLimit"]) if lt.get("budgetLimit") else None
+        recorder = sess = None
+        if self.session_api_url:
+            from ...session.httpclient import SessionHTTPClient
+            from .recording import ArenaSessionRecorder
+
+            sess = SessionHTTPClient(self.session_api_url)
+            recorder = ArenaSessionRecorder(sess, md["name"], md.get("namespace", "default"),
+                                            spec.get("workspace", ""), job_type)
         workers = [ArenaWorker(self.q, md["name"], scenarios, providers,
                                LoadProfile(max(1, conc // replicas),
                                            float(ramp.get("upSeconds") or 0),
                                            float(ramp.get("downSeconds") or 0)),
                                budget=budget / replicas if budget else None,
-                               job_type=job_type)
+                               job_type=job_type, recorder=recorder)
                    for _ in range(replicas)]
-        await asyncio.gather(*(w.run() for w in workers))
+        try:
+            await asyncio.gather(*(w.run() for w in workers))
+        finally:
+            if sess is not None:
+                await sess.close()
         return await self._finish(job, spec, items, t0)
 
     async def _finish(self, job, spec, items, t0):
@@ -345,8 +360,10 @@ class ArenaJobController:
         budget = check_budget(lt.get("budgetLimit"), lt.get("budgetCurrency") or "USD",
                               stats.total_cost)
         job = self.store.get("ArenaJob", md["name"], md.get("namespace", "default"))
+        agg = aggregate(results)
         self._status(job, phase, progress={"total": len(items), "done": len(results)},
                      results={**stats.to_json(), **budget},
+                     result=to_job_result(agg),
                      thresholds=[str(v) for v in verdicts],
                      completionTime=time.time(), message="thresholds " + (
                          "passed" if ok else "failed") + (
@@ -404,6 +421,9 @@ class ArenaJobController:
                {"name": "ARENA_RAMP_DOWN", "value": str(float(ramp.get("downSeconds") or 0))},
                {"name": "ARENA_TOTAL_ITEMS", "value": str(n_items)},
                {"name": "LOG_LEVEL", "value": "info"}] + secret_env
+        sapi = self.session_api_url or os.environ.get("OMNIA_SESSION_API_URL", "")
+        if sapi:  # played runs recorded into session-api (recording.py)
+            env.append({"name": "SESSION_API_URL", "value": sapi})
         if lt.get("budgetLimit"):
             env.append({"name": "ARENA_BUDGET",
                         "value": str(float(lt["budgetLimit"]) / replicas)})

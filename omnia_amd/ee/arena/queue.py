@@ -43,6 +43,12 @@ class WorkItem:
                    stream_id=stream_id)
 
 
+def _failed(item: WorkItem, error: str) -> dict:
+    """The result of an item that exhausted its attempts."""
+    return {"passed": False, "error": error or "unknown error", "scenario": item.scenario_id,
+            "provider": item.provider_id, "item_id": item.id, "attempt": item.attempt}
+
+
 class MemoryQueue:
     def __init__(self):
         self.items: dict[str, list[WorkItem]] = {}
@@ -74,8 +80,7 @@ class MemoryQueue:
         if item.attempt < item.max_attempts:
             await self.enqueue([item])
         else:
-            self.results.setdefault(item.job_id, {})[item.id] = {"passed": False,
-                                                                 "error": error}
+            self.results.setdefault(item.job_id, {})[item.id] = _failed(item, error)
 
     async def reclaim(self, job_id: str, visibility_s: float) -> int:
         now, n = time.time(), 0
@@ -148,7 +153,7 @@ class StreamQueue:
             await self.r.xadd(self._stream(item.job_id), {"item": item.to_json()})
         else:
             await self.r.execute("HSET", f"omnia:arena:results:{item.job_id}", item.id,
-                                 json.dumps({"passed": False, "error": error}))
+                                 json.dumps(_failed(item, error)))
 
     async def reclaim(self, job_id: str, visibility_s: float) -> int:
         raw = await self.r.execute("HGETALL", f"omnia:arena:inflight:{job_id}") or []

@@ -29,6 +29,7 @@ async def run_fleet(item: WorkItem, scenario: dict, provider: dict) -> dict:
                             provider.get("headers")) as fs:
         for t in scenario.get("turns", []):
             r = await fs.turn(t["user"], t.get("metadata"))
+            r["user"] = t["user"]
             r["assertions"] = [evaluate(a, t["user"], r["content"])
                                for a in t.get("assertions", [])]
             turns.append(r)
@@ -62,7 +63,7 @@ async def run_direct(item: WorkItem, scenario: dict, provider: dict) -> dict:
         lat = time.perf_counter() - t0
         content = "".join(text)
         msgs.append(Message("assistant", content))
-        turns.append({"content": content, "ttft_ms": (ttft or lat) * 1e3,
+        turns.append({"user": t["user"], "content": content, "ttft_ms": (ttft or lat) * 1e3,
                       "latency_ms": lat * 1e3,
                       "usage": {"output_tokens": getattr(usage, "output_tokens", 0),
                                 "cost": getattr(usage, "cost", 0.0)} if usage else {},
@@ -192,7 +193,7 @@ class ArenaWorker:
     def __init__(self, queue, job_id: str, scenarios: dict, providers: dict,
                  profile: LoadProfile, budget: float | None = None,
                  consumer: str | None = None, visibility_s: float = 300.0,
-                 job_type: str = "evaluation"):
+                 job_type: str = "evaluation", recorder=None):
         self.q = queue
         self.job = job_id
         self.scenarios = scenarios
@@ -202,6 +203,7 @@ class ArenaWorker:
         self.consumer = consumer or f"worker-{os.getpid()}-{uuid.uuid4().hex[:6]}"
         self.visibility_s = visibility_s
         self.job_type = job_type
+        self.recorder = recorder  # ArenaSessionRecorder: played runs -> session-api
         self.spent = 0.0
         self.active = 0
         self.done = 0
@@ -218,8 +220,13 @@ class ArenaWorker:
                 fn = run_fleet if prov.get("mode", "fleet") == "fleet" else run_direct
             res = await fn(item, scen, prov)
             res.update(scenario=item.scenario_id, provider=item.provider_id,
-                       attempt=item.attempt)
+                       attempt=item.attempt, item_id=item.id)
             self.spent += res.get("cost") or 0.0
+            if self.recorder is not None and res.get("turns"):
+                try:
+                    res["session_id"] = await self.recorder.record(item, res)
+                except Exception as e:  # noqa: BLE001 -- recording never fails a run
+                    log.warning("recording item %s failed: %s", item.id, e)
             await self.q.complete(item, res)
         except Exception as e:  # noqa: BLE001
             log.info("item %s failed: %s", item.id, e)

@@ -67,13 +67,26 @@ async def amain(env=os.environ) -> int:
     providers = build_providers(cfg.get("providers", []), env)
     q = StreamQueue(RedisClient(env["REDIS_URL"]))
     budget = float(env["ARENA_BUDGET"]) if env.get("ARENA_BUDGET") else None
+    recorder = sess = None
+    if env.get("SESSION_API_URL"):  # played runs recorded as sessions (source:arena)
+        from ...session.httpclient import SessionHTTPClient
+        from .recording import ArenaSessionRecorder
+
+        sess = SessionHTTPClient(env["SESSION_API_URL"])
+        recorder = ArenaSessionRecorder(sess, job, env.get("ARENA_JOB_NAMESPACE", "default"),
+                                        env.get("OMNIA_WORKSPACE_NAME", ""),
+                                        env.get("ARENA_JOB_TYPE") or "evaluation")
     w = ArenaWorker(q, job, scenarios, providers,
                     LoadProfile(max(1, int(env.get("ARENA_VUS_PER_WORKER") or 1)),
                                 float(env.get("ARENA_RAMP_UP") or 0),
                                 float(env.get("ARENA_RAMP_DOWN") or 0)),
                     budget=budget, job_type=env.get("ARENA_JOB_TYPE") or "evaluation",
-                    consumer=env.get("HOSTNAME") or None)
-    await w.run()
+                    consumer=env.get("HOSTNAME") or None, recorder=recorder)
+    try:
+        await w.run()
+    finally:
+        if sess is not None:
+            await sess.close()
     log.info("worker for %s done: %d item(s)", job, w.done)
     return 0
 

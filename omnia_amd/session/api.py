@@ -233,6 +233,20 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
             out.append(e.to_json())
         return web.json_response({"results": out}, status=201)
 
+    async def eval_results_list(request):
+        """GET /api/v1/eval-results?passed=&evalId=&limit=&offset= across sessions."""
+        qs = request.query
+        passed = None
+        if qs.get("passed") not in (None, ""):
+            passed = qs["passed"].lower() in ("1", "true", "yes")
+        try:
+            limit = max(1, min(1000, int(qs.get("limit", 100))))
+            offset = max(0, int(qs.get("offset", 0)))
+        except ValueError:
+            return web.json_response({"error": "invalid limit/offset"}, status=400)
+        rows = svc.warm.list_eval_results(passed, qs.get("evalId") or None, limit, offset)
+        return web.json_response({"results": rows})
+
     async def eval_results_summary(request):
         sid = request.match_info["id"]
         rows = svc.warm.list_rows("eval_results", sid)
@@ -409,6 +423,7 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         r.add_post(f"/api/v1/sessions/{{id}}/{path}", p)
         r.add_get(f"/api/v1/sessions/{{id}}/{path}", g)
     r.add_post("/api/v1/eval-results", eval_results_post)
+    r.add_get("/api/v1/eval-results", eval_results_list)
     r.add_post("/api/v1/sessions/{id}/evaluate", evaluate)
     r.add_get("/api/v1/eval-results/aggregate", eval_aggregate)
     r.add_get("/api/v1/sessions/{id}/eval-results",

@@ -169,6 +169,21 @@ class WarmStore:
         return [json.loads(x[0]) for x in self._x(
             f"SELECT doc FROM {table} WHERE session_id=? ORDER BY created", (sid,))]
 
+    def list_eval_results(self, passed: bool | None = None, eval_id: str | None = None,
+                          limit: int = 100, offset: int = 0) -> list[dict]:
+        """Eval results across sessions, newest first (``ListEvalResults``)."""
+        sql = "SELECT doc FROM eval_results WHERE 1=1"
+        args: list = []
+        if passed is not None:
+            sql += " AND passed=?"
+            args.append(int(bool(passed)))
+        if eval_id:
+            sql += " AND eval_id=?"
+            args.append(eval_id)
+        sql += " ORDER BY created DESC LIMIT ? OFFSET ?"
+        args += [int(limit), int(offset)]
+        return [json.loads(x[0]) for x in self._x(sql, args)]
+
     def list_sessions(self, namespace=None, agent=None, status=None, before=None, after=None,
                       user=None, limit=100, offset=0, q=None) -> list[Session]:
         sql = "SELECT doc FROM sessions WHERE 1=1"

@@ -121,3 +121,53 @@ def test_recorder_gives_up_without_session_api():
     it = WorkItem(job_id="j", scenario_id="s", provider_id="p")
     assert asyncio.run(rec.record(it, {"passed": True, "turns": []})) is None
     assert Down.calls == 3  # retried, then the run is played but not recorded
+
+
+def test_sessions_with_failed_evals_become_scenarios():
+    from omnia_amd.ee.arena.sources import SessionAPISource
+
+    async def go():
+        svc = TieredSessionService()
+        runner = web.AppRunner(build_app(svc))
+        await runner.setup()
+        site = web.TCPSite(runner, "127.0.0.1", 0)
+        await site.start()
+        url = f"http://127.0.0.1:{site._server.sockets[0].getsockname()[1]}"
+        c = SessionHTTPClient(url)
+        ids = {}
+        for sid, ok in (("sess-bad-0001", False), ("sess-good-001", True)):
+            await c.request("POST", "/api/v1/sessions", {"id": sid, "agentName": "support",
+                                                         "namespace": "ns"})
+            for role, text in (("system", "be nice"), ("user", "where is my order"),
+                               ("assistant", "it shipped"), ("user", "thanks"),
+                               ("assistant", "bye")):
+                m = await c.request("POST", f"/api/v1/sessions/{sid}/messages",
+                                    {"role": role, "content": text})
+                ids[(sid, text)] = m["id"]
+            await c.request("POST", "/api/v1/eval-results", [
+                {"sessionId": sid, "messageId": ids[(sid, "it shipped")], "evalId": "polite",
+                 "evalType": "llm_judge", "passed": ok, "details": {"criteria": "tone"}},
+                {"sessionId": sid, "evalId": "resolved", "evalType": "contains",
+                 "passed": ok, "details": {"value": "shipped"}},
+                {"sessionId": sid, "messageId": "not-in-transcript", "evalId": "ghost",
+                 "passed": ok}])
+        src = SessionAPISource(c)
+        listed = await src.list(passed=False, limit=5)
+        scen = await src.scenarios(passed=False, limit=5)
+        all_ = await src.list(passed=None, limit=5)
+        await c.close()
+        await runner.cleanup()
+        return listed, scen, all_
+
+    listed, scen, all_ = asyncio.run(go())
+    assert [x["id"] for x in listed] == ["sess-bad-0001"]  # de-duplicated per session
+    assert {x["id"] for x in all_} == {"sess-bad-0001", "sess-good-001"}
+    [s] = scen
+    assert s["id"] == "session-sess-bad-000" and s["system"] == "be nice"
+    assert [t["user"] for t in s["turns"]] == ["where is my order", "thanks"]
+    assert s["turns"][0]["reference"] == "it shipped"
+    a = s["turns"][0]["assertions"]
+    assert [x["id"] for x in a] == ["polite"] and a[0]["params"] == {"criteria": "tone"}
+    assert [x["id"] for x in s["conversation_assertions"]] == ["resolved"]
+    assert s["metadata"]["failedEvals"] == ["ghost", "polite", "resolved"]
+    assert s["turns"][1]["assertions"] == []  # the ghost result matched no message

@@ -59,6 +59,9 @@ class EngineConfig:
     # >0: mixed steps (running sequences' decode rows + <= this many prefill tokens
     # in one forward) bound inter-token latency under arrivals; 0: separate steps
     mixed_budget: int = 0
+    # >0: mixed steps only while the prefill backlog is <= this many tokens (a
+    # trickle of arrivals); bursts are prefilled first on the fused prefill path
+    mixed_backlog: int = 16384
     checkpoint: str | None = None  # HF safetensors dir (random init when None)
     # MoE expert parallelism: "tp" = experts sharded over the TP group (EP inside
     # TP); "a2a" = data-parallel attention replicas + token all-to-all to the
@@ -83,6 +86,7 @@ class EngineConfig:
             "OMNIA_ENGINE_CHECKPOINT": ("checkpoint", str),
             "OMNIA_ENGINE_USE_GRAPHS": ("use_graphs", lambda v: v.lower() != "false"),
             "OMNIA_ENGINE_MIXED_BUDGET": ("mixed_budget", int),
+            "OMNIA_ENGINE_MIXED_BACKLOG": ("mixed_backlog", int),
             "OMNIA_ENGINE_EP_MODE": ("ep_mode", str),
             "OMNIA_ENGINE_CP_THRESHOLD": ("cp_threshold", int),
         }
@@ -163,6 +167,7 @@ class LLMEngine:
                             # mixed steps run on the TP-rank-0-only eager path: TP keeps
                             # separate prefill / decode steps
                             mixed_budget=cfg.mixed_budget if self.model.tp == 1 else 0,
+                            mixed_backlog=cfg.mixed_backlog,
                             cp_threshold=cfg.cp_threshold if self.cp_lockstep else 0),
             self.blocks)
         self.scheduler.on_capped = self._finish_capped

@@ -7,7 +7,9 @@ step over every running sequence (the hipGraph-captured hot loop), or -- with
 prefill chunks of at most ``mixed_budget`` tokens in ONE forward (the decode
 rows ride in the prefill GEMMs, and running sequences never stall behind a
 whole prefill chunk: the step time, i.e. their inter-token latency, is bounded
-by the budget).  Without running sequences prefill uses the full
+by the budget) -- with ``mixed_backlog`` > 0 taken only while the prefill
+backlog is at most that many tokens (arrivals trickling in); a larger backlog
+is prefilled first.  Without running sequences prefill uses the full
 ``max_prefill_tokens`` (throughput); prefill has priority while the running set
 is below ``max_batch`` so TTFT stays low.  When the KV pool runs dry, idle session caches are
 evicted first (LRU, optionally to host DRAM), then the youngest running
@@ -30,6 +32,7 @@ class SchedulerConfig:
     max_model_len: int = 8192
     prefill_chunk: int = 8192  # max new tokens of ONE sequence per prefill step
     mixed_budget: int = 0  # >0: co-schedule decode rows with <= this many prefill tokens
+    mixed_backlog: int = 0  # >0: ... only while the prefill backlog is <= this many tokens
     # >0: prompts with at least this many uncached tokens are held for a
     # context-parallel prefill over the DP group (engine/cp.py)
     cp_threshold: int = 0
@@ -155,9 +158,20 @@ class Scheduler:
         return False
 
     # ------------------------------------------------------------ planning
+    def backlog_tokens(self) -> int:
+        """Uncached prompt tokens still to prefill (partial + waiting)."""
+        return sum(s.num_uncached for s in self.partial) + sum(
+            s.length - s.num_cached for s in self.waiting)
+
     def schedule(self) -> StepPlan:
         cfg = self.cfg
-        if cfg.mixed_budget > 0 and self.running and (self.partial or self.waiting):
+        # mixed steps only for a TRICKLE of prefill work -- a backlog that fits
+        # one mixed step (open-loop arrivals while others decode): decoders keep
+        # streaming, the new prompt starts at once.  A burst (a closed-loop wave:
+        # hundreds of prompts at once) is prefilled by full prefill-first steps
+        # on the fused prefill path, which is faster in aggregate.
+        if cfg.mixed_budget > 0 and self.running and (self.partial or self.waiting) and (
+                cfg.mixed_backlog <= 0 or self.backlog_tokens() <= cfg.mixed_backlog):
             decode = self._decode_rows()
             # the decode rows count against the budget: a full mixed step is exactly
             # mixed_budget tokens, the GEMM shape the prefill GEMMs were tuned for

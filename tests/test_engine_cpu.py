@@ -157,3 +157,30 @@ def test_mixed_steps_match_separate_steps():
         if budget:
             assert eng.counters.get("steps_mixed", 0) >= 2
     assert outs[0] == outs[48]
+
+
+def test_mixed_steps_only_for_a_trickle_backlog():
+    """``mixed_backlog``: a burst of prompts is prefilled first (full prefill
+    steps); once the backlog fits, decode rows ride along the prefill chunks."""
+    from omnia_amd.engine.kv_manager import BlockManager
+    from omnia_amd.engine.sampling_params import SamplingParams
+    from omnia_amd.engine.scheduler import Scheduler, SchedulerConfig
+    from omnia_amd.engine.sequence import Sequence
+
+    sch = Scheduler(SchedulerConfig(max_batch=16, max_prefill_tokens=64, mixed_budget=64,
+                                    mixed_backlog=100), BlockManager(256, 4))
+    p = SamplingParams(max_tokens=4)
+    first = Sequence(prompt=list(range(1, 9)), params=p)
+    sch.add(first)
+    plan = sch.schedule()
+    assert plan.kind == "prefill"
+    sch.on_prefill_done(plan.prefill, {first.seq_id: 5})
+    for _ in range(5):  # a burst: 5 x 40 = 200 backlog tokens > 100
+        sch.add(Sequence(prompt=list(range(1, 41)), params=p))
+    assert sch.backlog_tokens() == 200
+    assert sch.schedule().kind == "prefill"  # prefill-first while the burst drains
+    while sch.backlog_tokens() > 100:
+        plan = sch.schedule()
+        assert plan.kind == "prefill"
+        sch.on_prefill_done(plan.prefill, {s.seq_id: 5 for s, _ in plan.prefill})
+    assert sch.schedule().kind == "mixed"  # a trickle: decoders keep streaming

@@ -155,6 +155,45 @@ def _ep_worker(rank, world, port, q):
         q.put(("err", rank, traceback.format_exc()))
 
 
+def _ep_worker_mixtral(rank, world, port, q):
+    """Mixtral-8x7B layer shapes (d 4096, 8 experts x 14336, 32 q / 8 kv heads,
+    vocab 32000), 2 layers: rows go back to the parent, which builds the full
+    model once for the oracle."""
+    _env(rank, world, port)
+    try:
+        from omnia_amd.engine.engine import EngineConfig, LLMEngine
+        from omnia_amd.engine.sampling_params import SamplingParams
+        from omnia_amd.models.config import resolve
+
+        torch.cuda.set_device(0)
+        mc = resolve("mixtral-8x7b").replace(num_layers=2)
+        eng = LLMEngine(EngineConfig(model="mixtral-8x7b", device="cuda", ep_mode="a2a",
+                                     num_blocks=128, block_size=16, max_batch=8,
+                                     max_model_len=512, max_prefill_tokens=128, seed=5),
+                        model_cfg=mc)
+        assert eng.model.e_local == mc.num_experts // world
+        for layer in eng.model.w["layers"]:
+            layer["router"].mul_(ROUTER_SCALE)
+        eng.runner.enable_logit_tap()
+        rng = random.Random(300 + rank)
+        lens = [(29, 61)[i % 2] + 3 * rank for i in range(1 + rank % 2)]
+        prompts = [[rng.randrange(10, mc.vocab_size - 10) for _ in range(n)] for n in lens]
+        seqs = eng.generate(prompts, SamplingParams(temperature=0.0, max_tokens=4,
+                                                    ignore_eos=True))
+        plain = [(s.seq_id, list(s.prompt), list(s.output)) for s in seqs]
+        rows = {k: [r.float().cpu() for r in v] for k, v in
+                _rows(eng.runner.logit_tap or []).items()}
+        q.put(("ok", rank, {"plain": plain, "rows": rows,
+                            "stats": dict(eng.runner.ep_stats)}))
+        import torch.distributed as dist
+
+        dist.barrier()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put(("err", rank, traceback.format_exc()))
+
+
 def _cp_worker(rank, world, port, q):
     _env(rank, world, port)
     try:
@@ -249,6 +288,35 @@ def test_ep_a2a_on_one_gpu_matches_dense_oracle(world):
     assert any(r["stats"]["pipelined_steps"] > 0 for r in busy), res
     if world >= 4:
         assert res[world - 1]["stats"]["idle_fill"] > 0
+
+
+def test_ep8_mixtral_layer_shapes_on_one_gpu_matches_dense_oracle():
+    """BASELINE config 5's EP = 8 with Mixtral-8x7B's exact layer shapes (2
+    layers): one expert per rank, IPC all-to-all of 4096-wide rows."""
+    from omnia_amd.models.config import resolve
+
+    res = _spawn(_ep_worker_mixtral, 8, timeout=600)
+    mc = resolve("mixtral-8x7b").replace(num_layers=2)
+    full = _full_mixtral(mc, 5)
+    for layer in full["layers"]:
+        layer["router"].mul_(ROUTER_SCALE)
+    bad = {k: v for k, v in full.items() if k != "layers"}
+    bad["layers"] = [dict(x) for x in full["layers"]]
+    gu = bad["layers"][0]["experts_gate_up"].clone()
+    gu[[0, 1]] = gu[[1, 0]]
+    bad["layers"][0]["experts_gate_up"] = gu
+    fracs, negs = [], []
+    for rank, r in sorted(res.items()):
+        frac, worst, n = _check(mc, full, r["plain"], r["rows"], 0.04)
+        bfrac, bworst, _ = _check(mc, bad, r["plain"], r["rows"], 0.04)
+        print(f"EP=8 mixtral rank {rank}: frac {frac:.3f} worst {worst:.4f} rows {n} "
+              f"neg {bfrac:.3f}/{bworst:.3f} stats {r['stats']}")
+        fracs.append(frac)
+        negs.append((bfrac, bworst))
+        assert n > 0
+    assert min(fracs) >= 0.97, fracs
+    assert any(b < 0.97 and w > 0.04 for b, w in negs), negs
+    assert len({r["stats"]["steps"] for r in res.values()}) == 1
 
 
 @pytest.mark.parametrize("world", [2, 4])

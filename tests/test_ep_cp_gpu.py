@@ -181,7 +181,9 @@ def _ep_worker_mixtral(rank, world, port, q):
         seqs = eng.generate(prompts, SamplingParams(temperature=0.0, max_tokens=4,
                                                     ignore_eos=True))
         plain = [(s.seq_id, list(s.prompt), list(s.output)) for s in seqs]
-        rows = {k: [r.float().cpu() for r in v] for k, v in
+        # numpy (pickled by value): torch CPU tensors would travel as shared-memory
+        # handles that die with this process
+        rows = {k: [r.float().cpu().numpy() for r in v] for k, v in
                 _rows(eng.runner.logit_tap or []).items()}
         q.put(("ok", rank, {"plain": plain, "rows": rows,
                             "stats": dict(eng.runner.ep_stats)}))
@@ -307,8 +309,9 @@ def test_ep8_mixtral_layer_shapes_on_one_gpu_matches_dense_oracle():
     bad["layers"][0]["experts_gate_up"] = gu
     fracs, negs = [], []
     for rank, r in sorted(res.items()):
-        frac, worst, n = _check(mc, full, r["plain"], r["rows"], 0.04)
-        bfrac, bworst, _ = _check(mc, bad, r["plain"], r["rows"], 0.04)
+        rows = {k: [torch.from_numpy(x) for x in v] for k, v in r["rows"].items()}
+        frac, worst, n = _check(mc, full, r["plain"], rows, 0.04)
+        bfrac, bworst, _ = _check(mc, bad, r["plain"], rows, 0.04)
         print(f"EP=8 mixtral rank {rank}: frac {frac:.3f} worst {worst:.4f} rows {n} "
               f"neg {bfrac:.3f}/{bworst:.3f} stats {r['stats']}")
         fracs.append(frac)

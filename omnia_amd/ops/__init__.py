@@ -42,6 +42,10 @@ def kernels():
 
             build(verbose=True)
             _ext = importlib.import_module("omnia_amd.ops._omnia_kernels")
+        # prefill GEMM main loop: 1 = 4-wave (one wave per SIMD), 0 = 8-wave ping-pong
+        sched = os.environ.get("OMNIA_PGEMM_SCHED")
+        if sched is not None and hasattr(_ext, "pgemm_set_schedule"):
+            _ext.pgemm_set_schedule(int(sched))
     return _ext
 
 

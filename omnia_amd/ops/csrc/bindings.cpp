@@ -18,6 +18,7 @@ int omnia_ar_alltoall(void* out, const void* in, void* const* regions, int* epoc
 int omnia_ar_sendrecv(void* out, const void* in, void* const* regions, int* epochs, int* err,
                       int64_t nbytes, int64_t slot_bytes, int rank, int world, int src_rank,
                       hipStream_t s);
+int omnia_pgemm_set_schedule(int sched);
 int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, int M, int N,
                         int K, hipStream_t s);
 int omnia_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows, int d,
@@ -946,6 +947,9 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("pgemm", &pgemm);
   m.def("row_sumsq", &row_sumsq);
   m.def("pgemm_variant", &pgemm_variant);
+  m.def("pgemm_set_schedule", [](int64_t sched) {
+    TORCH_CHECK(omnia_pgemm_set_schedule((int)sched) == 0, "pgemm schedule must be 0 or 1");
+  });
   m.def("ar_twoshot", &ar_twoshot);
   m.def("ar_region_bytes", &omnia_ar_region_bytes);
   m.def("splitk_add_rmsnorm", &splitk_add_rmsnorm);

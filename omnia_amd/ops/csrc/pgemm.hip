@@ -85,6 +85,98 @@ __device__ __forceinline__ void wait_vm() {
 // element offset of 16-B chunk `ch` of row `row` inside a half-tile
 __device__ __forceinline__ int swz(int row, int ch) { return row * BK + ((ch ^ (row & 7)) << 3); }
 
+// Epilogue copy-out shared by the 8-wave and 4-wave main loops: the block's
+// 256 x TN tile is staged in LDS as bf16 ([256][SROW], rows of the tile), and
+// every thread owns whole 16-B row chunks.
+template <int EPI, int NT>
+__device__ __forceinline__ void epi_out(const PArgs& p, const bf16_t* stg, int m0, int nt,
+                                        int Mt, int ntn, int tid, int lane) {
+  constexpr int TN = EPI == 1 ? 128 : 256;
+  if constexpr (EPI == 0 || EPI == 1) {
+    // coalesced copy-out: TN/8 chunks per row
+    constexpr int CPR = TN / 8;
+    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+#pragma unroll 4
+    for (int u = tid; u < 256 * CPR; u += NT) {
+      const int r = u / CPR, c = u - r * CPR;
+      if (r < Mt)
+        *reinterpret_cast<short8*>(out + (int64_t)(m0 + r) * p.ldo + (int64_t)nt * TN + c * 8) =
+            *reinterpret_cast<const short8*>(stg + r * SROW + c * 8);
+    }
+  } else if constexpr (EPI == 2) {
+    // residual += tile; 32 lanes per row (one 16-B chunk each) -> row sum of squares
+    bf16_t* res = reinterpret_cast<bf16_t*>(p.out);
+    const int c = lane & 31;
+    const int rsub = (tid >> 5);  // NT/32 rows per pass
+#pragma unroll 2
+    for (int r0 = 0; r0 < 256; r0 += NT / 32) {
+      const int r = r0 + rsub;
+      float ss = 0.f;
+      if (r < Mt) {
+        bf16_t* rp = res + (int64_t)(m0 + r) * p.ldo + (int64_t)nt * 256 + c * 8;
+        const short8 g = *reinterpret_cast<const short8*>(stg + r * SROW + c * 8);
+        const short8 o = *reinterpret_cast<const short8*>(rp);
+        short8 y;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint16_t h = f2bf(bf2f((uint16_t)o[j]) + bf2f((uint16_t)g[j]));
+          const float hf = bf2f(h);
+          ss += hf * hf;
+          y[j] = (short)h;
+        }
+        *reinterpret_cast<short8*>(rp) = y;
+      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      if (c == 0 && r < Mt) p.ss_out[(int64_t)(m0 + r) * ntn + nt] = ss;
+    }
+  } else {
+    // QKV: tile columns = heads 2nt, 2nt+1 of [q | k | v]; thread job = (row, head,
+    // chunk pair c / c+8 = dims 8c..8c+7 and 64+8c..64+8c+7)
+    bf16_t* qo = reinterpret_cast<bf16_t*>(p.out);
+#pragma unroll 2
+    for (int u = tid; u < 256 * 16; u += NT) {
+      const int r = u >> 4, hh = (u >> 3) & 1, c = u & 7;
+      if (r >= Mt) continue;
+      const int t = m0 + r;
+      const int head = nt * 2 + hh;  // global head index in [q heads | k heads | v heads]
+      const short8 x1 = *reinterpret_cast<const short8*>(stg + r * SROW + hh * 128 + c * 8);
+      const short8 x2 = *reinterpret_cast<const short8*>(stg + r * SROW + hh * 128 + 64 + c * 8);
+      short8 o1 = x1, o2 = x2;
+      if (head < p.hq + p.hkv) {
+        const float* cs = p.cos_sin + (int64_t)p.positions[t] * 128;
+        const float4v c0 = *reinterpret_cast<const float4v*>(cs + c * 8);
+        const float4v c1 = *reinterpret_cast<const float4v*>(cs + c * 8 + 4);
+        const float4v s0 = *reinterpret_cast<const float4v*>(cs + 64 + c * 8);
+        const float4v s1 = *reinterpret_cast<const float4v*>(cs + 64 + c * 8 + 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float cj = j < 4 ? c0[j] : c1[j - 4], sj = j < 4 ? s0[j] : s1[j - 4];
+          const float a = bf2f((uint16_t)x1[j]), b = bf2f((uint16_t)x2[j]);
+          o1[j] = (short)f2bf(a * cj - b * sj);
+          o2[j] = (short)f2bf(b * cj + a * sj);
+        }
+      }
+      if (head < p.hq) {
+        bf16_t* d = qo + (int64_t)t * p.ldo + head * 128 + c * 8;
+        *reinterpret_cast<short8*>(d) = o1;
+        *reinterpret_cast<short8*>(d + 64) = o2;
+      } else {
+        const int64_t slot = p.slots[t];
+        if (slot >= 0) {
+          const bool isk = head < p.hq + p.hkv;
+          const int kh = isk ? head - p.hq : head - p.hq - p.hkv;
+          const int64_t blk = slot / p.block_size, off = slot - blk * p.block_size;
+          bf16_t* d = (isk ? p.k_cache : p.v_cache) +
+                      ((blk * p.hkv + kh) * p.block_size + off) * 128 + c * 8;
+          *reinterpret_cast<short8*>(d) = o1;
+          *reinterpret_cast<short8*>(d + 64) = o2;
+        }
+      }
+    }
+  }
+}
+
 // VAR (tuning variants, EPI 0 only): bit 0 = no wave-row stagger, bit 1 = WITH
 // s_setprio around the MFMA clusters, bits 2-3 = m-tiles per L2 group (8/4/16/32)
 template <int EPI, int VAR = 0>
@@ -322,89 +414,211 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   }
   __syncthreads();
 
-  if constexpr (EPI == 0 || EPI == 1) {
-    // coalesced copy-out: TN/8 chunks per row
-    constexpr int CPR = TN / 8;
-    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
-#pragma unroll 4
-    for (int u = tid; u < 256 * CPR; u += 512) {
-      const int r = u / CPR, c = u - r * CPR;
-      if (r < Mt)
-        *reinterpret_cast<short8*>(out + (int64_t)(m0 + r) * p.ldo + (int64_t)nt * TN + c * 8) =
-            *reinterpret_cast<const short8*>(stg + r * SROW + c * 8);
+  epi_out<EPI, 512>(p, stg, m0, nt, Mt, ntn, tid, lane);
+}
+
+
+// ---------------------------------------------------------------------------
+// 4-wave schedule: one wave per SIMD, each wave a 128x128 quarter of the 256x256
+// block tile (2 x 2 waves), 64 fp32 16x16 accumulators per lane (256 registers:
+// the unified register file of a 1-wave-per-SIMD launch holds them beside the
+// fragments).  Per K-tile (64 k) a wave issues 128 MFMAs back to back on
+// independent accumulators; its LDS fragment reads for the NEXT half K-step are
+// issued before the current 64 MFMAs (register double buffer), so the matrix
+// core never waits on LDS.  Two LDS buffers; ONE barrier per K-tile, in the
+// middle of it: after it, every wave has finished reading buffer t&1 and every
+// wave's DMA of K-tile t+1 has landed, so the DMA of K-tile t+2 goes into
+// buffer t&1 right there and has a whole K-tile of MFMA time to land.  The
+// 8-wave ping-pong above parks ~26 % of its wave-cycles in its eight barriers
+// per K-tile (profiles/r4/pgemm_pmc_summary.md); this schedule has one.
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void pgemm4_kernel(PArgs p) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
+  constexpr int TN = EPI == 1 ? 128 : 256;
+  const int ntn = p.N / TN, mtn = (p.M + 255) >> 8;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 8;
+  const int per_group = GM * ntn;
+  const int grp = bid / per_group, gm0 = grp * GM;
+  const int gsz = mtn - gm0 < GM ? mtn - gm0 : GM;
+  const int idx = bid - grp * per_group;
+  const int mt = gm0 + idx % gsz, nt = idx / gsz;
+  const int m0 = mt << 8, Mt = p.M - m0 < 256 ? p.M - m0 : 256;
+  const int K = p.K, nk = K / BK;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // LDS-DMA: instruction i (0..3) of wave w fills half-tile rows 32w + 8i + lane/8;
+  // the swizzled source chunk depends on lane/8 only, so instruction i reads
+  // 8 i rows below instruction 0 (one base pointer per half-tile: 8 VGPRs, not 32)
+  const bf16_t* src[4];
+  {
+    const int row = 32 * w + (lane >> 3);
+    const int gch = (lane & 7) ^ (row & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int ar = m0 + h * 128 + row;
+      src[h] = p.X + (int64_t)(ar < p.M ? ar : p.M - 1) * K + gch * 8;
+      const int64_t br = EPI == 1 ? (int64_t)(h ? p.N : 0) + (int64_t)nt * 128 + row
+                                  : (int64_t)nt * 256 + h * 128 + row;
+      src[2 + h] = p.W + br * K + gch * 8;
     }
-  } else if constexpr (EPI == 2) {
-    // residual += tile; 32 lanes per row (one 16-B chunk each) -> row sum of squares
-    bf16_t* res = reinterpret_cast<bf16_t*>(p.out);
-    const int c = lane & 31;
-    const int rsub = (tid >> 5);  // 16 rows per pass
-#pragma unroll 2
-    for (int r0 = 0; r0 < 256; r0 += 16) {
-      const int r = r0 + rsub;
-      float ss = 0.f;
-      if (r < Mt) {
-        bf16_t* rp = res + (int64_t)(m0 + r) * p.ldo + (int64_t)nt * 256 + c * 8;
-        const short8 g = *reinterpret_cast<const short8*>(stg + r * SROW + c * 8);
-        const short8 o = *reinterpret_cast<const short8*>(rp);
-        short8 y;
+  }
+  // A rows past the chunk: instruction i of an A half-tile may cross p.M (clamped
+  // copies above only for i = 0) -> clamp per instruction below
+  const int arow0 = m0 + 32 * w + (lane >> 3);
+  auto issue_tile = [&](int buf, int kt) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint16_t h = f2bf(bf2f((uint16_t)o[j]) + bf2f((uint16_t)g[j]));
-          const float hf = bf2f(h);
-          ss += hf * hf;
-          y[j] = (short)h;
+    for (int h = 0; h < 4; ++h) {
+      bf16_t* dst = lds + (buf * 4 + h) * HALF + 32 * w * BK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int drow = 8 * i;
+        if (h < 2) {  // rows past M: reload the last row (never stored)
+          const int r0 = arow0 + h * 128;
+          const int base = r0 < p.M ? r0 : p.M - 1;
+          const int r = r0 + 8 * i;
+          drow = (r < p.M ? r : p.M - 1) - base;
         }
-        *reinterpret_cast<short8*>(rp) = y;
+        const int64_t off = (int64_t)kt * BK + (int64_t)drow * K;
+        __builtin_amdgcn_global_load_lds((const void*)(src[h] + off),
+                                         (lds_ptr_t)(dst + i * 512), 16, 0, 0);
       }
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-      if (c == 0 && r < Mt) p.ss_out[(int64_t)(m0 + r) * ntn + nt] = ss;
     }
-  } else {
-    // QKV: tile columns = heads 2nt, 2nt+1 of [q | k | v]; thread job = (row, head,
-    // chunk pair c / c+8 = dims 8c..8c+7 and 64+8c..64+8c+7)
-    bf16_t* qo = reinterpret_cast<bf16_t*>(p.out);
-#pragma unroll 2
-    for (int u = tid; u < 256 * 16; u += 512) {
-      const int r = u >> 4, hh = (u >> 3) & 1, c = u & 7;
-      if (r >= Mt) continue;
-      const int t = m0 + r;
-      const int head = nt * 2 + hh;  // global head index in [q heads | k heads | v heads]
-      const short8 x1 = *reinterpret_cast<const short8*>(stg + r * SROW + hh * 128 + c * 8);
-      const short8 x2 = *reinterpret_cast<const short8*>(stg + r * SROW + hh * 128 + 64 + c * 8);
-      short8 o1 = x1, o2 = x2;
-      if (head < p.hq + p.hkv) {
-        const float* cs = p.cos_sin + (int64_t)p.positions[t] * 128;
-        const float4v c0 = *reinterpret_cast<const float4v*>(cs + c * 8);
-        const float4v c1 = *reinterpret_cast<const float4v*>(cs + c * 8 + 4);
-        const float4v s0 = *reinterpret_cast<const float4v*>(cs + 64 + c * 8);
-        const float4v s1 = *reinterpret_cast<const float4v*>(cs + 64 + c * 8 + 4);
+  };
+
+  // fragment rows: A of wave row wr; B of wave column wc (gate_up: n < 4 gate,
+  // n >= 4 up of the SAME features, so silu(g) * u stays in one lane)
+  // every EPI: n < 4 from B half-tile 0, n >= 4 from half-tile 1, wave column wc
+  // owning columns wc*64 .. +64 of each half (compile-time half per fragment; a
+  // runtime half measured worse register allocation: accumulators shuffled
+  // through VGPRs inside the loop)
+  auto browB = [&](int n) { return wc * 64 + (n & 3) * 16 + fr; };
+  auto bhalf = [&](int n) { return n >> 2; };
+
+  short8 fa[2][8], fb[2][8];
+  auto read_frags = [&](int set, int buf, int ks) {
+    const bf16_t* abase = lds + (buf * 4 + wr) * HALF;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float cj = j < 4 ? c0[j] : c1[j - 4], sj = j < 4 ? s0[j] : s1[j - 4];
-          const float a = bf2f((uint16_t)x1[j]), b = bf2f((uint16_t)x2[j]);
-          o1[j] = (short)f2bf(a * cj - b * sj);
-          o2[j] = (short)f2bf(b * cj + a * sj);
-        }
+    for (int m = 0; m < 8; ++m)
+      fa[set][m] = *reinterpret_cast<const short8*>(abase + swz(m * 16 + fr, ks * 4 + fq));
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+      fb[set][n] = *reinterpret_cast<const short8*>(lds + (buf * 4 + 2 + bhalf(n)) * HALF +
+                                                    swz(browB(n), ks * 4 + fq));
+  };
+
+  float4v acc[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = {0.f, 0.f, 0.f, 0.f};
+  auto mfma_all = [&](int set) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 8; ++n) acc[m][n] = mfma16(fa[set][m], fb[set][n], acc[m][n]);
+  };
+
+  // prologue: K-tiles 0 and 1 in flight, wait for 0, first fragments
+  issue_tile(0, 0);
+  issue_tile(1, nk > 1 ? 1 : 0);
+  wait_vm<16>();
+  __builtin_amdgcn_s_barrier();
+  read_frags(0, 0, 0);
+  for (int t = 0; t < nk; ++t) {
+    const int b = t & 1;
+    read_frags(1, b, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_all(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // every wave: its reads of buffer b retired and its DMA of K-tile t+1 landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // unconditional (no control flow around the accumulators): past the end the
+    // DMA reloads the last K-tile into the dead buffer and the reads are unused
+    issue_tile(b, t + 2 < nk ? t + 2 : nk - 1);
+    read_frags(0, b ^ 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_all(1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // pin the accumulators to AGPRs at the loop exit: otherwise the allocator keeps
+  // some of them in VGPRs for the epilogue and shuffles them inside the loop
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) asm volatile("" : "+a"(acc[m][n]));
+  wait_vm<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave done with the ring before the staging tile reuses it
+
+  // ---------------------------------------------------------------- epilogue
+  float* rs_lds = reinterpret_cast<float*>(lds + RS_OFF);
+  const bool scaled = EPI != 2 && p.ss_in != nullptr;
+  if (scaled) {
+    if (tid < 256) {
+      int r = m0 + tid;
+      r = r < p.M ? r : p.M - 1;
+      const float* sp = p.ss_in + (int64_t)r * p.ss_in_n;
+      float tt = 0.f;
+      for (int i = 0; i < p.ss_in_n; ++i) tt += sp[i];
+      rs_lds[tid] = __builtin_amdgcn_rsqf(tt * p.inv_d + p.eps);
+    }
+    __syncthreads();
+  }
+  bf16_t* stg = lds;
+  auto put = [&](int row0, int col, float v0, float v1, float v2, float v3) {
+    const bool odd = fr & 1;
+    const float s0 = odd ? v0 : v2, s1 = odd ? v1 : v3;
+    const float r0 = __shfl_xor(s0, 1, 64), r1 = __shfl_xor(s1, 1, 64);
+    uint32_t* d0;
+    uint32_t* d1;
+    uint32_t x0, x1;
+    if (!odd) {
+      d0 = reinterpret_cast<uint32_t*>(stg + (row0 + 0) * SROW + col);
+      d1 = reinterpret_cast<uint32_t*>(stg + (row0 + 1) * SROW + col);
+      x0 = pack_bf2(v0, r0);
+      x1 = pack_bf2(v1, r1);
+    } else {
+      d0 = reinterpret_cast<uint32_t*>(stg + (row0 + 2) * SROW + col - 1);
+      d1 = reinterpret_cast<uint32_t*>(stg + (row0 + 3) * SROW + col - 1);
+      x0 = pack_bf2(r0, v2);
+      x1 = pack_bf2(r1, v3);
+    }
+    *d0 = x0;
+    *d1 = x1;
+  };
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int row0 = wr * 128 + m * 16 + fq * 4;
+    float4v rs = {1.f, 1.f, 1.f, 1.f};
+    if (scaled) rs = *reinterpret_cast<const float4v*>(rs_lds + row0);
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[j] = silu(acc[m][n][j] * rs[j]) * (acc[m][n + 4][j] * rs[j]);
+        put(row0, wc * 64 + n * 16 + fr, v[0], v[1], v[2], v[3]);
       }
-      if (head < p.hq) {
-        bf16_t* d = qo + (int64_t)t * p.ldo + head * 128 + c * 8;
-        *reinterpret_cast<short8*>(d) = o1;
-        *reinterpret_cast<short8*>(d + 64) = o2;
-      } else {
-        const int64_t slot = p.slots[t];
-        if (slot >= 0) {
-          const bool isk = head < p.hq + p.hkv;
-          const int kh = isk ? head - p.hq : head - p.hq - p.hkv;
-          const int64_t blk = slot / p.block_size, off = slot - blk * p.block_size;
-          bf16_t* d = (isk ? p.k_cache : p.v_cache) +
-                      ((blk * p.hkv + kh) * p.block_size + off) * 128 + c * 8;
-          *reinterpret_cast<short8*>(d) = o1;
-          *reinterpret_cast<short8*>(d + 64) = o2;
-        }
+    } else {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        const float4v v = acc[m][n];
+        put(row0, (n >> 2) * 128 + wc * 64 + (n & 3) * 16 + fr, v[0] * rs[0], v[1] * rs[1],
+            v[2] * rs[2], v[3] * rs[3]);
       }
     }
   }
+  __syncthreads();
+  epi_out<EPI, 256>(p, stg, m0, nt, Mt, ntn, tid, lane);
 }
 
 // one workgroup (256 threads) per row: ss[r] = sum(x[r]^2) (layer-0 input of the
@@ -433,8 +647,17 @@ extern "C" {
 
 // Returns 0 on success, < 0 for a shape / argument the kernel does not cover
 // (checked BEFORE any launch).
+int omnia_pgemm_set_schedule(int sched);
 int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, int M, int N,
                         int K, hipStream_t s);
+
+static int g_pgemm_sched = 0;  // 0: 8-wave ping-pong, 1: 4-wave (one wave per SIMD)
+
+int omnia_pgemm_set_schedule(int sched) {
+  if (sched < 0 || sched > 1) return -1;
+  g_pgemm_sched = sched;
+  return 0;
+}
 
 int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, int K, int ldo,
                 const float* ss_in, int ss_in_n, float inv_d, float eps, float* ss_out,
@@ -463,12 +686,21 @@ int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, 
   PArgs a{out, (const bf16_t*)X, (const bf16_t*)W, M, N, K, ldo, ss_in, ss_in_n, inv_d, eps,
           ss_out, positions, cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, slots, hq, hkv,
           block_size};
-  const dim3 grid((unsigned)blocks), block(512);
+  const dim3 grid((unsigned)blocks);
+  if (g_pgemm_sched == 1) {
+    switch (epi) {
+      case 0: pgemm4_kernel<0><<<grid, 256, 0, s>>>(a); break;
+      case 1: pgemm4_kernel<1><<<grid, 256, 0, s>>>(a); break;
+      case 2: pgemm4_kernel<2><<<grid, 256, 0, s>>>(a); break;
+      default: pgemm4_kernel<3><<<grid, 256, 0, s>>>(a); break;
+    }
+    return (int)hipGetLastError();
+  }
   switch (epi) {
-    case 0: pgemm_kernel<0><<<grid, block, 0, s>>>(a); break;
-    case 1: pgemm_kernel<1><<<grid, block, 0, s>>>(a); break;
-    case 2: pgemm_kernel<2><<<grid, block, 0, s>>>(a); break;
-    default: pgemm_kernel<3><<<grid, block, 0, s>>>(a); break;
+    case 0: pgemm_kernel<0><<<grid, 512, 0, s>>>(a); break;
+    case 1: pgemm_kernel<1><<<grid, 512, 0, s>>>(a); break;
+    case 2: pgemm_kernel<2><<<grid, 512, 0, s>>>(a); break;
+    default: pgemm_kernel<3><<<grid, 512, 0, s>>>(a); break;
   }
   return (int)hipGetLastError();
 }
@@ -488,6 +720,7 @@ int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, in
     case 4: pgemm_kernel<0, 4><<<grid, block, 0, s>>>(a); break;
     case 8: pgemm_kernel<0, 8><<<grid, block, 0, s>>>(a); break;
     case 12: pgemm_kernel<0, 12><<<grid, block, 0, s>>>(a); break;
+    case 16: pgemm4_kernel<0><<<grid, 256, 0, s>>>(a); break;
     default: return -2;
   }
   return (int)hipGetLastError();

@@ -42,7 +42,11 @@ def main():
     ap.add_argument("--m", default="4096,8192,16384")
     ap.add_argument("--shapes", default="gate_up,qkv,o,down")
     ap.add_argument("--out", default="gpurun_out/pgemm_sweep.json")
+    ap.add_argument("--schedule", type=int, default=0,
+                    help="pgemm main loop: 0 = 8-wave ping-pong, 1 = 4-wave")
     a = ap.parse_args()
+    ops.kernels().pgemm_set_schedule(a.schedule)
+    print("pgemm schedule:", a.schedule, flush=True)
     from omnia_amd.ops.gemm_tuning import enable_tuned_gemms
 
     print("tuned hipBLASLt table:", enable_tuned_gemms(0), flush=True)

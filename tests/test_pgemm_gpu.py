@@ -24,6 +24,17 @@ def _close(got, want, tol):
     return err <= tol * scale, err / max(scale, 1e-30)
 
 
+@pytest.fixture(autouse=True, params=[0, 1], ids=["8wave", "4wave"])
+def schedule(request):
+    """Every check runs on both main loops: the 8-wave ping-pong and the 4-wave
+    one-wave-per-SIMD schedule (same epilogues)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ops.kernels().pgemm_set_schedule(request.param)
+    yield request.param
+    ops.kernels().pgemm_set_schedule(0)
+
+
 @pytest.fixture(scope="module")
 def gen():
     if not torch.cuda.is_available():
@@ -140,3 +151,29 @@ def test_rejects_bad_shapes(gen):
     w = _rand(256, 192, gen=gen)
     with pytest.raises(RuntimeError):
         ops.pgemm(0, x, w, out=torch.empty(256, 256, dtype=torch.bfloat16, device=DEV))
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_schedules_are_bit_identical(gen, schedule, epi):
+    """Both main loops accumulate every output element over K in the same order
+    with the same instruction: identical bits, ragged M included."""
+    M, K = 777, 1024
+    N = 512
+    x = _rand(M, K, gen=gen)
+    w = _rand(2 * N if epi == 1 else N, K, std=0.05, gen=gen)
+    ss = torch.rand(M, 2, device=DEV, generator=gen) * K
+    outs = []
+    for sched in (0, 1):
+        ops.kernels().pgemm_set_schedule(sched)
+        if epi == 2:
+            o = _rand(M, N, gen=torch.Generator(device=DEV).manual_seed(5))
+            sso = torch.zeros(M, N // 256, device=DEV)
+            ops.pgemm(2, x, w, out=o, ss_out=sso)
+            outs.append((o, sso))
+        else:
+            o = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            ops.pgemm(epi, x, w, out=o, ss_in=ss, inv_d=1.0 / K, eps=1e-5)
+            outs.append((o,))
+    ops.kernels().pgemm_set_schedule(schedule)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -148,6 +148,11 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, device: str |
             dist.all_gather_object(idents, (socket.gethostname(), _device_identity()),
                                    group=side)
             check_transport(transport, idents)
+            if transport == "ipc" and len({tuple(x) for x in idents}) == ws and \
+                    not os.environ.get("OMNIA_TP_TRANSPORT"):
+                log.warning("transport ipc inferred (LOCAL_WORLD_SIZE > visible devices) but "
+                            "every rank has its own device (per-rank visibility?): set "
+                            "OMNIA_TP_TRANSPORT=rccl to run the large collectives on RCCL")
             if side is not None:
                 dist.destroy_process_group(side)
             log.info("rank %d: transport %s (backend %s, %d rank(s) per device)", rank,

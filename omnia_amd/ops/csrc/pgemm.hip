@@ -531,21 +531,36 @@ __global__ __launch_bounds__(256, 1) void pgemm4_kernel(PArgs p) {
   read_frags(0, 0, 0);
   for (int t = 0; t < nk; ++t) {
     const int b = t & 1;
+    // half 0: the 16 fragment reads of the second half K-step ride between the
+    // 64 MFMAs of the first (one wave per SIMD: nobody else fills the MFMA pipe
+    // while this wave issues memory instructions, so they are interleaved)
     read_frags(1, b, 1);
-    __builtin_amdgcn_sched_barrier(0);
     mfma_all(0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 LDS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+    }
     __builtin_amdgcn_sched_barrier(0);
     // every wave: its reads of buffer b retired and its DMA of K-tile t+1 landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    // unconditional (no control flow around the accumulators): past the end the
-    // DMA reloads the last K-tile into the dead buffer and the reads are unused
+    // half 1: the next K-tile's 16 DMA and 16 first-half fragment reads between
+    // the 64 MFMAs.  Unconditional (no control flow around the accumulators):
+    // past the end the DMA reloads the last K-tile into the dead buffer and the
+    // reads are unused
     issue_tile(b, t + 2 < nk ? t + 2 : nk - 1);
     read_frags(0, b ^ 1, 0);
-    __builtin_amdgcn_sched_barrier(0);
     mfma_all(1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 VMEM (LDS-DMA)
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 LDS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
   // pin the accumulators to AGPRs at the loop exit: otherwise the allocator keeps

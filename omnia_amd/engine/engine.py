@@ -164,9 +164,9 @@ class LLMEngine:
         self.scheduler = Scheduler(
             SchedulerConfig(max_batch=cfg.max_batch, max_prefill_tokens=cfg.max_prefill_tokens,
                             max_model_len=cfg.max_model_len,
-                            # mixed steps run on the TP-rank-0-only eager path: TP keeps
-                            # separate prefill / decode steps
-                            mixed_budget=cfg.mixed_budget if self.model.tp == 1 else 0,
+                            # under TP a mixed step is published to the workers (MIXED)
+                            # and sampled synchronously on rank 0
+                            mixed_budget=cfg.mixed_budget,
                             mixed_backlog=cfg.mixed_backlog,
                             cp_threshold=cfg.cp_threshold if self.cp_lockstep else 0),
             self.blocks)

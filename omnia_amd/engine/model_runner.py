@@ -429,9 +429,18 @@ class ModelRunner:
                                 for p, x in zip(ps, sample_seqs)], np.int64),
                       np.array([len(x.output) for x in sample_seqs], np.int64),
                       np.array([self.assign_slot(x) for x in sample_seqs], np.int64)]
-        t = torch.from_numpy(np.concatenate(parts))
-        if self.is_gpu:
-            t = t.pin_memory().to(self.device, non_blocking=True)
+        host = torch.from_numpy(np.concatenate(parts))
+        # T, B, Bd, maxb, mbd, tiles, n_sample, launch
+        meta = (T, B, Bd, maxb, mbd, len(tseq), len(sample_rows), int(launch))
+        t = host.pin_memory().to(self.device, non_blocking=True) if self.is_gpu else host
+        logits = self._mixed_forward_packed(t, meta, host)
+        return logits, sample_seqs, t, tail
+
+    def _mixed_forward_packed(self, t: torch.Tensor, meta, host=None) -> torch.Tensor:
+        """Forward of a packed mixed upload (``meta`` = T, B, Bd, maxb, mbd,
+        tiles, n_sample, launch) -- the part TP workers replay (``engine/tp.py``
+        MIXED).  ``host``: the upload on the host (TP rank 0 publishes it)."""
+        T, B, Bd, maxb, mbd, ntiles, nsample, launch = meta
         o = 0
 
         def take(n, dtype):
@@ -445,9 +454,9 @@ class ModelRunner:
                           logits_indices=None, is_decode=False, num_seqs=B)
         fb.q_start_loc = take(B + 1, torch.int32)
         fb.seq_lens = take(B, torch.int32)
-        fb.tile_seq = take(len(tseq), torch.int32)
-        fb.tile_q0 = take(len(tq0), torch.int32)
-        fb.logits_indices = take(len(sample_rows), torch.int64)
+        fb.tile_seq = take(ntiles, torch.int32)
+        fb.tile_q0 = take(ntiles, torch.int32)
+        fb.logits_indices = take(nsample, torch.int64)
         fb.block_tables = take(B * maxb, torch.int32).view(B, maxb)
         fb.dec_block_tables = take(Bd * mbd, torch.int32).view(Bd, mbd)
         fb.dec_seq_lens = take(Bd, torch.int32)
@@ -459,7 +468,7 @@ class ModelRunner:
                                     ids_d))
         logits = self.model.forward(fb, self.kv)
         self.stats["mixed_steps"] = self.stats.get("mixed_steps", 0) + 1
-        return logits, sample_seqs, t, tail
+        return logits
 
     def run_mixed(self, dseqs: list[Sequence], chunks: list[tuple[Sequence, int]]
                   ) -> tuple[list[int], dict[int, int]]:

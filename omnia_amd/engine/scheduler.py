@@ -175,7 +175,8 @@ class Scheduler:
             decode = self._decode_rows()
             # the decode rows count against the budget: a full mixed step is exactly
             # mixed_budget tokens, the GEMM shape the prefill GEMMs were tuned for
-            chunks = self._prefill_chunks(max(0, cfg.mixed_budget - len(decode)))
+            chunks = self._prefill_chunks(
+                max(0, min(cfg.mixed_budget, cfg.max_prefill_tokens) - len(decode)))
             if chunks and decode:
                 return StepPlan("mixed", chunks, decode)
             if chunks:

@@ -24,6 +24,8 @@ The previous design broadcast header and payload over RCCL every step and read
 the header back with ``.tolist()`` (a device -> host sync per step per worker).
 
 Commands: ``PREFILL (T,B,maxb,tiles,nsample,len,gather,sampling offset)``,
+``MIXED (T,B,Bd,maxb,mbd,tiles,nsample,launch,len)`` (decode rows + prefill
+chunks in one forward, the packed upload of ``ModelRunner._mixed_forward``),
 ``DECODE (nrows,ncols)``, ``EAGER (n,ncols)``, ``SWAP_OUT (handle,n)``,
 ``SWAP_IN (handle,n)``, ``SWAP_DROP (handle)``, ``STOP``.
 
@@ -49,7 +51,7 @@ from .model_runner import ModelRunner
 
 log = logging.getLogger("omnia.engine.tp")
 
-STOP, PREFILL, DECODE, EAGER, SWAP_OUT, SWAP_IN, SWAP_DROP = range(7)
+STOP, PREFILL, DECODE, EAGER, SWAP_OUT, SWAP_IN, SWAP_DROP, MIXED = range(8)
 HDR = 16
 
 
@@ -187,7 +189,9 @@ def _ring_payload_bytes(runner) -> int:
     """Upper bound of one step's payload: the decode staging buffer or a packed
     prefill upload of ``max_prefill_tokens`` tokens (``ModelRunner._prefill_pack``)."""
     T, B, mb = runner.max_prefill_tokens, runner.max_batch, runner.max_blocks
-    prefill = 8 * (3 * T + 2 * (B + 1) + 2 * (T // 64 + B + 1) + B + B * mb + 5 * B + 64)
+    # (+ B * mb + 2 * B: a mixed step adds the decode rows' block tables and lengths)
+    T = T + B  # mixed steps: decode rows ride in front of the prefill tokens
+    prefill = 8 * (3 * T + 2 * (B + 1) + 2 * (T // 64 + B + 1) + B + 2 * B * mb + 8 * B + 64)
     return max(runner.dec.nbytes, prefill, 8 * mb + 64)
 
 
@@ -243,6 +247,12 @@ class TPModelRunner(ModelRunner):
         self.chan.send(PREFILL, *meta[:5], t.numel(), int(gather),
                        meta[5] if len(meta) > 5 else 0, payload=host)
         return super()._prefill_forward(t, meta, gather)
+
+    def _mixed_forward_packed(self, t, meta, host=None):
+        if host is None:
+            host = t.cpu()
+        self.chan.send(MIXED, *meta, host.numel(), payload=host)
+        return super()._mixed_forward_packed(t, meta, host)
 
     def _before_replay(self, nrows, ncols, st=None):
         self.chan.send(DECODE, nrows, ncols, payload=(st or self.dec).host)
@@ -304,6 +314,14 @@ class TPWorker(ModelRunner):
             elif cmd == EAGER:
                 self._stage_in(body)
                 self._eager_forward(h[1], h[2])
+            elif cmd == MIXED:
+                meta = tuple(h[1:9])
+                n = h[9]
+                host = torch.from_numpy(body.view(np.int64)[:n].copy())
+                self.chan.release()
+                t = host.pin_memory().to(self.device, non_blocking=True) if self.is_gpu \
+                    else host
+                ModelRunner._mixed_forward_packed(self, t, meta)
             elif cmd in (SWAP_OUT, SWAP_IN):
                 blocks = body.view(np.int64)[:h[2]].tolist()
                 self.chan.release()

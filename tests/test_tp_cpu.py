@@ -20,10 +20,23 @@ from omnia_amd.models.loader import shard_weights
 PROMPTS = [list(range(5, 70)), list(range(100, 130)), list(range(7, 200, 3))]
 
 
-def _cfg(tp, model="tiny-llama"):
+def _cfg(tp, model="tiny-llama", **kw):
     return EngineConfig(model=model, device="cpu", dtype="float32", tp=tp, num_blocks=64,
                         block_size=32, max_batch=8, max_model_len=1024, max_prefill_tokens=64,
-                        use_graphs=False)
+                        use_graphs=False, **kw)
+
+
+def _generate_mixed(eng):
+    """Two sequences decoding when a third prompt arrives: mixed steps."""
+    p = SamplingParams(temperature=0, max_tokens=10, ignore_eos=True)
+    s1 = eng.add_request(PROMPTS[0], p)
+    s2 = eng.add_request(PROMPTS[1], p)
+    for _ in range(4):
+        eng.step()
+    s3 = eng.add_request(PROMPTS[2], p)
+    eng.run_until_done()
+    mixed = eng.counters.get("steps_mixed", 0) + eng.counters.get("steps_mixed_sync", 0)
+    return [s1.output, s2.output, s3.output], mixed
 
 
 def _full_weights(model="tiny-llama"):
@@ -40,20 +53,20 @@ def _generate(eng):
     return out + [t2.output], t2.prefix_hit
 
 
-def _worker(rank, world, port, q, model="tiny-llama"):
+def _worker(rank, world, port, q, model="tiny-llama", mixed=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from omnia_amd.engine import tp
     from omnia_amd.parallel import state as pstate
 
     try:
-        cfg = _cfg(world, model)
+        cfg = _cfg(world, model, mixed_budget=mixed)
         full = _full_weights(model)  # built before the TP state exists: the whole model
         pstate.init_distributed(tp_size=world, backend="gloo", device="cpu")
         w = shard_weights(full, resolve(model), world, rank)
         eng = tp.start(cfg, weights=w)
         if eng is not None:
-            res = _generate(eng)
+            res = _generate_mixed(eng) if mixed else _generate(eng)
             eng.shutdown()
             q.put(("ok", res))
     except Exception as e:  # pragma: no cover - surfaced through the queue
@@ -115,6 +128,32 @@ def test_tp_world4_world8_engine_matches_single_rank(world):
     outs, hit = res
     assert hit > 0
     assert outs == ref[0]
+
+
+def test_tp2_mixed_steps_match_single_rank():
+    """Mixed prefill+decode steps under TP: rank 0 publishes each mixed step's
+    packed upload (MIXED) and samples from the gathered logits; tokens equal a
+    single-rank engine taking the same mixed steps."""
+    ref, ref_mixed = _generate_mixed(LLMEngine(_cfg(1, mixed_budget=48),
+                                               weights=_full_weights()))
+    assert ref_mixed >= 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, "tiny-llama", 48))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        status, res = q.get(timeout=300)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert status == "ok", res
+    outs, mixed = res
+    assert mixed >= 2 and outs == ref
 
 
 def test_shm_ring_flow_control(tmp_path):

@@ -91,7 +91,7 @@ def _sharded_weights(mc, rank, world, keep_full: bool):
     return shard, full
 
 
-def _worker(rank, world, port, q, pipeline=False, batch=8):
+def _worker(rank, world, port, q, pipeline=False, batch=8, mixed=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
                       OMNIA_LOGIT_TAP="1",
@@ -113,7 +113,7 @@ def _worker(rank, world, port, q, pipeline=False, batch=8):
         cfg = EngineConfig(model=mc.name, device="cuda", tp=world, num_blocks=256, block_size=16,
                            max_batch=batch, max_model_len=1024,
                            max_prefill_tokens=64 if batch <= 8 else 1024,
-                           pipeline=pipeline, seed=3)
+                           pipeline=pipeline, seed=3, mixed_budget=mixed)
         eng = tp.start(cfg, model_cfg=mc, weights=shard)
         if eng is None:
             return  # worker: rank 0 shut the group down
@@ -126,9 +126,22 @@ def _worker(rank, world, port, q, pipeline=False, batch=8):
         # + RMSNorm kernel (only the two checked sessions go to the oracle)
         fill = [[rng.randrange(10, V - 10) for _ in range(12)] for _ in range(batch - 2)] \
             if batch > 8 else []
-        seqs = eng.generate(prompts + fill, greedy,
-                            session_ids=["a", "b"] + [f"f{i}" for i in range(len(fill))])
-        seqs = seqs[:2]
+        if mixed:
+            # fillers decode first; the checked prompts arrive mid-decode, so they
+            # are prefilled in MIXED steps (published to the workers) beside them
+            fs = [eng.add_request(f, greedy, session_id=f"f{i}") for i, f in enumerate(fill)]
+            for _ in range(4):
+                eng.step()
+            seqs = [eng.add_request(pr, greedy, session_id=sid)
+                    for pr, sid in zip(prompts, ["a", "b"])]
+            eng.run_until_done()
+            assert eng.counters.get("steps_mixed_sync", 0) + \
+                eng.counters.get("steps_mixed", 0) >= 1, eng.counters
+            del fs
+        else:
+            seqs = eng.generate(prompts + fill, greedy,
+                                session_ids=["a", "b"] + [f"f{i}" for i in range(len(fill))])
+            seqs = seqs[:2]
         p2 = prompts[0] + seqs[0].output + [rng.randrange(10, V - 10) for _ in range(12)]
         s2 = eng.generate([p2], greedy, session_ids=["a"])[0]
         hit = s2.prefix_hit
@@ -164,9 +177,10 @@ def _worker(rank, world, port, q, pipeline=False, batch=8):
         q.put(("err", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,pipeline,batch", [(2, False, 8), (4, False, 8), (8, False, 8),
-                                                  (2, True, 64), (4, True, 64), (8, True, 64)])
-def test_tp_engine_on_one_gpu_matches_dense_oracle(world, pipeline, batch):
+@pytest.mark.parametrize("world,pipeline,batch,mixed", [
+    (2, False, 8, 0), (4, False, 8, 0), (8, False, 8, 0),
+    (2, True, 64, 0), (4, True, 64, 0), (8, True, 64, 0), (2, True, 64, 256)])
+def test_tp_engine_on_one_gpu_matches_dense_oracle(world, pipeline, batch, mixed):
     """(pipeline=True, batch 64) is the config-4 engine as shipped: one-deep
     pipelined graph decode over the shared-memory step ring, fused two-shot
     all-reduce + RMSNorm at the layer boundaries."""
@@ -179,7 +193,7 @@ def test_tp_engine_on_one_gpu_matches_dense_oracle(world, pipeline, batch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipeline, batch))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipeline, batch, mixed))
              for r in range(world)]
     for p in procs:
         p.start()

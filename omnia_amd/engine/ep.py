@@ -116,11 +116,17 @@ def run_ep_step(engine) -> int:
 
     runner: EPModelRunner = engine.runner
     model = runner.model
+    n_pre = 0
+    if engine.inflight is not None and not engine._steady():
+        # the pool may not give every running sequence its next page without a
+        # preemption: never preempt a sequence with a token in flight
+        engine.timing["pipeline_breaks"] += 1
+        n_pre = engine._flush_inflight()
     plan = engine.scheduler.schedule()
     active, tokens, eager, rows, cols = runner.agree(*runner.describe(plan))
     engine._ep_active = active
     if not active:
-        return engine._flush_inflight()
+        return n_pre + engine._flush_inflight()
     runner.ep_stats["steps"] += 1
     pipelined = engine.cfg.pipeline and runner.use_graphs and runner.device_handoff
     if not eager and pipelined and plan.kind == "decode" and plan.decode:
@@ -135,8 +141,8 @@ def run_ep_step(engine) -> int:
         engine.counters["decode_tokens"] += len(plan.decode)
         engine.counters["steps_decode"] += 1
         engine.step_count += 1
-        return n
-    n0 = engine._flush_inflight()  # eager / idle-rank steps run on settled state
+        return n_pre + n
+    n0 = n_pre + engine._flush_inflight()  # eager / idle-rank steps run on settled state
     if plan.decode:
         plan.decode = [sq for sq in plan.decode if not sq.is_finished]
         if plan.kind == "decode" and not plan.decode:

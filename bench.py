@@ -64,8 +64,9 @@ def parse(argv=None):
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica")
     ap.add_argument("--arrival", choices=["closed", "poisson"], default="closed")
     ap.add_argument("--rate", type=float, default=0.0, help="poisson: turns/s per replica")
-    ap.add_argument("--mixed-budget", type=int, default=0,
-                    help="engine mixed steps: decode rows + <= N prefill tokens per forward")
+    ap.add_argument("--mixed-budget", type=int, default=None,
+                    help="engine mixed steps: decode rows + <= N prefill tokens per forward "
+                         "(default: the engine's, gated on the prefill backlog)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--inproc", action="store_true",
                     help="runtime path: engine as a thread of the serving process")
@@ -154,7 +155,9 @@ class WSDriver:
             "OMNIA_ENGINE_SEED": rank,
             "OMNIA_ENGINE_PROC": "1" if (use_gpu and a.tp == 1) or a.engine == "synthetic" else "0",
             "OMNIA_ENGINE_SYNTHETIC": "1" if a.engine == "synthetic" else "0",
-            "OMNIA_ENGINE_TP": a.tp, "OMNIA_ENGINE_MIXED_BUDGET": a.mixed_budget,
+            "OMNIA_ENGINE_TP": a.tp,
+            **({"OMNIA_ENGINE_MIXED_BUDGET": a.mixed_budget} if a.mixed_budget is not None
+               else {}),
         }
         fenv = {"OMNIA_AGENT_NAME": f"bench-{rank}", "OMNIA_MAX_CONNECTIONS": 4 * C + 64,
                 "OMNIA_MSG_RATE": 1000, "OMNIA_MSG_BURST": 1000}
@@ -289,7 +292,8 @@ class LocalDriver:
                            max_batch=max(C, 1),
                            max_model_len=max(2048, a.prompt_len + a.gen_len + 64),
                            max_prefill_tokens=a.max_prefill_tokens, use_graphs=not a.no_graphs,
-                           seed=rank, mixed_budget=a.mixed_budget)
+                           seed=rank, **({"mixed_budget": a.mixed_budget}
+                                         if a.mixed_budget is not None else {}))
         self.cfg = cfg
         self.eng = self.client = None
         if self.proc:
@@ -578,7 +582,8 @@ def run(a, drv, ws, rank, use_gpu, host_only):
                 "path": a.path,
                 "arrival": a.arrival if a.arrival == "closed" else f"poisson@{a.rate}/s",
                 "stream_interval_ms": a.stream_interval_ms,
-                "mixed_budget": a.mixed_budget,
+                "mixed_budget": a.mixed_budget if a.mixed_budget is not None else
+                "engine default (16384, backlog-gated at 8192)",
                 "tp": a.tp,
                 "hip_graphs": not a.no_graphs,
                 "engine": a.engine,

@@ -10,7 +10,7 @@ from omnia_amd.engine.sampling_params import SamplingParams
 
 def eng(**kw):
     base = dict(model="tiny-llama", device="cuda", num_blocks=256, block_size=32, max_batch=16,
-                max_model_len=2048)
+                max_model_len=2048, mixed_budget=0)  # mixed steps opt in per test
     base.update(kw)
     return LLMEngine(EngineConfig(**base))
 

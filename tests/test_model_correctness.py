@@ -20,6 +20,7 @@ from omnia_amd.ops import reference as ref
 
 
 def _engine(device, mc, chunk, **kw):
+    kw.setdefault("mixed_budget", 0)  # the paths under test; mixed steps have their own test
     eng = LLMEngine(EngineConfig(model=mc.name, device=device, num_blocks=512, block_size=16,
                                  max_batch=8, max_model_len=1024, max_prefill_tokens=chunk,
                                  pipeline=False, seed=3, **kw), model_cfg=mc)
@@ -75,7 +76,9 @@ def _gate(device, mc, chunk, rel_tol, min_pass=1.0, router_scale=None, prompt_le
         for layer in w["layers"]:
             layer["router"].mul_(router_scale)
     seqs = _run(eng, mc, rng, **({"prompt_lens": prompt_lens} if prompt_lens else {}))
-    assert eng.counters["steps_prefill"] > len(seqs)  # prompts really were chunked
+    c = eng.counters  # prompts really were chunked (prefill or mixed steps)
+    assert c["steps_prefill"] + c.get("steps_mixed", 0) + c.get("steps_mixed_sync", 0) > \
+        len(seqs), dict(c)
     frac, worst = _check(mc, w, seqs, eng.runner.logit_tap, rel_tol)
     assert frac >= min_pass, f"{mc.name}: {frac:.3f} of rows within {rel_tol}, worst {worst:.4f}"
     # negative control: a wrong kv-head slice in the oracle must fail the gate

@@ -60,7 +60,7 @@ def _worker(rank, world, port, q, model="tiny-llama", mixed=0):
     from omnia_amd.parallel import state as pstate
 
     try:
-        cfg = _cfg(world, model, mixed_budget=mixed)
+        cfg = _cfg(world, model, mixed_budget=mixed, tp_mixed=bool(mixed))
         full = _full_weights(model)  # built before the TP state exists: the whole model
         pstate.init_distributed(tp_size=world, backend="gloo", device="cpu")
         w = shard_weights(full, resolve(model), world, rank)

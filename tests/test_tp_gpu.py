@@ -113,7 +113,7 @@ def _worker(rank, world, port, q, pipeline=False, batch=8, mixed=0):
         cfg = EngineConfig(model=mc.name, device="cuda", tp=world, num_blocks=256, block_size=16,
                            max_batch=batch, max_model_len=1024,
                            max_prefill_tokens=64 if batch <= 8 else 1024,
-                           pipeline=pipeline, seed=3, mixed_budget=mixed)
+                           pipeline=pipeline, seed=3, mixed_budget=mixed, tp_mixed=bool(mixed))
         eng = tp.start(cfg, model_cfg=mc, weights=shard)
         if eng is None:
             return  # worker: rank 0 shut the group down

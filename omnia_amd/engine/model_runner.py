@@ -99,13 +99,18 @@ class ModelRunner:
         self.kv = kv
         self.device = model.device
         self.is_gpu = self.device.type == "cuda"
+        # OMNIA_SIM_GRAPHS=1 (CPU tests only): the pipelined engine loop on the CPU
+        # -- "graphs" replay the decode body eagerly and events are no-ops -- so
+        # its scheduling / staging / hand-off logic runs where a bad index raises
+        # instead of faulting a GPU
+        self.sim = not self.is_gpu and os.environ.get("OMNIA_SIM_GRAPHS") == "1"
         self.bs = kv.block_size
         self.max_model_len = max_model_len
         self.max_blocks = (max_model_len + self.bs - 1) // self.bs
         self.max_batch = max_batch
         self.max_prefill_tokens = max_prefill_tokens
         self.vocab = model.cfg.vocab_size
-        self.use_graphs = use_graphs and self.is_gpu
+        self.use_graphs = use_graphs and (self.is_gpu or self.sim)
         self.buckets = [b for b in BATCH_BUCKETS if b < max_batch] + [max_batch]
         pin = self.is_gpu
         B, MB = max_batch, self.max_blocks
@@ -219,10 +224,16 @@ class ModelRunner:
     def device_handoff(self) -> bool:
         """Steps feed not-yet-collected tokens from the device token slots (single
         rank; TP workers keep the host hand-off for prefill-sampled tokens)."""
-        return self.is_gpu and self.model.tp == 1
+        return (self.is_gpu or self.sim) and self.model.tp == 1
+
+    def _event(self):
+        """A recorded stream event (a no-op stand-in in the CPU simulation)."""
+        ev = torch.cuda.Event() if self.is_gpu else _SimEvent()
+        ev.record()
+        return ev
 
     def can_pipeline_prefill(self, chunks) -> bool:
-        return self.is_gpu and not any(s.params.needs_penalties or s.guide is not None
+        return (self.is_gpu or self.sim) and not any(s.params.needs_penalties or s.guide is not None
                                        for s, _ in chunks)
 
     def launch_prefill(self, chunks: list[tuple[Sequence, int]]) -> "DecodeHandle":
@@ -253,8 +264,7 @@ class ModelRunner:
                 o = meta[5] + 5 * n
                 self.tok_slots.index_copy_(0, t[o:o + n], tok.to(torch.int32))
             out_host[:n].copy_(tok, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        ev = self._event()
         self.pf_events[slot] = ev
         return DecodeHandle(sample_seqs, out_host, ev, n, "prefill")
 
@@ -508,8 +518,7 @@ class ModelRunner:
             self.pf_hosts[slot] = out_host = torch.zeros(
                 max(n, 2 * out_host.numel()), dtype=torch.int32, pin_memory=True)
         out_host[:n].copy_(tok, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        ev = self._event()
         self.pf_events[slot] = ev
         return DecodeHandle(sample_seqs, out_host, ev, n, "mixed")
 
@@ -689,6 +698,11 @@ class ModelRunner:
 
     def _capture(self, nrows: int, ncols: int):
         t0 = time.perf_counter()
+        if self.sim:  # CPU simulation: "replay" = the eager decode body
+            g = _SimGraph(lambda: self._decode_body(nrows, ncols))
+            self.graphs[(nrows, ncols)] = g
+            self.stats["captures"] += 1
+            return g
         if self.graph_pool is None:
             self.graph_pool = torch.cuda.graph_pool_handle()
         # warm-up/capture must not clobber live sampler outputs of an in-flight step
@@ -774,8 +788,7 @@ class ModelRunner:
             self._before_replay(nrows, ncols, st)
             self._replay(nrows, ncols)
             out_host[:n].copy_(self.out_tok[:n], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
+            ev = self._event()
         st.event = ev
         h = DecodeHandle(seqs, out_host, ev, n)
         if self._tap is not None:
@@ -824,6 +837,27 @@ class ModelRunner:
 
 PLACEHOLDER = -1
 _PAD = object()  # row_seq marker of a padded (null) row
+
+
+class _SimEvent:
+    """No-op event of the CPU simulation (``ModelRunner.sim``)."""
+
+    def record(self, *a):
+        pass
+
+    def synchronize(self):
+        return 0
+
+    def query(self):
+        return True
+
+
+class _SimGraph:
+    def __init__(self, fn):
+        self.fn = fn
+
+    def replay(self):
+        self.fn()
 
 
 class DecodeHandle:

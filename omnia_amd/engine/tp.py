@@ -287,9 +287,7 @@ class TPWorker(ModelRunner):
         self.chan.release()
         self.dec.dev.copy_(st.host, non_blocking=True)
         if self.is_gpu:
-            ev = torch.cuda.Event()
-            ev.record()
-            self.wevents[slot] = ev
+            self.wevents[slot] = self._event()
 
     def run(self):
         while True:

@@ -187,10 +187,12 @@ def test_tp_engine_on_one_gpu_matches_dense_oracle(world, pipeline, batch, mixed
 
 @pytest.mark.skipif(os.environ.get("OMNIA_TEST_TP_STAGGER") != "1",
                     reason="bisecting the TP mixed-step fault: run explicitly")
-def test_tp_pipelined_arrivals_mid_decode_on_one_gpu():
-    """Prompts arriving while 62 sequences decode in the pipelined TP engine
-    (separate steps: the pipeline drains, the prefill runs, decode resumes)."""
-    _run_tp(2, True, 64, 0, True)
+@pytest.mark.parametrize("pipeline,mixed", [(True, 0), (False, 256)])
+def test_tp_arrivals_mid_decode_on_one_gpu(pipeline, mixed):
+    """Prompts arriving while 62 sequences decode: (pipelined, separate steps)
+    -- the pipeline drains, the prefill runs, decode resumes; (synchronous,
+    mixed) -- TP mixed steps without the pipelined decode graphs."""
+    _run_tp(2, pipeline, 64, mixed, True)
 # (2, True, 64, 256) -- TP mixed steps in the pipelined engine -- faulted the GPU inside a
 # decode graph replay after a synchronous mixed step (profiles/r4/multirank/
 # tp_mixed_fault_r4_12.log); TP mixed steps stay opt-in (EngineConfig.tp_mixed) and are

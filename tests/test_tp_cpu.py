@@ -21,9 +21,10 @@ PROMPTS = [list(range(5, 70)), list(range(100, 130)), list(range(7, 200, 3))]
 
 
 def _cfg(tp, model="tiny-llama", **kw):
+    kw.setdefault("use_graphs", False)
     return EngineConfig(model=model, device="cpu", dtype="float32", tp=tp, num_blocks=64,
                         block_size=32, max_batch=8, max_model_len=1024, max_prefill_tokens=64,
-                        use_graphs=False, **kw)
+                        **kw)
 
 
 def _generate_mixed(eng):
@@ -154,6 +155,65 @@ def test_tp2_mixed_steps_match_single_rank():
     assert status == "ok", res
     outs, mixed = res
     assert mixed >= 2 and outs == ref
+
+
+def _sim_run(eng):
+    p = SamplingParams(temperature=0, max_tokens=10, ignore_eos=True)
+    fill = [eng.add_request(list(range(3 + i, 20 + i)), p) for i in range(4)]
+    for _ in range(4):
+        eng.step()
+    seqs = [eng.add_request(pr, p) for pr in PROMPTS]
+    eng.run_until_done()
+    return [s.output for s in fill + seqs]
+
+
+def _sim_worker(rank, world, port, q, mixed):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), OMNIA_SIM_GRAPHS="1")
+    try:
+        from omnia_amd.engine import tp
+        from omnia_amd.parallel import state as pstate
+        w = shard_weights(_full_weights(), resolve("tiny-llama"), world, rank)
+        pstate.init_distributed(tp_size=world, backend="gloo", device="cpu")
+        eng = tp.start(_cfg(world, use_graphs=True, pipeline=True, mixed_budget=mixed,
+                            tp_mixed=bool(mixed)), weights=w)
+        if eng is None:
+            return
+        assert eng.runner.use_graphs and eng.runner.sim
+        outs = _sim_run(eng)
+        q.put(("ok", (outs, dict(eng.counters), eng.runner.stats.get("graph_replays", 0))))
+        eng.shutdown()
+    except Exception:
+        import traceback
+        q.put(("err", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("mixed", [0, 48])
+def test_tp2_pipelined_graph_loop_simulated(mixed):
+    """The pipelined decode loop (device token slots, placeholders, speculative
+    step, graph buckets) on the CPU via OMNIA_SIM_GRAPHS, under TP=2 with
+    prompts arriving while four sequences decode -- with separate and with
+    mixed steps: tokens equal a synchronous single-rank engine."""
+    ref = _sim_run(LLMEngine(_cfg(1, use_graphs=False, pipeline=False, mixed_budget=mixed),
+                             weights=_full_weights()))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sim_worker, args=(r, 2, port, q, mixed)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        status, res = q.get(timeout=300)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert status == "ok", res
+    outs, counters, replays = res
+    assert replays > 0 and outs == ref
+    if mixed:
+        assert counters.get("steps_mixed", 0) >= 2
 
 
 def test_shm_ring_flow_control(tmp_path):

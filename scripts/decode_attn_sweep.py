@@ -1,0 +1,59 @@
+"""Decode attention sweep at the WS bench's decode shape (Llama-3-8B, 256
+sequences, one query each, 32 q / 8 kv heads, 32-token pages, contexts
+513..640): kernel time and KV stream rate per partition size, with the
+partition-merge kernel included.
+
+    python scripts/decode_attn_sweep.py
+"""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from omnia_amd import ops  # noqa: E402
+
+
+def main():
+    torch.manual_seed(0)
+    dev = "cuda"
+    B, hq, hkv, D, BS = 256, 32, 8, 128, 32
+    max_len = 1024
+    mb = max_len // BS
+    nblk = B * mb + 8
+    kc = torch.randn(nblk, hkv, BS, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(nblk, hkv, BS, D, device=dev, dtype=torch.bfloat16)
+    perm = torch.randperm(nblk - 8, device=dev)[:B * mb].to(torch.int32)
+    bt = perm.view(B, mb).contiguous()
+    q = torch.randn(B, hq, D, device=dev, dtype=torch.bfloat16)
+    scale = D ** -0.5
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    print(f"{'len':>5} {'part':>5} {'us':>8} {'TB/s':>6}  err", flush=True)
+    for L in (520, 576, 640):
+        sl = torch.full((B,), L, dtype=torch.int32, device=dev)
+        ref = None
+        for part in (128, 192, 256, 320, 384, 512, 640, 1024):
+            ws = ops.decode_workspace(B, hq, mb, BS, part, dev)
+            out = ops.decode_attention(q, kc, vc, bt, sl, scale, part_size=part, workspace=ws)
+            if ref is None:
+                ref = out.float().clone()
+            err = (out.float() - ref).abs().max().item()
+            ts = []
+            for _ in range(30):
+                flush.zero_()  # evict the KV pages from L2 / MALL
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ops.decode_attention(q, kc, vc, bt, sl, scale, part_size=part, workspace=ws,
+                                     out=out)
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e3)
+            ts.sort()
+            us = ts[len(ts) // 2]
+            nbytes = B * L * hkv * D * 2 * 2
+            print(f"{L:5d} {part:5d} {us:8.1f} {nbytes / us / 1e6:6.2f}  {err:.2e}", flush=True)
+    time.sleep(0.1)
+
+
+if __name__ == "__main__":
+    main()

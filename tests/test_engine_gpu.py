@@ -166,5 +166,8 @@ def test_prefill_tokens_feed_next_decode_without_drain():
     e.step()  # launches decode straight away; collects the prefill
     assert e.inflight is not None and e.inflight.kind == "decode"
     e.run_until_done()
-    ref = [eng(use_graphs=False).generate([s.prompt], p)[0].output for s in seqs]
+    # the reference prefills the same 435-row chunk (fused prefill GEMMs from
+    # 257 rows): single-prompt chunks take another GEMM path, whose bf16
+    # rounding flips near-tied greedy picks of the random model
+    ref = [s.output for s in eng(use_graphs=False).generate([s.prompt for s in seqs], p)]
     assert [s.output for s in seqs] == ref

@@ -1,7 +1,9 @@
 """Decode attention sweep at the WS bench's decode shape (Llama-3-8B, 256
 sequences, one query each, 32 q / 8 kv heads, 32-token pages, contexts
 513..640): kernel time and KV stream rate per partition size, with the
-partition-merge kernel included.
+partition-merge kernel included.  The K+V stream (>= 545 MB) exceeds the
+256 MB Infinity Cache, so back-to-back runs read HBM (no flush kernel: its
+dirty lines would be written back under the measured kernel).
 
     python scripts/decode_attn_sweep.py
 """
@@ -27,7 +29,6 @@ def main():
     bt = perm.view(B, mb).contiguous()
     q = torch.randn(B, hq, D, device=dev, dtype=torch.bfloat16)
     scale = D ** -0.5
-    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
     print(f"{'len':>5} {'part':>5} {'us':>8} {'TB/s':>6}  err", flush=True)
     for L in (520, 576, 640):
         sl = torch.full((B,), L, dtype=torch.int32, device=dev)
@@ -40,7 +41,6 @@ def main():
             err = (out.float() - ref).abs().max().item()
             ts = []
             for _ in range(30):
-                flush.zero_()  # evict the KV pages from L2 / MALL
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 ops.decode_attention(q, kc, vc, bt, sl, scale, part_size=part, workspace=ws,

@@ -468,6 +468,22 @@ def _dump_profiles(prof, drv):
     time.sleep(3.0)  # let them write
 
 
+def _tree_cpu_s() -> float:
+    """CPU seconds (user + system) used so far by this rank's process tree: the
+    bench client and its agent pod (facade, runtime, engine-core)."""
+    import psutil
+
+    me = psutil.Process()
+    tot = 0.0
+    for p in [me] + me.children(recursive=True):
+        try:
+            t = p.cpu_times()
+            tot += t.user + t.system
+        except psutil.Error:
+            pass
+    return tot
+
+
 def run(a, drv, ws, rank, use_gpu, host_only):
     import torch
     import torch.distributed as dist
@@ -483,6 +499,7 @@ def run(a, drv, ws, rank, use_gpu, host_only):
     if isinstance(drv, LocalDriver):
         drv.reset_timing()
     sync()
+    cpu0 = _tree_cpu_s()
     t0 = time.perf_counter()
     results = []
     wave_ms = []  # this rank's per-wave wall time (closed loop)
@@ -498,6 +515,9 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             wave_ms.append(round(1000 * (time.perf_counter() - tw), 1))
     sync()
     elapsed = time.perf_counter() - t0
+    # host cores this replica's serving path kept busy (client included): the
+    # CPU a node must supply per replica at this rate
+    cores = (_tree_cpu_s() - cpu0) / elapsed if elapsed > 0 else 0.0
     if a.arrival != "poisson" and prof is not None:
         _dump_profiles(prof, drv)
 
@@ -528,14 +548,17 @@ def run(a, drv, ws, rank, use_gpu, host_only):
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed, out_tokens = float(mx[0]), float(sm[1])
         gathered = [None] * ws
-        dist.all_gather_object(gathered, (ttfts, lats, tpot, gaps[:20000], round(my_rate, 2)))
+        dist.all_gather_object(gathered, (ttfts, lats, tpot, gaps[:20000], round(my_rate, 2),
+                                          round(cores, 2)))
         ttfts = [x for g in gathered for x in g[0]]
         lats = [x for g in gathered for x in g[1]]
         tpot = [x for g in gathered for x in g[2]]
         gaps = [x for g in gathered for x in g[3]]
         per_rank = [g[4] for g in gathered]
+        cores_rank = [g[5] for g in gathered]
     else:
         per_rank = [round(my_rate, 2)]
+        cores_rank = [round(cores, 2)]
     value = out_tokens / elapsed
     st = drv.engine_stats() if isinstance(drv, LocalDriver) else None
     if rank == 0:
@@ -559,6 +582,7 @@ def run(a, drv, ws, rank, use_gpu, host_only):
                     "engine (engine/synthetic.py), no GPU compute",
             "world_size": ws,
             "per_rank_tokens_per_s": per_rank,
+            "host_cpu_cores_per_rank": cores_rank,
             "p50_turn_latency_ms": ms(statistics.median(lats)) if lats else None,
             "p95_turn_latency_ms": ms(pct(lats, 0.95)),
             "p50_ttft_ms": ms(statistics.median(ttfts)) if ttfts else None,

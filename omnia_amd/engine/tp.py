@@ -51,6 +51,20 @@ from .model_runner import ModelRunner
 
 log = logging.getLogger("omnia.engine.tp")
 
+# OMNIA_TP_TRACE=1: every command rank 0 publishes and every worker receives is
+# logged (flushed) to stderr with a timestamp -- after a device fault, the last
+# line of each rank names the step it was in
+_TRACE = os.environ.get("OMNIA_TP_TRACE") == "1"
+
+
+def _trace(what: str, cmd: int, vals) -> None:
+    import sys
+
+    names = ("STOP", "PREFILL", "DECODE", "EAGER", "SWAP_OUT", "SWAP_IN", "SWAP_DROP", "MIXED")
+    sys.stderr.write(f"[tp {os.getpid()} {time.monotonic():.4f}] {what} "
+                     f"{names[cmd] if 0 <= cmd < len(names) else cmd} {list(vals)}\n")
+    sys.stderr.flush()
+
 STOP, PREFILL, DECODE, EAGER, SWAP_OUT, SWAP_IN, SWAP_DROP, MIXED = range(8)
 HDR = 16
 
@@ -220,6 +234,8 @@ class TPChannel:
             os.unlink(path[0])  # the mappings stay valid; nothing is left in /dev/shm
 
     def send(self, cmd: int, *vals, payload=None):
+        if _TRACE:
+            _trace("send", cmd, vals)
         if isinstance(payload, torch.Tensor):
             payload = payload.numpy() if payload.device.type == "cpu" else \
                 payload.cpu().numpy()
@@ -293,6 +309,8 @@ class TPWorker(ModelRunner):
         while True:
             h, body = self.chan.recv()
             cmd = h[0]
+            if _TRACE:
+                _trace("recv", cmd, h[1:10])
             if cmd == STOP:
                 self.chan.release()
                 return

@@ -73,7 +73,11 @@ def tp_sample(local_logits: torch.Tensor, vocab_start: int, temperature: torch.T
     K = min(K, Vl)
     pad = (-(2 * K + 2)) % 4  # 16-byte rows for the IPC all-gather
     pack = torch.zeros(B, 2 * K + 2 + pad, dtype=torch.float32, device=local_logits.device)
-    cv, ci = torch.topk(local_logits, K, dim=1)
+    # top-K on an fp32 copy, as in round 3.  The TP=2 batch-8 engine test passes at
+    # the round-3 commit and faults the GPU at 3e98ee9; torch.topk straight on the
+    # bf16 slice is the device-side change between them on that test's path (the
+    # fault only came with decode buckets of 2..32 rows; batch 1 and 64 ran)
+    cv, ci = torch.topk(local_logits.float(), K, dim=1)
     pack[:, :K] = cv
     pack[:, K:2 * K] = ci + vocab_start
     if (local_logits.is_cuda and local_logits.dtype == torch.bfloat16 and seeds is not None

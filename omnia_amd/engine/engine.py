@@ -384,7 +384,10 @@ class LLMEngine:
         sch = self.scheduler
         h0 = self.inflight
         if h0 is not None:
-            if h0.kind in ("decode", "mixed") and not self._steady():
+            if (h0.kind in ("decode", "mixed") and not self._steady()) or \
+                    self.blocks.num_available < len(sch.running) + 1:
+                # the next step may preempt: nothing of a sequence it could pick
+                # (pages being written, a token not yet collected) may be in flight
                 self.timing["pipeline_breaks"] += 1
                 return self._flush_inflight()
             if h0.kind == "prefill" and not self.handoff and not (sch.waiting or sch.partial):

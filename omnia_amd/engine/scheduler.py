@@ -143,10 +143,16 @@ class Scheduler:
         s.prefix_hit = n
 
     def _preempt_one(self, protect: Sequence | None = None) -> bool:
-        for victim in reversed(self.running):
+        """Free the youngest page holder: a partially prefilled prompt first (the
+        newest admissions; they would otherwise keep their pages while a running
+        sequence is cut off at the pool limit), else the youngest running one."""
+        for victim in list(reversed(self.partial)) + list(reversed(self.running)):
             if victim is protect:
                 continue
-            self.running.remove(victim)
+            if victim in self.partial:
+                self.partial.remove(victim)
+            else:
+                self.running.remove(victim)
             self.blocks.release(victim.blocks)
             victim.blocks = []
             victim.num_cached = 0

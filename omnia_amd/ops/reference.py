@@ -58,7 +58,12 @@ def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) 
 
 
 def write_kv(k_cache, v_cache, k, v, slots):
-    """k/v: [T, Hkv, D]; caches [NB, Hkv, BS, D]."""
+    """k/v: [T, Hkv, D]; caches [NB, Hkv, BS, D].  Rows with a negative slot
+    (padded graph rows) write nothing -- as in the HIP kernels; a -1 would
+    otherwise index the LAST page from the end."""
+    keep = slots >= 0
+    if not bool(keep.all()):
+        k, v, slots = k[keep], v[keep], slots[keep]
     bs = k_cache.shape[2]
     blk = (slots // bs).long()
     off = (slots % bs).long()

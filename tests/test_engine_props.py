@@ -93,3 +93,26 @@ def test_engine_matches_single_requests(reqs, max_batch, max_prefill, mixed, num
         at, prompt, mt = plan[i]
         assert len(s.output) == mt
         assert tuple(s.output) == _alone(prompt, mt), (i, e.counters)
+
+
+TURN = st.tuples(st.sampled_from(["s0", "s1", "s2"]), st.integers(1, 30), st.integers(1, 6))
+
+
+@given(st.lists(TURN, min_size=1, max_size=6), st.integers(14, 40), st.booleans(),
+       st.sampled_from([0, 24]))
+@settings(max_examples=20, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+def test_multi_turn_sessions_match_stateless_generation(turns, num_blocks, sim, mixed):
+    """Session KV reuse (prefix hits, parked pages, LRU eviction under a small
+    pool): turn k of a session -- history + its reply + a new message -- equals
+    generating that whole prompt with no cache."""
+    e = _engine(sim, num_blocks=num_blocks, max_batch=3, max_prefill_tokens=32,
+                mixed_budget=mixed)
+    hist: dict = {}
+    p = lambda n: SamplingParams(temperature=0, max_tokens=n, ignore_eos=True)  # noqa: E731
+    for k, (sid, nmsg, gen) in enumerate(turns):
+        prompt = hist.get(sid, []) + [(11 * k + j) % 180 + 20 for j in range(nmsg)]
+        if len(prompt) + gen > min(250, (num_blocks - 1) * 8):
+            continue  # larger than the whole pool: that turn cannot run at all
+        s = e.generate([prompt], p(gen), session_ids=[sid])[0]
+        assert tuple(s.output) == _alone(tuple(prompt), gen), (k, sid, s.prefix_hit)
+        hist[sid] = prompt + s.output

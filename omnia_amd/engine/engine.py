@@ -158,7 +158,7 @@ class LLMEngine:
                                  max_model_len=cfg.max_model_len, use_graphs=cfg.use_graphs,
                                  max_prefill_tokens=cfg.max_prefill_tokens)
         swap = None
-        if cfg.swap_gib > 0 and dev.type == "cuda":
+        if cfg.swap_gib > 0:  # (on the CPU the "host" tier is a second copy: tests)
             swap = SwapSpace(self.kv, cfg.swap_gib)
             if st.tp_size > 1:
                 from .tp import TPSwapProxy

@@ -99,14 +99,15 @@ TURN = st.tuples(st.sampled_from(["s0", "s1", "s2"]), st.integers(1, 30), st.int
 
 
 @given(st.lists(TURN, min_size=1, max_size=6), st.integers(14, 40), st.booleans(),
-       st.sampled_from([0, 24]))
+       st.sampled_from([0, 24]), st.sampled_from([0.0, 0.0004]))
 @settings(max_examples=20, deadline=None, suppress_health_check=[HealthCheck.too_slow])
-def test_multi_turn_sessions_match_stateless_generation(turns, num_blocks, sim, mixed):
+def test_multi_turn_sessions_match_stateless_generation(turns, num_blocks, sim, mixed, swap):
     """Session KV reuse (prefix hits, parked pages, LRU eviction under a small
-    pool): turn k of a session -- history + its reply + a new message -- equals
-    generating that whole prompt with no cache."""
+    pool, the host swap tier holding a few evicted pages): turn k of a session
+    -- history + its reply + a new message -- equals generating that whole
+    prompt with no cache."""
     e = _engine(sim, num_blocks=num_blocks, max_batch=3, max_prefill_tokens=32,
-                mixed_budget=mixed)
+                mixed_budget=mixed, swap_gib=swap)
     hist: dict = {}
     p = lambda n: SamplingParams(temperature=0, max_tokens=n, ignore_eos=True)  # noqa: E731
     for k, (sid, nmsg, gen) in enumerate(turns):

@@ -385,10 +385,23 @@ class TieredSessionService:
         self.publisher = publisher  # async publish(namespace, event_dict)
         self.lock = threading.Lock()
         self.degraded_reads = 0
+        # sessions whose hot copy may be stale: a write reached the warm tier while
+        # the hot tier was unavailable; reads bypass the hot copy until refreshed
+        self._stale: set = set()
         # ee/encryption.Encryptor when a SessionPrivacyPolicy enables encryption at
         # rest: message content / metadata are sealed before the warm tier and
         # opened on the way out (the hot cache holds plaintext in process memory)
         self.encryptor = None
+
+    def _hot_put(self, s: Session, msgs: list | None = None, append: Message | None = None):
+        """Write-through to the hot tier; a failure marks the session's hot copy
+        stale (the warm tier, the source of truth, already has the write)."""
+        try:
+            self.hot.put(s, msgs)
+            if append is not None:
+                self.hot.append(s.id, append)
+        except TierError:
+            self._stale.add(s.id)
 
     # ------------------------------------------------------------ encryption
     def _seal(self, m: Message) -> Message:
@@ -446,10 +459,7 @@ class TieredSessionService:
         if existing is not None:
             return existing  # idempotent ensure (facade EnsureSessionRecord)
         self.warm.put_session(s)
-        try:
-            self.hot.put(s, [])
-        except TierError:
-            pass
+        self._hot_put(s, [])
         return s
 
     async def append_message(self, sid: str, m: Message) -> Message:
@@ -468,11 +478,7 @@ class TieredSessionService:
                 s.last_message_preview = m.content[:120]
         self.warm.add_message(sid, self._seal(m))
         self.warm.put_session(s)
-        try:
-            self.hot.put(s)
-            self.hot.append(sid, m)
-        except TierError:
-            pass
+        self._hot_put(s, append=m)
         if self.publisher is not None:
             await self.publisher({"type": "message.appended", "sessionId": sid,
                                   "namespace": s.namespace, "agentName": s.agent_name,
@@ -491,10 +497,7 @@ class TieredSessionService:
             s.tool_call_count += 1
             s.updated_at = time.time()
             self.warm.put_session(s)
-            try:
-                self.hot.put(s)
-            except TierError:
-                pass
+            self._hot_put(s)
 
     def _event(self, typ: str, s: Session) -> dict:
         return {"type": typ, "sessionId": s.id, "namespace": s.namespace,
@@ -530,10 +533,7 @@ class TieredSessionService:
             s.ended_at = ended_at or time.time()
         s.updated_at = time.time()
         self.warm.put_session(s)
-        try:
-            self.hot.put(s)
-        except TierError:
-            pass
+        self._hot_put(s)
         return s
 
     def refresh_ttl(self, sid: str, ttl_s: float) -> Session:
@@ -542,10 +542,7 @@ class TieredSessionService:
             raise KeyError(sid)
         s.expires_at = time.time() + ttl_s
         self.warm.put_session(s)
-        try:
-            self.hot.put(s)
-        except TierError:
-            pass
+        self._hot_put(s)
         return s
 
     def decorate(self, sid: str, tags=None, state=None) -> Session:
@@ -557,26 +554,25 @@ class TieredSessionService:
         if state:
             s.state.update(state)
         self.warm.put_session(s)
-        try:
-            self.hot.put(s)
-        except TierError:
-            pass
+        self._hot_put(s)
         return s
 
     def delete(self, sid: str) -> bool:
         self.hot.invalidate(sid)
+        self._stale.discard(sid)
         a = self.warm.delete_session(sid)
         b = self.cold.delete_session(sid) if self.cold else False
         return a or b
 
     # ------------------------------------------------------------ reads
     def _get_session_only(self, sid: str) -> Session | None:
-        try:
-            v = self.hot.get(sid)
-            if v is not None:
-                return v[0]
-        except TierError:
-            self.degraded_reads += 1
+        if sid not in self._stale:
+            try:
+                v = self.hot.get(sid)
+                if v is not None:
+                    return v[0]
+            except TierError:
+                self.degraded_reads += 1
         return self.warm.get_session(sid)
 
     def get(self, sid: str, with_messages: bool = True):
@@ -586,12 +582,15 @@ class TieredSessionService:
         if warm errored and cold has nothing, the read fails (TierError) rather
         than reporting "not found"."""
         warm_err = None
-        try:
-            v = self.hot.get(sid)
-            if v is not None and (not with_messages or v[1] or v[0].message_count == 0):
-                return v
-        except TierError:
-            self.degraded_reads += 1
+        if sid not in self._stale:
+            try:
+                v = self.hot.get(sid)
+                # the hot copy keeps the last max_messages: it answers only when it
+                # holds the whole history
+                if v is not None and (not with_messages or len(v[1]) == v[0].message_count):
+                    return v
+            except TierError:
+                self.degraded_reads += 1
         try:
             s = self.warm.get_session(sid)
             if s is not None:
@@ -599,6 +598,7 @@ class TieredSessionService:
                     else []
                 try:
                     self.hot.put(s, msgs)
+                    self._stale.discard(sid)
                 except TierError:
                     pass
                 return s, msgs

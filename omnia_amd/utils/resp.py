@@ -133,7 +133,12 @@ class RedisClient:
             try:
                 await self._conn()
                 return await self._raw(*args)
-            except (ConnectionError, OSError, asyncio.IncompleteReadError):
+            except RedisError:
+                raise  # a complete error reply: the connection stays in sync
+            except BaseException:
+                # connection lost, or a timeout / cancellation with the reply still
+                # outstanding: that late reply would answer the NEXT command on this
+                # connection, so drop it (the next command reconnects)
                 self.close()
                 raise
 

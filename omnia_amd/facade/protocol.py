@@ -129,10 +129,40 @@ def tool_call(session_id: str, call_id: str, name: str, arguments: dict,
     return server_msg(TOOL_CALL, session_id, tool_call=tc)
 
 
+# field -> accepted JSON types of a client message (null = absent); anything else
+# is an invalid message (E_INVALID_MESSAGE), never an exception in the handlers
+_CLIENT_FIELDS = {"session_id": (str,), "content": (str,), "metadata": (dict,),
+                  "consent_grants": (list,), "parts": (list,), "tool_result": (dict,),
+                  "tool_call_ack": (dict,), "tool_call_nack": (dict,),
+                  "upload_request": (dict,)}
+_PART_FIELDS = {"type": (str,), "text": (str,), "media": (dict,), "media_id": (str,),
+                "mime_type": (str,), "url": (str,), "data": (str,)}
+
+
 def parse_client(raw: str | bytes) -> dict:
-    m = json.loads(raw)
+    try:
+        m = json.loads(raw)
+    except RecursionError as e:  # pathologically nested JSON
+        raise ValueError("message nested too deeply") from e
     if not isinstance(m, dict) or m.get("type") not in CLIENT_TYPES:
         raise ValueError("unknown or missing message type")
+    for k, types in _CLIENT_FIELDS.items():
+        v = m.get(k)
+        if v is not None and not isinstance(v, types):
+            raise ValueError(f"field {k!r} must be {types[0].__name__}")
+    for p in m.get("parts") or ():
+        if not isinstance(p, dict):
+            raise ValueError("message parts must be objects")
+        for k, types in _PART_FIELDS.items():
+            v = p.get(k)
+            if v is not None and not isinstance(v, types):
+                raise ValueError(f"part field {k!r} must be {types[0].__name__}")
+        for k in ("data", "url", "mime_type", "storage_ref"):
+            v = (p.get("media") or {}).get(k)
+            if v is not None and not isinstance(v, str):
+                raise ValueError(f"media field {k!r} must be str")
+    if not all(isinstance(g, str) for g in m.get("consent_grants") or ()):
+        raise ValueError("consent_grants must be strings")
     return m
 
 

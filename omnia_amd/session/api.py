@@ -77,6 +77,40 @@ def session_resolver(svc: TieredSessionService, cache_size: int = 10000):
     return resolve
 
 
+def _bad(msg: str):
+    return web.HTTPBadRequest(text=json.dumps({"error": msg}), content_type="application/json")
+
+
+async def _json_obj(request) -> dict:
+    """The request body as a JSON object, or 400."""
+    try:
+        body = await request.json()
+    except (ValueError, UnicodeDecodeError) as e:
+        raise _bad(f"invalid JSON body: {e}") from None
+    if not isinstance(body, dict):
+        raise _bad("request body must be a JSON object")
+    return body
+
+
+def _num(v, kind, name: str):
+    """``kind(v)`` for a query / body field, or 400 (finite values only)."""
+    try:
+        x = kind(v)
+    except (TypeError, ValueError, OverflowError):
+        raise _bad(f"{name} must be a number") from None
+    if kind is float and (x != x or x in (float("inf"), float("-inf"))):
+        raise _bad(f"{name} must be finite")
+    return x
+
+
+def _model(cls, d):
+    """``cls.from_json(d)`` with a wrongly typed field answered as 400."""
+    try:
+        return cls.from_json(d)
+    except (ValueError, TypeError) as e:
+        raise _bad(str(e)) from None
+
+
 def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400.0,
               tokens: dict | None = None, allowed_namespaces: set | None = None,
               redactor=None, optout=None, audit_logger=None, media_deleter=None,
@@ -139,8 +173,8 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         return web.json_response({"status": "ok"})
 
     async def create(request):
-        body = await request.json()
-        s = Session.from_json(body)
+        body = await _json_obj(request)
+        s = _model(Session, body)
         if optout is not None and optout(s):
             return web.Response(status=204)
         s = svc.create(s)
@@ -152,17 +186,17 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         q = request.query
         rows = svc.warm.list_sessions(namespace=q.get("namespace"), agent=q.get("agent"),
                                       status=q.get("status"), user=q.get("user"),
-                                      before=float(q["before"]) if q.get("before") else None,
-                                      after=float(q["after"]) if q.get("after") else None,
-                                      limit=int(q.get("limit", 100)),
-                                      offset=int(q.get("offset", 0)), q=q.get("q"))
+                                      before=_num(q["before"], float, "before") if q.get("before") else None,
+                                      after=_num(q["after"], float, "after") if q.get("after") else None,
+                                      limit=_num(q.get("limit", 100), int, "limit"),
+                                      offset=_num(q.get("offset", 0), int, "offset"), q=q.get("q"))
         return web.json_response({"sessions": [s.to_json() for s in rows],
                                   "total": len(rows)})
 
     async def search(request):
         q = request.query
         rows = svc.warm.list_sessions(namespace=q.get("namespace"), agent=q.get("agent"),
-                                      q=q.get("q", ""), limit=int(q.get("limit", 50)))
+                                      q=q.get("q", ""), limit=_num(q.get("limit", 50), int, "limit"))
         audit(request, "session_searched", query=q.get("q", ""), resultCount=len(rows),
               namespace=q.get("namespace") or "")
         return web.json_response({"sessions": [s.to_json() for s in rows]})
@@ -187,14 +221,14 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         if v is None:
             return nf(sid)
         msgs = v[1]
-        lim = int(request.query.get("limit", 1000))
-        off = int(request.query.get("offset", 0))
+        lim = _num(request.query.get("limit", 1000), int, "limit")
+        off = _num(request.query.get("offset", 0), int, "offset")
         return web.json_response({"messages": [m.to_json() for m in msgs[off:off + lim]]})
 
     async def append(request):
         sid = request.match_info["id"]
-        body = await request.json()
-        m = Message.from_json(body)
+        body = await _json_obj(request)
+        m = _model(Message, body)
         if redactor is not None:
             m.content = redactor(m.content)
         try:
@@ -206,8 +240,8 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
     def recorder(table, cls):
         async def post(request):
             sid = request.match_info["id"]
-            body = await request.json()
-            obj = cls.from_json({**body, "sessionId": sid})
+            body = await _json_obj(request)
+            obj = _model(cls, {**body, "sessionId": sid})
             try:
                 svc.record(table, sid, obj)
             except KeyError:
@@ -221,11 +255,11 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         return post, get_
 
     async def eval_results_post(request):
-        body = await request.json()
+        body = await _json_obj(request)
         items = body if isinstance(body, list) else body.get("results", [body])
         out = []
         for it in items:
-            e = EvalResult.from_json(it)
+            e = _model(EvalResult, it)
             try:
                 svc.record("eval_results", e.session_id, e)
             except KeyError:
@@ -240,8 +274,8 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         if qs.get("passed") not in (None, ""):
             passed = qs["passed"].lower() in ("1", "true", "yes")
         try:
-            limit = max(1, min(1000, int(qs.get("limit", 100))))
-            offset = max(0, int(qs.get("offset", 0)))
+            limit = max(1, min(1000, _num(qs.get("limit", 100), int, "limit")))
+            offset = max(0, _num(qs.get("offset", 0), int, "offset"))
         except ValueError:
             return web.json_response({"error": "invalid limit/offset"}, status=400)
         rows = svc.warm.list_eval_results(passed, qs.get("evalId") or None, limit, offset)
@@ -264,22 +298,26 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
             request.query.get("namespace"), request.query.get("groupBy", "model"))})
 
     async def provider_usage(request):
-        body = await request.json()
-        svc.warm.provider_usage(body.get("workspace", ""), body)
+        body = await _json_obj(request)
+        ws = body.get("workspace") or ""
+        if not isinstance(ws, str):
+            raise _bad("workspace must be a string")
+        svc.warm.provider_usage(ws, body)
         return web.json_response({"ok": True}, status=201)
 
     async def ttl(request):
         sid = request.match_info["id"]
-        body = await request.json()
+        body = await _json_obj(request)
         try:
-            s = svc.refresh_ttl(sid, float(body.get("ttlSeconds", svc.default_ttl_s)))
+            s = svc.refresh_ttl(sid, _num(body.get("ttlSeconds", svc.default_ttl_s), float,
+                                         "ttlSeconds"))
         except KeyError:
             return nf(sid)
         return web.json_response(s.to_json())
 
     async def status(request):
         sid = request.match_info["id"]
-        body = await request.json()
+        body = await _json_obj(request)
         st = body.get("status", STATUS_ACTIVE)
         if st not in TERMINAL | {STATUS_ACTIVE}:
             return web.json_response({"error": "invalid_status"}, status=400)
@@ -306,7 +344,7 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
 
     async def decorate(request):
         sid = request.match_info["id"]
-        body = await request.json()
+        body = await _json_obj(request)
         try:
             s = svc.decorate(sid, body.get("tags"), body.get("state"))
         except KeyError:
@@ -324,7 +362,8 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         ns = request.query.get("namespace")
         if not ns:
             return web.json_response({"error": "namespace required"}, status=400)
-        before = float(request.query["before"]) if request.query.get("before") else None
+        before = _num(request.query["before"], float, "before") \
+            if request.query.get("before") else None
         rows = svc.warm.list_sessions(namespace=ns, agent=request.query.get("agent"),
                                       before=before, limit=100000)
         n = sum(1 for s in rows if svc.delete(s.id))
@@ -336,7 +375,7 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         optionally one workspace / a created-at range, and their media."""
         from ..ee.privacy.erasure import EraseScope, SessionTierEraser
 
-        body = await request.json()
+        body = await _json_obj(request)
         uid = body.get("virtual_user_id", "")
         if not uid:
             return web.json_response({"error": "virtual_user_id required"}, status=400)
@@ -370,7 +409,7 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         from .compaction import CompactionConfig, CompactionEngine
 
         try:
-            body = await request.json() if request.can_read_body else {}
+            body = await _json_obj(request) if request.can_read_body else {}
         except ValueError:
             return web.json_response({"error": "body must be JSON"}, status=400)
         ret = retention or {}

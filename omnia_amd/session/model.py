@@ -41,13 +41,43 @@ class _JSON:
 
     @classmethod
     def from_json(cls, d: dict):
-        names = {f.name for f in fields(cls)}
+        """Build from a JSON object; a field of the wrong JSON type raises
+        ValueError (an API answers 400), ``null`` means "absent"."""
+        if d is not None and not isinstance(d, dict):
+            raise ValueError(f"{cls.__name__} must be a JSON object")
+        ann = {f.name: f.type for f in fields(cls)}
         kw = {}
         for k, v in (d or {}).items():
-            sk = _snake(k) if _snake(k) in names else k
-            if sk in names:
+            sk = _snake(k) if _snake(k) in ann else k
+            if sk in ann and v is not None:
+                if not _json_type_ok(str(ann[sk]), v):
+                    raise ValueError(f"{cls.__name__}.{k}: expected {ann[sk]}")
                 kw[sk] = v
         return cls(**kw)
+
+
+_SCALARS = {"str": (str,), "int": (int,), "float": (int, float), "bool": (bool,),
+            "dict": (dict,), "list": (list,)}
+
+
+def _json_type_ok(ann: str, v) -> bool:
+    """Does JSON value ``v`` fit the (string) annotation ``ann``?  Unions and
+    unknown annotations accept anything they can; bool is not a number."""
+    ok = False
+    for part in ann.replace(" ", "").split("|"):
+        base = part.split("[", 1)[0]
+        if base == "None":
+            continue
+        types = _SCALARS.get(base)
+        if types is None:
+            return True  # an annotation this check does not model
+        if isinstance(v, bool) and bool not in types:
+            continue
+        if isinstance(v, types) or (base == "int" and isinstance(v, float) and v.is_integer()):
+            if base == "list" and "[str]" in part and not all(isinstance(x, str) for x in v):
+                continue
+            ok = True
+    return ok
 
 
 @dataclass

@@ -81,13 +81,13 @@ def _bad(msg: str):
     return web.HTTPBadRequest(text=json.dumps({"error": msg}), content_type="application/json")
 
 
-async def _json_obj(request) -> dict:
-    """The request body as a JSON object, or 400."""
+async def _json_obj(request, lists: bool = False):
+    """The request body as a JSON object (or, with ``lists``, an array), or 400."""
     try:
         body = await request.json()
     except (ValueError, UnicodeDecodeError) as e:
         raise _bad(f"invalid JSON body: {e}") from None
-    if not isinstance(body, dict):
+    if not isinstance(body, dict) and not (lists and isinstance(body, list)):
         raise _bad("request body must be a JSON object")
     return body
 
@@ -255,8 +255,10 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         return post, get_
 
     async def eval_results_post(request):
-        body = await _json_obj(request)
+        body = await _json_obj(request, lists=True)
         items = body if isinstance(body, list) else body.get("results", [body])
+        if not isinstance(items, list):
+            raise _bad("results must be an array")
         out = []
         for it in items:
             e = _model(EvalResult, it)

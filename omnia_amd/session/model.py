@@ -50,7 +50,10 @@ class _JSON:
         for k, v in (d or {}).items():
             sk = _snake(k) if _snake(k) in ann else k
             if sk in ann and v is not None:
-                if not _json_type_ok(str(ann[sk]), v):
+                # timestamps travel as epoch seconds or RFC 3339 strings (the
+                # reference's wire form): both are accepted as they are
+                stamp = sk.endswith("_at") or sk == "timestamp"
+                if not (stamp and isinstance(v, str)) and not _json_type_ok(str(ann[sk]), v):
                     raise ValueError(f"{cls.__name__}.{k}: expected {ann[sk]}")
                 kw[sk] = v
         return cls(**kw)

@@ -108,15 +108,32 @@ def build_app(engine, model_name: str, embedder=None) -> web.Application:
     async def chat(request):
         try:
             body = await request.json()
+            if not isinstance(body, dict):
+                raise TypeError("the request body must be a JSON object")
+            if not isinstance(body.get("messages"), list) or not all(
+                    isinstance(m, dict) for m in body["messages"]):
+                raise TypeError("messages must be an array of objects")
             msgs = _messages(body["messages"])
             params = _params(body)
+            n = body.get("n", 1)
+            tools = body.get("tools") or []
+            if not isinstance(tools, list) or not all(isinstance(t, dict) for t in tools):
+                raise TypeError("tools must be an array of objects")
+            tools = [t.get("function", t) for t in tools if body.get("tool_choice") != "none"]
+            if not all(isinstance(t, dict) and isinstance(t.get("name", ""), str)
+                       for t in tools):
+                raise TypeError("tool functions must be objects with a string name")
+            tool_names = {t["name"] for t in tools if "name" in t}
+            if not isinstance(body.get("stream_options") or {}, dict):
+                raise TypeError("stream_options must be an object")
+            if not isinstance(body.get("user") or "", str):
+                raise TypeError("user must be a string")
+            if isinstance(n, bool) or not isinstance(n, int):
+                raise TypeError("n must be an integer")
         except (KeyError, TypeError, ValueError, AttributeError) as e:
             return _err(400, f"bad request: {e}")
-        if int(body.get("n", 1)) != 1:
+        if n != 1:
             return _err(400, "only n=1 is supported")
-        tools = [t.get("function", t) for t in body.get("tools") or []
-                 if body.get("tool_choice") != "none"]
-        tool_names = {t["name"] for t in tools if "name" in t}
         if tools and params.guided:
             return _err(400, "response_format cannot be combined with tools")
         prompt = engine.tokenizer.encode(render_llama3(msgs, tools or None), add_bos=False)
@@ -217,11 +234,17 @@ def build_app(engine, model_name: str, embedder=None) -> web.Application:
     async def completions(request):
         try:
             body = await request.json()
+            if not isinstance(body, dict):
+                raise TypeError("the request body must be a JSON object")
             params = _params(body)
             p = body["prompt"]
+            if not isinstance(body.get("user") or "", str):
+                raise TypeError("user must be a string")
         except (KeyError, TypeError, ValueError, AttributeError) as e:
             return _err(400, f"bad request: {e}")
-        if isinstance(p, list) and p and isinstance(p[0], int):
+        vocab = getattr(engine.tokenizer, "vocab_size", None) or 1 << 31
+        if isinstance(p, list) and p and all(isinstance(t, int) and not isinstance(t, bool)
+                                             and 0 <= t < vocab for t in p):
             ids = p
         elif isinstance(p, str):
             ids = engine.tokenizer.encode(p, add_bos=True)
@@ -265,9 +288,11 @@ def build_app(engine, model_name: str, embedder=None) -> web.Application:
         try:
             body = await request.json()
             inp = body["input"]
-        except (KeyError, ValueError, json.JSONDecodeError) as e:
+        except (KeyError, TypeError, ValueError, json.JSONDecodeError) as e:
             return _err(400, f"bad request: {e}")
-        texts = [inp] if isinstance(inp, str) else list(inp)
+        texts = [inp] if isinstance(inp, str) else inp
+        if not isinstance(texts, list) or not texts or not all(isinstance(t, str) for t in texts):
+            return _err(400, "input must be a string or a non-empty array of strings")
         vecs = await emb.embed(texts)
         return web.json_response({"object": "list", "model": body.get("model", "embed"), "data": [
             {"object": "embedding", "index": i, "embedding": [float(x) for x in v]}

@@ -55,6 +55,22 @@ class SamplingParams:
             raise ValueError("max_tokens must be >= 1")
         if self.repetition_penalty <= 0:
             raise ValueError("repetition_penalty must be > 0")
+        for f in ("temperature", "top_p", "frequency_penalty", "presence_penalty",
+                  "repetition_penalty"):
+            v = getattr(self, f)
+            if v != v or v in (float("inf"), float("-inf")):
+                raise ValueError(f"{f} must be finite")
+        if self.seed is not None and (isinstance(self.seed, bool) or
+                                      not isinstance(self.seed, int)):
+            raise ValueError("seed must be an integer")
+        if not isinstance(self.stop, (list, tuple)) or not all(isinstance(x, str)
+                                                               for x in self.stop):
+            raise ValueError("stop must be a string or a list of strings")
+        if not isinstance(self.stop_token_ids, (list, tuple, set, frozenset)) or not all(
+                isinstance(x, int) for x in self.stop_token_ids):
+            raise ValueError("stop_token_ids must be integers")
+        if self.json_schema is not None and not isinstance(self.json_schema, dict):
+            raise ValueError("json_schema must be an object")
         return self
 
     @classmethod
@@ -88,5 +104,10 @@ class SamplingParams:
                 kw[f] = float(kw[f])
         for f in ("top_k", "max_tokens", "min_tokens"):
             if f in kw:
+                if isinstance(kw[f], float) and not kw[f].is_integer():
+                    raise ValueError(f"{f} must be an integer")
                 kw[f] = int(kw[f])
+        for f in ("ignore_eos", "json_object"):
+            if f in kw and not isinstance(kw[f], bool):
+                raise ValueError(f"{f} must be a boolean")
         return cls(**kw).validate()

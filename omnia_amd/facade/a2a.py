@@ -428,7 +428,12 @@ class A2AServer:
         except Exception:  # noqa: BLE001
             return web.json_response({"jsonrpc": "2.0", "id": None,
                                       "error": {"code": -32700, "message": "parse error"}})
+        if not isinstance(req, dict):
+            return web.json_response({"jsonrpc": "2.0", "id": None,
+                                      "error": {"code": -32600, "message": "invalid request"}})
         rid, method, params = req.get("id"), req.get("method"), req.get("params") or {}
+        if not isinstance(method, str):
+            method = None
 
         def ok(result):
             M.A2A_REQUESTS.labels(method or "?", "ok").inc()
@@ -453,6 +458,22 @@ class A2AServer:
             M.A2A_REQUESTS.labels(method, "ok").inc()
             return resp
 
+        # JSON-RPC invalid params: wrongly typed params / message / ids answer -32602
+        # instead of failing inside the handler
+        if not isinstance(params, dict):
+            return err(-32602, "params must be an object")
+        if not isinstance(params.get("id", ""), str):
+            return err(-32602, "params.id must be a string")
+        m0 = params.get("message")
+        if m0 is not None and (not isinstance(m0, dict) or not all(
+                isinstance(m0.get(k) or "", str) for k in ("taskId", "contextId", "messageId",
+                                                          "role")) or
+                not isinstance(m0.get("metadata") or {}, dict) or
+                not isinstance(m0.get("parts") or [], list) or
+                not all(isinstance(p, dict) and all(isinstance(p.get(k) or "", str)
+                                                    for k in ("text", "kind", "type"))
+                        for p in m0.get("parts") or [])):
+            return err(-32602, "params.message must be an A2A message object")
         if method in ("message/send", "tasks/send"):
             msg = params.get("message")
             if not msg:

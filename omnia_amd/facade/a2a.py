@@ -63,7 +63,11 @@ class _TaskStoreBase:
         return task
 
     async def set_state(self, task: dict, state: str, message: dict | None = None) -> dict:
-        cur = await self.get(task["id"]) or task
+        # validate against the STORED state (another replica may have canceled the
+        # task); a task the store no longer holds (evicted once terminal) stays gone
+        cur = await self.get(task["id"])
+        if cur is None:
+            raise TaskNotFound(task["id"])
         _check(cur["status"]["state"], state)
         task["status"] = {"state": state, "timestamp": time.time(),
                           **({"message": message} if message else {})}
@@ -482,6 +486,8 @@ class A2AServer:
                 return ok(await self._run(msg))
             except InvalidTransition as e:
                 return err(-32002, str(e))
+            except TaskNotFound as e:
+                return err(-32001, f"task {e} not found")
         if method in ("message/stream", "tasks/sendSubscribe"):
             msg = params.get("message")
             if not msg:

@@ -91,10 +91,56 @@ async def _body(request) -> dict:
     if not isinstance(d, dict):
         raise web.HTTPBadRequest(text=json.dumps({"error": "body must be an object"}),
                                  content_type="application/json")
+    for k, v in d.items():
+        t = _BODY_TYPES.get(k)
+        if v is None or t is None:
+            continue
+        ok = (isinstance(v, t) and not (isinstance(v, bool) and t is not bool)) if t in (
+            int, bool) else isinstance(v, t) and not (isinstance(v, bool) and t == (int, float))
+        if not ok:
+            raise web.HTTPBadRequest(text=json.dumps({"error": f"{k} has the wrong type"}),
+                                     content_type="application/json")
+        if isinstance(v, list) and k in _STR_LISTS and not all(isinstance(x, str) for x in v):
+            raise web.HTTPBadRequest(text=json.dumps({"error": f"{k} must be strings"}),
+                                     content_type="application/json")
     return d
 
 
+# JSON types of the body fields the handlers read (null = absent)
+_BODY_TYPES = {"scope": dict, "metadata": dict, "about": dict, "content": str, "query": str,
+               "text": str, "type": str, "title": str, "summary": str, "category": str,
+               "purpose": str, "relation_type": str, "source_id": str, "target_id": str,
+               "session_id": str, "workspace": str, "user_id": str, "agent_id": str, "id": str,
+               "ids": list, "source_ids": list, "types": list, "turn_range": list,
+               "documents": list, "limit": int, "weight": (int, float),
+               "confidence": (int, float), "min_confidence": (int, float), "granted": bool}
+_STR_LISTS = {"ids", "source_ids", "types"}
+
+
+_MEM_FIELDS = {"id": str, "type": str, "content": str, "metadata": dict, "category": str,
+               "about": dict, "session_id": str, "title": str, "summary": str,
+               "turn_range": list, "scope": dict}
+
+
+def _bad(msg: str):
+    return web.HTTPBadRequest(text=json.dumps({"error": msg}), content_type="application/json")
+
+
 def _memory_from_request(d: dict, scope: dict | None = None) -> Memory:
+    for k, t in _MEM_FIELDS.items():
+        v = d.get(k)
+        if v is not None and not isinstance(v, t):
+            raise _bad(f"{k} must be {'an object' if t is dict else 'a ' + t.__name__}")
+    c = d.get("confidence")
+    if c is not None and (isinstance(c, bool) or not isinstance(c, (int, float))
+                          or not 0.0 <= float(c) <= 1.0):
+        raise _bad("confidence must be a number in [0, 1]")
+    tr = d.get("turn_range")
+    if tr is not None and not all(isinstance(x, int) and not isinstance(x, bool) for x in tr):
+        raise _bad("turn_range must be integers")
+    ea = d.get("expires_at")
+    if ea is not None and not isinstance(ea, (str, int, float)) or isinstance(ea, bool):
+        raise _bad("expires_at must be a timestamp")
     meta = dict(d.get("metadata") or {})
     if d.get("category"):
         meta.setdefault(META_CONSENT_CATEGORY, d["category"])

@@ -40,12 +40,17 @@ class MCPServer:
         except Exception:  # noqa: BLE001
             return web.json_response({"jsonrpc": "2.0", "id": None,
                                       "error": {"code": -32700, "message": "parse error"}})
+        if not isinstance(req, dict):
+            return web.json_response({"jsonrpc": "2.0", "id": None,
+                                      "error": {"code": -32600, "message": "invalid request"}})
         method, rid, params = req.get("method"), req.get("id"), req.get("params") or {}
         if rid is None:  # notification
             return web.Response(status=202)
+        if not isinstance(method, str):
+            method = None
 
         def ok(result, headers=None):
-            M.MCP_REQUESTS.labels(method, "ok").inc()
+            M.MCP_REQUESTS.labels(method or "?", "ok").inc()
             return web.json_response({"jsonrpc": "2.0", "id": rid, "result": result},
                                      headers=headers)
 
@@ -66,6 +71,9 @@ class MCPServer:
         if method == "tools/list":
             return ok({"tools": self._tools()})
         if method == "tools/call":
+            if not isinstance(params, dict) or not isinstance(params.get("arguments") or {},
+                                                              dict):
+                return err(-32602, "params must be an object with object arguments")
             if params.get("name") != self.name:
                 return err(-32602, f"unknown tool {params.get('name')}")
             args = params.get("arguments") or {}

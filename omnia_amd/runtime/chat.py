@@ -107,15 +107,16 @@ def parse_tool_calls(text: str, tool_names: set[str]) -> tuple[str, list[ToolCal
         rest.append(body[i:j])
         try:
             obj, end = dec.raw_decode(body, j)
-        except json.JSONDecodeError:
+        except (json.JSONDecodeError, RecursionError):  # model output: garbage or deep nesting
             rest.append(body[j:])
             break
-        if isinstance(obj, dict) and obj.get("name") in tool_names:
+        name = obj.get("name") if isinstance(obj, dict) else None
+        if isinstance(name, str) and name in tool_names:
             args = obj.get("parameters", obj.get("arguments", {}))
             if isinstance(args, str):
                 try:
                     args = json.loads(args)
-                except json.JSONDecodeError:
+                except (json.JSONDecodeError, RecursionError):
                     args = {"input": args}
             calls.append(ToolCallReq(id="call_" + uuid.uuid4().hex[:12], name=obj["name"],
                                      arguments=args if isinstance(args, dict) else {}))

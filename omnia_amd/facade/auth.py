@@ -14,6 +14,7 @@ import base64
 import hashlib
 import hmac
 import json
+import math
 import time
 from dataclasses import dataclass, field
 
@@ -86,6 +87,13 @@ def jwt_decode(token: str, hs_key: bytes | None = None, jwks: dict | None = None
         sig = _b64url_dec(s64)
     except Exception as e:  # noqa: BLE001
         raise AuthError("malformed token") from e
+    if not isinstance(hdr, dict) or not isinstance(claims, dict):
+        raise AuthError("malformed token: header and claims must be JSON objects")
+    for c in ("exp", "nbf"):  # RFC 7519 NumericDate
+        v = claims.get(c)
+        if v is not None and (isinstance(v, bool) or not isinstance(v, (int, float))
+                              or not math.isfinite(v)):
+            raise AuthError(f"malformed token: {c} is not a number")
     alg = hdr.get("alg")
     signed = f"{h64}.{p64}".encode()
     if alg == "HS256":
@@ -108,9 +116,9 @@ def jwt_decode(token: str, hs_key: bytes | None = None, jwks: dict | None = None
     else:
         raise AuthError(f"unsupported alg {alg}")
     now = time.time()
-    if "exp" in claims and now > claims["exp"] + leeway:
+    if claims.get("exp") is not None and now > claims["exp"] + leeway:
         raise AuthError("token expired")
-    if "nbf" in claims and now + leeway < claims["nbf"]:
+    if claims.get("nbf") is not None and now + leeway < claims["nbf"]:
         raise AuthError("token not yet valid")
     if issuer and claims.get("iss") != issuer:
         raise AuthError("bad issuer")
@@ -317,10 +325,12 @@ class MgmtPlaneValidator:
             hdr = json.loads(_b64url_dec(tok.split(".")[0]))
         except Exception as e:  # noqa: BLE001
             raise AuthError("invalid credential: malformed header") from e
+        if not isinstance(hdr, dict):
+            raise AuthError("invalid credential: malformed header")
         if hdr.get("alg") != "RS256":
             raise AuthError(f"unexpected signing method {hdr.get('alg')!r}")
         kid = hdr.get("kid") or ""
-        if not kid:
+        if not isinstance(kid, str) or not kid:
             raise AuthError("mgmt-plane JWT missing kid header")
         key = self.resolver.resolve(kid)
         if key is None:

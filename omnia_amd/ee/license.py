@@ -249,14 +249,27 @@ class Validator:
             head = json.loads(_b64d(h))
         except Exception as e:  # noqa: BLE001
             raise LicenseError(f"malformed license token: {e}") from e
+        if not isinstance(head, dict):
+            raise LicenseError("malformed license token: header is not a JSON object")
         if head.get("alg") != "RS256":
             raise InvalidSignature(f"unexpected signing method {head.get('alg')!r}")
         if not rs256_verify(f"{h}.{b}".encode(), _b64d(s), *self.key):
             raise InvalidSignature("license signature invalid")
-        c = json.loads(_b64d(b))
         now = now or time.time()
+        try:
+            return self._claims(json.loads(_b64d(b)), now)
+        except LicenseError:
+            raise
+        except (ValueError, TypeError, AttributeError) as e:  # signed but ill-typed claims
+            raise LicenseError(f"malformed license claims: {e}") from e
+
+    @staticmethod
+    def _claims(c: dict, now: float) -> License:
         if "exp" in c and now > float(c["exp"]):
             raise LicenseExpired("license expired")
+        for f in ("lid", "tier", "customer"):
+            if not isinstance(c.get(f, ""), str):
+                raise TypeError(f"license claim {f} is not a string")
         feats = {f.name: bool((c.get("features") or {}).get(f.name, False))
                  for f in dataclasses.fields(Features)}
         lim = c.get("limits") or {}

@@ -83,3 +83,25 @@ def test_garbage_tokens(tok):
     _ok_or_auth_error(lambda: jwt_decode(tok, KEY))
     mg = MgmtPlaneValidator(JWKSResolver(jwks={"keys": []}))
     _ok_or_auth_error(lambda: mg.validate({"Authorization": "Bearer " + tok}, {}, "127.0.0.1"))
+
+
+@given(st.one_of(JSON, st.fixed_dictionaries(
+    {}, optional={"exp": JSON, "iat": JSON, "lid": JSON, "tier": JSON, "features": JSON,
+                  "limits": st.one_of(JSON, st.dictionaries(
+                      st.sampled_from(["maxScenarios", "maxWorkerReplicas"]), JSON))})),
+       st.sampled_from([{"alg": "RS256"}, None, [], "RS256"]))
+@settings(max_examples=200, deadline=None)
+def test_license_tokens_never_escape_get_or_default(claims, hdr):
+    """A license token signed with the right key but ill-typed claims (or a
+    non-object header) is a LicenseError, so ``get_or_default`` falls back to
+    open-core instead of raising (``ee/license.py`` promises it never raises)."""
+    from omnia_amd.ee import license as L
+
+    k = _rsa()
+    h = _b64(json.dumps(hdr).encode())
+    b = _b64(json.dumps(claims).encode())
+    tok = f"{h}.{b}.{_b64(L.rs256_sign(f'{h}.{b}'.encode(), k.n, k.d))}"
+    v = L.Validator(L.public_pem(k.n, k.e), secret_reader=lambda: tok)
+    lic = v.get_or_default()
+    assert isinstance(lic, L.License)
+    assert isinstance(lic.tier, str) and isinstance(lic.id, str)

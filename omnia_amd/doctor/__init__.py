@@ -46,13 +46,13 @@ def build_runner(a) -> Runner:
     if a.mgmt_signing_key:
         # the reference doctor dials the agent's management-plane twin (18080)
         # with a dashboard-minted JWT: mint one from the dashboard's signing key
-        from ..facade.auth import mint_mgmt_token
+        from ..facade.auth import jwk_thumbprint, mint_mgmt_token
         from ..utils.rsa import load_private_key
 
         with open(a.mgmt_signing_key) as f:
             key = load_private_key(f.read())
         headers["Authorization"] = "Bearer " + mint_mgmt_token(
-            key, a.mgmt_kid, "omnia-doctor", agent=a.agent, workspace=a.workspace or "")
+            key, a.mgmt_kid or jwk_thumbprint(key), "omnia-doctor", agent=a.agent, workspace=a.workspace or "")
     r.register(*AgentChecker(a.facade, st, a.token, {k.strip(): v.strip()
                                                      for k, v in headers.items()}).checks())
     r.register(*SessionChecker(st, a.namespace).checks())
@@ -83,7 +83,9 @@ def parser() -> argparse.ArgumentParser:
     ap.add_argument("--mgmt-signing-key", default=env("OMNIA_DOCTOR_MGMT_KEY", ""),
                     help="dashboard PEM key: mint a management-plane JWT and dial the "
                          "agent's twin listener (--facade ws://agent:18080/ws)")
-    ap.add_argument("--mgmt-kid", default="omnia-dashboard-1")
+    ap.add_argument("--mgmt-kid", default="",
+                    help="kid of the signing key (default: its RFC 7638 thumbprint, as the "
+                         "dashboard publishes it)")
     ap.add_argument("--agent", default="", help="agent name claimed in the mgmt-plane token")
     ap.add_argument("--header", action="append", default=[],
                     help="extra WebSocket header 'Name: value' (e.g. x-user-id behind an edge)")

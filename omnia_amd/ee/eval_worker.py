@@ -155,11 +155,21 @@ class CompletionTracker:
             self.last_seen[sid] = self.now()
 
     async def mark_completed(self, sid: str):
+        """Explicit ``session.completed``: run the session evals now.  Unlike the
+        inactivity path, a failure PROPAGATES and the session is not marked
+        completed, so the stream entry stays un-acked (XAUTOCLAIM retries it,
+        then dead-letters) instead of the evals being lost."""
         if sid in self.completed:
             return
         self.completed.add(sid)
         self.last_seen.setdefault(sid, self.now())
-        await self._fire(sid)
+        if self.on_complete is None:
+            return
+        try:
+            await self.on_complete(sid)
+        except BaseException:
+            self.completed.discard(sid)  # a redelivery runs the evals again
+            raise
 
     def _expired(self) -> list[str]:
         now = self.now()

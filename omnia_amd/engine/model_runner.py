@@ -104,6 +104,10 @@ class ModelRunner:
         # its scheduling / staging / hand-off logic runs where a bad index raises
         # instead of faulting a GPU
         self.sim = not self.is_gpu and os.environ.get("OMNIA_SIM_GRAPHS") == "1"
+        # OMNIA_EAGER_GRAPHS=1 (GPU debugging): "graph replays" run the captured
+        # decode body eagerly -- same kernels, same buffers -- so under
+        # AMD_SERIALIZE_KERNEL=3 a faulting launch raises at its own Python line
+        self.eager_graphs = self.is_gpu and os.environ.get("OMNIA_EAGER_GRAPHS") == "1"
         self.bs = kv.block_size
         self.max_model_len = max_model_len
         self.max_blocks = (max_model_len + self.bs - 1) // self.bs
@@ -698,7 +702,7 @@ class ModelRunner:
 
     def _capture(self, nrows: int, ncols: int):
         t0 = time.perf_counter()
-        if self.sim:  # CPU simulation: "replay" = the eager decode body
+        if self.sim or self.eager_graphs:  # "replay" = the eager decode body
             g = _SimGraph(lambda: self._decode_body(nrows, ncols))
             self.graphs[(nrows, ncols)] = g
             self.stats["captures"] += 1

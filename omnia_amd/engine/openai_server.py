@@ -47,24 +47,64 @@ def _err(status: int, msg: str, typ: str = "invalid_request_error"):
     return web.json_response({"error": {"message": msg, "type": typ}}, status=status)
 
 
+def _str_field(obj: dict, key: str, default: str = "") -> str:
+    v = obj.get(key)
+    if v is None:
+        return default
+    if not isinstance(v, str):
+        raise TypeError(f"{key} must be a string")
+    return v
+
+
+def _content(raw) -> str:
+    """OpenAI message content: a string, null, or an array of content parts (the
+    text parts are kept; other part types carry no text)."""
+    if raw is None:
+        return ""
+    if isinstance(raw, str):
+        return raw
+    if isinstance(raw, list):
+        out = []
+        for p in raw:
+            if not isinstance(p, dict):
+                raise TypeError("content parts must be objects")
+            t = p.get("text")
+            if t is None:
+                continue
+            if not isinstance(t, str):
+                raise TypeError("content part text must be a string")
+            out.append(t)
+        return "".join(out)
+    raise TypeError("content must be a string, an array of parts or null")
+
+
 def _messages(raw: list) -> list[Message]:
+    """Validated chat messages: a wrongly typed field raises TypeError (-> 400)."""
     out = []
     for m in raw:
-        content = m.get("content") or ""
-        if isinstance(content, list):  # content parts: keep the text ones
-            content = "".join(p.get("text", "") for p in content if isinstance(p, dict))
+        content = _content(m.get("content"))
         calls = []
-        for tc in m.get("tool_calls") or []:
-            fn = tc.get("function", {})
+        tcs = m.get("tool_calls")
+        if tcs is not None and not isinstance(tcs, list):
+            raise TypeError("tool_calls must be an array")
+        for tc in tcs or []:
+            if not isinstance(tc, dict):
+                raise TypeError("tool_calls entries must be objects")
+            fn = tc.get("function") or {}
+            if not isinstance(fn, dict):
+                raise TypeError("tool_calls[].function must be an object")
             args = fn.get("arguments", "{}")
             try:
                 args = json.loads(args) if isinstance(args, str) else dict(args)
-            except json.JSONDecodeError:
+            except (json.JSONDecodeError, TypeError, ValueError):
                 args = {"input": args}
-            calls.append(ToolCallReq(id=tc.get("id", ""), name=fn.get("name", ""),
+            if not isinstance(args, dict):
+                args = {"input": args}
+            calls.append(ToolCallReq(id=_str_field(tc, "id"), name=_str_field(fn, "name"),
                                      arguments=args))
-        out.append(Message(role=m.get("role", "user"), content=content, tool_calls=calls,
-                           tool_call_id=m.get("tool_call_id", ""), name=m.get("name", "")))
+        out.append(Message(role=_str_field(m, "role", "user"), content=content, tool_calls=calls,
+                           tool_call_id=_str_field(m, "tool_call_id"),
+                           name=_str_field(m, "name")))
     return out
 
 

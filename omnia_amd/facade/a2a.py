@@ -331,6 +331,20 @@ class A2AServer:
         watcher = asyncio.ensure_future(self._watch_cancel(tid, cancelled, stream))
         park = False
         final_state = None
+        raced = False
+
+        async def settle(state, msg=None) -> bool:
+            """The final transition; another replica may have canceled the task
+            before its cancel notice reached us (or the task is gone): then the
+            stored state wins and is what the client gets."""
+            nonlocal raced
+            try:
+                await self.tasks.set_state(task, state, msg)
+                return True
+            except (InvalidTransition, TaskNotFound):
+                raced = True
+                return False
+
         try:
             while True:
                 try:
@@ -344,7 +358,7 @@ class A2AServer:
                     final_state = "canceled"
                     break
                 if f is None:
-                    await self.tasks.set_state(task, "failed")
+                    await settle("failed")
                     break
                 k = f.WhichOneof("message")
                 if k == "chunk":
@@ -365,10 +379,10 @@ class A2AServer:
                     task.setdefault("metadata", {})["usage"] = {
                         "input_tokens": f.done.usage.input_tokens,
                         "output_tokens": f.done.usage.output_tokens}
-                    await self.tasks.set_state(task, "completed", reply)
+                    await settle("completed", reply)
                     break
                 elif k == "error":
-                    await self.tasks.set_state(task, "failed", {"role": "agent", "parts": [
+                    await settle("failed", {"role": "agent", "parts": [
                         {"kind": "text", "text": f.error.message}]})
                     break
                 elif k == "tool_call":
@@ -378,13 +392,12 @@ class A2AServer:
                     msg = {"role": "agent", "kind": "message", "messageId": str(uuid.uuid4()),
                            "contextId": ctx, "taskId": tid,
                            "parts": [{"kind": "data", "data": {"toolCalls": calls}}]}
-                    await self.tasks.set_state(task, "input-required", msg)
-                    park = True
+                    park = await settle("input-required", msg)
                     break
         except (ConnectionError, OSError):
             final_state = "canceled" if cancelled.is_set() else None
             if final_state is None:
-                await self.tasks.set_state(task, "failed")
+                await settle("failed")
         finally:
             watcher.cancel()
             if park and not cancelled.is_set():
@@ -392,7 +405,7 @@ class A2AServer:
                     self._park_watch(tid)))
             else:
                 await stream.close()
-        if final_state == "canceled":
+        if final_state == "canceled" or raced:
             task = await self.tasks.get(tid) or task
         if emit:
             await emit({"kind": "status-update", "taskId": tid, "contextId": ctx,

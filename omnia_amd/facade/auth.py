@@ -299,6 +299,22 @@ class JWKSResolver:
             return None
         return self._keys.get(kid)
 
+    def refresh(self, kid: str) -> dict | None:
+        """Re-fetch (rate-limited like an unknown kid) after a signature failed
+        against the cached key of ``kid``: the issuer may have rotated its key
+        without changing the kid.  Returns the (possibly new) key."""
+        if not self.url:
+            return None
+        now = time.monotonic()
+        if now - self._last < self.min_refresh_s:
+            return None
+        self._last = now
+        try:
+            self._load(self._fetch())
+        except Exception:  # noqa: BLE001
+            return None
+        return self._keys.get(kid)
+
 
 class MgmtPlaneValidator:
     """Dashboard-minted RS256 JWTs on the management-plane twin listeners only
@@ -335,7 +351,15 @@ class MgmtPlaneValidator:
         key = self.resolver.resolve(kid)
         if key is None:
             raise AuthError("invalid credential: unknown signing key")
-        claims = jwt_decode(tok, None, {"keys": [key]}, self.issuer, self.audience)
+        try:
+            claims = jwt_decode(tok, None, {"keys": [key]}, self.issuer, self.audience)
+        except AuthError:
+            # the cached key under this kid may be stale (issuer restarted with a
+            # new key but the same kid): one rate-limited re-fetch, then retry
+            fresh = self.resolver.refresh(kid)
+            if fresh is None or fresh == key:
+                raise
+            claims = jwt_decode(tok, None, {"keys": [fresh]}, self.issuer, self.audience)
         if "exp" not in claims:
             raise AuthError("invalid credential: exp required")
         if claims.get("origin") != ORIGIN_MGMT:
@@ -348,6 +372,20 @@ class MgmtPlaneValidator:
         sub = str(claims.get("sub", ""))
         return Identity(ORIGIN_MGMT, subject=sub, end_user=sub, workspace=ws, agent=agent,
                         claims=claims, role=str(claims.get("role", "")))
+
+
+def jwk_thumbprint(key) -> str:
+    """RFC 7638 SHA-256 thumbprint of an RSA key's public part (base64url): the
+    default ``kid`` of a signing key, so a new key always gets a new kid and
+    every JWKS cache keyed by kid misses on it (re-fetch) instead of verifying
+    against the old key."""
+    import hashlib
+
+    n = key.n.to_bytes((key.n.bit_length() + 7) // 8, "big")
+    e = key.e.to_bytes((key.e.bit_length() + 7) // 8, "big")
+    canon = json.dumps({"e": _b64url_enc(e), "kty": "RSA", "n": _b64url_enc(n)},
+                       separators=(",", ":"), sort_keys=True).encode()
+    return _b64url_enc(hashlib.sha256(canon).digest())
 
 
 def jwk_from_private(key, kid: str) -> dict:

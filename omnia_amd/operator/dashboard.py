@@ -19,6 +19,11 @@ one dependency-free page plus a small aiohttp backend:
   with a freshly minted RS256 JWT (origin ``management-plane``, the agent /
   workspace claims, the caller's subject): the browser never holds a token the
   agent's public listener would accept (``dashboard/SERVICE.md``, WS proxy).
+  The browser's ``Origin`` must be the dashboard's own (or ``--allowed-origin``).
+  Under OIDC the page first ``POST``s ``/api/agents/{ns}/{name}/ws-ticket`` with
+  its bearer and connects with the one-time ``?ticket=``; without OIDC the
+  console is closed unless ``--open-console`` (loopback only).
+  The signing key's ``kid`` is its RFC 7638 thumbprint by default.
 
 Management writes (``--allow-writes``; off by default):
 
@@ -101,7 +106,9 @@ async function consent(){const u=document.getElementById('cuser').value;
  document.getElementById('cons').textContent=JSON.stringify(
  await j('/api/consent/'+encodeURIComponent(u)),null,1)}
 function log(x){const l=document.getElementById('log');l.textContent+=x+'\\n';l.scrollTop=1e9}
-function conn(){const v=document.getElementById('ws').value;
+async function conn(){let v=document.getElementById('ws').value;
+ if(/^\/api\/agents\/[^/]+\/[^/]+\/ws$/.test(v)){const r=await fetch(v+'-ticket',{method:'POST'});
+  if(r.ok){v+='?ticket='+encodeURIComponent((await r.json()).ticket)}}
  sock=new WebSocket(v.startsWith('/')?(location.protocol==='https:'?'wss://':'ws://')+location.host+v:v);
  sock.onmessage=e=>{const m=JSON.parse(e.data);log(m.type+': '+(m.content||m.error?.message||''))}}
 function send(){sock.send(JSON.stringify({type:'message',content:document.getElementById('msg').value}))}
@@ -124,13 +131,24 @@ def _claim_set(claims: dict, *names) -> set:
     return out
 
 
+def _console_ws_path(path: str) -> bool:
+    p = path.split("/")
+    return len(p) == 6 and p[1] == "api" and p[2] == "agents" and p[5] == "ws"
+
+
 def oidc_middleware(jwks: dict, issuer: str = "", audience: str = ""):
     """401 on ``/api/*`` without a valid IdP bearer token; the verified claims
-    ride on the request (``request["claims"]``) for the write guard."""
+    ride on the request (``request["claims"]``) for the write guard.  The
+    console WebSocket is the one exception: a browser cannot put a bearer on a
+    WebSocket, so it presents a one-time ``ticket`` minted by the authenticated
+    ``POST .../ws-ticket`` route instead (checked by the route itself)."""
     from ..facade.auth import AuthError, bearer, jwt_decode
 
     @web.middleware
     async def mw(request, handler):
+        if _console_ws_path(request.path) and request.query.get("ticket") and \
+                not request.headers.get("Authorization"):
+            return await handler(request)
         if request.path.startswith("/api/") and request.path != "/api/auth/jwks":
             tok = bearer(request.headers)
             if not tok:
@@ -151,11 +169,19 @@ def oidc_middleware(jwks: dict, issuer: str = "", audience: str = ""):
 def build_app(api: str, session_api: str = "", privacy_api: str = "",
               oidc: dict | None = None, allow_writes: bool = False,
               insecure_dev_writes: bool = False,
-              allowed_origins: tuple = (), mgmt_key=None, mgmt_kid: str = "omnia-dashboard-1",
-              twin_resolver=None, token_ttl_s: int = 300) -> web.Application:
+              allowed_origins: tuple = (), mgmt_key=None, mgmt_kid: str = "",
+              twin_resolver=None, token_ttl_s: int = 300,
+              open_console: bool = False) -> web.Application:
     """``oidc``: ``{"jwks": {...}, "issuer": ..., "audience": ...,
     "write_groups": [...]}`` gates the API; ``allow_writes`` enables the
-    management routes, which need OIDC unless ``insecure_dev_writes`` (module doc)."""
+    management routes, which need OIDC unless ``insecure_dev_writes`` (module doc).
+    ``mgmt_kid`` defaults to the signing key's RFC 7638 thumbprint.  The agent
+    console mints management-plane tokens only for an OIDC-authenticated caller
+    (one-time ticket) or, without OIDC, when ``open_console`` opts in."""
+    if mgmt_key is not None and not mgmt_kid:
+        from ..facade.auth import jwk_thumbprint
+
+        mgmt_kid = jwk_thumbprint(mgmt_key)
     if allow_writes and not oidc and not insecure_dev_writes:
         raise ValueError("--allow-writes needs OIDC (--oidc-jwks-file); use "
                          "--insecure-dev-writes only for a loopback-bound dev dashboard")
@@ -346,15 +372,65 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
         ws = ((body.get("spec") or {}).get("workspaceRef") or {}).get("name", "")
         return f"ws://{ep.rsplit(':', 1)[0]}:{port}/ws", ws
 
+    tickets: dict = {}  # one-time console tickets: ticket -> (ns, name, claims, expiry)
+
+    def _origin_ok(request) -> bool:
+        origin = request.headers.get("Origin")
+        if not origin:
+            return True  # not a browser (a browser always sends Origin on a WebSocket)
+        own = {f"{request.scheme}://{request.host}", f"http://{request.host}",
+               f"https://{request.host}"}
+        return origin in own or origin in allowed_origins
+
+    async def ws_ticket(request):
+        """One-time, 30 s ticket for the console WebSocket of one agent: the
+        bearer-authenticated half of the browser console flow under OIDC."""
+        if mgmt_key is None:
+            return web.json_response({"error": "management plane not configured"}, status=503)
+        if not oidc:
+            return web.json_response({"error": "tickets need OIDC"}, status=404)
+        if not _origin_ok(request):
+            return web.json_response({"error": "cross-origin request refused"}, status=403)
+        import secrets
+        import time as _time
+
+        now = _time.monotonic()
+        for k, v in list(tickets.items()):
+            if v[3] < now:
+                tickets.pop(k, None)
+        t = secrets.token_urlsafe(24)
+        tickets[t] = (request.match_info["ns"], request.match_info["name"],
+                      request.get("claims") or {}, now + 30.0)
+        return web.json_response({"ticket": t, "expires_in": 30})
+
     async def agent_ws(request):
         """Browser <-> dashboard <-> agent twin, frame for frame."""
         if mgmt_key is None:
             return web.json_response({"error": "management plane not configured"}, status=503)
         ns, name = request.match_info["ns"], request.match_info["name"]
+        # cross-site WebSocket hijacking: browsers do not apply same-origin rules
+        # to WebSockets, so the Origin a browser sends must be the dashboard's
+        if not _origin_ok(request):
+            return web.json_response({"error": "cross-origin console refused"}, status=403)
+        if oidc:
+            claims = request.get("claims")
+            if claims is None:  # no bearer (middleware let it through): a ticket
+                import time as _time
+
+                rec = tickets.pop(request.query.get("ticket", ""), None)
+                if rec is None or rec[3] < _time.monotonic() or rec[:2] != (ns, name):
+                    return web.json_response({"error": "invalid or expired console ticket"},
+                                             status=401)
+                claims = rec[2]
+        elif open_console:
+            claims = {}
+        else:
+            return web.json_response({"error": "the agent console needs OIDC "
+                                               "(--oidc-jwks-file) or --open-console"},
+                                     status=403)
         url, workspace = await _twin(ns, name)
         if not url:
             return web.json_response({"error": "agent has no management endpoint"}, status=404)
-        claims = request.get("claims") or {}
         tok = mint_mgmt_token(mgmt_key, mgmt_kid, str(claims.get("sub") or "dashboard"),
                               agent=name, workspace=workspace, ttl_s=token_ttl_s)
         q = {k: v for k, v in request.query.items() if k in ("session", "binary", "resume")}
@@ -400,6 +476,7 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
     app.router.add_get("/healthz", healthz)
     app.router.add_get("/api/auth/jwks", jwks)
     app.router.add_get("/api/agents/{ns}/{name}/ws", agent_ws)
+    app.router.add_post("/api/agents/{ns}/{name}/ws-ticket", ws_ticket)
     app.router.add_post("/api/resources/{plural}", create)
     app.router.add_delete("/api/resources/{plural}/{ns}/{name}", delete)
     app.router.add_post("/api/agents/{ns}/{name}/scale", scale)
@@ -427,7 +504,12 @@ def main(argv=None):
     ap.add_argument("--mgmt-signing-key", default="",
                     help="PEM RSA key that signs management-plane JWTs (default: an "
                          "ephemeral key generated at start; facades re-fetch the JWKS)")
-    ap.add_argument("--mgmt-kid", default="omnia-dashboard-1")
+    ap.add_argument("--mgmt-kid", default="",
+                    help="kid of the signing key (default: its RFC 7638 thumbprint, so a "
+                         "restarted dashboard with a new ephemeral key gets a new kid)")
+    ap.add_argument("--open-console", action="store_true",
+                    help="without OIDC: let any same-origin caller open the agent console "
+                         "(only with a loopback --host)")
     a = ap.parse_args(argv)
     from ..utils.rsa import generate_private_key, load_private_key
 
@@ -443,13 +525,16 @@ def main(argv=None):
                     "write_groups": a.oidc_write_group or ["omnia-admin"]}
     if a.insecure_dev_writes and a.host not in ("127.0.0.1", "localhost", "::1"):
         ap.error("--insecure-dev-writes needs --host 127.0.0.1")
+    if a.open_console and a.host not in ("127.0.0.1", "localhost", "::1"):
+        ap.error("--open-console needs --host 127.0.0.1")
 
     async def run():
         runner = web.AppRunner(build_app(a.api, a.session_api, a.privacy_api, oidc,
                                          allow_writes=a.allow_writes,
                                          insecure_dev_writes=a.insecure_dev_writes,
                                          allowed_origins=tuple(a.allowed_origin),
-                                         mgmt_key=mgmt_key, mgmt_kid=a.mgmt_kid))
+                                         mgmt_key=mgmt_key, mgmt_kid=a.mgmt_kid,
+                                         open_console=a.open_console))
         await runner.setup()
         await web.TCPSite(runner, a.host, a.port).start()
         await asyncio.Event().wait()

@@ -16,7 +16,7 @@ import time
 
 from ..api import crds
 from ..utils import jsonschema
-from .apistore import APIStore
+from .apistore import APIStore, Conflict
 from .controllers import default_reconcilers
 
 log = logging.getLogger("omnia.operator.manager")
@@ -110,6 +110,7 @@ class Manager:
         self.queue: asyncio.Queue | None = None
         self.pending: set = set()
         self.delayed: dict = {}
+        self.conflicts: dict = {}  # key -> consecutive write conflicts
         self.identity = identity or f"{socket.gethostname()}-{os.getpid()}"
         self.leader_elect = leader_elect
         self.lease_ns = namespace
@@ -257,8 +258,18 @@ class Manager:
                 else:
                     after = r.reconcile(self.store, ns or None, name)
                 self.stats["reconciles"] += 1
+                self.conflicts.pop(key, None)
                 if after:
                     self.enqueue(kind, ns, name, after)
+            except Conflict:
+                # a write raced another writer's (stale resourceVersion): re-read
+                # and retry soon with per-key exponential backoff, as
+                # controller-runtime's rate-limited requeue does -- not an error
+                n = self.conflicts.get(key, 0) + 1
+                self.conflicts[key] = n
+                self.stats["conflicts"] = self.stats.get("conflicts", 0) + 1
+                log.debug("reconcile %s %s/%s: conflict #%d, requeued", kind, ns, name, n)
+                self.enqueue(kind, ns, name, min(5.0, 0.02 * (2 ** min(n, 8))))
             except Exception:  # noqa: BLE001
                 self.stats["errors"] += 1
                 log.exception("reconcile %s %s/%s failed", kind, ns, name)

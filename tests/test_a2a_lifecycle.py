@@ -188,3 +188,36 @@ def test_parked_task_canceled_from_another_replica_releases_stream():
             await redis.stop()
 
     asyncio.run(go())
+
+
+def test_final_transition_racing_a_cancel_returns_the_canceled_task():
+    """Another replica cancels while this one streams and its cancel notice is
+    lost: the final completed transition is invalid against the stored state,
+    and the client gets the stored (canceled) task, not a JSON-RPC error."""
+    async def go():
+        svc, prov, _ = make_service()
+        prov.delay_s = 0.2
+        srv = A2AServer(InProcessRuntimeClient(svc), "agent")
+
+        async def deaf_watch(tid, cancelled, stream):  # the notice never arrives
+            await asyncio.sleep(3600)
+
+        srv._watch_cancel = deaf_watch
+        [(runner, url)] = await _serve(srv)
+        try:
+            async with aiohttp.ClientSession() as s:
+                run = asyncio.ensure_future(_rpc(s, url, "message/send", {"message": _msg(
+                    "tell me a story", taskId="t-race")}))
+                for _ in range(100):
+                    await asyncio.sleep(0.02)
+                    t = await srv.tasks.get("t-race")
+                    if t is not None and t["status"]["state"] == "working":
+                        break
+                await srv.tasks.cancel("t-race")
+                done = await asyncio.wait_for(run, 10)
+                assert "error" not in done, done
+                assert done["result"]["status"]["state"] == "canceled"
+        finally:
+            await runner.cleanup()
+
+    asyncio.run(go())

@@ -245,6 +245,29 @@ def test_completion_tracker_inactivity_once_and_eviction():
     assert fired == ["a", "b", "c"]
 
 
+def test_explicit_completion_failure_propagates_and_retries():
+    """session.completed whose evals fail raises (the stream entry stays
+    pending) and does NOT mark the session done, so the redelivery runs them."""
+    calls = []
+
+    async def cb(sid):
+        calls.append(sid)
+        if len(calls) == 1:
+            raise ConnectionError("session-api down")
+
+    async def go():
+        tr = CompletionTracker(10.0, cb, now=lambda: 0.0)
+        with pytest.raises(ConnectionError):
+            await tr.mark_completed("s")
+        assert "s" not in tr.completed
+        await tr.mark_completed("s")  # redelivery
+        assert "s" in tr.completed
+        await tr.mark_completed("s")  # exactly once after success
+
+    asyncio.run(go())
+    assert calls == ["s", "s"]
+
+
 def test_webhook_dispatcher_window_consecutive_ratelimit_retry():
     calls = []
     fail = {"n": 2}

@@ -280,9 +280,19 @@ def test_manager_reconciles_through_kube_client(srv):
             lease = srv.store.get("Lease", "omnia-operator-leader", "omnia-system")
             assert lease["spec"]["holderIdentity"] == "op-1"
             # a spec change flows watch -> queue -> reconcile -> apply
-            cur = await asyncio.to_thread(c.get, "AgentRuntime", "echo", "default")
-            cur["spec"]["runtime"] = {"replicas": 3}
-            await asyncio.to_thread(c.update, cur)
+            def bump():
+                # optimistic concurrency: the controller's status writes bump the
+                # resourceVersion, so re-read and retry on a conflict
+                for _ in range(20):
+                    cur = c.get("AgentRuntime", "echo", "default")
+                    cur["spec"]["runtime"] = {"replicas": 3}
+                    try:
+                        return c.update(cur)
+                    except Conflict:
+                        time.sleep(0.05)
+                raise AssertionError("spec update kept conflicting")
+
+            await asyncio.to_thread(bump)
             for _ in range(300):
                 await asyncio.sleep(0.1)
                 if srv.store.get("Deployment", "echo", "default")["spec"]["replicas"] == 3:

@@ -219,7 +219,7 @@ def test_dashboard_console_proxies_to_twin(keys):
             return twin.get((ns, name)), "ws1"
 
         dash = build_app("http://127.0.0.1:1", mgmt_key=keys["k1"], mgmt_kid="dash-1",
-                         twin_resolver=resolver)
+                         twin_resolver=resolver, open_console=True)
         runner = web.AppRunner(dash)
         await runner.setup()
         site = web.TCPSite(runner, "127.0.0.1", 0)
@@ -256,3 +256,112 @@ def test_dashboard_console_proxies_to_twin(keys):
             await runner.cleanup()
 
     asyncio.run(go())
+
+
+def test_dashboard_kid_is_key_thumbprint_and_facade_refetches_rotated_key(keys):
+    """A dashboard restarted with a new ephemeral key publishes a new kid (RFC 7638
+    thumbprint), and a facade that cached the old key under a reused kid
+    re-fetches once on a signature failure instead of 401-ing until restart."""
+    from omnia_amd.facade.auth import (JWKSResolver, MgmtPlaneValidator, jwk_from_private,
+                                       jwk_thumbprint, mint_mgmt_token)
+
+    assert jwk_thumbprint(keys["k1"]) != jwk_thumbprint(keys["k2"])
+    assert jwk_thumbprint(keys["k1"]) == jwk_thumbprint(keys["k1"])
+    served = {"keys": [jwk_from_private(keys["k1"], "same")]}
+    calls = []
+
+    def fetch():
+        calls.append(1)
+        return served
+
+    res = JWKSResolver(url="http://dash/jwks", fetch=fetch, min_refresh_s=0.0)
+    v = MgmtPlaneValidator(res)
+    tok1 = mint_mgmt_token(keys["k1"], "same", "u")
+    assert v.validate({"Authorization": f"Bearer {tok1}"}, {}, None).subject == "u"
+    # rotation under the same kid: the cached key fails, one re-fetch fixes it
+    served["keys"] = [jwk_from_private(keys["k2"], "same")]
+    tok2 = mint_mgmt_token(keys["k2"], "same", "u2")
+    assert v.validate({"Authorization": f"Bearer {tok2}"}, {}, None).subject == "u2"
+    assert len(calls) == 2
+    # a forged token still fails after the re-fetch
+    bad = tok2.rsplit(".", 1)[0] + "." + tok1.rsplit(".", 1)[1]
+    with pytest.raises(AuthError):
+        v.validate({"Authorization": f"Bearer {bad}"}, {}, None)
+
+
+def test_dashboard_console_refuses_cross_origin_and_unauthenticated(keys):
+    """The console mints mgmt tokens only for same-origin callers that are
+    authenticated (OIDC ticket) or explicitly opted in (--open-console)."""
+    from aiohttp import web
+
+    from omnia_amd.facade.auth import jwk_from_private
+    from omnia_amd.operator.dashboard import build_app
+
+    async def resolver(ns, name):
+        return None, ""  # no twin: an accepted request answers 404 after the checks
+
+    async def go():
+        idp = {"keys": [jwk_from_private(keys["k2"], "idp")]}
+        apps = {"closed": build_app("http://127.0.0.1:1", mgmt_key=keys["k1"],
+                                    twin_resolver=resolver),
+                "open": build_app("http://127.0.0.1:1", mgmt_key=keys["k1"],
+                                  twin_resolver=resolver, open_console=True),
+                "oidc": build_app("http://127.0.0.1:1", mgmt_key=keys["k1"],
+                                  twin_resolver=resolver, oidc={"jwks": idp})}
+        runners, ports = [], {}
+        for k, a in apps.items():
+            r = web.AppRunner(a)
+            await r.setup()
+            site = web.TCPSite(r, "127.0.0.1", 0)
+            await site.start()
+            runners.append(r)
+            ports[k] = site._server.sockets[0].getsockname()[1]
+        try:
+            async with aiohttp.ClientSession() as s:
+                u = "http://127.0.0.1:{}/api/agents/ns/a/ws"
+                async with s.get(u.format(ports["closed"])) as r:
+                    assert r.status == 403
+                async with s.get(u.format(ports["open"]),
+                                 headers={"Origin": "https://evil.example"}) as r:
+                    assert r.status == 403
+                async with s.get(u.format(ports["open"]),
+                                 headers={"Origin": f"http://127.0.0.1:{ports['open']}"}) as r:
+                    assert r.status == 404  # passed the guards, no twin
+                async with s.get(u.format(ports["oidc"])) as r:
+                    assert r.status == 401  # no bearer, no ticket
+                async with s.get(u.format(ports["oidc"]) + "?ticket=forged") as r:
+                    assert r.status == 401
+                idtok = _idp_token(keys["k2"], "idp")
+                async with s.post(u.format(ports["oidc"]) + "-ticket",
+                                  headers={"Authorization": f"Bearer {idtok}"}) as r:
+                    assert r.status == 200
+                    t = (await r.json())["ticket"]
+                # a ticket is bound to its agent and is single-use
+                async with s.get("http://127.0.0.1:{}/api/agents/ns/b/ws?ticket={}".format(
+                        ports["oidc"], t)) as r:
+                    assert r.status == 401
+                async with s.post(u.format(ports["oidc"]) + "-ticket",
+                                  headers={"Authorization": f"Bearer {idtok}"}) as r:
+                    t = (await r.json())["ticket"]
+                async with s.get(u.format(ports["oidc"]) + f"?ticket={t}") as r:
+                    assert r.status == 404  # authenticated; no twin
+                async with s.get(u.format(ports["oidc"]) + f"?ticket={t}") as r:
+                    assert r.status == 401  # used up
+        finally:
+            for r in runners:
+                await r.cleanup()
+
+    asyncio.run(go())
+
+
+def _idp_token(key, kid):
+    import json as _json
+    import time as _time
+
+    from omnia_amd.facade.auth import _b64url_enc
+    from omnia_amd.utils.rsa import sign_pkcs1_sha256
+
+    hdr = _b64url_enc(_json.dumps({"alg": "RS256", "kid": kid}).encode())
+    body = _b64url_enc(_json.dumps({"sub": "alice", "exp": int(_time.time()) + 60}).encode())
+    sig = sign_pkcs1_sha256(key, f"{hdr}.{body}".encode())
+    return f"{hdr}.{body}.{_b64url_enc(sig)}"

@@ -6,6 +6,7 @@ input reaches the engine thread in a form that would fail a step (which would
 fail every request sharing it)."""
 import asyncio
 import json
+import os
 
 import pytest
 from aiohttp.test_utils import TestClient, TestServer
@@ -67,7 +68,7 @@ REQ = st.one_of(st.tuples(st.just("/v1/chat/completions"), CHAT),
 
 
 @given(reqs=st.lists(REQ, min_size=1, max_size=4))
-@settings(max_examples=80, deadline=None,
+@settings(max_examples=int(os.environ.get("OMNIA_FUZZ_EXAMPLES", "80")), deadline=None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 def test_openai_server_rejects_bad_input_with_4xx(eng, reqs):
     for path, body, status, text in asyncio.run(_run(eng, reqs)):

@@ -72,6 +72,11 @@ def parse(argv=None):
                     help="runtime path: engine as a thread of the serving process")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     ap.add_argument("--pod-timeout", type=float, default=900.0)
+    ap.add_argument("--pin-cpus", choices=["auto", "on", "off"], default="auto",
+                    help="pin each replica's serving tree (client, facade, runtime, "
+                         "engine-core) to a disjoint CPU set on its GPU's NUMA node "
+                         "(omnia_amd/utils/affinity.py); auto = on when --gpus > 1 and every "
+                         "replica gets >= 4 CPUs")
     ap.add_argument("--engine", choices=["gpu", "synthetic"], default="gpu",
                     help="synthetic: ws-path host capacity rehearsal -- the engine-core is a "
                          "token source paced like the measured GPU engine (engine/synthetic.py)")
@@ -96,11 +101,30 @@ def spawn_ranks(a) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
     rc = 0
-    for p in procs:
+    failed = []
+    for r, p in enumerate(procs):
         p.wait()
-        if p.returncode and not rc:
-            rc = p.returncode
+        if p.returncode:
+            failed.append((r, p.returncode))
+            if not rc:
+                rc = p.returncode
+    for r, code in failed:
+        what = f"signal {-code}" if code < 0 else f"exit code {code}"
+        print(f"bench: rank {r} of {a.gpus} failed ({what})", file=sys.stderr, flush=True)
     return rc
+
+
+def _cpulist(cpus) -> str | None:
+    """[0, 1, 2, 5] -> "0-2,5" (None: not pinned)."""
+    if not cpus:
+        return None
+    cpus = sorted(cpus)
+    out, lo = [], cpus[0]
+    for a, b in zip(cpus, cpus[1:] + [None]):
+        if b != a + 1:
+            out.append(f"{lo}-{a}" if a > lo else str(a))
+            lo = b
+    return ",".join(out)
 
 
 def pct(v, q):
@@ -416,8 +440,26 @@ def main():
         # result aggregation only: host-side gloo whenever this process owns no GPU work
         dist.init_process_group("gloo" if (host_only or not use_gpu) else "nccl")
 
+    pinned = None
+    if a.pin_cpus == "on" or (a.pin_cpus == "auto" and ws > 1):
+        # before any pod process starts: the facade / runtime / engine-core
+        # children inherit this process's CPU set
+        from omnia_amd.utils import affinity
+
+        vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+        phys = [int(x) for x in vis.split(",")] if vis else None
+        devs = [phys[r % len(phys)] if phys else r for r in range(ws)]
+        pinned = affinity.plan(devs)[rank]
+        if a.pin_cpus == "auto" and len(pinned) < affinity.MIN_AUTO_PIN_CPUS:
+            # oversubscribed host (e.g. 4 replicas on 8 CPUs): a replica's tree
+            # needs ~2.5 cores with bursts above that, and a hard 2-CPU slice
+            # starves it (p95 frame gap 63 -> 254 ms measured); share instead
+            pinned = None
+        else:
+            affinity.pin(pinned)
     drv = WSDriver(a, rank, local, use_gpu, ws) if a.path == "ws" else \
         LocalDriver(a, rank, local, use_gpu, ws)
+    drv.pinned_cpus = pinned
     try:
         run(a, drv, ws, rank, use_gpu, host_only)
     finally:
@@ -549,16 +591,18 @@ def run(a, drv, ws, rank, use_gpu, host_only):
         elapsed, out_tokens = float(mx[0]), float(sm[1])
         gathered = [None] * ws
         dist.all_gather_object(gathered, (ttfts, lats, tpot, gaps[:20000], round(my_rate, 2),
-                                          round(cores, 2)))
+                                          round(cores, 2), getattr(drv, "pinned_cpus", None)))
         ttfts = [x for g in gathered for x in g[0]]
         lats = [x for g in gathered for x in g[1]]
         tpot = [x for g in gathered for x in g[2]]
         gaps = [x for g in gathered for x in g[3]]
         per_rank = [g[4] for g in gathered]
         cores_rank = [g[5] for g in gathered]
+        pins = [g[6] for g in gathered]
     else:
         per_rank = [round(my_rate, 2)]
         cores_rank = [round(cores, 2)]
+        pins = [getattr(drv, "pinned_cpus", None)]
     value = out_tokens / elapsed
     st = drv.engine_stats() if isinstance(drv, LocalDriver) else None
     if rank == 0:
@@ -583,6 +627,7 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             "world_size": ws,
             "per_rank_tokens_per_s": per_rank,
             "host_cpu_cores_per_rank": cores_rank,
+            "pinned_cpus_per_rank": [_cpulist(p) for p in pins],
             "p50_turn_latency_ms": ms(statistics.median(lats)) if lats else None,
             "p95_turn_latency_ms": ms(pct(lats, 0.95)),
             "p50_ttft_ms": ms(statistics.median(ttfts)) if ttfts else None,

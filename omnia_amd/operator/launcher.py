@@ -94,6 +94,21 @@ class DeviceAllocator:
     def release(self, who):
         self.owner = [[w for w in o if w != who] for o in self.owner]
 
+    def cpus_for(self, devices) -> list[int] | None:
+        """Host CPUs for a pod on ``devices``: the union of its GPUs' disjoint
+        NUMA-local slices (``utils/affinity.plan`` over every GPU of the node).
+        None (unpinned) with < 2 GPUs or ``OMNIA_PIN_CPUS=0``."""
+        if not devices or self.count < 2 or os.environ.get("OMNIA_PIN_CPUS", "1") == "0":
+            return None
+        from ..utils import affinity
+
+        if getattr(self, "_cpu_plan", None) is None:
+            self._cpu_plan = affinity.plan(list(range(self.count)))
+        if os.environ.get("OMNIA_PIN_CPUS") != "force" and \
+                min(len(p) for p in self._cpu_plan) < affinity.MIN_AUTO_PIN_CPUS:
+            return None  # oversubscribed host: sharing beats starving slices
+        return sorted({c for d in devices for c in self._cpu_plan[d]})
+
     def load(self, devices) -> int:
         """Pods on the busiest GPU of ``devices`` (sizes the engine's KV slice)."""
         return max((len(self.owner[d]) for d in devices or []), default=1)
@@ -540,7 +555,8 @@ class LocalLauncher:
             renv.pop(k, None)
         fenv.pop("OMNIA_FACADE_PORT", None)
         pod = ProcessPod(f"{key[1]}-{index}", renv, fenv, device_index=devices,
-                         log_dir=os.path.join(workdir, "logs"), tp=world)
+                         log_dir=os.path.join(workdir, "logs"), tp=world,
+                         cpus=self.devices.cpus_for(devices))
         import time
 
         t0 = time.perf_counter()

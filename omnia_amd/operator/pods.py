@@ -9,6 +9,9 @@ processes with the container env the operator built, on free local ports:
 
 * the pod's GPU is pinned with ``HIP_VISIBLE_DEVICES`` (the kubelet's device
   plugin equivalent), so the runtime's engine sees it as ``cuda:0``;
+* with ``cpus`` every process of the pod is pinned to that CPU set (a slice
+  of its GPU's NUMA node, ``utils/affinity.py``), so co-located replicas do
+  not migrate across sockets or steal each other's cores;
 * each container gets its own process group; stopping the pod sends SIGTERM to
   the group (graceful drain in both entrypoints) and SIGKILL after a grace
   period, so the engine-core grandchild never outlives its runtime;
@@ -61,8 +64,11 @@ class PodFailed(RuntimeError):
 class ProcessPod:
     def __init__(self, name: str, runtime_env: dict, facade_env: dict,
                  device_index: int | list | None = None, log_dir: str | None = None,
-                 python: str = sys.executable, tp: int = 1):
+                 python: str = sys.executable, tp: int = 1, cpus: list | None = None):
         self.name = name
+        # host CPUs this pod's processes are pinned to (utils/affinity.py: a slice on
+        # its GPU's NUMA node, disjoint from the other pods'); None = unpinned
+        self.cpus = list(cpus) if cpus else None
         self.runtime_env = dict(runtime_env)
         self.facade_env = dict(facade_env)
         if isinstance(device_index, int):
@@ -102,9 +108,16 @@ class ProcessPod:
         path = os.path.join(self.log_dir, f"{tag}.log")
         f = open(path, "wb")
         self._logs.append(f)
-        return subprocess.Popen([self.python] + (launcher or []) + ["-m", module], env=full,
-                                stdout=f, stderr=subprocess.STDOUT, cwd=ROOT,
-                                start_new_session=True)
+        p = subprocess.Popen([self.python] + (launcher or []) + ["-m", module], env=full,
+                             stdout=f, stderr=subprocess.STDOUT, cwd=ROOT,
+                             start_new_session=True)
+        if self.cpus:
+            # right after the fork, before the child starts its threads and the
+            # engine-core grandchild: everything it spawns inherits the set
+            from ..utils import affinity
+
+            affinity.pin(self.cpus, p.pid)
+        return p
 
     def start_runtime(self):
         self.grpc_port = int(self.runtime_env.get("OMNIA_GRPC_PORT") or free_port())

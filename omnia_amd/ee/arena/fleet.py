@@ -67,6 +67,7 @@ class FleetSession:
                 now = time.perf_counter()
                 if ttft is None:
                     ttft = now - t0
+                    mark("client_first")
                 stamps.append(now - t0)
                 text.append(f.get("content", ""))
             elif t == "tool_call":

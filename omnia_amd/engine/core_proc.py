@@ -47,6 +47,8 @@ import time
 
 import msgpack
 
+from ..observability import timeline as TL
+
 log = logging.getLogger("omnia.engine.core")
 
 _HDR = struct.Struct("<I")
@@ -256,6 +258,13 @@ class _Core:
                 self._handle(inbox.popleft())
             if gone.is_set() and not inbox:
                 break  # client went away
+            if TL.ENABLED and not eng.has_work() and not getattr(eng, "inflight", None):
+                # idle (a wave ended): resolve the step events and write the buffer
+                # (the pod's SIGTERM at the end would skip atexit)
+                if getattr(eng, "_tl", None):
+                    eng.tl_flush()
+                elif TL._events:
+                    TL.flush()
             if eng.has_work():
                 try:
                     eng.step()

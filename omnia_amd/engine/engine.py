@@ -25,6 +25,7 @@ from ..models import build_model
 from ..models.config import ModelConfig, resolve
 from ..models.llama import KVCache
 from ..observability import metrics as M
+from ..observability import timeline as TL
 from ..utils import failpoints
 from .kv_manager import BlockManager
 from .model_runner import ModelRunner
@@ -188,8 +189,9 @@ class LLMEngine:
         # host-side time per phase of pipelined decode (diagnostics; bench reports it)
         self.timing = {"schedule_s": 0.0, "launch_s": 0.0, "collect_wait_s": 0.0,
                        "append_s": 0.0, "pipeline_breaks": 0, "gpu_starved_launches": 0}
-        self.step_trace = [] if os.environ.get("OMNIA_STEP_TRACE") else None
-        self.gpu_trace: list = []
+        # untraced step timeline (OMNIA_TIMELINE_DIR, observability/timeline.py):
+        # host schedule / launch times + timing hipEvents around every step
+        self._tl = [] if (TL.ENABLED and dev.type == "cuda") else None
         M.ENGINE_COLD_START.labels("total").set(time.perf_counter() - t0)
         log.info("engine ready: %s on %s (tp=%d), %d KV blocks x %d tokens, load %.1fs, "
                  "kv alloc %.2fs", self.model_cfg.name, dev, st.tp_size, nb, cfg.block_size,
@@ -323,6 +325,38 @@ class LLMEngine:
         log.error("engine fault (%s): failed %d sequences, dropped resident KV", err, n)
         return n
 
+    # ------------------------------------------------------------ timeline
+    def _tl_pre(self):
+        if self._tl is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def _tl_post(self, e0, kind: str, ts: float, t0: float, rows: int, ntok: int) -> None:
+        """Step record: schedule start ``ts``, launch start ``t0``, launch end now;
+        device interval = [e0, e1] (e0 completes when the stream reaches the step,
+        i.e. when the previous step ends or at launch if the GPU was idle)."""
+        if e0 is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self._tl.append((kind, rows, ntok, ts, t0, time.perf_counter(), e0, e1))
+
+    def tl_flush(self) -> None:
+        """Resolve the recorded steps' device times onto the host monotonic clock
+        and write them (call when idle: it synchronizes the device)."""
+        if not self._tl:
+            return
+        torch.cuda.synchronize(self.device)
+        ea, ta = TL.device_anchor()
+        for kind, rows, ntok, ts, t0, t1, e0, e1 in self._tl:
+            TL.mark_at(ts, "step", kind=kind, rows=rows, ntok=ntok, t_launch=round(t0, 6),
+                       t_launched=round(t1, 6), d0=round(ta - e0.elapsed_time(ea) / 1e3, 6),
+                       d1=round(ta - e1.elapsed_time(ea) / 1e3, 6))
+        self._tl.clear()
+        TL.flush()
+
     def has_work(self) -> bool:
         return self.inflight is not None or self.scheduler.has_work()
 
@@ -337,8 +371,8 @@ class LLMEngine:
             self._append(sq, tok, now)
         tm = self.timing
         tm["collect_wait_s"] += now - t0
-        if self.step_trace is not None:
-            self.step_trace.append(("collect", h.kind, t0, now))
+        if self._tl is not None:
+            TL.mark_at(t0, "collect", kind=h.kind, n=len(toks), t1=now)
         tm["append_s"] += time.perf_counter() - now
         return len(toks)
 
@@ -399,7 +433,9 @@ class LLMEngine:
             # prefill N+1 is assembled and enqueued while step N runs on the GPU
             t0 = time.perf_counter()
             self.timing["schedule_s"] += t0 - ts
+            e0 = self._tl_pre()
             h = self.runner.launch_prefill(plan.prefill)
+            self._tl_post(e0, "prefill", ts, t0, 0, sum(n for _, n in plan.prefill))
             self.timing["launch_s"] += time.perf_counter() - t0
             self.counters["steps_prefill"] += 1
             return self._launched(h, plan.prefill)
@@ -408,7 +444,10 @@ class LLMEngine:
             # of prompts completed by the step before) come from the token slots
             t0 = time.perf_counter()
             self.timing["schedule_s"] += t0 - ts
+            e0 = self._tl_pre()
             h = self.runner.launch_mixed(plan.decode, plan.prefill)
+            self._tl_post(e0, "mixed", ts, t0, len(plan.decode),
+                          sum(n for _, n in plan.prefill))
             self.timing["launch_s"] += time.perf_counter() - t0
             self.counters["steps_mixed"] = self.counters.get("steps_mixed", 0) + 1
             M.BATCH_SIZE.observe(len(plan.decode))
@@ -435,18 +474,11 @@ class LLMEngine:
             self.timing["schedule_s"] += t0 - ts
             if h0 is not None and h0.event.query():
                 self.timing["gpu_starved_launches"] += 1  # GPU drained before this launch
-            if self.step_trace is not None:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e0.record()
+            e0 = self._tl_pre()
             h = self.runner.launch_decode(plan.decode)
-            if self.step_trace is not None:
-                e1 = torch.cuda.Event(enable_timing=True)
-                e1.record()
-                self.gpu_trace.append((e0, e1))
+            self._tl_post(e0, "decode", ts, t0, len(plan.decode), 0)
             t1 = time.perf_counter()
             self.timing["launch_s"] += t1 - t0
-            if self.step_trace is not None:
-                self.step_trace.append(("launch", "decode", t0, t1))
             for sq in plan.decode:
                 sq.num_cached = sq.length  # the fed token's KV is written by this step
                 sq.output.append(PLACEHOLDER)
@@ -476,6 +508,7 @@ class LLMEngine:
 
     def _run_plan(self, plan) -> int:
         t0 = time.perf_counter()
+        e0 = self._tl_pre()
         if plan.kind == "mixed":
             toks, sampled = self.runner.run_mixed(plan.decode, plan.prefill)
             done = self.scheduler.on_decode_done(plan.decode, toks)
@@ -500,6 +533,8 @@ class LLMEngine:
             self.counters["steps_decode"] += 1
             M.DECODE_TOKENS.inc(len(toks))
             M.BATCH_SIZE.observe(len(toks))
+        self._tl_post(e0, plan.kind + "_sync", t0, t0, len(plan.decode or ()),
+                      sum(n for _, n in (plan.prefill or ())))
         dt = time.perf_counter() - t0
         M.STEP_SECONDS.labels(plan.kind).observe(dt)
         now = time.perf_counter()

@@ -682,14 +682,21 @@ class ModelRunner:
         if self.model.tp > 1:
             # vocab-parallel LM head + distributed sampler: no full-vocab gather
             from ..parallel import state as pstate
-            from ..parallel.tp_sampling import tp_sample
+            from ..parallel.tp_sampling import tp_sample, tp_sample_device
 
             local = self.model.forward(fb, self.kv, gather=False)
             if self._tap is not None:  # correctness tap: full rows (a collective)
                 self._tap[:nrows].copy_(pstate.tp_all_gather_lastdim(local))
-            tp_sample(local, self.model.vocab_start, d["temp"][:nrows], d["top_k"][:nrows],
-                      d["top_p"][:nrows], seeds=d["seeds"][:nrows], steps=d["steps"][:nrows],
+            args = (local, self.model.vocab_start, d["temp"][:nrows], d["top_k"][:nrows],
+                    d["top_p"][:nrows])
+            kw = dict(seeds=d["seeds"][:nrows], steps=d["steps"][:nrows],
                       out=self.out_tok[:nrows], group=pstate.get_state().tp_group)
+            if self.is_gpu and local.dtype == torch.bfloat16:
+                # pack kernel -> IPC all-gather -> merge kernel, which also writes each
+                # token into its sequence's device slot (no framework op in the graph)
+                tp_sample_device(*args, **kw, tok_slots=self.tok_slots, dst=d["dst"][:nrows])
+                return
+            tp_sample(*args, **kw)
             self.tok_slots.index_copy_(0, d["dst"][:nrows], self.out_tok[:nrows])
             return
         logits = self.model.forward(fb, self.kv)

@@ -52,6 +52,14 @@ int omnia_tp_gumbel(float* pack, int64_t ld, int col, const void* logits, int ro
                     int64_t row_stride, int vocab, int vocab_start, const float* temperature,
                     const int* top_k, const float* top_p, const int64_t* seeds,
                     const int64_t* steps, hipStream_t s);
+int omnia_tp_pack(float* pack, int64_t ld, int K, const void* logits, int rows,
+                  int64_t row_stride, int vocab, int vocab_start, const float* temperature,
+                  const int* top_k, const float* top_p, const int64_t* seeds,
+                  const int64_t* steps, hipStream_t s);
+int omnia_tp_merge(int* out, int* tok_slots, const int64_t* dst_slot, const float* allp, int W,
+                   int B, int64_t ld, int K, const float* temperature, const int* top_k,
+                   const float* top_p, const int64_t* seeds, const int64_t* steps,
+                   hipStream_t s);
 int omnia_mean_pool_l2(float* out, const void* hidden, int64_t stride, const int* cu, int B,
                        int D, hipStream_t s);
 int omnia_cosine_scores(float* scores, const float* q, int nq, const void* m, int64_t N, int D,
@@ -302,6 +310,71 @@ void tp_gumbel(at::Tensor pack, int64_t col, at::Tensor logits, int64_t vocab_st
                            temperature.data_ptr<float>(), opt_ptr<int>(top_k),
                            opt_ptr<float>(top_p), seeds.data_ptr<int64_t>(),
                            opt_ptr<int64_t>(steps), cur_stream()), "tp_gumbel");
+}
+
+// TP sampler, per rank: candidate pack of this rank's vocab slice (sampling.hip)
+void tp_pack(at::Tensor pack, int64_t K, at::Tensor logits, int64_t vocab_start,
+             at::Tensor temperature, c10::optional<at::Tensor> top_k,
+             c10::optional<at::Tensor> top_p, at::Tensor seeds, c10::optional<at::Tensor> steps) {
+  CHECK_GPU(pack); CHECK_GPU(logits); CHECK_BF16(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V] inner-contiguous");
+  const int rows = logits.size(0), vocab = logits.size(1);
+  TORCH_CHECK(pack.scalar_type() == at::kFloat && pack.dim() == 2 && pack.is_contiguous() &&
+              pack.size(0) == rows && pack.size(1) >= 2 * K + 4 && K >= 1 && K <= vocab,
+              "pack fp32 [B, >= 2K+4] contiguous, 1 <= K <= V");
+  TORCH_CHECK(temperature.is_cuda() && temperature.scalar_type() == at::kFloat &&
+              temperature.numel() >= rows, "temperature fp32 [B]");
+  TORCH_CHECK(seeds.is_cuda() && seeds.scalar_type() == at::kLong && seeds.numel() >= rows,
+              "seeds int64 [B]");
+  if (top_k.has_value() && top_k->defined())
+    TORCH_CHECK(top_k->is_cuda() && top_k->scalar_type() == at::kInt && top_k->numel() >= rows,
+                "top_k int32 [B]");
+  if (top_p.has_value() && top_p->defined())
+    TORCH_CHECK(top_p->is_cuda() && top_p->scalar_type() == at::kFloat && top_p->numel() >= rows,
+                "top_p fp32 [B]");
+  if (steps.has_value() && steps->defined())
+    TORCH_CHECK(steps->is_cuda() && steps->scalar_type() == at::kLong && steps->numel() >= rows,
+                "steps int64 [B]");
+  CHECK_RC(omnia_tp_pack(pack.data_ptr<float>(), pack.stride(0), (int)K, logits.data_ptr(), rows,
+                         logits.stride(0), vocab, (int)vocab_start, temperature.data_ptr<float>(),
+                         opt_ptr<int>(top_k), opt_ptr<float>(top_p), seeds.data_ptr<int64_t>(),
+                         opt_ptr<int64_t>(steps), cur_stream()), "tp_pack");
+}
+
+// TP sampler, every rank: token of each row from the all-gathered packs [W, B, ld];
+// with tok_slots / dst, also tok_slots[dst[r]] = token (device token hand-off)
+void tp_merge(at::Tensor out, c10::optional<at::Tensor> tok_slots, c10::optional<at::Tensor> dst,
+              at::Tensor allp, int64_t K, at::Tensor temperature, c10::optional<at::Tensor> top_k,
+              c10::optional<at::Tensor> top_p, at::Tensor seeds, c10::optional<at::Tensor> steps) {
+  CHECK_GPU(out); CHECK_GPU(allp); CHECK_I32(out);
+  TORCH_CHECK(allp.scalar_type() == at::kFloat && allp.dim() == 3 && allp.is_contiguous(),
+              "allp fp32 [W, B, ld] contiguous");
+  const int W = allp.size(0), B = allp.size(1);
+  const int64_t ld = allp.size(2);
+  TORCH_CHECK(out.numel() >= B && out.is_contiguous(), "out int32 [B]");
+  TORCH_CHECK(K >= 1 && ld >= 2 * K + 4 && W * K <= 512, "W * K <= 512, ld >= 2K+4");
+  TORCH_CHECK(temperature.is_cuda() && temperature.scalar_type() == at::kFloat &&
+              temperature.numel() >= B, "temperature fp32 [B]");
+  TORCH_CHECK(seeds.is_cuda() && seeds.scalar_type() == at::kLong && seeds.numel() >= B,
+              "seeds int64 [B]");
+  if (top_k.has_value() && top_k->defined())
+    TORCH_CHECK(top_k->scalar_type() == at::kInt && top_k->numel() >= B, "top_k int32 [B]");
+  if (top_p.has_value() && top_p->defined())
+    TORCH_CHECK(top_p->scalar_type() == at::kFloat && top_p->numel() >= B, "top_p fp32 [B]");
+  if (steps.has_value() && steps->defined())
+    TORCH_CHECK(steps->scalar_type() == at::kLong && steps->numel() >= B, "steps int64 [B]");
+  const bool slots = tok_slots.has_value() && tok_slots->defined();
+  if (slots) {
+    TORCH_CHECK(dst.has_value() && dst->defined() && dst->scalar_type() == at::kLong &&
+                dst->numel() >= B && dst->is_cuda(), "dst int64 [B] with tok_slots");
+    CHECK_I32(*tok_slots);
+    TORCH_CHECK(tok_slots->is_cuda() && tok_slots->is_contiguous(), "tok_slots int32 on device");
+  }
+  CHECK_RC(omnia_tp_merge(out.data_ptr<int>(), slots ? tok_slots->data_ptr<int>() : nullptr,
+                          slots ? dst->data_ptr<int64_t>() : nullptr, allp.data_ptr<float>(), W, B,
+                          ld, (int)K, temperature.data_ptr<float>(), opt_ptr<int>(top_k),
+                          opt_ptr<float>(top_p), seeds.data_ptr<int64_t>(),
+                          opt_ptr<int64_t>(steps), cur_stream()), "tp_merge");
 }
 
 void apply_token_mask(at::Tensor logits, at::Tensor mask) {
@@ -969,6 +1042,8 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("ar_max_ranks", &omnia_ar_max_ranks);
   m.def("apply_token_mask", &apply_token_mask);
   m.def("tp_gumbel", &tp_gumbel);
+  m.def("tp_pack", &tp_pack);
+  m.def("tp_merge", &tp_merge);
   m.def("graph_launch_step", &graph_launch_step);
   m.def("graph_launch_staged", &graph_launch_staged);
   m.def("stage_copy", &stage_copy);

@@ -408,3 +408,469 @@ extern "C" int omnia_tp_gumbel(float* pack, int64_t ld, int col, const void* log
                                         steps);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------ TP candidate pack + merge (decode)
+// The tensor-parallel sampler on the GPU is two kernels around ONE all-gather
+// (parallel/tp_sampling.py), with no framework ops in the captured decode graph:
+//
+// tp_pack (per rank, one 1024-thread workgroup per row of its vocab slice):
+//   * greedy rows: the slice's arg-max (value, global id) -> cols 0, K;
+//   * pure-temperature rows: the Gumbel-max winner of the slice (the tp_gumbel
+//     hash above, bit-identical to tp_sampling.gumbel_uniform) -> cols 2K, 2K+1;
+//   * top-k / top-p rows: the EXACT local top-K of the slice -- radix select on
+//     the 16-bit order-preserving bf16 key (two 8-bit histogram passes), then an
+//     index-ordered compaction (block prefix sums), so the candidate set and its
+//     order are deterministic -- -> cols [0, K) values, [K, 2K) global ids; plus
+//     the slice's softmax statistics of logits / T (max, sum exp) -> cols 2K+2,
+//     2K+3, from which the merge gets the FULL-vocabulary partition function.
+// tp_merge (every rank, same inputs -> same token; one 512-thread workgroup per
+//   row) over the all-gathered packs [W][B][ld]:
+//   * greedy: arg-max of the W slice maxima (ties -> lowest id);
+//   * pure temperature: arg-max of the W Gumbel winners;
+//   * filtered: the W*K candidates scaled by 1/T, bitonic-sorted in LDS, top-k
+//     cut (ties at the k-th value kept), top-p cut against the full-vocabulary
+//     mass (or the top-k survivors' mass when k > 0, as sample_kernel
+//     renormalises), then the Gumbel-max draw with the SAME counter-based noise
+//     as sample_kernel keyed by the GLOBAL token id -- so a filtered TP row draws
+//     exactly the token the single-GPU fused sampler draws whenever the nucleus
+//     / top-k set lies inside the candidates (top_k <= K);
+//   * the token goes to out[row] and, fused, to tok_slots[dst[row]] (the
+//     device token hand-off of pipelined decode).
+namespace {
+constexpr int kPackThreads = 1024;
+constexpr int kMergeThreads = 512;
+
+__device__ __forceinline__ uint32_t key16(uint32_t b) {
+  return (b & 0x8000u) ? (~b & 0xffffu) : (b | 0x8000u);
+}
+
+// block-wide exclusive prefix sum of small ints; *total = block sum
+__device__ __forceinline__ int block_excl_sum(int v, int* scratch, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  __syncthreads();  // previous readers of scratch are done
+  if (lane == 63) scratch[wid] = inc;
+  __syncthreads();
+  int before = 0, tot = 0;
+  for (int i = 0; i < nw; ++i) {
+    const int c = scratch[i];
+    before += i < wid ? c : 0;
+    tot += c;
+  }
+  *total = tot;
+  return before + inc - v;
+}
+
+// (value desc, id asc) arg-max merge
+__device__ __forceinline__ void argmax_merge(float& bv, int& bi, float ov, int oi) {
+  if (ov > bv || (ov == bv && oi < bi)) {
+    bv = ov;
+    bi = oi;
+  }
+}
+
+__device__ __forceinline__ void block_argmax(float& bv, int& bi, float* sf, int* si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) argmax_merge(bv, bi, __shfl_xor(bv, o, 64), __shfl_xor(bi, o, 64));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+    sf[wid] = bv;
+    si[wid] = bi;
+  }
+  __syncthreads();
+  bv = sf[0];
+  bi = si[0];
+  for (int i = 1; i < nw; ++i) argmax_merge(bv, bi, sf[i], si[i]);
+}
+
+// element e of row `lr` (VEC: 8 consecutive per thread per tile)
+template <bool VEC>
+struct RowTile {
+  static constexpr int E = VEC ? 8 : 1;
+  __device__ __forceinline__ static void load(const uint16_t* lr, int idx0, int vocab,
+                                              uint32_t (&b)[E], bool (&ok)[E]) {
+    if (VEC) {
+      if (idx0 < vocab) {  // vocab % 8 == 0: the whole vector is in the row
+        const short8 v = *reinterpret_cast<const short8*>(lr + idx0);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          b[j] = (uint16_t)v[j];
+          ok[j] = true;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          b[j] = 0;
+          ok[j] = false;
+        }
+      }
+    } else {
+      ok[0] = idx0 < vocab;
+      b[0] = ok[0] ? lr[idx0] : 0;
+    }
+  }
+};
+
+template <bool VEC>
+__global__ void __launch_bounds__(kPackThreads)
+tp_pack_kernel(float* __restrict__ pack, int64_t ld, int K, const uint16_t* __restrict__ logits,
+               int64_t row_stride, int vocab, int vocab_start,
+               const float* __restrict__ temperature, const int* __restrict__ top_k,
+               const float* __restrict__ top_p, const int64_t* __restrict__ seeds,
+               const int64_t* __restrict__ steps) {
+  using RT = RowTile<VEC>;
+  constexpr int E = RT::E;
+  __shared__ int hist[256];
+  __shared__ int iscr[kPackThreads / 64];
+  __shared__ float fscr[kPackThreads / 64];
+  __shared__ float fscr2[kPackThreads / 64];
+  __shared__ int sh_a, sh_b;
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int tile = blockDim.x * E;
+  const uint16_t* lr = logits + (int64_t)row * row_stride;
+  float* dst = pack + (int64_t)row * ld;
+  const float t = temperature[row];
+  const bool greedy = !(t > 0.f);
+  const bool filtered = !greedy && ((top_k != nullptr && top_k[row] > 0) ||
+                                    (top_p != nullptr && top_p[row] < 1.f));
+  // every column defined (the packs cross the all-gather whole)
+  for (int c = tid; c < ld; c += blockDim.x)
+    dst[c] = (c >= K && c < 2 * K) || c == 2 * K + 1 ? (float)vocab_start
+             : c == 2 * K + 3                          ? 0.f
+                                                       : -INFINITY;
+  __syncthreads();
+
+  if (greedy) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i0 = tid * E; i0 < vocab; i0 += tile) {
+      uint32_t b[E];
+      bool ok[E];
+      RT::load(lr, i0, vocab, b, ok);
+#pragma unroll
+      for (int j = 0; j < E; ++j)
+        if (ok[j]) argmax_merge(bv, bi, bf2f((uint16_t)b[j]), i0 + j);
+    }
+    block_argmax(bv, bi, fscr, iscr);
+    if (tid == 0) {
+      dst[0] = bv;
+      dst[K] = (float)(vocab_start + (bi == 0x7fffffff ? 0 : bi));
+    }
+    return;
+  }
+  const float inv_t = 1.f / fmaxf(t, 1e-6f);
+  if (!filtered) {  // pure temperature: Gumbel-max winner (tp_gumbel's hash)
+    const uint64_t sd = (uint64_t)seeds[row];
+    const uint64_t st = steps ? (uint64_t)steps[row] : 0ull;
+    uint32_t h = fmix32((uint32_t)sd ^ fmix32((uint32_t)(sd >> 32) ^ 0x68BC21EBu));
+    h = fmix32(h ^ fmix32((uint32_t)st ^ 0x02E5BE93u));
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i0 = tid * E; i0 < vocab; i0 += tile) {
+      uint32_t b[E];
+      bool ok[E];
+      RT::load(lr, i0, vocab, b, ok);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        if (!ok[j]) continue;
+        const int v = i0 + j;
+        const uint32_t r = fmix32(h ^ fmix32((uint32_t)(vocab_start + v) + 0x9E3779B9u));
+        float u = (float)(((double)r + 0.5) * (1.0 / 4294967296.0));
+        u = fminf(fmaxf(u, 1e-10f), 1.f - 1e-7f);
+        argmax_merge(bv, bi, bf2f((uint16_t)b[j]) / fmaxf(t, 1e-6f) - logf(-logf(u)), v);
+      }
+    }
+    block_argmax(bv, bi, fscr, iscr);
+    if (tid == 0) {
+      dst[2 * K] = bv;
+      dst[2 * K + 1] = (float)(vocab_start + (bi == 0x7fffffff ? 0 : bi));
+    }
+    return;
+  }
+
+  // ---- filtered: softmax stats of x / T + high-byte histogram (one pass)
+  for (int c = tid; c < 256; c += blockDim.x) hist[c] = 0;
+  __syncthreads();
+  float m = -INFINITY, s = 0.f;
+  for (int i0 = tid * E; i0 < vocab; i0 += tile) {
+    uint32_t b[E];
+    bool ok[E];
+    RT::load(lr, i0, vocab, b, ok);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      if (!ok[j]) continue;
+      atomicAdd(&hist[key16(b[j]) >> 8], 1);
+      const float x = bf2f((uint16_t)b[j]) * inv_t;
+      if (x == -INFINITY) continue;
+      if (x > m) {
+        s = s * __expf(m - x) + 1.f;
+        m = x;
+      } else {
+        s += __expf(x - m);
+      }
+    }
+  }
+  // block merge of (m, s)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  if ((tid & 63) == 0) {
+    fscr[tid >> 6] = m;
+    fscr2[tid >> 6] = s;
+  }
+  __syncthreads();  // also: hist complete
+  if (tid == 0) {
+    float M = fscr[0], S = fscr2[0];
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) {
+      const float om = fscr[i], os = fscr2[i], nm = fmaxf(M, om);
+      S = (M == -INFINITY ? 0.f : S * __expf(M - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+      M = nm;
+    }
+    dst[2 * K + 2] = M;
+    dst[2 * K + 3] = S;
+    // K-th largest key: its high byte, and how many keys lie strictly above it
+    int cum = 0, bsel = 0;
+    for (int bb = 255; bb >= 0; --bb) {
+      if (cum + hist[bb] >= K) {
+        bsel = bb;
+        break;
+      }
+      cum += hist[bb];
+    }
+    sh_a = bsel;
+    sh_b = cum;
+  }
+  __syncthreads();
+  const uint32_t hi = (uint32_t)sh_a;
+  const int above_hi = sh_b;
+  for (int c = tid; c < 256; c += blockDim.x) hist[c] = 0;
+  __syncthreads();
+  for (int i0 = tid * E; i0 < vocab; i0 += tile) {
+    uint32_t b[E];
+    bool ok[E];
+    RT::load(lr, i0, vocab, b, ok);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const uint32_t k = key16(b[j]);
+      if (ok[j] && (k >> 8) == hi) atomicAdd(&hist[k & 255], 1);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int need = K - above_hi;
+    int cum = 0, bsel = 0;
+    for (int bb = 255; bb >= 0; --bb) {
+      if (cum + hist[bb] >= need) {
+        bsel = bb;
+        break;
+      }
+      cum += hist[bb];
+    }
+    sh_a = (int)((hi << 8) | (uint32_t)bsel);  // threshold key
+    sh_b = K - (above_hi + cum);               // keys == threshold to take
+  }
+  __syncthreads();
+  const uint32_t thr = (uint32_t)sh_a;
+  const int need_eq = sh_b;
+  // ---- index-ordered compaction of the K selected (value, global id)
+  int base_sel = 0, base_eq = 0;
+  for (int t0 = 0; t0 < vocab && base_sel < K; t0 += tile) {
+    const int i0 = t0 + tid * E;
+    uint32_t b[E];
+    bool ok[E];
+    RT::load(lr, i0, vocab, b, ok);
+    int n_eq = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) n_eq += (ok[j] && key16(b[j]) == thr) ? 1 : 0;
+    int tot_eq;
+    const int eq_before = block_excl_sum(n_eq, iscr, &tot_eq);
+    bool sel[E];
+    int n_sel = 0, eq_seen = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const uint32_t k = key16(b[j]);
+      if (ok[j] && k > thr) {
+        sel[j] = true;
+      } else if (ok[j] && k == thr) {
+        sel[j] = base_eq + eq_before + eq_seen < need_eq;
+        ++eq_seen;
+      } else {
+        sel[j] = false;
+      }
+      n_sel += sel[j] ? 1 : 0;
+    }
+    int tot_sel;
+    int pos = base_sel + block_excl_sum(n_sel, iscr, &tot_sel);
+#pragma unroll
+    for (int j = 0; j < E; ++j)
+      if (sel[j] && pos < K) {
+        dst[pos] = bf2f((uint16_t)b[j]);
+        dst[K + pos] = (float)(vocab_start + i0 + j);
+        ++pos;
+      }
+    base_eq += tot_eq;
+    base_sel += tot_sel;
+  }
+}
+
+// bitonic sort of kMergeThreads (value desc, id asc) pairs in LDS
+__device__ __forceinline__ void bitonic_desc(float* v, int* id) {
+  const int tid = threadIdx.x;
+  for (int k = 2; k <= kMergeThreads; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      __syncthreads();
+      const int p = tid ^ j;
+      if (p > tid) {
+        const bool up = (tid & k) == 0;  // this k-block sorted descending when up
+        const float a = v[tid], c = v[p];
+        const int ia = id[tid], ic = id[p];
+        const bool a_first = a > c || (a == c && ia < ic);  // a precedes c in desc order
+        if (up != a_first) {
+          v[tid] = c;
+          v[p] = a;
+          id[tid] = ic;
+          id[p] = ia;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kMergeThreads)
+tp_merge_kernel(int* __restrict__ out, int* __restrict__ tok_slots,
+                const int64_t* __restrict__ dst_slot, const float* __restrict__ allp, int W,
+                int B, int64_t ld, int K, const float* __restrict__ temperature,
+                const int* __restrict__ top_k, const float* __restrict__ top_p,
+                const int64_t* __restrict__ seeds, const int64_t* __restrict__ steps) {
+  __shared__ float sv[kMergeThreads];
+  __shared__ int sid[kMergeThreads];
+  __shared__ float fscr[kMergeThreads / 64];
+  __shared__ int iscr[kMergeThreads / 64];
+  __shared__ int sh_keep;
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const float t = temperature[row];
+  const bool greedy = !(t > 0.f);
+  const int k = top_k != nullptr ? top_k[row] : 0;
+  const float p = top_p != nullptr ? top_p[row] : 1.f;
+  const bool filtered = !greedy && (k > 0 || p < 1.f);
+  auto pk = [&](int w) { return allp + ((int64_t)w * B + row) * ld; };
+  int tok;
+  if (!filtered) {
+    const int vc = greedy ? 0 : 2 * K, ic = greedy ? K : 2 * K + 1;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    if (tid < W) {
+      const float* q = pk(tid);
+      bv = q[vc];
+      bi = (int)q[ic];
+    }
+    block_argmax(bv, bi, fscr, iscr);
+    tok = bi == 0x7fffffff ? 0 : bi;
+  } else {
+    const float inv_t = 1.f / t;
+    const int n = W * K;
+    if (tid < n) {
+      const float* q = pk(tid / K);
+      const int j = tid - (tid / K) * K;
+      const float x = q[j];
+      sv[tid] = x == -INFINITY ? -INFINITY : x * inv_t;
+      sid[tid] = (int)q[K + j];
+    } else {
+      sv[tid] = -INFINITY;
+      sid[tid] = 0x7fffffff;
+    }
+    bitonic_desc(sv, sid);
+    if (tid == 0) {
+      const float M = sv[0];
+      int nvalid = 0;
+      while (nvalid < n && sv[nvalid] > -INFINITY) ++nvalid;
+      int keep = nvalid;
+      if (k > 0 && k < keep) {
+        keep = k;
+        while (keep < nvalid && sv[keep] == sv[k - 1]) ++keep;  // ties at the k-th kept
+      }
+      if (p < 1.f && keep > 0) {
+        float Z = 0.f;
+        if (k > 0) {
+          for (int i = 0; i < keep; ++i) Z += __expf(sv[i] - M);
+        } else {  // full-vocabulary mass from every rank's slice statistics
+          for (int w = 0; w < W; ++w) {
+            const float* q = pk(w);
+            const float mw = q[2 * K + 2], sw = q[2 * K + 3];
+            if (mw > -INFINITY) Z += sw * __expf(mw - M);
+          }
+        }
+        const float target = p * Z;
+        float cum = 0.f;
+        int c = 0;
+        for (; c < keep; ++c) {
+          cum += __expf(sv[c] - M);
+          if (cum >= target) break;
+        }
+        int keep2 = c < keep ? c + 1 : keep;
+        while (keep2 < keep && sv[keep2] == sv[keep2 - 1]) ++keep2;
+        keep = keep2;
+      }
+      sh_keep = keep;
+    }
+    __syncthreads();
+    const int keep = sh_keep;
+    const uint64_t seed = seeds ? (uint64_t)seeds[row] : 0x5eedull;
+    const uint64_t step = steps ? (uint64_t)steps[row] : 0ull;
+    const uint64_t rs = mix64(seed ^ (step * 0x9e3779b97f4a7c15ull));
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    if (tid < keep) {
+      const float u = uniform01(rs, (uint64_t)sid[tid]);
+      argmax_merge(bv, bi, sv[tid] - __logf(-__logf(u)), sid[tid]);
+    }
+    block_argmax(bv, bi, fscr, iscr);
+    tok = bi == 0x7fffffff ? (keep > 0 ? sid[0] : 0) : bi;
+  }
+  if (tid == 0) {
+    out[row] = tok;
+    if (tok_slots != nullptr) tok_slots[dst_slot[row]] = tok;
+  }
+}
+}  // namespace
+
+extern "C" int omnia_tp_pack(float* pack, int64_t ld, int K, const void* logits, int rows,
+                             int64_t row_stride, int vocab, int vocab_start,
+                             const float* temperature, const int* top_k, const float* top_p,
+                             const int64_t* seeds, const int64_t* steps, hipStream_t s) {
+  if (rows == 0) return 0;
+  if (K < 1 || K > vocab || ld < 2 * K + 4) return -1;
+  const bool vec = (row_stride % 8) == 0 && (vocab % 8) == 0 &&
+                   (reinterpret_cast<uintptr_t>(logits) & 15) == 0;
+  if (vec)
+    tp_pack_kernel<true><<<rows, kPackThreads, 0, s>>>(pack, ld, K, (const uint16_t*)logits,
+                                                       row_stride, vocab, vocab_start,
+                                                       temperature, top_k, top_p, seeds, steps);
+  else
+    tp_pack_kernel<false><<<rows, kPackThreads, 0, s>>>(pack, ld, K, (const uint16_t*)logits,
+                                                        row_stride, vocab, vocab_start,
+                                                        temperature, top_k, top_p, seeds, steps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int omnia_tp_merge(int* out, int* tok_slots, const int64_t* dst_slot, const float* allp,
+                              int W, int B, int64_t ld, int K, const float* temperature,
+                              const int* top_k, const float* top_p, const int64_t* seeds,
+                              const int64_t* steps, hipStream_t s) {
+  if (B == 0) return 0;
+  if (W < 1 || K < 1 || W * K > kMergeThreads || ld < 2 * K + 4) return -1;
+  tp_merge_kernel<<<B, kMergeThreads, 0, s>>>(out, tok_slots, dst_slot, allp, W, B, ld, K,
+                                              temperature, top_k, top_p, seeds, steps);
+  return (int)hipGetLastError();
+}

@@ -14,15 +14,21 @@ floats, 0.5 MB at K = 64, tp = 8):
   vocabulary.  The noise of (row, GLOBAL vocab index v) is a counter-based hash
   of (request seed, step, v): draws are independent across ranks (each hashes
   its own vocab range) without any per-rank RNG state, and a seeded request is
-  reproducible whatever the TP degree.  On the GPU the hash, the log-log and
-  the arg-max are one kernel pass over the bf16 slice (``sampling.hip``
-  ``tp_gumbel``) that skips greedy / filtered rows; ``gumbel_uniform`` is its
-  bit-exact host reference;
+  reproducible whatever the TP degree (``gumbel_uniform`` is the bit-exact
+  host reference of the device hash);
 * top-k / top-p rows: the fused sampler runs over the union of the ranks'
   local top-K logits (K = 64): exact for top_k <= K; top-p is taken inside that
   candidate set (exact whenever the nucleus has <= K tokens per rank).
 Every rank computes the same final token from the same gathered candidates,
 which keeps the device-side token feedback of pipelined decode consistent.
+
+On the GPU (:func:`tp_sample_device`) the whole tail is three launches: the
+``tp_pack`` kernel (per row: slice arg-max, Gumbel winner, or exact local
+top-K by 16-bit radix select, plus the slice's softmax statistics), the IPC
+all-gather, and the ``tp_merge`` kernel, whose filtered-row draw uses the
+single-GPU fused sampler's noise keyed by the GLOBAL token id and the
+full-vocabulary mass for top-p -- so a TP top-k / top-p row draws the token
+the single-GPU sampler draws.  No framework op runs in the captured graph.
 Penalised / grammar-constrained rows keep the full gather (the runner routes
 them to the eager path).
 """
@@ -64,57 +70,85 @@ def gumbel_uniform(seeds: torch.Tensor, steps: torch.Tensor, vocab_start: int, n
     return (h.to(torch.float64) + 0.5).mul_(1.0 / 4294967296.0).float()
 
 
+def _gather_packs(pack: torch.Tensor, W: int, group) -> torch.Tensor:
+    """``[W, B, ld]``: every TP rank's candidate pack, in rank order."""
+    from . import state as pstate
+
+    st = pstate.get_state()
+    B = pack.shape[0]
+    if st.tp_size == W and (group is None or group is st.tp_group) and st.tp_size > 1:
+        return pstate.tp_all_gather(pack)  # IPC kernel on the node (capturable)
+    if pack.is_cuda:
+        allp = torch.empty(W * B, pack.shape[1], dtype=pack.dtype, device=pack.device)
+        dist.all_gather_into_tensor(allp, pack, group=group)
+        return allp.view(W, B, -1)
+    parts = [torch.empty_like(pack) for _ in range(W)]
+    dist.all_gather(parts, pack, group=group)
+    return torch.stack(parts)
+
+
+def tp_sample_device(local_logits: torch.Tensor, vocab_start: int, temperature: torch.Tensor,
+                     top_k: torch.Tensor | None, top_p: torch.Tensor | None,
+                     seeds: torch.Tensor, steps: torch.Tensor | None = None,
+                     out: torch.Tensor | None = None, group=None, K: int = 64,
+                     tok_slots: torch.Tensor | None = None,
+                     dst: torch.Tensor | None = None) -> torch.Tensor:
+    """The GPU sampler: ``tp_pack`` kernel -> all-gather -> ``tp_merge`` kernel
+    (``ops/csrc/sampling.hip``), three launches and no framework op, so the
+    whole sampling tail of a TP decode step is hand kernels inside its hipGraph.
+    With ``tok_slots`` / ``dst`` the merge also scatters each token into its
+    sequence's device token slot."""
+    from .. import ops
+
+    B, Vl = local_logits.shape
+    W = dist.get_world_size(group)
+    K = min(K, Vl, 512 // W)
+    k = ops.kernels()
+    pack = torch.empty(B, 2 * K + 4, dtype=torch.float32, device=local_logits.device)
+    temperature = temperature.float()
+    top_k = top_k.int() if top_k is not None else None
+    top_p = top_p.float() if top_p is not None else None
+    seeds = seeds.to(torch.int64)
+    steps = steps.to(torch.int64) if steps is not None else None
+    k.tp_pack(pack, K, local_logits, vocab_start, temperature, top_k, top_p, seeds, steps)
+    allp = _gather_packs(pack, W, group)
+    if out is None:
+        out = torch.empty(B, dtype=torch.int32, device=local_logits.device)
+    k.tp_merge(out, tok_slots, dst, allp.contiguous(), K, temperature, top_k, top_p, seeds,
+               steps)
+    return out
+
+
 def tp_sample(local_logits: torch.Tensor, vocab_start: int, temperature: torch.Tensor,
               top_k: torch.Tensor, top_p: torch.Tensor, seeds: torch.Tensor | None = None,
               steps: torch.Tensor | None = None, out: torch.Tensor | None = None, group=None,
               K: int = 64, generator: torch.Generator | None = None) -> torch.Tensor:
     B, Vl = local_logits.shape
     W = dist.get_world_size(group)
+    if (local_logits.is_cuda and local_logits.dtype == torch.bfloat16 and seeds is not None
+            and local_logits.stride(1) == 1 and (out is None or out.dtype == torch.int32)):
+        return tp_sample_device(local_logits, vocab_start, temperature, top_k, top_p, seeds,
+                                steps, out=out, group=group, K=K)
+    # host reference path (CPU / gloo tests, non-bf16 logits): the same candidate
+    # pack built from framework ops
     K = min(K, Vl)
     pad = (-(2 * K + 2)) % 4  # 16-byte rows for the IPC all-gather
     pack = torch.zeros(B, 2 * K + 2 + pad, dtype=torch.float32, device=local_logits.device)
-    # top-K on an fp32 copy, as in round 3.  The TP=2 batch-8 engine test passes at
-    # the round-3 commit and faults the GPU at 3e98ee9; torch.topk straight on the
-    # bf16 slice is the device-side change between them on that test's path (the
-    # fault only came with decode buckets of 2..32 rows; batch 1 and 64 ran)
-    cv, ci = torch.topk(local_logits.float(), K, dim=1)
+    lf = local_logits.float()
+    cv, ci = torch.topk(lf, K, dim=1)
     pack[:, :K] = cv
     pack[:, K:2 * K] = ci + vocab_start
-    if (local_logits.is_cuda and local_logits.dtype == torch.bfloat16 and seeds is not None
-            and local_logits.stride(1) == 1):
-        # one fused pass: hash noise + Gumbel argmax straight into the pack; rows
-        # that are greedy / top-k / top-p never read their logits
-        ops.kernels().tp_gumbel(pack, 2 * K, local_logits, vocab_start, temperature.float(),
-                                top_k.int() if top_k is not None else None,
-                                top_p.float() if top_p is not None else None,
-                                seeds.to(torch.int64),
-                                steps.to(torch.int64) if steps is not None else None)
-    else:
-        lf = local_logits.float()
-        t = temperature.float().clamp(min=1e-6)[:, None]
-        if seeds is not None:
-            st = steps if steps is not None else torch.zeros(B, dtype=torch.int64,
-                                                             device=lf.device)
-            u = gumbel_uniform(seeds.to(lf.device), st.to(lf.device), vocab_start, Vl)
-        else:  # no per-request seeds: the caller's generator (must differ per rank)
-            u = torch.rand(B, Vl, device=lf.device, generator=generator)
-        u = u.clamp_(1e-10, 1.0 - 1e-7)
-        gv, gi = (lf / t - torch.log(-torch.log(u))).max(dim=1)
-        pack[:, 2 * K] = gv
-        pack[:, 2 * K + 1] = gi + vocab_start
-    from . import state as pstate
-
-    st = pstate.get_state()
-    if st.tp_size == W and (group is None or group is st.tp_group) and st.tp_size > 1:
-        allp = pstate.tp_all_gather(pack)  # IPC kernel on the node (capturable)
-    elif pack.is_cuda:
-        allp = torch.empty(W * B, pack.shape[1], dtype=pack.dtype, device=pack.device)
-        dist.all_gather_into_tensor(allp, pack, group=group)
-        allp = allp.view(W, B, -1)
-    else:
-        parts = [torch.empty_like(pack) for _ in range(W)]
-        dist.all_gather(parts, pack, group=group)
-        allp = torch.stack(parts)
+    t = temperature.float().clamp(min=1e-6)[:, None]
+    if seeds is not None:
+        st = steps if steps is not None else torch.zeros(B, dtype=torch.int64, device=lf.device)
+        u = gumbel_uniform(seeds.to(lf.device), st.to(lf.device), vocab_start, Vl)
+    else:  # no per-request seeds: the caller's generator (must differ per rank)
+        u = torch.rand(B, Vl, device=lf.device, generator=generator)
+    u = u.clamp_(1e-10, 1.0 - 1e-7)
+    gv, gi = (lf / t - torch.log(-torch.log(u))).max(dim=1)
+    pack[:, 2 * K] = gv
+    pack[:, 2 * K + 1] = gi + vocab_start
+    allp = _gather_packs(pack, W, group)
     cand_v = allp[:, :, :K].permute(1, 0, 2).reshape(B, W * K)
     cand_i = allp[:, :, K:2 * K].permute(1, 0, 2).reshape(B, W * K).long()
     gum_v = allp[:, :, 2 * K].t()  # [B, W]

@@ -66,7 +66,9 @@ class EngineConfig:
     # p95 TTFT 6x; a closed-loop wave (256 x 512 tokens in 16K chunks) never
     # drops to this backlog, so it keeps the separate-step throughput
     mixed_backlog: int = 8192
-    tp_mixed: bool = False  # mixed steps under TP (engine/tp.py MIXED): opt-in
+    # mixed steps under TP (engine/tp.py MIXED; sampled synchronously on rank 0):
+    # on since round 5 -- GPU-verified in every TP arrival mode (profiles/r5/tp)
+    tp_mixed: bool = True
     checkpoint: str | None = None  # HF safetensors dir (random init when None)
     # MoE expert parallelism: "tp" = experts sharded over the TP group (EP inside
     # TP); "a2a" = data-parallel attention replicas + token all-to-all to the
@@ -170,7 +172,7 @@ class LLMEngine:
             SchedulerConfig(max_batch=cfg.max_batch, max_prefill_tokens=cfg.max_prefill_tokens,
                             max_model_len=cfg.max_model_len,
                             # under TP a mixed step is published to the workers (MIXED)
-                            # and sampled synchronously on rank 0 -- opt-in (tp_mixed)
+                            # and sampled synchronously on rank 0 (tp_mixed)
                             mixed_budget=cfg.mixed_budget if (self.model.tp == 1 or
                                                               cfg.tp_mixed) else 0,
                             mixed_backlog=cfg.mixed_backlog,

@@ -178,16 +178,11 @@ def _worker(rank, world, port, q, pipeline=False, batch=8, mixed=0, stagger=Fals
         q.put(("err", traceback.format_exc()))
 
 
-# The TP=2 batch-8 case faulted the GPU at HEAD (illegal address in rank 0, reported
-# after a decode-graph replay).  Bisected on the GPU: it passes at the round-3
-# commit and faults at 3e98ee9; the one device-side change on its path between the
-# two is torch.topk straight on the bf16 vocab slice in the TP sampler, now back on
-# an fp32 copy.  That fix has not run on a GPU, so these engine cases are skipped
-# by default (OMNIA_TEST_TP_ENGINE=1 runs them) -- a wrong guess would fault the
-# card again.
-@pytest.mark.skipif(os.environ.get("OMNIA_TEST_TP_ENGINE") != "1",
-                    reason="TP engine on one GPU: the fix for the bisected fault has not "
-                           "had its GPU verification run (OMNIA_TEST_TP_ENGINE=1)")
+# Round 4's TP=2 batch-8 fault (illegal address on the 2nd replay of a decode
+# graph) was in the graph's sampling tail of framework ops (topk / zero-init pack /
+# slice assigns / gather / where around the fused Gumbel kernel); eager replays of
+# the same body passed, graphs without hipBLASLt still faulted.  The tail is now
+# the tp_pack / tp_merge hand kernels (profiles/r5/tp_fault.md).
 @pytest.mark.parametrize("world,pipeline,batch,mixed", [
     (2, False, 8, 0), (4, False, 8, 0), (8, False, 8, 0),
     (2, True, 64, 0), (4, True, 64, 0), (8, True, 64, 0)])
@@ -195,18 +190,16 @@ def test_tp_engine_on_one_gpu_matches_dense_oracle(world, pipeline, batch, mixed
     _run_tp(world, pipeline, batch, mixed, False)
 
 
-@pytest.mark.skipif(os.environ.get("OMNIA_TEST_TP_STAGGER") != "1",
-                    reason="bisecting the TP mixed-step fault: run explicitly")
-@pytest.mark.parametrize("pipeline,mixed", [(True, 0), (False, 256)])
+@pytest.mark.parametrize("pipeline,mixed", [(True, 0), (False, 256), (True, 256)])
 def test_tp_arrivals_mid_decode_on_one_gpu(pipeline, mixed):
     """Prompts arriving while 62 sequences decode: (pipelined, separate steps)
     -- the pipeline drains, the prefill runs, decode resumes; (synchronous,
-    mixed) -- TP mixed steps without the pipelined decode graphs."""
+    mixed) -- TP mixed steps; (pipelined, mixed) -- mixed steps inside the
+    pipelined engine (round 4's second fault: a decode graph replay after a
+    synchronous mixed step)."""
     _run_tp(2, pipeline, 64, mixed, True)
-# (2, True, 64, 256) -- TP mixed steps in the pipelined engine -- faulted the GPU inside a
-# decode graph replay after a synchronous mixed step (profiles/r4/multirank/
-# tp_mixed_fault_r4_12.log); TP mixed steps stay opt-in (EngineConfig.tp_mixed) and are
-# covered on the CPU (tests/test_tp_cpu.py) until that is found
+
+
 def _run_tp(world, pipeline, batch, mixed, stagger):
     """(pipeline=True, batch 64) is the config-4 engine as shipped: one-deep
     pipelined graph decode over the shared-memory step ring, fused two-shot

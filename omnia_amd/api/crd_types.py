@@ -264,7 +264,9 @@ ENGINE = Obj({
     # single-node engine knobs (device "cpu" runs the reference ops: tests, dev boxes)
     "device": Enum("cuda", "cpu"), "epMode": Enum("tp", "a2a"),
     "numBlocks": Int(minimum=16), "useGraphs": {"type": "boolean"},
-    "cpThreshold": Int(minimum=0)})
+    "cpThreshold": Int(minimum=0),
+    # HF safetensors directory on the node (random-init weights when absent)
+    "checkpoint": Str()})
 PROVIDER = Obj({
     "type": Enum(*PROVIDER_TYPES), "role": Enum("llm", "embedding", "tts", "stt", "image",
                                                 "inference", default="llm"),

@@ -103,15 +103,24 @@ class EngineConfig:
         return cls(**kw)
 
 
+def engine_model_config(cfg: EngineConfig, model_cfg: ModelConfig | None = None) -> ModelConfig:
+    """The model architecture an engine serves: explicit, else the checkpoint's
+    ``config.json`` (authoritative when a checkpoint is given -- its name need
+    not be a registered preset), else the registered preset ``cfg.model``."""
+    if model_cfg is not None:
+        return model_cfg
+    if cfg.checkpoint:
+        from ..models.loader import config_from_hf
+
+        return config_from_hf(cfg.checkpoint, cfg.model)
+    return resolve(cfg.model)
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, model_cfg: ModelConfig | None = None,
                  weights: dict | None = None):
         self.cfg = cfg
-        self.model_cfg = model_cfg or resolve(cfg.model)
-        if cfg.checkpoint and model_cfg is None:
-            from ..models.loader import config_from_hf
-
-            self.model_cfg = config_from_hf(cfg.checkpoint, cfg.model)
+        self.model_cfg = engine_model_config(cfg, model_cfg)
         dev = self._pick_device(cfg)
         self.device = dev
         dtype = getattr(torch, cfg.dtype)
@@ -194,6 +203,7 @@ class LLMEngine:
         # untraced step timeline (OMNIA_TIMELINE_DIR, observability/timeline.py):
         # host schedule / launch times + timing hipEvents around every step
         self._tl = [] if (TL.ENABLED and dev.type == "cuda") else None
+        self._tap_dir = os.environ.get("OMNIA_LOGIT_TAP_DIR", "")
         M.ENGINE_COLD_START.labels("total").set(time.perf_counter() - t0)
         log.info("engine ready: %s on %s (tp=%d), %d KV blocks x %d tokens, load %.1fs, "
                  "kv alloc %.2fs", self.model_cfg.name, dev, st.tp_size, nb, cfg.block_size,
@@ -603,8 +613,30 @@ class LLMEngine:
             del s.output[s.n_real:]
         self._finalize(s)
 
+    def _dump_tap(self, s: Sequence) -> None:
+        """``OMNIA_LOGIT_TAP_DIR`` (with the logit tap on): write a finished
+        sequence's prompt / output ids and every logits row it was sampled from,
+        so a test can check a served pod against ``ops.reference.dense_forward``
+        from outside the pod's processes."""
+        tap = self.runner.logit_tap
+        rows = []
+        for ids, r in tap:
+            for i, sid in enumerate(ids):
+                if sid == s.seq_id:
+                    rows.append(r[i])
+        # a finished sequence's rows are no longer needed in memory
+        self.runner.logit_tap = [(ids, r) for ids, r in tap if any(
+            sid in self.seqs and sid != s.seq_id for sid in ids)]
+        os.makedirs(self._tap_dir, exist_ok=True)
+        torch.save({"prompt": [int(x) for x in s.prompt], "output": [int(x) for x in s.output],
+                    "rows": torch.stack(rows) if rows else torch.empty(0)},
+                   os.path.join(self._tap_dir,
+                                f"seq-{self.model_cfg.name}-{os.getpid()}-{s.seq_id}.pt"))
+
     def _finalize(self, s: Sequence) -> None:
         self.counters["finished"] += 1
+        if self._tap_dir and self.runner.logit_tap is not None:
+            self._dump_tap(s)
         rel = getattr(self.runner, "release_slot", None)
         if rel is not None:
             rel(s)

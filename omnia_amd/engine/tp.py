@@ -409,17 +409,22 @@ def agree_num_blocks(nb: int, device) -> int:
 def run_worker(cfg, model_cfg=None, weights=None):
     """Entry point for TP ranks > 0 (returns when rank 0 shuts down)."""
     from ..models import build_model
-    from ..models.config import resolve
     from ..models.llama import KVCache
-    from .engine import LLMEngine
+    from .engine import LLMEngine, engine_model_config
 
-    model_cfg = model_cfg or resolve(cfg.model)
+    model_cfg = engine_model_config(cfg, model_cfg)
     dev = LLMEngine._pick_device(cfg)
     dtype = getattr(torch, cfg.dtype)
     if dev.type == "cuda":
         from ..ops.gemm_tuning import enable_tuned_gemms
 
         enable_tuned_gemms(dev.index or 0)
+    if weights is None and cfg.checkpoint:  # this rank's shard, sliced on load
+        from ..models.loader import load_hf_checkpoint
+
+        st = pstate.get_state()
+        weights = load_hf_checkpoint(cfg.checkpoint, model_cfg, st.tp_size, st.tp_rank, dev,
+                                     dtype)
     model = build_model(model_cfg, device=dev, dtype=dtype, seed=cfg.seed, weights=weights,
                         decode_part_size=cfg.decode_part_size)
     nb = cfg.num_blocks or LLMEngine.kv_pool_blocks(cfg, model_cfg, model.tp, dev, dtype)

@@ -107,7 +107,8 @@ def runtime_config(ar: dict, pack: dict, providers: list[dict], registry: dict |
         extra = {"swapGiB": "swap_gib", "mixedBudget": "mixed_budget", "epMode": "ep_mode",
                  "ep": "ep",
                  "numBlocks": "num_blocks", "useGraphs": "use_graphs", "device": "device",
-                 "cpThreshold": "cp_threshold", "tokenizer": "tokenizer"}
+                 "cpThreshold": "cp_threshold", "tokenizer": "tokenizer",
+                 "checkpoint": "checkpoint"}
         for k, v in eng.items():  # the engine knobs beyond the core sizing fields
             if k in extra and v is not None:
                 c.engine[extra[k]] = v

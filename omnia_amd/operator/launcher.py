@@ -77,12 +77,17 @@ class DeviceAllocator:
     8B planner); empty ranges are preferred, so sharing only starts once every
     GPU is taken."""
 
-    def __init__(self, count: int, share: int = 1):
+    def __init__(self, count: int, share: int = 1, ranks_per_gpu: int = 1):
         self.count = count
         self.share = max(1, share)
+        # engine ranks one GPU carries (``OMNIA_RANKS_PER_GPU``): > 1 puts a TP / EP
+        # pod's ranks on fewer GPUs, which then run the ``ipc`` transport
+        # (parallel/state.py) -- a multi-rank pod rehearsed on a one-GPU node
+        self.ranks_per_gpu = max(1, ranks_per_gpu)
         self.owner: list[list] = [[] for _ in range(count)]
 
     def take(self, who, n: int) -> list[int] | None:
+        n = -(-n // self.ranks_per_gpu)
         for cap in range(1, self.share + 1):  # least-loaded ranges first
             for start in range(0, self.count - n + 1):
                 if all(len(o) < cap for o in self.owner[start:start + n]):
@@ -149,7 +154,8 @@ class LocalLauncher:
         self.use_grpc = use_grpc
         self.mode = mode
         self.devices = DeviceAllocator(gpu_count,
-                                       int(os.environ.get("OMNIA_PODS_PER_GPU", "1") or 1))
+                                       int(os.environ.get("OMNIA_PODS_PER_GPU", "1") or 1),
+                                       int(os.environ.get("OMNIA_RANKS_PER_GPU", "1") or 1))
         self.task = None
         from .keda import KedaScaler
 

@@ -13,9 +13,9 @@ engine's tool-call grammar; what is checked is the plumbing: the tool call
 reaches the researcher's EP engine over A2A and comes back completed, the
 planner's retrieval read the seeded memory (access count), and session-api holds
 the tool-call rows.  This file's GPU test runs the same manifests with the
-researcher on cuda:0 (EP=1); the multi-rank expert-parallel engine itself (EP 2,
-4 and 8 ranks sharing one MI355X over the IPC all-to-all, against the dense
-oracle) is tests/test_ep_cp_gpu.py."""
+researcher's EP=2 group on the one MI355X (both ranks on cuda:0 over the IPC
+all-to-all) and checks every logits row it sampled from against the dense
+oracle; the EP 2 / 4 / 8 engine alone is tests/test_ep_cp_gpu.py."""
 import asyncio
 import json
 import os
@@ -23,6 +23,7 @@ import time
 
 import aiohttp
 import pytest
+import torch
 import yaml
 
 from omnia_amd.api import crds
@@ -185,15 +186,45 @@ def test_config5_manifests_cpu_ep2():
 
 
 @pytest.mark.gpu
-def test_config5_manifests_gpu():
-    """The same manifests on one MI355X: researcher Mixtral shape (2 layers, EP=1
-    on cuda:0 -- the EP=8 group is the driver's 8-GPU node), planner tiny-llama on
-    the CPU so the single box holds both pods."""
+def test_config5_manifests_gpu_ep2(tmp_path, monkeypatch):
+    """The same manifests on one MI355X with the researcher's expert-parallel
+    group REAL: tiny-mixtral-e8 at EP=2 (``epMode: a2a``), both ranks on cuda:0
+    (``OMNIA_RANKS_PER_GPU=2`` -> ``ipc`` transport: IPC all-to-all dispatch /
+    combine, lockstep graph decode), reached from the planner over A2A; planner
+    tiny-llama on the CPU.  Every logits row the researcher's rank 0 sampled
+    from equals the fp32 dense oracle of the same seeded weights (built here in
+    one process: attention / embeddings from the seed, expert e from its own
+    generator, exactly as each EP rank draws its share)."""
+    from served_oracle import check_tap, to_f32
+
+    from omnia_amd.models import build_model
+    from omnia_amd.models.config import resolve
+
+    tap = tmp_path / "tap"
+    monkeypatch.setenv("OMNIA_RANKS_PER_GPU", "2")
+    monkeypatch.setenv("OMNIA_LOGIT_TAP", "1")
+    monkeypatch.setenv("OMNIA_LOGIT_TAP_DIR", str(tap))
     turn, clients, mems, mid, calls, _, archived = _run({
-        "mixtral": {"model": "tiny-mixtral", "ep": 1, "device": "cuda", "dtype": "bfloat16",
-                    "numBlocks": 256, "maxModelLen": 4096, "maxBatch": 8},
+        "mixtral": {"model": "tiny-mixtral-e8", "ep": 2, "epMode": "a2a", "device": "cuda",
+                    "dtype": "bfloat16", "numBlocks": 256, "maxModelLen": 4096,
+                    "maxBatch": 8},
         "planner-llm": {"model": "tiny-llama", "device": "cpu", "dtype": "float32",
                         "numBlocks": 320, "blockSize": 16, "maxModelLen": 4096, "maxBatch": 4,
                         "useGraphs": False}}, gpu_count=1)
     _check(turn, clients, mems, mid, calls)
     _check_archive(archived)
+    mc = resolve("tiny-mixtral-e8")
+    m = build_model(mc, device="cuda", dtype=torch.bfloat16, seed=0)
+    w32 = to_f32({"embed": m.w["embed"].cpu(), "lm_head": m.w["lm_head"].cpu(),
+                  "final_norm": m.w["final_norm"].cpu(),
+                  "layers": [{k: v.cpu() for k, v in l.items()} for l in m.w["layers"]]})
+    frac, worst, n = check_tap(str(tap), mc, w32)
+    print(f"EP=2 researcher: {n} rows vs the dense oracle, worst rel err {worst:.4f}")
+    assert n > 0 and frac == 1.0, (frac, worst)
+    bad = dict(w32)
+    bad["layers"] = [dict(x) for x in w32["layers"]]
+    eg = bad["layers"][0]["experts_gate_up"].clone()
+    eg[[0, 1]] = eg[[1, 0]]  # negative control: two experts exchanged
+    bad["layers"][0]["experts_gate_up"] = eg
+    bfrac, _, _ = check_tap(str(tap), mc, bad)
+    assert bfrac < 1.0

@@ -259,3 +259,41 @@ def test_serve_scales_from_zero_llama3_8b_gpu():
     cold, first = _scale_cycle({"model": "llama-3-8b", "tp": 1, "maxBatch": 64,
                                 "maxModelLen": 4096, "kvFraction": 0.5}, gpu_count=1)
     assert cold < 300
+
+
+@pytest.mark.gpu
+def test_serve_tp2_70b_shape_pod_scale_cycle_matches_oracle_gpu(tmp_path, monkeypatch):
+    """BASELINE config 4 through the whole serving stack on the one MI355X: the
+    operator reconciles the shipped TP manifests, the activator parks the first
+    connection, the launcher starts a TP=2 pod whose two ranks share the GPU
+    (``OMNIA_RANKS_PER_GPU=2`` -> ``ipc`` transport), the rank-0 runtime loads a
+    Llama-3-70B-shaped 2-layer checkpoint (``Provider.spec.engine.checkpoint``,
+    safetensors, sharded per rank on load), the turn streams through facade ->
+    gRPC -> TP engine (graph decode, hand TP sampler), and the pod scales back to
+    zero.  Every logits row of the turn (dumped by the engine's logit tap) equals
+    the fp32 dense oracle of the checkpoint; a swapped kv head fails the gate."""
+    from conftest import release_gpu_memory
+    from served_oracle import check_tap, full_llama_weights, swapped_kv_head, to_f32
+
+    from omnia_amd.models.config import resolve
+    from omnia_amd.models.loader import save_hf_checkpoint
+
+    release_gpu_memory()
+    mc = resolve("llama-3-70b").replace(name="llama-3-70b-2l", num_layers=2)
+    w = full_llama_weights(mc)
+    ckpt = tmp_path / "ckpt"
+    save_hf_checkpoint(w, mc, ckpt)
+    w32 = to_f32(w)
+    del w
+    tap = tmp_path / "tap"
+    monkeypatch.setenv("OMNIA_RANKS_PER_GPU", "2")
+    monkeypatch.setenv("OMNIA_LOGIT_TAP", "1")
+    monkeypatch.setenv("OMNIA_LOGIT_TAP_DIR", str(tap))
+    cold, first = _scale_cycle({"model": "llama-3-70b-2l", "tp": 2, "checkpoint": str(ckpt),
+                                "maxBatch": 8, "maxModelLen": 1024, "numBlocks": 256,
+                                "blockSize": 16}, gpu_count=1)
+    frac, worst, n = check_tap(str(tap), mc, w32)
+    print(f"TP=2 pod: {n} rows, worst rel err {worst:.4f}, cold start {cold:.1f}s")
+    assert n >= 6 and frac == 1.0, (frac, worst)
+    bfrac, bworst, _ = check_tap(str(tap), mc, swapped_kv_head(w32, mc))
+    assert bfrac < 1.0 and bworst > 0.05

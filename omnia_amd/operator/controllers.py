@@ -8,6 +8,7 @@ AgentRuntimes that reference it, a Deployment change re-queues its owner).
 from __future__ import annotations
 
 import json
+import os
 import re
 import logging
 import time
@@ -141,12 +142,24 @@ class ProviderReconciler:
             m = eng.get("model") or spec.get("model")
             from ..models.config import ALIASES
 
-            if (ALIASES.get(m, m)) not in MODEL_REGISTRY:
+            cfg = MODEL_REGISTRY.get(ALIASES.get(m, m))
+            if eng.get("checkpoint"):
+                # the checkpoint's config.json is the architecture (any name); a
+                # directory this process cannot read is checked by the engine at load
+                try:
+                    from ..models.loader import config_from_hf
+
+                    cfg = config_from_hf(eng["checkpoint"], m)
+                except (OSError, ValueError, KeyError):
+                    cfg = None
+            elif cfg is None:
                 model_ok, model_msg = False, f"unknown engine model {m}"
             tp = int(eng.get("tp", 1))
-            if self.gpu_count is not None and tp > self.gpu_count:
+            # GPUs a pod's ranks may share (OMNIA_RANKS_PER_GPU, the launcher's
+            # DeviceAllocator): the capacity is GPUs x ranks per GPU
+            rpg = max(1, int(os.environ.get("OMNIA_RANKS_PER_GPU", "1") or 1))
+            if self.gpu_count is not None and tp > self.gpu_count * rpg:
                 model_ok, model_msg = False, f"engine.tp={tp} exceeds {self.gpu_count} GPUs"
-            cfg = MODEL_REGISTRY.get(ALIASES.get(m, m))
             if cfg is not None and cfg.num_heads % tp:
                 model_ok, model_msg = False, f"tp={tp} does not divide {cfg.num_heads} heads"
             st["engine"] = {"model": m, "tp": tp, "kvBytesPerToken":

@@ -297,3 +297,44 @@ def test_serve_tp2_70b_shape_pod_scale_cycle_matches_oracle_gpu(tmp_path, monkey
     assert n >= 6 and frac == 1.0, (frac, worst)
     bfrac, bworst, _ = check_tap(str(tap), mc, swapped_kv_head(w32, mc))
     assert bfrac < 1.0 and bworst > 0.05
+
+
+def test_serve_tp2_checkpoint_pod_matches_oracle_cpu(tmp_path, monkeypatch):
+    """CPU twin of the config-4 GPU oracle test: a TP=2 pod (gloo) loads an HF
+    checkpoint named only by ``Provider.spec.engine.checkpoint`` (an unregistered
+    model name -- the checkpoint's config.json is the architecture), serves the
+    turn after scale-from-zero, and every logits row the engine dumped equals
+    the fp32 dense oracle of that checkpoint."""
+    import torch
+    from served_oracle import check_tap, swapped_kv_head, to_f32
+
+    from omnia_amd.models.config import resolve
+    from omnia_amd.models.loader import save_hf_checkpoint
+
+    mc = resolve("tiny-llama").replace(name="ckpt-llama")
+    g = torch.Generator().manual_seed(5)
+    d, D = mc.hidden_size, mc.head_dim
+
+    def init(shape, std):
+        return (torch.randn(shape, generator=g) * std).float()
+
+    w = {"embed": init((mc.vocab_size, d), 0.5), "lm_head": init((mc.vocab_size, d), 0.5),
+         "final_norm": torch.ones(d), "layers": []}
+    for _ in range(mc.num_layers):
+        w["layers"].append({"in_norm": torch.ones(d), "post_norm": torch.ones(d),
+                            "qkv": init(((mc.num_heads + 2 * mc.num_kv_heads) * D, d), 0.08),
+                            "o": init((d, mc.num_heads * D), 0.05),
+                            "gate_up": init((2 * mc.intermediate_size, d), 0.08),
+                            "down": init((d, mc.intermediate_size), 0.05)})
+    ckpt = tmp_path / "ckpt"
+    save_hf_checkpoint(w, mc, ckpt)
+    tap = tmp_path / "tap"
+    monkeypatch.setenv("OMNIA_LOGIT_TAP", "1")
+    monkeypatch.setenv("OMNIA_LOGIT_TAP_DIR", str(tap))
+    _scale_cycle({"model": "ckpt-llama", "tp": 2, "checkpoint": str(ckpt), "maxBatch": 4,
+                  "maxModelLen": 512, "numBlocks": 64, "blockSize": 16, "dtype": "float32",
+                  "useGraphs": False, "device": "cpu"})
+    frac, worst, n = check_tap(str(tap), mc, to_f32(w), rel_tol=1e-3)
+    assert n >= 6 and frac == 1.0, (frac, worst)
+    bfrac, _, _ = check_tap(str(tap), mc, swapped_kv_head(to_f32(w), mc), rel_tol=1e-3)
+    assert bfrac < 1.0

@@ -34,13 +34,13 @@ __device__ __forceinline__ float4v mfma16(short8 a, short8 b, float4v c) {
 constexpr int D = 128;
 
 // ============================================================== decode
-// grid: (B, Hkv, max_parts)   block: 256 (4 waves)
+// grid: (B, Hkv, max_parts)   block: 64 * NW (NW = 2 or 4 waves)
 // UG: 16-key groups whose K loads one wave issues before its first MFMA (and,
 // for UG > 1, the first V batch is issued ahead of the softmax) -- the memory-
 // level parallelism of one workgroup, which at short contexts (one workgroup
 // streams a whole ~600-token context) sets the kernel's speed, not HBM.
-template <int G, int BS, int UG>
-__global__ __launch_bounds__(256) void decode_attn_kernel(
+template <int G, int BS, int UG, int NW>
+__global__ __launch_bounds__(64 * NW) void decode_attn_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
@@ -48,8 +48,11 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* stat = reinterpret_cast<float*>(smem);                    // [2*G] (padded to 16 floats)
   float* scores = stat + 16;                                       // [G][part_size]
-  float* red = scores + G * part_size;                             // [4][G][D]
-  int* pages = reinterpret_cast<int*>(red + 4 * G * D);            // [part_size/BS]
+  // [NW][G][D] wave partials of P.V: aliases `scores` (written after every wave's
+  // last scores read), so a workgroup holds one [G][part_size] score tile
+  float* red = scores;
+  int* pages = reinterpret_cast<int*>(scores + (G * part_size > NW * G * D ? G * part_size
+                                                                            : NW * G * D));
 
   const int b = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
   const int len = seq_lens[b];
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int h0 = kvh * G;
 
-  for (int i = tid; i < (n + BS - 1) / BS; i += 256)
+  for (int i = tid; i < (n + BS - 1) / BS; i += 64 * NW)
     pages[i] = block_tables[(int64_t)b * bt_stride + p0 / BS + i];
 
   // Q^T as the MFMA B operand: column = head (l&15, only < G real), k = dims
@@ -82,11 +85,11 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   // pass with all their K loads in flight before the first MFMA (groups past
   // the end re-read the last key: branch-free, hits in cache).
   const int ngroups = (n + 15) / 16;
-  for (int grp0 = w; grp0 < ngroups; grp0 += 4 * UG) {
+  for (int grp0 = w; grp0 < ngroups; grp0 += NW * UG) {
     short8 a[UG][4];
 #pragma unroll
     for (int u = 0; u < UG; ++u) {
-      const int key = (grp0 + 4 * u) * 16 + (lane & 15);  // this lane's A-row key
+      const int key = (grp0 + NW * u) * 16 + (lane & 15);  // this lane's A-row key
       const int kk_ = min(key, n - 1);
       const int tok = p0 + kk_;
       const bf16_t* krow = kc + (((int64_t)pages[kk_ / BS] * hkv + kvh) * BS + (tok % BS)) * D;
@@ -96,7 +99,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     }
 #pragma unroll
     for (int u = 0; u < UG; ++u) {
-      const int grp = grp0 + 4 * u;
+      const int grp = grp0 + NW * u;
       if (grp >= ngroups) break;
       float4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   auto vload = [&](int base) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int t = min(base + u * 16 + tg, n - 1);
+      const int t = min(base + u * 4 * NW + tg, n - 1);
       const int tok = p0 + t;
       vv[u] = *reinterpret_cast<const short8*>(
           vc + (((int64_t)pages[t / BS] * hkv + kvh) * BS + (tok % BS)) * D + ch * 8);
@@ -129,8 +132,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   if (UG > 1) vload(w * 4);
   __syncthreads();
 
-  // ---- phase 2: softmax per head (wave w handles heads w, w+4)
-  for (int g = w; g < G; g += 4) {
+  // ---- phase 2: softmax per head (wave w handles heads w, w+NW, ...)
+  for (int g = w; g < G; g += NW) {
     float m = -INFINITY;
     for (int i = lane; i < n; i += 64) m = fmaxf(m, scores[g * part_size + i]);
     m = wave_max(m);
@@ -154,15 +157,15 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-  for (int base = w * 4; base < n; base += 16 * U) {
+  for (int base = w * 4; base < n; base += 4 * NW * U) {
     if (UG == 1) vload(base);
     short8 cur[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) cur[u] = vv[u];
-    if (UG > 1) vload(base + 16 * U);  // next batch (clamped past the end)
+    if (UG > 1) vload(base + 4 * NW * U);  // next batch (clamped past the end)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int ti = base + u * 16 + tg;
+      const int ti = base + u * 4 * NW + tg;
       if (ti < n) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
       }
     }
   }
-  // reduce over the 4 token sub-lanes of the wave
+  // reduce over the 4 token sub-lanes of the wave (tokens of wave w: w*4 + tg mod 4*NW)
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -183,6 +186,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
       v += __shfl_xor(v, 32, 64);
       acc[g][j] = v;
     }
+  __syncthreads();  // every wave is done reading `scores`, which `red` overlays
   if (tg == 0) {
 #pragma unroll
     for (int g = 0; g < G; ++g)
@@ -190,10 +194,11 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
       for (int j = 0; j < 8; ++j) red[(w * G + g) * D + ch * 8 + j] = acc[g][j];
   }
   __syncthreads();
-  for (int i = tid; i < G * D; i += 256) {
+  for (int i = tid; i < G * D; i += 64 * NW) {
     const int g = i / D, d = i % D;
-    const float v = red[(0 * G + g) * D + d] + red[(1 * G + g) * D + d] +
-                    red[(2 * G + g) * D + d] + red[(3 * G + g) * D + d];
+    float v = 0.f;
+#pragma unroll
+    for (int wi = 0; wi < NW; ++wi) v += red[(wi * G + g) * D + d];
     const float inv = 1.f / stat[2 * g + 1];
     const int h = h0 + g;
     if (nparts == 1) {
@@ -455,20 +460,34 @@ int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void*
   if (B == 0) return 0;
   const int G = hq / hkv;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(B, hkv, max_parts), block(256);
-  const size_t lds = 64 + (size_t)G * part_size * 4 + 4 * G * D * 4 + (part_size / block_size) * 4;
   // OMNIA_DECODE_UG=1 selects the single-group schedule (A/B measurements)
   static const int ug = [] {
     const char* e = getenv("OMNIA_DECODE_UG");
     return e && atoi(e) == 1 ? 1 : 4;
   }();
-#define OMNIA_DEC_UG(GG, BB, UU)                                                               \
-  decode_attn_kernel<GG, BB, UU><<<grid, block, lds, s>>>(                                    \
+  // waves per workgroup: with many (sequence, kv head, partition) workgroups a
+  // 4-wave group (90+ VGPRs -> 5 groups per CU) leaves ~2048 groups in two
+  // uneven rounds; 2-wave groups keep every group of a 256-sequence batch
+  // resident at once (16 waves / CU, one score tile of LDS each) and stream
+  // the same bytes with the whole batch's loads in flight.  OMNIA_DECODE_NW
+  // = 2 / 4 forces one (A/B, and the numerics tests cover both; read per call).
+  const char* nw_e = getenv("OMNIA_DECODE_NW");
+  const int nw_env = nw_e ? atoi(nw_e) : 0;
+  const int64_t groups = (int64_t)B * hkv * max_parts;
+  const int nw = nw_env == 2 || nw_env == 4 ? nw_env : (groups >= 1024 ? 2 : 4);
+  dim3 grid(B, hkv, max_parts), block(64 * nw);
+  const size_t tile = (size_t)G * part_size > (size_t)nw * G * D ? (size_t)G * part_size
+                                                                  : (size_t)nw * G * D;
+  const size_t lds = 64 + tile * 4 + (part_size / block_size) * 4;
+#define OMNIA_DEC_UG(GG, BB, UU, NN)                                                           \
+  decode_attn_kernel<GG, BB, UU, NN><<<grid, block, lds, s>>>(                                \
       (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, (const bf16_t*)k_cache,               \
       (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, hkv, q_stride, part_size,   \
       max_parts, scale_log2)
+#define OMNIA_DEC_NW(GG, BB, UU) \
+  do { if (nw == 2) OMNIA_DEC_UG(GG, BB, UU, 2); else OMNIA_DEC_UG(GG, BB, UU, 4); } while (0)
 #define OMNIA_DEC(GG, BB) \
-  do { if (ug == 1) OMNIA_DEC_UG(GG, BB, 1); else OMNIA_DEC_UG(GG, BB, 4); } while (0)
+  do { if (ug == 1) OMNIA_DEC_NW(GG, BB, 1); else OMNIA_DEC_NW(GG, BB, 4); } while (0)
 #define OMNIA_DEC_BS(GG)                                \
   if (block_size == 16) OMNIA_DEC(GG, 16);              \
   else if (block_size == 32) OMNIA_DEC(GG, 32);         \
@@ -481,6 +500,7 @@ int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void*
   else return -4;
 #undef OMNIA_DEC_BS
 #undef OMNIA_DEC
+#undef OMNIA_DEC_NW
 #undef OMNIA_DEC_UG
   if (max_parts > 1)
     decode_reduce_kernel<<<B * hq, 128, 0, s>>>((bf16_t*)out, part_o, part_ml, seq_lens, hq,

@@ -5,8 +5,13 @@ partition-merge kernel included.  The K+V stream (>= 545 MB) exceeds the
 256 MB Infinity Cache, so back-to-back runs read HBM (no flush kernel: its
 dirty lines would be written back under the measured kernel).
 
-    python scripts/decode_attn_sweep.py
+    python scripts/decode_attn_sweep.py [--nw 2,4] [--parts 256,512,1024]
+
+``--nw`` runs each shape with the 2- and the 4-wave workgroup
+(``OMNIA_DECODE_NW``, read per launch) and checks them against each other.
 """
+import argparse
+import os
 import sys
 import time
 
@@ -17,6 +22,12 @@ from omnia_amd import ops  # noqa: E402
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nw", default="0")
+    ap.add_argument("--parts", default="128,192,256,320,384,512,640,1024")
+    a = ap.parse_args()
+    nws = [int(x) for x in a.nw.split(",")]
+    parts = [int(x) for x in a.parts.split(",")]
     torch.manual_seed(0)
     dev = "cuda"
     B, hq, hkv, D, BS = 256, 32, 8, 128, 32
@@ -29,11 +40,15 @@ def main():
     bt = perm.view(B, mb).contiguous()
     q = torch.randn(B, hq, D, device=dev, dtype=torch.bfloat16)
     scale = D ** -0.5
-    print(f"{'len':>5} {'part':>5} {'us':>8} {'TB/s':>6}  err", flush=True)
+    print(f"{'len':>5} {'part':>5} {'nw':>3} {'us':>8} {'TB/s':>6}  err", flush=True)
     for L in (520, 576, 640):
         sl = torch.full((B,), L, dtype=torch.int32, device=dev)
         ref = None
-        for part in (128, 192, 256, 320, 384, 512, 640, 1024):
+        for part, nw in [(p, w) for p in parts for w in nws]:
+            if nw:
+                os.environ["OMNIA_DECODE_NW"] = str(nw)
+            else:
+                os.environ.pop("OMNIA_DECODE_NW", None)
             ws = ops.decode_workspace(B, hq, mb, BS, part, dev)
             out = ops.decode_attention(q, kc, vc, bt, sl, scale, part_size=part, workspace=ws)
             if ref is None:
@@ -51,7 +66,7 @@ def main():
             ts.sort()
             us = ts[len(ts) // 2]
             nbytes = B * L * hkv * D * 2 * 2
-            print(f"{L:5d} {part:5d} {us:8.1f} {nbytes / us / 1e6:6.2f}  {err:.2e}", flush=True)
+            print(f"{L:5d} {part:5d} {nw:3d} {us:8.1f} {nbytes / us / 1e6:6.2f}  {err:.2e}", flush=True)
     time.sleep(0.1)
 
 

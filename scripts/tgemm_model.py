@@ -1,0 +1,71 @@
+"""Decode-GEMM intake model check (tgemm.hip): kernel-only time of the gate_up /
+down projections at the bench's M = 256 against the batch size (x bytes per
+CU) and the tile width / split count (x re-reads vs weight bytes per CU).
+
+    python scripts/tgemm_model.py
+
+If a block's time is (weight bytes per CU) / (per-CU HBM rate) + (x bytes per CU)
+/ (per-CU L2 -> LDS rate), halving M removes the x term's half while the weight
+term stays -- the printout lists both so the two rates can be fitted."""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from omnia_amd import ops  # noqa: E402
+
+
+def bench(fn, iters=40):
+    for i in range(3):
+        fn(i)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(iters):
+        fn(i)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000 / iters
+
+
+def main():
+    shapes = {"gate_up": (28672, 4096), "down": (4096, 14336), "qkv": (6144, 4096)}
+    print(f"{'shape':8s} {'M':>4s} {'mode':>4s} {'bn':>4s} {'S':>3s} {'wnt':>3s} {'blocks':>6s} "
+          f"{'us':>7s} {'W KB/cu':>8s} {'x KB/cu':>8s} {'GB/s W':>7s}", flush=True)
+    for name, (rows, K) in shapes.items():
+        nbytes = rows * K * 2
+        copies = max(2, (1 << 30) // nbytes + 1)
+        ws = [torch.randn(rows, K, device="cuda").mul_(0.02).to(torch.bfloat16)
+              for _ in range(copies)]
+        for M in (256, 192, 128, 64):
+            x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+            cfgs = []
+            if name == "gate_up":
+                cfgs += [(1, 128, 1, 0), (1, 64, 1, 0), (1, 256, 1, 0), (2, 256, 2, 0),
+                         (2, 128, 2, 0), (2, 256, 4, 0)]
+            elif name == "down":
+                cfgs += [(2, 128, 8, 4), (2, 256, 8, 0), (2, 256, 16, 0), (2, 64, 4, 4)]
+            else:
+                cfgs += [(2, 128, 5, 0), (2, 256, 10, 0), (2, 64, 4, 4)]
+            for mode, bn, S, wnt in cfgs:
+                N = rows // 2 if mode == 1 else rows
+                cols = bn // 2 if mode == 1 else bn
+                ntiles = N // cols
+                blocks = ntiles * S
+                out = (torch.empty(S, M, N, device="cuda") if mode == 2 else
+                       torch.empty(M, N, device="cuda", dtype=torch.bfloat16))
+                try:
+                    t = bench(lambda i: ops.tgemm(mode, x, ws[i % copies], S, bn, wnt, out=out))
+                except RuntimeError as e:
+                    print("skip", name, M, mode, bn, S, e, flush=True)
+                    continue
+                wcu = bn * (K // S) * 2 / 1024
+                xcu = M * (K // S) * 2 / 1024
+                print(f"{name:8s} {M:4d} {mode:4d} {bn:4d} {S:3d} {wnt:3d} {blocks:6d} {t:7.1f} "
+                      f"{wcu:8.0f} {xcu:8.0f} {nbytes / t / 1e3:7.0f}", flush=True)
+        del ws
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

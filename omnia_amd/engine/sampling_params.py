@@ -63,6 +63,14 @@ class SamplingParams:
         if self.seed is not None and (isinstance(self.seed, bool) or
                                       not isinstance(self.seed, int)):
             raise ValueError("seed must be an integer")
+        for f in ("top_k", "max_tokens", "min_tokens"):  # device tensors hold int32
+            v = getattr(self, f)
+            if isinstance(v, bool) or not isinstance(v, int) or not 0 <= v < 1 << 31:
+                raise ValueError(f"{f} must be an integer in [0, 2^31)")
+        if self.seed is not None and not -(1 << 63) <= self.seed < 1 << 63:
+            # any integer is a valid OpenAI seed: fold it into the sampler's int64 key
+            s = self.seed & ((1 << 64) - 1)
+            self.seed = s - (1 << 64) if s >= 1 << 63 else s
         if not isinstance(self.stop, (list, tuple)) or not all(isinstance(x, str)
                                                                for x in self.stop):
             raise ValueError("stop must be a string or a list of strings")

@@ -112,7 +112,12 @@ def test_request_burst_never_blocks_the_client_during_a_stalled_step():
                      for i in range(400)]
             await asyncio.sleep(0)  # every generate() has sent its add
             sent = time.perf_counter() - t0
-            await asyncio.gather(first, *tasks)
+            # the claim is about the sends: finish a few turns end to end and abort
+            # the rest (400 CPU prefills take minutes on a loaded box)
+            await asyncio.gather(first, *tasks[:16])
+            for t in tasks[16:]:
+                t.cancel()
+            await asyncio.gather(*tasks[16:], return_exceptions=True)
             return sent
 
         sent = asyncio.run(go())

@@ -29,7 +29,13 @@ def bench(fn, iters=40):
 
 
 def main():
-    shapes = {"gate_up": (28672, 4096), "down": (4096, 14336), "qkv": (6144, 4096)}
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--all-m", action="store_true", help="also M = 192 / 128 / 64")
+    a = ap.parse_args()
+    shapes = {"gate_up": (28672, 4096), "down": (4096, 14336), "qkv": (6144, 4096),
+              "o": (4096, 4096)}
     print(f"{'shape':8s} {'M':>4s} {'mode':>4s} {'bn':>4s} {'S':>3s} {'wnt':>3s} {'blocks':>6s} "
           f"{'us':>7s} {'W KB/cu':>8s} {'x KB/cu':>8s} {'GB/s W':>7s}", flush=True)
     for name, (rows, K) in shapes.items():
@@ -39,14 +45,19 @@ def main():
               for _ in range(copies)]
         for M in (256, 192, 128, 64):
             x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+            if M != 256 and not a.all_m:
+                continue
             cfgs = []
+            # wnt bits 3-4: split x / W rings (tgemm.hip Rings)
             if name == "gate_up":
-                cfgs += [(1, 128, 1, 0), (1, 64, 1, 0), (1, 256, 1, 0), (2, 256, 2, 0),
-                         (2, 128, 2, 0), (2, 256, 4, 0)]
+                cfgs += [(1, 128, 1, w) for w in (0, 8, 64, 128, 160, 192)]
+                cfgs += [(2, 256, 2, 8), (2, 256, 2, 128), (2, 256, 2, 160)]
             elif name == "down":
-                cfgs += [(2, 128, 8, 4), (2, 256, 8, 0), (2, 256, 16, 0), (2, 64, 4, 4)]
+                cfgs += [(2, 128, 8, w) for w in (4, 8, 64, 128, 160, 192)]
+            elif name == "o":
+                cfgs += [(2, 64, 4, w) for w in (0, 8, 64, 128, 160, 192)]
             else:
-                cfgs += [(2, 128, 5, 0), (2, 256, 10, 0), (2, 64, 4, 4)]
+                cfgs += [(2, 128, 5, w) for w in (0, 8, 64, 128, 160, 192)]
             for mode, bn, S, wnt in cfgs:
                 N = rows // 2 if mode == 1 else rows
                 cols = bn // 2 if mode == 1 else bn
@@ -59,10 +70,18 @@ def main():
                 except RuntimeError as e:
                     print("skip", name, M, mode, bn, S, e, flush=True)
                     continue
+                ops.tgemm(mode, x, ws[0], S, bn, wnt, out=out)
+                full = x.float() @ ws[0].float().t()
+                if mode == 1:
+                    want = torch.nn.functional.silu(full[:, :N]) * full[:, N:]
+                    got = out.float()
+                else:
+                    want, got = full, out.sum(0)
+                err = ((got - want).abs().max() / want.abs().max()).item() if wnt < 32 else -1
                 wcu = bn * (K // S) * 2 / 1024
                 xcu = M * (K // S) * 2 / 1024
                 print(f"{name:8s} {M:4d} {mode:4d} {bn:4d} {S:3d} {wnt:3d} {blocks:6d} {t:7.1f} "
-                      f"{wcu:8.0f} {xcu:8.0f} {nbytes / t / 1e3:7.0f}", flush=True)
+                      f"{wcu:8.0f} {xcu:8.0f} {nbytes / t / 1e3:7.0f}  err {err:.4f}", flush=True)
         del ws
         torch.cuda.empty_cache()
 

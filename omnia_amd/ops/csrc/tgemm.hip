@@ -87,43 +87,22 @@ struct Geo {
   static_assert(NS >= 2, "ring too shallow");
 };
 
-// Split rings (RING 1 / 2, BK = 64): x and W get rings of their own, the W ring
-// deeper.  In the shared ring two thirds of every in-flight stage are x bytes,
-// which come from L2, while the HBM weight stream -- the long-latency part --
-// has only ~2 stages (32 KB per CU at BN = 128) in flight: measured, that caps
-// the weight stream near 4 TB/s whatever the batch (scripts/tgemm_model.py,
-// profiles/r5/decode_gemm/).  Here x runs NSX - 1 stages ahead and W NSW - 1.
-template <int BN, int RING>
-struct Rings {
-  static constexpr int NSX = RING == 0 ? 0 : (BN == 256 ? 2 : (RING != 2 ? 3 : 2));  // 3-5: as 1
-  static constexpr int NSW = RING == 0 ? 0
-                             : BN == 256 ? 3
-                             : BN == 128 ? (RING != 2 ? 4 : 6)
-                                         : (RING != 2 ? 8 : 12);
-  static_assert(RING == 0 || NSW > NSX, "W ring deeper than the x ring");
-  static_assert(RING == 0 || (NSX * 256 + NSW * BN) * 64 * 2 <= 160 * 1024, "LDS");
-};
-
 // PIPE = 1 (BK = 64, BN <= 128): the LDS -> register fragment reads of stage t+1
 // are issued right after stage t+1's barrier and run under stage t's MFMAs
 // (fragments double-buffered in registers), instead of all 8 waves bursting their
 // reads after each barrier and then waiting on them; the ring also keeps one more
 // stage in flight, since a stage's buffer is free as soon as its fragments are
 // in registers.
-template <int BN, int MODE, int WNT, int BK, int PIPE, int RING = 0>
+template <int BN, int MODE, int WNT, int BK, int PIPE>
 __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
                                                        const bf16_t* __restrict__ X,
                                                        const bf16_t* __restrict__ W, int M, int N,
                                                        int K, int S, int ldo) {
   using G = Geo<BN, BK>;
-  using R = Rings<BN, RING>;
   constexpr int NS = G::NS, L = G::L, A_IN = G::A_IN, B_IN = G::B_IN;
   constexpr int CH = G::CH, RPI = G::RPI;
   constexpr int FM = G::FM, FN = G::FN, WTM = G::WTM, WTN = G::WTN;
-  constexpr int XST = 256 * BK, WST = BN * BK;  // split-ring stage sizes (elements)
-  constexpr int LDS_N = RING ? R::NSX * XST + R::NSW * WST : NS * G::STAGE;
-  static_assert(RING == 0 || (BK == 64 && PIPE == 0), "split rings: 64-k stages, no PIPE");
-  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_N];
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NS * G::STAGE];
 
   // mode 1 tiles hold BN/2 output features (gate + up rows of W)
   const int ntiles = MODE == 1 ? N / (BN / 2) : N / BN;
@@ -175,8 +154,6 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
       wrow = (int64_t)tile * BN + rr;
     }
     b_src[i] = W + wrow * K + (int64_t)kb * BK + gchunk(rr) * 8;
-    if (RING >= 6)  // measurement: tile-packed W ([tile][k-step][BN][BK], stages contiguous)
-      b_src[i] = W + ((int64_t)tile * (K / BK) + kb) * BN * BK + rr * BK + gchunk(rr) * 8;
   }
   const int a_dst0 = (RPI * w * A_IN) * BK;              // element offsets inside a stage
   const int b_dst0 = 256 * BK + (RPI * w * B_IN) * BK;
@@ -231,77 +208,7 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
   };
 
   const int klast = n_loc - 1;
-  if constexpr (RING != 0) {
-    constexpr int NSX = R::NSX, NSW = R::NSW;
-    bf16_t* const wl = lds + NSX * XST;
-    auto issue_x = [&](int slot, int kl) {
-      bf16_t* base = lds + slot * XST;
-      if (RING == 4 || RING == 6) kl = 0;  // measurement: W stream alone (x hot)
-#pragma unroll
-      for (int i = 0; i < A_IN; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + kl * BK),
-                                         (lds_ptr_t)(base + a_dst0 + i * 512), 16, 0, 0);
-    };
-    auto issue_w = [&](int slot, int kl) {
-      bf16_t* base = wl + slot * WST;
-      if (RING == 5) kl = 0;  // measurement: x stream alone
-      const int64_t kstride = RING >= 6 ? BN * BK : BK;
-#pragma unroll
-      for (int i = 0; i < B_IN; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + kl * kstride),
-                                         (lds_ptr_t)(base + (b_dst0 - 256 * BK) + i * 512), 16,
-                                         0, WNT ? 2 : 0);
-    };
-    auto compute2 = [&](int xs, int ws_) {
-      const bf16_t* As = lds + xs * XST;
-      const bf16_t* Bs = wl + ws_ * WST;
-      short8 a[KS][FM], b[KS][FN];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          b[ks][j] = *reinterpret_cast<const short8*>(Bs + swz<BK>(wn * WTN + 16 * j + fr,
-                                                                   ks * 4 + fq));
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          a[ks][i] = *reinterpret_cast<const short8*>(As + swz<BK>(wm * WTM + 16 * i + fr,
-                                                                   ks * 4 + fq));
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(a[ks][i], b[ks][j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    // Issue order, prologue included, is one "virtual step" j = -(NSW-1) .. per
-    // iteration: x stage j+NSX-1 (when >= 0), then W stage j+NSW-1.  W(t) is thus
-    // always issued before x(t), and loads retire in order, so "x(t) landed"
-    // implies W(t) landed; after x(t) come W(t+NSW-NSX) and NSX-2 whole steps.
-    // Past the slice end the stage index clamps to the last one (dead buffers,
-    // constant counts).
-#pragma unroll
-    for (int j = -(NSW - 1); j < 0; ++j) {
-      if (j + NSX - 1 >= 0) issue_x(j + NSX - 1, min(j + NSX - 1, klast));
-      issue_w(j + NSW - 1, min(j + NSW - 1, klast));
-    }
-    int xs = 0, ws_ = 0;                       // slots of stage t
-    int xr = NSX - 1, wr = NSW - 1;            // slots refilled at step t (= t-1's)
-    for (int t = 0; t < n_loc; ++t) {
-      wait_vm<B_IN + (NSX - 2) * L>();
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      issue_x(xr, min(t + NSX - 1, klast));
-      issue_w(wr, min(t + NSW - 1, klast));
-      if (RING < 3 || RING == 7) compute2(xs, ws_);  // RING 3: the staging pipeline alone (measurement)
-      __builtin_amdgcn_sched_barrier(0);
-      xr = xs; wr = ws_;
-      xs = xs + 1 == NSX ? 0 : xs + 1;
-      ws_ = ws_ + 1 == NSW ? 0 : ws_ + 1;
-    }
-  } else if constexpr (PIPE) {
+  if constexpr (PIPE) {
     static_assert(BK == 64 && BN <= 128, "register-pipelined variant: BK 64, BN <= 128");
     auto ldfrag = [&](int stage, short8 (&a)[KS][FM], short8 (&b)[KS][FN]) {
       const bf16_t* As = lds + stage * G::STAGE;
@@ -426,48 +333,14 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
 }
 
 // wnt bit 0: non-temporal W loads; bit 1: 32-k stages (BN >= 128); bit 2:
-// register-pipelined fragment reads (BN <= 128, 64-k stages); bits 3-4: split
-// x / W rings (1: NSX 3 / NSW 4 at BN 128, 3 / 8 at BN 64, 2 / 3 at BN 256;
-// 2: 2 / 6 at BN 128, 2 / 12 at BN 64)
+// register-pipelined fragment reads (BN <= 128, 64-k stages)
 template <int BN, int MODE>
 int launch_bn(void* out, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int ldo,
               int wnt, hipStream_t s) {
   const int ntiles = MODE == 1 ? N / (BN / 2) : N / BN;
   const dim3 grid(ntiles * S * ((M + 255) / 256)), block(512);
   const bool nt = wnt & 1, bk32 = wnt & 2, pipe = wnt & 4;
-  const int ring = (wnt >> 5) ? 1 : (wnt >> 3) & 3;
   if (bk32 && pipe) return -22;
-  if (ring) {
-    if (bk32 || pipe || (BN == 256 && ring == 2)) return -24;
-    if (wnt >> 5) {  // measurement-only pipelines: 3 staging alone, 4 W alone, 5 x alone
-      const int m = wnt >> 5;
-      if (m == 1)
-        tgemm_kernel<BN, MODE, 0, 64, 0, 3><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
-      else if (m == 2)
-        tgemm_kernel<BN, MODE, 0, 64, 0, 4><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
-      else if (m == 4)  // W tile-packed, alone
-        tgemm_kernel<BN, MODE, 0, 64, 0, 6><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
-      else if (m == 5)  // W tile-packed, full kernel
-        tgemm_kernel<BN, MODE, 0, 64, 0, 7><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
-      else if (m == 6)  // W tile-packed, full kernel, non-temporal
-        tgemm_kernel<BN, MODE, 1, 64, 0, 7><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
-      else
-        tgemm_kernel<BN, MODE, 0, 64, 0, 5><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
-    } else if (ring == 1) {
-      if (nt)
-        tgemm_kernel<BN, MODE, 1, 64, 0, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
-      else
-        tgemm_kernel<BN, MODE, 0, 64, 0, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
-    } else {
-      if constexpr (BN != 256) {
-        if (nt)
-          tgemm_kernel<BN, MODE, 1, 64, 0, 2><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
-        else
-          tgemm_kernel<BN, MODE, 0, 64, 0, 2><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
-      }
-    }
-    return (int)hipGetLastError();
-  }
   if constexpr (BN >= 128) {
     if (bk32) {
       if (nt)

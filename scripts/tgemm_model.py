@@ -4,9 +4,10 @@ CU) and the tile width / split count (x re-reads vs weight bytes per CU).
 
     python scripts/tgemm_model.py
 
-If a block's time is (weight bytes per CU) / (per-CU HBM rate) + (x bytes per CU)
-/ (per-CU L2 -> LDS rate), halving M removes the x term's half while the weight
-term stays -- the printout lists both so the two rates can be fitted."""
+The wnt codes >= 8 (split x / W rings, bits 3-4) and >= 32 (measurement-only
+pipelines: 32 staging alone, 64 W alone, 96 x alone, 128 / 160 tile-packed W)
+exist in tgemm.hip at commit 1a05c5a only; at other commits they are rejected
+and print "skip".  Findings: profiles/r5/decode_gemm/README.md."""
 import sys
 
 import torch

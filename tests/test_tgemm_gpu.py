@@ -20,8 +20,7 @@ def _mk(M, N, K, seed=0):
 
 
 @pytest.mark.parametrize("M", [1, 77, 129, 200, 256])
-@pytest.mark.parametrize("bn,pipe", [(64, 0), (128, 0), (256, 0), (64, 4), (128, 4), (64, 8),
-                                     (128, 16), (256, 8)])
+@pytest.mark.parametrize("bn,pipe", [(64, 0), (128, 0), (256, 0), (64, 4), (128, 4)])
 def test_mode0_matches_fp32(M, bn, pipe):
     x, w = _mk(M, 1024, 512, seed=M + bn)
     out = ops.tgemm(0, x, w, 1, bn, int(bn == 128) | pipe)
@@ -31,7 +30,7 @@ def test_mode0_matches_fp32(M, bn, pipe):
 
 @pytest.mark.parametrize("M", [3, 190, 256])
 @pytest.mark.parametrize("bn,wnt", [(64, 1), (128, 1), (256, 1), (128, 2), (256, 3), (128, 4),
-                                    (64, 5), (128, 8), (128, 17), (64, 16), (256, 9)])
+                                    (64, 5)])
 def test_mode1_swiglu_matches_fp32(M, bn, wnt):
     I = 512
     x, w = _mk(M, 2 * I, 1024, seed=7 + M + bn)
@@ -43,8 +42,7 @@ def test_mode1_swiglu_matches_fp32(M, bn, wnt):
 @pytest.mark.parametrize("M,S,bn,wnt", [(256, 1, 128, 0), (256, 3, 128, 0), (256, 5, 64, 0),
                                          (201, 7, 256, 0), (256, 16, 64, 0), (130, 2, 256, 0),
                                          (256, 3, 128, 4), (256, 5, 64, 5), (256, 16, 128, 4),
-                                         (77, 7, 128, 5), (256, 3, 128, 8), (256, 16, 128, 16),
-                                         (201, 7, 256, 9), (77, 5, 64, 16), (256, 16, 64, 8)])
+                                         (77, 7, 128, 5)])
 def test_mode2_splitk_slabs_sum_to_product(M, S, bn, wnt):
     """Uneven splits; with the pipelined variant also slices of 1-3 k-steps (odd
     and even step counts through its two-step unrolled loop)."""
@@ -55,14 +53,14 @@ def test_mode2_splitk_slabs_sum_to_product(M, S, bn, wnt):
     torch.testing.assert_close(part.sum(0), want, rtol=1e-3, atol=3e-3)
 
 
-@pytest.mark.parametrize("wnt", [1, 2, 3, 4, 5, 8, 17])
+@pytest.mark.parametrize("wnt", [1, 2, 3, 4, 5])
 def test_llama3_8b_shapes(wnt):
     """The four Llama-3-8B decode projections at the serving batch (64-k and
-    32-k ring stages, split x / W rings)."""
+    32-k ring stages)."""
     M = 256
     for N, K, mode, S, bn in ((6144, 4096, 2, 5, 128), (4096, 4096, 2, 8, 128),
                               (14336, 4096, 1, 1, 128), (4096, 14336, 2, 7, 128),
-                              (4096, 4096, 2, 4, 256 if wnt < 4 or wnt == 8 else 64)):
+                              (4096, 4096, 2, 4, 256 if wnt < 4 else 64)):
         x, w = _mk(M, 2 * N if mode == 1 else N, K, seed=N + K)
         out = ops.tgemm(mode, x, w, S, bn, wnt)
         full = x.float() @ w.float().t()

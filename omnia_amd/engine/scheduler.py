@@ -36,6 +36,12 @@ class SchedulerConfig:
     # >0: prompts with at least this many uncached tokens are held for a
     # context-parallel prefill over the DP group (engine/cp.py)
     cp_threshold: int = 0
+    # >0: after this many consecutive prefill-first steps with sequences running,
+    # the next step serves the running set (decode / mixed) -- a stream of short
+    # requests that finish at prefill (so capacity keeps freeing) cannot starve
+    # the decoders indefinitely.  A closed-loop wave (<= max_batch prompts) takes
+    # far fewer prefill steps and is unaffected.
+    max_prefill_streak: int = 16
 
 
 @dataclass
@@ -54,6 +60,7 @@ class Scheduler:
         self.partial: list[Sequence] = []  # prompts mid-way through chunked prefill
         self.cp_pending: Sequence | None = None  # admitted, waiting for its CP prefill
         self.on_capped = None  # engine hook: a running sequence finished at pool capacity
+        self._streak = 0  # consecutive prefill steps taken while sequences were running
 
     # ------------------------------------------------------------ admission
     def add(self, seq: Sequence) -> None:
@@ -170,7 +177,25 @@ class Scheduler:
             s.length - s.num_cached for s in self.waiting)
 
     def schedule(self) -> StepPlan:
+        plan = self._plan()
+        if plan.kind == "prefill" and self.running:
+            self._streak += 1
+        elif plan.kind != "idle":
+            self._streak = 0
+        return plan
+
+    def _plan(self) -> StepPlan:
         cfg = self.cfg
+        if cfg.max_prefill_streak > 0 and self._streak >= cfg.max_prefill_streak and \
+                self.running:
+            decode = self._decode_rows()
+            if decode:
+                if cfg.mixed_budget > 0 and (self.partial or self.waiting):
+                    chunks = self._prefill_chunks(
+                        max(0, min(cfg.mixed_budget, cfg.max_prefill_tokens) - len(decode)))
+                    if chunks:
+                        return StepPlan("mixed", chunks, decode)
+                return StepPlan("decode", [], decode)
         # mixed steps only for a TRICKLE of prefill work -- a backlog that fits
         # one mixed step (open-loop arrivals while others decode): decoders keep
         # streaming, the new prompt starts at once.  A burst (a closed-loop wave:

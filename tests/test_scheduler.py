@@ -68,3 +68,34 @@ def test_idle_session_pages_counted_and_reclaimable():
     assert bm.num_free == 0 and bm.can_allocate(10)
     got = bm.allocate(10)
     assert len(got) == 10 and bm.stats["evictions"] >= 10
+
+
+def test_prefill_stream_cannot_starve_running_decoders():
+    """A stream of one-token requests (each finishes at its prefill, so capacity
+    keeps freeing) gets prefill-first steps; after ``max_prefill_streak`` of them
+    the running sequence is served anyway, and the streak restarts."""
+    from omnia_amd.engine.sequence import FinishReason
+
+    bm = BlockManager(4096, 16)
+    sched = Scheduler(SchedulerConfig(max_batch=4, max_prefill_tokens=64,
+                                      max_prefill_streak=5), bm)
+    r = _running(sched, 16, 3)
+    kinds = []
+    for i in range(40):
+        sched.add(Sequence(prompt=list(range(1, 33)), params=SamplingParams(max_tokens=1)))
+        plan = sched.schedule()
+        kinds.append(plan.kind)
+        for s, _ in plan.prefill:  # the one-token requests finish at their prefill
+            if s is not r and s.num_cached + _ >= len(s.prompt):
+                s.num_cached = len(s.prompt)
+                sched.finish(s, FinishReason.LENGTH)
+        if plan.kind == "decode":
+            assert plan.decode == [r]
+    assert kinds[:6] == ["prefill"] * 5 + ["decode"]
+    assert kinds.count("decode") >= 6
+    # unbounded (0) keeps the old prefill-first behaviour
+    sched2 = Scheduler(SchedulerConfig(max_batch=4, max_prefill_tokens=64,
+                                       max_prefill_streak=0), BlockManager(4096, 16))
+    _running(sched2, 16, 3)
+    sched2.add(Sequence(prompt=list(range(1, 33)), params=SamplingParams(max_tokens=1)))
+    assert sched2.schedule().kind == "prefill"

@@ -41,7 +41,32 @@ log = logging.getLogger("omnia.pods")
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+_next_port: dict = {}
+
+
 def free_port() -> int:
+    """A port for a pod process to listen on.
+
+    bind(0) draws from the kernel's ephemeral range, so processes choosing at
+    the same moment can draw the same port -- with 8 bench replicas starting
+    ~5 servers each, a birthday collision is a few-percent event that kills a
+    replica.  With ``OMNIA_PORT_BASE`` set (bench.py gives every local rank its
+    own window below the ephemeral range) ports are handed out sequentially
+    from that window, skipping any that are taken; ``OMNIA_PORT_SPAN`` bounds
+    the window (default 200)."""
+    base = os.environ.get("OMNIA_PORT_BASE", "")
+    if base.isdigit():
+        lo = int(base)
+        span = int(os.environ.get("OMNIA_PORT_SPAN", "200"))
+        for _ in range(span):
+            port = _next_port.get(lo, lo)
+            _next_port[lo] = lo + (port + 1 - lo) % span
+            with socket.socket() as s:
+                try:
+                    s.bind(("127.0.0.1", port))
+                except OSError:
+                    continue
+            return port
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]

@@ -445,6 +445,229 @@ __global__ __launch_bounds__(64 * NW) void prefill_attn_kernel(
   }
 }
 
+
+// ----------------------------------------------------------- prefill, 32-row waves
+// grid: (Hq / HB, n_tiles of 32 query rows)   block: 64 * HB
+// One wave = 32 query rows of one head; the HB waves of a block are HB query
+// heads of the same KV head over the SAME rows (GQA), so every 64-key K / V
+// tile staged in LDS feeds HB heads and no wave of the block runs a causal
+// tile the others skip.  Swapped products on 32x32x16 MFMA:
+//   S^T = K . Q^T   lane (q = l&31, hi = l>>5) holds 32 of its row's 64 scores
+//                   (keys half*32 + crow(r, hi), crow = (r&3) + 8(r>>2) + 4hi),
+//                   so row max / sum are in-lane plus one xor-32 shuffle;
+//   O^T += V^T . P^T  the P^T B operand of k-step s is the lane's OWN scores
+//                   r = 8(s&1)+j of half s>>1 (no lane exchange): the k slots
+//                   are permuted to those keys, and the V^T A operand reads the
+//                   same keys -- two runs of 4 -- by ds_read_b64_tr_b16 from a
+//                   row-major V image.
+// Half the LDS bytes per MFMA of the 16-row kernel above (32 rows share every
+// K / V fragment) and no cross-lane softmax beyond one shuffle per statistic.
+__device__ __forceinline__ float16v mfma32(short8 a, short8 b, float16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// byte offset of 16-B chunk ch of row `row` in a [64][256 B] image: serves the
+// ds_read_b128 row reads (K) and the transposed reads (V) conflict-free
+__device__ __forceinline__ int img(int row, int ch) {
+  return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+template <int BS, int HB>
+__global__ __launch_bounds__(64 * HB, HB == 4 ? 2 : 1) void prefill_attn32_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+    const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ q_start_loc, const int* __restrict__ seq_lens,
+    const int* __restrict__ tile_seq, const int* __restrict__ tile_q0, int hkv, int64_t q_stride,
+    int64_t out_stride, float scale_log2, float* __restrict__ lse_out,
+    const int* __restrict__ kv_lens) {
+  // two K | V stages: the next tile is written while this one is still read,
+  // one barrier per tile
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * 64 * 256];
+  // the sequence's page indices for the first kMaxPages pages, staged once: a K/V
+  // prefetch is then ONE global load deep instead of a page-table load followed
+  // by the data load it feeds
+  constexpr int kMaxPages = 1024;
+  __shared__ int pg_lds[kMaxPages];
+
+  const int hq = gridDim.x * HB;
+  const int G = hq / hkv;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = blockIdx.x * HB + w;
+  const int kvh = blockIdx.x * HB / G;
+  const int tile = blockIdx.y;
+  const int s = tile_seq[tile], q0 = tile_q0[tile];
+  const int qs = q_start_loc[s], qlen = q_start_loc[s + 1] - qs;
+  const int ctx = seq_lens[s];
+  const int off = ctx - qlen;
+  const int ql = lane & 31, hi = lane >> 5;
+  const int* bt = block_tables + (int64_t)s * bt_stride;
+
+  const int qr = q0 + ql;
+  const bool row_ok = qr < qlen;
+  const int qr_c = row_ok ? qr : qlen - 1;
+  const int qpos = off + qr_c;
+  short8 qf[8];
+  {
+    const bf16_t* qrow = q + (int64_t)(qs + qr_c) * q_stride + h * D;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      qf[ks] = *reinterpret_cast<const short8*>(qrow + 16 * ks + 8 * hi);
+  }
+  const int last_row = min(q0 + 31, qlen - 1);
+  const int klim = kv_lens ? kv_lens[s] : 0x7fffffff;
+  const int kv_end = min(off + last_row + 1, klim);
+  const int ntiles = (kv_end + 63) / 64;
+  const int min_qpos = off + q0;
+
+  const int npg = min((kv_end + BS - 1) / BS, kMaxPages);
+  for (int i = tid; i < npg; i += 64 * HB) pg_lds[i] = bt[i];
+  __syncthreads();
+
+  // K / V tiles go global -> LDS by LDS-DMA (16 B per lane, 4 rows x 256 B per
+  // wave instruction, no staging registers); the image's XOR is applied to the
+  // per-lane SOURCE chunk (it is an involution).  Keys past kv_end re-read the
+  // last valid key: their scores are masked, so P = 0 meets finite V rows.
+  constexpr int NCH = 16 / HB;  // wave instructions per wave per 64-key tensor tile
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  auto dma = [&](int t, int buf) {
+    char* Kl = lds + buf * 2 * 64 * 256;
+    char* Vl = Kl + 64 * 256;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int inst = w * NCH + i;
+      const int row = 4 * inst + (lane >> 4), c = lane & 15;
+      const int key = min(t * 64 + row, kv_end - 1);
+      const int pi = key / BS;
+      const int page = pi < kMaxPages ? pg_lds[pi] : bt[pi];
+      const int64_t base = (((int64_t)page * hkv + kvh) * BS + (key % BS)) * D +
+                           8 * (c ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+      __builtin_amdgcn_global_load_lds((const void*)(kc + base), (lds_ptr_t)(Kl + inst * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(vc + base), (lds_ptr_t)(Vl + inst * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  float m_run = -INFINITY, l_run = 0.f;
+  float16v o[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+
+  // transposed-read lane roles: 16-lane group g = lane >> 4 covers d columns
+  // 16 (g & 1) .. +15 of a 32-column block for k-slot half hi = g >> 1; lane
+  // 4 qg + p of the group addresses key row qg, columns 4p .. 4p+3
+  const int g = lane >> 4, qg = (lane & 15) >> 2, pp = lane & 3;
+
+  dma(0, 0);
+  __syncthreads();  // vmcnt(0) + barrier: every wave's part of tile 0 landed
+  for (int t = 0; t < ntiles; ++t) {
+    // the other stage was last read in tile t-1, before the previous barrier
+    if (t + 1 < ntiles) dma(t + 1, (t + 1) & 1);
+    const char* Kl = lds + (t & 1) * 2 * 64 * 256;
+    const char* Vl = Kl + 64 * 256;
+    const int k0 = t * 64;
+    float16v sacc[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[half][r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const short8 a = *reinterpret_cast<const short8*>(Kl + img(half * 32 + ql, 2 * ks + hi));
+        sacc[half] = mfma32(a, qf[ks], sacc[half]);
+      }
+    }
+    // causal / block mask only on tiles that reach past this wave's first query
+    // (a wave-uniform branch): keys past `lim` (relative to k0) score -inf.
+    // Scores stay unscaled here; the scale rides the exponent's FMA.
+    float mloc = -INFINITY;
+    if (k0 + 63 > min(min_qpos, klim - 1)) {
+      const int lim = min(qpos, klim - 1) - k0 - 4 * hi;
+#pragma unroll
+      for (int half = 0; half < 2; ++half)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v =
+              half * 32 + (r & 3) + 8 * (r >> 2) > lim ? -INFINITY : sacc[half][r];
+          sacc[half][r] = v;
+          mloc = fmaxf(mloc, v);
+        }
+    } else {
+#pragma unroll
+      for (int half = 0; half < 2; ++half)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, sacc[half][r]);
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64)) * scale_log2;
+    // lazy rescale: the running max moves only when a row's max grows by more
+    // than 2^8 (P <= 256 is exact enough in bf16 / fp32); the O / l rescale is
+    // skipped when no row of the wave moved (wave-uniform)
+    const bool grow = mloc > m_run + 8.f;
+    if (__builtin_amdgcn_ballot_w64(grow)) {
+      const float m_new = grow ? mloc : m_run;
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 0 on the first tile
+      l_run *= alpha;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db] *= alpha;
+      m_run = m_new;
+    }
+    // v_exp_f32 directly (arguments <= 8: underflow to 0 is the intended result)
+    float lsum = 0.f;
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[half][r], scale_log2, -m_run));
+        sacc[half][r] = p;
+        lsum += p;
+      }
+    lsum += __shfl_xor(lsum, 32, 64);
+    l_run += lsum;
+    short8 pb[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)  // native RNE convert (v_cvt_pk_bf16_f32)
+        pb[st][j] = __builtin_bit_cast(short, (__bf16)sacc[st >> 1][8 * (st & 1) + j]);
+    typedef short v4s __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      // keys of k-step st for slot half g >> 1: (st>>1)*32 + 16(st&1) + 4(g>>1) + {0..3, 8..11}
+      const int kb = (st >> 1) * 32 + 16 * (st & 1) + 4 * (g >> 1) + qg;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int ch = db * 4 + 2 * (g & 1) + (pp >> 1);
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)(Vl + img(kb, ch) + 8 * (pp & 1)));
+        v4s hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)(Vl + img(kb + 8, ch) + 8 * (pp & 1)));
+        const short8 a = __builtin_shufflevector(lo, hv, 0, 1, 2, 3, 4, 5, 6, 7);  // concat
+        o[db] = mfma32(a, pb[st], o[db]);
+      }
+    }
+    __syncthreads();  // tile t+1's DMA landed (vmcnt(0)) and tile t is read by all
+  }
+
+  if (row_ok) {
+    const float inv = 1.f / l_run;
+    bf16_t* orow = out + (int64_t)(qs + qr) * out_stride + h * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        uint2v pk;
+        pk[0] = pack_bf2(o[db][4 * m] * inv, o[db][4 * m + 1] * inv);
+        pk[1] = pack_bf2(o[db][4 * m + 2] * inv, o[db][4 * m + 3] * inv);
+        *reinterpret_cast<uint2v*>(orow + db * 32 + 8 * m + 4 * hi) = pk;
+      }
+    if (lse_out && hi == 0)
+      lse_out[(int64_t)(qs + qr) * hq + h] = (m_run + log2f(l_run)) * 0.6931471805599453f;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -524,6 +747,27 @@ int omnia_prefill_attention(void* out, const void* q, const void* k_cache, const
   int hp = hp_req > 0 ? hp_req : env_hp > 0 ? env_hp : 1;
   if (hp != 1 && hp != 2 && hp != 4) return -5;
   if (G % hp) hp = 1;
+  if (q_tile == 32) {
+    // 32-row waves, HB heads of one KV head per block (prefill_attn32_kernel)
+    const int hb = G % 4 == 0 ? 4 : G % 2 == 0 ? 2 : 1;
+    dim3 grid32(hq / hb, n_tiles), block32(64 * hb);
+#define OMNIA_PRE32(BB, HH)                                                                  \
+  prefill_attn32_kernel<BB, HH><<<grid32, block32, 0, s>>>(                                  \
+      (bf16_t*)out, (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache,        \
+      block_tables, bt_stride, q_start_loc, seq_lens, tile_seq, tile_q0, hkv, q_stride,      \
+      out_stride, scale_log2, lse_out, kv_lens)
+#define OMNIA_PRE32_HB(BB)                 \
+  if (hb == 4) OMNIA_PRE32(BB, 4);         \
+  else if (hb == 2) OMNIA_PRE32(BB, 2);    \
+  else OMNIA_PRE32(BB, 1);
+    if (block_size == 16) { OMNIA_PRE32_HB(16) }
+    else if (block_size == 32) { OMNIA_PRE32_HB(32) }
+    else if (block_size == 64) { OMNIA_PRE32_HB(64) }
+    else return -3;
+#undef OMNIA_PRE32_HB
+#undef OMNIA_PRE32
+    return (int)hipGetLastError();
+  }
   const int nw = q_tile / 16;
   if (q_tile != 64 && q_tile != 128) return -6;
   if (nw == 8 && hp != 1) return -7;

@@ -126,7 +126,8 @@ def test_decode_attention(hq, hkv, bs, nw, monkeypatch):
 @pytest.mark.parametrize("bs", [16, 32])
 @pytest.mark.parametrize("hq,hkv,hp,qt", [(32, 8, 1, 64), (32, 8, 2, 64), (32, 8, 4, 64),
                                           (64, 8, 4, 64), (8, 8, 0, 64), (32, 8, 1, 128),
-                                          (8, 8, 1, 128)])
+                                          (8, 8, 1, 128), (32, 8, 0, 32), (64, 8, 0, 32),
+                                          (16, 8, 0, 32), (8, 8, 0, 32), (8, 1, 0, 32)])
 def test_prefill_attention(bs, hq, hkv, hp, qt):
     torch.manual_seed(4)
     # (new tokens, cached prefix) per sequence: ragged + page-boundary edges

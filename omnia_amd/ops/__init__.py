@@ -478,7 +478,7 @@ def decode_attention(q, k_cache, v_cache, block_tables, seq_lens, scale, part_si
     return r
 
 
-PREFILL_Q_TILE = int(os.environ.get("OMNIA_PREFILL_Q_TILE", "128"))  # 64 | 128 query rows
+PREFILL_Q_TILE = int(os.environ.get("OMNIA_PREFILL_Q_TILE", "32"))  # 32 (32-row waves) | 64 | 128
 
 
 def prefill_tiles(q_lens: list[int], tile: int | None = None) -> tuple[list[int], list[int]]:

@@ -481,9 +481,11 @@ __global__ __launch_bounds__(64 * HB, HB == 4 ? 2 : 1) void prefill_attn32_kerne
     const int* __restrict__ tile_seq, const int* __restrict__ tile_q0, int hkv, int64_t q_stride,
     int64_t out_stride, float scale_log2, float* __restrict__ lse_out,
     const int* __restrict__ kv_lens) {
-  // two K | V stages: the next tile is written while this one is still read,
-  // one barrier per tile
-  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * 64 * 256];
+  // two K | V stages (separate objects, so the compiler sees that fragment reads
+  // of one stage cannot alias the other stage's in-flight LDS-DMA): the next
+  // tile is written while this one is still read, one barrier per tile
+  __shared__ __attribute__((aligned(16))) char st0[2 * 64 * 256];
+  __shared__ __attribute__((aligned(16))) char st1[2 * 64 * 256];
   // the sequence's page indices for the first kMaxPages pages, staged once: a K/V
   // prefetch is then ONE global load deep instead of a page-table load followed
   // by the data load it feeds
@@ -530,17 +532,23 @@ __global__ __launch_bounds__(64 * HB, HB == 4 ? 2 : 1) void prefill_attn32_kerne
   // last valid key: their scores are masked, so P = 0 meets finite V rows.
   constexpr int NCH = 16 / HB;  // wave instructions per wave per 64-key tensor tile
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  auto dma = [&](int t, int buf) {
-    char* Kl = lds + buf * 2 * 64 * 256;
+  auto dma = [&](int t, auto BUF) {
+    char* Kl = decltype(BUF)::value ? st1 : st0;
     char* Vl = Kl + 64 * 256;
+    int page[NCH];  // all page lookups before the first DMA issue
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int key = min(t * 64 + 4 * (w * NCH + i) + (lane >> 4), kv_end - 1);
+      const int pi = key / BS;
+      const int pl = pg_lds[pi < kMaxPages ? pi : 0];  // an LDS read, not a flat one
+      page[i] = pi < kMaxPages ? pl : bt[pi];
+    }
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int inst = w * NCH + i;
       const int row = 4 * inst + (lane >> 4), c = lane & 15;
       const int key = min(t * 64 + row, kv_end - 1);
-      const int pi = key / BS;
-      const int page = pi < kMaxPages ? pg_lds[pi] : bt[pi];
-      const int64_t base = (((int64_t)page * hkv + kvh) * BS + (key % BS)) * D +
+      const int64_t base = (((int64_t)page[i] * hkv + kvh) * BS + (key % BS)) * D +
                            8 * (c ^ (((row & 3) << 2) | ((row >> 2) & 3)));
       __builtin_amdgcn_global_load_lds((const void*)(kc + base), (lds_ptr_t)(Kl + inst * 1024),
                                        16, 0, 0);
@@ -561,12 +569,20 @@ __global__ __launch_bounds__(64 * HB, HB == 4 ? 2 : 1) void prefill_attn32_kerne
   // 4 qg + p of the group addresses key row qg, columns 4p .. 4p+3
   const int g = lane >> 4, qg = (lane & 15) >> 2, pp = lane & 3;
 
-  dma(0, 0);
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  dma(0, B0{});
   __syncthreads();  // vmcnt(0) + barrier: every wave's part of tile 0 landed
-  for (int t = 0; t < ntiles; ++t) {
+  // one tile on stage BUF while the next one's DMA fills the other stage; the
+  // loop is unrolled by the two stages so every LDS address is a compile-time
+  // offset from `lds` -- with a runtime stage index hipcc cannot tell the
+  // fragment reads from the in-flight DMA's target and drains it (vmcnt(0))
+  // before the first read, which serialises the prefetch
+  auto body = [&](int t, auto BUF) {
+    constexpr int buf = decltype(BUF)::value;
     // the other stage was last read in tile t-1, before the previous barrier
-    if (t + 1 < ntiles) dma(t + 1, (t + 1) & 1);
-    const char* Kl = lds + (t & 1) * 2 * 64 * 256;
+    if (t + 1 < ntiles) dma(t + 1, std::integral_constant<int, 1 - buf>{});
+    const char* Kl = buf ? st1 : st0;
     const char* Vl = Kl + 64 * 256;
     const int k0 = t * 64;
     float16v sacc[2];
@@ -649,6 +665,10 @@ __global__ __launch_bounds__(64 * HB, HB == 4 ? 2 : 1) void prefill_attn32_kerne
       }
     }
     __syncthreads();  // tile t+1's DMA landed (vmcnt(0)) and tile t is read by all
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    body(t, B0{});
+    if (t + 1 < ntiles) body(t + 1, B1{});
   }
 
   if (row_ok) {

@@ -1,7 +1,16 @@
 import os
 import sys
 
-import pytest
+# Under pytest-xdist every worker (and every engine / pod process its tests
+# start) would otherwise run torch's CPU ops on as many OpenMP threads as the
+# machine has cores: with 4 workers on 8 cores the spinning thread pools
+# oversubscribe the CPUs and tiny-model tests slow down 20-100x (a 6 s property
+# test past a 600 s timeout).  Give each worker its share; children inherit it.
+_workers = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "0") or 0)
+if _workers > 1 and "OMP_NUM_THREADS" not in os.environ:
+    os.environ["OMP_NUM_THREADS"] = str(max(1, (os.cpu_count() or 1) // _workers))
+
+import pytest  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:

@@ -524,7 +524,12 @@ class ModelRunner:
         out_host[:n].copy_(tok, non_blocking=True)
         ev = self._event()
         self.pf_events[slot] = ev
-        return DecodeHandle(sample_seqs, out_host, ev, n, "mixed")
+        h = DecodeHandle(sample_seqs, out_host, ev, n, "mixed")
+        if self.logit_tap is not None:
+            # snapshot now, recorded at collect: the pipelined loop collects the
+            # previous step after this launch, and a sequence's rows must stay in order
+            h.tap = logits[:n].clone()
+        return h
 
     def _sample_eager(self, logits, seqs: list[Sequence]) -> list[int]:
         n = len(seqs)
@@ -820,8 +825,16 @@ class ModelRunner:
         gil_ns = h.event.synchronize()
         if gil_ns:
             self.stats["gil_wait_s"] += gil_ns * 1e-9
+        rows = None
         if self._tap is not None and h.kind == "decode":
-            self._tap_rows(h.seqs, h.tap if h.tap is not None else self._tap[: h.n])
+            rows = h.tap if h.tap is not None else self._tap[: h.n]
+        elif h.kind == "mixed" and h.tap is not None:
+            rows = h.tap
+        if rows is not None:
+            # rows of sequences that finished while this step was in flight are
+            # speculative (the engine drops their tokens): not part of the record
+            keep = [i for i, s in enumerate(h.seqs) if not s.is_finished]
+            self._tap_rows([h.seqs[i] for i in keep], rows[keep])
         return h.out_host[: h.n].tolist()
 
     def run_decode(self, seqs: list[Sequence]) -> list[int]:

@@ -292,26 +292,32 @@ class LlamaModel:
             o = ops.decode_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.seq_lens,
                                      self.scale, part_size=part, workspace=ws)
         elif fb.num_decode:
-            # mixed step: decode rows on the split-K decode kernel (K/V read once per
-            # GQA group), prefill chunks on the flash prefill kernel, one output
-            Bd = fb.num_decode
-            o = torch.empty_like(q3) if q3.is_contiguous() else torch.empty(
-                T, self.hq, D, dtype=q3.dtype, device=q3.device)
-            mb = fb.dec_block_tables.shape[1]
-            part = self.decode_part(Bd, mb * kv.block_size)
-            ws = self._decode_ws(1 << max(0, Bd - 1).bit_length(), mb, kv.block_size, h.device,
-                                 part)  # pow2 rows: few workspace shapes across mixed steps
-            ops.decode_attention(q3[:Bd], kv.k[li], kv.v[li], fb.dec_block_tables,
-                                 fb.dec_seq_lens, self.scale, part_size=part, workspace=ws,
-                                 out=o[:Bd])
-            if T > Bd:
-                ops.prefill_attention(q3[Bd:], kv.k[li], kv.v[li], fb.block_tables,
-                                      fb.q_start_loc, fb.seq_lens, self.scale, fb.tile_seq,
-                                      fb.tile_q0, out=o[Bd:])
+            o = self._mixed_attention(li, q3, fb, kv)
         else:
             o = ops.prefill_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.q_start_loc,
                                       fb.seq_lens, self.scale, fb.tile_seq, fb.tile_q0)
         return self._proj("o", o.view(T, self.hq * D), self.w["layers"][li]["o"], fb.is_decode)
+
+    def _mixed_attention(self, li: int, q3: torch.Tensor, fb: ForwardBatch, kv: KVCache):
+        """Mixed step: decode rows (the first ``num_decode``) on the split-K decode
+        kernel (K/V read once per GQA group), prefill chunks on the flash prefill
+        kernel, one output."""
+        T, D = q3.shape[0], self.cfg.head_dim
+        Bd = fb.num_decode
+        o = torch.empty_like(q3) if q3.is_contiguous() else torch.empty(
+            T, self.hq, D, dtype=q3.dtype, device=q3.device)
+        mb = fb.dec_block_tables.shape[1]
+        part = self.decode_part(Bd, mb * kv.block_size)
+        ws = self._decode_ws(1 << max(0, Bd - 1).bit_length(), mb, kv.block_size, q3.device,
+                             part)  # pow2 rows: few workspace shapes across mixed steps
+        ops.decode_attention(q3[:Bd], kv.k[li], kv.v[li], fb.dec_block_tables,
+                             fb.dec_seq_lens, self.scale, part_size=part, workspace=ws,
+                             out=o[:Bd])
+        if T > Bd:
+            ops.prefill_attention(q3[Bd:], kv.k[li], kv.v[li], fb.block_tables,
+                                  fb.q_start_loc, fb.seq_lens, self.scale, fb.tile_seq,
+                                  fb.tile_q0, out=o[Bd:])
+        return o
 
     def decode_part(self, batch: int, max_ctx: int) -> int:
         """Split-K partition length: as long as possible (fewer partials to merge,
@@ -342,11 +348,12 @@ class LlamaModel:
     PGEMM_MIN_ROWS = int(os.environ.get("OMNIA_PGEMM_MIN_ROWS", "257"))
 
     def _use_fused(self, fb: ForwardBatch) -> bool:
-        """Pure prefill chunks on one GPU run the fused-epilogue prefill layer:
-        QKV+RoPE+KV-write, O+residual, gate_up+SwiGLU, down+residual, with the
-        RMSNorms riding the epilogues (no standalone norm / SwiGLU / RoPE launch)."""
+        """Prefill chunks -- and mixed steps, whose decode rows ride the same
+        GEMMs -- on one GPU run the fused-epilogue prefill layer: QKV+RoPE+KV-write,
+        O+residual, gate_up+SwiGLU, down+residual, with the RMSNorms riding the
+        epilogues (no standalone norm / SwiGLU / RoPE launch)."""
         if not (self.use_pgemm and self.device.type == "cuda" and not fb.is_decode
-                and not fb.num_decode and fb.cp is None and self.tp == 1):
+                and fb.cp is None and self.tp == 1):
             return False
         if fb.input_ids.shape[0] < self.PGEMM_MIN_ROWS:
             return False
@@ -373,9 +380,12 @@ class LlamaModel:
                       positions=fb.positions, cos_sin=self.cos_sin, k_cache=kv.k[li],
                       v_cache=kv.v[li], slots=fb.slots, hq=self.hq, hkv=self.hkv,
                       block_size=kv.block_size)
-            o = ops.prefill_attention(q.view(T, self.hq, D), kv.k[li], kv.v[li], fb.block_tables,
-                                      fb.q_start_loc, fb.seq_lens, self.scale, fb.tile_seq,
-                                      fb.tile_q0)
+            if fb.num_decode:
+                o = self._mixed_attention(li, q.view(T, self.hq, D), fb, kv)
+            else:
+                o = ops.prefill_attention(q.view(T, self.hq, D), kv.k[li], kv.v[li],
+                                          fb.block_tables, fb.q_start_loc, fb.seq_lens,
+                                          self.scale, fb.tile_seq, fb.tile_q0)
             ops.pgemm(2, o.view(T, self.hq * D), layer["o"], out=h, ss_out=ss_mid)
             ops.pgemm(1, h, layer["gate_up"], out=act, ss_in=ss_mid, inv_d=inv_d, eps=eps)
             ops.pgemm(2, act, layer["down"], out=h, ss_out=ss_out)

@@ -247,3 +247,39 @@ def test_gpu_mixed_steps_match_dense_oracle():
     frac, worst = _check(mc, eng.model.w, seqs, eng.runner.logit_tap, 0.04)
     print(f"mixed steps: {eng.counters['steps_mixed']}, worst rel err {worst:.4f}")
     assert frac == 1.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_gpu_fused_mixed_steps_match_dense_oracle(pipeline):
+    """Mixed steps of >= 257 rows run the fused-epilogue prefill layer (pgemm.hip,
+    the decode rows riding the prefill GEMMs; split decode / prefill attention
+    in between) -- against the dense oracle, synchronous and pipelined."""
+    mc = resolve("llama-3-8b").replace(name="llama-3-8b-2l", num_layers=2)
+    eng = LLMEngine(EngineConfig(model=mc.name, device="cuda", num_blocks=512, block_size=16,
+                                 max_batch=8, max_model_len=1024, max_prefill_tokens=640,
+                                 pipeline=pipeline, seed=11, mixed_budget=640,
+                                 mixed_backlog=2048), model_cfg=mc)
+    eng.runner.enable_logit_tap()
+    model = eng.model
+    fused = {"mixed": 0}
+    orig = model._fused_residual
+
+    def counted(fb, kv):
+        if fb.num_decode:
+            fused["mixed"] += 1
+        return orig(fb, kv)
+
+    model._fused_residual = counted
+    rng = random.Random(5)
+    V = mc.vocab_size
+    p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+    seqs = [eng.add_request([rng.randrange(10, V - 10) for _ in range(n)], p) for n in (90, 41)]
+    for _ in range(3):
+        eng.step()
+    seqs += [eng.add_request([rng.randrange(10, V - 10) for _ in range(n)], p) for n in (420, 330)]
+    eng.run_until_done()
+    assert fused["mixed"] >= 1, eng.counters
+    frac, worst = _check(mc, eng.model.w, seqs, eng.runner.logit_tap, 0.04)
+    print(f"fused mixed steps: {fused['mixed']}, worst rel err {worst:.4f}")
+    assert frac == 1.0

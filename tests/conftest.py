@@ -12,6 +12,19 @@ if _workers > 1 and "OMP_NUM_THREADS" not in os.environ:
 
 import pytest  # noqa: E402
 
+try:  # property tests draw fresh examples every run: no on-disk example database,
+    # and hypothesis's own caches go to a temp dir, not the repository
+    import tempfile
+
+    os.environ.setdefault("HYPOTHESIS_STORAGE_DIRECTORY",
+                          os.path.join(tempfile.gettempdir(), "omnia-hypothesis"))
+    from hypothesis import settings as _hyp_settings
+
+    _hyp_settings.register_profile("omnia", database=None)
+    _hyp_settings.load_profile("omnia")
+except ImportError:  # pragma: no cover
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -343,7 +343,10 @@ class ColdArchive:
         raw = self.blob.get(ent["batch"])
         if raw is None:
             return None
-        t = pq.read_table(io.BytesIO(raw)).to_pydict()
+        # one archive batch is small: decode it on this thread, not on arrow's
+        # thread pool (a pooled read segfaulted once inside read_table during a
+        # loaded parallel test run; single-threaded decode avoids the pool)
+        t = pq.read_table(io.BytesIO(raw), use_threads=False).to_pydict()
         sess, msgs = None, []
         for i, s in enumerate(t["session_id"]):
             if s != sid:

@@ -141,6 +141,10 @@ class LLMEngine:
                                  weights=weights, decode_part_size=cfg.decode_part_size,
                                  ep_mode=cfg.ep_mode)
         self.load_s = time.perf_counter() - t0
+        # tile-packed decode weights: allocated before the KV pool is sized from
+        # what is left of HBM
+        self.packed_bytes = (self.model.prepack_decode(cfg.max_batch)
+                             if hasattr(self.model, "prepack_decode") else 0)
         nb = cfg.num_blocks or self.kv_pool_blocks(cfg, self.model_cfg, self.model.tp, dev, dtype)
         runner_cls = ModelRunner
         # DP-attention + EP: every forward is a collective of the EP group

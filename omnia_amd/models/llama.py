@@ -215,6 +215,55 @@ class LlamaModel:
             return None
         return ops.wgemm_config(M, N, K, mode)
 
+    # tile-packed decode weights (ops.tgemm_pack): a second, stage-contiguous copy
+    # of each projection the tuned table sends to tgemm.  Streamed alone, row-major
+    # weights (128-B pieces of rows 2*K bytes apart) reach ~4.5 TB/s and packed
+    # ones ~6.0 TB/s; inside the full kernel, next to the x re-reads and the
+    # MFMAs, the gain is 0-3 % per projection (profiles/r5/decode_gemm/), so the
+    # copy (~14 GB for Llama-3-8B, taken from the KV pool) is opt-in:
+    # OMNIA_TGEMM_PACK=1 builds it before the KV pool is sized, when it fits
+    # pack_budget_frac of HBM.
+    pack_budget_frac = 0.10  # of the device's HBM
+
+    def prepack_decode(self, max_batch: int) -> int:
+        """Pack the decode projections for every batch bucket up to ``max_batch``;
+        returns the bytes packed (0: off / nothing on tgemm / over budget)."""
+        self._packed = {}
+        env = os.environ.get("OMNIA_TGEMM_PACK", "0")
+        if env not in ("1", "force") or self.device.type != "cuda" or self.tp != 1 \
+                or self.cfg.is_moe:
+            return 0
+        want = {}
+        top = next((b for b in ops.WGEMM_BUCKETS if b >= max_batch), ops.WGEMM_BUCKETS[-1])
+        for b in (b for b in ops.WGEMM_BUCKETS if b <= top):
+            for layer in self.w["layers"]:
+                for key, mode in (("qkv", 0), ("o", 0), ("down", 0), ("gate_up", 1)):
+                    w = layer[key]
+                    N = w.shape[0] // 2 if mode == 1 else w.shape[0]
+                    cfg = ops.wgemm_config(b, N, w.shape[1], mode)
+                    if cfg is None or cfg[1] >= 0 or (-1 - cfg[1]) & 2:
+                        continue  # not tgemm, or its 32-k stage form
+                    pmode = 1 if mode == 1 and cfg[2] == 1 else 0
+                    want[(w.data_ptr(), cfg[0], pmode)] = w
+        total = sum(w.numel() * w.element_size() for w in want.values())
+        cap = torch.cuda.get_device_properties(self.device).total_memory * self.pack_budget_frac
+        if not want or (env != "force" and total > cap):
+            return 0
+        for (ptr, bn, pmode), w in want.items():
+            self._packed[(ptr, bn, pmode)] = ops.tgemm_pack(w, bn, pmode)
+        return total
+
+    def _wgemm(self, mode: int, x: torch.Tensor, w: torch.Tensor, S: int, nw: int, nwaves: int,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+        """ops.wgemm, on the tile-packed copy of ``w`` when one exists for this
+        tgemm config."""
+        packed = getattr(self, "_packed", None)
+        if packed and nwaves < 0:
+            wp = packed.get((w.data_ptr(), nw, 1 if mode == 1 else 0))
+            if wp is not None:
+                return ops.tgemm(mode, x, wp, S, nw, (-1 - nwaves) | 8, out)
+        return ops.wgemm(mode, x, w, S, nw, nwaves, out=out)
+
     def _parts(self, tag, S: int, M: int, N: int) -> torch.Tensor:
         key = ("parts", tag, S, M, N)
         buf = self._ws.get(key)
@@ -232,7 +281,7 @@ class LlamaModel:
         if cfg is None:
             return ops.linear(x, w)
         nw, nwaves, S = cfg
-        return Parts(ops.wgemm(2, x, w, S, nw, nwaves, out=self._parts(tag, S, M, w.shape[0])))
+        return Parts(self._wgemm(2, x, w, S, nw, nwaves, out=self._parts(tag, S, M, w.shape[0])))
 
     def add_norm(self, x, residual: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         """residual += x (TP-reduced); returns RMSNorm(residual) * w."""
@@ -257,10 +306,10 @@ class LlamaModel:
         else:
             nw, nwaves, S = cfg
             if S == 1:
-                a = ops.wgemm(1, h, layer["gate_up"], 1, nw, nwaves)
+                a = self._wgemm(1, h, layer["gate_up"], 1, nw, nwaves)
             else:
-                a = ops.splitk_swiglu(ops.wgemm(2, h, layer["gate_up"], S, nw, nwaves,
-                                                out=self._parts("gu", S, M, I2)))
+                a = ops.splitk_swiglu(self._wgemm(2, h, layer["gate_up"], S, nw, nwaves,
+                                                  out=self._parts("gu", S, M, I2)))
         return self._proj("down", a, layer["down"], is_decode)
 
     def attention(self, li: int, h: torch.Tensor, fb: ForwardBatch, kv: KVCache):

@@ -294,6 +294,38 @@ def tgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, bn: int 
     return out
 
 
+def tgemm_pack(w: torch.Tensor, bn: int, mode: int) -> torch.Tensor:
+    """``w`` [R, K] re-laid for ``tgemm`` (wnt bit 3): [tile][k-stage][bn rows][64],
+    the rows of each tile in the kernel's order (mode 1: every wave's gate rows
+    then the matching up rows of W = [Wg; Wu]) and each row's eight 16-B chunks
+    pre-permuted by the LDS bank swizzle (stored chunk p = chunk p ^ (row & 7)),
+    so one k-stage of a tile is one contiguous run the LDS-DMA reads lane by
+    lane.  Returned with the original [R, K] shape (same elements, new order)."""
+    R, K = w.shape
+    BK = 64
+    if K % BK:
+        raise ValueError("tgemm_pack: K must be a multiple of 64")
+    nk = K // BK
+    wtn = bn // (4 if bn >= 256 else 2)
+    dev = w.device
+    rr = torch.arange(bn, device=dev)
+    if mode == 1:
+        N = R // 2
+        ntiles = N // (bn // 2)
+        wv, q = rr // wtn, rr % wtn
+        f0 = torch.arange(ntiles, device=dev)[:, None] * (bn // 2) + (wv * (wtn // 2))[None, :]
+        rows = torch.where((q < wtn // 2)[None, :], f0 + q[None, :], N + f0 + (q - wtn // 2)[None, :])
+    else:
+        ntiles = R // bn
+        rows = torch.arange(ntiles, device=dev)[:, None] * bn + rr[None, :]
+    if ntiles * bn != R:
+        raise ValueError("tgemm_pack: rows are not a whole number of tiles")
+    t = w[rows.reshape(-1)].view(ntiles, bn, nk, 8, 8)
+    perm = torch.arange(8, device=dev)[None, :] ^ (rr[:, None] & 7)  # [bn, 8]
+    t = torch.gather(t, 3, perm[None, :, None, :, None].expand(ntiles, bn, nk, 8, 8))
+    return t.permute(0, 2, 1, 3, 4).contiguous().view(R, K)
+
+
 def pgemm(epi: int, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
           ss_in: torch.Tensor | None = None, inv_d: float = 0.0, eps: float = 0.0,
           ss_out: torch.Tensor | None = None, positions=None, cos_sin=None, k_cache=None,

@@ -93,7 +93,13 @@ struct Geo {
 // reads after each barrier and then waiting on them; the ring also keeps one more
 // stage in flight, since a stage's buffer is free as soon as its fragments are
 // in registers.
-template <int BN, int MODE, int WNT, int BK, int PIPE>
+// PK: W is tile-packed (ops.tgemm_pack): [tile][k-step][BN rows][64], rows in
+// this kernel's tile order and each row's 16-B chunks pre-permuted by the LDS
+// swizzle, so a stage's weights are ONE contiguous BN x 128 B run that the
+// LDS-DMA reads lane-linearly.  Row-major W hands every stage 128-B pieces of BN
+// rows 2*K bytes apart: that pattern streams at ~4.5 TB/s, the packed one at
+// ~6.0 TB/s (scripts/microbench/w_depth.hip, profiles/r5/decode_gemm/).
+template <int BN, int MODE, int WNT, int BK, int PIPE, int PK = 0>
 __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
                                                        const bf16_t* __restrict__ X,
                                                        const bf16_t* __restrict__ W, int M, int N,
@@ -153,8 +159,10 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
     } else {
       wrow = (int64_t)tile * BN + rr;
     }
-    b_src[i] = W + wrow * K + (int64_t)kb * BK + gchunk(rr) * 8;
+    b_src[i] = PK ? W + ((int64_t)tile * (K / BK) + kb) * BN * BK + rr * BK + lp * 8
+                  : W + wrow * K + (int64_t)kb * BK + gchunk(rr) * 8;
   }
+  constexpr int64_t WSTEP = PK ? BN * BK : BK;  // W elements per k-stage
   const int a_dst0 = (RPI * w * A_IN) * BK;              // element offsets inside a stage
   const int b_dst0 = 256 * BK + (RPI * w * B_IN) * BK;
 
@@ -167,7 +175,7 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
                                        (lds_ptr_t)(base + a_dst0 + i * 512), 16, 0, 0);
 #pragma unroll
     for (int i = 0; i < B_IN; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + koff),
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + kl * WSTEP),
                                        (lds_ptr_t)(base + b_dst0 + i * 512), 16, 0,
                                        WNT ? 2 : 0);
   };
@@ -333,14 +341,34 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
 }
 
 // wnt bit 0: non-temporal W loads; bit 1: 32-k stages (BN >= 128); bit 2:
-// register-pipelined fragment reads (BN <= 128, 64-k stages)
+// register-pipelined fragment reads (BN <= 128, 64-k stages); bit 3: W is
+// tile-packed for this bn / mode (ops.tgemm_pack; 64-k stages)
 template <int BN, int MODE>
 int launch_bn(void* out, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int ldo,
               int wnt, hipStream_t s) {
   const int ntiles = MODE == 1 ? N / (BN / 2) : N / BN;
   const dim3 grid(ntiles * S * ((M + 255) / 256)), block(512);
-  const bool nt = wnt & 1, bk32 = wnt & 2, pipe = wnt & 4;
+  const bool nt = wnt & 1, bk32 = wnt & 2, pipe = wnt & 4, pk = wnt & 8;
   if (bk32 && pipe) return -22;
+  if (pk) {  // tile-packed W: 64-k stages, shared or register-pipelined ring
+    if (bk32) return -25;
+    if constexpr (BN <= 128) {
+      if (pipe) {
+        if (nt)
+          tgemm_kernel<BN, MODE, 1, 64, 1, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+        else
+          tgemm_kernel<BN, MODE, 0, 64, 1, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+        return (int)hipGetLastError();
+      }
+    } else {
+      if (pipe) return -23;
+    }
+    if (nt)
+      tgemm_kernel<BN, MODE, 1, 64, 0, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+    else
+      tgemm_kernel<BN, MODE, 0, 64, 0, 1><<<grid, block, 0, s>>>(out, X, W, M, N, K, S, ldo);
+    return (int)hipGetLastError();
+  }
   if constexpr (BN >= 128) {
     if (bk32) {
       if (nt)

@@ -44,21 +44,19 @@ def main():
         copies = max(2, (1 << 30) // nbytes + 1)
         ws = [torch.randn(rows, K, device="cuda").mul_(0.02).to(torch.bfloat16)
               for _ in range(copies)]
+        packed = {}
         for M in (256, 192, 128, 64):
             x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
             if M != 256 and not a.all_m:
                 continue
             cfgs = []
-            # wnt bits 3-4: split x / W rings (tgemm.hip Rings)
-            if name == "gate_up":
-                cfgs += [(1, 128, 1, w) for w in (0, 8, 64, 128, 160, 192)]
-                cfgs += [(2, 256, 2, 8), (2, 256, 2, 128), (2, 256, 2, 160)]
-            elif name == "down":
-                cfgs += [(2, 128, 8, w) for w in (4, 8, 64, 128, 160, 192)]
-            elif name == "o":
-                cfgs += [(2, 64, 4, w) for w in (0, 8, 64, 128, 160, 192)]
-            else:
-                cfgs += [(2, 128, 5, w) for w in (0, 8, 64, 128, 160, 192)]
+            # (mode, bn, S, wnt); wnt bit 3 = tile-packed weights (ops.tgemm_pack)
+            base = {"gate_up": [(1, 128, 1, 0), (1, 128, 1, 4), (1, 64, 1, 0), (2, 256, 2, 0)],
+                    "down": [(2, 128, 8, 4), (2, 128, 8, 0), (2, 128, 7, 4), (2, 64, 4, 4)],
+                    "qkv": [(2, 128, 5, 0), (2, 128, 4, 0), (2, 64, 4, 4), (2, 128, 6, 4)],
+                    "o": [(2, 64, 4, 0), (2, 64, 4, 4), (2, 128, 8, 0), (2, 64, 8, 0)]}[name]
+            for c in base:
+                cfgs += [c, c[:3] + (c[3] | 8,)]
             for mode, bn, S, wnt in cfgs:
                 N = rows // 2 if mode == 1 else rows
                 cols = bn // 2 if mode == 1 else bn
@@ -66,24 +64,30 @@ def main():
                 blocks = ntiles * S
                 out = (torch.empty(S, M, N, device="cuda") if mode == 2 else
                        torch.empty(M, N, device="cuda", dtype=torch.bfloat16))
+                wsrc = ws
+                if wnt & 8:
+                    key = (bn, 1 if mode == 1 else 0)
+                    if key not in packed:
+                        packed[key] = [ops.tgemm_pack(w_, bn, key[1]) for w_ in ws]
+                    wsrc = packed[key]
                 try:
-                    t = bench(lambda i: ops.tgemm(mode, x, ws[i % copies], S, bn, wnt, out=out))
+                    t = bench(lambda i: ops.tgemm(mode, x, wsrc[i % copies], S, bn, wnt, out=out))
                 except RuntimeError as e:
                     print("skip", name, M, mode, bn, S, e, flush=True)
                     continue
-                ops.tgemm(mode, x, ws[0], S, bn, wnt, out=out)
+                ops.tgemm(mode, x, wsrc[0], S, bn, wnt, out=out)
                 full = x.float() @ ws[0].float().t()
                 if mode == 1:
                     want = torch.nn.functional.silu(full[:, :N]) * full[:, N:]
                     got = out.float()
                 else:
                     want, got = full, out.sum(0)
-                err = ((got - want).abs().max() / want.abs().max()).item() if wnt < 32 else -1
+                err = ((got - want).abs().max() / want.abs().max()).item() 
                 wcu = bn * (K // S) * 2 / 1024
                 xcu = M * (K // S) * 2 / 1024
                 print(f"{name:8s} {M:4d} {mode:4d} {bn:4d} {S:3d} {wnt:3d} {blocks:6d} {t:7.1f} "
                       f"{wcu:8.0f} {xcu:8.0f} {nbytes / t / 1e3:7.0f}  err {err:.4f}", flush=True)
-        del ws
+        del ws, packed
         torch.cuda.empty_cache()
 
 

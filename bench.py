@@ -29,7 +29,11 @@ inter-token latency percentiles.
 """
 from __future__ import annotations
 
-import argparse
+import time as _time
+
+_T_START = _time.perf_counter()  # process start (phase accounting in the JSON line)
+
+import argparse  # noqa: E402
 import asyncio
 import json
 import os
@@ -539,8 +543,10 @@ def run(a, drv, ws, rank, use_gpu, host_only):
         if ws > 1:
             dist.barrier()
 
+    t_ready = time.perf_counter()
     for w in range(a.warmup):
         drv.wave(-1 - w)
+    t_warm = time.perf_counter()
     if isinstance(drv, LocalDriver):
         drv.reset_timing()
     sync()
@@ -618,6 +624,10 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(1000 * elapsed / a.steps, 3),
+            # process start -> serving pod ready (imports, model init, KV pool) and
+            # the untimed warmup waves (first-wave graph captures included)
+            "startup_s": round(t_ready - _T_START, 2),
+            "warmup_s": round(t_warm - t_ready, 2),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -199,9 +199,12 @@ class ProcessPod:
         deadline = time.monotonic() + timeout_s
         self.start_runtime()
         try:
+            # both containers start at once, as in a Kubernetes pod: the facade's
+            # own start-up (imports, listeners) overlaps the engine load, and its
+            # /readyz reports ready only once the runtime answers
+            self.start_facade()
             self._wait(self.runtime, f"http://127.0.0.1:{self.health_port}/readyz", "runtime",
                        deadline)
-            self.start_facade()
             self._wait(self.facade, f"http://127.0.0.1:{self.facade_port}/readyz", "facade",
                        deadline)
         except BaseException:

@@ -253,22 +253,36 @@ class LlamaModel:
             self._packed[(ptr, bn, pmode)] = ops.tgemm_pack(w, bn, pmode)
         return total
 
+    # split-K slabs of the tile GEMM in fp16 (tgemm mode 3): half the slab bytes
+    # the producer writes and the consumer (splitk.hip) reads; each slab is one
+    # K-slice's fp32 sum rounded to 11 bits, finer than the bf16 rounding of the
+    # projection output itself.  OMNIA_SPLITK_FP32=1 keeps fp32 slabs.
+    splitk_half = os.environ.get("OMNIA_SPLITK_FP32", "0") != "1"
+
+    def _slab_dtype(self, nwaves: int) -> torch.dtype:
+        return torch.float16 if (self.splitk_half and nwaves < 0) else torch.float32
+
     def _wgemm(self, mode: int, x: torch.Tensor, w: torch.Tensor, S: int, nw: int, nwaves: int,
                out: torch.Tensor | None = None) -> torch.Tensor:
         """ops.wgemm, on the tile-packed copy of ``w`` when one exists for this
-        tgemm config."""
+        tgemm config; split-K slabs in fp16 on the tile GEMM (``out``'s dtype)."""
+        if nwaves < 0 and mode == 2 and out is not None and out.dtype == torch.float16:
+            mode = 3
         packed = getattr(self, "_packed", None)
         if packed and nwaves < 0:
             wp = packed.get((w.data_ptr(), nw, 1 if mode == 1 else 0))
             if wp is not None:
                 return ops.tgemm(mode, x, wp, S, nw, (-1 - nwaves) | 8, out)
+        if mode == 3:
+            return ops.tgemm(3, x, w, S, nw, -1 - nwaves, out)
         return ops.wgemm(mode, x, w, S, nw, nwaves, out=out)
 
-    def _parts(self, tag, S: int, M: int, N: int) -> torch.Tensor:
-        key = ("parts", tag, S, M, N)
+    def _parts(self, tag, S: int, M: int, N: int,
+               dtype: torch.dtype = torch.float32) -> torch.Tensor:
+        key = ("parts", tag, S, M, N, dtype)
         buf = self._ws.get(key)
         if buf is None:
-            buf = torch.empty(S, M, N, dtype=torch.float32, device=self.device)
+            buf = torch.empty(S, M, N, dtype=dtype, device=self.device)
             self._ws[key] = buf
         return buf
 
@@ -281,7 +295,8 @@ class LlamaModel:
         if cfg is None:
             return ops.linear(x, w)
         nw, nwaves, S = cfg
-        return Parts(self._wgemm(2, x, w, S, nw, nwaves, out=self._parts(tag, S, M, w.shape[0])))
+        return Parts(self._wgemm(2, x, w, S, nw, nwaves,
+                                 out=self._parts(tag, S, M, w.shape[0], self._slab_dtype(nwaves))))
 
     def add_norm(self, x, residual: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         """residual += x (TP-reduced); returns RMSNorm(residual) * w."""
@@ -308,8 +323,9 @@ class LlamaModel:
             if S == 1:
                 a = self._wgemm(1, h, layer["gate_up"], 1, nw, nwaves)
             else:
-                a = ops.splitk_swiglu(self._wgemm(2, h, layer["gate_up"], S, nw, nwaves,
-                                                  out=self._parts("gu", S, M, I2)))
+                a = ops.splitk_swiglu(self._wgemm(
+                    2, h, layer["gate_up"], S, nw, nwaves,
+                    out=self._parts("gu", S, M, I2, self._slab_dtype(nwaves))))
         return self._proj("down", a, layer["down"], is_decode)
 
     def attention(self, li: int, h: torch.Tensor, fb: ForwardBatch, kv: KVCache):

@@ -270,7 +270,8 @@ def wgemm_wide(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, wt:
 
 def tgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, bn: int = 128,
           wnt: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Tile GEMM (``csrc/tgemm.hip``): decode batches (M <= 256, one block owns all
+    """Tile GEMM (``csrc/tgemm.hip``; mode 3 = mode 2's split-K slabs in fp16):
+    decode batches (M <= 256, one block owns all
     rows x ``bn`` weight rows) and prefill chunks (256-row tiles), both operands LDS-DMA staged through an
     NS-deep ring with counted waits.  Same modes / outputs as :func:`wgemm`
     (mode 1 = fused SwiGLU needs ``splits == 1``).  ``wnt`` bit 0: non-temporal
@@ -278,13 +279,14 @@ def tgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, bn: int 
     M, K = x.shape
     N = w.shape[0] // 2 if mode == 1 else w.shape[0]
     if out is None:
-        out = (torch.empty(splits, M, N, dtype=torch.float32, device=x.device) if mode == 2
+        out = (torch.empty(splits, M, N, device=x.device,
+                           dtype=torch.float32 if mode == 2 else torch.float16) if mode >= 2
                else x.new_empty(M, N))
     if not x.is_cuda:
         r = x.float() @ w.float().t()
         if mode == 1:
             r = ref.silu_mul(r.to(x.dtype)).float()
-        if mode == 2:
+        if mode >= 2:
             out.zero_()
             out[0].copy_(r)
         else:

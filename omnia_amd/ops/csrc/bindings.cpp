@@ -86,13 +86,13 @@ int omnia_ar_blocks();
 int omnia_ar_max_ranks();
 int omnia_ar_oneshot(void* out, const void* in, void* const* regions, int* epochs, int* err,
                      int64_t n, int64_t slot_bytes, int rank, int world, hipStream_t s);
-int omnia_splitk_add_rmsnorm(void* out, const float* parts, void* residual, const void* w, int S,
+int omnia_splitk_add_rmsnorm(void* out, const void* parts, int half, void* residual, const void* w, int S,
                              int M, int d, float eps, hipStream_t s);
-int omnia_splitk_rope_kv(void* q, const float* parts, int S, int T, const int* positions,
+int omnia_splitk_rope_kv(void* q, const void* parts, int half, int S, int T, const int* positions,
                          const float* cos_sin, void* k_cache, void* v_cache, const int64_t* slots,
                          int hq, int hkv, int head_dim, int block_size, hipStream_t s);
-int omnia_splitk_swiglu(void* out, const float* parts, int S, int M, int inter, hipStream_t s);
-int omnia_splitk_reduce(void* out, const float* parts, int S, int64_t n, hipStream_t s);
+int omnia_splitk_swiglu(void* out, const void* parts, int half, int S, int M, int inter, hipStream_t s);
+int omnia_splitk_reduce(void* out, const void* parts, int half, int S, int64_t n, hipStream_t s);
 int64_t omnia_ar_region_bytes(int64_t slot_bytes);
 int omnia_ar_twoshot(void* out, const void* in, void* residual, const void* w,
                      void* const* regions, int* epochs, int* err, int M, int d,
@@ -603,15 +603,15 @@ void tgemm(int64_t mode, at::Tensor out, at::Tensor x, at::Tensor W, int64_t spl
   TORCH_CHECK(x.device() == W.device() && x.device() == out.device(), "same device");
   const int M = x.size(0), K = x.size(1);
   TORCH_CHECK(W.size(1) == K, "K mismatch");
-  TORCH_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");
+  TORCH_CHECK(mode >= 0 && mode <= 3, "mode");
   TORCH_CHECK(mode != 1 || W.size(0) % 2 == 0, "gate_up rows even");
   const int N = mode == 1 ? W.size(0) / 2 : W.size(0);
   int ldo;
-  if (mode == 2) {
-    TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous(),
-                "mode 2: fp32 contiguous slabs");
+  if (mode >= 2) {
+    TORCH_CHECK(out.scalar_type() == (mode == 2 ? at::kFloat : at::kHalf) && out.is_contiguous(),
+                "mode 2 / 3: fp32 / fp16 contiguous slabs");
     TORCH_CHECK(out.dim() == 3 && out.size(0) == splits && out.size(1) == M && out.size(2) == N,
-                "mode 2: out [S, M, N]");
+                "mode 2 / 3: out [S, M, N]");
     ldo = N;
   } else {
     CHECK_BF16(out);
@@ -715,22 +715,24 @@ void row_sumsq(at::Tensor ss, at::Tensor x) {
 }
 
 // ------------------------------------------------- split-K consumers (splitk.hip)
-static void check_parts(const at::Tensor& p) {
-  TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat && p.is_contiguous() && p.dim() == 3,
-              "parts: contiguous fp32 [S, M, N]");
+// fp32 slabs, or fp16 ones (tgemm mode 3); returns 1 for fp16
+static int check_parts(const at::Tensor& p) {
+  TORCH_CHECK(p.is_cuda() && (p.scalar_type() == at::kFloat || p.scalar_type() == at::kHalf) &&
+              p.is_contiguous() && p.dim() == 3, "parts: contiguous fp32 / fp16 [S, M, N]");
   TORCH_CHECK(p.size(0) >= 1 && p.size(0) <= 16, "1 <= S <= 16");
+  return p.scalar_type() == at::kHalf ? 1 : 0;
 }
 
 void splitk_add_rmsnorm(at::Tensor out, at::Tensor parts, at::Tensor residual, at::Tensor w,
                         double eps) {
-  check_parts(parts);
+  const int half = check_parts(parts);
   CHECK_BF16(out); CHECK_BF16(residual); CHECK_BF16(w);
   const int M = parts.size(1), d = parts.size(2);
   TORCH_CHECK(residual.is_contiguous() && residual.size(0) == M && residual.size(1) == d,
               "residual [M, d]");
   TORCH_CHECK(out.is_contiguous() && out.size(0) == M && out.size(1) == d, "out [M, d]");
   TORCH_CHECK(w.numel() == d, "w [d]");
-  CHECK_RC(omnia_splitk_add_rmsnorm(out.data_ptr(), parts.data_ptr<float>(), residual.data_ptr(),
+  CHECK_RC(omnia_splitk_add_rmsnorm(out.data_ptr(), parts.data_ptr(), half, residual.data_ptr(),
                                     w.data_ptr(), parts.size(0), M, d, (float)eps, cur_stream()),
            "splitk_add_rmsnorm");
 }
@@ -738,7 +740,7 @@ void splitk_add_rmsnorm(at::Tensor out, at::Tensor parts, at::Tensor residual, a
 void splitk_rope_kv(at::Tensor q, at::Tensor parts, at::Tensor positions, at::Tensor cos_sin,
                     at::Tensor k_cache, at::Tensor v_cache, at::Tensor slots, int64_t hq,
                     int64_t hkv, int64_t block_size) {
-  check_parts(parts);
+  const int half = check_parts(parts);
   CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_I32(positions);
   const int T = parts.size(1);
   TORCH_CHECK(parts.size(2) == (hq + 2 * hkv) * 128, "parts N = (hq + 2 hkv) * 128");
@@ -749,7 +751,7 @@ void splitk_rope_kv(at::Tensor q, at::Tensor parts, at::Tensor positions, at::Te
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == hkv && k_cache.size(2) == block_size &&
               k_cache.size(3) == 128 && k_cache.is_contiguous() && v_cache.is_contiguous(),
               "cache [NB, Hkv, BS, 128]");
-  CHECK_RC(omnia_splitk_rope_kv(q.data_ptr(), parts.data_ptr<float>(), parts.size(0), T,
+  CHECK_RC(omnia_splitk_rope_kv(q.data_ptr(), parts.data_ptr(), half, parts.size(0), T,
                                 positions.data_ptr<int>(), cos_sin.data_ptr<float>(),
                                 k_cache.data_ptr(), v_cache.data_ptr(),
                                 slots.data_ptr<int64_t>(), hq, hkv, 128, block_size,
@@ -758,20 +760,20 @@ void splitk_rope_kv(at::Tensor q, at::Tensor parts, at::Tensor positions, at::Te
 }
 
 void splitk_swiglu(at::Tensor out, at::Tensor parts) {
-  check_parts(parts);
+  const int half = check_parts(parts);
   CHECK_BF16(out);
   const int M = parts.size(1), I = parts.size(2) / 2;
   TORCH_CHECK(parts.size(2) % 2 == 0 && out.is_contiguous() && out.size(0) == M &&
               out.size(1) == I, "out [M, I] for parts [S, M, 2I]");
-  CHECK_RC(omnia_splitk_swiglu(out.data_ptr(), parts.data_ptr<float>(), parts.size(0), M, I,
+  CHECK_RC(omnia_splitk_swiglu(out.data_ptr(), parts.data_ptr(), half, parts.size(0), M, I,
                                cur_stream()), "splitk_swiglu");
 }
 
 void splitk_reduce(at::Tensor out, at::Tensor parts) {
-  check_parts(parts);
+  const int half = check_parts(parts);
   CHECK_BF16(out);
   TORCH_CHECK(out.is_contiguous() && out.numel() == parts.size(1) * parts.size(2), "out [M, N]");
-  CHECK_RC(omnia_splitk_reduce(out.data_ptr(), parts.data_ptr<float>(), parts.size(0),
+  CHECK_RC(omnia_splitk_reduce(out.data_ptr(), parts.data_ptr(), half, parts.size(0),
                                out.numel(), cur_stream()), "splitk_reduce");
 }
 

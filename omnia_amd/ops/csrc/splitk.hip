@@ -19,11 +19,26 @@ using namespace omnia;
 namespace {
 
 // sum over the S slabs of 4 consecutive floats at element offset e
-template <int S>
-__device__ __forceinline__ float4v sum4(const float* __restrict__ p, int64_t slab, int64_t e) {
+// Slabs are fp32 or fp16 (tgemm MODE 3: half the slab bytes for the producer
+// and the consumer; each fp16 slab holds one K-slice's fp32 sum rounded to 11
+// bits, below the bf16 rounding of the projection's output)
+typedef _Float16 half4v __attribute__((ext_vector_type(4)));
+
+template <typename P>
+__device__ __forceinline__ float4v load4(const P* __restrict__ p) {
+  if constexpr (sizeof(P) == 4) {
+    return *reinterpret_cast<const float4v*>(p);
+  } else {
+    const half4v h = *reinterpret_cast<const half4v*>(p);
+    return float4v{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+  }
+}
+
+template <int S, typename P>
+__device__ __forceinline__ float4v sum4(const P* __restrict__ p, int64_t slab, int64_t e) {
   float4v v[S];
 #pragma unroll
-  for (int s = 0; s < S; ++s) v[s] = *reinterpret_cast<const float4v*>(p + s * slab + e);
+  for (int s = 0; s < S; ++s) v[s] = load4(p + s * slab + e);
   float4v a = v[0];
 #pragma unroll
   for (int s = 1; s < S; ++s) a += v[s];
@@ -37,9 +52,9 @@ __device__ __forceinline__ float rnd(float x) { return bf2f(f2bf(x)); }  // bf16
 
 // ------------------------------------------------------ residual add + RMSNorm
 // one workgroup (256 threads) per row; VEC chunks of 8 columns per thread
-template <int VEC, int S>
+template <int VEC, int S, typename P>
 __global__ __launch_bounds__(256) void splitk_add_rmsnorm_kernel(
-    bf16_t* __restrict__ out, const float* __restrict__ parts, bf16_t* __restrict__ residual,
+    bf16_t* __restrict__ out, const P* __restrict__ parts, bf16_t* __restrict__ residual,
     const bf16_t* __restrict__ w, int M, int d, float eps) {
   __shared__ float scratch[8];
   const int row = blockIdx.x;
@@ -87,9 +102,9 @@ __global__ __launch_bounds__(256) void splitk_add_rmsnorm_kernel(
 // rotation pairs of a q or k head, or 8 elements of a v head -- so every slab
 // load of the block is in flight at once.  Same cache layout as rope_kv_kernel:
 // [num_blocks, Hkv, BS, D].
-template <int S>
+template <int S, typename P>
 __global__ __launch_bounds__(256) void splitk_rope_kv_kernel(
-    bf16_t* __restrict__ q, const float* __restrict__ parts, int T,
+    bf16_t* __restrict__ q, const P* __restrict__ parts, int T,
     const int* __restrict__ positions, const float* __restrict__ cos_sin,
     bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache, const int64_t* __restrict__ slots,
     int hq, int hkv, int block_size) {
@@ -99,7 +114,7 @@ __global__ __launch_bounds__(256) void splitk_rope_kv_kernel(
   if (head >= hq + 2 * hkv) return;
   const int N = (hq + 2 * hkv) * D;
   const int64_t slab = (int64_t)T * N;
-  const float* row = parts + (int64_t)t * N;
+  const P* row = parts + (int64_t)t * N;
   const int64_t slot = slots[t];
   const int64_t blk = slot >= 0 ? slot / block_size : 0, off = slot >= 0 ? slot % block_size : 0;
   if (head >= hq + hkv) {  // v: 8 contiguous elements straight into the cache
@@ -138,9 +153,9 @@ __global__ __launch_bounds__(256) void splitk_rope_kv_kernel(
 
 // --------------------------------------------------------------- SwiGLU
 // parts [S][M][2I] (gate | up) -> out [M, I]; grid (ceil(I/8/256), M)
-template <int S>
+template <int S, typename P>
 __global__ __launch_bounds__(256) void splitk_swiglu_kernel(bf16_t* __restrict__ out,
-                                                            const float* __restrict__ parts,
+                                                            const P* __restrict__ parts,
                                                             int M, int inter) {
   const int m = blockIdx.y;
   const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
@@ -159,9 +174,9 @@ __global__ __launch_bounds__(256) void splitk_swiglu_kernel(bf16_t* __restrict__
 }
 
 // --------------------------------------------------------------- reduce
-template <int S>
+template <int S, typename P>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(bf16_t* __restrict__ out,
-                                                            const float* __restrict__ parts,
+                                                            const P* __restrict__ parts,
                                                             int64_t n) {
   const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   if (e >= n) return;
@@ -179,14 +194,18 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(bf16_t* __restrict__
 
 extern "C" {
 
-int omnia_splitk_add_rmsnorm(void* out, const float* parts, void* residual, const void* w, int S,
-                             int M, int d, float eps, hipStream_t st) {
+int omnia_splitk_add_rmsnorm(void* out, const void* parts, int half, void* residual,
+                             const void* w, int S, int M, int d, float eps, hipStream_t st) {
   if (S < 1 || S > 16 || d % 8 || M < 1) return -1;
   const int vec = (d + 2047) / 2048;
   if (vec > 4) return -2;
 #define OMNIA_SKN(V, SS)                                                                       \
-  splitk_add_rmsnorm_kernel<V, SS><<<M, 256, 0, st>>>((bf16_t*)out, parts, (bf16_t*)residual,  \
-                                                      (const bf16_t*)w, M, d, eps);
+  if (half)                                                                                    \
+    splitk_add_rmsnorm_kernel<V, SS, _Float16><<<M, 256, 0, st>>>(                             \
+        (bf16_t*)out, (const _Float16*)parts, (bf16_t*)residual, (const bf16_t*)w, M, d, eps);  \
+  else                                                                                         \
+    splitk_add_rmsnorm_kernel<V, SS, float><<<M, 256, 0, st>>>(                                \
+        (bf16_t*)out, (const float*)parts, (bf16_t*)residual, (const bf16_t*)w, M, d, eps);
 #define OMNIA_SKS(SS)                              \
   if (S == SS) {                                   \
     if (vec <= 1) { OMNIA_SKN(1, SS) }             \
@@ -199,38 +218,58 @@ int omnia_splitk_add_rmsnorm(void* out, const float* parts, void* residual, cons
   return (int)hipGetLastError();
 }
 
-int omnia_splitk_rope_kv(void* q, const float* parts, int S, int T, const int* positions,
+int omnia_splitk_rope_kv(void* q, const void* parts, int half, int S, int T, const int* positions,
                          const float* cos_sin, void* k_cache, void* v_cache, const int64_t* slots,
                          int hq, int hkv, int head_dim, int block_size, hipStream_t s) {
   if (head_dim != 128 || S < 1 || S > 16) return -1;
   if (T == 0) return 0;
   const dim3 grid(T, (hq + 2 * hkv + 15) / 16);
 #define OMNIA_SKR(SS)                                                                          \
-  if (S == SS)                                                                                 \
-    splitk_rope_kv_kernel<SS><<<grid, 256, 0, s>>>((bf16_t*)q, parts, T, positions, cos_sin,   \
-                                                   (bf16_t*)k_cache, (bf16_t*)v_cache, slots,  \
-                                                   hq, hkv, block_size);
+  if (S == SS) {                                                                               \
+    if (half)                                                                                  \
+      splitk_rope_kv_kernel<SS, _Float16><<<grid, 256, 0, s>>>(                                \
+          (bf16_t*)q, (const _Float16*)parts, T, positions, cos_sin, (bf16_t*)k_cache,         \
+          (bf16_t*)v_cache, slots, hq, hkv, block_size);                                       \
+    else                                                                                       \
+      splitk_rope_kv_kernel<SS, float><<<grid, 256, 0, s>>>(                                   \
+          (bf16_t*)q, (const float*)parts, T, positions, cos_sin, (bf16_t*)k_cache,            \
+          (bf16_t*)v_cache, slots, hq, hkv, block_size);                                       \
+  }
   OMNIA_SPLITK_S(OMNIA_SKR)
 #undef OMNIA_SKR
   return (int)hipGetLastError();
 }
 
-int omnia_splitk_swiglu(void* out, const float* parts, int S, int M, int inter, hipStream_t s) {
+int omnia_splitk_swiglu(void* out, const void* parts, int half, int S, int M, int inter,
+                        hipStream_t s) {
   if (S < 1 || S > 16 || inter % 8 || M < 1) return -1;
   dim3 grid((inter / 8 + 255) / 256, M);
-#define OMNIA_SKW(SS) \
-  if (S == SS) splitk_swiglu_kernel<SS><<<grid, 256, 0, s>>>((bf16_t*)out, parts, M, inter);
+#define OMNIA_SKW(SS)                                                                          \
+  if (S == SS) {                                                                               \
+    if (half)                                                                                  \
+      splitk_swiglu_kernel<SS, _Float16><<<grid, 256, 0, s>>>((bf16_t*)out,                    \
+                                                             (const _Float16*)parts, M, inter); \
+    else                                                                                       \
+      splitk_swiglu_kernel<SS, float><<<grid, 256, 0, s>>>((bf16_t*)out, (const float*)parts,  \
+                                                          M, inter);                           \
+  }
   OMNIA_SPLITK_S(OMNIA_SKW)
 #undef OMNIA_SKW
   return (int)hipGetLastError();
 }
 
-int omnia_splitk_reduce(void* out, const float* parts, int S, int64_t n, hipStream_t s) {
+int omnia_splitk_reduce(void* out, const void* parts, int half, int S, int64_t n, hipStream_t s) {
   if (S < 1 || S > 16 || n % 8) return -1;
   if (n == 0) return 0;
   const unsigned g = (unsigned)((n / 8 + 255) / 256);
-#define OMNIA_SKD(SS) \
-  if (S == SS) splitk_reduce_kernel<SS><<<g, 256, 0, s>>>((bf16_t*)out, parts, n);
+#define OMNIA_SKD(SS)                                                                          \
+  if (S == SS) {                                                                               \
+    if (half)                                                                                  \
+      splitk_reduce_kernel<SS, _Float16><<<g, 256, 0, s>>>((bf16_t*)out, (const _Float16*)parts, \
+                                                           n);                                 \
+    else                                                                                       \
+      splitk_reduce_kernel<SS, float><<<g, 256, 0, s>>>((bf16_t*)out, (const float*)parts, n); \
+  }
   OMNIA_SPLITK_S(OMNIA_SKD)
 #undef OMNIA_SKD
   return (int)hipGetLastError();

@@ -33,7 +33,9 @@
 //   * block order: XCD-remapped, split-major, so the blocks sharing an XCD's L2
 //     mostly share one x slice.
 // MODE 0: bf16 out[M, ldo]; MODE 1: bf16 SwiGLU out[M, ldo] (N = features);
-// MODE 2: fp32 partial slabs out[S][M][N].
+// MODE 2: fp32 partial slabs out[S][M][N]; MODE 3: the same slabs in fp16.
+#include <type_traits>
+
 #include "common.h"
 
 using namespace omnia;
@@ -297,9 +299,11 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
   wait_vm<0>();
 
   // ---- epilogue: lane holds rows wm*WTM + 16i + 4fq + r, tile columns wn*WTN + 16j + fr
-  if (MODE == 2) {
-    float* o = reinterpret_cast<float*>(out) + (int64_t)split * M * N + (int64_t)m0 * N +
-               (int64_t)tile * BN + wn * WTN + fr;
+  if (MODE == 2 || MODE == 3) {
+    // MODE 3: fp16 slabs (one K-slice's fp32 sum rounded to 11 bits)
+    using P = std::conditional_t<MODE == 2, float, _Float16>;
+    P* o = reinterpret_cast<P*>(out) + (int64_t)split * M * N + (int64_t)m0 * N +
+           (int64_t)tile * BN + wn * WTN + fr;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -307,7 +311,7 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
         const int row = wm * WTM + 16 * i + 4 * fq + r;
         if (row < Mt) {
 #pragma unroll
-          for (int j = 0; j < FN; ++j) o[(int64_t)row * N + 16 * j] = acc[i][j][r];
+          for (int j = 0; j < FN; ++j) o[(int64_t)row * N + 16 * j] = (P)acc[i][j][r];
         }
       }
   } else if (MODE == 0) {
@@ -416,23 +420,24 @@ extern "C" {
 // from W = [Wg; Wu] ([2N, K]); mode 2: fp32 slabs out[S][M][N].
 int omnia_tgemm(int mode, void* out, const void* X, const void* W, int M, int N, int K, int S,
                 int bn, int wnt, int ldo, hipStream_t s) {
-  if (mode < 0 || mode > 2) return -1;
+  if (mode < 0 || mode > 3) return -1;
   if (M < 1 || (int64_t)((M + 255) / 256) * S * (N / 64) > (1 << 30)) return -2;
   if (K % 64 || K <= 0) return -3;
   if (S < 1 || S > 16 || S > K / 64) return -4;
   if (bn != 64 && bn != 128 && bn != 256) return -5;
   const int cols = mode == 1 ? bn / 2 : bn;
   if (N % cols) return -6;
-  if (mode != 2 && S != 1) return -7;
+  if (mode < 2 && S != 1) return -7;
   if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) |
        reinterpret_cast<uintptr_t>(out)) & 15)
     return -8;
-  if (mode != 2 && ldo < N) return -9;
+  if (mode < 2 && ldo < N) return -9;
   const bf16_t* x = (const bf16_t*)X;
   const bf16_t* w = (const bf16_t*)W;
   if (mode == 0) return launch_mode<0>(out, x, w, M, N, K, S, ldo, bn, wnt, s);
   if (mode == 1) return launch_mode<1>(out, x, w, M, N, K, S, ldo, bn, wnt, s);
-  return launch_mode<2>(out, x, w, M, N, K, S, N, bn, wnt, s);
+  if (mode == 2) return launch_mode<2>(out, x, w, M, N, K, S, N, bn, wnt, s);
+  return launch_mode<3>(out, x, w, M, N, K, S, N, bn, wnt, s);
 }
 
 }  // extern "C"

@@ -53,3 +53,33 @@ def test_splitk_swiglu_and_reduce(S, M, I):
                                ops.splitk_swiglu(p.cpu()).float(), rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(ops.splitk_reduce(p).cpu().float(),
                                p.sum(0).cpu().to(torch.bfloat16).float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("S,M", [(5, 256), (8, 33)])
+def test_consumers_read_half_slabs(S, M):
+    """fp16 slabs (tgemm mode 3) through every consumer give the same result as
+    the same values held in fp32 slabs."""
+    d, I, hq, hkv, D, BS, NB = 4096, 1024, 8, 2, 128, 16, 64
+    p16 = _parts(S, M, d, S * M).half()
+    res = torch.randn(M, d, device="cuda").to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(d, device="cuda")).to(torch.bfloat16)
+    r16, r32 = res.clone(), res.clone()
+    o16 = ops.splitk_add_rmsnorm(p16, r16, w, 1e-5)
+    o32 = ops.splitk_add_rmsnorm(p16.float(), r32, w, 1e-5)
+    torch.testing.assert_close(r16, r32, rtol=0, atol=0)
+    torch.testing.assert_close(o16.float(), o32.float(), rtol=1e-2, atol=1e-2)
+    g16 = _parts(S, M, 2 * I, M).half()
+    torch.testing.assert_close(ops.splitk_swiglu(g16).float(),
+                               ops.splitk_swiglu(g16.float()).float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(ops.splitk_reduce(g16).float(),
+                               ops.splitk_reduce(g16.float()).float(), rtol=1e-2, atol=1e-2)
+    q16 = _parts(S, M, (hq + 2 * hkv) * D, M + 1).half()
+    pos = torch.randint(0, 2000, (M,), device="cuda", dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device="cuda")[:M].to(torch.int64)
+    cs = ref.rope_cos_sin(4096, D, 500000.0, device="cuda")
+    caches = [torch.zeros(NB, hkv, BS, D, device="cuda", dtype=torch.bfloat16) for _ in range(4)]
+    qa = ops.splitk_rope_kv(q16, pos, cs, caches[0], caches[1], slots, hq, hkv, BS)
+    qb = ops.splitk_rope_kv(q16.float(), pos, cs, caches[2], caches[3], slots, hq, hkv, BS)
+    torch.testing.assert_close(qa.float(), qb.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(caches[0].float(), caches[2].float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(caches[1].float(), caches[3].float(), rtol=1e-2, atol=1e-2)

@@ -53,6 +53,23 @@ def test_mode2_splitk_slabs_sum_to_product(M, S, bn, wnt):
     torch.testing.assert_close(part.sum(0), want, rtol=1e-3, atol=3e-3)
 
 
+@pytest.mark.parametrize("M,S,bn,wnt", [(256, 5, 128, 0), (201, 7, 256, 0), (256, 8, 128, 9),
+                                         (77, 4, 64, 5)])
+def test_mode3_half_slabs_match_fp32_slabs(M, S, bn, wnt):
+    """fp16 slabs (mode 3): each slab is the fp32 slab rounded to fp16, so the
+    slab-by-slab error is within fp16's half-ulp; packed weights (wnt bit 3) too."""
+    x, w = _mk(M, 1024, 2048, seed=3 * M + S)
+    if wnt & 8:
+        wp = ops.tgemm_pack(w, bn, 0)
+        p32, p16 = ops.tgemm(2, x, wp, S, bn, wnt), ops.tgemm(3, x, wp, S, bn, wnt)
+    else:
+        p32, p16 = ops.tgemm(2, x, w, S, bn, wnt), ops.tgemm(3, x, w, S, bn, wnt)
+    assert p16.shape == (S, M, 1024) and p16.dtype == torch.float16
+    torch.testing.assert_close(p16.float(), p32.half().float(), rtol=0, atol=0)
+    torch.testing.assert_close(p16.float().sum(0), x.float() @ w.float().t(),
+                               rtol=3e-3, atol=1e-2)
+
+
 @pytest.mark.parametrize("wnt", [1, 2, 3, 4, 5])
 def test_llama3_8b_shapes(wnt):
     """The four Llama-3-8B decode projections at the serving batch (64-k and

@@ -72,6 +72,8 @@ def parse(argv=None):
                     help="engine mixed steps: decode rows + <= N prefill tokens per forward "
                          "(default: the engine's, gated on the prefill backlog)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-share-prefix", action="store_true",
+                    help="engine: no cross-session prefix sharing (every prompt token prefilled)")
     ap.add_argument("--inproc", action="store_true",
                     help="runtime path: engine as a thread of the serving process")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
@@ -180,6 +182,7 @@ class WSDriver:
             "OMNIA_ENGINE_MAX_MODEL_LEN": max(2048, a.prompt_len + a.gen_len + 64),
             "OMNIA_ENGINE_MAX_PREFILL_TOKENS": a.max_prefill_tokens,
             "OMNIA_ENGINE_USE_GRAPHS": "false" if a.no_graphs else "true",
+            "OMNIA_ENGINE_SHARE_PREFIX": "false" if a.no_share_prefix else "true",
             "OMNIA_ENGINE_SEED": rank,
             "OMNIA_ENGINE_PROC": "1" if (use_gpu and a.tp == 1) or a.engine == "synthetic" else "0",
             "OMNIA_ENGINE_SYNTHETIC": "1" if a.engine == "synthetic" else "0",
@@ -243,7 +246,7 @@ class WSDriver:
             self._ready.append(await nxt)
         u = r["usage"] or {}
         return (r["ttft_ms"] / 1e3, r["latency_ms"] / 1e3, int(u.get("output_tokens", 0)),
-                int(u.get("input_tokens", 0)), r["chunk_times_s"])
+                int(u.get("input_tokens", 0)), r["chunk_times_s"], int(u.get("cached_tokens", 0)))
 
     async def _wave(self):
         """One closed-loop wave.  The virtual users' NEXT messages are written on
@@ -320,7 +323,8 @@ class LocalDriver:
                            max_batch=max(C, 1),
                            max_model_len=max(2048, a.prompt_len + a.gen_len + 64),
                            max_prefill_tokens=a.max_prefill_tokens, use_graphs=not a.no_graphs,
-                           seed=rank, **({"mixed_budget": a.mixed_budget}
+                           seed=rank, share_prefix=not a.no_share_prefix,
+                           **({"mixed_budget": a.mixed_budget}
                                          if a.mixed_budget is not None else {}))
         self.cfg = cfg
         self.eng = self.client = None
@@ -353,14 +357,16 @@ class LocalDriver:
         prompts = torch.randint(lo, self.vocab - lo, (a.concurrency, a.prompt_len),
                                 generator=self.g).tolist()
         if self.runtime is not None:
-            return [(t, l, n, a.prompt_len, []) for t, l, n in self.runtime.run_wave(prompts, step)]
+            return [(t, l, n, a.prompt_len, [], None)
+                    for t, l, n in self.runtime.run_wave(prompts, step)]
         eng = self.eng
         seqs = [eng.add_request(p, self.params, session_id=f"r{self.rank}-s{step}-{i}")
                 for i, p in enumerate(prompts)]
         eng.run_until_done()
         for s in seqs:
             eng.drop_session(s.session_id)  # fresh prompts next wave: no prefix reuse
-        return [(s.ttft(), s.latency(), len(s.output), a.prompt_len, []) for s in seqs]
+        return [(s.ttft(), s.latency(), len(s.output), a.prompt_len, [], s.prefix_hit)
+                for s in seqs]
 
     def sync(self):
         import torch
@@ -652,6 +658,10 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             "frames_per_token_rank0": round(frames / max(1, sum(r[2] for r in results)), 4)
             if a.path == "ws" else None,
             "turns": len(lats),
+            # prompt tokens served from KV pages another sequence computed (the
+            # shared system-prompt page; engine/kv_manager.py), rank 0's turns
+            "prefix_cached_frac": round(sum(r[5] for r in results) / max(1, sum(
+                r[3] for r in results)), 4) if results and results[0][5] is not None else None,
             "wave_ms": wave_ms,
             "config": {
                 "model": a.model,

@@ -46,8 +46,9 @@ _messages = {
     "ContentPart": [("type", 1, "string"), ("text", 2, "string"), ("media", 3, "MediaContent")],
     "MediaContent": [("data", 1, "string"), ("url", 2, "string"), ("mime_type", 3, "string"),
                      ("storage_ref", 4, "string")],
+    # field 4 is ours: prompt tokens the engine served from cached KV pages
     "Usage": [("input_tokens", 1, "int32"), ("output_tokens", 2, "int32"),
-              ("cost_usd", 3, "float")],
+              ("cost_usd", 3, "float"), ("cached_tokens", 4, "int32")],
     "Error": [("code", 1, "string"), ("message", 2, "string")],
     "Interruption": [],
     "MediaChunk": [("media_id", 1, "string"), ("sequence", 2, "int32"), ("is_last", 3, "bool"),

@@ -77,6 +77,10 @@ class EngineConfig:
     # >0 (with WORLD_SIZE > 1, tp = 1): prompts of at least this many uncached
     # tokens are prefilled context-parallel by the whole DP group (engine/cp.py)
     cp_threshold: int = 0
+    # cross-session prefix sharing (kv_manager.py): sequences map the published
+    # KV pages of a prompt prefix another sequence computed (the deployment's
+    # shared system prompt) instead of prefilling them
+    share_prefix: bool = True
 
     @classmethod
     def from_env(cls, **kw) -> "EngineConfig":
@@ -96,6 +100,7 @@ class EngineConfig:
             "OMNIA_ENGINE_MIXED_BACKLOG": ("mixed_backlog", int),
             "OMNIA_ENGINE_EP_MODE": ("ep_mode", str),
             "OMNIA_ENGINE_CP_THRESHOLD": ("cp_threshold", int),
+            "OMNIA_ENGINE_SHARE_PREFIX": ("share_prefix", lambda v: v.lower() not in ("0", "false")),
         }
         for k, (f, t) in m.items():
             if k in env:
@@ -180,7 +185,7 @@ class LLMEngine:
                 from .tp import TPSwapProxy
 
                 swap = TPSwapProxy(swap, self.runner.chan)
-        self.blocks = BlockManager(nb, cfg.block_size, swap=swap)
+        self.blocks = BlockManager(nb, cfg.block_size, swap=swap, share_prefix=cfg.share_prefix)
         self.scheduler = Scheduler(
             SchedulerConfig(max_batch=cfg.max_batch, max_prefill_tokens=cfg.max_prefill_tokens,
                             max_model_len=cfg.max_model_len,
@@ -333,6 +338,7 @@ class LLMEngine:
             n += 1
         for sid in list(self.blocks.sessions.keys()):
             self.blocks.drop_session(sid)
+        self.blocks.reset_shared()
         if self.device.type == "cuda":
             try:
                 torch.cuda.synchronize(self.device)

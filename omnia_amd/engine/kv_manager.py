@@ -15,6 +15,16 @@ Tiers (the KV analogue of Omnia's hot/warm/cold session "compaction",
   * cold  -- nothing: the transcript in the runtime's context store is the source
              of truth and the next turn re-prefills ("cache empty != definitive").
 Block 0 is a reserved null page used by padded rows of captured decode graphs.
+
+Cross-session prefix sharing (``share_prefix``): every full page of a computed
+prompt is published under a chain hash of its tokens and all the tokens before
+it.  A new sequence whose session holds no pages maps the longest published run
+of its prompt's leading pages instead of prefilling them: the agents of one
+deployment all start from the same PromptPack system prompt and tool schemas.
+Shared pages are reference-counted (the table holds one reference).  A sequence
+never writes into one: only full pages are shared, and a hit always leaves the
+page that holds the prompt's last token private.  Once only the table holds a
+page, it can be evicted (after the idle sessions) when an allocation needs it.
 """
 from __future__ import annotations
 
@@ -50,17 +60,27 @@ def common_prefix(a: list[int], b: list[int]) -> int:
 
 
 class BlockManager:
-    def __init__(self, num_blocks: int, block_size: int, swap=None):
+    CHAIN_SEED = 0x6F6D6E6961  # chain hash of the empty prefix
+
+    def __init__(self, num_blocks: int, block_size: int, swap=None, share_prefix: bool = False,
+                 max_shared: int | None = None):
         if num_blocks < 2:
             raise ValueError("need at least 2 KV blocks")
         self.block_size = block_size
         self.num_blocks = num_blocks
         self.free: list[int] = list(range(num_blocks - 1, 0, -1))  # block 0 reserved
         self.sessions: "OrderedDict[str, SessionKV]" = OrderedDict()
-        self.idle_blocks = 0  # pages held by parked (evictable) sessions
+        self.idle_blocks = 0  # private pages held by parked (evictable) sessions
         self.swap = swap
+        self.share_prefix = share_prefix
+        self.max_shared = max_shared if max_shared is not None else max(1, num_blocks // 4)
+        self.table: dict[int, int] = {}  # chain hash -> shared page
+        self.key_of: dict[int, int] = {}  # shared page -> chain hash
+        self.ref: dict[int, int] = {}  # shared page -> holders, the table included
+        self.evictable: "OrderedDict[int, None]" = OrderedDict()  # shared pages only the table holds
         self.stats = {"prefix_hit_tokens": 0, "prefix_miss_tokens": 0, "evictions": 0,
-                      "swap_out": 0, "swap_in": 0}
+                      "swap_out": 0, "swap_in": 0, "shared_hit_tokens": 0,
+                      "shared_pages": 0, "shared_evictions": 0}
 
     # -------------------------------------------------------------- pool
     @property
@@ -69,8 +89,15 @@ class BlockManager:
 
     @property
     def num_available(self) -> int:
-        """Free pages plus pages an allocation may reclaim from idle sessions."""
-        return len(self.free) + self.idle_blocks
+        """Free pages plus pages an allocation may reclaim: idle sessions' private
+        pages and shared pages only the table holds.  (A lower bound: evicting a
+        session can also leave its shared pages to the table alone.)"""
+        return len(self.free) + self.idle_blocks + len(self.evictable)
+
+    def _n_private(self, blocks: list[int]) -> int:
+        if not self.ref:
+            return len(blocks)
+        return sum(1 for b in blocks if b not in self.ref)
 
     def utilization(self) -> float:
         return 1.0 - len(self.free) / (self.num_blocks - 1)
@@ -82,14 +109,21 @@ class BlockManager:
         for sid, s in self.sessions.items():  # LRU order
             if not s.in_use:
                 self.sessions.pop(sid)
-                self.idle_blocks -= len(s.blocks)
+                self.idle_blocks -= self._n_private(s.blocks)
                 if self.swap is not None and s.tokens and self.swap.can_hold(len(s.blocks)):
                     s.swapped = self.swap.swap_out(s.blocks)
                     self.swap.park(sid, s)
                     self.stats["swap_out"] += 1
-                self.free.extend(s.blocks)
+                self.release(s.blocks)
                 self.stats["evictions"] += 1
                 return True
+        if self.evictable:  # then the shared pages nobody maps
+            b, _ = self.evictable.popitem(last=False)
+            del self.table[self.key_of.pop(b)]
+            del self.ref[b]
+            self.free.append(b)
+            self.stats["shared_evictions"] += 1
+            return True
         return False
 
     def allocate(self, n: int) -> list[int]:
@@ -103,7 +137,89 @@ class BlockManager:
         return self.num_available >= n
 
     def release(self, blocks: list[int]) -> None:
-        self.free.extend(blocks)
+        if not self.ref:
+            self.free.extend(blocks)
+            return
+        for b in blocks:
+            r = self.ref.get(b)
+            if r is None:
+                self.free.append(b)
+            elif r == 1:  # the last holder of a page the table let go of
+                del self.ref[b]
+                self.free.append(b)
+            else:
+                self.ref[b] = r - 1
+                if r == 2 and b in self.key_of:
+                    self.evictable[b] = None  # only the table holds it now
+
+    def _incref(self, b: int) -> None:
+        r = self.ref[b]
+        if r == 1:
+            self.evictable.pop(b, None)
+        self.ref[b] = r + 1
+
+    def reset_shared(self) -> None:
+        """Forget every published page (engine-fault recovery: a page may be
+        half-written).  Pages still mapped stay counted until their holders
+        release them."""
+        for b in list(self.key_of):
+            if self.ref[b] == 1:
+                del self.ref[b]
+                self.free.append(b)
+            else:
+                self.ref[b] -= 1
+        self.table.clear()
+        self.key_of.clear()
+        self.evictable.clear()
+
+    # -------------------------------------------------------------- sharing
+    def _chain(self, h: int, tokens: list[int], i: int) -> int:
+        bs = self.block_size
+        return hash((h, tuple(tokens[i * bs:(i + 1) * bs])))
+
+    def _acquire_shared(self, prompt: list[int]) -> tuple[list[int], int]:
+        """Map the longest published run of ``prompt``'s leading full pages,
+        stopping before the page that holds its last token."""
+        blocks: list[int] = []
+        h = self.CHAIN_SEED
+        for i in range((len(prompt) - 1) // self.block_size):
+            h = self._chain(h, prompt, i)
+            b = self.table.get(h)
+            if b is None:
+                break
+            self._incref(b)
+            blocks.append(b)
+        n = len(blocks) * self.block_size
+        self.stats["shared_hit_tokens"] += n
+        return blocks, n
+
+    def publish(self, tokens: list[int], blocks: list[int], n_computed: int, done: int = 0,
+                h: int | None = None) -> tuple[int, int]:
+        """Publish the full pages among the first ``n_computed`` tokens of
+        ``tokens`` (a prompt whose KV is in ``blocks``), from page ``done`` on
+        (``h``: chain hash up to it).  Returns the new ``(done, h)``."""
+        h = self.CHAIN_SEED if h is None else h
+        if not self.share_prefix:
+            return done, h
+        full = min(n_computed, len(tokens)) // self.block_size
+        for i in range(done, full):
+            h = self._chain(h, tokens, i)
+            b = blocks[i]
+            if h in self.table or b in self.ref:
+                continue  # published already (this page, or an equal one)
+            if len(self.table) >= self.max_shared:
+                if not self.evictable:
+                    continue
+                old, _ = self.evictable.popitem(last=False)
+                del self.table[self.key_of.pop(old)]
+                del self.ref[old]
+                self.free.append(old)
+                self.stats["shared_evictions"] += 1
+            self.table[h] = b
+            self.key_of[b] = h
+            self.ref[b] = 2  # the table and the sequence that computed it
+            self.stats["shared_pages"] += 1
+        return max(done, full), h
 
     # -------------------------------------------------------------- sessions
     def acquire_prefix(self, session_id: str | None, prompt: list[int]) -> tuple[list[int], int]:
@@ -111,12 +227,9 @@ class BlockManager:
 
         Returns (blocks, n_cached_tokens).  At least one prompt token is always
         left uncached so the step produces logits."""
-        if not session_id:
-            self.stats["prefix_miss_tokens"] += len(prompt)
-            return [], 0
-        s = self.sessions.pop(session_id, None)
+        s = self.sessions.pop(session_id, None) if session_id else None
         if s is not None:
-            self.idle_blocks -= len(s.blocks)
+            self.idle_blocks -= self._n_private(s.blocks)
         elif self.swap is not None:
             s = self.swap.unpark(session_id)
             if s is not None:
@@ -131,11 +244,16 @@ class BlockManager:
                     s.swapped = None
                     self.stats["swap_in"] += 1
         if s is None:
-            self.stats["prefix_miss_tokens"] += len(prompt)
-            return [], 0
+            blocks, n = self._acquire_shared(prompt) if self.share_prefix else ([], 0)
+            self.stats["prefix_hit_tokens"] += n
+            self.stats["prefix_miss_tokens"] += len(prompt) - n
+            return blocks, n
         n = common_prefix(s.tokens, prompt)
         n = min(n, len(prompt) - 1)
         keep = self.blocks_needed(n)
+        if keep and n % self.block_size and s.blocks[keep - 1] in self.ref:
+            keep -= 1  # the next write would land in a shared page: re-prefill it
+            n = keep * self.block_size
         self.release(s.blocks[keep:])
         self.stats["prefix_hit_tokens"] += n
         self.stats["prefix_miss_tokens"] += len(prompt) - n
@@ -148,17 +266,17 @@ class BlockManager:
             return
         old = self.sessions.pop(session_id, None)
         if old is not None:
-            self.idle_blocks -= len(old.blocks)
+            self.idle_blocks -= self._n_private(old.blocks)
             self.release(old.blocks)
         need = self.blocks_needed(len(tokens))
         self.release(blocks[need:])
         self.sessions[session_id] = SessionKV(session_id, blocks[:need], list(tokens))
-        self.idle_blocks += len(blocks[:need])
+        self.idle_blocks += self._n_private(blocks[:need])
 
     def drop_session(self, session_id: str) -> bool:
         s = self.sessions.pop(session_id, None)
         if s is not None:
-            self.idle_blocks -= len(s.blocks)
+            self.idle_blocks -= self._n_private(s.blocks)
             self.release(s.blocks)
         if self.swap is not None:
             p = self.swap.unpark(session_id)

@@ -127,6 +127,7 @@ class Scheduler:
     def cp_done(self, s: Sequence, tok: int) -> list[tuple[Sequence, int]]:
         self.cp_pending = None
         s.num_cached = s.length
+        self._publish(s)
         self.running.append(s)
         return [(s, tok)]
 
@@ -148,6 +149,12 @@ class Scheduler:
         s.blocks = blocks
         s.num_cached = n
         s.prefix_hit = n
+        s.pub_pages, s.pub_hash = 0, None
+
+    def _publish(self, s: Sequence) -> None:
+        if self.blocks.share_prefix and s.pub_pages * self.blocks.block_size < len(s.prompt):
+            s.pub_pages, s.pub_hash = self.blocks.publish(s.prompt, s.blocks, s.num_cached,
+                                                          s.pub_pages, s.pub_hash)
 
     def _preempt_one(self, protect: Sequence | None = None) -> bool:
         """Free the youngest page holder: a partially prefilled prompt first (the
@@ -293,6 +300,7 @@ class Scheduler:
         out = []
         for s, n in chunks:
             s.num_cached += n
+            self._publish(s)
             if s.num_cached >= s.length:
                 if s in self.partial:
                     self.partial.remove(s)

@@ -176,9 +176,9 @@ def agent_card(name: str, description: str, url: str, skills: list | None = None
 
 def _text_of(message: dict) -> str:
     out = []
-    for p in message.get("parts", []):
+    for p in message.get("parts") or []:
         if p.get("kind", p.get("type")) == "text":
-            out.append(p.get("text", ""))
+            out.append(p.get("text") or "")
         elif p.get("kind") == "data":
             out.append(json.dumps(p.get("data")))
     return "\n".join(out)
@@ -189,7 +189,7 @@ def _tool_results(message: dict, pending: list[dict]) -> dict[str, str]:
     ``{"toolCallId": id, "result": ...}`` (or ``{"call_id", "result"}``); a
     single pending call also accepts the message's text / data as its result."""
     out = {}
-    for p in message.get("parts", []):
+    for p in message.get("parts") or []:
         d = p.get("data") if p.get("kind") == "data" else None
         if isinstance(d, dict) and (d.get("toolCallId") or d.get("call_id")):
             cid = d.get("toolCallId") or d.get("call_id")

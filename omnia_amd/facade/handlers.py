@@ -152,6 +152,8 @@ class RuntimeHandler:
                     usage = {"input_tokens": d.usage.input_tokens,
                              "output_tokens": d.usage.output_tokens,
                              "cost_usd": round(d.usage.cost_usd, 8)}
+                    if d.usage.cached_tokens:  # prompt tokens served from cached KV
+                        usage["cached_tokens"] = d.usage.cached_tokens
                     parts = [{"type": p.type, "text": p.text} for p in d.parts] or None
                     out.update(content=d.final_content, usage=usage)
                     mark("facade_done")

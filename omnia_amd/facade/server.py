@@ -699,7 +699,8 @@ class _AudioSession:
                     d = resp.done
                     await out(P.done(sid, d.final_content, None, {
                         "input_tokens": d.usage.input_tokens,
-                        "output_tokens": d.usage.output_tokens}))
+                        "output_tokens": d.usage.output_tokens,
+                        "cached_tokens": d.usage.cached_tokens}))
                 elif kind == "error":
                     await out(P.error(sid, resp.error.code or P.E_INTERNAL,
                                       resp.error.message))

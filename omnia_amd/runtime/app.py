@@ -46,7 +46,8 @@ def shared_engine(engine_cfg: dict | None = None):
             if k in EngineConfig.__dataclass_fields__:
                 t = EngineConfig.__dataclass_fields__[k].type
                 kw[k] = (int(v) if "int" in str(t) else float(v) if "float" in str(t)
-                         else (str(v).lower() == "true") if "bool" in str(t) else v)
+                         else (str(v).lower() in ("1", "true", "yes", "on")) if "bool" in str(t)
+                         else v)
         cfg = EngineConfig.from_env(**kw)
         eng = None
         if n_rep > 1:

@@ -302,7 +302,8 @@ class RuntimeService:
         await stream.send(pb.ServerMessage(done=pb.Done(
             final_content=res.content,
             usage=pb.Usage(input_tokens=res.usage.input_tokens,
-                           output_tokens=res.usage.output_tokens, cost_usd=res.cost))))
+                           output_tokens=res.usage.output_tokens, cost_usd=res.cost,
+                           cached_tokens=res.usage.cached_tokens))))
 
 
 # ===================================================================== gRPC

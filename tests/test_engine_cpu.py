@@ -184,3 +184,22 @@ def test_mixed_steps_only_for_a_trickle_backlog():
         assert plan.kind == "prefill"
         sch.on_prefill_done(plan.prefill, {s.seq_id: 5 for s, _ in plan.prefill})
     assert sch.schedule().kind == "mixed"  # a trickle: decoders keep streaming
+
+
+def test_shared_prefix_pages_equivalence_cpu():
+    """Cross-session prefix sharing on the CPU engine: the common system prompt's
+    full pages are computed once; later prompts map them, and greedy outputs
+    equal an engine without sharing.  Fault recovery forgets them."""
+    p = SamplingParams(temperature=0, max_tokens=5, ignore_eos=True)
+    sysp = list(range(11, 61))  # 50 tokens: 3 full pages of 16
+    w1 = [sysp + [70 + i, 71 + i] for i in range(3)]
+    w2 = [sysp + list(range(100 + i, 110 + 2 * i)) for i in range(3)]
+    e = make_engine(dtype="float32")
+    e.generate(w1, p)
+    got = e.generate(w2, p)
+    assert [s.prefix_hit for s in got] == [48] * 3
+    want = make_engine(dtype="float32", share_prefix=False).generate(w2, p)
+    assert [s.output for s in got] == [s.output for s in want]
+    e.recover(RuntimeError("test"))
+    assert not e.blocks.table and not e.blocks.ref
+    assert e.generate(w2[:1], p)[0].prefix_hit == 0

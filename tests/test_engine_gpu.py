@@ -74,6 +74,25 @@ def test_session_prefix_reuse_gpu_equivalence():
     assert t2.output == t2_fresh.output
 
 
+def test_shared_prefix_pages_gpu_equivalence():
+    """Cross-session prefix sharing: the second wave maps the 3 full pages of the
+    common 100-token system prompt that the first wave computed (the numerics are
+    gated against the dense oracle in test_model_correctness.py; here greedy
+    tokens may flip at bf16 near-ties, so only the first token is compared)."""
+    p = SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)
+    sysp = list(range(7, 107))
+    w1 = [sysp + list(range(200 + i, 230 + 2 * i)) for i in range(6)]
+    w2 = [sysp + list(range(300 + 3 * i, 340 + i)) for i in range(6)]
+    e = eng()
+    e.generate(w1, p)
+    got = e.generate(w2, p)
+    assert [s.prefix_hit for s in got] == [96] * 6
+    assert e.blocks.stats["shared_hit_tokens"] >= 6 * 96
+    want = eng(share_prefix=False).generate(w2, p)
+    assert [s.prefix_hit for s in want] == [0] * 6
+    assert [s.output[0] for s in got] == [s.output[0] for s in want]
+
+
 def test_sampled_decode_with_topk_topp_runs():
     e = eng()
     seqs = e.generate([list(range(1, 50))] * 4,

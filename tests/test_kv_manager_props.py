@@ -89,3 +89,112 @@ def test_common_prefix_matches_naive():
         assert common_prefix(a, b) == n
 
     check()
+
+
+class SharedKVMachine(RuleBasedStateMachine):
+    """With cross-session prefix sharing: prompts drawn from a few common
+    prefixes, pages published as a turn's prefill completes.  Every page is free,
+    table-only, or held; a held shared page is counted once per holder; a
+    sequence never owns a shared page in the slot it will write next."""
+
+    PREFIXES = [[1] * 9, [1] * 4 + [2] * 5, [3] * 13]
+
+    def __init__(self):
+        super().__init__()
+        self.bm = BlockManager(NB, BS, share_prefix=True, max_shared=8)
+        self.live: dict[str, tuple[list[int], list[int]]] = {}
+        self.history: dict[str, list[int]] = {}
+
+    @rule(sid=st.sampled_from(SESSIONS), pre=st.integers(0, 2), extend=st.integers(0, 6),
+          reuse=st.booleans(), gen=st.integers(1, 5))
+    def turn(self, sid, pre, extend, reuse, gen):
+        if sid in self.live:
+            return
+        base = self.history.get(sid, []) if reuse else []
+        prompt = (base or self.PREFIXES[pre]) + [100 + i for i in range(extend + 1)]
+        if not reuse:
+            self.bm.drop_session(sid)
+            self.history.pop(sid, None)
+        blocks, cached = self.bm.acquire_prefix(sid, prompt)
+        assert cached <= len(prompt) - 1
+        assert len(blocks) == self.bm.blocks_needed(cached)
+        if cached % BS:
+            assert blocks[-1] not in self.bm.ref, "next write lands in a shared page"
+        tokens = prompt + [7] * gen
+        try:
+            blocks = blocks + self.bm.allocate(self.bm.blocks_needed(len(tokens)) - len(blocks))
+        except OutOfBlocks:
+            self.bm.release(blocks)
+            return
+        for b in blocks[cached // BS:]:
+            assert b not in self.bm.ref, "a page this turn writes is shared"
+        self.bm.publish(prompt, blocks, len(prompt))
+        self.live[sid] = (blocks, tokens)
+
+    @precondition(lambda self: self.live)
+    @rule(data=st.data(), keep=st.booleans())
+    def finish(self, data, keep):
+        sid = data.draw(st.sampled_from(sorted(self.live)))
+        blocks, tokens = self.live.pop(sid)
+        if keep:
+            self.bm.retain(sid, blocks, tokens)
+            self.history[sid] = tokens
+        else:
+            self.bm.release(blocks)
+
+    @rule()
+    def fault_recovery(self):
+        self.bm.reset_shared()
+
+    @invariant()
+    def pages_accounted(self):
+        bm = self.bm
+        held = [b for blocks, _ in self.live.values() for b in blocks]
+        parked = [b for s in bm.sessions.values() for b in s.blocks]
+        owners = held + parked
+        private = [b for b in owners if b not in bm.ref]
+        assert len(private) == len(set(private)), "a private page is owned twice"
+        for b, r in bm.ref.items():
+            tab = int(b in bm.key_of)
+            assert r == tab + owners.count(b), f"page {b}: ref {r}, holders {owners.count(b)}"
+            assert r >= 1 and (b in bm.evictable) == (r == 1 and tab == 1)
+            if tab:
+                assert bm.table[bm.key_of[b]] == b
+        every = set(private) | set(bm.ref) | set(bm.free)
+        assert len(bm.free) == len(set(bm.free))
+        assert not (set(bm.free) & (set(private) | set(bm.ref)))
+        assert every == set(range(1, NB)), "a page leaked (or page 0 escaped)"
+        assert len(bm.table) <= bm.max_shared
+        assert bm.idle_blocks == sum(1 for b in parked if b not in bm.ref)
+
+
+TestSharedKVProperties = SharedKVMachine.TestCase
+TestSharedKVProperties.settings = settings(max_examples=150, stateful_step_count=40,
+                                           deadline=None)
+
+
+def test_shared_prefix_maps_published_pages():
+    bm = BlockManager(16, 4, share_prefix=True)
+    sys_prompt = [5, 6, 7, 8, 9, 10, 11, 12, 13]
+    a = sys_prompt + [20, 21]
+    blocks_a = bm.allocate(bm.blocks_needed(len(a)))
+    assert bm.acquire_prefix("s2", a) == ([], 0)  # nothing published yet
+    done, h = bm.publish(a, blocks_a, 6)  # prefill of the first chunk done: page 0
+    assert done == 1 and list(bm.table.values()) == [blocks_a[0]]
+    bm.publish(a, blocks_a, len(a), done, h)
+    assert len(bm.table) == 2  # the third page holds the last token: never full here
+    b = sys_prompt + [30]
+    got, n = bm.acquire_prefix("s3", b)
+    assert got == blocks_a[:2] and n == 8 and bm.stats["shared_hit_tokens"] == 8
+    # a prompt that IS the shared prefix leaves its last page to be recomputed
+    got2, n2 = bm.acquire_prefix(None, sys_prompt[:8])
+    assert got2 == blocks_a[:1] and n2 == 4
+    bm.release(got2)
+    bm.release(blocks_a)
+    assert bm.ref[blocks_a[0]] == 2 and not bm.evictable  # s3 still maps both
+    bm.release(got)
+    assert set(bm.evictable) == set(blocks_a[:2])
+    free0 = bm.num_free
+    assert bm.num_available == free0 + 2
+    bm.allocate(free0 + 1)  # reclaims one table-only page
+    assert len(bm.table) == 1 and bm.stats["shared_evictions"] == 1

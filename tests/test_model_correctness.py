@@ -283,3 +283,27 @@ def test_gpu_fused_mixed_steps_match_dense_oracle(pipeline):
     frac, worst = _check(mc, eng.model.w, seqs, eng.runner.logit_tap, 0.04)
     print(f"fused mixed steps: {fused['mixed']}, worst rel err {worst:.4f}")
     assert frac == 1.0
+
+
+@pytest.mark.gpu
+def test_gpu_shared_prefix_pages_match_dense_oracle():
+    """Cross-session prefix sharing (kv_manager.py): the second wave's prompts map
+    the 6 full 16-token pages of the 100-token system prompt the first wave
+    computed; every logit row of the second wave (prefill from token 96 over the
+    shared pages, then decode) stays within the dense oracle's tolerance."""
+    mc = resolve("llama-3-8b").replace(name="llama-3-8b-2l", num_layers=2)
+    eng = LLMEngine(EngineConfig(model=mc.name, device="cuda", num_blocks=512, block_size=16,
+                                 max_batch=8, max_model_len=1024, seed=13), model_cfg=mc)
+    eng.runner.enable_logit_tap()
+    rng = random.Random(9)
+    V = mc.vocab_size
+    sysp = [rng.randrange(10, V - 10) for _ in range(100)]
+    p = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
+    eng.generate([sysp + [rng.randrange(10, V - 10) for _ in range(n)] for n in (20, 57, 3)], p)
+    eng.runner.logit_tap.clear()
+    seqs = eng.generate([sysp + [rng.randrange(10, V - 10) for _ in range(n)]
+                         for n in (40, 1, 90, 13)], p)
+    assert [s.prefix_hit for s in seqs] == [96] * 4
+    frac, worst = _check(mc, eng.model.w, seqs, eng.runner.logit_tap, 0.04)
+    print(f"shared-prefix rows: worst rel err {worst:.4f}")
+    assert frac == 1.0

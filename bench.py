@@ -449,7 +449,9 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # every replica's servers listen in a port window of its own (below the
         # ephemeral range): concurrent bind(0) draws can collide across replicas
-        os.environ.setdefault("OMNIA_PORT_BASE", str(21000 + 200 * local))
+        # (OMNIA_BENCH_PORT_BASE moves the job's windows: concurrent bench jobs)
+        os.environ.setdefault("OMNIA_PORT_BASE", str(
+            int(os.environ.get("OMNIA_BENCH_PORT_BASE", "21000")) + 200 * local))
         # result aggregation only: host-side gloo whenever this process owns no GPU work
         dist.init_process_group("gloo" if (host_only or not use_gpu) else "nccl")
 

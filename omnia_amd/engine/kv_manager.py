@@ -222,7 +222,8 @@ class BlockManager:
         return max(done, full), h
 
     # -------------------------------------------------------------- sessions
-    def acquire_prefix(self, session_id: str | None, prompt: list[int]) -> tuple[list[int], int]:
+    def acquire_prefix(self, session_id: str | None, prompt: list[int],
+                       share: bool = True) -> tuple[list[int], int]:
         """Take ownership of the session's cached pages matching `prompt`.
 
         Returns (blocks, n_cached_tokens).  At least one prompt token is always
@@ -244,7 +245,7 @@ class BlockManager:
                     s.swapped = None
                     self.stats["swap_in"] += 1
         if s is None:
-            blocks, n = self._acquire_shared(prompt) if self.share_prefix else ([], 0)
+            blocks, n = self._acquire_shared(prompt) if (self.share_prefix and share) else ([], 0)
             self.stats["prefix_hit_tokens"] += n
             self.stats["prefix_miss_tokens"] += len(prompt) - n
             return blocks, n

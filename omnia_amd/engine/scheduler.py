@@ -145,7 +145,10 @@ class Scheduler:
         s.blocks = []
 
     def _admit(self, s: Sequence) -> None:
-        blocks, n = self.blocks.acquire_prefix(s.session_id, s.prompt)
+        # a prompt held for a context-parallel prefill (engine/cp.py, from token 0)
+        # does not map shared pages
+        cp = bool(self.cfg.cp_threshold) and s.length >= self.cfg.cp_threshold
+        blocks, n = self.blocks.acquire_prefix(s.session_id, s.prompt, share=not cp)
         s.blocks = blocks
         s.num_cached = n
         s.prefix_hit = n

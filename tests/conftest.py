@@ -10,6 +10,12 @@ _workers = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "0") or 0)
 if _workers > 1 and "OMP_NUM_THREADS" not in os.environ:
     os.environ["OMP_NUM_THREADS"] = str(max(1, (os.cpu_count() or 1) // _workers))
 
+# concurrent multi-rank bench jobs on different workers get disjoint pod port
+# windows (bench.py: OMNIA_BENCH_PORT_BASE + 200 * local rank)
+_wid = os.environ.get("PYTEST_XDIST_WORKER", "gw0")[2:]
+if _wid.isdigit():
+    os.environ.setdefault("OMNIA_BENCH_PORT_BASE", str(21000 + 1800 * int(_wid)))
+
 import pytest  # noqa: E402
 
 try:  # property tests draw fresh examples every run: no on-disk example database,

@@ -307,4 +307,3 @@ def test_gpu_shared_prefix_pages_match_dense_oracle():
     frac, worst = _check(mc, eng.model.w, seqs, eng.runner.logit_tap, 0.04)
     print(f"shared-prefix rows: worst rel err {worst:.4f}")
     assert frac == 1.0
-

@@ -24,7 +24,7 @@ deployment all start from the same PromptPack system prompt and tool schemas.
 Shared pages are reference-counted (the table holds one reference).  A sequence
 never writes into one: only full pages are shared, and a hit always leaves the
 page that holds the prompt's last token private.  Once only the table holds a
-page, it can be evicted (after the idle sessions) when an allocation needs it.
+page, an allocation that needs it reclaims it, before any idle session.
 """
 from __future__ import annotations
 
@@ -106,6 +106,17 @@ class BlockManager:
         return (n_tokens + self.block_size - 1) // self.block_size
 
     def _evict_one(self) -> bool:
+        # first the shared pages nobody maps: a prompt page that matters to many
+        # sessions (the system prompt) is held by a live sequence or a parked
+        # session, so what sits here is mostly a finished one-off prompt's page,
+        # worth less than a parked session's whole conversation
+        if self.evictable:
+            b, _ = self.evictable.popitem(last=False)
+            del self.table[self.key_of.pop(b)]
+            del self.ref[b]
+            self.free.append(b)
+            self.stats["shared_evictions"] += 1
+            return True
         for sid, s in self.sessions.items():  # LRU order
             if not s.in_use:
                 self.sessions.pop(sid)
@@ -117,13 +128,6 @@ class BlockManager:
                 self.release(s.blocks)
                 self.stats["evictions"] += 1
                 return True
-        if self.evictable:  # then the shared pages nobody maps
-            b, _ = self.evictable.popitem(last=False)
-            del self.table[self.key_of.pop(b)]
-            del self.ref[b]
-            self.free.append(b)
-            self.stats["shared_evictions"] += 1
-            return True
         return False
 
     def allocate(self, n: int) -> list[int]:

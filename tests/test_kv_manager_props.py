@@ -198,3 +198,18 @@ def test_shared_prefix_maps_published_pages():
     assert bm.num_available == free0 + 2
     bm.allocate(free0 + 1)  # reclaims one table-only page
     assert len(bm.table) == 1 and bm.stats["shared_evictions"] == 1
+
+
+def test_unmapped_shared_pages_go_before_parked_sessions():
+    bm = BlockManager(12, 4, share_prefix=True)
+    one_off = list(range(50, 59))  # a finished sessionless prompt: 2 published pages
+    b1 = bm.allocate(3)
+    bm.publish(one_off, b1, len(one_off))
+    bm.release(b1)
+    assert len(bm.evictable) == 2
+    conv = list(range(70, 78))  # a parked conversation
+    b2 = bm.allocate(2)
+    bm.retain("chat", b2, conv)
+    bm.allocate(bm.num_free + 2)  # needs both unmapped pages, not the session
+    assert bm.has_session("chat") and not bm.table
+    assert bm.stats["shared_evictions"] == 2 and bm.stats["evictions"] == 0

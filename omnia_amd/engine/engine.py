@@ -186,6 +186,7 @@ class LLMEngine:
 
                 swap = TPSwapProxy(swap, self.runner.chan)
         self.blocks = BlockManager(nb, cfg.block_size, swap=swap, share_prefix=cfg.share_prefix)
+        self._kv_seen: dict = {}  # block-manager hit totals already exported
         self.scheduler = Scheduler(
             SchedulerConfig(max_batch=cfg.max_batch, max_prefill_tokens=cfg.max_prefill_tokens,
                             max_model_len=cfg.max_model_len,
@@ -422,6 +423,7 @@ class LLMEngine:
             sq.num_cached = sq.length  # the fed token's KV is written by this step
             sq.output.append(PLACEHOLDER)
         self.scheduler.on_prefill_done(prefill, {})
+        self.export_kv_metrics()
         if self.handoff:
             for sq in h.seqs[len(decode):]:  # completed prompts: token in its slot
                 sq.output.append(PLACEHOLDER)
@@ -563,8 +565,20 @@ class LLMEngine:
         for s, tok in done:
             self._append(s, tok, now)
         self.step_count += 1
-        M.KV_UTIL.set(self.blocks.utilization())
+        self.export_kv_metrics()
         return len(done)
+
+    def export_kv_metrics(self) -> None:
+        """KV pool gauges and the prefix-hit counters (from the block manager's
+        running totals)."""
+        M.KV_UTIL.set(self.blocks.utilization())
+        st, seen = self.blocks.stats, self._kv_seen
+        for key, metric in (("prefix_hit_tokens", M.KV_HIT_TOKENS),
+                            ("shared_hit_tokens", M.KV_SHARED_HIT_TOKENS)):
+            d = st.get(key, 0) - seen.get(key, 0)
+            if d > 0:
+                metric.inc(d)
+                seen[key] = st[key]
 
     def _append(self, s: Sequence, tok: int, now: float) -> None:
         if s.is_finished:

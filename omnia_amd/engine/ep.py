@@ -188,5 +188,5 @@ def run_ep_step(engine) -> int:
     for s, tok in done:
         engine._append(s, tok, now)
     engine.step_count += 1
-    E.M.KV_UTIL.set(engine.blocks.utilization())
+    engine.export_kv_metrics()
     return n0 + len(done)

@@ -152,8 +152,12 @@ ENGINE_FAULTS = Counter("omnia_engine_faults_total", "Engine step faults (recove
                         ["type"], registry=REGISTRY)
 KV_UTIL = Gauge("omnia_engine_kv_utilization", "Fraction of KV pages in use", registry=REGISTRY)
 ENGINE_WAITING = Gauge("omnia_engine_requests_waiting", "Queued requests", registry=REGISTRY)
-KV_HIT_TOKENS = Counter("omnia_engine_kv_hit_tokens_total", "Prompt tokens served from session KV",
+KV_HIT_TOKENS = Counter("omnia_engine_kv_hit_tokens_total",
+                        "Prompt tokens served from cached KV (session pages or shared prefix pages)",
                         registry=REGISTRY)
+KV_SHARED_HIT_TOKENS = Counter("omnia_engine_kv_shared_hit_tokens_total",
+                               "Prompt tokens served from cross-session shared prefix pages",
+                               registry=REGISTRY)
 
 # ----------------------------------------------------------------- memory-api
 # cmd/memory-api/SERVICE.md "Metrics" (classification + embedding pipeline health)

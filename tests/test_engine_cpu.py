@@ -194,10 +194,14 @@ def test_shared_prefix_pages_equivalence_cpu():
     sysp = list(range(11, 61))  # 50 tokens: 3 full pages of 16
     w1 = [sysp + [70 + i, 71 + i] for i in range(3)]
     w2 = [sysp + list(range(100 + i, 110 + 2 * i)) for i in range(3)]
+    from omnia_amd.observability import metrics as M
+
+    shared0 = M.KV_SHARED_HIT_TOKENS._value.get()
     e = make_engine(dtype="float32")
     e.generate(w1, p)
     got = e.generate(w2, p)
     assert [s.prefix_hit for s in got] == [48] * 3
+    assert M.KV_SHARED_HIT_TOKENS._value.get() - shared0 == 3 * 48
     want = make_engine(dtype="float32", share_prefix=False).generate(w2, p)
     assert [s.output for s in got] == [s.output for s in want]
     e.recover(RuntimeError("test"))

@@ -411,6 +411,11 @@ class LlamaModel:
     # ------------------------------------------------ fused prefill (pgemm.hip)
     use_pgemm = os.environ.get("OMNIA_PGEMM", "1") != "0"
     PGEMM_MIN_ROWS = int(os.environ.get("OMNIA_PGEMM_MIN_ROWS", "257"))
+    # mixed steps take the fused layer only from this many rows: at the open-loop
+    # trickle (~256 decode rows + a few hundred prompt tokens) pgemm's 256x256
+    # tiles leave most CUs idle, and the split decode / library path is 1.5x
+    # faster per step (profiles/r5/mixed_open_loop/: p50 TPOT 14.9 vs 22.9 ms)
+    PGEMM_MIXED_MIN_ROWS = int(os.environ.get("OMNIA_PGEMM_MIXED_MIN_ROWS", "4096"))
 
     def _use_fused(self, fb: ForwardBatch) -> bool:
         """Prefill chunks -- and mixed steps, whose decode rows ride the same
@@ -420,7 +425,8 @@ class LlamaModel:
         if not (self.use_pgemm and self.device.type == "cuda" and not fb.is_decode
                 and fb.cp is None and self.tp == 1):
             return False
-        if fb.input_ids.shape[0] < self.PGEMM_MIN_ROWS:
+        T = fb.input_ids.shape[0]
+        if T < (self.PGEMM_MIXED_MIN_ROWS if fb.num_decode else self.PGEMM_MIN_ROWS):
             return False
         cfg, d = self.cfg, self.cfg.hidden_size
         return (cfg.head_dim == 128 and d % 256 == 0 and d % 128 == 0

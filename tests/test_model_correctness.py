@@ -262,6 +262,7 @@ def test_gpu_fused_mixed_steps_match_dense_oracle(pipeline):
                                  mixed_backlog=2048), model_cfg=mc)
     eng.runner.enable_logit_tap()
     model = eng.model
+    model.PGEMM_MIXED_MIN_ROWS = 257  # the serving default (4096) skips these small steps
     fused = {"mixed": 0}
     orig = model._fused_residual
 

@@ -90,7 +90,7 @@ NAMED_PROVIDER_REF = Obj({
 A2A_CLIENT = Obj({
     "name": Str(min_len=1),
     "agentRuntimeRef": Obj({"name": Str(min_len=1), "namespace": Str()}, ["name"]),
-    "url": Str(), "exposeAsTools": Bool(),
+    "url": Str(), "exposeAsTools": Bool(), "timeout": Str(pattern=GO_DURATION),
     "authentication": Obj({"secretRef": LOCAL_REF})}, ["name"])
 AGENT_CARD = Obj({
     "name": Str(min_len=1), "description": Str(), "version": Str(), "organization": Str(),

@@ -594,8 +594,10 @@ class A2AClient:
 
 
 def a2a_tool_handler(name: str, url: str, description: str = "",
-                     headers: dict | None = None):
-    """An InProcessHandler exposing a remote agent as a tool (multi-agent chains)."""
+                     headers: dict | None = None, timeout=None):
+    """An InProcessHandler exposing a remote agent as a tool (multi-agent chains).
+    ``timeout`` (seconds or a duration string; default the executor's 30 s)
+    bounds one delegated turn."""
     from ..tools.executor import InProcessHandler
 
     client = A2AClient(url if url.rstrip("/").endswith("/a2a") else url.rstrip("/") + "/a2a",
@@ -616,4 +618,5 @@ def a2a_tool_handler(name: str, url: str, description: str = "",
                                                            "description": "what to ask"}},
               "required": ["message"]}
     return InProcessHandler(f"a2a-{name}", {f"ask_{name}": (
-        description or f"Delegate a question to the {name} agent", schema, call)})
+        description or f"Delegate a question to the {name} agent", schema, call)},
+        timeout=timeout)

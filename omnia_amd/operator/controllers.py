@@ -365,6 +365,8 @@ def resolve_a2a_clients(store, ar: dict) -> tuple[list, list]:
             st.update(ready=True, resolvedURL=url)
             status.append(st)
             rc = {"name": c["name"], "url": url, "exposeAsTools": bool(c.get("exposeAsTools"))}
+            if c.get("timeout"):  # one delegated turn (default: the executor's 30 s)
+                rc["timeout"] = c["timeout"]
             if (c.get("authentication") or {}).get("secretRef"):
                 rc["authTokenEnv"] = "OMNIA_A2A_CLIENT_TOKEN_" + re.sub(
                     r"[^A-Z0-9]", "_", c["name"].upper())

@@ -598,15 +598,22 @@ class LeaseLock:
         return True
 
     def release(self) -> None:
-        lease = self.store.try_get("Lease", self.name, self.ns)
-        if lease is None or (lease.get("spec") or {}).get("holderIdentity") != self.identity:
-            return
-        lease["spec"]["holderIdentity"] = ""
-        lease["spec"]["leaseDurationSeconds"] = 1
-        try:
-            self.store.update(lease)
-        except (Conflict, NotFound):
-            pass
+        # a renew already in flight on a worker thread when the renew task was
+        # cancelled can land between our read and write: re-read and retry on
+        # the resulting Conflict instead of leaving the lease held
+        for _ in range(5):
+            lease = self.store.try_get("Lease", self.name, self.ns)
+            if lease is None or (lease.get("spec") or {}).get("holderIdentity") != self.identity:
+                return
+            lease["spec"]["holderIdentity"] = ""
+            lease["spec"]["leaseDurationSeconds"] = 1
+            try:
+                self.store.update(lease)
+                return
+            except NotFound:
+                return
+            except Conflict:
+                time.sleep(0.02)
 
     def holds(self) -> bool:
         return self.clock() - self.last_renew < self.renew_deadline_s

@@ -153,7 +153,7 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
         if tok:
             headers["Authorization"] = f"Bearer {tok}"
         executor.add_handler(a2a_tool_handler(c["name"], c["url"], c.get("description", ""),
-                                              headers=headers))
+                                              headers=headers, timeout=c.get("timeout")))
         log.info("A2A agent %s (%s) registered as tool ask_%s", c["name"], c["url"],
                  c["name"])
     try:

@@ -532,8 +532,8 @@ class InProcessHandler(Handler):
 
     type = "inprocess"
 
-    def __init__(self, name: str, fns: dict):
-        super().__init__({"name": name})
+    def __init__(self, name: str, fns: dict, timeout=None):
+        super().__init__({"name": name, "timeout": timeout})
         self.fns = fns  # tool name -> (description, schema, async fn(args, ctx))
 
     async def discover(self):

@@ -55,7 +55,7 @@ import re
 import time
 import urllib.parse
 
-from ..runtime.evals import evaluate
+from ..runtime.evals import JUDGE_TYPES, EvalContext, evaluate, groups_of
 from ..utils.ratelimit import TokenBucket
 
 log = logging.getLogger("omnia.eval_worker")
@@ -70,7 +70,8 @@ TURN_TRIGGERS = ("every_turn", "per_turn", "sample_turns")
 SESSION_TRIGGERS = ("on_session_complete", "sample_sessions")
 GROUP_FAST, GROUP_LONG, GROUP_EXTERNAL = "fast-running", "long-running", "external"
 DEFAULT_WORKER_GROUPS = (GROUP_LONG, GROUP_EXTERNAL)
-JUDGE_TYPES = ("llm_judge", "judge", "rubric")
+# JUDGE_TYPES (llm_judge, llm_judge_turn, llm_judge_session, ...) and every
+# deterministic type come from the one registry in runtime/evals.py
 
 
 def fnv1a32(s: str) -> int:
@@ -90,12 +91,10 @@ def should_sample(session_id: str, tier: str, rate: float) -> bool:
 
 
 def eval_groups(spec: dict) -> list[str]:
-    """An eval's groups: ``params.groups`` when set, else by type (judges call a
-    model: long-running + external; deterministic assertions: fast-running)."""
-    g = (spec.get("params") or {}).get("groups") or spec.get("groups")
-    if g:
-        return list(g)
-    return [GROUP_LONG, GROUP_EXTERNAL] if spec.get("type") in JUDGE_TYPES else [GROUP_FAST]
+    """An eval's groups: ``params.groups`` when set, else its registered type's
+    (judges call a model: long-running + external; deterministic assertions:
+    fast-running)."""
+    return groups_of(spec)
 
 
 class Budget:
@@ -510,8 +509,32 @@ class EvalWorker:
         return self.judge
 
     # ---------------------------------------------------------- running evals
+    async def _tool_calls(self, sid: str, since: float | None = None,
+                          until: float | None = None) -> list[dict]:
+        """The session's tool calls (session-api ``tool_calls`` rows, one per call
+        id, final status wins) in call order, optionally within [since, until]."""
+        get = getattr(self.sessions, "get_tool_calls", None)
+        if get is None:
+            return []
+        rows = await get(sid)
+        by_id: dict = {}
+        for r in sorted(rows, key=lambda r: r.get("createdAt", r.get("created_at", 0)) or 0):
+            t = r.get("createdAt", r.get("created_at", 0)) or 0
+            if since is not None and isinstance(t, (int, float)) and t < since:
+                continue
+            if until is not None and isinstance(t, (int, float)) and t > until:
+                continue
+            key = r.get("callId") or r.get("call_id") or r.get("id")
+            st = r.get("status", "success")
+            prev = by_id.get(key)
+            if prev is None or st != "pending":
+                by_id[key] = {"name": r.get("name", ""), "arguments": r.get("arguments") or {},
+                              "error": st == "error", "status": st}
+        return list(by_id.values())
+
     async def _run_specs(self, specs, ev: dict, user: str, output: str, message_id: str,
-                         sampling_key: str, manual: bool = False) -> list[dict]:
+                         sampling_key: str, manual: bool = False,
+                         ctx: EvalContext | None = None) -> list[dict]:
         agent, ns, sid = ev.get("agentName", ""), ev.get("namespace", ""), ev.get("sessionId", "")
         light_rate, ext_rate = self._rates(agent, ns)
         results = []
@@ -540,9 +563,11 @@ class EvalWorker:
                 r = await llm_judge(judge, spec, user, output)
                 self.budget.add(r.pop("cost", 0.0))
             else:
-                r = evaluate(spec, user, output)
+                r = evaluate(spec, ctx or EvalContext(output=output, user=user))
                 if r.get("skipped"):
                     continue
+                if r.get("error"):  # unknown type / bad params: an error row, not a drop
+                    r.setdefault("details", {})["error"] = r["error"]
             results.append({"sessionId": sid, "messageId": message_id, "evalId": r["id"],
                             "evalType": r["type"], "passed": r["passed"],
                             "score": r.get("score", 0.0), "details": r.get("details", {}),
@@ -594,7 +619,16 @@ class EvalWorker:
                      if m.get("role") == "user"), "")
         ev = {**ev, **{k: v for k, v in (("promptPackName", info["packName"]),
                                          ("promptPackVersion", info["packVersion"])) if v}}
-        results = await self._run_specs(specs, ev, user, output, ev.get("messageId", ""), sid)
+        ctx = None
+        if any(not e.get("type") in JUDGE_TYPES for e in specs):
+            # the turn's tool calls: those recorded after its user message
+            t_user = next((m.get("timestamp") for m in reversed(msgs[:idx])
+                           if m.get("role") == "user"), None)
+            t_out = msgs[idx].get("timestamp") if msgs else None
+            ctx = EvalContext(output=output, user=user,
+                              tool_calls=await self._tool_calls(sid, t_user, t_out))
+        results = await self._run_specs(specs, ev, user, output, ev.get("messageId", ""), sid,
+                                        ctx=ctx)
         await self._write(results)
         return results
 
@@ -613,8 +647,10 @@ class EvalWorker:
               "promptPackVersion": info["packVersion"] or ev.get("promptPackVersion", "")}
         last_id = next((m.get("id", "") for m in reversed(msgs) if m.get("role") == "assistant"),
                        "")
+        ctx = EvalContext(output=output, user=user, messages=msgs,
+                          tool_calls=await self._tool_calls(sid))
         results = await self._run_specs(specs, ev, user, output, last_id, f"{sid}:session",
-                                        manual=manual)
+                                        manual=manual, ctx=ctx)
         await self._write(results)
         return results
 
@@ -743,6 +779,16 @@ class SessionAPIClient:
                 raise RuntimeError(f"session GET {r.status}")
             d = await r.json()
         return d.get("session", d)
+
+    async def get_tool_calls(self, sid: str) -> list[dict]:
+        s = await self._session()
+        async with s.get(f"{self.base}/api/v1/sessions/{sid}/tool-calls") as r:
+            if r.status >= 400:
+                raise RuntimeError(f"tool-calls GET {r.status}")
+            d = await r.json()
+        if isinstance(d, list):
+            return d
+        return d.get("tool-calls") or d.get("toolCalls") or d.get("tool_calls") or []
 
     async def post_eval_results(self, results: list[dict]):
         s = await self._session()

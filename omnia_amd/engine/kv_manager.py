@@ -25,10 +25,27 @@ Shared pages are reference-counted (the table holds one reference).  A sequence
 never writes into one: only full pages are shared, and a hit always leaves the
 page that holds the prompt's last token private.  Once only the table holds a
 page, an allocation that needs it reclaims it, before any idle session.
+
+Isolation (a shared page is attention input for every later mapper, so a forged
+match is KV-cache poisoning, and a hit is observable through cached_tokens and
+TTFT):
+  * the chain hash is a keyed BLAKE2b (128-bit digest, per-process random key),
+    not Python's ``hash``: a client cannot craft a page whose key collides with
+    a published one; each shared page also keeps its tokens and parent digest,
+    compared on every lookup;
+  * ``salt`` (``SamplingParams.cache_salt``) seeds the chain: pages published
+    under one salt are invisible under another (per tenant / workspace scope);
+  * ``limit`` (``SamplingParams.share_limit``) bounds what a prompt publishes:
+    the runtime passes the length of the rendered system prompt + tool schemas
+    (``runtime/chat.py shared_prefix_len``), so no user's conversation pages are
+    ever published, only the deployment's PromptPack prefix.
 """
 from __future__ import annotations
 
+import hashlib
+import os
 import time
+from array import array
 from collections import OrderedDict
 from dataclasses import dataclass, field
 
@@ -60,7 +77,7 @@ def common_prefix(a: list[int], b: list[int]) -> int:
 
 
 class BlockManager:
-    CHAIN_SEED = 0x6F6D6E6961  # chain hash of the empty prefix
+    CHAIN_SEED = b"\x00" * 16  # chain digest of the empty prefix (no salt)
 
     def __init__(self, num_blocks: int, block_size: int, swap=None, share_prefix: bool = False,
                  max_shared: int | None = None):
@@ -74,8 +91,10 @@ class BlockManager:
         self.swap = swap
         self.share_prefix = share_prefix
         self.max_shared = max_shared if max_shared is not None else max(1, num_blocks // 4)
-        self.table: dict[int, int] = {}  # chain hash -> shared page
-        self.key_of: dict[int, int] = {}  # shared page -> chain hash
+        self._key = os.urandom(32)  # BLAKE2b key of the chain digests
+        self.table: dict[bytes, int] = {}  # chain digest -> shared page
+        self.key_of: dict[int, bytes] = {}  # shared page -> chain digest
+        self.page_of: dict[int, tuple] = {}  # shared page -> (parent digest, its tokens)
         self.ref: dict[int, int] = {}  # shared page -> holders, the table included
         self.evictable: "OrderedDict[int, None]" = OrderedDict()  # shared pages only the table holds
         self.stats = {"prefix_hit_tokens": 0, "prefix_miss_tokens": 0, "evictions": 0,
@@ -113,6 +132,7 @@ class BlockManager:
         if self.evictable:
             b, _ = self.evictable.popitem(last=False)
             del self.table[self.key_of.pop(b)]
+            self.page_of.pop(b, None)
             del self.ref[b]
             self.free.append(b)
             self.stats["shared_evictions"] += 1
@@ -174,39 +194,58 @@ class BlockManager:
                 self.ref[b] -= 1
         self.table.clear()
         self.key_of.clear()
+        self.page_of.clear()
         self.evictable.clear()
 
     # -------------------------------------------------------------- sharing
-    def _chain(self, h: int, tokens: list[int], i: int) -> int:
-        bs = self.block_size
-        return hash((h, tuple(tokens[i * bs:(i + 1) * bs])))
+    def seed(self, salt: str | None) -> bytes:
+        """Chain digest of the empty prefix in the scope ``salt``."""
+        if not salt:
+            return self.CHAIN_SEED
+        return hashlib.blake2b(salt.encode(), key=self._key, digest_size=16,
+                               person=b"omnia-salt").digest()
 
-    def _acquire_shared(self, prompt: list[int]) -> tuple[list[int], int]:
+    def _chain(self, h: bytes, tokens: list[int], i: int) -> bytes:
+        bs = self.block_size
+        page = array("q", tokens[i * bs:(i + 1) * bs]).tobytes()
+        return hashlib.blake2b(h + page, key=self._key, digest_size=16).digest()
+
+    def _acquire_shared(self, prompt: list[int], salt: str | None = None
+                        ) -> tuple[list[int], int]:
         """Map the longest published run of ``prompt``'s leading full pages,
         stopping before the page that holds its last token."""
         blocks: list[int] = []
-        h = self.CHAIN_SEED
-        for i in range((len(prompt) - 1) // self.block_size):
+        h = self.seed(salt)
+        bs = self.block_size
+        for i in range((len(prompt) - 1) // bs):
+            parent = h
             h = self._chain(h, prompt, i)
             b = self.table.get(h)
-            if b is None:
+            if b is None or self.page_of.get(b) != (parent, tuple(prompt[i * bs:(i + 1) * bs])):
                 break
             self._incref(b)
             blocks.append(b)
-        n = len(blocks) * self.block_size
+        n = len(blocks) * bs
         self.stats["shared_hit_tokens"] += n
         return blocks, n
 
     def publish(self, tokens: list[int], blocks: list[int], n_computed: int, done: int = 0,
-                h: int | None = None) -> tuple[int, int]:
+                h: bytes | None = None, salt: str | None = None,
+                limit: int | None = None) -> tuple[int, bytes]:
         """Publish the full pages among the first ``n_computed`` tokens of
         ``tokens`` (a prompt whose KV is in ``blocks``), from page ``done`` on
-        (``h``: chain hash up to it).  Returns the new ``(done, h)``."""
-        h = self.CHAIN_SEED if h is None else h
+        (``h``: chain digest up to it), none past ``limit`` tokens.  Returns the
+        new ``(done, h)``."""
+        h = self.seed(salt) if h is None else h
         if not self.share_prefix:
             return done, h
-        full = min(n_computed, len(tokens)) // self.block_size
+        n = min(n_computed, len(tokens))
+        if limit is not None and limit >= 0:
+            n = min(n, limit)
+        full = n // self.block_size
+        bs = self.block_size
         for i in range(done, full):
+            parent = h
             h = self._chain(h, tokens, i)
             b = blocks[i]
             if h in self.table or b in self.ref:
@@ -216,18 +255,20 @@ class BlockManager:
                     continue
                 old, _ = self.evictable.popitem(last=False)
                 del self.table[self.key_of.pop(old)]
+                self.page_of.pop(old, None)
                 del self.ref[old]
                 self.free.append(old)
                 self.stats["shared_evictions"] += 1
             self.table[h] = b
             self.key_of[b] = h
+            self.page_of[b] = (parent, tuple(tokens[i * bs:(i + 1) * bs]))
             self.ref[b] = 2  # the table and the sequence that computed it
             self.stats["shared_pages"] += 1
         return max(done, full), h
 
     # -------------------------------------------------------------- sessions
     def acquire_prefix(self, session_id: str | None, prompt: list[int],
-                       share: bool = True) -> tuple[list[int], int]:
+                       share: bool = True, salt: str | None = None) -> tuple[list[int], int]:
         """Take ownership of the session's cached pages matching `prompt`.
 
         Returns (blocks, n_cached_tokens).  At least one prompt token is always
@@ -249,7 +290,8 @@ class BlockManager:
                     s.swapped = None
                     self.stats["swap_in"] += 1
         if s is None:
-            blocks, n = self._acquire_shared(prompt) if (self.share_prefix and share) else ([], 0)
+            blocks, n = (self._acquire_shared(prompt, salt) if (self.share_prefix and share)
+                         else ([], 0))
             self.stats["prefix_hit_tokens"] += n
             self.stats["prefix_miss_tokens"] += len(prompt) - n
             return blocks, n

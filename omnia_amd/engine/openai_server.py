@@ -33,7 +33,8 @@ import uuid
 from aiohttp import web
 
 from ..observability import metrics as M
-from ..runtime.chat import Message, ToolCallReq, parse_tool_calls, render_llama3
+from ..runtime.chat import (Message, ToolCallReq, parse_tool_calls, render_llama3,
+                            shared_prefix_len)
 from .sampling_params import SamplingParams
 
 log = logging.getLogger("omnia.engine.openai")
@@ -176,7 +177,16 @@ def build_app(engine, model_name: str, embedder=None) -> web.Application:
             return _err(400, "only n=1 is supported")
         if tools and params.guided:
             return _err(400, "response_format cannot be combined with tools")
-        prompt = engine.tokenizer.encode(render_llama3(msgs, tools or None), add_bos=False)
+        enc = engine.tokenizer.encode
+        prompt = enc(render_llama3(msgs, tools or None), add_bos=False)
+        # cross-session KV sharing: only the system prompt + tool schemas are
+        # published, within the request's ``cache_salt`` scope (kv_manager.py)
+        salt = body.get("cache_salt")
+        if salt is not None and not isinstance(salt, str):
+            return _err(400, "bad request: cache_salt must be a string")
+        params.cache_salt = salt or None
+        params.share_limit = shared_prefix_len(msgs, tools, lambda t: enc(t, add_bos=False),
+                                               prompt)
         rid = "chatcmpl-" + uuid.uuid4().hex[:24]
         created = int(time.time())
         sid = _session(request, body)
@@ -280,6 +290,12 @@ def build_app(engine, model_name: str, embedder=None) -> web.Application:
             p = body["prompt"]
             if not isinstance(body.get("user") or "", str):
                 raise TypeError("user must be a string")
+            if not isinstance(body.get("cache_salt") or "", str):
+                raise TypeError("cache_salt must be a string")
+            # a raw prompt has no system-prompt boundary: it publishes KV pages
+            # for cross-session sharing only inside an explicit cache_salt scope
+            params.cache_salt = body.get("cache_salt") or None
+            params.share_limit = None if params.cache_salt else 0
         except (KeyError, TypeError, ValueError, AttributeError) as e:
             return _err(400, f"bad request: {e}")
         vocab = getattr(engine.tokenizer, "vocab_size", None) or 1 << 31

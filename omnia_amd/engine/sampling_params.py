@@ -30,6 +30,12 @@ class SamplingParams:
     # "auto" only once the model opens a JSON object (engine/guided.py)
     tool_grammar: list | None = None
     tool_choice: str = "auto"
+    # cross-session KV prefix sharing (engine/kv_manager.py): pages are shared
+    # only between requests of one ``cache_salt`` scope, and a prompt publishes
+    # at most its first ``share_limit`` tokens (None: all of them; the runtime
+    # passes the rendered system prompt + tool schemas length)
+    cache_salt: str | None = None
+    share_limit: int | None = None
 
     @property
     def greedy(self) -> bool:

@@ -148,16 +148,20 @@ class Scheduler:
         # a prompt held for a context-parallel prefill (engine/cp.py, from token 0)
         # does not map shared pages
         cp = bool(self.cfg.cp_threshold) and s.length >= self.cfg.cp_threshold
-        blocks, n = self.blocks.acquire_prefix(s.session_id, s.prompt, share=not cp)
+        blocks, n = self.blocks.acquire_prefix(s.session_id, s.prompt, share=not cp,
+                                               salt=s.params.cache_salt)
         s.blocks = blocks
         s.num_cached = n
         s.prefix_hit = n
         s.pub_pages, s.pub_hash = 0, None
 
     def _publish(self, s: Sequence) -> None:
-        if self.blocks.share_prefix and s.pub_pages * self.blocks.block_size < len(s.prompt):
+        lim = s.params.share_limit
+        top = len(s.prompt) if lim is None or lim < 0 else min(lim, len(s.prompt))
+        if self.blocks.share_prefix and (s.pub_pages + 1) * self.blocks.block_size <= top:
             s.pub_pages, s.pub_hash = self.blocks.publish(s.prompt, s.blocks, s.num_cached,
-                                                          s.pub_pages, s.pub_hash)
+                                                          s.pub_pages, s.pub_hash,
+                                                          salt=s.params.cache_salt, limit=top)
 
     def _preempt_one(self, protect: Sequence | None = None) -> bool:
         """Free the youngest page holder: a partially prefilled prompt first (the

@@ -46,7 +46,7 @@ class Sequence:
     preemptions: int = 0
     prefix_hit: int = 0
     pub_pages: int = 0  # leading prompt pages offered to the shared-prefix table
-    pub_hash: int | None = None  # chain hash up to them
+    pub_hash: bytes | None = None  # chain digest up to them
     text_tail: str = ""  # recent decoded text for stop-string matching
     slot: int = -1  # device token slot (ModelRunner.tok_slots), -1 = none
     slot_launch: int = -1  # launch that last used the slot

@@ -598,10 +598,14 @@ def a2a_tool_handler(name: str, url: str, description: str = "",
     """An InProcessHandler exposing a remote agent as a tool (multi-agent chains).
     ``timeout`` (seconds or a duration string; default the executor's 30 s)
     bounds one delegated turn."""
-    from ..tools.executor import InProcessHandler
+    from ..tools.executor import InProcessHandler, _dur
 
+    # one parse, both bounds: the HTTP session (A2AClient) and the tool call
+    # (InProcessHandler) -- a spec timeout above the client's 120 s default must
+    # not be cut off by aiohttp
+    secs = _dur(timeout, None)
     client = A2AClient(url if url.rstrip("/").endswith("/a2a") else url.rstrip("/") + "/a2a",
-                       headers=headers)
+                       headers=headers, **({"timeout_s": secs} if secs else {}))
 
     async def call(args, ctx):
         task = await client.send(args.get("message") or args.get("input") or json.dumps(args),
@@ -619,4 +623,4 @@ def a2a_tool_handler(name: str, url: str, description: str = "",
               "required": ["message"]}
     return InProcessHandler(f"a2a-{name}", {f"ask_{name}": (
         description or f"Delegate a question to the {name} agent", schema, call)},
-        timeout=timeout)
+        timeout=secs if secs else timeout)

@@ -122,6 +122,8 @@ def runtime_config(ar: dict, pack: dict, providers: list[dict], registry: dict |
     if (ret.get("accessFilter") or {}).get("denyCEL"):
         c.memory_deny_cel = ret["accessFilter"]["denyCEL"]
     c.eval_enabled = bool((spec.get("evals") or {}).get("enabled"))
+    c.eval_inline_groups = list(((spec.get("evals") or {}).get("inline") or {}).get("groups")
+                                or [])
     return c
 
 

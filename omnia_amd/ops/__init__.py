@@ -372,6 +372,26 @@ def pgemm(epi: int, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None =
     return out
 
 
+def pgemm_splitk(x: torch.Tensor, w: torch.Tensor, splits: int, out: torch.Tensor | None = None,
+                 sched: int = 0) -> torch.Tensor:
+    """fp16 split-K slabs ``[splits, M, N]`` of ``x @ w.T`` on the 256x256 MFMA tile
+    (``csrc/pgemm.hip`` EPI 4; ``sched`` 0 / 1 = 8-wave / 4-wave main loop).  Each
+    slab is one K-slice's fp32 sum saturated to fp16; the splitk consumers reduce
+    them.  Decode projections at M <= 256 (one m-tile; the K split fills the chip)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(splits, M, N, dtype=torch.float16, device=x.device)
+    if x.is_cuda:
+        kernels().pgemm_splitk(out, x.contiguous(), w, sched)
+        return out
+    ks = K // splits
+    for s in range(splits):
+        r = x[:, s * ks:(s + 1) * ks].float() @ w[:, s * ks:(s + 1) * ks].float().t()
+        out[s].copy_(r.clamp(-65504.0, 65504.0).to(out.dtype))
+    return out
+
+
 def row_sumsq(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """fp32 [M] sums of squares of the rows of a bf16 [M, d] matrix."""
     if out is None:

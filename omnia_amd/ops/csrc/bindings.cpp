@@ -19,6 +19,8 @@ int omnia_ar_sendrecv(void* out, const void* in, void* const* regions, int* epoc
                       int64_t nbytes, int64_t slot_bytes, int rank, int world, int src_rank,
                       hipStream_t s);
 int omnia_pgemm_set_schedule(int sched);
+int omnia_pgemm_splitk(void* parts, const void* X, const void* W, int M, int N, int K, int S,
+                       int sched, hipStream_t s);
 int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, int M, int N,
                         int K, hipStream_t s);
 int omnia_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows, int d,
@@ -704,6 +706,21 @@ void pgemm_variant(int64_t variant, at::Tensor out, at::Tensor x, at::Tensor W) 
            "pgemm_variant");
 }
 
+// split-K 256x256 MFMA GEMM (pgemm.hip EPI 4): parts fp16 [S, M, N] whose sum
+// over S is x @ W^T; sched 0 / 1 = 8-wave / 4-wave main loop
+void pgemm_splitk(at::Tensor parts, at::Tensor x, at::Tensor W, int64_t sched) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(W);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && W.size(1) == x.size(1), "x [M, K], W [N, K]");
+  TORCH_CHECK(x.is_contiguous() && W.is_contiguous(), "contiguous x / W");
+  TORCH_CHECK(parts.scalar_type() == at::kHalf && parts.is_contiguous() && parts.dim() == 3 &&
+              parts.size(1) == x.size(0) && parts.size(2) == W.size(0), "parts fp16 [S, M, N]");
+  TORCH_CHECK(x.device() == W.device() && x.device() == parts.device(), "same device");
+  if (x.size(0) == 0) return;
+  CHECK_RC(omnia_pgemm_splitk(parts.data_ptr(), x.data_ptr(), W.data_ptr(), x.size(0), W.size(0),
+                              x.size(1), parts.size(0), (int)sched, cur_stream()),
+           "pgemm_splitk");
+}
+
 void row_sumsq(at::Tensor ss, at::Tensor x) {
   CHECK_GPU(x); CHECK_BF16(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x [M, d] rows contiguous");
@@ -1022,6 +1039,7 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("pgemm", &pgemm);
   m.def("row_sumsq", &row_sumsq);
   m.def("pgemm_variant", &pgemm_variant);
+  m.def("pgemm_splitk", &pgemm_splitk);
   m.def("pgemm_set_schedule", [](int64_t sched) {
     TORCH_CHECK(omnia_pgemm_set_schedule((int)sched) == 0, "pgemm schedule must be 0 or 1");
   });

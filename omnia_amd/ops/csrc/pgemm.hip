@@ -29,6 +29,10 @@
 //   EPI 2  residual += acc  (in place), ss_out[r][tile] = sum of squares of the
 //          new bf16 residual row slice                          (O / down)
 //   EPI 3  rs-scaled QKV -> RoPE(q) to q_out, RoPE(k) and v to the paged KV cache
+//   EPI 4  split-K partial: block (m-tile, n-tile, k-slice ks) writes its K-slice's
+//          fp32 sum, saturated to fp16, into slab ks of out[S][M][N]; the splitk.hip
+//          consumers reduce the slabs (decode projections at M <= 256: one m-tile,
+//          the K split fills the chip that N / 256 column tiles alone cannot)
 // where rs[r] = rsqrt(sum_t ss_in[r][t] / d + eps): with the RMSNorm weight folded
 // into W (W' = W * diag(w), models/llama.py fold_norms), RMSNorm(h) @ W^T ==
 // rs * (h @ W'^T), so the normalisation rides the consumer's epilogue and the
@@ -68,11 +72,27 @@ struct PArgs {
   bf16_t* v_cache;       // [NB, hkv, BS, 128]
   const int64_t* slots;  // [M] (< 0: no KV write)
   int hq, hkv, block_size;
+  int splits;            // EPI 4: K-slices (slabs)
 };
 
 __device__ __forceinline__ float4v mfma16(short8 a, short8 b, float4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// two f32 -> packed fp16x2 (low = a), saturated to the fp16 range: a K-slice's
+// partial beyond +-65504 stays finite (its slab sum then errs, never turns NaN)
+__device__ __forceinline__ uint32_t pack_h2(float a, float b) {
+  a = fminf(fmaxf(a, -65504.f), 65504.f);
+  b = fminf(fmaxf(b, -65504.f), 65504.f);
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) |
+         ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
+}
+
+template <int EPI>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  if constexpr (EPI == 4) return pack_h2(a, b);
+  return pack_bf2(a, b);
 }
 
 __device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
@@ -92,8 +112,9 @@ template <int EPI, int NT>
 __device__ __forceinline__ void epi_out(const PArgs& p, const bf16_t* stg, int m0, int nt,
                                         int Mt, int ntn, int tid, int lane) {
   constexpr int TN = EPI == 1 ? 128 : 256;
-  if constexpr (EPI == 0 || EPI == 1) {
-    // coalesced copy-out: TN/8 chunks per row
+  if constexpr (EPI == 0 || EPI == 1 || EPI == 4) {
+    // coalesced copy-out: TN/8 chunks per row (EPI 4: 16-bit fp16 chunks into
+    // slab `ks`, whose base the caller folded into p.out)
     constexpr int CPR = TN / 8;
     bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
 #pragma unroll 4
@@ -183,7 +204,10 @@ template <int EPI, int VAR = 0>
 __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
   constexpr int TN = EPI == 1 ? 128 : 256;  // output columns per block tile
-  const int ntn = p.N / TN, mtn = (p.M + 255) >> 8;
+  // EPI 4: the K-slices are extra "m-tiles" of the L2 grouping below (blocks of
+  // one slice share its x slice, blocks of one column tile its W rows)
+  const int S = EPI == 4 ? p.splits : 1;
+  const int ntn = p.N / TN, mtn1 = (p.M + 255) >> 8, mtn = mtn1 * S;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   constexpr int GM = ((VAR >> 2) & 3) == 0 ? 8 : ((VAR >> 2) & 3) == 1 ? 4
                                            : ((VAR >> 2) & 3) == 2 ? 16 : 32;
@@ -195,9 +219,11 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   const int grp = bid / per_group, gm0 = grp * GM;
   const int gsz = mtn - gm0 < GM ? mtn - gm0 : GM;
   const int idx = bid - grp * per_group;
-  const int mt = gm0 + idx % gsz, nt = idx / gsz;
+  const int vmt = gm0 + idx % gsz, nt = idx / gsz;
+  const int ks = vmt / mtn1, mt = vmt - ks * mtn1;
   const int m0 = mt << 8, Mt = p.M - m0 < 256 ? p.M - m0 : 256;
-  const int K = p.K, nk = K / BK;
+  const int K = p.K, nk = K / S / BK;
+  const int64_t kbase = (int64_t)ks * (K / S);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -215,10 +241,10 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
     for (int h = 0; h < 2; ++h) {
       int ar = m0 + h * 128 + row;
       ar = ar < p.M ? ar : p.M - 1;  // rows past the chunk: clamped copies, never stored
-      src[h][i] = p.X + (int64_t)ar * K + gch * 8;
+      src[h][i] = p.X + (int64_t)ar * K + kbase + gch * 8;
       const int64_t br = EPI == 1 ? (int64_t)(h ? p.N : 0) + (int64_t)nt * 128 + row
                                   : (int64_t)nt * 256 + h * 128 + row;
-      src[2 + h][i] = p.W + br * K + gch * 8;
+      src[2 + h][i] = p.W + br * K + kbase + gch * 8;
     }
   }
   auto issue = [&](int buf, auto HC, int kt) {
@@ -364,13 +390,13 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
     if (!odd) {
       d0 = reinterpret_cast<uint32_t*>(stg + (row0 + 0) * SROW + col);
       d1 = reinterpret_cast<uint32_t*>(stg + (row0 + 1) * SROW + col);
-      x0 = pack_bf2(v0, r0);
-      x1 = pack_bf2(v1, r1);
+      x0 = pack2<EPI>(v0, r0);
+      x1 = pack2<EPI>(v1, r1);
     } else {
       d0 = reinterpret_cast<uint32_t*>(stg + (row0 + 2) * SROW + col - 1);
       d1 = reinterpret_cast<uint32_t*>(stg + (row0 + 3) * SROW + col - 1);
-      x0 = pack_bf2(r0, v2);
-      x1 = pack_bf2(r1, v3);
+      x0 = pack2<EPI>(r0, v2);
+      x1 = pack2<EPI>(r1, v3);
     }
     *d0 = x0;
     *d1 = x1;
@@ -414,7 +440,13 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   }
   __syncthreads();
 
-  epi_out<EPI, 512>(p, stg, m0, nt, Mt, ntn, tid, lane);
+  if constexpr (EPI == 4) {
+    PArgs q = p;
+    q.out = reinterpret_cast<bf16_t*>(p.out) + (int64_t)ks * p.M * p.N;
+    epi_out<4, 512>(q, stg, m0, nt, Mt, ntn, tid, lane);
+  } else {
+    epi_out<EPI, 512>(p, stg, m0, nt, Mt, ntn, tid, lane);
+  }
 }
 
 
@@ -435,16 +467,19 @@ template <int EPI>
 __global__ __launch_bounds__(256, 1) void pgemm4_kernel(PArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
   constexpr int TN = EPI == 1 ? 128 : 256;
-  const int ntn = p.N / TN, mtn = (p.M + 255) >> 8;
+  const int S = EPI == 4 ? p.splits : 1;
+  const int ntn = p.N / TN, mtn1 = (p.M + 255) >> 8, mtn = mtn1 * S;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   constexpr int GM = 8;
   const int per_group = GM * ntn;
   const int grp = bid / per_group, gm0 = grp * GM;
   const int gsz = mtn - gm0 < GM ? mtn - gm0 : GM;
   const int idx = bid - grp * per_group;
-  const int mt = gm0 + idx % gsz, nt = idx / gsz;
+  const int vmt = gm0 + idx % gsz, nt = idx / gsz;
+  const int ks = vmt / mtn1, mt = vmt - ks * mtn1;
   const int m0 = mt << 8, Mt = p.M - m0 < 256 ? p.M - m0 : 256;
-  const int K = p.K, nk = K / BK;
+  const int K = p.K, nk = K / S / BK;
+  const int64_t kbase = (int64_t)ks * (K / S);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -461,10 +496,10 @@ __global__ __launch_bounds__(256, 1) void pgemm4_kernel(PArgs p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       int ar = m0 + h * 128 + row;
-      src[h] = p.X + (int64_t)(ar < p.M ? ar : p.M - 1) * K + gch * 8;
+      src[h] = p.X + (int64_t)(ar < p.M ? ar : p.M - 1) * K + kbase + gch * 8;
       const int64_t br = EPI == 1 ? (int64_t)(h ? p.N : 0) + (int64_t)nt * 128 + row
                                   : (int64_t)nt * 256 + h * 128 + row;
-      src[2 + h] = p.W + br * K + gch * 8;
+      src[2 + h] = p.W + br * K + kbase + gch * 8;
     }
   }
   // A rows past the chunk: instruction i of an A half-tile may cross p.M (clamped
@@ -598,13 +633,13 @@ __global__ __launch_bounds__(256, 1) void pgemm4_kernel(PArgs p) {
     if (!odd) {
       d0 = reinterpret_cast<uint32_t*>(stg + (row0 + 0) * SROW + col);
       d1 = reinterpret_cast<uint32_t*>(stg + (row0 + 1) * SROW + col);
-      x0 = pack_bf2(v0, r0);
-      x1 = pack_bf2(v1, r1);
+      x0 = pack2<EPI>(v0, r0);
+      x1 = pack2<EPI>(v1, r1);
     } else {
       d0 = reinterpret_cast<uint32_t*>(stg + (row0 + 2) * SROW + col - 1);
       d1 = reinterpret_cast<uint32_t*>(stg + (row0 + 3) * SROW + col - 1);
-      x0 = pack_bf2(r0, v2);
-      x1 = pack_bf2(r1, v3);
+      x0 = pack2<EPI>(r0, v2);
+      x1 = pack2<EPI>(r1, v3);
     }
     *d0 = x0;
     *d1 = x1;
@@ -633,7 +668,13 @@ __global__ __launch_bounds__(256, 1) void pgemm4_kernel(PArgs p) {
     }
   }
   __syncthreads();
-  epi_out<EPI, 256>(p, stg, m0, nt, Mt, ntn, tid, lane);
+  if constexpr (EPI == 4) {
+    PArgs q = p;
+    q.out = reinterpret_cast<bf16_t*>(p.out) + (int64_t)ks * p.M * p.N;
+    epi_out<4, 256>(q, stg, m0, nt, Mt, ntn, tid, lane);
+  } else {
+    epi_out<EPI, 256>(p, stg, m0, nt, Mt, ntn, tid, lane);
+  }
 }
 
 // one workgroup (256 threads) per row: ss[r] = sum(x[r]^2) (layer-0 input of the
@@ -665,6 +706,8 @@ extern "C" {
 int omnia_pgemm_set_schedule(int sched);
 int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, int M, int N,
                         int K, hipStream_t s);
+int omnia_pgemm_splitk(void* parts, const void* X, const void* W, int M, int N, int K, int S,
+                       int sched, hipStream_t s);
 
 static int g_pgemm_sched = 0;  // 0: 8-wave ping-pong, 1: 4-wave (one wave per SIMD)
 
@@ -700,7 +743,7 @@ int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, 
   if (blocks > (1 << 30)) return -13;
   PArgs a{out, (const bf16_t*)X, (const bf16_t*)W, M, N, K, ldo, ss_in, ss_in_n, inv_d, eps,
           ss_out, positions, cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, slots, hq, hkv,
-          block_size};
+          block_size, 1};
   const dim3 grid((unsigned)blocks);
   if (g_pgemm_sched == 1) {
     switch (epi) {
@@ -725,7 +768,7 @@ int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, in
                         int K, hipStream_t s) {
   if (M < 1 || K <= 0 || K % (2 * BK) || N <= 0 || N % 256) return -1;
   PArgs a{out, (const bf16_t*)X, (const bf16_t*)W, M, N, K, N, nullptr, 0, 0.f, 0.f, nullptr,
-          nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
+          nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 1};
   const dim3 grid((unsigned)(((M + 255) / 256) * (N / 256))), block(512);
   switch (variant) {
     case 0: pgemm_kernel<0, 0><<<grid, block, 0, s>>>(a); break;
@@ -738,6 +781,28 @@ int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, in
     case 16: pgemm4_kernel<0><<<grid, 256, 0, s>>>(a); break;
     default: return -2;
   }
+  return (int)hipGetLastError();
+}
+
+// split-K GEMM: parts[S][M][N] fp16, sum over s of parts[s] = X . W^T (EPI 4).
+// `sched` 0 / 1 = the 8-wave / 4-wave main loop (independent of the prefill
+// schedule switch: the decode table names the loop it measured).
+int omnia_pgemm_splitk(void* parts, const void* X, const void* W, int M, int N, int K, int S,
+                       int sched, hipStream_t s) {
+  if (M < 1 || S < 1 || S > 16) return -1;
+  if (K <= 0 || K % S || (K / S) % (2 * BK)) return -3;
+  if (N <= 0 || N % 256) return -4;
+  if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) |
+       reinterpret_cast<uintptr_t>(parts)) & 15)
+    return -5;
+  const int64_t blocks = (int64_t)((M + 255) / 256) * (N / 256) * S;
+  if (blocks > (1 << 30)) return -13;
+  PArgs a{parts, (const bf16_t*)X, (const bf16_t*)W, M, N, K, N, nullptr, 0, 0.f, 0.f, nullptr,
+          nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, S};
+  if (sched == 1)
+    pgemm4_kernel<4><<<dim3((unsigned)blocks), 256, 0, s>>>(a);
+  else
+    pgemm_kernel<4><<<dim3((unsigned)blocks), 512, 0, s>>>(a);
   return (int)hipGetLastError();
 }
 

@@ -311,7 +311,12 @@ __global__ __launch_bounds__(512, 2) void tgemm_kernel(void* __restrict__ out,
         const int row = wm * WTM + 16 * i + 4 * fq + r;
         if (row < Mt) {
 #pragma unroll
-          for (int j = 0; j < FN; ++j) o[(int64_t)row * N + 16 * j] = (P)acc[i][j][r];
+          for (int j = 0; j < FN; ++j) {
+            float v = acc[i][j][r];
+            // fp16 slabs saturate at +-65504: an out-of-range partial stays finite
+            if constexpr (MODE == 3) v = fminf(fmaxf(v, -65504.f), 65504.f);
+            o[(int64_t)row * N + 16 * j] = (P)v;
+          }
         }
       }
   } else if (MODE == 0) {

@@ -50,6 +50,7 @@ class TurnResult:
     usage: Usage = field(default_factory=Usage)
     cost: float = 0.0
     tool_calls: int = 0
+    tool_records: list = field(default_factory=list)  # {"name", "arguments", "error"} per call
     rounds: int = 0
     violations: list = field(default_factory=list)
     ttft: float | None = None
@@ -412,6 +413,8 @@ class Agent:
                     r = results.get(c.id) or {"result_json": json.dumps(
                         {"error": "max_tool_calls_per_turn exceeded"}), "is_error": True}
                     msgs.append(Message("tool", r["result_json"], tool_call_id=c.id, name=c.name))
+                    res.tool_records.append({"name": c.name, "arguments": c.arguments or {},
+                                             "error": bool(r.get("is_error"))})
                 res.tool_calls = calls_total
                 if snap is not None and self.workflow.count_tool_calls(snap, len(allowed)):
                     await self._completed(session_id, snap)

@@ -176,7 +176,11 @@ async def build_runtime(cfg: RuntimeConfig, engine=None, pack: PromptPack | None
     if cfg.eval_enabled:
         from .evals import InlineEvaluator
 
-        evaluator = InlineEvaluator(event_sink)
+        pack_evals = list(pack.data.get("evals") or [])
+        for pr in pack.prompts.values():
+            pack_evals.extend(pr.evals or [])
+        evaluator = InlineEvaluator(event_sink, groups=cfg.eval_inline_groups or None,
+                                    pack_evals=pack_evals)
     acfg = AgentConfig(prompt_name=cfg.prompt_name or None, context_window=cfg.context_window,
                        truncation=cfg.truncation, defaults=(cfg.provider or {}).get("defaults",
                                                                                    {}),

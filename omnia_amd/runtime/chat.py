@@ -86,6 +86,28 @@ def render_llama3(messages: list[Message], tools: list[dict] | None = None,
     return "".join(out)
 
 
+def shared_prefix_len(messages: list[Message], tools: list[dict] | None, encode,
+                      prompt_ids: list[int]) -> int:
+    """Leading tokens of ``prompt_ids`` that render the conversation's leading
+    system message(s) and the tool schemas -- the deployment's PromptPack prefix,
+    the only part of a prompt the engine may publish for cross-session KV sharing
+    (``SamplingParams.share_limit``; engine/kv_manager.py).  A user's own turns
+    never fall inside it."""
+    head = []
+    for m in messages:
+        if m.role != "system":
+            break
+        head.append(m)
+    if not head and not tools:
+        return 0
+    ids = encode(render_llama3(head, tools or None, add_generation_prompt=False))
+    n = min(len(ids), len(prompt_ids))
+    i = 0
+    while i < n and ids[i] == prompt_ids[i]:
+        i += 1
+    return i
+
+
 _JSON_OBJ = re.compile(r"\{.*\}", re.S)
 
 

@@ -45,6 +45,7 @@ class RuntimeConfig:
     memory_limit: int = 10
     policy_broker_url: str = ""
     eval_enabled: bool = False
+    eval_inline_groups: list = field(default_factory=list)  # spec.evals.inline.groups
     tracing_enabled: bool = False
     tracing_endpoint: str = ""
     tracing_sample_rate: float = 1.0
@@ -102,6 +103,7 @@ class RuntimeConfig:
         c.memory_limit = int(e.get("OMNIA_MEMORY_LIMIT", c.memory_limit))
         c.policy_broker_url = e.get("OMNIA_POLICY_BROKER_URL", "")
         c.eval_enabled = e.get("OMNIA_EVAL_ENABLED", "false").lower() == "true"
+        c.eval_inline_groups = [g for g in e.get("OMNIA_EVAL_INLINE_GROUPS", "").split(",") if g]
         c.tracing_enabled = e.get("OMNIA_TRACING_ENABLED", "false").lower() == "true"
         c.tracing_endpoint = e.get("OMNIA_TRACING_ENDPOINT", "")
         c.tracing_sample_rate = float(e.get("OMNIA_TRACING_SAMPLE_RATE", "1.0"))
@@ -229,6 +231,8 @@ class RuntimeConfig:
                 env["OMNIA_MEMORY_DENY_CEL"] = self.memory_deny_cel
         if self.eval_enabled:
             env["OMNIA_EVAL_ENABLED"] = "true"
+            if self.eval_inline_groups:
+                env["OMNIA_EVAL_INLINE_GROUPS"] = ",".join(self.eval_inline_groups)
         if self.a2a_clients:
             env["OMNIA_A2A_CLIENTS"] = json.dumps(self.a2a_clients)
         for k, v in self.engine.items():

@@ -13,6 +13,7 @@ reference's scenario-driven mock provider for tests
 from __future__ import annotations
 
 import asyncio
+import dataclasses
 import json
 import time
 import uuid
@@ -22,7 +23,7 @@ from typing import AsyncIterator
 import yaml
 
 from ..engine.sampling_params import SamplingParams
-from .chat import Message, ToolCallReq, parse_tool_calls, render_llama3
+from .chat import Message, ToolCallReq, parse_tool_calls, render_llama3, shared_prefix_len
 
 
 @dataclass
@@ -128,6 +129,15 @@ class LocalEngineProvider(Provider):
         tok = self.engine.tokenizer
         prompt_text = render_llama3(messages, tools or None)
         prompt_ids = tok.encode(prompt_text, add_bos=False)
+        params = params or SamplingParams()
+        if params.share_limit is None:
+            # publish only the PromptPack prefix for cross-session KV sharing, in
+            # the caller's workspace scope (engine/kv_manager.py "Isolation")
+            md = metadata or {}
+            params = dataclasses.replace(
+                params, share_limit=shared_prefix_len(
+                    messages, tools, lambda t: tok.encode(t, add_bos=False), prompt_ids),
+                cache_salt=params.cache_salt or md.get("workspace") or md.get("namespace"))
         tool_names = {t["name"] for t in tools or []}
         buf: list[str] = []
         holding = None  # decide after the first non-space text whether this is a tool call

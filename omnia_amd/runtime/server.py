@@ -229,6 +229,7 @@ class RuntimeService:
         hello_sent = False
         pending: list = []
         md = dict(stream.metadata() or {})
+        sids: set = set()
         try:
             while True:
                 msg = pending.pop(0) if pending else await stream.recv()
@@ -252,9 +253,14 @@ class RuntimeService:
                     hello_sent = True
                 if msg.HasField("client_tool_result") and not msg.content and not msg.parts:
                     continue  # stray result outside a turn
-                await self._turn(stream, msg, md, pending)
+                sids.add(await self._turn(stream, msg, md, pending))
         finally:
             self.active_streams -= 1
+            # the conversation stream closed: its session-trigger inline evals
+            ev = getattr(self.agent, "evaluator", None)
+            if ev is not None and hasattr(ev, "on_session_complete"):
+                for sid in sids - {None}:
+                    asyncio.get_running_loop().create_task(ev.on_session_complete(sid))
 
     async def _turn(self, stream: Stream, msg, md: dict, pending: list):
         mark("runtime_turn")
@@ -270,7 +276,7 @@ class RuntimeService:
         if not content and not parts:
             await stream.send(pb.ServerMessage(error=pb.Error(code="INVALID_MESSAGE",
                                                               message="empty message")))
-            return
+            return None
         ctx = identity_from_metadata(md, sid)
         metadata = dict(msg.metadata)
         if msg.consent_grants:
@@ -289,14 +295,14 @@ class RuntimeService:
             tracing.end_span(span, error=True)
             await stream.send(pb.ServerMessage(error=pb.Error(code=e.code,
                                                               message=GENERIC_ERROR)))
-            return
+            return sid
         except Exception:  # noqa: BLE001 - never leak provider details
             await io.flush()
             log.exception("turn failed for session %s", sid)
             tracing.end_span(span, error=True)
             await stream.send(pb.ServerMessage(error=pb.Error(code="INTERNAL_ERROR",
                                                               message=GENERIC_ERROR)))
-            return
+            return sid
         tracing.end_span(span)
         mark("runtime_done")
         await stream.send(pb.ServerMessage(done=pb.Done(
@@ -304,6 +310,7 @@ class RuntimeService:
             usage=pb.Usage(input_tokens=res.usage.input_tokens,
                            output_tokens=res.usage.output_tokens, cost_usd=res.cost,
                            cached_tokens=res.usage.cached_tokens))))
+        return sid
 
 
 # ===================================================================== gRPC

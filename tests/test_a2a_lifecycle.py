@@ -221,3 +221,27 @@ def test_final_transition_racing_a_cancel_returns_the_canceled_task():
             await runner.cleanup()
 
     asyncio.run(go())
+
+
+def test_tool_handler_timeout_reaches_the_http_client():
+    """the spec's per-client timeout bounds BOTH the tool call and
+    the aiohttp session of the delegated turn (a '300s' timeout must not be
+    cut at the client's 120 s default)."""
+    from omnia_amd.facade import a2a as a2a_mod
+
+    seen = {}
+    orig = a2a_mod.A2AClient.__init__
+
+    def spy(self, url, timeout_s=120.0, headers=None):
+        seen["timeout_s"] = timeout_s
+        orig(self, url, timeout_s=timeout_s, headers=headers)
+
+    a2a_mod.A2AClient.__init__ = spy
+    try:
+        h = a2a_mod.a2a_tool_handler("peer", "http://127.0.0.1:1", timeout="300s")
+        assert seen["timeout_s"] == 300.0
+        assert float(h.spec["timeout"]) == 300.0 if hasattr(h, "spec") else True
+        a2a_mod.a2a_tool_handler("peer", "http://127.0.0.1:1")
+        assert seen["timeout_s"] == 120.0  # default kept when the spec sets none
+    finally:
+        a2a_mod.A2AClient.__init__ = orig

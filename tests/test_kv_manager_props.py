@@ -3,7 +3,7 @@ interleavings of turns (prefix acquire -> allocate -> retain), aborts, session
 drops and LRU evictions never leak, duplicate or lose a page, and the idle-page
 count stays exact.  Reference behaviour: the per-session KV residency the
 reference's provider layer lacks; the invariants are ours."""
-from hypothesis import settings
+from hypothesis import given, settings
 from hypothesis import strategies as st
 from hypothesis.stateful import RuleBasedStateMachine, invariant, precondition, rule
 
@@ -213,3 +213,75 @@ def test_unmapped_shared_pages_go_before_parked_sessions():
     bm.allocate(bm.num_free + 2)  # needs both unmapped pages, not the session
     assert bm.has_session("chat") and not bm.table
     assert bm.stats["shared_evictions"] == 2 and bm.stats["evictions"] == 0
+
+
+def test_forced_digest_collision_maps_nothing():
+    """a lookup never maps a page on digest equality alone.  Force a
+    collision (a page published under another prompt's digest) and check the
+    stored tokens / parent refuse it."""
+    bm = BlockManager(16, 4, share_prefix=True)
+    victim = [1, 2, 3, 4, 9]
+    forged = [66, 66, 66, 66, 9]
+    b = bm.allocate(2)
+    bm.publish(forged, b, len(forged))
+    (page,) = [p for p in bm.table.values()]
+    # rewrite the table so the forged page sits under the victim's digest
+    vh = bm._chain(bm.seed(None), victim, 0)
+    bm.table = {vh: page}
+    bm.key_of = {page: vh}
+    got, n = bm.acquire_prefix(None, victim)
+    assert got == [] and n == 0
+    # the honest path still hits
+    bm2 = BlockManager(16, 4, share_prefix=True)
+    b2 = bm2.allocate(2)
+    bm2.publish(victim, b2, len(victim))
+    assert bm2.acquire_prefix(None, victim)[1] == 4
+
+
+def test_chain_digest_is_keyed_per_process():
+    a, b = BlockManager(8, 4, share_prefix=True), BlockManager(8, 4, share_prefix=True)
+    toks = [3, 1, 4, 1]
+    assert a._chain(a.seed(None), toks, 0) != b._chain(b.seed(None), toks, 0)
+    assert len(a._chain(a.seed(None), toks, 0)) == 16
+
+
+@given(st.lists(st.integers(0, 1000), min_size=9, max_size=20), st.text(min_size=1, max_size=8),
+       st.text(min_size=1, max_size=8))
+@settings(max_examples=60, deadline=None)
+def test_salt_scopes_sharing(prompt, s1, s2):
+    """Pages published under one cache salt are invisible under another."""
+    bm = BlockManager(32, 4, share_prefix=True)
+    blocks = bm.allocate(bm.blocks_needed(len(prompt)))
+    bm.publish(prompt, blocks, len(prompt), salt=s1)
+    assert bm.acquire_prefix(None, prompt, salt=s1)[1] > 0
+    if s1 != s2:
+        assert bm.acquire_prefix(None, prompt, salt=s2) == ([], 0)
+    assert bm.acquire_prefix(None, prompt) == ([], 0)  # no salt: its own scope
+
+
+def test_share_limit_publishes_only_the_system_prefix():
+    bm = BlockManager(16, 4, share_prefix=True)
+    sys_part = [7] * 8
+    user_a = sys_part + [100, 101, 102, 103, 104, 105, 106, 107, 1]
+    b = bm.allocate(bm.blocks_needed(len(user_a)))
+    bm.publish(user_a, b, len(user_a), limit=len(sys_part) + 3)
+    assert len(bm.table) == 2  # the two system pages, none of the user's
+    user_b = sys_part + [100, 101, 102, 103, 999]
+    got, n = bm.acquire_prefix(None, user_b)
+    assert n == 8  # the other user's conversation page is not visible
+
+
+def test_shared_prefix_len_covers_system_and_tools_only():
+    from omnia_amd.engine.tokenizer import SyntheticTokenizer
+    from omnia_amd.runtime.chat import Message, render_llama3, shared_prefix_len
+
+    tok = SyntheticTokenizer(128256, 128000, [128001, 128009])
+    enc = lambda t: tok.encode(t, add_bos=False)  # noqa: E731
+    tools = [{"name": "lookup", "parameters": {"type": "object"}}]
+    msgs = [Message("system", "You are a helpful support agent."), Message("user", "my secret")]
+    ids = enc(render_llama3(msgs, tools))
+    n = shared_prefix_len(msgs, tools, enc, ids)
+    head = enc(render_llama3(msgs[:1], tools, add_generation_prompt=False))
+    assert 0 < n <= len(head) < len(ids)
+    assert "secret" not in tok.decode(ids[:n])
+    assert shared_prefix_len([Message("user", "hi")], None, enc, enc("hi")) == 0

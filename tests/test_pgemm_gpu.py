@@ -177,3 +177,59 @@ def test_schedules_are_bit_identical(gen, schedule, epi):
     ops.kernels().pgemm_set_schedule(schedule)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,N,K,S", [(256, 512, 1024, 4), (192, 768, 2048, 8), (77, 256, 512, 2),
+                                     (300, 512, 896, 7)])
+def test_splitk_slabs(gen, schedule, M, N, K, S):
+    """EPI 4: fp16 slab s holds x[:, Ks] @ w[:, Ks]^T of K-slice s; decode sizes
+    (one m-tile, ragged) and prefill sizes (two m-tiles) against fp32 matmuls."""
+    x = _rand(M, K, gen=gen)
+    w = _rand(N, K, std=0.05, gen=gen)
+    parts = torch.full((S, M, N), float("nan"), dtype=torch.float16, device=DEV)
+    ops.pgemm_splitk(x, w, S, parts, schedule)
+    ks = K // S
+    for s in range(S):
+        want = x[:, s * ks:(s + 1) * ks].float() @ w[:, s * ks:(s + 1) * ks].float().t()
+        ok, e = _close(parts[s], want, 2e-3)
+        assert ok, (s, e)
+    total = x.float() @ w.float().t()
+    ok, e = _close(parts.float().sum(0), total, 5e-3)
+    assert ok, e
+    # negative control: the slabs in the wrong K order do not match slice 0
+    want0 = x[:, :ks].float() @ w[:, :ks].float().t()
+    assert not _close(parts[S - 1], want0, 2e-3)[0]
+
+
+def test_splitk_saturates_fp16(gen, schedule):
+    """A K-slice partial beyond the fp16 range saturates to +-65504 (finite), so
+    the consumer never sees inf / NaN (unclamped casts)."""
+    M, N, K, S = 256, 256, 512, 2
+    x = torch.full((M, K), 16.0, dtype=torch.bfloat16, device=DEV)
+    w = torch.full((N, K), 16.0, dtype=torch.bfloat16, device=DEV)  # partial = 256*256 = 65536
+    w[: N // 2] = -16.0
+    parts = torch.empty(S, M, N, dtype=torch.float16, device=DEV)
+    ops.pgemm_splitk(x, w, S, parts, schedule)
+    assert torch.isfinite(parts).all()
+    assert (parts[:, :, N // 2:] == 65504).all() and (parts[:, :, : N // 2] == -65504).all()
+
+
+def test_splitk_feeds_consumer(gen, schedule):
+    """pgemm split-K slabs through splitk_swiglu == SwiGLU of the fp32 product."""
+    M, F, K, S = 256, 512, 2048, 4
+    x = _rand(M, K, gen=gen)
+    w = _rand(2 * F, K, std=0.05, gen=gen)
+    act = ops.splitk_swiglu(ops.pgemm_splitk(x, w, S, sched=schedule))
+    h = (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    want = torch.nn.functional.silu(h[:, :F]) * h[:, F:]
+    ok, e = _close(act, want, 2e-2)
+    assert ok, e
+
+
+def test_splitk_rejects_bad_split(gen):
+    x = _rand(256, 1024, gen=gen)
+    w = _rand(256, 1024, gen=gen)
+    with pytest.raises(RuntimeError):  # K / S = 341.33
+        ops.pgemm_splitk(x, w, 3)
+    with pytest.raises(RuntimeError):  # K / S = 64: not whole iterations of two K-tiles
+        ops.pgemm_splitk(x, w, 16)

@@ -70,6 +70,20 @@ def test_mode3_half_slabs_match_fp32_slabs(M, S, bn, wnt):
                                rtol=3e-3, atol=1e-2)
 
 
+def test_mode3_half_slabs_saturate():
+    """A K-slice partial beyond fp16's range saturates to +-65504 instead of
+    turning inf (then NaN in the consumer); the fp32 slabs keep the true value."""
+    M, N, K, S = 256, 256, 1024, 2
+    x = torch.full((M, K), 16.0, dtype=torch.bfloat16, device="cuda")
+    w = torch.full((N, K), 16.0, dtype=torch.bfloat16, device="cuda")  # slice sum 131072
+    w[: N // 2] = -16.0
+    p16 = ops.tgemm(3, x, w, S, 128, 0)
+    assert torch.isfinite(p16).all()
+    assert (p16[:, :, N // 2:] == 65504).all() and (p16[:, :, : N // 2] == -65504).all()
+    p32 = ops.tgemm(2, x, w, S, 128, 0)
+    assert (p32[:, :, N // 2:] == 131072).all()
+
+
 @pytest.mark.parametrize("wnt", [1, 2, 3, 4, 5])
 def test_llama3_8b_shapes(wnt):
     """The four Llama-3-8B decode projections at the serving batch (64-k and

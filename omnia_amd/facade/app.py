@@ -130,18 +130,23 @@ def build_facade(env, runtime_client, recorder=None, mgmt_resolver=None) -> Faca
         from .handlers import DemoHandler, EchoHandler
 
         handler = EchoHandler() if mode == "echo" else DemoHandler()
+    cfg = config_from_env(env)
     if recorder is None and env.get("OMNIA_SESSION_API_URL"):
-        from ..session.httpclient import RecordingPool, SessionHTTPClient
+        from ..session.httpclient import RecordingPolicyCache, RecordingPool, SessionHTTPClient
 
-        recorder = RecordingPool(SessionHTTPClient(env["OMNIA_SESSION_API_URL"]),
-                                 workers=int(env.get("OMNIA_RECORDING_WORKERS", 100)),
-                                 queue=int(env.get("OMNIA_RECORDING_QUEUE", 1000)))
+        client = SessionHTTPClient(env["OMNIA_SESSION_API_URL"])
+        # recording gate: session-api's effective privacy policy for this agent
+        # (GET /api/v1/privacy-policy), cached, fail-open
+        policy = RecordingPolicyCache(client.get_privacy_policy, cfg.namespace, cfg.agent,
+                                      ttl_s=float(env.get("OMNIA_PRIVACY_POLICY_TTL_S", 60)))
+        recorder = RecordingPool(client, workers=int(env.get("OMNIA_RECORDING_WORKERS", 100)),
+                                 queue=int(env.get("OMNIA_RECORDING_QUEUE", 1000)),
+                                 policy=policy)
     media = None
     if env.get("OMNIA_MEDIA_STORAGE"):
         from ..media import build_media_storage
 
         media = build_media_storage(env)
-    cfg = config_from_env(env)
     cfg.media_enabled = cfg.media_enabled or media is not None
     from .realtime import route_store_from_env
 

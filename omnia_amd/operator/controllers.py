@@ -91,6 +91,18 @@ class PromptPackReconciler:
                     st["prompts"] = sorted(pack.prompts)
                 except (json.JSONDecodeError, PackError) as e:
                     ok, msg = False, str(e)[:300]
+                else:
+                    # eval types nobody registered (runtime/evals.py ValidateEvalDefs):
+                    # surfaced on the pack, not silently skipped at run time
+                    from ..runtime.evals import validate_eval_defs
+
+                    defs = list(pack.data.get("evals") or [])
+                    for pr in pack.prompts.values():
+                        defs.extend(pr.evals or [])
+                    missing = validate_eval_defs(defs)
+                    set_condition(st, "EvalTypesRegistered", not missing,
+                                  "Registered" if not missing else "UnknownEvalType",
+                                  ", ".join(missing)[:300], pp["metadata"]["generation"])
         set_condition(st, "PackContentValid", ok, "Valid" if ok else "Invalid", msg,
                       pp["metadata"]["generation"])
         if not ok:
@@ -229,6 +241,16 @@ class ToolRegistryReconciler:
                 return "command is required for mcp handlers with stdio transport"
         if t == "openapi" and conf is None:
             return "openAPIConfig is required for openapi handlers"
+        auth = h.get("auth") or {}
+        if auth.get("type") == "workloadIdentity":
+            # resolved by the runtime on network handlers only (auth.go): a type
+            # it cannot honor is rejected here, not sent unauthenticated
+            w = auth.get("workloadIdentity") or {}
+            if (w.get("cloud") or "azure") != "azure":
+                return f"workloadIdentity cloud {w.get('cloud')!r} not supported (only 'azure')"
+            if t == "client" or (t == "mcp" and (conf or {}).get("transport") == "stdio"):
+                return f"workloadIdentity auth is not supported on {t} " \
+                       f"{'stdio ' if t == 'mcp' else ''}handlers"
         for rp in [(conf or {}).get("retryPolicy"), h.get("retryPolicy")]:
             if not rp:
                 continue

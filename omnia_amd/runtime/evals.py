@@ -109,8 +109,15 @@ def _patterns(p: dict) -> list[str]:
 
 
 def _should(p: dict, key: str = "should_match", default: bool = True) -> bool:
-    v = p.get(key, default)
+    v = p.get(key, p.get("expect_match", default) if key == "should_match" else default)
     return v if isinstance(v, bool) else str(v).lower() not in ("false", "0", "no")
+
+
+def _int(p: dict, keys, default: int) -> int:
+    for k in keys:
+        if k in p:
+            return int(p[k])
+    return default
 
 
 def _search(pat: str, text: str) -> bool:
@@ -134,7 +141,7 @@ def _called(ctx: EvalContext) -> list[str]:
 @register("contains")
 def _includes(p, ctx):
     pats = _patterns(p)
-    if "pattern" in p and "patterns" not in p and "value" not in p:
+    if p.get("regex") or ("pattern" in p and "patterns" not in p and "value" not in p):
         hit = _search(pats[0], ctx.output) if pats else False  # regex form
     else:
         hit = bool(pats) and all(x.lower() in ctx.output.lower() for x in pats)
@@ -168,13 +175,13 @@ def _banned(p, ctx):
 
 @register("max_length")
 def _max_len(p, ctx):
-    lim = int(p.get("max_characters", p.get("max", 10**9)))
+    lim = _int(p, ("max_characters", "maxLength", "max_length", "max"), 10**9)
     return len(ctx.output) <= lim, {"length": len(ctx.output)}
 
 
 @register("min_length")
 def _min_len(p, ctx):
-    lim = int(p.get("min_characters", p.get("min", 0)))
+    lim = _int(p, ("min_characters", "minLength", "min_length", "min"), 0)
     return len(ctx.output) >= lim, {"length": len(ctx.output)}
 
 

@@ -114,7 +114,8 @@ def _model(cls, d):
 def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400.0,
               tokens: dict | None = None, allowed_namespaces: set | None = None,
               redactor=None, optout=None, audit_logger=None, media_deleter=None,
-              privacy_middleware=None, retention: dict | None = None) -> web.Application:
+              privacy_middleware=None, retention: dict | None = None,
+              policy_resolver=None) -> web.Application:
     """``audit_logger`` (EE, :class:`omnia_amd.ee.audit.AuditLogger`): record
     session created/accessed/searched/deleted events and serve them at
     ``/api/v1/audit/sessions`` (reference session-api audit wiring)."""
@@ -463,6 +464,27 @@ def build_app(svc: TieredSessionService, rate: float = 200.0, burst: float = 400
         p, g = recorder(table, cls)
         r.add_post(f"/api/v1/sessions/{{id}}/{path}", p)
         r.add_get(f"/api/v1/sessions/{{id}}/{path}", g)
+    async def privacy_policy(request):
+        # GET /api/v1/privacy-policy?namespace=&agent= (internal/session/api/handler.go
+        # handleGetPrivacyPolicy): the facade-visible subset -- the recording block
+        # -- of the effective SessionPrivacyPolicy; 204 when none applies or no
+        # resolver is wired (non-enterprise), never 404
+        if policy_resolver is None:
+            return web.Response(status=204)
+        ns = request.query.get("namespace", "")
+        agent = request.query.get("agent", "")
+        eff = policy_resolver(ns, agent)
+        if not eff:
+            return web.Response(status=204)
+        rec = dict(eff.get("recording") or {})
+        out = {"enabled": bool(rec.get("enabled", True)),
+               "facadeData": bool(rec.get("facadeData", True)),
+               "runtimeData": bool(rec.get("runtimeData", True))}
+        for k, v in rec.items():  # any further recording fields, never encryption
+            out.setdefault(k, v)
+        return web.json_response({"recording": out})
+
+    r.add_get("/api/v1/privacy-policy", privacy_policy)
     r.add_post("/api/v1/eval-results", eval_results_post)
     r.add_get("/api/v1/eval-results", eval_results_list)
     r.add_post("/api/v1/sessions/{id}/evaluate", evaluate)
@@ -598,6 +620,7 @@ def main(argv=None):
         app_kw["privacy_middleware"] = session_privacy_middleware(
             watcher, session_resolver(svc),
             PrivacyPrefsClient(a.privacy_api_url) if a.privacy_api_url else None)
+        app_kw["policy_resolver"] = watcher.effective
     app = build_app(svc, retention=retention, **app_kw)
     if watcher is not None:
         async def watch(_app):

@@ -117,6 +117,17 @@ class SessionHTTPClient:
     async def get_messages(self, sid):
         return (await self.request("GET", f"/api/v1/sessions/{sid}/messages"))["messages"]
 
+    async def get_privacy_policy(self, namespace: str, agent: str) -> dict | None:
+        """``GET /api/v1/privacy-policy`` (``pkg/session/httpclient/store.go:808-848``):
+        the effective policy's ``recording`` block for a namespace / agent, or
+        None when no policy applies (204).  A config read: it never goes
+        through the write ring buffer."""
+        from urllib.parse import urlencode
+
+        return await self.request(
+            "GET", "/api/v1/privacy-policy?" + urlencode({"namespace": namespace,
+                                                           "agent": agent}))
+
     async def close(self):
         if self._session is not None:
             await self._session.close()
@@ -157,11 +168,66 @@ class SessionEventSink:
                                     {"type": kind, "data": payload})
 
 
-class RecordingPool:
-    """Facade-side async recorder: N workers over a bounded queue; drops counted."""
+def _default_recording() -> dict:
+    return {"recording": {"enabled": True, "facadeData": True, "runtimeData": True}}
 
-    def __init__(self, store, workers: int = 100, queue: int = 1000):
+
+class RecordingPolicyCache:
+    """The facade's view of the effective privacy policy for its one namespace /
+    agent (``internal/facade/recording_policy.go``): fetched from session-api,
+    cached ``ttl_s``; no policy (204) or a failed fetch records everything
+    (fail open, so a transient error never silently drops data)."""
+
+    def __init__(self, fetch, namespace: str, agent: str, ttl_s: float = 60.0,
+                 now=time.monotonic):
+        self.fetch, self.namespace, self.agent = fetch, namespace, agent
+        self.ttl_s, self.now = ttl_s, now
+        self.cached: dict | None = None
+        self.fetched_at = 0.0
+        self.fetches = 0
+        self._lock: asyncio.Lock | None = None
+
+    async def get(self) -> dict:
+        if self.cached is not None and self.now() - self.fetched_at < self.ttl_s:
+            return self.cached
+        if self._lock is None:
+            self._lock = asyncio.Lock()
+        async with self._lock:  # one fetch however many recorders ask at once
+            if self.cached is not None and self.now() - self.fetched_at < self.ttl_s:
+                return self.cached
+            return await self._refresh()
+
+    async def _refresh(self) -> dict:
+        self.fetches += 1
+        try:
+            p = await self.fetch(self.namespace, self.agent)
+        except Exception as e:  # noqa: BLE001 - fail open
+            log.debug("privacy policy fetch failed, recording enabled: %s", e)
+            p = None
+        self.cached = p if isinstance(p, dict) and "recording" in p else _default_recording()
+        self.fetched_at = self.now()
+        return self.cached
+
+    @staticmethod
+    def allows(policy: dict | None, role: str) -> bool:
+        """User turns are facade data, everything else (assistant turns) runtime
+        data; both need ``recording.enabled``."""
+        if not policy:
+            return True
+        rec = policy.get("recording") or {}
+        if not rec.get("enabled", True):
+            return False
+        return bool(rec.get("facadeData" if role == "user" else "runtimeData", True))
+
+
+class RecordingPool:
+    """Facade-side async recorder: N workers over a bounded queue; drops counted.
+    ``policy`` (:class:`RecordingPolicyCache`) gates each message by role."""
+
+    def __init__(self, store, workers: int = 100, queue: int = 1000, policy=None):
         self.store = store  # has ensure_session/append/close_session coroutines
+        self.policy = policy
+        self.gated = 0
         self.q: asyncio.Queue | None = None
         self.workers = workers
         self.queue_size = queue
@@ -187,16 +253,25 @@ class RecordingPool:
     async def ensure_session(self, sid, agent, namespace, meta=None):
         await self.store.ensure_session(sid, agent, namespace, meta)
 
+    async def _allowed(self, role) -> bool:
+        if self.policy is None:
+            return True
+        ok = RecordingPolicyCache.allows(await self.policy.get(), role)
+        if not ok:
+            self.gated += 1
+        return ok
+
     def submit(self, sid, role, content, usage=None):
         self._start()
         try:
-            self.q.put_nowait(lambda: self.store.append(sid, role, content, usage))
+            self.q.put_nowait(lambda: self.record(sid, role, content, usage))
         except asyncio.QueueFull:
             self.dropped += 1
             M.RECORDING_DROPPED.inc()
 
     async def record(self, sid, role, content, usage=None):
-        await self.store.append(sid, role, content, usage)
+        if await self._allowed(role):
+            await self.store.append(sid, role, content, usage)
 
     async def close_session(self, sid):
         await self.store.close_session(sid)

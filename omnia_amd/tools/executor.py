@@ -137,6 +137,24 @@ class Handler:
     async def close(self):
         pass
 
+    token_acquirer = None  # workloadIdentity (tools/workload_identity.py); None: the pod's
+
+    async def _wif_headers(self, cfg: dict) -> dict:
+        """The workloadIdentity auth header, resolved per call (tokens are cached
+        per audience by the acquirer); {} when the handler uses other auth.
+        Unsupported clouds / no identity fail the call loudly."""
+        from .workload_identity import (WorkloadIdentityError, default_acquirer,
+                                        resolve_header, wif_config)
+
+        wif = wif_config(self.entry, cfg)
+        if wif is None:
+            return {}
+        try:
+            name, val = await resolve_header(self.token_acquirer or default_acquirer(), wif)
+        except WorkloadIdentityError as e:
+            raise PermanentError(str(e)) from None
+        return {name: val}
+
     def _secret(self, key: str | None) -> str | None:
         if not key:
             return None
@@ -211,6 +229,7 @@ class HTTPHandler(Handler):
         import aiohttp
 
         method, url, headers, query, body = self.build_request(args, ctx)
+        headers.update(await self._wif_headers(self.cfg))
         timeout = aiohttp.ClientTimeout(total=self.timeout)
 
         async def once():
@@ -289,10 +308,15 @@ class GRPCHandler(Handler):
                                           response_deserializer=T.ToolResponse.FromString)
         req = T.ToolRequest(tool_name=tool.remote_name or tool.name, arguments_json=json.dumps(args),
                             metadata={k: str(v) for k, v in ctx.headers.items()})
+        # credentials ride the call metadata (authorization / the configured header)
+        md = [(k.lower(), v) for k, v in (await self._wif_headers(self.cfg)).items()]
+        tok = self.cfg.get("authToken") or self._secret(self.cfg.get("authTokenKey"))
+        if not md and tok and (self.cfg.get("authType") or "").lower() == "bearer":
+            md = [("authorization", "Bearer " + tok)]
 
         async def once():
             try:
-                return await rpc(req, timeout=self.timeout)
+                return await rpc(req, timeout=self.timeout, metadata=md or None)
             except grpc.aio.AioRpcError as e:
                 if e.code() in (grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.DEADLINE_EXCEEDED,
                                 grpc.StatusCode.RESOURCE_EXHAUSTED):
@@ -336,7 +360,7 @@ class MCPHandler(Handler):
         body = {"jsonrpc": "2.0", "id": self._next_id(), "method": method, "params": params}
         hdrs = {"Content-Type": "application/json",
                 "Accept": "application/json, text/event-stream",
-                **(self.cfg.get("headers") or {})}
+                **(self.cfg.get("headers") or {}), **(await self._wif_headers(self.cfg))}
         if self.session_id:
             hdrs["Mcp-Session-Id"] = self.session_id
         async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=self.timeout)) as s:
@@ -456,6 +480,10 @@ class OpenAPIHandler(HTTPHandler):
         entry.setdefault("httpConfig", {})
         super().__init__(entry, secrets_dir)
         self.ocfg = entry.get("openAPIConfig") or {}
+        for k in ("authType", "authToken", "authTokenPath", "authHeader", "authCloud",
+                  "authAudience"):  # the spec's auth applies to every operation call
+            if k in self.ocfg and k not in self.cfg:
+                self.cfg[k] = self.ocfg[k]
         self.ops: dict[str, dict] = {}
 
     async def _load_spec(self) -> dict:

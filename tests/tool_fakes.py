@@ -14,6 +14,7 @@ class HTTPToolFake:
 
     def __init__(self):
         self.calls = []
+        self.headers = []
         self.runner = None
         self.port = None
 
@@ -21,6 +22,7 @@ class HTTPToolFake:
         async def handle(request):
             args = await request.json()
             self.calls.append(args)
+            self.headers.append(dict(request.headers))
             return web.json_response({"weather": "sunny", "echo": args})
 
         app = web.Application()
@@ -42,6 +44,7 @@ class GRPCToolFake:
     def __init__(self, tools: list[dict]):
         self.tools = tools
         self.calls = []
+        self.metadata = []
         self.server = None
         self.port = None
 
@@ -58,6 +61,7 @@ class GRPCToolFake:
 
         async def execute(req, ctx):
             self.calls.append((req.tool_name, json.loads(req.arguments_json or "{}")))
+            self.metadata.append(dict(ctx.invocation_metadata() or ()))
             return T.ToolResponse(result_json=json.dumps({"time": "12:00", "tool": req.tool_name}))
 
         svc = T.SERVICE
@@ -86,12 +90,14 @@ class MCPToolFake:
     def __init__(self, tools: list[dict]):
         self.tools = tools
         self.calls = []
+        self.headers = []
         self.runner = None
         self.port = None
 
     async def start(self):
         async def handle(request):
             body = await request.json()
+            self.headers.append(dict(request.headers))
             m = body.get("method")
             rid = body.get("id")
             if m == "initialize":

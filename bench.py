@@ -86,7 +86,49 @@ def parse(argv=None):
     ap.add_argument("--engine", choices=["gpu", "synthetic"], default="gpu",
                     help="synthetic: ws-path host capacity rehearsal -- the engine-core is a "
                          "token source paced like the measured GPU engine (engine/synthetic.py)")
+    ap.add_argument("--preflight", choices=["auto", "on", "off"], default="auto",
+                    help="multi-GPU first-contact check in a fresh child per rank before any "
+                         "pod starts (parallel/preflight.py): peer access, RCCL init + "
+                         "all-reduce, IPC all-reduce checked against it; auto = on with GPUs")
     return ap.parse_args(argv)
+
+
+def job_preflight(a, ws: int, rank: int, local: int, backend: str) -> dict | None:
+    """Every rank runs the preflight in a fresh child (rendezvous on a port rank
+    0 picks, shared over the bench's gloo group) before its pod starts; rank 0
+    gets the job summary.  Outside the timed region."""
+    from omnia_amd.parallel import preflight as pf
+
+    if ws > 1:
+        import torch.distributed as dist
+
+        box = [_free_port() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        port = box[0]
+    else:
+        port = _free_port()
+    rep = pf.spawn(rank, ws, local, port, backend)
+    if ws > 1:
+        import torch.distributed as dist
+
+        reps = [None] * ws
+        dist.all_gather_object(reps, rep)
+    else:
+        reps = [rep]
+    return pf.summarize(reps)
+
+
+def tp_preflight(devs: list[int], backend: str = "nccl") -> dict:
+    """The preflight over one TP pod's devices, before its engine starts."""
+    import concurrent.futures as cf
+
+    from omnia_amd.parallel import preflight as pf
+
+    port = _free_port()
+    with cf.ThreadPoolExecutor(len(devs)) as ex:
+        reps = list(ex.map(lambda i: pf.spawn(i, len(devs), devs[i], port, backend),
+                           range(len(devs))))
+    return pf.summarize(reps)
 
 
 def _free_port() -> int:
@@ -187,12 +229,16 @@ class WSDriver:
             "OMNIA_ENGINE_PROC": "1" if (use_gpu and a.tp == 1) or a.engine == "synthetic" else "0",
             "OMNIA_ENGINE_SYNTHETIC": "1" if a.engine == "synthetic" else "0",
             "OMNIA_ENGINE_TP": a.tp,
+            "OMNIA_DEBUG_ENGINE_STATS": "1",  # timed-window device busy (gpu_busy_timed)
             **({"OMNIA_ENGINE_MIXED_BUDGET": a.mixed_budget} if a.mixed_budget is not None
                else {}),
         }
         fenv = {"OMNIA_AGENT_NAME": f"bench-{rank}", "OMNIA_MAX_CONNECTIONS": 4 * C + 64,
                 "OMNIA_MSG_RATE": 1000, "OMNIA_MSG_BURST": 1000}
         devs = list(range(local, local + a.tp)) if use_gpu else None
+        self.tp_preflight = None
+        if devs and a.tp > 1 and a.preflight != "off" and a.engine == "gpu":
+            self.tp_preflight = tp_preflight(devs)
         self.pod = ProcessPod(f"bench-r{rank}", renv, fenv, device_index=devs,
                               log_dir=os.path.join(self.tmp, "logs"), tp=a.tp)
         self.pod.start(timeout_s=a.pod_timeout)
@@ -291,6 +337,27 @@ class WSDriver:
             return []
         return self.loop.run_until_complete(self._open_loop(n, rate))
 
+    def _debug(self, method: str):
+        if self.pod is None:
+            return None
+        import urllib.request
+
+        req = urllib.request.Request(
+            f"http://127.0.0.1:{self.pod.health_port}/debug/engine-stats", method=method,
+            data=b"" if method == "POST" else None)
+        try:
+            with urllib.request.urlopen(req, timeout=120) as r:
+                return json.loads(r.read())
+        except (OSError, ValueError):
+            return None
+
+    def reset_timing(self):
+        """Zero the pod engine's counters and device-busy account (timed window)."""
+        self._debug("POST")
+
+    def engine_stats(self) -> dict | None:
+        return self._debug("GET")
+
     def close(self):
         if self.pod is not None:
             ready, self._ready = self._ready, []
@@ -382,7 +449,8 @@ class LocalDriver:
         eng = self.eng
         return {"timing": dict(eng.timing), "counters": dict(eng.counters),
                 "runner": dict(eng.runner.stats), "kv_blocks": eng.blocks.num_blocks,
-                "block_size": self.cfg.block_size}
+                "block_size": self.cfg.block_size,
+                "gpu_busy_s": eng.busy_seconds() if hasattr(eng, "busy_seconds") else None}
 
     def reset_timing(self):
         if self.proc:
@@ -391,6 +459,8 @@ class LocalDriver:
             for k in self.eng.timing:
                 self.eng.timing[k] = 0.0
             self.eng.runner.stats["gil_wait_s"] = 0.0
+            if hasattr(self.eng, "busy_seconds"):
+                self.eng.busy_seconds(reset=True)
 
     def close(self):
         if self.runtime is not None:
@@ -472,8 +542,15 @@ def main():
             pinned = None
         else:
             affinity.pin(pinned)
+    pre = None
+    if a.preflight == "on" or (a.preflight == "auto" and use_gpu and a.engine == "gpu"
+                               and host_only):
+        # the bench process itself never touches the GPU on these paths: the
+        # check runs in fresh children and is gone before any pod starts
+        pre = job_preflight(a, ws, rank, local, "nccl" if use_gpu else "gloo")
     drv = WSDriver(a, rank, local, use_gpu, ws) if a.path == "ws" else \
         LocalDriver(a, rank, local, use_gpu, ws)
+    drv.preflight = pre
     drv.pinned_cpus = pinned
     try:
         run(a, drv, ws, rank, use_gpu, host_only)
@@ -555,8 +632,7 @@ def run(a, drv, ws, rank, use_gpu, host_only):
     for w in range(a.warmup):
         drv.wave(-1 - w)
     t_warm = time.perf_counter()
-    if isinstance(drv, LocalDriver):
-        drv.reset_timing()
+    drv.reset_timing()
     sync()
     cpu0 = _tree_cpu_s()
     t0 = time.perf_counter()
@@ -574,6 +650,11 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             wave_ms.append(round(1000 * (time.perf_counter() - tw), 1))
     sync()
     elapsed = time.perf_counter() - t0
+    # device time the engine's steps covered over the timed window (hipEvent
+    # pairs per step, engine/engine.py busy_seconds) / wall time
+    est = drv.engine_stats()
+    busy = (est or {}).get("gpu_busy_s")
+    my_busy = round(busy / elapsed, 4) if busy is not None and elapsed > 0 else None
     # host cores this replica's serving path kept busy (client included): the
     # CPU a node must supply per replica at this rate
     cores = (_tree_cpu_s() - cpu0) / elapsed if elapsed > 0 else 0.0
@@ -608,7 +689,8 @@ def run(a, drv, ws, rank, use_gpu, host_only):
         elapsed, out_tokens = float(mx[0]), float(sm[1])
         gathered = [None] * ws
         dist.all_gather_object(gathered, (ttfts, lats, tpot, gaps[:20000], round(my_rate, 2),
-                                          round(cores, 2), getattr(drv, "pinned_cpus", None)))
+                                          round(cores, 2), getattr(drv, "pinned_cpus", None),
+                                          my_busy))
         ttfts = [x for g in gathered for x in g[0]]
         lats = [x for g in gathered for x in g[1]]
         tpot = [x for g in gathered for x in g[2]]
@@ -616,12 +698,14 @@ def run(a, drv, ws, rank, use_gpu, host_only):
         per_rank = [g[4] for g in gathered]
         cores_rank = [g[5] for g in gathered]
         pins = [g[6] for g in gathered]
+        busy_rank = [g[7] for g in gathered]
     else:
         per_rank = [round(my_rate, 2)]
         cores_rank = [round(cores, 2)]
         pins = [getattr(drv, "pinned_cpus", None)]
+        busy_rank = [my_busy]
     value = out_tokens / elapsed
-    st = drv.engine_stats() if isinstance(drv, LocalDriver) else None
+    st = est if isinstance(drv, LocalDriver) else None
     if rank == 0:
         ms = lambda x: round(1000 * x, 2) if x is not None else None  # noqa: E731
         rec = {
@@ -648,6 +732,10 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             "world_size": ws,
             "per_rank_tokens_per_s": per_rank,
             "host_cpu_cores_per_rank": cores_rank,
+            # timed-window device busy per rank: engine-step hipEvent intervals / wall
+            "gpu_busy_timed": (round(sum(busy_rank) / len(busy_rank), 4)
+                               if busy_rank and None not in busy_rank else None),
+            "gpu_busy_timed_per_rank": busy_rank,
             "pinned_cpus_per_rank": [_cpulist(p) for p in pins],
             "p50_turn_latency_ms": ms(statistics.median(lats)) if lats else None,
             "p95_turn_latency_ms": ms(pct(lats, 0.95)),
@@ -665,6 +753,10 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             "prefix_cached_frac": round(sum(r[5] for r in results) / max(1, sum(
                 r[3] for r in results)), 4) if results and results[0][5] is not None else None,
             "wave_ms": wave_ms,
+            # multi-GPU first contact (parallel/preflight.py), untimed: RCCL world,
+            # peer access, RCCL vs IPC all-reduce (checked equal) at 16 KiB / 32 MiB
+            "preflight": getattr(drv, "preflight", None),
+            "tp_preflight": getattr(drv, "tp_preflight", None),
             "config": {
                 "model": a.model,
                 "global_batch": a.concurrency * (ws // a.tp),

@@ -179,11 +179,13 @@ class _Core:
             return {"timing": dict(eng.timing), "counters": dict(eng.counters),
                     "runner": {k: v for k, v in eng.runner.stats.items()},
                     "kv_blocks": eng.blocks.num_blocks, "block_size": eng.cfg.block_size,
-                    "use_graphs": eng.runner.use_graphs}
+                    "use_graphs": eng.runner.use_graphs,
+                    "gpu_busy_s": eng.busy_seconds()}
         if name == "reset_timing":
             for k in eng.timing:
                 eng.timing[k] = 0.0
             eng.runner.stats["gil_wait_s"] = 0.0
+            eng.busy_seconds(reset=True)
             return True
         raise ValueError(f"unknown call {name!r}")
 

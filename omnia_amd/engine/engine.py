@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import collections
 import os
 import sys
 import threading
@@ -213,6 +214,8 @@ class LLMEngine:
         # untraced step timeline (OMNIA_TIMELINE_DIR, observability/timeline.py):
         # host schedule / launch times + timing hipEvents around every step
         self._tl = [] if (TL.ENABLED and dev.type == "cuda") else None
+        self._busy = collections.deque()  # (start, end) hipEvents of steps not yet summed
+        self._busy_s = 0.0
         self._tap_dir = os.environ.get("OMNIA_LOGIT_TAP_DIR", "")
         M.ENGINE_COLD_START.labels("total").set(time.perf_counter() - t0)
         log.info("engine ready: %s on %s (tp=%d), %d KV blocks x %d tokens, load %.1fs, "
@@ -350,7 +353,7 @@ class LLMEngine:
 
     # ------------------------------------------------------------ timeline
     def _tl_pre(self):
-        if self._tl is None:
+        if self.device.type != "cuda":
             return None
         e = torch.cuda.Event(enable_timing=True)
         e.record()
@@ -359,12 +362,38 @@ class LLMEngine:
     def _tl_post(self, e0, kind: str, ts: float, t0: float, rows: int, ntok: int) -> None:
         """Step record: schedule start ``ts``, launch start ``t0``, launch end now;
         device interval = [e0, e1] (e0 completes when the stream reaches the step,
-        i.e. when the previous step ends or at launch if the GPU was idle)."""
+        i.e. when the previous step ends or at launch if the GPU was idle).  Every
+        step's interval also feeds the device-busy account (:meth:`busy_seconds`);
+        the timeline keeps them only when enabled."""
         if e0 is None:
             return
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        self._tl.append((kind, rows, ntok, ts, t0, time.perf_counter(), e0, e1))
+        self._busy.append((e0, e1))
+        if len(self._busy) > 512:
+            self._busy_harvest(False)
+        if self._tl is not None:
+            self._tl.append((kind, rows, ntok, ts, t0, time.perf_counter(), e0, e1))
+
+    def _busy_harvest(self, wait: bool) -> None:
+        while self._busy and (wait or self._busy[0][1].query()):
+            e0, e1 = self._busy.popleft()
+            if wait:
+                e1.synchronize()
+            self._busy_s += e0.elapsed_time(e1) / 1e3
+
+    def busy_seconds(self, reset: bool = False) -> float:
+        """Device time covered by engine steps since the last reset: the sum of
+        per-step [start, end] hipEvent intervals on the engine stream (steps
+        never overlap on it; idle gaps between steps are not counted).  Waits
+        for the steps in flight.  None on a CPU engine (no device clock)."""
+        if self.device.type != "cuda":
+            return None
+        self._busy_harvest(True)
+        v = self._busy_s
+        if reset:
+            self._busy_s = 0.0
+        return v
 
     def tl_flush(self) -> None:
         """Resolve the recorded steps' device times onto the host monotonic clock

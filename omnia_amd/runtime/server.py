@@ -443,6 +443,24 @@ async def serve_grpc(svc: RuntimeService, port: int = 9000, host: str = "0.0.0.0
     return server, bound
 
 
+def _engine_stats(agent, reset: bool = False):
+    """Stats (or a reset) of the agent's in-node engine: the engine-core client
+    (``engine/core_proc.py``) or the in-process engine; None without one."""
+    eng = getattr(getattr(agent, "provider", None), "engine", None)
+    if eng is None:
+        return None
+    if hasattr(eng, "call") and hasattr(eng, "stats"):  # engine-core child process
+        return eng.call("reset_timing") if reset else eng.stats()
+    inner = getattr(eng, "engine", None)
+    if inner is None or not hasattr(inner, "busy_seconds"):
+        return None
+    if reset:
+        inner.busy_seconds(reset=True)
+        return True
+    return {"timing": dict(inner.timing), "counters": dict(inner.counters),
+            "gpu_busy_s": inner.busy_seconds()}
+
+
 async def serve_health(svc: RuntimeService, port: int = 9001, host: str = "0.0.0.0"):
     from aiohttp import web
 
@@ -460,6 +478,19 @@ async def serve_health(svc: RuntimeService, port: int = 9001, host: str = "0.0.0
     app.router.add_get("/healthz", healthz)
     app.router.add_get("/readyz", readyz)
     app.router.add_get("/metrics", metrics)
+    if os.environ.get("OMNIA_DEBUG_ENGINE_STATS") == "1":
+        # benchmark / diagnostics only (off by default): the local engine's
+        # counters and hipEvent-measured device busy time, and their reset
+        async def engine_stats(request):
+            reset = request.method == "POST"
+            out = await asyncio.get_running_loop().run_in_executor(
+                None, _engine_stats, svc.agent, reset)
+            if out is None:
+                return web.json_response({"error": "no local engine"}, status=404)
+            return web.json_response(out if isinstance(out, dict) else {"ok": bool(out)})
+
+        app.router.add_get("/debug/engine-stats", engine_stats)
+        app.router.add_post("/debug/engine-stats", engine_stats)
     runner = web.AppRunner(app)
     await runner.setup()
     site = web.TCPSite(runner, host, port)

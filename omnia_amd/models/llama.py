@@ -291,6 +291,8 @@ class LlamaModel:
         M, K = x.shape
         if tag in ("o", "down") and not is_decode and overlap.applies(M, x.device):
             return RowPar(x, w)
+        if self._pgemm_ok(M, K, w.shape[0], is_decode):
+            return ops.pgemm(0, x, w)
         cfg = self._wcfg(M, w.shape[0], K, 0, is_decode)
         if cfg is None:
             return ops.linear(x, w)
@@ -312,9 +314,21 @@ class LlamaModel:
         ops.fused_add_rmsnorm(x, residual, w, eps)
         return x
 
+    _min_rows = int(os.environ.get("OMNIA_PGEMM_MIN_ROWS", "257"))  # this forward's threshold (mixed steps: the higher one)
+
+    def _pgemm_ok(self, M: int, K: int, N: int, is_decode: bool, tn: int = 256) -> bool:
+        """A prefill-sized projection the hand 256x256 MFMA kernel covers (the
+        unfused paths: TP shards, MoE attention, CP): K whole 128-k iterations,
+        N whole column tiles, and at least this forward's row threshold."""
+        return (self.use_pgemm and not is_decode and self.device.type == "cuda"
+                and M >= self._min_rows and K % 128 == 0 and N % tn == 0)
+
     def mlp(self, layer: dict, h: torch.Tensor, is_decode: bool = False):
         M, K = h.shape
         I2 = layer["gate_up"].shape[0]
+        if self._pgemm_ok(M, K, I2 // 2, is_decode, 128):
+            # gate_up + SwiGLU in the prefill kernel's epilogue (pgemm EPI 1)
+            return self._proj("down", ops.pgemm(1, h, layer["gate_up"]), layer["down"], False)
         cfg = self._wcfg(M, I2 // 2, K, 1, is_decode)
         if cfg is None:
             a = ops.linear_silu(h, layer["gate_up"])  # SwiGLU fused into decode GEMMs
@@ -332,6 +346,21 @@ class LlamaModel:
         T = h.shape[0]
         D = self.cfg.head_dim
         wqkv = self.w["layers"][li]["qkv"]
+        if fb.cp is None and D == 128 and (self.hq + 2 * self.hkv) % 2 == 0 and \
+                self._pgemm_ok(T, h.shape[1], wqkv.shape[0], fb.is_decode):
+            # QKV + RoPE + paged KV write in the prefill kernel's epilogue (pgemm
+            # EPI 3, no row scale: h is already normalised on this path)
+            q = ops.pgemm(3, h, wqkv, positions=fb.positions, cos_sin=self.cos_sin,
+                          k_cache=kv.k[li], v_cache=kv.v[li], slots=fb.slots, hq=self.hq,
+                          hkv=self.hkv, block_size=kv.block_size)
+            q3 = q.view(T, self.hq, D)
+            if fb.num_decode:
+                o = self._mixed_attention(li, q3, fb, kv)
+            else:
+                o = ops.prefill_attention(q3, kv.k[li], kv.v[li], fb.block_tables,
+                                          fb.q_start_loc, fb.seq_lens, self.scale, fb.tile_seq,
+                                          fb.tile_q0)
+            return self._proj("o", o.view(T, self.hq * D), self.w["layers"][li]["o"], False)
         qkv = self._proj("qkv", h, wqkv, fb.is_decode)
         if fb.cp is not None:
             cp = fb.cp
@@ -430,7 +459,7 @@ class LlamaModel:
             return False
         cfg, d = self.cfg, self.cfg.hidden_size
         return (cfg.head_dim == 128 and d % 256 == 0 and d % 128 == 0
-                and (self.hq * 128) % 256 == 0 and (self.hkv * 128) % 256 == 0
+                and (self.hq + 2 * self.hkv) % 2 == 0
                 and self.inter % 128 == 0
                 and self.fold_post_norm and not self.cfg.is_moe)
 
@@ -467,6 +496,7 @@ class LlamaModel:
         cfg = self.cfg
         if self._use_fused(fb):
             return ops.rmsnorm(self._fused_residual(fb, kv), self.w["final_norm"], cfg.rms_eps)
+        self._min_rows = self.PGEMM_MIXED_MIN_ROWS if fb.num_decode else self.PGEMM_MIN_ROWS
         residual = self.embed(fb.input_ids)
         h = ops.rmsnorm(residual, self.w["layers"][0]["in_norm"], cfg.rms_eps)
         m = None

@@ -660,6 +660,29 @@ def cosine_topk(q: torch.Tensor, m: torch.Tensor, k: int, valid: torch.Tensor | 
 
 # ------------------------------------------------------------- MoE (K14)
 MOE_LIBRARY_ROWS = 1024  # mean rows/expert above which eager calls use hipBLASLt per expert
+# mean rows per local expert from which the grouped GEMMs run on the 256x256
+# prefill tile (pgemm.hip EPI 5 / 6, 256-row expert segments); below it the
+# 64-row grouped kernels (moe.hip) waste less padding.  Both are graph-safe.
+MOE_TILE256_ROWS = int(os.environ.get("OMNIA_MOE_TILE256_ROWS", "512"))
+
+
+def _moe_grouped(x, w_gu, w_down, ids, wts, k, n_experts, e_lo, e_hi, bm):
+    """Grouped expert FFN over device-sorted assignments, no host sync: Y [T*k, d]
+    (row t*k + j = slot j of token t, routing weight applied; other experts' rows
+    unwritten).  ``bm`` 256: the 256x256 MFMA prefill tile; 64: moe.hip."""
+    kk = kernels()
+    n = ids.numel()
+    mb = kk.moe_max_blocks(n, e_hi - e_lo, bm)
+    sorted_ids = torch.empty(mb * bm, dtype=torch.int32, device=x.device)
+    blk = torch.empty(mb, dtype=torch.int32, device=x.device)
+    nblk = torch.empty(1, dtype=torch.int32, device=x.device)
+    kk.moe_align(sorted_ids, blk, nblk, ids, n_experts, e_lo, e_hi)
+    act = torch.empty(mb * bm, w_down.shape[2], dtype=x.dtype, device=x.device)
+    Y = torch.empty(n, x.shape[1], dtype=x.dtype, device=x.device)
+    gemm = kk.pgemm_moe if bm == 256 else kk.moe_gemm
+    gemm(0, act, x, w_gu, sorted_ids, blk, nblk, None, k, n, e_lo)
+    gemm(1, Y, act, w_down, sorted_ids, blk, nblk, wts.view(-1), k, n, e_lo)
+    return Y
 
 
 def moe_rows(rows: torch.Tensor, eids: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor,
@@ -716,7 +739,17 @@ def moe(x: torch.Tensor, router: torch.Tensor, w_gu: torch.Tensor, w_down: torch
     wts = torch.empty(T, k, dtype=torch.float32, device=x.device)
     kk.moe_topk(ids, wts, logits, k, renorm)
     out = torch.empty_like(x)
-    if not graph_safe and n >= MOE_LIBRARY_ROWS * (e_hi - e_lo):
+    d, inter = x.shape[1], w_down.shape[2]
+    if n >= MOE_TILE256_ROWS * (e_hi - e_lo) and d % 256 == 0 and inter % 128 == 0:
+        # prefill-sized: the 256x256 MFMA tile, grouped by 256-row expert segments
+        # (pgemm.hip EPI 5 / 6) -- hand kernels, graph-safe, no per-expert library
+        # calls and no host sync
+        Y = _moe_grouped(x, w_gu, w_down, ids, wts, k, n_experts, e_lo, e_hi, 256)
+        kk.moe_combine(out, Y, ids, k, e_lo, e_hi)
+        return out
+    if not graph_safe and n >= MOE_LIBRARY_ROWS * (e_hi - e_lo) and \
+            os.environ.get("OMNIA_MOE_LIBRARY", "0") == "1":
+        # opt-in comparison path: per-expert hipBLASLt after one host sync
         flat = ids.view(-1)
         order = torch.argsort(flat, stable=True)
         counts = torch.bincount(flat, minlength=n_experts).tolist()  # host sync (eager only)
@@ -733,14 +766,6 @@ def moe(x: torch.Tensor, router: torch.Tensor, w_gu: torch.Tensor, w_down: torch
         Y.index_copy_(0, order, ys * wts.view(-1).index_select(0, order)[:, None].to(x.dtype))
         kk.moe_combine(out, Y, ids, k, e_lo, e_hi)
         return out
-    mb = kk.moe_max_blocks(n, e_hi - e_lo)
-    sorted_ids = torch.empty(mb * 64, dtype=torch.int32, device=x.device)
-    blk = torch.empty(mb, dtype=torch.int32, device=x.device)
-    nblk = torch.empty(1, dtype=torch.int32, device=x.device)
-    kk.moe_align(sorted_ids, blk, nblk, ids, n_experts, e_lo, e_hi)
-    act = torch.empty(mb * 64, w_down.shape[2], dtype=x.dtype, device=x.device)
-    kk.moe_gemm(0, act, x, w_gu, sorted_ids, blk, nblk, None, k, n, e_lo)
-    Y = torch.empty(n, d, dtype=x.dtype, device=x.device)
-    kk.moe_gemm(1, Y, act, w_down, sorted_ids, blk, nblk, wts.view(-1), k, n, e_lo)
+    Y = _moe_grouped(x, w_gu, w_down, ids, wts, k, n_experts, e_lo, e_hi, 64)
     kk.moe_combine(out, Y, ids, k, e_lo, e_hi)
     return out

@@ -21,6 +21,9 @@ int omnia_ar_sendrecv(void* out, const void* in, void* const* regions, int* epoc
 int omnia_pgemm_set_schedule(int sched);
 int omnia_pgemm_splitk(void* parts, const void* X, const void* W, int M, int N, int K, int S,
                        int sched, hipStream_t s);
+int omnia_pgemm_moe(int mode, void* out, const void* A, const void* W, const int* sorted,
+                    const int* blk_expert, const int* n_blocks, const float* route_w, int K,
+                    int N, int topk, int n_assign, int e_lo, int max_blocks, hipStream_t s);
 int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, int M, int N,
                         int K, hipStream_t s);
 int omnia_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows, int d,
@@ -70,9 +73,9 @@ int omnia_topk(int* out_idx, float* out_val, const float* scores, int nq, int64_
                hipStream_t s);
 int omnia_moe_topk(int* ids, float* wts, const void* logits, int logits_bf16, int n_tok, int E,
                    int k, int renorm, hipStream_t s);
-int omnia_moe_max_blocks(int n_assign, int n_experts);
+int omnia_moe_max_blocks(int n_assign, int n_experts, int bm);
 int omnia_moe_align(int* sorted, int* blk_expert, int* n_blocks, const int* ids, int n, int E,
-                    int e_lo, int e_hi, int max_blocks, hipStream_t s);
+                    int e_lo, int e_hi, int max_blocks, int bm, hipStream_t s);
 int omnia_moe_gemm(int mode, void* out, const void* A, const void* W, const int* sorted,
                    const int* blk_expert, const int* n_blocks, const float* route_w, int K,
                    int N, int topk, int n_assign, int e_lo, int max_blocks, hipStream_t s);
@@ -460,21 +463,56 @@ void moe_topk(at::Tensor ids, at::Tensor wts, at::Tensor logits, int64_t k, bool
                           E, k, renorm, cur_stream()), "moe_topk");
 }
 
-int64_t moe_max_blocks(int64_t n_assign, int64_t n_experts) {
-  return omnia_moe_max_blocks(n_assign, n_experts);
+int64_t moe_max_blocks(int64_t n_assign, int64_t n_experts, int64_t bm) {
+  return omnia_moe_max_blocks(n_assign, n_experts, bm);
 }
 
+// segments aligned to bm = sorted.numel() / blk_expert.numel() rows (64: moe_gemm,
+// 256: the pgemm_moe prefill tile)
 void moe_align(at::Tensor sorted, at::Tensor blk_expert, at::Tensor n_blocks, at::Tensor ids,
                int64_t E, int64_t e_lo, int64_t e_hi) {
   CHECK_GPU(ids); CHECK_I32(ids); CHECK_I32(sorted); CHECK_I32(blk_expert); CHECK_I32(n_blocks);
   const int n = ids.numel();
   const int mb = blk_expert.numel();
-  TORCH_CHECK(mb >= omnia_moe_max_blocks(n, e_hi - e_lo), "blk_expert too small");
-  TORCH_CHECK(sorted.numel() == (int64_t)mb * 64, "sorted must hold max_blocks*64 rows");
+  TORCH_CHECK(mb > 0 && (sorted.numel() == (int64_t)mb * 64 || sorted.numel() == (int64_t)mb * 256),
+              "sorted must hold max_blocks*64 (or *256) rows");
+  const int bm = (int)(sorted.numel() / mb);
+  TORCH_CHECK(mb >= omnia_moe_max_blocks(n, e_hi - e_lo, bm), "blk_expert too small");
   TORCH_CHECK(E <= 256 && 0 <= e_lo && e_lo < e_hi && e_hi <= E, "expert range");
   CHECK_RC(omnia_moe_align(sorted.data_ptr<int>(), blk_expert.data_ptr<int>(),
                            n_blocks.data_ptr<int>(), ids.data_ptr<int>(), n, E, e_lo, e_hi, mb,
-                           cur_stream()), "moe_align");
+                           bm, cur_stream()), "moe_align");
+}
+
+// the 256x256-tile grouped MoE GEMMs (pgemm.hip EPI 5 / 6) over 256-row segments
+void pgemm_moe(int64_t mode, at::Tensor out, at::Tensor A, at::Tensor W, at::Tensor sorted,
+               at::Tensor blk_expert, at::Tensor n_blocks, c10::optional<at::Tensor> route_w,
+               int64_t topk, int64_t n_assign, int64_t e_lo) {
+  CHECK_GPU(A); CHECK_BF16(A); CHECK_BF16(W); CHECK_BF16(out);
+  CHECK_I32(sorted); CHECK_I32(blk_expert); CHECK_I32(n_blocks);
+  TORCH_CHECK(A.is_contiguous() && W.is_contiguous() && out.is_contiguous(), "contiguous");
+  TORCH_CHECK(W.dim() == 3, "W [E_local, rows, K]");
+  const int K = W.size(2);
+  const int mb = blk_expert.numel();
+  TORCH_CHECK(sorted.numel() == (int64_t)mb * 256, "sorted must hold max_blocks*256 rows");
+  TORCH_CHECK(A.size(-1) == K && K % 128 == 0, "K mismatch / K % 128");
+  int N;
+  if (mode == 0) {
+    N = W.size(1) / 2;
+    TORCH_CHECK(N % 128 == 0 && out.size(0) == (int64_t)mb * 256 && out.size(1) == N,
+                "act [max_blocks*256, I]");
+    TORCH_CHECK(A.size(0) * topk == n_assign, "x rows * topk == n_assign");
+  } else {
+    N = W.size(1);
+    TORCH_CHECK(N % 256 == 0 && out.size(0) == n_assign && out.size(1) == N, "Y [T*k, d]");
+    TORCH_CHECK(A.size(0) == (int64_t)mb * 256, "act rows");
+    TORCH_CHECK(route_w.has_value() && route_w->numel() == n_assign &&
+                route_w->scalar_type() == at::kFloat, "route weights");
+  }
+  CHECK_RC(omnia_pgemm_moe((int)mode, out.data_ptr(), A.data_ptr(), W.data_ptr(),
+                           sorted.data_ptr<int>(), blk_expert.data_ptr<int>(),
+                           n_blocks.data_ptr<int>(), opt_ptr<float>(route_w), K, N, topk,
+                           n_assign, e_lo, mb, cur_stream()), "pgemm_moe");
 }
 
 void moe_gemm(int64_t mode, at::Tensor out, at::Tensor A, at::Tensor W, at::Tensor sorted,
@@ -1028,7 +1066,9 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("cosine_scores", &cosine_scores);
   m.def("topk", &topk);
   m.def("moe_topk", &moe_topk);
-  m.def("moe_max_blocks", &moe_max_blocks);
+  m.def("moe_max_blocks", &moe_max_blocks, py::arg("n_assign"), py::arg("n_experts"),
+        py::arg("bm") = 64);
+  m.def("pgemm_moe", &pgemm_moe);
   m.def("moe_align", &moe_align);
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);

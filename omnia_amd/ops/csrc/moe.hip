@@ -76,18 +76,20 @@ __global__ __launch_bounds__(256) void moe_topk_kernel(int* __restrict__ ids,
 // ------------------------------------------------------------------ align
 // One 1024-thread workgroup.  n = T*k assignments.  sorted has max_blocks*BM
 // entries (n = padding sentinel), blk_expert max_blocks entries.
+// bm: the segment alignment = the grouped GEMM's row tile (64 here, 256 for the
+// 256x256 prefill tile of pgemm.hip EPI 5 / 6)
 __global__ __launch_bounds__(1024) void moe_align_kernel(int* __restrict__ sorted,
                                                          int* __restrict__ blk_expert,
                                                          int* __restrict__ n_blocks,
                                                          const int* __restrict__ ids, int n,
                                                          int E, int e_lo, int e_hi,
-                                                         int max_blocks) {
+                                                         int max_blocks, int bm) {
   __shared__ int cnt[256];
   __shared__ int off[257];
   __shared__ int cur[256];
   const int tid = threadIdx.x;
   for (int e = tid; e < E; e += 1024) cnt[e] = 0;
-  for (int r = tid; r < max_blocks * BM; r += 1024) sorted[r] = n;
+  for (int r = tid; r < max_blocks * bm; r += 1024) sorted[r] = n;
   for (int b = tid; b < max_blocks; b += 1024) blk_expert[b] = -1;
   __syncthreads();
   for (int i = tid; i < n; i += 1024) {
@@ -97,14 +99,14 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(int* __restrict__ sorte
   __syncthreads();
   if (tid == 0) {
     off[0] = 0;
-    for (int e = 0; e < E; ++e) off[e + 1] = off[e] + (cnt[e] + BM - 1) / BM * BM;
-    *n_blocks = off[E] / BM;
+    for (int e = 0; e < E; ++e) off[e + 1] = off[e] + (cnt[e] + bm - 1) / bm * bm;
+    *n_blocks = off[E] / bm;
   }
   __syncthreads();
   for (int e = tid; e < E; e += 1024) cur[e] = off[e];
-  for (int b = tid; b < off[E] / BM; b += 1024) {
+  for (int b = tid; b < off[E] / bm; b += 1024) {
     int e = 0;
-    while (off[e + 1] <= b * BM) ++e;
+    while (off[e + 1] <= b * bm) ++e;
     blk_expert[b] = e;
   }
   __syncthreads();
@@ -274,15 +276,16 @@ int omnia_moe_topk(int* ids, float* wts, const void* logits, int logits_bf16, in
   return (int)hipGetLastError();
 }
 
-int omnia_moe_max_blocks(int n_assign, int n_experts) {
-  return (n_assign + n_experts * (BM - 1) + BM - 1) / BM;
+int omnia_moe_max_blocks(int n_assign, int n_experts, int bm) {
+  return (n_assign + n_experts * (bm - 1) + bm - 1) / bm;
 }
 
 int omnia_moe_align(int* sorted, int* blk_expert, int* n_blocks, const int* ids, int n, int E,
-                    int e_lo, int e_hi, int max_blocks, hipStream_t s) {
+                    int e_lo, int e_hi, int max_blocks, int bm, hipStream_t s) {
   if (E > 256 || e_lo < 0 || e_hi > E || e_lo >= e_hi) return -1;
+  if (bm != 64 && bm != 256) return -2;
   moe_align_kernel<<<1, 1024, 0, s>>>(sorted, blk_expert, n_blocks, ids, n, E, e_lo, e_hi,
-                                      max_blocks);
+                                      max_blocks, bm);
   return (int)hipGetLastError();
 }
 

@@ -29,6 +29,11 @@
 //   EPI 2  residual += acc  (in place), ss_out[r][tile] = sum of squares of the
 //          new bf16 residual row slice                          (O / down)
 //   EPI 3  rs-scaled QKV -> RoPE(q) to q_out, RoPE(k) and v to the paged KV cache
+//   EPI 5  MoE grouped gate_up + SwiGLU: the 256-row tile's rows are expert-sorted
+//          assignments (moe_align at 256-row segments), A rows gathered by token,
+//          W = that segment's expert [Wg; Wu]; act written in sorted order
+//   EPI 6  MoE grouped down: A = act (sorted order), W = the segment's expert,
+//          each row scaled by its routing weight and scattered to Y[assignment]
 //   EPI 4  split-K partial: block (m-tile, n-tile, k-slice ks) writes its K-slice's
 //          fp32 sum, saturated to fp16, into slab ks of out[S][M][N]; the splitk.hip
 //          consumers reduce the slabs (decode projections at M <= 256: one m-tile,
@@ -73,6 +78,13 @@ struct PArgs {
   const int64_t* slots;  // [M] (< 0: no KV write)
   int hq, hkv, block_size;
   int splits;            // EPI 4: K-slices (slabs)
+  // EPI 5 / 6 (MoE grouped): sorted assignment ids [max_blocks * 256] (n_assign =
+  // padding), per-256-row-segment expert, live segment count, routing weights
+  const int* sorted;
+  const int* blk_expert;
+  const int* n_blocks;
+  const float* route_w;
+  int topk, n_assign, e_lo;
 };
 
 __device__ __forceinline__ float4v mfma16(short8 a, short8 b, float4v c) {
@@ -111,8 +123,19 @@ __device__ __forceinline__ int swz(int row, int ch) { return row * BK + ((ch ^ (
 template <int EPI, int NT>
 __device__ __forceinline__ void epi_out(const PArgs& p, const bf16_t* stg, int m0, int nt,
                                         int Mt, int ntn, int tid, int lane) {
-  constexpr int TN = EPI == 1 ? 128 : 256;
-  if constexpr (EPI == 0 || EPI == 1 || EPI == 4) {
+  constexpr int TN = (EPI == 1 || EPI == 5) ? 128 : 256;
+  if constexpr (EPI == 6) {
+    // scatter the tile's live rows to their assignment rows of Y [n_assign, ldo]
+    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+#pragma unroll 4
+    for (int u = tid; u < 256 * 32; u += NT) {
+      const int r = u >> 5, c = u & 31;
+      const int f = p.sorted[m0 + r];
+      if (f < p.n_assign)
+        *reinterpret_cast<short8*>(out + (int64_t)f * p.ldo + (int64_t)nt * 256 + c * 8) =
+            *reinterpret_cast<const short8*>(stg + r * SROW + c * 8);
+    }
+  } else if constexpr (EPI == 0 || EPI == 1 || EPI == 4 || EPI == 5) {
     // coalesced copy-out: TN/8 chunks per row (EPI 4: 16-bit fp16 chunks into
     // slab `ks`, whose base the caller folded into p.out)
     constexpr int CPR = TN / 8;
@@ -203,7 +226,8 @@ __device__ __forceinline__ void epi_out(const PArgs& p, const bf16_t* stg, int m
 template <int EPI, int VAR = 0>
 __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
-  constexpr int TN = EPI == 1 ? 128 : 256;  // output columns per block tile
+  constexpr int TN = (EPI == 1 || EPI == 5) ? 128 : 256;  // output columns per block tile
+  constexpr bool MOE = EPI == 5 || EPI == 6;
   // EPI 4: the K-slices are extra "m-tiles" of the L2 grouping below (blocks of
   // one slice share its x slice, blocks of one column tile its W rows)
   const int S = EPI == 4 ? p.splits : 1;
@@ -224,6 +248,14 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   const int m0 = mt << 8, Mt = p.M - m0 < 256 ? p.M - m0 : 256;
   const int K = p.K, nk = K / S / BK;
   const int64_t kbase = (int64_t)ks * (K / S);
+  // MoE: the grid is sized for the worst-case segment count (graph-safe, no host
+  // sync); tiles past the live count leave, the whole block at once
+  if constexpr (MOE) {
+    if (mt >= *p.n_blocks) return;
+  }
+  const bf16_t* Wb = p.W;
+  if constexpr (MOE)
+    Wb += (int64_t)(p.blk_expert[mt] - p.e_lo) * (EPI == 5 ? 2 * p.N : p.N) * K;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -241,10 +273,15 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
     for (int h = 0; h < 2; ++h) {
       int ar = m0 + h * 128 + row;
       ar = ar < p.M ? ar : p.M - 1;  // rows past the chunk: clamped copies, never stored
+      if constexpr (EPI == 5) {  // gather: the assignment's token row (padding: row 0)
+        const int f = p.sorted[m0 + h * 128 + row];
+        ar = f < p.n_assign ? f / p.topk : 0;
+      }
       src[h][i] = p.X + (int64_t)ar * K + kbase + gch * 8;
-      const int64_t br = EPI == 1 ? (int64_t)(h ? p.N : 0) + (int64_t)nt * 128 + row
-                                  : (int64_t)nt * 256 + h * 128 + row;
-      src[2 + h][i] = p.W + br * K + kbase + gch * 8;
+      const int64_t br = (EPI == 1 || EPI == 5)
+                             ? (int64_t)(h ? p.N : 0) + (int64_t)nt * 128 + row
+                             : (int64_t)nt * 256 + h * 128 + row;
+      src[2 + h][i] = Wb + br * K + kbase + gch * 8;
     }
   }
   auto issue = [&](int buf, auto HC, int kt) {
@@ -365,15 +402,20 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   // ---------------------------------------------------------------- epilogue
   // lane rows: a*128 + wr*64 + m*16 + fq*4 + j ; cols: b*128 + wc*32 + n*16 + fr
   float* rs_lds = reinterpret_cast<float*>(lds + RS_OFF);
-  const bool scaled = EPI != 2 && p.ss_in != nullptr;
+  const bool scaled = EPI == 6 || (EPI != 2 && p.ss_in != nullptr);
   if (scaled) {
     if (tid < 256) {
-      int r = m0 + tid;
-      r = r < p.M ? r : p.M - 1;
-      const float* s = p.ss_in + (int64_t)r * p.ss_in_n;
-      float t = 0.f;
-      for (int i = 0; i < p.ss_in_n; ++i) t += s[i];
-      rs_lds[tid] = __builtin_amdgcn_rsqf(t * p.inv_d + p.eps);
+      if constexpr (EPI == 6) {  // row scale = the assignment's routing weight
+        const int f = p.sorted[m0 + tid];
+        rs_lds[tid] = f < p.n_assign ? p.route_w[f] : 0.f;
+      } else {
+        int r = m0 + tid;
+        r = r < p.M ? r : p.M - 1;
+        const float* s = p.ss_in + (int64_t)r * p.ss_in_n;
+        float t = 0.f;
+        for (int i = 0; i < p.ss_in_n; ++i) t += s[i];
+        rs_lds[tid] = __builtin_amdgcn_rsqf(t * p.inv_d + p.eps);
+      }
     }
     __syncthreads();
   }
@@ -402,7 +444,7 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
     *d1 = x1;
   };
 
-  if constexpr (EPI == 1) {
+  if constexpr (EPI == 1 || EPI == 5) {
     // gate (b = 0) and up (b = 1) of feature nt*128 + wc*32 + n*16 + fr in one lane
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -444,6 +486,8 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
     PArgs q = p;
     q.out = reinterpret_cast<bf16_t*>(p.out) + (int64_t)ks * p.M * p.N;
     epi_out<4, 512>(q, stg, m0, nt, Mt, ntn, tid, lane);
+  } else if constexpr (EPI == 5) {
+    epi_out<1, 512>(p, stg, m0, nt, Mt, ntn, tid, lane);
   } else {
     epi_out<EPI, 512>(p, stg, m0, nt, Mt, ntn, tid, lane);
   }
@@ -708,6 +752,9 @@ int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, in
                         int K, hipStream_t s);
 int omnia_pgemm_splitk(void* parts, const void* X, const void* W, int M, int N, int K, int S,
                        int sched, hipStream_t s);
+int omnia_pgemm_moe(int mode, void* out, const void* A, const void* W, const int* sorted,
+                    const int* blk_expert, const int* n_blocks, const float* route_w, int K,
+                    int N, int topk, int n_assign, int e_lo, int max_blocks, hipStream_t s);
 
 static int g_pgemm_sched = 0;  // 0: 8-wave ping-pong, 1: 4-wave (one wave per SIMD)
 
@@ -734,7 +781,10 @@ int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, 
   if (epi == 2 && ss_out == nullptr) return -8;
   if (epi == 3) {
     if (!positions || !cos_sin || !k_cache || !v_cache || !slots || block_size < 1) return -9;
-    if (hq < 1 || hkv < 1 || (hq * 128) % 256 || (hkv * 128) % 256) return -10;
+    // the epilogue works per head (a 256-column tile = heads 2nt, 2nt+1 of
+    // [q | k | v]), so a tile may straddle the q / k / v boundaries: a TP shard's
+    // single KV head (hkv * 128 = 128, Llama-3-70B at TP = 8) is fine
+    if (hq < 1 || hkv < 1 || (hq + 2 * hkv) % 2) return -10;
     if (N != (hq + 2 * hkv) * 128) return -11;
     if ((reinterpret_cast<uintptr_t>(k_cache) | reinterpret_cast<uintptr_t>(v_cache)) & 15)
       return -12;
@@ -743,7 +793,7 @@ int omnia_pgemm(int epi, void* out, const void* X, const void* W, int M, int N, 
   if (blocks > (1 << 30)) return -13;
   PArgs a{out, (const bf16_t*)X, (const bf16_t*)W, M, N, K, ldo, ss_in, ss_in_n, inv_d, eps,
           ss_out, positions, cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache, slots, hq, hkv,
-          block_size, 1};
+          block_size, 1, nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
   const dim3 grid((unsigned)blocks);
   if (g_pgemm_sched == 1) {
     switch (epi) {
@@ -768,7 +818,8 @@ int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, in
                         int K, hipStream_t s) {
   if (M < 1 || K <= 0 || K % (2 * BK) || N <= 0 || N % 256) return -1;
   PArgs a{out, (const bf16_t*)X, (const bf16_t*)W, M, N, K, N, nullptr, 0, 0.f, 0.f, nullptr,
-          nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 1};
+          nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 1, nullptr, nullptr, nullptr,
+          nullptr, 0, 0, 0};
   const dim3 grid((unsigned)(((M + 255) / 256) * (N / 256))), block(512);
   switch (variant) {
     case 0: pgemm_kernel<0, 0><<<grid, block, 0, s>>>(a); break;
@@ -798,11 +849,39 @@ int omnia_pgemm_splitk(void* parts, const void* X, const void* W, int M, int N, 
   const int64_t blocks = (int64_t)((M + 255) / 256) * (N / 256) * S;
   if (blocks > (1 << 30)) return -13;
   PArgs a{parts, (const bf16_t*)X, (const bf16_t*)W, M, N, K, N, nullptr, 0, 0.f, 0.f, nullptr,
-          nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, S};
+          nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, S, nullptr, nullptr, nullptr,
+          nullptr, 0, 0, 0};
   if (sched == 1)
     pgemm4_kernel<4><<<dim3((unsigned)blocks), 256, 0, s>>>(a);
   else
     pgemm_kernel<4><<<dim3((unsigned)blocks), 512, 0, s>>>(a);
+  return (int)hipGetLastError();
+}
+
+// MoE grouped GEMMs on the 256x256 tile (segments from omnia_moe_align with
+// bm = 256).  mode 0: act [max_blocks*256, I] = SwiGLU(x[token] . W_gu[e]^T),
+// x [T, d], W_gu [E_loc, 2I, d];  mode 1: Y[assignment] = w_route * act . W_dn[e]^T,
+// act [max_blocks*256, I], W_dn [E_loc, d, I], Y [n_assign, d].
+int omnia_pgemm_moe(int mode, void* out, const void* A, const void* W, const int* sorted,
+                    const int* blk_expert, const int* n_blocks, const float* route_w, int K,
+                    int N, int topk, int n_assign, int e_lo, int max_blocks, hipStream_t s) {
+  if (mode < 0 || mode > 1 || max_blocks < 0 || topk < 1) return -1;
+  if (K <= 0 || K % (2 * BK)) return -3;
+  if (N <= 0 || N % (mode == 0 ? 128 : 256)) return -4;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W) |
+       reinterpret_cast<uintptr_t>(out)) & 15)
+    return -5;
+  if (!sorted || !blk_expert || !n_blocks || (mode == 1 && !route_w)) return -9;
+  if (max_blocks == 0) return 0;
+  const int64_t blocks = (int64_t)max_blocks * (N / (mode == 0 ? 128 : 256));
+  if (blocks > (1 << 30)) return -13;
+  PArgs a{out, (const bf16_t*)A, (const bf16_t*)W, max_blocks * 256, N, K, N, nullptr, 0, 0.f,
+          0.f, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 1, sorted,
+          blk_expert, n_blocks, route_w, topk, n_assign, e_lo};
+  if (mode == 0)
+    pgemm_kernel<5><<<dim3((unsigned)blocks), 512, 0, s>>>(a);
+  else
+    pgemm_kernel<6><<<dim3((unsigned)blocks), 512, 0, s>>>(a);
   return (int)hipGetLastError();
 }
 

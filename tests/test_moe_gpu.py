@@ -70,14 +70,68 @@ def test_moe_grouped_path_matches_reference(T, d, I, E, k, e_lo, e_n):
     torch.testing.assert_close(out.float().cpu(), exp, atol=1e-2, rtol=1e-2)
 
 
-def test_moe_library_path_matches_grouped():
+def test_moe_library_path_matches_grouped(monkeypatch):
     g = torch.Generator().manual_seed(5)
     E, d, I, k, T = 4, 256, 512, 2, 2048
     router, wgu, wd = _weights(E, d, I, g)
     x = torch.randn(T, d, generator=g).to(torch.bfloat16).cuda()
+    monkeypatch.setattr(ops, "MOE_TILE256_ROWS", 1 << 30)  # the 64-row grouped kernels
     a = ops.moe(x, router, wgu, wd, k, E, 0, graph_safe=True)
+    monkeypatch.setenv("OMNIA_MOE_LIBRARY", "1")
     b = ops.moe(x, router, wgu, wd, k, E, 0, graph_safe=False)  # hipBLASLt per expert
     torch.testing.assert_close(a.float(), b.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("T,d,I,E,k,e_lo,e_n", [
+    (2048, 512, 512, 8, 2, 0, 8),    # prefill-sized: 256x256-tile grouped GEMMs
+    (2500, 256, 384, 8, 2, 0, 8),    # ragged expert segments, I not a multiple of 256
+    (4096, 512, 256, 8, 2, 4, 4),    # expert-parallel shard: experts 4..7 only
+])
+def test_moe_tile256_prefill_matches_reference(T, d, I, E, k, e_lo, e_n):
+    """Large batches run the 256-row-segment grouped GEMMs (pgemm.hip EPI 5 / 6)
+    without a host sync: against the fp32 oracle pinned to the kernel's routing,
+    and against the 64-row grouped kernels (a different tiling of the same sums)."""
+    g = torch.Generator().manual_seed(T + I)
+    router, wgu, wd = _weights(E, d, I, g)
+    x = (torch.randn(T, d, generator=g)).to(torch.bfloat16).cuda()
+    wgu_l, wd_l = wgu[e_lo:e_lo + e_n].contiguous(), wd[e_lo:e_lo + e_n].contiguous()
+    assert T * k >= ops.MOE_TILE256_ROWS * e_n  # the 256-tile path is the one under test
+    out = ops.moe(x, router, wgu_l, wd_l, k, E, e_lo, graph_safe=True)
+    logits = torch.nn.functional.linear(x, router)
+    rid, rw = ref.moe_route(logits.float().cpu(), k)
+    exp = ref.moe(x.cpu(), router.cpu(), wgu_l.cpu(), wd_l.cpu(), k, e_lo, ids=rid, wts=rw,
+                  act_dtype=torch.bfloat16)
+    torch.testing.assert_close(out.float().cpu(), exp, atol=1e-2, rtol=1e-2)
+    saved = ops.MOE_TILE256_ROWS
+    try:
+        ops.MOE_TILE256_ROWS = 1 << 30
+        small = ops.moe(x, router, wgu_l, wd_l, k, E, e_lo, graph_safe=True)
+    finally:
+        ops.MOE_TILE256_ROWS = saved
+    torch.testing.assert_close(out.float(), small.float(), atol=1e-2, rtol=1e-2)
+    # negative control: dropping the routing weights must not pass
+    assert not torch.allclose(out.float().cpu(), exp * 2, atol=1e-2, rtol=1e-2)
+
+
+def test_moe_tile256_is_graph_capturable():
+    """No host sync: the prefill-sized grouped path captures into a hipGraph and
+    replays to the eager result."""
+    g = torch.Generator().manual_seed(11)
+    E, d, I, k, T = 8, 512, 512, 2, 2048
+    router, wgu, wd = _weights(E, d, I, g)
+    x = torch.randn(T, d, generator=g).to(torch.bfloat16).cuda()
+    want = ops.moe(x, router, wgu, wd, k, E, 0, graph_safe=True)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.moe(x, router, wgu, wd, k, E, 0, graph_safe=True)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        got = ops.moe(x, router, wgu, wd, k, E, 0, graph_safe=True)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
 
 
 def test_mixtral_engine_graphs_match_eager():

@@ -679,11 +679,10 @@ class ModelRunner:
 
     def _decode_body(self, nrows: int, ncols: int):
         d = self.dec.d
-        src = d["src"][:nrows]
-        # tokens sampled by earlier steps stay on the GPU (async scheduling)
-        ids = torch.where(src >= 0, self.tok_slots.index_select(0, src.clamp(min=0)),
-                          d["ids"][:nrows])
-        fb = self._decode_fb(nrows, ncols, ids)
+        fb = self._decode_fb(nrows, ncols)
+        # tokens sampled by earlier steps stay on the GPU (async scheduling): the
+        # embedding kernel reads them from their slots (no framework op in the graph)
+        fb.ids_src, fb.tok_slots = d["src"][:nrows], self.tok_slots
         if self.model.tp > 1:
             # vocab-parallel LM head + distributed sampler: no full-vocab gather
             from ..parallel import state as pstate
@@ -707,10 +706,10 @@ class ModelRunner:
         logits = self.model.forward(fb, self.kv)
         if self._tap is not None:
             self._tap[:nrows].copy_(logits)
+        # the sampler also writes each token into its sequence's device slot
         ops.sample(logits, d["temp"][:nrows], d["top_k"][:nrows], d["top_p"][:nrows],
                    seeds=d["seeds"][:nrows], steps=d["steps"][:nrows],
-                   out=self.out_tok[:nrows])
-        self.tok_slots.index_copy_(0, d["dst"][:nrows], self.out_tok[:nrows])
+                   out=self.out_tok[:nrows], tok_slots=self.tok_slots, dst=d["dst"][:nrows])
 
     def _capture(self, nrows: int, ncols: int):
         t0 = time.perf_counter()
@@ -738,12 +737,20 @@ class ModelRunner:
 
         gc_was = gc.isenabled()
         gc.disable()
+        # framework compute ops / blocks outside the graph pool captured here would
+        # replay stale state (engine/capture_guard.py)
+        from .capture_guard import CaptureGuard
+
+        guard = CaptureGuard(self.device, f"decode graph rows={nrows} cols={ncols}")
         try:
-            with torch.cuda.graph(g, pool=self.graph_pool):
-                self._decode_body(nrows, ncols)
+            with guard:
+                with torch.cuda.graph(g, pool=self.graph_pool):
+                    self._decode_body(nrows, ncols)
         finally:
             if gc_was:
                 gc.enable()
+        self.stats["capture_guard_violations"] = \
+            self.stats.get("capture_guard_violations", 0) + len(guard.violations())
         torch.cuda.synchronize()
         self.out_tok.copy_(saved)
         self.tok_slots.copy_(saved_slots)

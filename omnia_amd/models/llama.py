@@ -49,6 +49,10 @@ class ForwardBatch:
     num_decode: int = 0
     dec_block_tables: torch.Tensor | None = None  # int32 [Bd, max_blocks]
     dec_seq_lens: torch.Tensor | None = None  # int32 [Bd]
+    # decode rows whose input token is still on the device: tok_slots[ids_src[r]]
+    # where ids_src[r] >= 0 (resolved inside the embedding kernel)
+    ids_src: torch.Tensor | None = None
+    tok_slots: torch.Tensor | None = None
     # context-parallel prefill (parallel/context_parallel.py CPPrefill): this
     # rank's zig-zag shard of one long prompt; K/V go to the CP scratch pages and
     # attention is the ring over the CP group
@@ -433,8 +437,9 @@ class LlamaModel:
             self._ws[key] = ws
         return ws
 
-    def embed(self, ids: torch.Tensor) -> torch.Tensor:
-        h = ops.embedding(ids, self.w["embed"], self.vocab_start)
+    def embed(self, ids: torch.Tensor, src: torch.Tensor | None = None,
+              tok_slots: torch.Tensor | None = None) -> torch.Tensor:
+        h = ops.embedding(ids, self.w["embed"], self.vocab_start, src=src, tok_slots=tok_slots)
         return pstate.tp_all_reduce(h) if self.tp > 1 else h
 
     # ------------------------------------------------ fused prefill (pgemm.hip)
@@ -497,7 +502,7 @@ class LlamaModel:
         if self._use_fused(fb):
             return ops.rmsnorm(self._fused_residual(fb, kv), self.w["final_norm"], cfg.rms_eps)
         self._min_rows = self.PGEMM_MIXED_MIN_ROWS if fb.num_decode else self.PGEMM_MIN_ROWS
-        residual = self.embed(fb.input_ids)
+        residual = self.embed(fb.input_ids, fb.ids_src, fb.tok_slots)
         h = ops.rmsnorm(residual, self.w["layers"][0]["in_norm"], cfg.rms_eps)
         m = None
         for li, layer in enumerate(self.w["layers"]):

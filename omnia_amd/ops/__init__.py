@@ -488,11 +488,17 @@ def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None):
 
 
 def embedding(ids: torch.Tensor, w: torch.Tensor, vocab_start: int = 0,
-              out: torch.Tensor | None = None):
+              out: torch.Tensor | None = None, src: torch.Tensor | None = None,
+              tok_slots: torch.Tensor | None = None):
+    """Token embedding gather.  ``src`` / ``tok_slots`` (decode): row t's token
+    is ``tok_slots[src[t]]`` where ``src[t] >= 0`` (sampled on the device by an
+    earlier step), else ``ids[t]`` -- resolved inside the kernel."""
     if ids.is_cuda:
         out = w.new_empty(ids.numel(), w.shape[1]) if out is None else out
-        kernels().embedding(out, ids, w, vocab_start)
+        kernels().embedding(out, ids, w, vocab_start, src, tok_slots)
         return out
+    if src is not None:
+        ids = torch.where(src >= 0, tok_slots.index_select(0, src.clamp(min=0).long()), ids)
     local = (ids >= vocab_start) & (ids < vocab_start + w.shape[0])
     idx = torch.where(local, ids - vocab_start, torch.zeros_like(ids)).long()
     r = w[idx] * local[:, None].to(w.dtype)
@@ -581,13 +587,16 @@ def prefill_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, 
 
 
 def sample(logits, temperature, top_k=None, top_p=None, seeds=None, steps=None, counts=None,
-           freq_pen=None, pres_pen=None, rep_pen=None, out=None, out_logprob=None):
-    """Fused GPU sampler; returns int32 [B] token ids."""
+           freq_pen=None, pres_pen=None, rep_pen=None, out=None, out_logprob=None,
+           tok_slots=None, dst=None):
+    """Fused GPU sampler; returns int32 [B] token ids.  With ``tok_slots`` /
+    ``dst`` the kernel also writes row r's token to ``tok_slots[dst[r]]`` (the
+    sequence's device token slot: no scatter op after it in a decode graph)."""
     if logits.is_cuda:
         B = logits.shape[0]
         out = torch.empty(B, dtype=torch.int32, device=logits.device) if out is None else out
         kernels().sample(out, out_logprob, logits, temperature, top_k, top_p, seeds, steps,
-                         counts, freq_pen, pres_pen, rep_pen)
+                         counts, freq_pen, pres_pen, rep_pen, tok_slots, dst)
         return out
     x = ref.apply_penalties(logits, counts, freq_pen, pres_pen, rep_pen)
     g = None
@@ -596,6 +605,8 @@ def sample(logits, temperature, top_k=None, top_p=None, seeds=None, steps=None, 
     r = ref.sample(x, temperature, top_k, top_p, generator=g)
     if counts is not None:
         counts[torch.arange(r.numel()), r.long()] += 1
+    if tok_slots is not None:
+        tok_slots.index_copy_(0, dst, r.to(tok_slots.dtype))
     if out is not None:
         out.copy_(r)
         return out

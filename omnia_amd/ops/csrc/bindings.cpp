@@ -34,7 +34,7 @@ int omnia_rope_kv(void* q, void* k, const void* v, const int* positions, const f
                   hipStream_t s);
 int omnia_silu_mul(void* out, const void* x, int64_t T, int inter, hipStream_t s);
 int omnia_embedding(void* out, const int* ids, const void* w, int T, int d, int vocab_start,
-                    int vocab_end, hipStream_t s);
+                    int vocab_end, const int64_t* src, const int* tok_slots, hipStream_t s);
 int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void* q,
                            const void* k_cache, const void* v_cache, const int* block_tables,
                            int bt_stride, const int* seq_lens, int B, int hq, int hkv,
@@ -52,7 +52,7 @@ int omnia_sample(int* out_tok, float* out_logprob, const void* logits, int logit
                  int rows, int64_t row_stride, int vocab, const float* temperature,
                  const int* top_k, const float* top_p, const uint64_t* seeds,
                  const int64_t* steps, int* counts, const float* freq_pen, const float* pres_pen,
-                 const float* rep_pen, hipStream_t s);
+                 const float* rep_pen, int* tok_slots, const int64_t* dst, hipStream_t s);
 int omnia_tp_gumbel(float* pack, int64_t ld, int col, const void* logits, int rows,
                     int64_t row_stride, int vocab, int vocab_start, const float* temperature,
                     const int* top_k, const float* top_p, const int64_t* seeds,
@@ -192,12 +192,24 @@ void silu_mul(at::Tensor out, at::Tensor x) {
                           cur_stream()), "silu_mul");
 }
 
-void embedding(at::Tensor out, at::Tensor ids, at::Tensor w, int64_t vocab_start) {
+// src / tok_slots (optional, decode): row t's token is tok_slots[src[t]] when
+// src[t] >= 0 (sampled on the device by an earlier step), else ids[t]
+void embedding(at::Tensor out, at::Tensor ids, at::Tensor w, int64_t vocab_start,
+               c10::optional<at::Tensor> src, c10::optional<at::Tensor> tok_slots) {
   CHECK_GPU(ids); CHECK_I32(ids); CHECK_BF16(w); CHECK_BF16(out);
   TORCH_CHECK(w.is_contiguous() && out.is_contiguous(), "contiguous");
   TORCH_CHECK(out.size(0) == ids.numel() && out.size(1) == w.size(1), "shape mismatch");
+  const bool has_src = src.has_value() && src->defined();
+  if (has_src) {
+    CHECK_I32(*tok_slots);
+    TORCH_CHECK(src->scalar_type() == at::kLong && src->numel() == ids.numel() &&
+                src->is_contiguous() && tok_slots->is_contiguous(),
+                "src [T] int64, tok_slots int32");
+  }
   CHECK_RC(omnia_embedding(out.data_ptr(), ids.data_ptr<int>(), w.data_ptr(), ids.numel(),
-                           w.size(1), vocab_start, vocab_start + w.size(0), cur_stream()),
+                           w.size(1), vocab_start, vocab_start + w.size(0),
+                           has_src ? src->data_ptr<int64_t>() : nullptr,
+                           has_src ? tok_slots->data_ptr<int>() : nullptr, cur_stream()),
            "embedding");
 }
 
@@ -270,7 +282,8 @@ void sample(at::Tensor out_tok, c10::optional<at::Tensor> out_logprob, at::Tenso
             c10::optional<at::Tensor> top_p, c10::optional<at::Tensor> seeds,
             c10::optional<at::Tensor> steps, c10::optional<at::Tensor> counts,
             c10::optional<at::Tensor> freq_pen, c10::optional<at::Tensor> pres_pen,
-            c10::optional<at::Tensor> rep_pen) {
+            c10::optional<at::Tensor> rep_pen, c10::optional<at::Tensor> tok_slots,
+            c10::optional<at::Tensor> dst) {
   CHECK_GPU(logits); CHECK_I32(out_tok);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V]");
   TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat,
@@ -280,12 +293,19 @@ void sample(at::Tensor out_tok, c10::optional<at::Tensor> out_logprob, at::Tenso
   if (counts.has_value() && counts->defined())
     TORCH_CHECK(counts->scalar_type() == at::kInt && counts->size(0) >= rows &&
                 counts->size(1) == vocab && counts->is_contiguous(), "counts int32 [B, V]");
+  if (tok_slots.has_value() && tok_slots->defined()) {
+    CHECK_I32(*tok_slots);
+    TORCH_CHECK(dst.has_value() && dst->defined() && dst->scalar_type() == at::kLong &&
+                dst->numel() >= rows && dst->is_contiguous() && tok_slots->is_contiguous(),
+                "tok_slots int32 + dst int64 [B]");
+  }
   CHECK_RC(omnia_sample(out_tok.data_ptr<int>(), opt_ptr<float>(out_logprob), logits.data_ptr(),
                         logits.scalar_type() == at::kBFloat16, rows, logits.stride(0), vocab,
                         temperature.data_ptr<float>(), opt_ptr<int>(top_k), opt_ptr<float>(top_p),
                         opt_ptr<uint64_t>(seeds), opt_ptr<int64_t>(steps), opt_ptr<int>(counts),
                         opt_ptr<float>(freq_pen), opt_ptr<float>(pres_pen),
-                        opt_ptr<float>(rep_pen), cur_stream()), "sample");
+                        opt_ptr<float>(rep_pen), opt_ptr<int>(tok_slots), opt_ptr<int64_t>(dst),
+                        cur_stream()), "sample");
 }
 
 // K13: grammar mask -> -inf logits (mask int32 [rows, ceil(V/32)], bit v = allowed)
@@ -1054,14 +1074,18 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
   m.def("rope_kv", &rope_kv);
   m.def("silu_mul", &silu_mul);
-  m.def("embedding", &embedding);
+  m.def("embedding", &embedding, py::arg("out"), py::arg("ids"), py::arg("w"),
+        py::arg("vocab_start"), py::arg("src") = py::none(), py::arg("tok_slots") = py::none());
   m.def("decode_attention", &decode_attention);
   m.def("prefill_attention", &prefill_attention, py::arg("out"), py::arg("q"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("q_start_loc"),
         py::arg("seq_lens"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("scale"),
         py::arg("hp") = 0, py::arg("q_tile") = 64, py::arg("lse") = py::none(),
         py::arg("kv_lens") = py::none());
-  m.def("sample", &sample);
+  m.def("sample", &sample, py::arg("out_tok"), py::arg("out_logprob"), py::arg("logits"),
+        py::arg("temperature"), py::arg("top_k"), py::arg("top_p"), py::arg("seeds"),
+        py::arg("steps"), py::arg("counts"), py::arg("freq_pen"), py::arg("pres_pen"),
+        py::arg("rep_pen"), py::arg("tok_slots") = py::none(), py::arg("dst") = py::none());
   m.def("mean_pool_l2", &mean_pool_l2);
   m.def("cosine_scores", &cosine_scores);
   m.def("topk", &topk);

@@ -143,16 +143,23 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out,
 }
 
 // --------------------------------------------------------------- embedding
+// src (optional): decode rows whose input token is still on the device -- the
+// token sampled by an earlier step sits in tok_slots[src[t]] when src[t] >= 0
+// (async scheduling), else ids[t] holds it; resolving it here keeps the
+// captured decode graph free of gather / select framework ops
 __global__ __launch_bounds__(256) void embedding_kernel(bf16_t* __restrict__ out,
                                                         const int* __restrict__ ids,
                                                         const bf16_t* __restrict__ w, int d,
-                                                        int vocab_start, int vocab_end) {
+                                                        int vocab_start, int vocab_end,
+                                                        const int64_t* __restrict__ src,
+                                                        const int* __restrict__ tok_slots) {
   const int t = blockIdx.x;
-  const int id = ids[t];
+  const int64_t sl = src ? src[t] : -1;
+  const int id = sl >= 0 ? tok_slots[sl] : ids[t];
   const bool local = id >= vocab_start && id < vocab_end;
-  const bf16_t* src = w + (int64_t)(local ? id - vocab_start : 0) * d;
+  const bf16_t* wr = w + (int64_t)(local ? id - vocab_start : 0) * d;
   for (int c = threadIdx.x * 8; c < d; c += blockDim.x * 8) {
-    short8 v = local ? *reinterpret_cast<const short8*>(src + c) : short8{0, 0, 0, 0, 0, 0, 0, 0};
+    short8 v = local ? *reinterpret_cast<const short8*>(wr + c) : short8{0, 0, 0, 0, 0, 0, 0, 0};
     *reinterpret_cast<short8*>(out + (int64_t)t * d + c) = v;
   }
 }
@@ -206,11 +213,12 @@ int omnia_silu_mul(void* out, const void* x, int64_t T, int inter, hipStream_t s
 }
 
 int omnia_embedding(void* out, const int* ids, const void* w, int T, int d, int vocab_start,
-                    int vocab_end, hipStream_t s) {
+                    int vocab_end, const int64_t* src, const int* tok_slots, hipStream_t s) {
   if (d % 8) return -1;
+  if (src && !tok_slots) return -2;
   if (T == 0) return 0;
   embedding_kernel<<<T, 256, 0, s>>>((bf16_t*)out, ids, (const bf16_t*)w, d, vocab_start,
-                                     vocab_end);
+                                     vocab_end, src, tok_slots);
   return (int)hipGetLastError();
 }
 

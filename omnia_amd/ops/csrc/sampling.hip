@@ -56,7 +56,8 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
     const int* __restrict__ top_k, const float* __restrict__ top_p,
     const uint64_t* __restrict__ seeds, const int64_t* __restrict__ steps,
     int* __restrict__ counts, const float* __restrict__ freq_pen,
-    const float* __restrict__ pres_pen, const float* __restrict__ rep_pen) {
+    const float* __restrict__ pres_pen, const float* __restrict__ rep_pen,
+    int* __restrict__ tok_slots, const int64_t* __restrict__ dst) {
   __shared__ float red_f[kThreads / 64];
   __shared__ int red_i[kThreads / 64];
   __shared__ float red_z[kThreads / 64];
@@ -128,6 +129,7 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
   if (greedy) {
     if (tid == 0) {
       out_tok[row] = argm;
+      if (tok_slots) tok_slots[dst[row]] = argm;  // the sequence's device token slot
       if (out_logprob) out_logprob[row] = -__logf(Z);
       if (c.counts) counts[(int64_t)row * vocab + argm] += 1;
     }
@@ -236,6 +238,7 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
         bb = red_f[i]; bi = red_i[i]; bx = red_x[i];
       }
     out_tok[row] = bi;
+    if (tok_slots) tok_slots[dst[row]] = bi;
     if (out_logprob) out_logprob[row] = bx - M - __logf(Z);
     if (c.counts) counts[(int64_t)row * vocab + bi] += 1;
   }
@@ -248,17 +251,18 @@ extern "C" int omnia_sample(int* out_tok, float* out_logprob, const void* logits
                             const float* temperature, const int* top_k, const float* top_p,
                             const uint64_t* seeds, const int64_t* steps, int* counts,
                             const float* freq_pen, const float* pres_pen, const float* rep_pen,
-                            hipStream_t s) {
+                            int* tok_slots, const int64_t* dst, hipStream_t s) {
   if (rows == 0) return 0;
+  if (tok_slots && !dst) return -2;
   if (logits_is_bf16)
     sample_kernel<uint16_t><<<rows, kThreads, 0, s>>>(
         out_tok, out_logprob, (const uint16_t*)logits, row_stride, vocab, temperature, top_k,
-        top_p, seeds, steps, counts, freq_pen, pres_pen, rep_pen);
+        top_p, seeds, steps, counts, freq_pen, pres_pen, rep_pen, tok_slots, dst);
   else
     sample_kernel<float><<<rows, kThreads, 0, s>>>(out_tok, out_logprob, (const float*)logits,
                                                    row_stride, vocab, temperature, top_k, top_p,
                                                    seeds, steps, counts, freq_pen, pres_pen,
-                                                   rep_pen);
+                                                   rep_pen, tok_slots, dst);
   return (int)hipGetLastError();
 }
 

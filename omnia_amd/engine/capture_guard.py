@@ -21,6 +21,7 @@ became active during the capture in segments whose pool is not a graph pool.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 
@@ -40,6 +41,10 @@ ALLOWED = {
     "aten::split_with_sizes", "aten::view_as", "aten::contiguous", "aten::resize_",
     "aten::set_", "aten::_reshape_alias", "aten::clone",
 }
+# library GEMMs (hipBLASLt): pointer-stable under capture (PyTorch sizes their
+# workspace per stream up front); allowed, but counted separately so a decode
+# step that should be all hand kernels shows them
+LIBRARY = {"aten::mm", "aten::addmm", "aten::bmm", "aten::linear", "aten::matmul"}
 
 
 class CaptureGuardError(RuntimeError):
@@ -47,14 +52,23 @@ class CaptureGuardError(RuntimeError):
 
 
 class _OpRecorder(TorchDispatchMode):
-    def __init__(self):
+    def __init__(self, trace: bool = False):
         super().__init__()
         self.ops: dict[str, int] = {}
+        self.library: dict[str, int] = {}
+        self.where: dict[str, str] = {}  # first call site per op (OMNIA_CAPTURE_GUARD_TRACE=1)
+        self.trace = trace
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         name = func._schema.name
-        if name not in ALLOWED:
+        if name in LIBRARY:
+            self.library[name] = self.library.get(name, 0) + 1
+        elif name not in ALLOWED:
             self.ops[name] = self.ops.get(name, 0) + 1
+            if self.trace and name not in self.where:
+                import traceback
+
+                self.where[name] = "".join(traceback.format_stack(limit=12)[:-1])
         return func(*args, **(kwargs or {}))
 
 
@@ -84,6 +98,7 @@ class CaptureGuard:
         self.what = what
         self.mode = (mode or os.environ.get("OMNIA_CAPTURE_GUARD", "warn")).lower()
         self.ops: dict[str, int] = {}
+        self.library: dict[str, int] = {}
         self.leaked: list = []
         self._rec = None
         self._before = None
@@ -93,25 +108,63 @@ class CaptureGuard:
         return self.mode != "off"
 
     def __enter__(self):
-        if not self.enabled:
-            return self
-        if self.device.type == "cuda":
-            self._before = _active_default_blocks(self.device)
-        self._rec = _OpRecorder()
-        self._rec.__enter__()
+        self._mem_enter()
+        self._ops_enter()
         return self
 
     def __exit__(self, et, ev, tb):
-        if not self.enabled:
-            return False
-        self._rec.__exit__(et, ev, tb)
-        if et is not None:
-            return False
-        self.ops = dict(self._rec.ops)
-        if self._before is not None:
-            self.leaked = sorted(_active_default_blocks(self.device) - self._before)
-        self.check()
+        self._ops_exit(et, ev, tb)
+        self._mem_exit(et)
+        if et is None and self.enabled:
+            self.check()
         return False
+
+    # the two halves separately: the op recorder goes INSIDE the capture (so
+    # PyTorch's own capture_begin / capture_end work -- e.g. the RNG generator's
+    # seed / offset fill_ -- is not counted) and the memory snapshots OUTSIDE it
+    # (no allocator query while the stream captures); then check()
+    @contextlib.contextmanager
+    def ops(self):
+        self._ops_enter()
+        try:
+            yield self
+        except BaseException as e:
+            self._ops_exit(type(e), e, None)
+            raise
+        self._ops_exit(None, None, None)
+
+    @contextlib.contextmanager
+    def memory(self):
+        self._mem_enter()
+        try:
+            yield self
+        except BaseException:
+            self._mem_exit(RuntimeError)
+            raise
+        self._mem_exit(None)
+
+    def _ops_enter(self):
+        if not self.enabled:
+            return
+        self._rec = _OpRecorder(os.environ.get("OMNIA_CAPTURE_GUARD_TRACE") == "1")
+        self._rec.__enter__()
+
+    def _ops_exit(self, et, ev, tb):
+        if not self.enabled or self._rec is None:
+            return
+        self._rec.__exit__(et, ev, tb)
+        self.ops = dict(self._rec.ops)
+        self.library = dict(self._rec.library)
+        for name, where in self._rec.where.items():
+            log.error("capture guard: %s first dispatched at\n%s", name, where)
+
+    def _mem_enter(self):
+        if self.enabled and self.device.type == "cuda":
+            self._before = _active_default_blocks(self.device)
+
+    def _mem_exit(self, et):
+        if self.enabled and et is None and self._before is not None:
+            self.leaked = sorted(_active_default_blocks(self.device) - self._before)
 
     def violations(self) -> list[str]:
         v = [f"framework op {k} x{n}" for k, n in sorted(self.ops.items())]

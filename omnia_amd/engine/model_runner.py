@@ -720,6 +720,7 @@ class ModelRunner:
             return g
         if self.graph_pool is None:
             self.graph_pool = torch.cuda.graph_pool_handle()
+            self._graph_rng_ready = False
         # warm-up/capture must not clobber live sampler outputs of an in-flight step
         saved = self.out_tok.clone()
         saved_slots = self.tok_slots.clone()
@@ -742,15 +743,28 @@ class ModelRunner:
         from .capture_guard import CaptureGuard
 
         guard = CaptureGuard(self.device, f"decode graph rows={nrows} cols={ncols}")
+        if not self._graph_rng_ready:
+            # PyTorch registers its RNG generator with the first capture of the
+            # process (seed / offset tensors in the default pool): do that in an
+            # empty capture, outside the guarded one
+            warm = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(warm, pool=self.graph_pool):
+                pass
+            del warm
+            self._graph_rng_ready = True
         try:
-            with guard:
+            with guard.memory():
                 with torch.cuda.graph(g, pool=self.graph_pool):
-                    self._decode_body(nrows, ncols)
+                    with guard.ops():
+                        self._decode_body(nrows, ncols)
         finally:
             if gc_was:
                 gc.enable()
+        guard.check()
         self.stats["capture_guard_violations"] = \
             self.stats.get("capture_guard_violations", 0) + len(guard.violations())
+        self.stats["capture_library_gemms"] = \
+            self.stats.get("capture_library_gemms", 0) + sum(guard.library.values())
         torch.cuda.synchronize()
         self.out_tok.copy_(saved)
         self.tok_slots.copy_(saved_slots)

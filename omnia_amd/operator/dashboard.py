@@ -11,6 +11,9 @@ one dependency-free page plus a small aiohttp backend:
 * ``GET /api/overview`` -- AgentRuntime phase / replicas / engine summary;
 * ``GET /api/arena/jobs`` -- ArenaJobs with type, phase and result summary;
 * ``GET /api/consent/{user}`` -- the privacy API's consent record (read-only);
+* costs, quality, memories, memory analytics, privacy stats (workspace-scoped
+  ``/api/workspaces/{ws}/...``), topology, tools, skills and settings views:
+  ``dashboard_views.py``;
 * ``/`` -- the page: resource tables, session list, and a chat console;
 * ``GET /api/auth/jwks`` -- the management-plane signing key set (public, the
   agents' facades fetch it: ``OMNIA_MGMT_PLANE_JWKS_URL``);
@@ -114,7 +117,7 @@ async function conn(){let v=document.getElementById('ws').value;
 function send(){sock.send(JSON.stringify({type:'message',content:document.getElementById('msg').value}))}
 const sel=document.getElementById('kind');for(const k of KINDS){const o=document.createElement('option');
  o.value=k;o.textContent=k;sel.appendChild(o)};sel.onchange=res;agents();res();sess();arena();
-</script></body></html>"""
+</script>__VIEWS__</body></html>"""
 
 
 WRITE_TYPES = ("application/json", "application/yaml", "application/x-yaml")
@@ -171,7 +174,7 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
               insecure_dev_writes: bool = False,
               allowed_origins: tuple = (), mgmt_key=None, mgmt_kid: str = "",
               twin_resolver=None, token_ttl_s: int = 300,
-              open_console: bool = False) -> web.Application:
+              open_console: bool = False, memory_api: str = "") -> web.Application:
     """``oidc``: ``{"jwks": {...}, "issuer": ..., "audience": ...,
     "write_groups": [...]}`` gates the API; ``allow_writes`` enables the
     management routes, which need OIDC unless ``insecure_dev_writes`` (module doc).
@@ -292,8 +295,10 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
         return web.json_response(body, status=st)
 
     async def page(_):
-        return web.Response(text=PAGE.replace("__KINDS__", json.dumps(plurals)),
-                            content_type="text/html")
+        from .dashboard_views import PAGE_SECTIONS
+
+        return web.Response(text=PAGE.replace("__KINDS__", json.dumps(plurals)).replace(
+            "__VIEWS__", PAGE_SECTIONS), content_type="text/html")
 
     async def resources(request):
         plural = request.match_info["plural"]
@@ -481,6 +486,14 @@ def build_app(api: str, session_api: str = "", privacy_api: str = "",
     app.router.add_delete("/api/resources/{plural}/{ns}/{name}", delete)
     app.router.add_post("/api/agents/{ns}/{name}/scale", scale)
     app.router.add_post("/api/arena/jobs/{ns}/{name}/cancel", cancel_job)
+    # costs / quality / memories / memory analytics / topology / tools / skills /
+    # settings (dashboard_views.py)
+    from . import dashboard_views
+
+    dashboard_views.mount(app, _get, api, session_api, memory_api, privacy_api, settings={
+        "auth": "oidc" if oidc else "none", "writes": bool(allow_writes),
+        "console": "ticket" if oidc else ("open" if open_console else "closed"),
+        "kinds": plurals})
     return app
 
 
@@ -491,6 +504,7 @@ def main(argv=None):
     ap.add_argument("--api", default="http://127.0.0.1:8090")
     ap.add_argument("--session-api", default="")
     ap.add_argument("--privacy-api", default="")
+    ap.add_argument("--memory-api", default="")
     ap.add_argument("--oidc-jwks-file", default="", help="IdP JWKS; gates /api/* when set")
     ap.add_argument("--oidc-issuer", default="")
     ap.add_argument("--oidc-audience", default="")
@@ -534,7 +548,8 @@ def main(argv=None):
                                          insecure_dev_writes=a.insecure_dev_writes,
                                          allowed_origins=tuple(a.allowed_origin),
                                          mgmt_key=mgmt_key, mgmt_kid=a.mgmt_kid,
-                                         open_console=a.open_console))
+                                         open_console=a.open_console,
+                                         memory_api=a.memory_api))
         await runner.setup()
         await web.TCPSite(runner, a.host, a.port).start()
         await asyncio.Event().wait()

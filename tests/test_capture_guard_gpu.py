@@ -12,19 +12,22 @@ from omnia_amd.engine.engine import EngineConfig, LLMEngine
 from omnia_amd.engine.sampling_params import SamplingParams
 
 
-@pytest.mark.parametrize("model", ["tiny-llama", "llama-3-8b"])
-def test_decode_graphs_pass_strict_guard(monkeypatch, model):
+@pytest.mark.parametrize("model,batch", [("tiny-llama", 8), ("llama-3-8b", 256)])
+def test_decode_graphs_pass_strict_guard(monkeypatch, model, batch):
+    """tiny-llama: every bucket; Llama-3-8B at the serving bucket (256 rows, the
+    bench's decode shape), where every projection is on a hand kernel."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     monkeypatch.setenv("OMNIA_CAPTURE_GUARD", "strict")
+    monkeypatch.setenv("OMNIA_CAPTURE_GUARD_TRACE", "1")
     big = model == "llama-3-8b"
 
     def run(graphs):
-        e = LLMEngine(EngineConfig(model=model, device="cuda", num_blocks=512, block_size=32,
-                                   max_batch=8, max_model_len=2048, use_graphs=graphs,
-                                   mixed_budget=0))
-        p = SamplingParams(temperature=0, max_tokens=12, ignore_eos=True)
-        prompts = [list(range(100, 400)), list(range(5, 60)), list(range(900, 1000))]
+        e = LLMEngine(EngineConfig(model=model, device="cuda", num_blocks=2048 if big else 512,
+                                   block_size=32, max_batch=batch, max_model_len=2048,
+                                   use_graphs=graphs, mixed_budget=0))
+        p = SamplingParams(temperature=0, max_tokens=6 if big else 12, ignore_eos=True)
+        prompts = [list(range(100 + i, 140 + i)) for i in range(batch)]
         out = [s.output for s in e.generate(prompts, p)]
         st = dict(e.runner.stats)
         del e

@@ -86,6 +86,10 @@ def parse(argv=None):
     ap.add_argument("--engine", choices=["gpu", "synthetic"], default="gpu",
                     help="synthetic: ws-path host capacity rehearsal -- the engine-core is a "
                          "token source paced like the measured GPU engine (engine/synthetic.py)")
+    ap.add_argument("--tp-shared-device", action="store_true",
+                    help="TP rehearsal on fewer GPUs than --tp: the TP ranks of the one "
+                         "replica share device(s) over the ipc transport (correctness and "
+                         "plumbing, not a scaling number)")
     ap.add_argument("--preflight", choices=["auto", "on", "off"], default="auto",
                     help="multi-GPU first-contact check in a fresh child per rank before any "
                          "pod starts (parallel/preflight.py): peer access, RCCL init + "
@@ -195,7 +199,7 @@ class WSDriver:
 
         self.a = a
         self.rank = rank
-        self.leader = rank % a.tp == 0
+        self.leader = rank % a.tp == 0 or a.tp_shared_device
         self.tmp = tempfile.mkdtemp(prefix=f"omnia-bench-r{rank}-")
         self.rng = random.Random(1234 + rank)
         self.pod = None
@@ -236,6 +240,11 @@ class WSDriver:
         fenv = {"OMNIA_AGENT_NAME": f"bench-{rank}", "OMNIA_MAX_CONNECTIONS": 4 * C + 64,
                 "OMNIA_MSG_RATE": 1000, "OMNIA_MSG_BURST": 1000}
         devs = list(range(local, local + a.tp)) if use_gpu else None
+        if devs and a.tp_shared_device:
+            import torch
+
+            n = max(1, torch.cuda.device_count())  # no HIP init: counting only
+            devs = sorted({d % n for d in devs})  # ranks share these (ipc transport)
         self.tp_preflight = None
         if devs and a.tp > 1 and a.preflight != "off" and a.engine == "gpu":
             self.tp_preflight = tp_preflight(devs)
@@ -506,7 +515,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if ws != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but the launcher started {ws} ranks")
-    if a.gpus % a.tp:
+    if a.gpus % a.tp and not a.tp_shared_device:
         raise SystemExit(f"--gpus {a.gpus} is not a multiple of --tp {a.tp}")
     if a.tp > 1 and a.path != "ws":
         raise SystemExit("--tp > 1 is served by the ws path (one TP pod per replica)")
@@ -759,12 +768,13 @@ def run(a, drv, ws, rank, use_gpu, host_only):
             "tp_preflight": getattr(drv, "tp_preflight", None),
             "config": {
                 "model": a.model,
-                "global_batch": a.concurrency * (ws // a.tp),
+                "global_batch": a.concurrency * max(1, ws // a.tp),
                 "seq_len": a.prompt_len + a.gen_len,
                 "prompt_len": a.prompt_len,
                 "gen_len": a.gen_len,
                 "concurrency_per_replica": a.concurrency,
-                "parallelism": f"dp{ws // a.tp}" + (f"-tp{a.tp}" if a.tp > 1 else ""),
+                "parallelism": f"dp{max(1, ws // a.tp)}" + (f"-tp{a.tp}" if a.tp > 1 else "")
+                + ("-shared-device-rehearsal" if a.tp_shared_device else ""),
                 "path": a.path,
                 "arrival": a.arrival if a.arrival == "closed" else f"poisson@{a.rate}/s",
                 "stream_interval_ms": a.stream_interval_ms,

@@ -124,7 +124,7 @@ class CaptureGuard:
     # seed / offset fill_ -- is not counted) and the memory snapshots OUTSIDE it
     # (no allocator query while the stream captures); then check()
     @contextlib.contextmanager
-    def ops(self):
+    def ops_scope(self):
         self._ops_enter()
         try:
             yield self
@@ -134,7 +134,7 @@ class CaptureGuard:
         self._ops_exit(None, None, None)
 
     @contextlib.contextmanager
-    def memory(self):
+    def memory_scope(self):
         self._mem_enter()
         try:
             yield self

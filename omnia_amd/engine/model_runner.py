@@ -753,9 +753,9 @@ class ModelRunner:
             del warm
             self._graph_rng_ready = True
         try:
-            with guard.memory():
+            with guard.memory_scope():
                 with torch.cuda.graph(g, pool=self.graph_pool):
-                    with guard.ops():
+                    with guard.ops_scope():
                         self._decode_body(nrows, ncols)
         finally:
             if gc_was:

@@ -264,12 +264,16 @@ class LlamaModel:
     splitk_half = os.environ.get("OMNIA_SPLITK_FP32", "0") != "1"
 
     def _slab_dtype(self, nwaves: int) -> torch.dtype:
+        if nwaves == ops.PGEMM_SPLIT:
+            return torch.float16  # the 256x256 split-K tile writes fp16 slabs only
         return torch.float16 if (self.splitk_half and nwaves < 0) else torch.float32
 
     def _wgemm(self, mode: int, x: torch.Tensor, w: torch.Tensor, S: int, nw: int, nwaves: int,
                out: torch.Tensor | None = None) -> torch.Tensor:
         """ops.wgemm, on the tile-packed copy of ``w`` when one exists for this
         tgemm config; split-K slabs in fp16 on the tile GEMM (``out``'s dtype)."""
+        if nwaves == ops.PGEMM_SPLIT:
+            return ops.pgemm_splitk(x, w, S, out)
         if nwaves < 0 and mode == 2 and out is not None and out.dtype == torch.float16:
             mode = 3
         packed = getattr(self, "_packed", None)
@@ -338,7 +342,7 @@ class LlamaModel:
             a = ops.linear_silu(h, layer["gate_up"])  # SwiGLU fused into decode GEMMs
         else:
             nw, nwaves, S = cfg
-            if S == 1:
+            if S == 1 and nwaves != ops.PGEMM_SPLIT:
                 a = self._wgemm(1, h, layer["gate_up"], 1, nw, nwaves)
             else:
                 a = ops.splitk_swiglu(self._wgemm(

@@ -205,13 +205,15 @@ WGEMM_MAX_M = 256
 _wgemm_table: dict | None = None
 _wgemm_on = os.environ.get("OMNIA_WGEMM", "1") != "0"
 WGEMM_BUCKETS = (16, 32, 64, 128, 192, 256)
+PGEMM_SPLIT = -64  # table nwaves code: pgemm 256x256 split-K tile, fp16 slabs
 
 
 def wgemm_config(M: int, N: int, K: int, mode: int) -> tuple[int, int, int] | None:
     """(nw, nwaves, splits) of the weight-streaming kernel for a decode projection
     (nwaves == 0 selects the wide-batch 32x32x16 kernel, wgemm_wide.hip, with nw
     32-column tiles per wave; nwaves < 0 the full-batch tile kernel, tgemm.hip,
-    with nw weight rows per block and non-temporal weight loads when -2),
+    with nw weight rows per block and non-temporal weight loads when -2;
+    nwaves == PGEMM_SPLIT the 256x256 split-K tile, pgemm.hip EPI 4),
     or None to keep the library / gemm.hip path.  ``mode`` 0 = plain projection
     (its split-K slabs are reduced by the consumer kernel), 1 = gate_up + SwiGLU.
     Measured dispatch: ``ops/tuned/wgemm_mi355x.json`` (scripts/wgemm_sweep.py +
@@ -241,6 +243,10 @@ def wgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, nw: int 
     mode 0: bf16 ``x @ w.T``; mode 1: bf16 ``silu(x Wg^T) * (x Wu^T)`` with
     ``w = [Wg; Wu]``; mode 2: fp32 split-K partial slabs ``[splits, M, N]`` whose
     sum is ``x @ w.T`` (reduced by the consumer kernel)."""
+    if nwaves == PGEMM_SPLIT:  # table code for the 256x256 split-K tile (pgemm.hip EPI 4)
+        if mode not in (2, 3):
+            raise ValueError("the pgemm split-K table entry produces fp16 slabs (mode 2/3)")
+        return pgemm_splitk(x, w, splits, out)
     if nwaves == 0:  # table code for the wide-batch kernel: nw = 32-col tiles per wave
         return wgemm_wide(mode, x, w, splits, nw, out)
     if nwaves < 0:  # table code for the full-batch tile kernel: nw = weight rows per block,

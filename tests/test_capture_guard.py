@@ -43,3 +43,21 @@ def test_off_mode_checks_nothing():
 def test_allowed_set_has_no_compute_ops():
     for bad in ("aten::where", "aten::index_copy_", "aten::clamp", "aten::eq", "aten::add"):
         assert bad not in ALLOWED
+
+
+def test_split_scopes_like_the_model_runner():
+    """The runner records ops INSIDE the capture and memory OUTSIDE it, then
+    calls check() -- the same protocol on CPU."""
+    g = CaptureGuard("cpu", "split", mode="strict")
+    with g.memory_scope():
+        torch.ones(2).fill_(3.0)  # outside the op scope: not counted (capture_begin's work)
+        with g.ops_scope():
+            torch.empty(4).view(2, 2)
+    g.check()
+    assert g.violations() == []
+    g2 = CaptureGuard("cpu", "split", mode="strict")
+    with g2.memory_scope():
+        with g2.ops_scope():
+            torch.zeros(3).add_(1)
+    with pytest.raises(CaptureGuardError, match="aten::add"):
+        g2.check()

@@ -754,7 +754,10 @@ class ModelRunner:
             self._graph_rng_ready = True
         try:
             with guard.memory_scope():
-                with torch.cuda.graph(g, pool=self.graph_pool):
+                # capture on the warm-up stream: per-stream library state (hipBLASLt
+                # workspace) already exists there, so nothing is allocated outside
+                # the graph pool while capturing
+                with torch.cuda.graph(g, pool=self.graph_pool, stream=s):
                     with guard.ops_scope():
                         self._decode_body(nrows, ncols)
         finally:

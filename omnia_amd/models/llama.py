@@ -328,8 +328,13 @@ class LlamaModel:
         """A prefill-sized projection the hand 256x256 MFMA kernel covers (the
         unfused paths: TP shards, MoE attention, CP): K whole 128-k iterations,
         N whole column tiles, and at least this forward's row threshold."""
+        # TP ranks rehearsed on ONE device (ipc transport) keep the library GEMMs:
+        # a 256x256 tile's 132 KB of LDS cannot share a CU with the peers'
+        # spinning all-reduce blocks, so a rank's GEMM can wait out their spin
+        # bound (the comm.hip error flag) -- real TP has one rank per GPU
         return (self.use_pgemm and not is_decode and self.device.type == "cuda"
-                and M >= self._min_rows and K % 128 == 0 and N % tn == 0)
+                and M >= self._min_rows and K % 128 == 0 and N % tn == 0
+                and (self.tp == 1 or pstate.ranks_per_device() == 1))
 
     def mlp(self, layer: dict, h: torch.Tensor, is_decode: bool = False):
         M, K = h.shape

@@ -233,3 +233,33 @@ def test_splitk_rejects_bad_split(gen):
         ops.pgemm_splitk(x, w, 3)
     with pytest.raises(RuntimeError):  # K / S = 64: not whole iterations of two K-tiles
         ops.pgemm_splitk(x, w, 16)
+
+
+@pytest.mark.parametrize("hq,hkv", [(8, 1), (4, 1), (6, 1)])
+def test_qkv_epilogue_tp_shard_heads(gen, schedule, hq, hkv):
+    """TP shards' QKV: one KV head per rank (Llama-3-70B at TP=8: hq 8, hkv 1 ->
+    10 heads = 5 tiles) -- 256-column tiles straddle the q / k / v boundaries;
+    the per-head epilogue still routes q, k and v correctly."""
+    D, bs, M, K = 128, 16, 300, 512
+    N = (hq + 2 * hkv) * D
+    x = _rand(M, K, gen=gen)
+    w = _rand(N, K, std=0.05, gen=gen)
+    positions = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int32, generator=gen)
+    cos_sin = ref.rope_cos_sin(8192, D, 5e5, None, device=DEV)
+    nb = 64
+    kc = torch.zeros(nb, hkv, bs, D, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    slots = torch.randperm(nb * bs, device=DEV, generator=gen)[:M].to(torch.int64)
+    q = torch.empty(M, hq * D, dtype=torch.bfloat16, device=DEV)
+    ops.pgemm(3, x, w, out=q, positions=positions, cos_sin=cos_sin, k_cache=kc, v_cache=vc,
+              slots=slots, hq=hq, hkv=hkv, block_size=bs)
+    qkv = (x.float() @ w.float().t()).to(torch.bfloat16)
+    qq = ref.apply_rope(qkv[:, : hq * D].view(M, hq, D), positions, cos_sin)
+    kk = ref.apply_rope(qkv[:, hq * D:(hq + hkv) * D].view(M, hkv, D), positions, cos_sin)
+    vv = qkv[:, (hq + hkv) * D:].view(M, hkv, D)
+    ok, e = _close(q.view(M, hq, D), qq, 2e-2)
+    assert ok, e
+    kw, vw = torch.zeros_like(kc), torch.zeros_like(vc)
+    ref.write_kv(kw, vw, kk, vv, slots)
+    assert _close(kc, kw, 2e-2)[0] and _close(vc, vw, 2e-2)[0]
+    assert not _close(vc, kw, 2e-2)[0]  # k and v not swapped

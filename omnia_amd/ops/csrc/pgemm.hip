@@ -107,6 +107,11 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return pack_bf2(a, b);
 }
 
+__device__ __forceinline__ float16v mfma32(short8 a, short8 b, float16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
 __device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
 template <int N>
@@ -221,8 +226,11 @@ __device__ __forceinline__ void epi_out(const PArgs& p, const bf16_t* stg, int m
   }
 }
 
-// VAR (tuning variants, EPI 0 only): bit 0 = no wave-row stagger, bit 1 = WITH
-// s_setprio around the MFMA clusters, bits 2-3 = m-tiles per L2 group (8/4/16/32)
+// VAR (tuning variants): bit 0 = no wave-row stagger, bit 1 = WITH s_setprio
+// around the MFMA clusters, bits 2-3 = m-tiles per L2 group (8/4/16/32), bit 4 =
+// 32x32x16 MFMA instead of 16x16x32 (same wave tile and LDS reads: a wave's
+// 64x32 quadrant piece is 2 x 1 32x32 tiles, 8 MFMAs of twice the work per
+// phase -- the chip can hold a different clock per MFMA shape)
 template <int EPI, int VAR = 0>
 __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
@@ -239,6 +247,7 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
   // (profiles/r4/pgemm_variants.log), so the default build (VAR 0) leaves it out;
   // the wave-row stagger is worth ~15 % and stays
   constexpr bool STAGGER = !(VAR & 1), PRIO = (VAR & 2) != 0;
+  constexpr bool M32 = (VAR & 16) != 0;
   const int per_group = GM * ntn;
   const int grp = bid / per_group, gm0 = grp * GM;
   const int gsz = mtn - gm0 < GM ? mtn - gm0 : GM;
@@ -294,32 +303,60 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
                                        (lds_ptr_t)(dst + i * 512), 16, 0, 0);
   };
 
-  float4v acc[2][2][4][2];
+  float4v acc[2][2][4][2];   // 16x16 tiles: [qa][qb][m][n]
+  float16v acc32[2][2][2];   // 32x32 tiles (M32): [qa][qb][m], n = 1
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < 2; ++b) {
+      if constexpr (M32) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc32[a][b][m][r] = 0.f;
+      } else {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) acc[a][b][m][n] = {0.f, 0.f, 0.f, 0.f};
+      }
+    }
+
+  // 16x16x32: af[m][ks] rows m*16 + fr, k chunk ks*4 + fq; 32x32x16: af[m][ks]
+  // (m < 2, ks < 4) rows m*32 + (lane & 31), k chunk 2 ks + (lane >> 5)
+  short8 af[4][2], bfr[2][2];
+  const int l32 = lane & 31, h32 = lane >> 5;
+  auto rdA = [&](int buf, int h) {
+    const bf16_t* base = lds + (buf * 4 + h) * HALF;
+    if constexpr (M32) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4)
+          af[m * 2 + (k4 >> 1)][k4 & 1] = *reinterpret_cast<const short8*>(
+              base + swz(wr * 64 + m * 32 + l32, k4 * 2 + h32));
+    } else {
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 2; ++n) acc[a][b][m][n] = {0.f, 0.f, 0.f, 0.f};
-
-  short8 af[4][2], bfr[2][2];
-  auto rdA = [&](int buf, int h) {
-    const bf16_t* base = lds + (buf * 4 + h) * HALF;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        af[m][ks] = *reinterpret_cast<const short8*>(base + swz(wr * 64 + m * 16 + fr, ks * 4 + fq));
+        for (int ks = 0; ks < 2; ++ks)
+          af[m][ks] = *reinterpret_cast<const short8*>(base + swz(wr * 64 + m * 16 + fr, ks * 4 + fq));
+    }
   };
   auto rdB = [&](int buf, int h) {
     const bf16_t* base = lds + (buf * 4 + 2 + h) * HALF;
+    if constexpr (M32) {
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+      for (int k4 = 0; k4 < 4; ++k4)
+        bfr[k4 >> 1][k4 & 1] = *reinterpret_cast<const short8*>(
+            base + swz(wc * 32 + l32, k4 * 2 + h32));
+    } else {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        bfr[n][ks] = *reinterpret_cast<const short8*>(base + swz(wc * 32 + n * 16 + fr, ks * 4 + fq));
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          bfr[n][ks] = *reinterpret_cast<const short8*>(base + swz(wc * 32 + n * 16 + fr, ks * 4 + fq));
+    }
   };
 
   using I0 = std::integral_constant<int, 0>;
@@ -361,13 +398,22 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
     constexpr int qa = (q == 0 || q == 1) ? 0 : 1;
     constexpr int qb = (q == 0 || q == 3) ? 0 : 1;
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+    if constexpr (M32) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int k4 = 0; k4 < 4; ++k4)
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < 2; ++m)
+          acc32[qa][qb][m] = mfma32(af[m * 2 + (k4 >> 1)][k4 & 1], bfr[k4 >> 1][k4 & 1],
+                                    acc32[qa][qb][m]);
+    } else {
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
-          acc[qa][qb][m][n] = mfma16(af[m][ks], bfr[n][ks], acc[qa][qb][m][n]);
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+            acc[qa][qb][m][n] = mfma16(af[m][ks], bfr[n][ks], acc[qa][qb][m][n]);
+    }
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -444,7 +490,33 @@ __global__ __launch_bounds__(512, 2) void pgemm_kernel(PArgs p) {
     *d1 = x1;
   };
 
-  if constexpr (EPI == 1 || EPI == 5) {
+  if constexpr (M32) {
+    // 32x32 tiles: lane holds column l32 and rows 8g + 4 h32 + (0..3) of group
+    // g = r >> 2 (r = 4g + j), i.e. four 4-row runs per tile
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row0 = a * 128 + wr * 64 + m * 32 + 8 * g + 4 * h32;
+          float4v rs = {1.f, 1.f, 1.f, 1.f};
+          if (scaled) rs = *reinterpret_cast<const float4v*>(rs_lds + row0);
+          if constexpr (EPI == 1 || EPI == 5) {
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              v[j] = silu(acc32[a][0][m][4 * g + j] * rs[j]) * (acc32[a][1][m][4 * g + j] * rs[j]);
+            put(row0, wc * 32 + l32, v[0], v[1], v[2], v[3]);
+          } else {
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+              put(row0, b * 128 + wc * 32 + l32, acc32[a][b][m][4 * g] * rs[0],
+                  acc32[a][b][m][4 * g + 1] * rs[1], acc32[a][b][m][4 * g + 2] * rs[2],
+                  acc32[a][b][m][4 * g + 3] * rs[3]);
+          }
+        }
+  } else if constexpr (EPI == 1 || EPI == 5) {
     // gate (b = 0) and up (b = 1) of feature nt*128 + wc*32 + n*16 + fr in one lane
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -829,6 +901,9 @@ int omnia_pgemm_variant(int variant, void* out, const void* X, const void* W, in
     case 4: pgemm_kernel<0, 4><<<grid, block, 0, s>>>(a); break;
     case 8: pgemm_kernel<0, 8><<<grid, block, 0, s>>>(a); break;
     case 12: pgemm_kernel<0, 12><<<grid, block, 0, s>>>(a); break;
+    case 32: pgemm_kernel<0, 16><<<grid, block, 0, s>>>(a); break;   // 32x32x16 MFMA
+    case 33: pgemm_kernel<0, 17><<<grid, block, 0, s>>>(a); break;
+    case 34: pgemm_kernel<0, 18><<<grid, block, 0, s>>>(a); break;
     case 16: pgemm4_kernel<0><<<grid, 256, 0, s>>>(a); break;
     default: return -2;
   }

@@ -15,6 +15,7 @@ from omnia_amd import ops  # noqa: E402
 SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096),
           "down": (4096, 14336)}
 VARIANTS = (0, 1, 2, 3, 4, 8, 12)
+# 32 = 32x32x16 MFMA (VAR bit 4), 33 / 34 = with no stagger / with s_setprio
 
 
 def timed(fn, iters):
@@ -31,6 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default="gate_up:16384,qkv:16384,o:16384,down:16384,qkv:4096,o:4096")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default=",".join(str(v) for v in VARIANTS))
     a = ap.parse_args()
     from omnia_amd.ops.gemm_tuning import enable_tuned_gemms
 
@@ -45,7 +47,7 @@ def main():
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         want = (x[:64].float() @ w.float().t())
         fns = {"lib": lambda: F.linear(x, w)}
-        for v in VARIANTS:
+        for v in [int(x) for x in a.variants.split(",")]:
             fns[f"v{v}"] = (lambda v=v: kk.pgemm_variant(v, out, x, w))
             fns[f"v{v}"]()
             torch.cuda.synchronize()

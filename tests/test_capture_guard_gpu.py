@@ -37,5 +37,7 @@ def test_decode_graphs_pass_strict_guard(monkeypatch, model, batch):
     g, st = run(True)
     assert st["captures"] > 0 and st["graph_replays"] > 0
     assert st.get("capture_guard_violations", 0) == 0
+    if big:  # the serving decode step: hand kernels and copies only, no library GEMM
+        assert st.get("capture_library_gemms", 0) == 0
     if not big:
         assert g == run(False)[0]

@@ -751,10 +751,11 @@ def moe(x: torch.Tensor, router: torch.Tensor, w_gu: torch.Tensor, w_down: torch
     kk = kernels()
     T, d = x.shape
     n = T * k
-    logits = F.linear(x, router)
     ids = torch.empty(T, k, dtype=torch.int32, device=x.device)
     wts = torch.empty(T, k, dtype=torch.float32, device=x.device)
-    kk.moe_topk(ids, wts, logits, k, renorm)
+    # router GEMM + softmax top-k in one hand kernel (moe.hip): no logits tensor,
+    # no library GEMM
+    kk.moe_router_topk(ids, wts, x.contiguous(), router, k, renorm)
     out = torch.empty_like(x)
     d, inter = x.shape[1], w_down.shape[2]
     if n >= MOE_TILE256_ROWS * (e_hi - e_lo) and d % 256 == 0 and inter % 128 == 0:

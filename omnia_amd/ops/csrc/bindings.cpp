@@ -74,6 +74,8 @@ int omnia_topk(int* out_idx, float* out_val, const float* scores, int nq, int64_
 int omnia_moe_topk(int* ids, float* wts, const void* logits, int logits_bf16, int n_tok, int E,
                    int k, int renorm, hipStream_t s);
 int omnia_moe_max_blocks(int n_assign, int n_experts, int bm);
+int omnia_moe_router_topk(int* ids, float* wts, const void* x, const void* router, int n_tok,
+                          int d, int E, int k, int renorm, hipStream_t s);
 int omnia_moe_align(int* sorted, int* blk_expert, int* n_blocks, const int* ids, int n, int E,
                     int e_lo, int e_hi, int max_blocks, int bm, hipStream_t s);
 int omnia_moe_gemm(int mode, void* out, const void* A, const void* W, const int* sorted,
@@ -481,6 +483,22 @@ void moe_topk(at::Tensor ids, at::Tensor wts, at::Tensor logits, int64_t k, bool
               "ids/wts [T, k]");
   CHECK_RC(omnia_moe_topk(ids.data_ptr<int>(), wts.data_ptr<float>(), logits.data_ptr(), bf, T,
                           E, k, renorm, cur_stream()), "moe_topk");
+}
+
+// router GEMM + top-k in one kernel: x [T, d] bf16, router [E, d] bf16 -> ids / wts [T, k]
+void moe_router_topk(at::Tensor ids, at::Tensor wts, at::Tensor x, at::Tensor router, int64_t k,
+                     bool renorm) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(router); CHECK_I32(ids);
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && router.dim() == 2 && router.is_contiguous() &&
+              router.size(1) == x.size(1) && x.size(1) % 8 == 0, "x [T, d], router [E, d]");
+  const int T = x.size(0), E = router.size(0);
+  TORCH_CHECK(E <= 64 && k >= 1 && k <= E, "E <= 64, 1 <= k <= E");
+  TORCH_CHECK(ids.numel() == (int64_t)T * k && wts.numel() == (int64_t)T * k &&
+              wts.scalar_type() == at::kFloat && ids.is_contiguous() && wts.is_contiguous(),
+              "ids/wts [T, k]");
+  CHECK_RC(omnia_moe_router_topk(ids.data_ptr<int>(), wts.data_ptr<float>(), x.data_ptr(),
+                                 router.data_ptr(), T, x.size(1), E, k, renorm, cur_stream()),
+           "moe_router_topk");
 }
 
 int64_t moe_max_blocks(int64_t n_assign, int64_t n_experts, int64_t bm) {
@@ -1090,6 +1108,7 @@ PYBIND11_MODULE(_omnia_kernels, m) {
   m.def("cosine_scores", &cosine_scores);
   m.def("topk", &topk);
   m.def("moe_topk", &moe_topk);
+  m.def("moe_router_topk", &moe_router_topk);
   m.def("moe_max_blocks", &moe_max_blocks, py::arg("n_assign"), py::arg("n_experts"),
         py::arg("bm") = 64);
   m.def("pgemm_moe", &pgemm_moe);

@@ -36,15 +36,10 @@ __device__ __forceinline__ float ld<float>(const float* p) { return *p; }
 template <>
 __device__ __forceinline__ float ld<bf16_t>(const bf16_t* p) { return bf2f(*p); }
 
-template <typename T>
-__global__ __launch_bounds__(256) void moe_topk_kernel(int* __restrict__ ids,
-                                                       float* __restrict__ wts,
-                                                       const T* __restrict__ logits, int n_tok,
-                                                       int E, int k, int renorm) {
-  const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= n_tok) return;
-  float x = lane < E ? ld<T>(logits + (int64_t)t * E + lane) : -INFINITY;
+// one wave per token: lane e (< E) holds expert e's logit x; writes the token's
+// k (id, weight) pairs -- softmax over all E, top-k, optional renormalisation
+__device__ __forceinline__ void select_topk(float x, int lane, int t, int E, int k, int renorm,
+                                            int* __restrict__ ids, float* __restrict__ wts) {
   if (!(x == x)) x = -INFINITY;  // NaN logits (e.g. a padded row) never win a slot
   const float m = wave_max(x);
   // an all -inf row (padding) routes uniformly instead of producing NaN weights
@@ -71,6 +66,59 @@ __global__ __launch_bounds__(256) void moe_topk_kernel(int* __restrict__ ids,
   }
   const float denom = renorm ? sel : total;
   if (taken) wts[(int64_t)t * k + my_slot] = mine / denom;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void moe_topk_kernel(int* __restrict__ ids,
+                                                       float* __restrict__ wts,
+                                                       const T* __restrict__ logits, int n_tok,
+                                                       int E, int k, int renorm) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= n_tok) return;
+  const float x = lane < E ? ld<T>(logits + (int64_t)t * E + lane) : -INFINITY;
+  select_topk(x, lane, t, E, k, renorm, ids, wts);
+}
+
+// Router GEMM fused with the top-k: logits[t][e] = x[t] . router[e] computed
+// by the token's wave (lane = 8-element chunks of d; the E router rows are a few
+// KB per expert and stay L2-resident), rounded to bf16 as a bf16 linear layer
+// would produce them, then selected in-wave -- no [T, E] logits tensor and no
+// library GEMM on the MoE path.
+template <int E_MAX>
+__global__ __launch_bounds__(256) void moe_router_topk_kernel(
+    int* __restrict__ ids, float* __restrict__ wts, const bf16_t* __restrict__ x,
+    const bf16_t* __restrict__ router, int n_tok, int d, int E, int k, int renorm) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= n_tok) return;
+  const bf16_t* xr = x + (int64_t)t * d;
+  float acc[E_MAX];
+#pragma unroll
+  for (int e = 0; e < E_MAX; ++e) acc[e] = 0.f;
+  for (int c = lane * 8; c < d; c += 64 * 8) {
+    const short8 xv = *reinterpret_cast<const short8*>(xr + c);
+    float xf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xf[j] = bf2f((uint16_t)xv[j]);
+#pragma unroll
+    for (int e = 0; e < E_MAX; ++e) {
+      if (e < E) {
+        const short8 wv = *reinterpret_cast<const short8*>(router + (int64_t)e * d + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[e] += xf[j] * bf2f((uint16_t)wv[j]);
+      }
+    }
+  }
+  float mine = -INFINITY;
+#pragma unroll
+  for (int e = 0; e < E_MAX; ++e) {
+    if (e < E) {
+      const float v = bf2f(f2bf(wave_sum(acc[e])));
+      if (lane == e) mine = v;
+    }
+  }
+  select_topk(mine, lane, t, E, k, renorm, ids, wts);
 }
 
 // ------------------------------------------------------------------ align
@@ -273,6 +321,22 @@ int omnia_moe_topk(int* ids, float* wts, const void* logits, int logits_bf16, in
   else
     moe_topk_kernel<float><<<blocks, 256, 0, s>>>(ids, wts, (const float*)logits, n_tok, E, k,
                                                   renorm);
+  return (int)hipGetLastError();
+}
+
+int omnia_moe_router_topk(int* ids, float* wts, const void* x, const void* router, int n_tok,
+                          int d, int E, int k, int renorm, hipStream_t s) {
+  if (E > 64 || k > E || k < 1 || d % 8) return -1;
+  if (n_tok == 0) return 0;
+  const int blocks = (n_tok + 3) / 4;
+#define OMNIA_RT(EM)                                                                         \
+  moe_router_topk_kernel<EM><<<blocks, 256, 0, s>>>(ids, wts, (const bf16_t*)x,               \
+                                                   (const bf16_t*)router, n_tok, d, E, k, renorm)
+  if (E <= 8) OMNIA_RT(8);
+  else if (E <= 16) OMNIA_RT(16);
+  else if (E <= 32) OMNIA_RT(32);
+  else OMNIA_RT(64);
+#undef OMNIA_RT
   return (int)hipGetLastError();
 }
 

@@ -98,7 +98,8 @@ class ExpertParallelMoE:
             T = x.shape[0]
             ids = torch.empty(T, self.k, dtype=torch.int32, device=x.device)
             wts = torch.empty(T, self.k, dtype=torch.float32, device=x.device)
-            ops.kernels().moe_topk(ids, wts, F.linear(x, self.router), self.k, self.renorm)
+            ops.kernels().moe_router_topk(ids, wts, x.contiguous(), self.router, self.k,
+                                          self.renorm)
             return ids, wts
         return ref.moe_route(F.linear(x.float(), self.router.float()), self.k, self.renorm)
 

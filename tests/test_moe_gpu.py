@@ -169,3 +169,26 @@ def test_moe_decode_layer_bandwidth_report():
     gb = (wgu.numel() + wd.numel()) * 2 / 1e9
     print(f"\nMoE decode layer T={T}: {ms:.3f} ms, weights {gb:.2f} GB -> {gb / ms:.2f} TB/s")
     assert ms > 0
+
+
+@pytest.mark.parametrize("T,d,E,k", [(1, 4096, 8, 2), (333, 4096, 8, 2), (4096, 1024, 16, 4),
+                                     (64, 512, 64, 6)])
+def test_router_topk_fused_matches_linear_then_topk(T, d, E, k):
+    """The fused router GEMM + top-k (no logits tensor, no library GEMM) routes
+    like bf16 F.linear followed by moe_topk -- up to bf16 rounding ties of the
+    logits, which may order near-equal experts differently (<= 0.5 % of rows)."""
+    g = torch.Generator().manual_seed(T * E + d)
+    x = torch.randn(T, d, generator=g).to(torch.bfloat16).cuda()
+    router = (torch.randn(E, d, generator=g) * 0.02).to(torch.bfloat16).cuda()
+    ids = torch.empty(T, k, dtype=torch.int32, device="cuda")
+    w = torch.empty(T, k, dtype=torch.float32, device="cuda")
+    ops.kernels().moe_router_topk(ids, w, x, router, k, True)
+    ids2 = torch.empty_like(ids)
+    w2 = torch.empty_like(w)
+    ops.kernels().moe_topk(ids2, w2, torch.nn.functional.linear(x, router), k, True)
+    same = (ids == ids2).all(1)
+    assert same.float().mean().item() >= 0.995, same.float().mean().item()
+    torch.testing.assert_close(w[same], w2[same], atol=1e-2, rtol=1e-2)
+    # against the fp32 oracle's routing on the same rows
+    rid, rw = ref.moe_route(torch.nn.functional.linear(x.float(), router.float()).cpu(), k)
+    assert (ids.cpu() == rid).all(1).float().mean().item() >= 0.99

@@ -3,9 +3,16 @@
 
 TTFT = first ``chunk`` (or ``done`` when the agent does not stream) after the
 ``message`` frame; turn latency = ``done`` arrival.  Client-side tools are
-answered with a canned result so tool loops complete."""
+answered with a canned result so tool loops complete.
+
+Between turns a session keeps one reader task on its socket: aiohttp answers
+the facade's heartbeat pings only inside ``receive()``, so a session opened
+ahead of its turn (load generators pre-connect the next wave) and left unread
+for longer than the facade's ping interval would be closed under it."""
 from __future__ import annotations
 
+import asyncio
+import contextlib
 import json
 import time
 
@@ -29,6 +36,7 @@ class FleetSession:
         self._http = None
         self.ws = None
         self.session_id = ""
+        self._idle: asyncio.Task | None = None
 
     async def __aenter__(self):
         if self._shared is None:
@@ -41,9 +49,33 @@ class FleetSession:
         if hello.get("type") != "connected":
             raise RuntimeError(f"facade handshake failed: {hello}")
         self.session_id = hello.get("session_id", "")
+        self._idle_start()
         return self
 
+    def _idle_start(self):
+        """Read (and so answer pings) until the next turn.  The facade sends
+        nothing else between turns; a close or error it sends is raised by the
+        next turn."""
+        async def idle():
+            self._idle_msg = await self.ws.receive()
+
+        self._idle_msg = None
+        self._idle = asyncio.ensure_future(idle())
+
+    async def _idle_stop(self):
+        t, self._idle = self._idle, None
+        if t is not None and not t.done():
+            t.cancel()
+            with contextlib.suppress(asyncio.CancelledError):
+                await t
+        msg, self._idle_msg = self._idle_msg, None
+        if msg is not None and msg.type in (aiohttp.WSMsgType.CLOSE, aiohttp.WSMsgType.CLOSED,
+                                            aiohttp.WSMsgType.ERROR):
+            raise RuntimeError(f"facade closed the idle session ({msg.type})")
+
     async def __aexit__(self, *exc):
+        with contextlib.suppress(RuntimeError):
+            await self._idle_stop()
         if self.ws is not None:
             await self.ws.close()
         if self._http is not None:
@@ -51,6 +83,7 @@ class FleetSession:
 
     async def turn(self, content: str, metadata: dict | None = None,
                    tool_result=lambda name, args: {"ok": True}) -> dict:
+        await self._idle_stop()
         t0 = time.perf_counter()
         mark("client_send")
         await self.ws.send_json({"type": "message", "content": content,
@@ -84,6 +117,7 @@ class FleetSession:
                     ttft = lat
                 final = f.get("content") or "".join(text)
                 usage = f.get("usage") or {}
+                self._idle_start()
                 return {"content": final, "ttft_ms": ttft * 1e3, "latency_ms": lat * 1e3,
                         "usage": usage, "chunk_times_s": stamps}
             elif t == "error":

@@ -176,7 +176,8 @@ def test_moe_decode_layer_bandwidth_report():
 def test_router_topk_fused_matches_linear_then_topk(T, d, E, k):
     """The fused router GEMM + top-k (no logits tensor, no library GEMM) routes
     like bf16 F.linear followed by moe_topk -- up to bf16 rounding ties of the
-    logits, which may order near-equal experts differently (<= 0.5 % of rows)."""
+    logits, which may order near-equal experts differently (<= 0.5 % of rows
+    against the library GEMM; 2-6 % against fp32 at E=16-64, k=4-6)."""
     g = torch.Generator().manual_seed(T * E + d)
     x = torch.randn(T, d, generator=g).to(torch.bfloat16).cuda()
     router = (torch.randn(E, d, generator=g) * 0.02).to(torch.bfloat16).cuda()
@@ -189,6 +190,15 @@ def test_router_topk_fused_matches_linear_then_topk(T, d, E, k):
     same = (ids == ids2).all(1)
     assert same.float().mean().item() >= 0.995, same.float().mean().item()
     torch.testing.assert_close(w[same], w2[same], atol=1e-2, rtol=1e-2)
-    # against the fp32 oracle's routing on the same rows
-    rid, rw = ref.moe_route(torch.nn.functional.linear(x.float(), router.float()).cpu(), k)
-    assert (ids.cpu() == rid).all(1).float().mean().item() >= 0.99
+    # against the fp32 oracle: every chosen expert's fp32 logit, in the kernel's
+    # order, equals the fp32 top-k value at that rank up to bf16 rounding (the
+    # kernel, like the library GEMM, rounds logits to bf16, so near-ties may swap)
+    lf = torch.nn.functional.linear(x.float(), router.float()).cpu()
+    rid, rw = ref.moe_route(lf, k)
+    sel = lf.gather(1, ids.cpu().long())
+    top = lf.topk(k, dim=1).values
+    tol = 2.0 ** -7 * lf.abs().amax(1, keepdim=True)
+    assert ((sel - top).abs() <= tol).all()
+    m = (ids.cpu() == rid).all(1)  # rows whose order no near-tie swapped
+    assert m.float().mean().item() >= 0.9
+    torch.testing.assert_close(w.cpu()[m], rw[m], atol=1e-2, rtol=1e-2)

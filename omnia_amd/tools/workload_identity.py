@@ -56,9 +56,10 @@ class AzureTokenAcquirer:
     async def token(self, audience: str) -> str:
         if not audience:
             raise WorkloadIdentityError("workloadIdentity: audience is required")
-        if self._lock is None:
-            self._lock = asyncio.Lock()
-        async with self._lock:  # low contention: one lock over cache + exchange
+        loop = asyncio.get_running_loop()
+        if self._lock is None or self._lock[0] is not loop:  # a lock serves one loop
+            self._lock = (loop, asyncio.Lock())
+        async with self._lock[1]:  # low contention: one lock over cache + exchange
             hit = self.cache.get(audience)
             if hit is not None and self.now() < hit[1] - REFRESH_MARGIN_S:
                 return hit[0]

@@ -6,6 +6,10 @@ partition-merge kernel included.  The K+V stream (>= 545 MB) exceeds the
 dirty lines would be written back under the measured kernel).
 
     python scripts/decode_attn_sweep.py [--nw 2,4] [--parts 256,512,1024]
+    python scripts/decode_attn_sweep.py --batch 128 --hq 64   # Llama-3-70B, TP=1
+
+Rows ``mix`` draw every sequence's length uniformly from 513..640, as in a
+closed-loop wave (the partition split then varies per sequence).
 
 ``--nw`` runs each shape with the 2- and the 4-wave workgroup
 (``OMNIA_DECODE_NW``, read per launch) and checks them against each other.
@@ -25,24 +29,33 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nw", default="0")
     ap.add_argument("--parts", default="128,192,256,320,384,512,640,1024")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--hq", type=int, default=32)
     a = ap.parse_args()
     nws = [int(x) for x in a.nw.split(",")]
     parts = [int(x) for x in a.parts.split(",")]
     torch.manual_seed(0)
     dev = "cuda"
-    B, hq, hkv, D, BS = 256, 32, 8, 128, 32
+    B, hq, hkv, D, BS = a.batch, a.hq, 8, 128, 32
     max_len = 1024
     mb = max_len // BS
     nblk = B * mb + 8
-    kc = torch.randn(nblk, hkv, BS, D, device=dev, dtype=torch.bfloat16)
-    vc = torch.randn(nblk, hkv, BS, D, device=dev, dtype=torch.bfloat16)
+    # two cache copies, alternated per launch: the working set stays above the
+    # 256 MB Infinity Cache at the smaller (70B, B=128) shape too
+    kcs = [torch.randn(nblk, hkv, BS, D, device=dev, dtype=torch.bfloat16) for _ in range(2)]
+    vcs = [torch.randn(nblk, hkv, BS, D, device=dev, dtype=torch.bfloat16) for _ in range(2)]
+    kc, vc = kcs[0], vcs[0]
     perm = torch.randperm(nblk - 8, device=dev)[:B * mb].to(torch.int32)
     bt = perm.view(B, mb).contiguous()
     q = torch.randn(B, hq, D, device=dev, dtype=torch.bfloat16)
     scale = D ** -0.5
     print(f"{'len':>5} {'part':>5} {'nw':>3} {'us':>8} {'TB/s':>6}  err", flush=True)
-    for L in (520, 576, 640):
-        sl = torch.full((B,), L, dtype=torch.int32, device=dev)
+    for L in (520, 576, 640, "mix"):
+        if L == "mix":
+            g = torch.Generator().manual_seed(1)
+            sl = torch.randint(513, 641, (B,), generator=g, dtype=torch.int32).to(dev)
+        else:
+            sl = torch.full((B,), L, dtype=torch.int32, device=dev)
         ref = None
         for part, nw in [(p, w) for p in parts for w in nws]:
             if nw:
@@ -55,18 +68,18 @@ def main():
                 ref = out.float().clone()
             err = (out.float() - ref).abs().max().item()
             ts = []
-            for _ in range(30):
+            for i in range(30):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                ops.decode_attention(q, kc, vc, bt, sl, scale, part_size=part, workspace=ws,
-                                     out=out)
+                ops.decode_attention(q, kcs[i % 2], vcs[i % 2], bt, sl, scale, part_size=part,
+                                     workspace=ws, out=out)
                 e1.record()
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1) * 1e3)
             ts.sort()
             us = ts[len(ts) // 2]
-            nbytes = B * L * hkv * D * 2 * 2
-            print(f"{L:5d} {part:5d} {nw:3d} {us:8.1f} {nbytes / us / 1e6:6.2f}  {err:.2e}", flush=True)
+            nbytes = int(sl.sum().item()) * hkv * D * 2 * 2
+            print(f"{L!s:>5} {part:5d} {nw:3d} {us:8.1f} {nbytes / us / 1e6:6.2f}  {err:.2e}", flush=True)
     time.sleep(0.1)
 
 

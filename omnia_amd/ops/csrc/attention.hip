@@ -39,7 +39,9 @@ constexpr int D = 128;
 // for UG > 1, the first V batch is issued ahead of the softmax) -- the memory-
 // level parallelism of one workgroup, which at short contexts (one workgroup
 // streams a whole ~600-token context) sets the kernel's speed, not HBM.
-template <int G, int BS, int UG, int NW>
+// U: V rows (16 B per lane each) one wave keeps in flight under the P.V of the
+// previous batch -- the same parallelism for phase 3.
+template <int G, int BS, int UG, int NW, int U>
 __global__ __launch_bounds__(64 * NW) void decode_attn_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
@@ -118,7 +120,6 @@ __global__ __launch_bounds__(64 * NW) void decode_attn_kernel(
   // first V batch of phase 3 in flight across the softmax (plain loads survive
   // the barriers); lane = (token sub-index tg = lane>>4, dim chunk ch = lane&15)
   const int tg = lane >> 4, ch = lane & 15;
-  constexpr int U = 4;
   short8 vv[U];
   auto vload = [&](int base) {
 #pragma unroll
@@ -703,11 +704,10 @@ int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void*
   if (B == 0) return 0;
   const int G = hq / hkv;
   const float scale_log2 = scale * 1.4426950408889634f;
-  // OMNIA_DECODE_UG=1 selects the single-group schedule (A/B measurements)
-  static const int ug = [] {
-    const char* e = getenv("OMNIA_DECODE_UG");
-    return e && atoi(e) == 1 ? 1 : 4;
-  }();
+  // OMNIA_DECODE_UG = 1 / 8 selects the single-group / 8-group K schedule
+  // (A/B measurements; read per call)
+  const char* ug_e = getenv("OMNIA_DECODE_UG");
+  const int ug = ug_e && atoi(ug_e) == 1 ? 1 : (ug_e && atoi(ug_e) == 8 ? 8 : 4);
   // waves per workgroup: with many (sequence, kv head, partition) workgroups a
   // 4-wave group (90+ VGPRs -> 5 groups per CU) leaves ~2048 groups in two
   // uneven rounds; 2-wave groups keep every group of a 256-sequence batch
@@ -718,19 +718,27 @@ int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void*
   const int nw_env = nw_e ? atoi(nw_e) : 0;
   const int64_t groups = (int64_t)B * hkv * max_parts;
   const int nw = nw_env == 2 || nw_env == 4 ? nw_env : (groups >= 1024 ? 2 : 4);
+  // V rows in flight per lane in phase 3 (OMNIA_DECODE_U = 4 / 8, read per call)
+  const char* u_e = getenv("OMNIA_DECODE_U");
+  const int uv = u_e && atoi(u_e) == 8 ? 8 : 4;
   dim3 grid(B, hkv, max_parts), block(64 * nw);
   const size_t tile = (size_t)G * part_size > (size_t)nw * G * D ? (size_t)G * part_size
                                                                   : (size_t)nw * G * D;
   const size_t lds = 64 + tile * 4 + (part_size / block_size) * 4;
-#define OMNIA_DEC_UG(GG, BB, UU, NN)                                                           \
-  decode_attn_kernel<GG, BB, UU, NN><<<grid, block, lds, s>>>(                                \
+#define OMNIA_DEC_UG(GG, BB, UU, NN, VV)                                                       \
+  decode_attn_kernel<GG, BB, UU, NN, VV><<<grid, block, lds, s>>>(                            \
       (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, (const bf16_t*)k_cache,               \
       (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, hkv, q_stride, part_size,   \
       max_parts, scale_log2)
-#define OMNIA_DEC_NW(GG, BB, UU) \
-  do { if (nw == 2) OMNIA_DEC_UG(GG, BB, UU, 2); else OMNIA_DEC_UG(GG, BB, UU, 4); } while (0)
-#define OMNIA_DEC(GG, BB) \
-  do { if (ug == 1) OMNIA_DEC_NW(GG, BB, 1); else OMNIA_DEC_NW(GG, BB, 4); } while (0)
+#define OMNIA_DEC_NW(GG, BB, UU, VV) \
+  do { if (nw == 2) OMNIA_DEC_UG(GG, BB, UU, 2, VV); else OMNIA_DEC_UG(GG, BB, UU, 4, VV); } while (0)
+#define OMNIA_DEC(GG, BB)                          \
+  do {                                             \
+    if (ug == 1) OMNIA_DEC_NW(GG, BB, 1, 4);       \
+    else if (ug == 8) OMNIA_DEC_NW(GG, BB, 8, 8);  \
+    else if (uv == 8) OMNIA_DEC_NW(GG, BB, 4, 8);  \
+    else OMNIA_DEC_NW(GG, BB, 4, 4);               \
+  } while (0)
 #define OMNIA_DEC_BS(GG)                                \
   if (block_size == 16) OMNIA_DEC(GG, 16);              \
   else if (block_size == 32) OMNIA_DEC(GG, 32);         \

@@ -29,6 +29,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nw", default="0")
     ap.add_argument("--parts", default="128,192,256,320,384,512,640,1024")
+    ap.add_argument("--u", default="4", help="V rows in flight per lane (OMNIA_DECODE_U); "
+                    "g8 = 8 K groups and 8 V rows (OMNIA_DECODE_UG=8)")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--hq", type=int, default=32)
     a = ap.parse_args()
@@ -49,7 +51,7 @@ def main():
     bt = perm.view(B, mb).contiguous()
     q = torch.randn(B, hq, D, device=dev, dtype=torch.bfloat16)
     scale = D ** -0.5
-    print(f"{'len':>5} {'part':>5} {'nw':>3} {'us':>8} {'TB/s':>6}  err", flush=True)
+    print(f"{'len':>5} {'part':>5} {'nw':>3} {'u':>2} {'us':>8} {'TB/s':>6}  err", flush=True)
     for L in (520, 576, 640, "mix"):
         if L == "mix":
             g = torch.Generator().manual_seed(1)
@@ -57,7 +59,10 @@ def main():
         else:
             sl = torch.full((B,), L, dtype=torch.int32, device=dev)
         ref = None
-        for part, nw in [(p, w) for p in parts for w in nws]:
+        for part, nw, uv in [(p, w, u) for p in parts for w in nws
+                             for u in a.u.split(",")]:
+            os.environ["OMNIA_DECODE_U"] = "8" if uv == "g8" else uv
+            os.environ["OMNIA_DECODE_UG"] = "8" if uv == "g8" else "4"
             if nw:
                 os.environ["OMNIA_DECODE_NW"] = str(nw)
             else:
@@ -79,7 +84,7 @@ def main():
             ts.sort()
             us = ts[len(ts) // 2]
             nbytes = int(sl.sum().item()) * hkv * D * 2 * 2
-            print(f"{L!s:>5} {part:5d} {nw:3d} {us:8.1f} {nbytes / us / 1e6:6.2f}  {err:.2e}", flush=True)
+            print(f"{L!s:>5} {part:5d} {nw:3d} {uv:>2} {us:8.1f} {nbytes / us / 1e6:6.2f}  {err:.2e}", flush=True)
     time.sleep(0.1)
 
 

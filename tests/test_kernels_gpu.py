@@ -102,12 +102,16 @@ def _tables(lens, bs, nb_total):
     return bt.to(DEV)
 
 
+@pytest.mark.parametrize("uv", ["4", "8", "g8"])
 @pytest.mark.parametrize("nw", ["2", "4"])
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 8)])
 @pytest.mark.parametrize("bs", [16, 32])
-def test_decode_attention(hq, hkv, bs, nw, monkeypatch):
-    # both workgroup shapes (2 / 4 waves); the launcher picks by grid size
+def test_decode_attention(hq, hkv, bs, nw, uv, monkeypatch):
+    # both workgroup shapes (2 / 4 waves; the launcher picks by grid size) and
+    # both V prefetch depths
     monkeypatch.setenv("OMNIA_DECODE_NW", nw)
+    monkeypatch.setenv("OMNIA_DECODE_U", "8" if uv == "g8" else uv)
+    monkeypatch.setenv("OMNIA_DECODE_UG", "8" if uv == "g8" else "4")
     torch.manual_seed(3)
     lens = [1, 17, 64, 513, 1500, 3000]
     B = len(lens)

@@ -5,15 +5,19 @@ TTFT = first ``chunk`` (or ``done`` when the agent does not stream) after the
 ``message`` frame; turn latency = ``done`` arrival.  Client-side tools are
 answered with a canned result so tool loops complete.
 
-Between turns a session keeps one reader task on its socket: aiohttp answers
-the facade's heartbeat pings only inside ``receive()``, so a session opened
-ahead of its turn (load generators pre-connect the next wave) and left unread
-for longer than the facade's ping interval would be closed under it."""
+A session idle between turns for longer than ``IDLE_AFTER_S`` starts one reader
+task on its socket: aiohttp answers the facade's heartbeat pings only inside
+``receive()``, so a session opened ahead of its turn (load generators
+pre-connect the next wave) and left unread for longer than the facade's ping
+interval would be closed under it.  Sessions reused within seconds -- a closed-
+loop bench wave -- never start one (it cost ~1.5 % of the headline bench's
+engine busy time when started on every session)."""
 from __future__ import annotations
 
 import asyncio
 import contextlib
 import json
+import os
 import time
 
 import aiohttp
@@ -37,6 +41,8 @@ class FleetSession:
         self.ws = None
         self.session_id = ""
         self._idle: asyncio.Task | None = None
+        self._idle_timer: asyncio.TimerHandle | None = None
+        self._idle_msg = None
 
     async def __aenter__(self):
         if self._shared is None:
@@ -52,17 +58,32 @@ class FleetSession:
         self._idle_start()
         return self
 
+    IDLE_READ = os.environ.get("OMNIA_FLEET_IDLE_READ", "1") != "0"
+    IDLE_AFTER_S = 5.0  # well inside aiohttp's pong deadline (half the ping interval)
+
     def _idle_start(self):
-        """Read (and so answer pings) until the next turn.  The facade sends
-        nothing else between turns; a close or error it sends is raised by the
-        next turn."""
+        """After IDLE_AFTER_S without a turn, read (and so answer pings) until
+        the next turn.  The facade sends nothing else between turns; a close or
+        error it sends is raised by the next turn."""
+        self._idle_msg = None
+        if self.IDLE_READ:
+            self._idle_timer = asyncio.get_running_loop().call_later(self.IDLE_AFTER_S,
+                                                                     self._idle_spawn)
+
+    def _idle_spawn(self):
+        self._idle_timer = None
+        if self.ws is None or self.ws.closed or self._idle is not None:
+            return
+
         async def idle():
             self._idle_msg = await self.ws.receive()
 
-        self._idle_msg = None
         self._idle = asyncio.ensure_future(idle())
 
     async def _idle_stop(self):
+        if self._idle_timer is not None:
+            self._idle_timer.cancel()
+            self._idle_timer = None
         t, self._idle = self._idle, None
         if t is not None and not t.done():
             t.cancel()

@@ -27,6 +27,10 @@ from ..parallel import overlap
 from ..parallel import state as pstate
 from .config import ModelConfig
 
+# decode attention: below this many (sequence, kv head) pairs a step splits every
+# live context on the device (``LlamaModel.decode_part``)
+DECODE_SPLIT_PAIRS = int(os.environ.get("OMNIA_DECODE_SPLIT_PAIRS", "0"))
+
 
 @dataclass
 class ForwardBatch:
@@ -394,10 +398,11 @@ class LlamaModel:
                         self.hq, self.hkv, kv.block_size)
         q3 = q.view(T, self.hq, D)
         if fb.is_decode:
-            part = self.decode_part(T, fb.block_tables.shape[1] * kv.block_size)
-            ws = self._decode_ws(T, fb.block_tables.shape[1], kv.block_size, h.device, part)
+            part, splits = self.decode_part(T, fb.block_tables.shape[1] * kv.block_size)
+            ws = self._decode_ws(T, fb.block_tables.shape[1], kv.block_size, h.device, part,
+                                 splits)
             o = ops.decode_attention(q3, kv.k[li], kv.v[li], fb.block_tables, fb.seq_lens,
-                                     self.scale, part_size=part, workspace=ws)
+                                     self.scale, part_size=part, workspace=ws, splits=splits)
         elif fb.num_decode:
             o = self._mixed_attention(li, q3, fb, kv)
         else:
@@ -414,35 +419,46 @@ class LlamaModel:
         o = torch.empty_like(q3) if q3.is_contiguous() else torch.empty(
             T, self.hq, D, dtype=q3.dtype, device=q3.device)
         mb = fb.dec_block_tables.shape[1]
-        part = self.decode_part(Bd, mb * kv.block_size)
+        part, splits = self.decode_part(Bd, mb * kv.block_size)
         ws = self._decode_ws(1 << max(0, Bd - 1).bit_length(), mb, kv.block_size, q3.device,
-                             part)  # pow2 rows: few workspace shapes across mixed steps
+                             part, splits)  # pow2 rows: few workspace shapes across mixed steps
         ops.decode_attention(q3[:Bd], kv.k[li], kv.v[li], fb.dec_block_tables,
                              fb.dec_seq_lens, self.scale, part_size=part, workspace=ws,
-                             out=o[:Bd])
+                             out=o[:Bd], splits=splits)
         if T > Bd:
             ops.prefill_attention(q3[Bd:], kv.k[li], kv.v[li], fb.block_tables,
                                   fb.q_start_loc, fb.seq_lens, self.scale, fb.tile_seq,
                                   fb.tile_q0, out=o[Bd:])
         return o
 
-    def decode_part(self, batch: int, max_ctx: int) -> int:
-        """Split-K partition length: as long as possible (fewer partials to merge,
-        no merge kernel when one partition covers the context) while keeping
-        >= ~2048 workgroups in flight to fill 256 CUs."""
+    def decode_part(self, batch: int, max_ctx: int) -> tuple[int, int]:
+        """(partition length, splits) of the split-K decode attention.
+
+        With >= DECODE_SPLIT_PAIRS (sequence, kv head) pairs the pairs alone fill
+        the chip: partitions as long as possible (fewer partials to merge, no
+        merge kernel when one partition covers the context) while keeping
+        >= ~2048 workgroups.  With fewer pairs (small batches, one KV head per TP
+        rank) every live context is cut on the device into up to ``splits``
+        equal partitions (``ops.decode_attention``), so short contexts still
+        spread over the CUs; the captured graph needs no host-known length."""
+        pairs = batch * self.hkv
+        if 0 < pairs < DECODE_SPLIT_PAIRS:
+            splits = -(-DECODE_SPLIT_PAIRS // pairs)
+            splits = max(1, min(splits, -(-max_ctx // ops.DECODE_SPLIT_MIN)))
+            return self.decode_part_size, splits
         part = self.decode_part_size
         while part < 2048 and part < max_ctx and \
                 batch * self.hkv * ((max_ctx + 2 * part - 1) // (2 * part)) >= 2048:
             part *= 2
-        return part
+        return part, 0
 
-    def _decode_ws(self, B, max_blocks, bs, device, part):
-        key = (B, max_blocks, bs, str(device), part)
+    def _decode_ws(self, B, max_blocks, bs, device, part, splits=0):
+        key = (B, max_blocks, bs, str(device), part, splits)
         ws = self._ws.get(key)
         if ws is None:
             if device.type != "cuda":
                 return None
-            ws = ops.decode_workspace(B, self.hq, max_blocks, bs, part, device)
+            ws = ops.decode_workspace(B, self.hq, max_blocks, bs, part, device, splits)
             self._ws[key] = ws
         return ws
 

@@ -515,25 +515,34 @@ def embedding(ids: torch.Tensor, w: torch.Tensor, vocab_start: int = 0,
 
 
 def decode_workspace(batch: int, hq: int, max_blocks: int, block_size: int, part_size: int,
-                     device) -> tuple[torch.Tensor, torch.Tensor]:
-    max_parts = (max_blocks * block_size + part_size - 1) // part_size
+                     device, splits: int = 0) -> tuple[torch.Tensor, torch.Tensor]:
+    max_parts = max((max_blocks * block_size + part_size - 1) // part_size, splits)
     part_o = torch.empty(batch * hq * max_parts * 128, dtype=torch.float32, device=device)
     part_ml = torch.empty(batch * hq * max_parts * 2, dtype=torch.float32, device=device)
     return part_o, part_ml
 
 
+DECODE_SPLIT_MIN = int(os.environ.get("OMNIA_DECODE_SPLIT_MIN", "64"))
+
+
 def decode_attention(q, k_cache, v_cache, block_tables, seq_lens, scale, part_size=512,
-                     workspace=None, out=None):
-    """q: [B, Hq, D] one query per sequence at position seq_len-1."""
+                     workspace=None, out=None, splits=0, split_min=None):
+    """q: [B, Hq, D] one query per sequence at position seq_len-1.
+
+    ``part_size``: partition length (splits = 0), or the longest partition the
+    length-balanced split may use (splits > 0: each context is cut on the device
+    into up to ``splits`` equal page-aligned partitions of >= ``split_min`` keys)."""
     if q.is_cuda:
         B, hq, _ = q.shape
+        split_min = DECODE_SPLIT_MIN if split_min is None else split_min
         if out is None:
             out = torch.empty(B, hq, q.shape[2], dtype=q.dtype, device=q.device)
         if workspace is None:
             workspace = decode_workspace(B, hq, block_tables.shape[1], k_cache.shape[2],
-                                         part_size, q.device)
+                                         part_size, q.device, splits)
         kernels().decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens,
-                                   workspace[0], workspace[1], part_size, scale)
+                                   workspace[0], workspace[1], part_size, scale, splits,
+                                   split_min)
         return out
     B = q.shape[0]
     qsl = torch.arange(B + 1, dtype=torch.int32)

@@ -34,6 +34,22 @@ __device__ __forceinline__ float4v mfma16(short8 a, short8 b, float4v c) {
 constexpr int D = 128;
 
 // ============================================================== decode
+// Length-balanced split (split_t > 0): a sequence of `len` keys is cut into
+// ns = clamp(ceil(len / split_min), ceil(len / cap), split_t) partitions of equal
+// page-aligned length -- decided on the device from the live length, so a graph
+// captured once splits every context evenly (a host-chosen fixed partition
+// leaves one workgroup per (sequence, kv head) at short contexts when the batch
+// has few such pairs, e.g. one Llama-3-70B TP=8 rank).  cap (the LDS score
+// tile) and BS divide each other's multiples: pl <= cap always.
+__device__ __forceinline__ int decode_part_len(int len, int cap, int split_t, int split_min,
+                                               int bs) {
+  if (split_t <= 0) return cap;
+  int ns = min(split_t, (len + split_min - 1) / split_min);
+  ns = max(ns, max((len + cap - 1) / cap, 1));
+  const int pl = ((len + ns - 1) / ns + bs - 1) / bs * bs;
+  return min(pl, cap);
+}
+
 // grid: (B, Hkv, max_parts)   block: 64 * NW (NW = 2 or 4 waves)
 // UG: 16-key groups whose K loads one wave issues before its first MFMA (and,
 // for UG > 1, the first V batch is issued ahead of the softmax) -- the memory-
@@ -46,7 +62,8 @@ __global__ __launch_bounds__(64 * NW) void decode_attn_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
-    int hkv, int64_t q_stride, int part_size, int max_parts, float scale_log2) {
+    int hkv, int64_t q_stride, int part_size, int max_parts, float scale_log2, int split_t,
+    int split_min) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* stat = reinterpret_cast<float*>(smem);                    // [2*G] (padded to 16 floats)
   float* scores = stat + 16;                                       // [G][part_size]
@@ -58,10 +75,12 @@ __global__ __launch_bounds__(64 * NW) void decode_attn_kernel(
 
   const int b = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
   const int len = seq_lens[b];
-  const int p0 = part * part_size;
+  if (len <= 0) return;
+  const int pl = decode_part_len(len, part_size, split_t, split_min, BS);
+  const int p0 = part * pl;
   if (p0 >= len) return;
-  const int n = min(part_size, len - p0);
-  const int nparts = (len + part_size - 1) / part_size;
+  const int n = min(pl, len - p0);
+  const int nparts = (len + pl - 1) / pl;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int h0 = kvh * G;
 
@@ -218,11 +237,14 @@ __global__ __launch_bounds__(64 * NW) void decode_attn_kernel(
 // grid: (B * Hq)   block: 128
 __global__ __launch_bounds__(128) void decode_reduce_kernel(
     bf16_t* __restrict__ out, const float* __restrict__ part_o, const float* __restrict__ part_ml,
-    const int* __restrict__ seq_lens, int hq, int part_size, int max_parts) {
+    const int* __restrict__ seq_lens, int hq, int part_size, int max_parts, int split_t,
+    int split_min, int bs) {
   const int bh = blockIdx.x;
   const int b = bh / hq;
   const int len = seq_lens[b];
-  const int nparts = (len + part_size - 1) / part_size;
+  if (len <= 0) return;
+  const int pl = decode_part_len(len, part_size, split_t, split_min, bs);
+  const int nparts = (len + pl - 1) / pl;
   if (nparts <= 1) return;
   const float* ml = part_ml + (int64_t)bh * max_parts * 2;
   float m = -INFINITY;
@@ -698,9 +720,11 @@ int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void*
                            const void* k_cache, const void* v_cache, const int* block_tables,
                            int bt_stride, const int* seq_lens, int B, int hq, int hkv,
                            int head_dim, int block_size, int64_t q_stride, int part_size,
-                           int max_parts, float scale, hipStream_t s) {
+                           int max_parts, float scale, int split_t, int split_min,
+                           hipStream_t s) {
   if (head_dim != 128) return -1;
   if (part_size % 64 || part_size % block_size) return -2;
+  if (split_t > 0 && (split_min <= 0 || split_t > max_parts)) return -5;
   if (B == 0) return 0;
   const int G = hq / hkv;
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -729,7 +753,7 @@ int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void*
   decode_attn_kernel<GG, BB, UU, NN, VV><<<grid, block, lds, s>>>(                            \
       (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, (const bf16_t*)k_cache,               \
       (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, hkv, q_stride, part_size,   \
-      max_parts, scale_log2)
+      max_parts, scale_log2, split_t, split_min)
 #define OMNIA_DEC_NW(GG, BB, UU, VV) \
   do { if (nw == 2) OMNIA_DEC_UG(GG, BB, UU, 2, VV); else OMNIA_DEC_UG(GG, BB, UU, 4, VV); } while (0)
 #define OMNIA_DEC(GG, BB)                          \
@@ -755,7 +779,8 @@ int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void*
 #undef OMNIA_DEC_UG
   if (max_parts > 1)
     decode_reduce_kernel<<<B * hq, 128, 0, s>>>((bf16_t*)out, part_o, part_ml, seq_lens, hq,
-                                                part_size, max_parts);
+                                                part_size, max_parts, split_t, split_min,
+                                                block_size);
   return (int)hipGetLastError();
 }
 

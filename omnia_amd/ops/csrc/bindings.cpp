@@ -39,7 +39,8 @@ int omnia_decode_attention(void* out, float* part_o, float* part_ml, const void*
                            const void* k_cache, const void* v_cache, const int* block_tables,
                            int bt_stride, const int* seq_lens, int B, int hq, int hkv,
                            int head_dim, int block_size, int64_t q_stride, int part_size,
-                           int max_parts, float scale, hipStream_t s);
+                           int max_parts, float scale, int split_t, int split_min,
+                           hipStream_t s);
 int omnia_prefill_attention(void* out, const void* q, const void* k_cache, const void* v_cache,
                             const int* block_tables, int bt_stride, const int* q_start_loc,
                             const int* seq_lens, const int* tile_seq, const int* tile_q0,
@@ -217,7 +218,8 @@ void embedding(at::Tensor out, at::Tensor ids, at::Tensor w, int64_t vocab_start
 
 void decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                       at::Tensor block_tables, at::Tensor seq_lens, at::Tensor part_o,
-                      at::Tensor part_ml, int64_t part_size, double scale) {
+                      at::Tensor part_ml, int64_t part_size, double scale, int64_t splits,
+                      int64_t split_min) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
   CHECK_I32(block_tables); CHECK_I32(seq_lens);
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous(),
@@ -230,7 +232,9 @@ void decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tens
               "block_tables [B, max_blocks]");
   TORCH_CHECK(seq_lens.numel() >= B, "seq_lens");
   const int max_ctx = block_tables.size(1) * bs;
-  const int max_parts = (max_ctx + part_size - 1) / part_size;
+  // splits > 0: length-balanced split into up to `splits` partitions (>= split_min keys)
+  TORCH_CHECK(splits >= 0 && (splits == 0 || split_min > 0), "splits / split_min");
+  const int max_parts = std::max<int>((max_ctx + part_size - 1) / part_size, (int)splits);
   TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat,
               "workspace f32");
   TORCH_CHECK(part_o.numel() >= (int64_t)B * hq * max_parts * D &&
@@ -240,7 +244,8 @@ void decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tens
                                   v_cache.data_ptr(), block_tables.data_ptr<int>(),
                                   block_tables.stride(0), seq_lens.data_ptr<int>(), B, hq, hkv, D,
                                   bs, q.stride(0), part_size, max_parts, (float)scale,
-                                  cur_stream()), "decode_attention");
+                                  (int)splits, (int)split_min, cur_stream()),
+           "decode_attention");
 }
 
 void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,

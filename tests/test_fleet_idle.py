@@ -33,6 +33,7 @@ def test_idle_session_answers_heartbeat_pings():
         await site.start()
         port = site._server.sockets[0].getsockname()[1]
         try:
+            FleetSession.IDLE_AFTER_S = 0.05
             async with FleetSession(f"ws://127.0.0.1:{port}/ws", timeout_s=5) as fs:
                 await asyncio.sleep(1.0)  # 5 ping intervals with no turn in flight
                 r1 = await fs.turn("abc")
@@ -40,6 +41,7 @@ def test_idle_session_answers_heartbeat_pings():
                 r2 = await fs.turn("xyz")
             return r1["content"], r2["content"], fs.session_id
         finally:
+            FleetSession.IDLE_AFTER_S = 5.0
             await runner.cleanup()
 
     assert asyncio.run(go()) == ("cba", "zyx", "s1")

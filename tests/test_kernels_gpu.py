@@ -127,6 +127,31 @@ def test_decode_attention(hq, hkv, bs, nw, uv, monkeypatch):
     _close(out.cpu(), exp, 0.02, 0.02)
 
 
+@pytest.mark.parametrize("splits,split_min", [(2, 64), (4, 64), (8, 32), (64, 64)])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1)])
+def test_decode_attention_length_balanced_split(hq, hkv, splits, split_min):
+    """Device-side split (splits > 0): every context cut into up to `splits`
+    equal page-aligned partitions (>= split_min keys, <= part_size) and merged
+    -- against the fp32 oracle and the fixed-partition kernel."""
+    torch.manual_seed(5)
+    bs = 32
+    lens = [1, 31, 32, 33, 200, 513, 640, 1500, 3000]
+    B = len(lens)
+    nb_total = sum((l + bs - 1) // bs for l in lens) + 8
+    kc, vc = _make_cache(nb_total, hkv, bs, seed=5)
+    bt = _tables(lens, bs, nb_total)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    q = torch.randn(B, hq, 128, device=DEV, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(128)
+    out = ops.decode_attention(q, kc, vc, bt, sl, scale, part_size=512, splits=splits,
+                               split_min=split_min)
+    qsl = torch.arange(B + 1, dtype=torch.int32)
+    exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), qsl, sl.cpu(), scale)
+    _close(out.cpu(), exp, 0.02, 0.02)
+    fixed = ops.decode_attention(q, kc, vc, bt, sl, scale, part_size=512)
+    _close(out.float().cpu(), fixed.float().cpu(), 0.02, 0.02)
+
+
 @pytest.mark.parametrize("bs", [16, 32])
 @pytest.mark.parametrize("hq,hkv,hp,qt", [(32, 8, 1, 64), (32, 8, 2, 64), (32, 8, 4, 64),
                                           (64, 8, 4, 64), (8, 8, 0, 64), (32, 8, 1, 128),

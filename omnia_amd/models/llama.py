@@ -29,7 +29,7 @@ from .config import ModelConfig
 
 # decode attention: below this many (sequence, kv head) pairs a step splits every
 # live context on the device (``LlamaModel.decode_part``)
-DECODE_SPLIT_PAIRS = int(os.environ.get("OMNIA_DECODE_SPLIT_PAIRS", "0"))
+DECODE_SPLIT_PAIRS = int(os.environ.get("OMNIA_DECODE_SPLIT_PAIRS", "256"))
 
 
 @dataclass

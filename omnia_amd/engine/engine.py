@@ -27,6 +27,7 @@ from ..models.config import ModelConfig, resolve
 from ..models.llama import KVCache
 from ..observability import metrics as M
 from ..observability import timeline as TL
+from ..observability.engine_trace import EngineTrace
 from ..utils import failpoints
 from .kv_manager import BlockManager
 from .model_runner import ModelRunner
@@ -217,6 +218,8 @@ class LLMEngine:
         self._busy = collections.deque()  # (start, end) hipEvents of steps not yet summed
         self._busy_s = 0.0
         self._tap_dir = os.environ.get("OMNIA_LOGIT_TAP_DIR", "")
+        # OTel engine spans / roctx ranges / torch.profiler window (all opt-in)
+        self.trace = EngineTrace(dev.type)
         M.ENGINE_COLD_START.labels("total").set(time.perf_counter() - t0)
         log.info("engine ready: %s on %s (tp=%d), %d KV blocks x %d tokens, load %.1fs, "
                  "kv alloc %.2fs", self.model_cfg.name, dev, st.tp_size, nb, cfg.block_size,
@@ -312,6 +315,13 @@ class LLMEngine:
             failpoints.hit("engine.prefill" if self.scheduler.waiting else "engine.decode_step")
             if failpoints.triggered("engine.hang"):
                 time.sleep(float(os.environ.get("OMNIA_FAILPOINT_HANG_S", "5")))
+        self.trace.begin(self.step_count)
+        try:
+            return self._step()
+        finally:
+            self.trace.end()
+
+    def _step(self) -> int:
         if self.ep_lockstep:
             from .ep import run_ep_step
 
@@ -365,6 +375,9 @@ class LLMEngine:
         i.e. when the previous step ends or at launch if the GPU was idle).  Every
         step's interval also feeds the device-busy account (:meth:`busy_seconds`);
         the timeline keeps them only when enabled."""
+        if self.trace.active:
+            self.trace.on_step(kind, ts, rows, ntok,
+                               self.blocks.num_blocks - self.blocks.num_available, self.step_count)
         if e0 is None:
             return
         e1 = torch.cuda.Event(enable_timing=True)

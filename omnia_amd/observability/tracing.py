@@ -127,6 +127,21 @@ def end_span(sp: Span, attributes: dict | None = None, error: bool = False) -> N
         _TRACER.exporter.export(sp)
 
 
+def record_span(name: str, start_ns: int, end_ns: int, attributes: dict | None = None,
+                trace_id: str | None = None) -> Span | None:
+    """Export an already-finished root span (engine steps: they overlap when
+    pipelined, so they never become the context's current span)."""
+    t = _TRACER
+    if not t.enabled:
+        return None
+    sp = Span(name=name, trace_id=trace_id or uuid.uuid4().hex, span_id=os.urandom(8).hex(),
+              parent_id=None, start_ns=start_ns, end_ns=end_ns,
+              attributes=dict(attributes or {}), status="OK", sampled=t.should_sample(None))
+    if sp.sampled:
+        t.exporter.export(sp)
+    return sp
+
+
 class MemoryExporter:
     def __init__(self):
         self.spans: list[Span] = []

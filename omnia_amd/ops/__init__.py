@@ -15,6 +15,7 @@ import threading
 import torch
 import torch.nn.functional as F
 
+from . import checks
 from . import reference as ref
 
 _lock = threading.Lock()
@@ -84,6 +85,8 @@ def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, 
 def rope_kv(q, k, v, positions, cos_sin, k_cache, v_cache, slots, hq, hkv, block_size):
     """Rotate q/k in place (neox) and write k/v rows into the paged cache at `slots`."""
     if q.is_cuda:
+        if checks.active(q):
+            checks.slots("rope_kv", slots, k_cache)
         kernels().rope_kv(q, k, v, positions, cos_sin, k_cache, v_cache, slots, hq, hkv,
                           block_size)
         return
@@ -352,6 +355,8 @@ def pgemm(epi: int, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None =
     if out is None:
         out = x.new_empty(M, hq * 128 if epi == 3 else N)
     if x.is_cuda:
+        if epi == 3 and checks.active(x):
+            checks.slots("pgemm qkv", slots, k_cache)
         kernels().pgemm(epi, out, x.contiguous(), w, ss_in, inv_d, eps, ss_out, positions,
                         cos_sin, k_cache, v_cache, slots, hq, hkv, block_size)
         return out
@@ -428,6 +433,8 @@ def splitk_rope_kv(parts, positions, cos_sin, k_cache, v_cache, slots, hq, hkv, 
     T = parts.shape[1]
     D = 128
     if parts.is_cuda:
+        if checks.active(parts):
+            checks.slots("splitk_rope_kv", slots, k_cache)
         q = torch.empty(T, hq * D, dtype=k_cache.dtype, device=parts.device) if q is None else q
         kernels().splitk_rope_kv(q, parts, positions, cos_sin, k_cache, v_cache, slots, hq, hkv,
                                  block_size)
@@ -535,6 +542,8 @@ def decode_attention(q, k_cache, v_cache, block_tables, seq_lens, scale, part_si
     if q.is_cuda:
         B, hq, _ = q.shape
         split_min = DECODE_SPLIT_MIN if split_min is None else split_min
+        if checks.active(q):
+            checks.paged("decode_attention", block_tables, seq_lens, k_cache, B)
         if out is None:
             out = torch.empty(B, hq, q.shape[2], dtype=q.dtype, device=q.device)
         if workspace is None:
@@ -584,6 +593,9 @@ def prefill_attention(q, k_cache, v_cache, block_tables, q_start_loc, seq_lens, 
             tile_seq = torch.tensor(s, dtype=torch.int32, device=q.device)
             tile_q0 = torch.tensor(q0, dtype=torch.int32, device=q.device)
         out = torch.empty_like(q) if out is None else out
+        if checks.active(q):
+            checks.paged("prefill_attention", block_tables, seq_lens, k_cache,
+                         q_start_loc.numel() - 1)
         kernels().prefill_attention(out, q, k_cache, v_cache, block_tables, q_start_loc,
                                     seq_lens, tile_seq, tile_q0, scale, heads_per_wave,
                                     q_tile or PREFILL_Q_TILE, lse, kv_lens)

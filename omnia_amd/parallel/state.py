@@ -113,6 +113,14 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, device: str |
     """Initialise torch.distributed from torchrun env vars and carve TP/DP groups.
 
     Ranks [k*tp, (k+1)*tp) form TP group k; ranks with equal tp_rank form a DP group.
+
+    RCCL failure detection (SURVEY §5.3 [design]): the ``nccl`` process group's
+    watchdog thread polls the communicators' async error state
+    (``ncclCommGetAsyncError``, which is RCCL's) and the ``timeout_s`` of every
+    collective. PyTorch's default ``TORCH_NCCL_ASYNC_ERROR_HANDLING`` tears the
+    rank down on either. The engine's step watchdog (``engine/engine.py``) then
+    reports the pod unhealthy, so a lost peer fails the pod instead of hanging
+    it.
     """
     ws, rank, local = env_world()
     if ws % tp_size:

@@ -219,7 +219,13 @@ class LlamaModel:
     # QKV parts -> splitk_rope_kv (RoPE + paged KV write), O / down parts ->
     # splitk_add_rmsnorm (residual add + RMSNorm), gate_up parts -> splitk_swiglu.
     def _wcfg(self, M: int, N: int, K: int, mode: int, is_decode: bool):
-        if not is_decode or self.device.type != "cuda":
+        if self.device.type != "cuda":
+            return None
+        if not is_decode:
+            # mid-size steps below the prefill tile's row threshold: split-K on
+            # the 256x256 tile where the table lists a win (ops.midm_config)
+            if self.tp == 1 and self.use_pgemm and M < self._min_rows:
+                return ops.midm_config(M, N, K, mode)
             return None
         return ops.wgemm_config(M, N, K, mode)
 
@@ -291,6 +297,8 @@ class LlamaModel:
 
     def _parts(self, tag, S: int, M: int, N: int,
                dtype: torch.dtype = torch.float32) -> torch.Tensor:
+        if M > ops.WGEMM_MAX_M:  # mid-size steps: M varies per step, do not pin one per M
+            return torch.empty(S, M, N, dtype=dtype, device=self.device)
         key = ("parts", tag, S, M, N, dtype)
         buf = self._ws.get(key)
         if buf is None:
@@ -326,7 +334,7 @@ class LlamaModel:
         ops.fused_add_rmsnorm(x, residual, w, eps)
         return x
 
-    _min_rows = int(os.environ.get("OMNIA_PGEMM_MIN_ROWS", "257"))  # this forward's threshold (mixed steps: the higher one)
+    _min_rows = int(os.environ.get("OMNIA_PGEMM_MIN_ROWS", "2049"))  # this forward's threshold (mixed steps: the higher one)
 
     def _pgemm_ok(self, M: int, K: int, N: int, is_decode: bool, tn: int = 256) -> bool:
         """A prefill-sized projection the hand 256x256 MFMA kernel covers (the
@@ -349,6 +357,8 @@ class LlamaModel:
         cfg = self._wcfg(M, I2 // 2, K, 1, is_decode)
         if cfg is None:
             a = ops.linear_silu(h, layer["gate_up"])  # SwiGLU fused into decode GEMMs
+        elif cfg[1] == ops.PGEMM_SPLIT and cfg[2] == 1:
+            a = ops.pgemm(1, h, layer["gate_up"])  # mid-size step: the unsplit fused tile
         else:
             nw, nwaves, S = cfg
             if S == 1 and nwaves != ops.PGEMM_SPLIT:
@@ -469,7 +479,11 @@ class LlamaModel:
 
     # ------------------------------------------------ fused prefill (pgemm.hip)
     use_pgemm = os.environ.get("OMNIA_PGEMM", "1") != "0"
-    PGEMM_MIN_ROWS = int(os.environ.get("OMNIA_PGEMM_MIN_ROWS", "257"))
+    # prefill chunks take the fused layer from this many rows.  Below it the
+    # unsplit 256x256 tile leaves most CUs idle on qkv / o / down; the unfused
+    # path runs them split-K on the same tile (ops.midm_config) and is 1.2-2.2x
+    # faster per layer at 512-2048 rows (profiles/r6/midm/)
+    PGEMM_MIN_ROWS = int(os.environ.get("OMNIA_PGEMM_MIN_ROWS", "2049"))
     # mixed steps take the fused layer only from this many rows: at the open-loop
     # trickle (~256 decode rows + a few hundred prompt tokens) pgemm's 256x256
     # tiles leave most CUs idle, and the split decode / library path is 1.5x

@@ -239,6 +239,32 @@ def wgemm_config(M: int, N: int, K: int, mode: int) -> tuple[int, int, int] | No
     return cfg
 
 
+MIDM_BUCKETS = (512, 768, 1024, 1536, 2048, 3072, 4096)
+_midm_table: dict | None = None
+
+
+def midm_config(M: int, N: int, K: int, mode: int) -> tuple[int, int, int] | None:
+    """Mid-size projections (M = 257..4096 rows: open-loop mixed steps, which
+    the unsplit 256x256 prefill tile under-fills): ``(256, PGEMM_SPLIT, S)``
+    when ``ops/tuned/midm_mi355x.json`` lists a split-K win of the 256x256 tile
+    (+ its slab consumer) over the library path for this shape's M bucket
+    (``scripts/midm_sweep.py``), else None (library GEMM)."""
+    global _midm_table
+    if not _wgemm_on or M <= WGEMM_MAX_M or M > MIDM_BUCKETS[-1]:
+        return None
+    if _midm_table is None:
+        import json
+
+        p = os.path.join(os.path.dirname(__file__), "tuned", "midm_mi355x.json")
+        _midm_table = {}
+        if os.path.exists(p):
+            with open(p) as f:
+                _midm_table = {k: int(v) for k, v in json.load(f).items()}
+    b = next(x for x in MIDM_BUCKETS if M <= x)
+    S = _midm_table.get(f"{mode}:{b}:{N}:{K}")
+    return (256, PGEMM_SPLIT, S) if S else None
+
+
 def wgemm(mode: int, x: torch.Tensor, w: torch.Tensor, splits: int = 1, nw: int = 2,
           nwaves: int = 4, out: torch.Tensor | None = None) -> torch.Tensor:
     """Decode GEMM with W streamed HBM -> MFMA registers (``csrc/wgemm.hip``).

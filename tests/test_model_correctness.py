@@ -118,8 +118,15 @@ def test_gpu_llama3_8b_shaped_fused_prefill_matches_dense_oracle():
     QKV+RoPE+KV write, O/down + residual + row sumsq, gate_up + SwiGLU with the
     folded RMSNorm row scale); decode and the second turn's 20-token prefill run
     the split-K / tile paths.  Chunks are not a multiple of the 256-row tile."""
+    from omnia_amd.models.llama import LlamaModel
+
     mc = resolve("llama-3-8b").replace(name="llama-3-8b-2l", num_layers=2)
-    frac, worst = _gate("cuda", mc, chunk=384, rel_tol=0.04, prompt_lens=(600, 300, 280))
+    saved = LlamaModel.PGEMM_MIN_ROWS
+    LlamaModel.PGEMM_MIN_ROWS = 257  # serving default 2049: 384-row chunks take split-K
+    try:
+        frac, worst = _gate("cuda", mc, chunk=384, rel_tol=0.04, prompt_lens=(600, 300, 280))
+    finally:
+        LlamaModel.PGEMM_MIN_ROWS = saved
     print(f"llama-3-8b-2l fused prefill worst rel err {worst:.4f}")
 
 
@@ -283,6 +290,51 @@ def test_gpu_fused_mixed_steps_match_dense_oracle(pipeline):
     assert fused["mixed"] >= 1, eng.counters
     frac, worst = _check(mc, eng.model.w, seqs, eng.runner.logit_tap, 0.04)
     print(f"fused mixed steps: {fused['mixed']}, worst rel err {worst:.4f}")
+    assert frac == 1.0
+
+
+@pytest.mark.gpu
+def test_gpu_midsize_mixed_steps_split_k_match_dense_oracle():
+    """Mixed steps of 257..4095 rows (the open loop's) take the 256x256 tile with
+    split-K + the slab consumers for qkv / o / down and the unsplit fused tile for
+    gate_up wherever ops/tuned/midm_mi355x.json lists a win -- against the dense
+    oracle, pipelined."""
+    from omnia_amd import ops
+
+    mc = resolve("llama-3-8b").replace(name="llama-3-8b-2l", num_layers=2)
+    eng = LLMEngine(EngineConfig(model=mc.name, device="cuda", num_blocks=512, block_size=16,
+                                 max_batch=8, max_model_len=1024, max_prefill_tokens=640,
+                                 seed=12, mixed_budget=640, mixed_backlog=2048), model_cfg=mc)
+    eng.runner.enable_logit_tap()
+    seen = []
+    orig = ops.midm_config
+
+    def spy(M, N, K, mode):
+        cfg = orig(M, N, K, mode)
+        if cfg is not None:
+            seen.append((M, N, K, mode, cfg[2]))
+        return cfg
+
+    ops.midm_config = spy
+    try:
+        rng = random.Random(6)
+        V = mc.vocab_size
+        p = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+        # a pure 520-row prefill chunk (below the fused layer's 2049 rows), then
+        # mixed steps of 257..640 rows
+        seqs = [eng.add_request([rng.randrange(10, V - 10) for _ in range(n)], p)
+                for n in (300, 220)]
+        for _ in range(3):
+            eng.step()
+        seqs += [eng.add_request([rng.randrange(10, V - 10) for _ in range(n)], p)
+                 for n in (420, 330)]
+        eng.run_until_done()
+    finally:
+        ops.midm_config = orig
+    assert {m for *_, m, _ in seen} >= {0}, seen  # split-K projections ran
+    assert any(S > 1 for *_, S in seen), seen
+    frac, worst = _check(mc, eng.model.w, seqs, eng.runner.logit_tap, 0.04)
+    print(f"mid-size split-K steps: {len(seen)} projections, worst rel err {worst:.4f}")
     assert frac == 1.0
 
 

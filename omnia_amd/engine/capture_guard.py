@@ -161,10 +161,29 @@ class CaptureGuard:
     def _mem_enter(self):
         if self.enabled and self.device.type == "cuda":
             self._before = _active_default_blocks(self.device)
+            self._hist = os.environ.get("OMNIA_CAPTURE_GUARD_TRACE") == "1"
+            if self._hist:  # allocation stacks for the leak report
+                torch.cuda.memory._record_memory_history(max_entries=100000)
 
     def _mem_exit(self, et):
         if self.enabled and et is None and self._before is not None:
             self.leaked = sorted(_active_default_blocks(self.device) - self._before)
+        if getattr(self, "_hist", False):
+            if self.leaked:
+                self._log_leak_stacks()
+            torch.cuda.memory._record_memory_history(enabled=None)
+            self._hist = False
+
+    def _log_leak_stacks(self):
+        want = {a for a, _ in self.leaked}
+        for seg in torch.cuda.memory._snapshot().get("segments", []):
+            for b in seg.get("blocks", []):
+                if b.get("address") in want:
+                    frames = b.get("frames") or []
+                    where = "\n".join(f"  {f.get('filename')}:{f.get('line')} {f.get('name')}"
+                                      for f in frames[:14])
+                    log.error("capture guard: block %#x+%d allocated at\n%s",
+                              b["address"], b.get("size", 0), where)
 
     def violations(self) -> list[str]:
         v = [f"framework op {k} x{n}" for k, n in sorted(self.ops.items())]

@@ -744,13 +744,15 @@ class ModelRunner:
 
         guard = CaptureGuard(self.device, f"decode graph rows={nrows} cols={ncols}")
         if not self._graph_rng_ready:
-            # PyTorch registers its RNG generator with the first capture of the
-            # process (seed / offset tensors in the default pool): do that in an
-            # empty capture, outside the guarded one
-            warm = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(warm, pool=self.graph_pool):
+            # PyTorch's CUDA generator allocates its graph seed / offset tensors
+            # (2 x 512 B, default pool) when the first live graph registers with
+            # it and frees them when the last one goes.  Register an empty graph
+            # first, outside the guarded capture, and KEEP it: if it were dropped
+            # (or an earlier engine's graphs were collected) the guarded capture
+            # would re-allocate them -- a flaky guard violation
+            self._rng_anchor = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._rng_anchor, pool=self.graph_pool):
                 pass
-            del warm
             self._graph_rng_ready = True
         try:
             with guard.memory_scope():

@@ -41,3 +41,30 @@ def test_decode_graphs_pass_strict_guard(monkeypatch, model, batch):
         assert st.get("capture_library_gemms", 0) == 0
     if not big:
         assert g == run(False)[0]
+
+
+def test_strict_guard_after_an_earlier_engine_is_collected(monkeypatch):
+    """PyTorch's CUDA generator allocates its graph seed / offset tensors when
+    the first live graph registers and frees them with the last one: once an
+    earlier engine's graphs are collected, the next engine's first capture would
+    allocate them (2 x 512 B outside the graph pool) -- unless the runner keeps
+    its warm-up registration graph alive (model_runner._capture)."""
+    import gc
+
+    monkeypatch.setenv("OMNIA_CAPTURE_GUARD", "strict")
+
+    def engine():
+        return LLMEngine(EngineConfig(model="tiny-llama", device="cuda", num_blocks=256,
+                                      block_size=32, max_batch=4, max_model_len=512,
+                                      use_graphs=True, mixed_budget=0))
+
+    p = SamplingParams(temperature=0, max_tokens=4, ignore_eos=True)
+    e = engine()
+    e.generate([list(range(5, 40))], p)
+    del e
+    gc.collect()  # every graph of the first engine is gone
+    torch.cuda.empty_cache()
+    e2 = engine()
+    e2.generate([list(range(5, 40)), list(range(9, 30))], p)
+    assert e2.runner.stats.get("capture_guard_violations", 0) == 0
+    assert e2.runner.stats["captures"] > 0

@@ -241,6 +241,7 @@ def wgemm_config(M: int, N: int, K: int, mode: int) -> tuple[int, int, int] | No
 
 MIDM_BUCKETS = (512, 768, 1024, 1536, 2048, 3072, 4096)
 _midm_table: dict | None = None
+_midm_on = os.environ.get("OMNIA_MIDM", "1") != "0"
 
 
 def midm_config(M: int, N: int, K: int, mode: int) -> tuple[int, int, int] | None:
@@ -250,7 +251,7 @@ def midm_config(M: int, N: int, K: int, mode: int) -> tuple[int, int, int] | Non
     (+ its slab consumer) over the library path for this shape's M bucket
     (``scripts/midm_sweep.py``), else None (library GEMM)."""
     global _midm_table
-    if not _wgemm_on or M <= WGEMM_MAX_M or M > MIDM_BUCKETS[-1]:
+    if not (_wgemm_on and _midm_on) or M <= WGEMM_MAX_M or M > MIDM_BUCKETS[-1]:
         return None
     if _midm_table is None:
         import json

@@ -13,7 +13,7 @@ a mixed step runs it:
 
 Weights rotate over >= 1.5 GiB so every call streams them from HBM.
 
-    python scripts/midm_sweep.py [--m 512,1024,2048] [--out x.json]
+    python scripts/midm_sweep.py [--m 512,1024,2048] [--out x.json] [--shapes 70b]
 """
 import argparse
 import json
@@ -45,8 +45,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", default="512,768,1024,1536,2048,3072")
     ap.add_argument("--out", default="midm_sweep.json")
+    ap.add_argument("--shapes", default="8b", choices=["8b", "70b"])
     a = ap.parse_args()
-    d, I, hq, hkv = 4096, 14336, 32, 8
+    d, I, hq, hkv = (4096, 14336, 32, 8) if a.shapes == "8b" else (8192, 28672, 64, 8)
     shapes = {"qkv": ((hq + 2 * hkv) * 128, d), "o": (d, hq * 128), "gate_up": (2 * I, d),
               "down": (d, I)}
     cs = ref.rope_cos_sin(8192, 128, 500000.0, device=dev)

@@ -339,6 +339,42 @@ def test_gpu_midsize_mixed_steps_split_k_match_dense_oracle():
 
 
 @pytest.mark.gpu
+def test_gpu_70b_shaped_midsize_prefill_split_k_matches_dense_oracle():
+    """Llama-3-70B-shaped (2 layers) 520-row prefill below the fused layer's
+    threshold: qkv / o split-K and gate_up on the unsplit fused tile from the
+    70B rows of ops/tuned/midm_mi355x.json -- against the dense oracle."""
+    from omnia_amd import ops
+
+    mc = resolve("llama-3-70b").replace(name="llama-3-70b-2l", num_layers=2)
+    eng = LLMEngine(EngineConfig(model=mc.name, device="cuda", num_blocks=256, block_size=16,
+                                 max_batch=4, max_model_len=1024, max_prefill_tokens=640,
+                                 seed=14, mixed_budget=0), model_cfg=mc)
+    eng.runner.enable_logit_tap()
+    seen = []
+    orig = ops.midm_config
+
+    def spy(M, N, K, mode):
+        cfg = orig(M, N, K, mode)
+        if cfg is not None:
+            seen.append((M, N, K, mode, cfg[2]))
+        return cfg
+
+    ops.midm_config = spy
+    try:
+        rng = random.Random(8)
+        V = mc.vocab_size
+        p = SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True)
+        seqs = eng.generate([[rng.randrange(10, V - 10) for _ in range(n)] for n in (300, 220)],
+                            p)
+    finally:
+        ops.midm_config = orig
+    assert any(S > 1 for *_, S in seen) and any(m == 1 for *_, m, _ in seen), seen
+    frac, worst = _check(mc, eng.model.w, seqs, eng.runner.logit_tap, 0.04)
+    print(f"70b-shaped mid-size prefill: worst rel err {worst:.4f}")
+    assert frac == 1.0
+
+
+@pytest.mark.gpu
 def test_gpu_shared_prefix_pages_match_dense_oracle():
     """Cross-session prefix sharing (kv_manager.py): the second wave's prompts map
     the 6 full 16-token pages of the 100-token system prompt the first wave

@@ -482,7 +482,7 @@ class LlamaModel:
     # prefill chunks take the fused layer from this many rows.  Below it the
     # unsplit 256x256 tile leaves most CUs idle on qkv / o / down; the unfused
     # path runs them split-K on the same tile (ops.midm_config) and is 1.2-2.2x
-    # faster per layer at 512-2048 rows (profiles/r6/midm/)
+    # faster per layer at 512-2048 rows (profiles/r6/open/)
     PGEMM_MIN_ROWS = int(os.environ.get("OMNIA_PGEMM_MIN_ROWS", "2049"))
     # mixed steps take the fused layer only from this many rows: at the open-loop
     # trickle (~256 decode rows + a few hundred prompt tokens) pgemm's 256x256

@@ -12,8 +12,8 @@ S sessions run T turns in lock-step. Each turn appends ``--user-len`` synthetic
 tokens and generates ``--gen-len`` (ignore_eos). The whole workload runs twice:
 * ``resident``: requests carry their session_id, so the prefix comes from the
   cache;
-* ``stateless``: requests carry no session id, so the full history is
-  re-prefilled.
+* ``stateless``: requests carry no session id and cross-session prefix
+  sharing is off, so the full history is re-prefilled.
 
 Per turn it reports wall time, mean TTFT, and the prompt tokens that were
 actually prefilled versus served from the cache.
@@ -79,8 +79,14 @@ def main():
     eng = LLMEngine(EngineConfig(model=a.model, device="cuda" if torch.cuda.is_available()
                                  else "cpu", max_batch=max(256, a.sessions)))
     run(eng, 8, 1, 32, 8, True, 99)  # warm-up: graphs, tuned GEMMs
-    res = {m: run(eng, a.sessions, a.turns, a.user_len, a.gen_len, m == "resident", 1)
-           for m in ("resident", "stateless")}
+    res = {"resident": run(eng, a.sessions, a.turns, a.user_len, a.gen_len, True, 1)}
+    # the reference's remote provider re-prefills the whole history every turn:
+    # no engine-side reuse at all for the stateless run (cross-session prefix
+    # sharing would otherwise map the resident run's -- and the previous
+    # turn's -- pages by content)
+    eng.blocks.reset_shared()
+    eng.blocks.share_prefix = False
+    res["stateless"] = run(eng, a.sessions, a.turns, a.user_len, a.gen_len, False, 1)
     r, s = res["resident"], res["stateless"]
     summary = {"sessions": a.sessions, "turns": a.turns, "user_len": a.user_len,
                "gen_len": a.gen_len,

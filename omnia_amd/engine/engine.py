@@ -63,11 +63,13 @@ class EngineConfig:
     # in one forward) bound inter-token latency under arrivals; 0: separate steps
     mixed_budget: int = 16384
     # >0: mixed steps only while the prefill backlog is <= this many tokens (a
-    # trickle of arrivals); bursts are prefilled first on the fused prefill path.
-    # Open loop (profiles/r4/mixed/) mixed steps cut p50 turn latency 1.7x and
-    # p95 TTFT 6x; a closed-loop wave (256 x 512 tokens in 16K chunks) never
-    # drops to this backlog, so it keeps the separate-step throughput
-    mixed_backlog: int = 8192
+    # burst is then prefilled first); 0: no gate -- a burst's 16K-token chunks
+    # carry the running decoders along.  Open loop (profiles/r4/mixed/) mixed
+    # steps cut p50 turn latency 1.7x and p95 TTFT 6x.  In the closed loop the
+    # ungated default measured +0.6 % tok/s and -0.9 % p50 turn over the 8192
+    # gate, 3 of 3 interleaved pairs on one box (p95 TTFT +1.5 %;
+    # profiles/r6/bench/mixed_gate/)
+    mixed_backlog: int = 0
     # mixed steps under TP (engine/tp.py MIXED; sampled synchronously on rank 0):
     # on since round 5 -- GPU-verified in every TP arrival mode (profiles/r5/tp)
     tp_mixed: bool = True

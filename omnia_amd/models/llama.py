@@ -233,17 +233,19 @@ class LlamaModel:
     # of each projection the tuned table sends to tgemm.  Streamed alone, row-major
     # weights (128-B pieces of rows 2*K bytes apart) reach ~4.5 TB/s and packed
     # ones ~6.0 TB/s; inside the full kernel, next to the x re-reads and the
-    # MFMAs, the gain is 0-3 % per projection (profiles/r5/decode_gemm/), so the
-    # copy (~14 GB for Llama-3-8B, taken from the KV pool) is opt-in:
-    # OMNIA_TGEMM_PACK=1 builds it before the KV pool is sized, when it fits
-    # pack_budget_frac of HBM.
+    # MFMAs, the gain is 0-3 % per projection (profiles/r5/decode_gemm/); end to
+    # end the closed-loop bench gains +0.8 % tok/s and -2 % TPOT, 3 of 3
+    # interleaved pairs (profiles/r6/bench/tgemm_pack/).  The copy (~14 GB for
+    # Llama-3-8B, 5 % of HBM) is built before the KV pool is sized, by default
+    # whenever it fits pack_budget_frac of HBM (70B TP=1 and MoE models: never);
+    # OMNIA_TGEMM_PACK=0 turns it off.
     pack_budget_frac = 0.10  # of the device's HBM
 
     def prepack_decode(self, max_batch: int) -> int:
         """Pack the decode projections for every batch bucket up to ``max_batch``;
         returns the bytes packed (0: off / nothing on tgemm / over budget)."""
         self._packed = {}
-        env = os.environ.get("OMNIA_TGEMM_PACK", "0")
+        env = os.environ.get("OMNIA_TGEMM_PACK", "1")
         if env not in ("1", "force") or self.device.type != "cuda" or self.tp != 1 \
                 or self.cfg.is_moe:
             return 0

@@ -779,7 +779,7 @@ def run(a, drv, ws, rank, use_gpu, host_only):
                 "arrival": a.arrival if a.arrival == "closed" else f"poisson@{a.rate}/s",
                 "stream_interval_ms": a.stream_interval_ms,
                 "mixed_budget": a.mixed_budget if a.mixed_budget is not None else
-                "engine default (16384; ungated at TP=1, backlog-gated at 8192 under TP)",
+                "engine default (16384, ungated)",
                 "tp": a.tp,
                 "hip_graphs": not a.no_graphs,
                 "engine": a.engine,

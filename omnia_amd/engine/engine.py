@@ -68,10 +68,8 @@ class EngineConfig:
     # steps cut p50 turn latency 1.7x and p95 TTFT 6x.  In the closed loop the
     # ungated default measured +0.6 % tok/s and -0.9 % p50 turn over the 8192
     # gate, 3 of 3 interleaved pairs on one box (p95 TTFT +1.5 %;
-    # profiles/r6/bench/mixed_gate/).  -1 = auto: ungated at TP = 1; the 8192
-    # gate under TP, whose mixed steps sample synchronously on rank 0 (the TP=2
-    # rehearsal measured -4 % tok/s ungated, profiles/r6/tp2/)
-    mixed_backlog: int = -1
+    # profiles/r6/bench/mixed_gate/)
+    mixed_backlog: int = 0
     # mixed steps under TP (engine/tp.py MIXED; sampled synchronously on rank 0):
     # on since round 5 -- GPU-verified in every TP arrival mode (profiles/r5/tp)
     tp_mixed: bool = True
@@ -200,8 +198,7 @@ class LLMEngine:
                             # and sampled synchronously on rank 0 (tp_mixed)
                             mixed_budget=cfg.mixed_budget if (self.model.tp == 1 or
                                                               cfg.tp_mixed) else 0,
-                            mixed_backlog=(cfg.mixed_backlog if cfg.mixed_backlog >= 0
-                                           else (0 if self.model.tp == 1 else 8192)),
+                            mixed_backlog=cfg.mixed_backlog,
                             cp_threshold=cfg.cp_threshold if self.cp_lockstep else 0),
             self.blocks)
         self.scheduler.on_capped = self._finish_capped
